@@ -1,0 +1,111 @@
+// Shared device helpers for the cgnn_amd HIP kernels (gfx950 / CDNA4 only).
+//
+//  * Philox4x32-10 counter-based RNG.  Every random number in the framework is
+//    a pure function of (key, counter): key = per-model 64-bit key derived on
+//    the host from (seed, run, salt); counter = (row, stream-id, step, purpose).
+//    Results therefore do not depend on batching, launch geometry or on how
+//    many GPUs share the work.  The Python mirror used by
+//    the CPU path lives in cgnn_amd/utils/philox.py and is bit-identical in the
+//    integer part.
+//  * 64-lane wave reductions (wavefront = 64 on CDNA4, never 32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CGNN_WAVE 64
+
+namespace cgnn {
+
+// ---------------------------------------------------------------- Philox
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ void mulhilo32(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  hi = (uint32_t)(p >> 32);
+  lo = (uint32_t)p;
+}
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, lo0, hi1, lo1;
+    mulhilo32(M0, c.x, hi0, lo0);
+    mulhilo32(M1, c.z, hi1, lo1);
+    u32x4 n;
+    n.x = hi1 ^ c.y ^ k0;
+    n.y = lo1;
+    n.z = hi0 ^ c.w ^ k1;
+    n.w = lo0;
+    c = n;
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// uniform in (0,1): 24 random bits, centred in their bucket (never 0 or 1).
+__device__ __forceinline__ float u01(uint32_t x) {
+  return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+// One standard normal from one Philox block (Box-Muller, cos branch).
+// v_log_f32 is log2 and v_cos_f32 takes revolutions, so
+//   n = sqrt(-2 ln2 * log2(u1)) * cos(2*pi*u2)  ->  two transcendental ops.
+__device__ __forceinline__ float normal_from(u32x4 r) {
+  float u1 = u01(r.x), u2 = u01(r.y);
+  float rad = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+  return rad * __builtin_amdgcn_cosf(u2);
+}
+
+// Two independent normals from one Philox block (cos and sin branches).
+__device__ __forceinline__ void normal2_from(u32x4 r, float& n0, float& n1) {
+  float u1 = u01(r.x), u2 = u01(r.y);
+  float rad = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
+  n0 = rad * __builtin_amdgcn_cosf(u2);
+  n1 = rad * __builtin_amdgcn_sinf(u2);
+}
+
+// RNG purposes (4th counter word).
+enum RngPurpose : uint32_t {
+  RNG_NODE_NOISE = 1u,   // per-node generator noise  e_v      (row, var, step)
+  RNG_CONF_NOISE = 2u,   // per-skeleton-edge noise   xi_uv    (row, edge, step)
+  RNG_PARAM_INIT = 3u,   // parameter init            N(0,s^2) (param, 0, 0)
+  RNG_RFF_FREQ   = 4u,   // Fourier-MMD frequencies            (feat, dim, step)
+  RNG_DROPOUT    = 5u,   // GNN dropout masks                  (row, col/4, step)
+};
+
+__device__ __forceinline__ float rng_normal(uint32_t k0, uint32_t k1, uint32_t a, uint32_t b,
+                                            uint32_t step, uint32_t purpose) {
+  u32x4 c = {a, b, step, purpose};
+  return normal_from(philox4x32_10(c, k0, k1));
+}
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, CGNN_WAVE);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, CGNN_WAVE));
+  return v;
+}
+
+// Deterministic block sum (fixed tree), result valid in every thread.
+// `scratch` needs blockDim.x / 64 floats.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int w = 0; w < nw; ++w) t += scratch[w];
+  return t;
+}
+
+}  // namespace cgnn

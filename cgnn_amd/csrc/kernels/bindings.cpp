@@ -1,0 +1,175 @@
+// pybind11 surface of the HIP extension `cgnn_amd._hip`.
+// Every device pointer crosses the boundary as an integer (tensor.data_ptr()),
+// every stream as the integer handle of torch.cuda.current_stream(); the
+// extension never allocates device memory itself, PyTorch's caching allocator
+// owns all buffers.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+extern "C" {
+int cgnn_mmd_supported_d(int);
+int cgnn_gen_supported_h(int);
+int cgnn_gen_bwd_blocks(int);
+size_t cgnn_gen_bwd_lds(int, int);
+int cgnn_launch_mmd(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
+                    float, hipStream_t);
+int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
+                              const int*, int, int, hipStream_t);
+int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, const uint32_t*,
+                        const int*, int, int, int, int, int, hipStream_t);
+int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int, int,
+                        float*, const uint32_t*, const int*, int, int, int, int, int, float*,
+                        hipStream_t);
+int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
+                     int, float, float, float, float, int, hipStream_t);
+int cgnn_launch_init(float*, float*, float*, const int*, int, int, const uint32_t*, float, int,
+                     hipStream_t);
+int cgnn_launch_advance(int*, int, int, hipStream_t);
+void* cgnn_engine_create(const int*, const float*, const void* const*, hipStream_t);
+void cgnn_engine_destroy(void*);
+int cgnn_engine_gen_blocks(void*);
+int cgnn_engine_n_parts(void*);
+void cgnn_engine_init(void*);
+void cgnn_engine_tt(void*);
+void cgnn_engine_run(void*, int, int, int, int);
+// Fourier (random-feature) MMD
+int rff_launch_freqs(float*, const uint32_t*, const int*, int, int, int, int, int, int, hipStream_t);
+int rff_launch_fwd_bwd(int, const float*, const float*, const float*, float*, float*, float*, int,
+                       int, int, int, int, float, hipStream_t);
+// GNN track
+int gnn_launch_spmm(const int*, const int*, const void*, void*, const float*, const float*, int,
+                    int, int, int, int, int, int, hipStream_t);
+int gnn_launch_spmm_ce(const int*, const int*, const void*, const float*, const float*,
+                       const int*, const uint8_t*, float*, void*, float*, int, int, int, int, float,
+                       hipStream_t);
+int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, float, float, float,
+                    const int*, hipStream_t);
+int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
+}
+
+static inline hipStream_t S(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
+template <class T> static inline T* Pt(uint64_t p) { return reinterpret_cast<T*>(p); }
+
+static void chk(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + ": HIP launch failed (code " + std::to_string(rc) + ")");
+}
+
+class PyEngine {
+ public:
+  PyEngine(std::vector<int> icfg, std::vector<float> fcfg, std::vector<uint64_t> ptrs, uint64_t stream) {
+    if (icfg.size() < 13 || fcfg.size() < 5 || ptrs.size() < 18) throw std::invalid_argument("engine config size");
+    std::vector<const void*> p(ptrs.size());
+    for (size_t k = 0; k < ptrs.size(); ++k) p[k] = reinterpret_cast<const void*>(ptrs[k]);
+    h_ = cgnn_engine_create(icfg.data(), fcfg.data(), p.data(), S(stream));
+  }
+  ~PyEngine() { if (h_) cgnn_engine_destroy(h_); }
+  int gen_blocks() { return cgnn_engine_gen_blocks(h_); }
+  int n_parts() { return cgnn_engine_n_parts(h_); }
+  void init() { cgnn_engine_init(h_); }
+  void tt() { cgnn_engine_tt(h_); }
+  void run(int kind, int steps, int chunk, bool hist) { cgnn_engine_run(h_, kind, steps, chunk, hist ? 1 : 0); }
+ private:
+  void* h_ = nullptr;
+};
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "cgnn_amd HIP kernels for MI355X (gfx950)";
+  m.def("arch", []() { return std::string("gfx950"); });
+  m.def("device_count", []() { int n = 0; if (hipGetDeviceCount(&n) != hipSuccess) return 0; return n; });
+  m.def("mmd_supported_d", &cgnn_mmd_supported_d);
+  m.def("gen_supported_h", &cgnn_gen_supported_h);
+  m.def("gen_bwd_blocks", &cgnn_gen_bwd_blocks);
+  m.def("gen_bwd_lds", &cgnn_gen_bwd_lds);
+
+  m.def("mmd", [](int mode, int D, uint64_t xhat, uint64_t data, uint64_t gp, uint64_t lp, int N, int R,
+                  int row_tiles, int n_chunks, int tpc, float gscale, uint64_t st) {
+    chk(cgnn_launch_mmd(mode, D, Pt<const float>(xhat), Pt<const float>(data), Pt<float>(gp), Pt<float>(lp),
+                        N, R, row_tiles, n_chunks, tpc, gscale, S(st)), "mmd");
+  });
+  m.def("loss_finalize", [](uint64_t lp, int n_parts, uint64_t tt, uint64_t last, uint64_t acc, float inv_n2,
+                            int flags, uint64_t hist, int hist_stride, uint64_t step, int step_off, int R,
+                            uint64_t st) {
+    chk(cgnn_launch_loss_finalize(Pt<const float>(lp), n_parts, Pt<float>(tt), Pt<float>(last), Pt<float>(acc),
+                                  inv_n2, flags, Pt<float>(hist), hist_stride, Pt<const int>(step), step_off,
+                                  R, S(st)), "loss_finalize");
+  });
+  m.def("gen_fwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t data, uint64_t xhat, uint64_t keys,
+                      uint64_t step, int off, int N, int D, int H, int R, uint64_t st) {
+    chk(cgnn_launch_gen_fwd(Pt<const int>(prog), ps, Pt<const float>(params), P, Pt<const float>(data),
+                            Pt<float>(xhat), Pt<const uint32_t>(keys), Pt<const int>(step), off, N, D, H, R,
+                            S(st)), "gen_fwd");
+  });
+  m.def("gen_bwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t xhat, uint64_t gradp, int nch,
+                      int R, uint64_t dxhat, uint64_t keys, uint64_t step, int off, int N, int D, int H,
+                      int max_in, uint64_t gpart, uint64_t st) {
+    chk(cgnn_launch_gen_bwd(Pt<const int>(prog), ps, Pt<const float>(params), P, Pt<const float>(xhat),
+                            Pt<const float>(gradp), nch, R, Pt<float>(dxhat), Pt<const uint32_t>(keys),
+                            Pt<const int>(step), off, N, D, H, max_in, Pt<float>(gpart), S(st)), "gen_bwd");
+  });
+  m.def("adam", [](uint64_t params, uint64_t mm, uint64_t vv, uint64_t gpart, int G, uint64_t prog, int ps, int P,
+                   uint64_t step, int off, float lr, float b1, float b2, float eps, int R, uint64_t st) {
+    chk(cgnn_launch_adam(Pt<float>(params), Pt<float>(mm), Pt<float>(vv), Pt<const float>(gpart), G,
+                         Pt<const int>(prog), ps, P, Pt<const int>(step), off, lr, b1, b2, eps, R, S(st)),
+        "adam");
+  });
+  m.def("init_params", [](uint64_t params, uint64_t mm, uint64_t vv, uint64_t prog, int ps, int P, uint64_t keys,
+                          float std, int R, uint64_t st) {
+    chk(cgnn_launch_init(Pt<float>(params), Pt<float>(mm), Pt<float>(vv), Pt<const int>(prog), ps, P,
+                         Pt<const uint32_t>(keys), std, R, S(st)), "init_params");
+  });
+  m.def("advance", [](uint64_t step, int dr, int dopt, uint64_t st) {
+    chk(cgnn_launch_advance(Pt<int>(step), dr, dopt, S(st)), "advance");
+  });
+
+  m.def("rff_freqs", [](uint64_t w, uint64_t keys, uint64_t step, int off, int k, int d, int n_gamma, int d_true,
+                        int R, uint64_t st) {
+    chk(rff_launch_freqs(Pt<float>(w), Pt<const uint32_t>(keys), Pt<const int>(step), off, k, d, n_gamma, d_true,
+                         R, S(st)),
+        "rff_freqs");
+  });
+  m.def("rff_fwd_bwd", [](int mode, uint64_t xhat, uint64_t data, uint64_t w, uint64_t feat, uint64_t loss,
+                          uint64_t grad, int N, int D, int F, int R, int k, float norm, uint64_t st) {
+    chk(rff_launch_fwd_bwd(mode, Pt<const float>(xhat), Pt<const float>(data), Pt<const float>(w),
+                           Pt<float>(feat), Pt<float>(loss), Pt<float>(grad), N, D, F, R, k, norm, S(st)),
+        "rff_fwd_bwd");
+  });
+
+  m.def("gnn_spmm", [](uint64_t rowptr, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, uint64_t bias,
+                       int n_rows, int F, int ld_x, int ld_y, int x_bf16, int y_bf16, int relu, uint64_t st) {
+    chk(gnn_launch_spmm(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(x), Pt<void>(y),
+                        Pt<const float>(rscale), Pt<const float>(bias), n_rows, F, ld_x, ld_y, x_bf16,
+                        y_bf16, relu, S(st)), "gnn_spmm");
+  });
+  m.def("gnn_spmm_ce", [](uint64_t rowptr, uint64_t col, uint64_t z, uint64_t rscale, uint64_t bias,
+                          uint64_t labels, uint64_t mask, uint64_t loss_part, uint64_t dlogits, uint64_t correct,
+                          int n_rows, int C, int ld, int mode, float inv_count, uint64_t st) {
+    chk(gnn_launch_spmm_ce(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(z), Pt<const float>(rscale),
+                           Pt<const float>(bias), Pt<const int>(labels), Pt<const uint8_t>(mask),
+                           Pt<float>(loss_part), Pt<void>(dlogits), Pt<float>(correct), n_rows, C, ld, mode,
+                           inv_count, S(st)), "gnn_spmm_ce");
+  });
+  m.def("gnn_adam", [](uint64_t p, uint64_t mm, uint64_t vv, uint64_t g, int n, float lr, float b1, float b2,
+                       float eps, float wd, uint64_t step, uint64_t st) {
+    chk(gnn_launch_adam(Pt<float>(p), Pt<float>(mm), Pt<float>(vv), Pt<const float>(g), n, lr, b1, b2, eps, wd,
+                        Pt<const int>(step), S(st)), "gnn_adam");
+  });
+  m.def("gnn_cast_bf16", [](uint64_t src, uint64_t dst, long n, uint64_t st) {
+    chk(gnn_launch_cast_bf16(Pt<const float>(src), Pt<void>(dst), n, S(st)), "gnn_cast_bf16");
+  });
+
+  py::class_<PyEngine>(m, "CgnnEngine")
+      .def(py::init<std::vector<int>, std::vector<float>, std::vector<uint64_t>, uint64_t>())
+      .def("gen_blocks", &PyEngine::gen_blocks)
+      .def("n_parts", &PyEngine::n_parts)
+      .def("init", &PyEngine::init)
+      .def("tt", &PyEngine::tt)
+      .def("run", &PyEngine::run, py::arg("kind"), py::arg("steps"), py::arg("chunk") = 0,
+           py::arg("hist") = false);
+}

@@ -1,0 +1,541 @@
+// CGNN device kernels for MI355X (gfx950).  One launch always serves a whole
+// batch of R independent generative models ("runs x candidates"), so the
+// reference's ~48k tiny TF session calls per search candidate
+// become a handful of fused launches per optimisation step.
+//
+//   K3/K4 mmd_rbf_kernel   fused multi-bandwidth Gaussian MMD^2: loss and the
+//                          analytic gradient wrt the generated samples, never
+//                          materialising the [2N,2N] Gram (replaces Loss.py:12-32
+//                          and its TF autodiff).
+//   K1    gen_fwd_kernel   DAG generator forward: CSR-parent gather, in-kernel
+//                          Philox noise, Linear->ReLU->Linear per node in
+//                          topological order (CGNN.py:63-90, GNN.py:64-67,
+//                          CGNN_confounders.py:66-104).
+//   K2    gen_bwd_kernel   reverse-topological backward with deterministic
+//                          LDS slab reduction of parameter gradients.
+//   K5    adam_tf1_kernel  TF1 AdamOptimizer update (epsilon outside the bias
+//                          correction) fused with the cross-workgroup gradient sum.
+//
+// Layouts (all fp32):
+//   data, xhat, dxhat : [R][D][N]    feature-major, so a wave of 64 consecutive
+//                                    samples touches 256 contiguous bytes.
+//   params, m, v      : [R][P]       per-node blocks W1[nin][H], b1[H], W2[H], b2.
+//   prog              : [R][stride]  int32 "DAG program", see engine/program.py.
+#include "cgnn_common.h"
+
+using namespace cgnn;
+
+namespace {
+
+constexpr int PROG_HDR = 4;      // n_nodes, n_params, n_conf, reserved
+constexpr int NODE_REC = 8;      // var, kind, n_par, par_off, n_cf, cf_off, param_off, n_in
+constexpr int KIND_GEN = 0;
+constexpr int KIND_OBS = 1;
+constexpr float MMD_SENTINEL = 1.0e17f;   // padded columns: exp(-g*d2) == 0 exactly
+
+// Seven bandwidths of Loss.py:10: {0.005, 0.05, 0.25, 0.5, 1, 5, 50}.
+// exp(-0.5 d2) and exp(-d2) are squares of exp(-0.25 d2); the others are one
+// v_exp_f32 each (a square costs 4 issue cycles, an exp 8 + its pre-scale 4,
+// so powering further would cost more than it saves and lose accuracy).
+__device__ __forceinline__ void rbf7(float d2, float& ks, float& w) {
+  const float L2E = 1.4426950408889634f;
+  float e1 = __builtin_amdgcn_exp2f(d2 * (-0.005f * L2E));
+  float e2 = __builtin_amdgcn_exp2f(d2 * (-0.05f * L2E));
+  float e3 = __builtin_amdgcn_exp2f(d2 * (-0.25f * L2E));
+  float e4 = e3 * e3;
+  float e5 = e4 * e4;
+  float e6 = __builtin_amdgcn_exp2f(d2 * (-5.0f * L2E));
+  float e7 = __builtin_amdgcn_exp2f(d2 * (-50.0f * L2E));
+  ks = ((e1 + e2) + (e3 + e4)) + ((e5 + e6) + e7);
+  w = ((0.005f * e1 + 0.05f * e2) + (0.25f * e3 + 0.5f * e4)) + ((e5 + 5.0f * e6) + 50.0f * e7);
+}
+
+}  // namespace
+
+// ============================================================================
+// K3/K4: fused MMD.  grid = (row_tiles, n_chunks, R), block = 256.
+//   MODE 0: train  -> loss partial + gradient partial per column chunk
+//   MODE 1: eval   -> loss partial only
+//   MODE 2: const  -> true-true block (rows and columns from `data`)
+// Each thread owns one row i of the generated block and streams 256-column
+// tiles of the joint [pred; true] column space through LDS (broadcast reads).
+// Per pair: 3D flops for distance + gradient, 5 exp + 2 squares for the kernel.
+//   grad_i += sign * w_ij * (x_j - p_i),  sign = +1 (pred col), -1 (true col)
+//   loss   += (+1 | -2) * sum_gamma exp(-gamma d2)
+// dL/dp_i = 4/N^2 * grad_i  (derivation in docs/KERNELS.md).
+// ============================================================================
+template <int D, int MODE>
+__global__ __launch_bounds__(256) void mmd_rbf_kernel(
+    const float* __restrict__ xhat, const float* __restrict__ data,
+    float* __restrict__ grad_part, float* __restrict__ loss_part,
+    int N, int R, int tiles_per_chunk, float grad_scale) {
+  constexpr int T = 256;
+  __shared__ __attribute__((aligned(16))) float s_x[T * D];
+  __shared__ float s_red[4];
+
+  const int rt = blockIdx.x, chunk = blockIdx.y, r = blockIdx.z;
+  const int n_chunks = gridDim.y, row_tiles = gridDim.x;
+  const int t = threadIdx.x;
+  const int i = rt * T + t;
+  const bool valid = i < N;
+  const size_t mbase = (size_t)r * D * N;
+  const float* P = (MODE == 2 ? data : xhat) + mbase;
+  const float* Tm = data + mbase;
+
+  float p[D], g[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    p[k] = valid ? P[(size_t)k * N + i] : 0.f;
+    g[k] = 0.f;
+  }
+  float lacc = 0.f;
+
+  const int ct = (N + T - 1) / T;               // tiles per block
+  const int n_tiles = (MODE == 2) ? ct : 2 * ct;
+  const int tile_lo = chunk * tiles_per_chunk;
+  const int tile_hi = min(n_tiles, tile_lo + tiles_per_chunk);
+
+  for (int tile = tile_lo; tile < tile_hi; ++tile) {
+    const bool is_pred = (MODE != 2) && tile < ct;
+    const float* src = is_pred ? P : Tm;
+    const int col0 = (is_pred || MODE == 2 ? tile : tile - ct) * T;
+    const int c = col0 + t;
+    __syncthreads();
+    if (c < N) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) s_x[t * D + k] = src[(size_t)k * N + c];
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) s_x[t * D + k] = MMD_SENTINEL;
+    }
+    __syncthreads();
+    const float lsign = (MODE == 2 || is_pred) ? 1.f : -2.f;
+    const float gsign = is_pred ? 1.f : -1.f;
+    float tl = 0.f;
+#pragma unroll 2
+    for (int jj = 0; jj < T; ++jj) {
+      const float* xj = s_x + jj * D;
+      float diff[D];
+      float d2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        diff[k] = xj[k] - p[k];
+        d2 = fmaf(diff[k], diff[k], d2);
+      }
+      float ks, w;
+      rbf7(d2, ks, w);
+      tl += ks;
+      if (MODE == 0) {
+        const float sw = gsign * w;
+#pragma unroll
+        for (int k = 0; k < D; ++k) g[k] = fmaf(sw, diff[k], g[k]);
+      }
+    }
+    lacc = fmaf(lsign, tl, lacc);
+  }
+
+  // deterministic block reduction of the loss partial
+  float v = valid ? lacc : 0.f;
+  v = wave_sum(v);
+  if ((t & 63) == 0) s_red[t >> 6] = v;
+  __syncthreads();
+  if (t == 0) {
+    float s = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+    loss_part[((size_t)r * n_chunks + chunk) * row_tiles + rt] = s;
+  }
+  if (MODE == 0 && valid) {
+    float* gp = grad_part + ((size_t)chunk * R + r) * D * N;
+#pragma unroll
+    for (int k = 0; k < D; ++k) gp[(size_t)k * N + i] = g[k] * grad_scale;
+  }
+}
+
+// ============================================================================
+// Loss finalize: one block per model, fixed-order sum of the partials.
+//   L = (sum_partials + tt_const[r]) * inv_n2
+//   flags bit0: accumulate into loss_acc (evaluation average)
+//   flags bit1: write raw sum into tt_const (true-true constant pass)
+// ============================================================================
+__global__ __launch_bounds__(256) void loss_finalize_kernel(
+    const float* __restrict__ loss_part, int n_parts, float* __restrict__ tt_const,
+    float* __restrict__ loss_last, float* __restrict__ loss_acc, float inv_n2, int flags,
+    float* __restrict__ loss_hist, int hist_stride, const int* __restrict__ step_base, int step_off) {
+  __shared__ float s_red[4];
+  const int r = blockIdx.x;
+  const float* lp = loss_part + (size_t)r * n_parts;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < n_parts; k += blockDim.x) s += lp[k];
+  s = block_sum(s, s_red);
+  if (threadIdx.x == 0) {
+    if (flags & 2) {
+      tt_const[r] = s;
+    } else {
+      float L = (s + tt_const[r]) * inv_n2;
+      loss_last[r] = L;
+      if (flags & 1) loss_acc[r] += L;
+      if (loss_hist) {
+        int st = step_off + (step_base ? step_base[1] : 0);
+        if (st < hist_stride) loss_hist[(size_t)r * hist_stride + st] = L;
+      }
+    }
+  }
+}
+
+// ============================================================================
+// K1: generator forward.  grid = (ceil(N/256), R), one thread per sample.
+// Weights are read with wave-uniform addresses (scalar loads / broadcast).
+// ============================================================================
+template <int H>
+__global__ __launch_bounds__(256) void gen_fwd_kernel(
+    const int* __restrict__ prog, int prog_stride, const float* __restrict__ params, int P,
+    const float* __restrict__ data, float* __restrict__ xhat,
+    const uint32_t* __restrict__ keys, const int* __restrict__ step_base, int step_off,
+    int N, int D, int Hrt) {
+  const int r = blockIdx.y;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int* pr = prog + (size_t)r * prog_stride;
+  const int nn = pr[0];
+  const uint32_t step = (uint32_t)(step_base[0] + step_off);
+  const uint32_t k0 = keys[2 * r], k1 = keys[2 * r + 1];
+  const float* th = params + (size_t)r * P;
+  float* xr = xhat + (size_t)r * D * N;
+  const float* dr = data + (size_t)r * D * N;
+  const int Hh = (H > 0) ? H : Hrt;
+
+  for (int kk = 0; kk < nn; ++kk) {
+    const int* nd = pr + PROG_HDR + kk * NODE_REC;
+    const int var = nd[0];
+    if (nd[1] == KIND_OBS) {
+      xr[(size_t)var * N + n] = dr[(size_t)var * N + n];
+      continue;
+    }
+    const int npar = nd[2], paroff = nd[3], ncf = nd[4], cfoff = nd[5], poff = nd[6];
+    const int nin = npar + 1 + ncf;
+    const float* W1 = th + poff;
+    const float* b1 = W1 + (size_t)nin * Hh;
+    const float* W2 = b1 + Hh;
+    const float b2 = W2[Hh];
+    float pre[H > 0 ? H : 1];
+    if (H > 0) {
+#pragma unroll
+      for (int q = 0; q < H; ++q) pre[q] = b1[q];
+      for (int j = 0; j < npar; ++j) {
+        const float x = xr[(size_t)pr[paroff + j] * N + n];
+#pragma unroll
+        for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[j * H + q], x, pre[q]);
+      }
+      {
+        const float e = rng_normal(k0, k1, (uint32_t)n, (uint32_t)var, step, RNG_NODE_NOISE);
+#pragma unroll
+        for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[npar * H + q], e, pre[q]);
+      }
+      for (int c = 0; c < ncf; ++c) {
+        const float e = rng_normal(k0, k1, (uint32_t)n, (uint32_t)pr[cfoff + c], step, RNG_CONF_NOISE);
+#pragma unroll
+        for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[(npar + 1 + c) * H + q], e, pre[q]);
+      }
+      float out = b2;
+#pragma unroll
+      for (int q = 0; q < H; ++q) out = fmaf(W2[q], fmaxf(pre[q], 0.f), out);
+      xr[(size_t)var * N + n] = out;
+    } else {
+      // generic hidden width: hidden unit outer loop (no register array)
+      float out = b2;
+      const float e0 = rng_normal(k0, k1, (uint32_t)n, (uint32_t)var, step, RNG_NODE_NOISE);
+      for (int q = 0; q < Hh; ++q) {
+        float a = b1[q];
+        for (int j = 0; j < npar; ++j) a = fmaf(W1[j * Hh + q], xr[(size_t)pr[paroff + j] * N + n], a);
+        a = fmaf(W1[npar * Hh + q], e0, a);
+        for (int c = 0; c < ncf; ++c)
+          a = fmaf(W1[(npar + 1 + c) * Hh + q],
+                   rng_normal(k0, k1, (uint32_t)n, (uint32_t)pr[cfoff + c], step, RNG_CONF_NOISE), a);
+        out = fmaf(W2[q], fmaxf(a, 0.f), out);
+      }
+      xr[(size_t)var * N + n] = out;
+    }
+  }
+}
+
+// ============================================================================
+// K2: generator backward.  grid = (G, R), block = BS samples (one per thread).
+// Per node (reverse topological order):
+//   1. each thread recomputes inputs (parents from xhat, noise from Philox),
+//      the pre-activation and dh_q = g * W2_q * [pre_q > 0]; pushes
+//      dL/dparent = W1 dh into dxhat of the parents (own sample -> no race);
+//   2. the block reduces the per-sample outer products over its BS samples
+//      from LDS in a fixed order and writes one partial slab
+//      gpart[r][blk][param] -- no atomics, bitwise reproducible.
+// LDS: s_in [BS][MI+1] (inputs + bias column), s_dh/s_relu [BS][H+1], s_g [BS].
+// ============================================================================
+template <int H, int BS>
+__global__ __launch_bounds__(BS) void gen_bwd_kernel(
+    const int* __restrict__ prog, int prog_stride, const float* __restrict__ params, int P,
+    const float* __restrict__ xhat, const float* __restrict__ grad_part, int n_chunks, int R,
+    float* __restrict__ dxhat, const uint32_t* __restrict__ keys,
+    const int* __restrict__ step_base, int step_off, int N, int D, int max_in,
+    float* __restrict__ gpart) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int SI = max_in + 2;        // odd-ish stride -> conflict-free row access
+  const int SH = H + 1;
+  float* s_in = smem;
+  float* s_dh = s_in + BS * SI;
+  float* s_relu = s_dh + BS * SH;
+  float* s_g = s_relu + BS * SH;
+
+  const int r = blockIdx.y, blk = blockIdx.x, G = gridDim.x;
+  const int t = threadIdx.x;
+  const int n = blk * BS + t;
+  const bool valid = n < N;
+  const int* pr = prog + (size_t)r * prog_stride;
+  const int nn = pr[0];
+  const uint32_t step = (uint32_t)(step_base[0] + step_off);
+  const uint32_t k0 = keys[2 * r], k1 = keys[2 * r + 1];
+  const float* th = params + (size_t)r * P;
+  const float* xr = xhat + (size_t)r * D * N;
+  float* dx = dxhat + (size_t)r * D * N;
+  float* gp = gpart + ((size_t)r * G + blk) * P;
+
+  // dL/dxhat from the MMD kernel: fixed-order sum over column chunks
+  if (valid) {
+    for (int v = 0; v < D; ++v) {
+      float s = 0.f;
+      for (int c = 0; c < n_chunks; ++c) s += grad_part[(((size_t)c * R + r) * D + v) * N + n];
+      dx[(size_t)v * N + n] = s;
+    }
+  }
+
+  for (int kk = nn - 1; kk >= 0; --kk) {
+    const int* nd = pr + PROG_HDR + kk * NODE_REC;
+    if (nd[1] == KIND_OBS) continue;
+    const int var = nd[0], npar = nd[2], paroff = nd[3], ncf = nd[4], cfoff = nd[5], poff = nd[6];
+    const int nin = npar + 1 + ncf;
+    const float* W1 = th + poff;
+    const float* b1 = W1 + (size_t)nin * H;
+    const float* W2 = b1 + H;
+
+    float* my_in = s_in + t * SI;
+    float pre[H];
+#pragma unroll
+    for (int q = 0; q < H; ++q) pre[q] = b1[q];
+    for (int j = 0; j < nin; ++j) {
+      float x;
+      if (j < npar) {
+        x = valid ? xr[(size_t)pr[paroff + j] * N + n] : 0.f;
+      } else if (j == npar) {
+        x = rng_normal(k0, k1, (uint32_t)n, (uint32_t)var, step, RNG_NODE_NOISE);
+      } else {
+        x = rng_normal(k0, k1, (uint32_t)n, (uint32_t)pr[cfoff + (j - npar - 1)], step, RNG_CONF_NOISE);
+      }
+      if (!valid) x = 0.f;
+      my_in[j] = x;
+#pragma unroll
+      for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[j * H + q], x, pre[q]);
+    }
+    my_in[nin] = valid ? 1.f : 0.f;   // bias column
+    const float gout = valid ? dx[(size_t)var * N + n] : 0.f;
+    float dh[H];
+#pragma unroll
+    for (int q = 0; q < H; ++q) {
+      const bool on = pre[q] > 0.f;
+      dh[q] = on ? gout * W2[q] : 0.f;
+      s_dh[t * SH + q] = dh[q];
+      s_relu[t * SH + q] = on ? pre[q] : 0.f;
+    }
+    s_g[t] = gout;
+    if (valid) {
+      for (int j = 0; j < npar; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < H; ++q) s = fmaf(W1[j * H + q], dh[q], s);
+        dx[(size_t)pr[paroff + j] * N + n] += s;
+      }
+    }
+    __syncthreads();
+    const int n_w1b1 = (nin + 1) * H;
+    const int np = n_w1b1 + H + 1;
+    for (int pidx = t; pidx < np; pidx += BS) {
+      float acc = 0.f;
+      if (pidx < n_w1b1) {
+        const int j = pidx / H, q = pidx - (pidx / H) * H;
+        for (int s = 0; s < BS; ++s) acc = fmaf(s_in[s * SI + j], s_dh[s * SH + q], acc);
+      } else if (pidx < n_w1b1 + H) {
+        const int q = pidx - n_w1b1;
+        for (int s = 0; s < BS; ++s) acc = fmaf(s_relu[s * SH + q], s_g[s], acc);
+      } else {
+        for (int s = 0; s < BS; ++s) acc += s_g[s];
+      }
+      gp[poff + pidx] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================================
+// K5: TF1 Adam with fused fixed-order reduction of the G gradient slabs.
+//   lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t);  theta -= lr_t * m / (sqrt(v) + eps)
+// grid = (ceil(P/256), R)
+// ============================================================================
+__global__ __launch_bounds__(256) void adam_tf1_kernel(
+    float* __restrict__ params, float* __restrict__ m, float* __restrict__ v,
+    const float* __restrict__ gpart, int G, const int* __restrict__ prog, int prog_stride, int P,
+    const int* __restrict__ step_base, int step_off, float lr, float beta1, float beta2, float eps) {
+  const int r = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int Pr = prog[(size_t)r * prog_stride + 1];
+  if (p >= Pr) return;
+  float g = 0.f;
+  const float* gp = gpart + (size_t)r * G * P + p;
+  for (int k = 0; k < G; ++k) g += gp[(size_t)k * P];
+  const float tstep = (float)(step_base[1] + step_off + 1);   // optimizer step count
+  const float lr_t = lr * sqrtf(1.f - powf(beta2, tstep)) / (1.f - powf(beta1, tstep));
+  const size_t idx = (size_t)r * P + p;
+  const float mm = beta1 * m[idx] + (1.f - beta1) * g;
+  const float vv = beta2 * v[idx] + (1.f - beta2) * g * g;
+  m[idx] = mm;
+  v[idx] = vv;
+  params[idx] -= lr_t * mm / (sqrtf(vv) + eps);
+}
+
+// Parameter init N(0, std^2) from Philox (weights AND biases, CGNN.py:71-74).
+__global__ void init_params_kernel(float* __restrict__ params, float* __restrict__ m,
+                                   float* __restrict__ v, const int* __restrict__ prog,
+                                   int prog_stride, int P, const uint32_t* __restrict__ keys,
+                                   float init_std) {
+  const int r = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const int Pr = prog[(size_t)r * prog_stride + 1];
+  const size_t idx = (size_t)r * P + p;
+  params[idx] = p < Pr ? init_std * rng_normal(keys[2 * r], keys[2 * r + 1], (uint32_t)p, 0u, 0u,
+                                               RNG_PARAM_INIT)
+                       : 0.f;
+  m[idx] = 0.f;
+  v[idx] = 0.f;
+}
+
+// step_base[0]: RNG step (advances every train AND eval step);
+// step_base[1]: optimizer step (advances on train steps only).
+__global__ void advance_step_kernel(int* step_base, int d_rng, int d_opt) {
+  step_base[0] += d_rng;
+  step_base[1] += d_opt;
+}
+
+// ============================================================================
+// host-side launchers (C ABI, called from the pybind11 module)
+// ============================================================================
+#define CGNN_CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return (int)e_; } while (0)
+
+template <int D>
+static int launch_mmd_d(int mode, const float* xhat, const float* data, float* gpart, float* lpart,
+                        int N, int R, int row_tiles, int n_chunks, int tpc, float gscale,
+                        hipStream_t st) {
+  dim3 grid(row_tiles, n_chunks, R), block(256);
+  if (mode == 0) hipLaunchKernelGGL((mmd_rbf_kernel<D, 0>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
+  else if (mode == 1) hipLaunchKernelGGL((mmd_rbf_kernel<D, 1>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
+  else hipLaunchKernelGGL((mmd_rbf_kernel<D, 2>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
+  return (int)hipGetLastError();
+}
+
+extern "C" int cgnn_mmd_supported_d(int D) {
+  switch (D) { case 1: case 2: case 3: case 4: case 6: case 8: case 12: case 16: case 20: case 24:
+    case 32: case 48: case 64: return 1; default: return 0; }
+}
+
+extern "C" int cgnn_launch_mmd(int mode, int D, const float* xhat, const float* data, float* gpart,
+                               float* lpart, int N, int R, int row_tiles, int n_chunks, int tpc,
+                               float gscale, hipStream_t st) {
+  switch (D) {
+#define CASE_D(d) case d: return launch_mmd_d<d>(mode, xhat, data, gpart, lpart, N, R, row_tiles, n_chunks, tpc, gscale, st);
+    CASE_D(1) CASE_D(2) CASE_D(3) CASE_D(4) CASE_D(6) CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20)
+    CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64)
+#undef CASE_D
+    default: return -1;
+  }
+}
+
+extern "C" int cgnn_launch_loss_finalize(const float* lpart, int n_parts, float* tt, float* last,
+                                         float* acc, float inv_n2, int flags, float* hist,
+                                         int hist_stride, const int* step_base, int step_off,
+                                         int R, hipStream_t st) {
+  hipLaunchKernelGGL(loss_finalize_kernel, dim3(R), dim3(256), 0, st, lpart, n_parts, tt, last, acc,
+                     inv_n2, flags, hist, hist_stride, step_base, step_off);
+  return (int)hipGetLastError();
+}
+
+#define CGNN_H_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(16) X(20) X(24) X(30) X(32) \
+  X(40) X(48) X(50) X(64)
+
+extern "C" int cgnn_gen_supported_h(int H) {
+  switch (H) {
+#define CASE_H(h) case h: return 1;
+    CGNN_H_LIST(CASE_H)
+#undef CASE_H
+    default: return 0;
+  }
+}
+
+extern "C" int cgnn_launch_gen_fwd(const int* prog, int prog_stride, const float* params, int P,
+                                   const float* data, float* xhat, const uint32_t* keys,
+                                   const int* step_base, int step_off, int N, int D, int H, int R,
+                                   hipStream_t st) {
+  dim3 grid((N + 255) / 256, R), block(256);
+  switch (H) {
+#define CASE_H(h) case h: hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, 0, st, prog, prog_stride, params, P, data, xhat, keys, step_base, step_off, N, D, H); break;
+    CGNN_H_LIST(CASE_H)
+#undef CASE_H
+    default:
+      hipLaunchKernelGGL((gen_fwd_kernel<0>), grid, block, 0, st, prog, prog_stride, params, P, data,
+                         xhat, keys, step_base, step_off, N, D, H);
+  }
+  return (int)hipGetLastError();
+}
+
+constexpr int GEN_BWD_BS = 128;
+
+extern "C" int cgnn_gen_bwd_blocks(int N) { return (N + GEN_BWD_BS - 1) / GEN_BWD_BS; }
+
+extern "C" size_t cgnn_gen_bwd_lds(int H, int max_in) {
+  return sizeof(float) * ((size_t)GEN_BWD_BS * (max_in + 2) + 2 * (size_t)GEN_BWD_BS * (H + 1) + GEN_BWD_BS);
+}
+
+extern "C" int cgnn_launch_gen_bwd(const int* prog, int prog_stride, const float* params, int P,
+                                   const float* xhat, const float* gradp, int n_chunks, int R,
+                                   float* dxhat, const uint32_t* keys, const int* step_base,
+                                   int step_off, int N, int D, int H, int max_in, float* gpart,
+                                   hipStream_t st) {
+  const int G = cgnn_gen_bwd_blocks(N);
+  dim3 grid(G, R), block(GEN_BWD_BS);
+  const size_t lds = cgnn_gen_bwd_lds(H, max_in);
+  if (lds > 160 * 1024) return -2;
+  switch (H) {
+#define CASE_H(h) case h: hipLaunchKernelGGL((gen_bwd_kernel<h, GEN_BWD_BS>), grid, block, lds, st, prog, prog_stride, params, P, xhat, gradp, n_chunks, R, dxhat, keys, step_base, step_off, N, D, max_in, gpart); break;
+    CGNN_H_LIST(CASE_H)
+#undef CASE_H
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int cgnn_launch_adam(float* params, float* m, float* v, const float* gpart, int G,
+                                const int* prog, int prog_stride, int P, const int* step_base,
+                                int step_off, float lr, float b1, float b2, float eps, int R,
+                                hipStream_t st) {
+  dim3 grid((P + 255) / 256, R), block(256);
+  hipLaunchKernelGGL(adam_tf1_kernel, grid, block, 0, st, params, m, v, gpart, G, prog, prog_stride,
+                     P, step_base, step_off, lr, b1, b2, eps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int cgnn_launch_init(float* params, float* m, float* v, const int* prog, int prog_stride,
+                                int P, const uint32_t* keys, float init_std, int R, hipStream_t st) {
+  dim3 grid((P + 255) / 256, R), block(256);
+  hipLaunchKernelGGL(init_params_kernel, grid, block, 0, st, params, m, v, prog, prog_stride, P, keys,
+                     init_std);
+  return (int)hipGetLastError();
+}
+
+extern "C" int cgnn_launch_advance(int* step_base, int d_rng, int d_opt, hipStream_t st) {
+  hipLaunchKernelGGL(advance_step_kernel, dim3(1), dim3(1), 0, st, step_base, d_rng, d_opt);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,285 @@
+// GNN track (beyond the reference, SURVEY §0 Phase B): sparse message passing
+// kernels for MI355X.
+//
+//   spmm_kernel     Y[i,:] = act( rscale[i] * sum_{j in N(i)} X[j,:] + bias )
+//                   CSR neighbour aggregate (gather-sum).  Symmetric GCN
+//                   normalisation D^-1/2 (A+I) D^-1/2 is split into a row scale
+//                   here and a column scale folded into the producer of X, so
+//                   no per-edge value is ever read: the kernel streams only
+//                   col[] and the gathered rows.
+//   spmm_ce_kernel  layer-2 aggregate fused with bias, log-softmax,
+//                   cross-entropy, accuracy counting and the loss gradient
+//                   (pre-scaled by rscale for the backward SpMM).
+//
+// Mapping: a sub-group of L lanes owns one row; each lane owns 8 consecutive
+// features (one 16-byte bf16 load per gathered row).  L = 16 covers F <= 128
+// (4 rows per wave64), L = 8 covers F <= 64 (8 rows per wave64).  The L column
+// indices of the next L edges are fetched with one coalesced load and
+// broadcast inside the sub-group with ds_bpermute; four gathered rows are kept
+// in flight per lane.  Accumulation is fp32; storage is bf16.
+#include "cgnn_common.h"
+
+using namespace cgnn;
+
+namespace {
+
+struct bf16x8 { uint32_t w[4]; };
+
+__device__ __forceinline__ void bf16x8_to_f32(const uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint32_t f32_to_bf16_rne(float x) {
+  uint32_t u = __float_as_uint(x);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+__device__ __forceinline__ uint4 f32x8_to_bf16(const float* f) {
+  uint4 o;
+  o.x = f32_to_bf16_rne(f[0]) | (f32_to_bf16_rne(f[1]) << 16);
+  o.y = f32_to_bf16_rne(f[2]) | (f32_to_bf16_rne(f[3]) << 16);
+  o.z = f32_to_bf16_rne(f[4]) | (f32_to_bf16_rne(f[5]) << 16);
+  o.w = f32_to_bf16_rne(f[6]) | (f32_to_bf16_rne(f[7]) << 16);
+  return o;
+}
+
+template <bool XBF>
+__device__ __forceinline__ void load8(const void* X, size_t off, float* f) {
+  if (XBF) {
+    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(X) + off);
+    bf16x8_to_f32(v, f);
+  } else {
+    const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + off);
+    const float4 a = p[0], b = p[1];
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+}
+
+// Sum the rows X[col[e]] for e in [e0, e1) into acc (8 features at f0).
+template <int L, bool XBF>
+__device__ __forceinline__ void gather_sum(const int* __restrict__ col, const void* __restrict__ X,
+                                           int e0, int e1, int ldx, int f0, bool fv, int sub_base,
+                                           int sl, float* acc) {
+  for (int e = e0; e < e1; e += L) {
+    const int myj = (e + sl < e1) ? col[e + sl] : 0;
+    const int cnt = min(L, e1 - e);
+    int k = 0;
+    for (; k + 4 <= cnt; k += 4) {
+      const int j0 = __shfl(myj, sub_base + k + 0, 64);
+      const int j1 = __shfl(myj, sub_base + k + 1, 64);
+      const int j2 = __shfl(myj, sub_base + k + 2, 64);
+      const int j3 = __shfl(myj, sub_base + k + 3, 64);
+      if (fv) {
+        float a[8], b[8], c[8], d[8];
+        load8<XBF>(X, (size_t)j0 * ldx + f0, a);
+        load8<XBF>(X, (size_t)j1 * ldx + f0, b);
+        load8<XBF>(X, (size_t)j2 * ldx + f0, c);
+        load8<XBF>(X, (size_t)j3 * ldx + f0, d);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += (a[q] + b[q]) + (c[q] + d[q]);
+      }
+    }
+    for (; k < cnt; ++k) {
+      const int j = __shfl(myj, sub_base + k, 64);
+      if (fv) {
+        float a[8];
+        load8<XBF>(X, (size_t)j * ldx + f0, a);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += a[q];
+      }
+    }
+  }
+}
+
+}  // namespace
+
+template <int L, bool XBF, bool YBF>
+__global__ __launch_bounds__(256) void spmm_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
+    void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
+    int n_rows, int F, int ldx, int ldy, int relu) {
+  constexpr int RPW = 64 / L;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / L, sl = lane - sub * L;
+  const int row = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
+  const bool rv = row < n_rows;
+  const int f0 = sl * 8;
+  const bool fv = rv && f0 < F;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
+  gather_sum<L, XBF>(col, X, e0, e1, ldx, f0, fv, sub * L, sl, acc);
+  if (!rv || f0 >= ldy) return;
+  const float rs = rscale ? rscale[row] : 1.f;
+  float y[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int f = f0 + q;
+    float v = acc[q] * rs + ((bias && f < F) ? bias[f] : 0.f);
+    if (relu) v = fmaxf(v, 0.f);
+    y[q] = f < F ? v : 0.f;
+  }
+  if (YBF) {
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
+  } else {
+    float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(Y) + (size_t)row * ldy + f0);
+    p[0] = make_float4(y[0], y[1], y[2], y[3]);
+    p[1] = make_float4(y[4], y[5], y[6], y[7]);
+  }
+}
+
+// Layer-2 aggregate + bias + log-softmax + NLL.  L = 8 lanes per row, C <= 64.
+//   mask[i]: 0 = unused, 1 = train, 2 = valid, 3 = test
+//   stats[block][4] = {sum train loss, #correct train, #correct valid, #correct test}
+//   mode 0: also write G[i,:] = rscale[i] * (softmax - onehot) / n_train  (train rows)
+__global__ __launch_bounds__(256) void spmm_ce_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Z,
+    const float* __restrict__ rscale, const float* __restrict__ bias, const int* __restrict__ labels,
+    const uint8_t* __restrict__ mask, float* __restrict__ stats, void* __restrict__ G,
+    int n_rows, int C, int ld, int mode, float inv_count) {
+  constexpr int L = 8, RPW = 8;
+  __shared__ float s_red[4][4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int sub = lane / L, sl = lane - sub * L;
+  const int row = (blockIdx.x * (blockDim.x >> 6) + wid) * RPW + sub;
+  const bool rv = row < n_rows;
+  const int f0 = sl * 8;
+  const bool fv = rv && f0 < C;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
+  gather_sum<L, true>(col, Z, e0, e1, ld, f0, fv, sub * L, sl, acc);
+
+  const float rs = rv ? rscale[row] : 0.f;
+  float lg[8];
+  float mx = -INFINITY;
+  int amax = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int c = f0 + q;
+    lg[q] = (c < C) ? acc[q] * rs + bias[c] : -INFINITY;
+    if (lg[q] > mx) { mx = lg[q]; amax = c; }
+  }
+  // arg-max / max over the 8-lane sub-group (ties -> lowest class id)
+#pragma unroll
+  for (int off = 1; off < L; off <<= 1) {
+    const float om = __shfl_xor(mx, off, 64);
+    const int oa = __shfl_xor(amax, off, 64);
+    if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) se += (f0 + q < C) ? __expf(lg[q] - mx) : 0.f;
+#pragma unroll
+  for (int off = 1; off < L; off <<= 1) se += __shfl_xor(se, off, 64);
+  const float lse = mx + __logf(se);
+  const int y = rv ? labels[row] : -1;
+  const int split = rv ? (int)mask[row] : 0;
+  float my_loss = 0.f;
+  if (split == 1 && y >= f0 && y < f0 + 8) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) if (f0 + q == y) my_loss = lse - lg[q];
+  }
+  if (mode == 0 && rv && f0 < ld) {
+    float gq[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = f0 + q;
+      float g = 0.f;
+      if (split == 1 && c < C) g = (__expf(lg[q] - lse) - (c == y ? 1.f : 0.f)) * inv_count * rs;
+      gq[q] = g;
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(G) + (size_t)row * ld + f0) = f32x8_to_bf16(gq);
+  }
+  // statistics: one contribution per row (sub-group lane 0), fixed-order block reduce
+  const bool lead = rv && sl == 0;
+  const float hit = (lead && amax == y) ? 1.f : 0.f;
+  float v0 = wave_sum(my_loss);
+  float v1 = wave_sum(split == 1 ? hit : 0.f);
+  float v2 = wave_sum(split == 2 ? hit : 0.f);
+  float v3 = wave_sum(split == 3 ? hit : 0.f);
+  if (lane == 0) { s_red[wid][0] = v0; s_red[wid][1] = v1; s_red[wid][2] = v2; s_red[wid][3] = v3; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    stats[(size_t)blockIdx.x * 4 + k] = (s_red[0][k] + s_red[1][k]) + (s_red[2][k] + s_red[3][k]);
+  }
+}
+
+// PyTorch-semantics Adam (bias-corrected, eps inside) with optional decoupled
+// weight decay, over one flat fp32 parameter buffer.  t = *step + 1.
+__global__ void gnn_adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                const float* __restrict__ g, int n, float lr, float b1, float b2,
+                                float eps, float wd, const int* __restrict__ step) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float t = (float)(*step + 1);
+  const float gi = g[i];
+  const float mi = b1 * m[i] + (1.f - b1) * gi;
+  const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float mh = mi / (1.f - powf(b1, t));
+  const float vh = vi / (1.f - powf(b2, t));
+  p[i] -= lr * (mh / (sqrtf(vh) + eps) + wd * p[i]);
+}
+
+__global__ void cast_bf16_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (uint16_t)f32_to_bf16_rne(src[i]);
+}
+
+// ---------------------------------------------------------------- launchers
+template <int L>
+static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
+                         const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
+                         int relu, hipStream_t st) {
+  constexpr int RPB = 4 * (64 / L);   // rows per 256-thread block
+  dim3 grid((n_rows + RPB - 1) / RPB), block(256);
+  if (xbf && ybf) hipLaunchKernelGGL((spmm_kernel<L, true, true>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu);
+  else if (xbf) hipLaunchKernelGGL((spmm_kernel<L, true, false>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu);
+  else if (ybf) hipLaunchKernelGGL((spmm_kernel<L, false, true>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu);
+  else hipLaunchKernelGGL((spmm_kernel<L, false, false>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X, void* Y,
+                               const float* rscale, const float* bias, int n_rows, int F, int ldx,
+                               int ldy, int xbf, int ybf, int relu, hipStream_t st) {
+  if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
+  if (F <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
+  if (F <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
+  if (F <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
+  if (F <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
+  return -1;
+}
+
+extern "C" int gnn_spmm_ce_blocks(int n_rows) { return (n_rows + 31) / 32; }
+
+extern "C" int gnn_launch_spmm_ce(const int* rowptr, const int* col, const void* Z,
+                                  const float* rscale, const float* bias, const int* labels,
+                                  const uint8_t* mask, float* stats, void* G, float* unused,
+                                  int n_rows, int C, int ld, int mode, float inv_count,
+                                  hipStream_t st) {
+  (void)unused;
+  if (C > 64 || (ld % 8) || C > ld) return -3;
+  hipLaunchKernelGGL(spmm_ce_kernel, dim3(gnn_spmm_ce_blocks(n_rows)), dim3(256), 0, st, rowptr, col,
+                     Z, rscale, bias, labels, mask, stats, G, n_rows, C, ld, mode, inv_count);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_launch_adam(float* p, float* m, float* v, const float* g, int n, float lr,
+                               float b1, float b2, float eps, float wd, const int* step,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(gnn_adam_kernel, dim3((n + 255) / 256), dim3(256), 0, st, p, m, v, g, n, lr, b1,
+                     b2, eps, wd, step);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_launch_cast_bf16(const float* src, void* dst, long n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src,
+                     (uint16_t*)dst, n);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,355 @@
+// cgnn_amd._rt -- host C++ runtime (no GPU dependency, builds and runs on CPU).
+//
+//  * dag_program      compiles one causal DAG (+ optional confounder skeleton)
+//                     into the int32 "DAG program" the HIP generator kernels
+//                     execute (layout documented in engine/program.py).  The
+//                     generation order reproduces the reference's sweep
+//                     (CGNN.py:63-84): repeated passes over the variable list,
+//                     emitting every variable whose parents are all generated.
+//  * is_acyclic / topo_order / canonical_hash   graph algorithms used by the
+//                     structure searches (fix for SURVEY §2.6 B11: hash of the
+//                     sorted edge list instead of list-of-dict comparisons).
+//  * csr_from_edges   parallel counting-sort CSR builder (optional symmetrise,
+//                     self loops, duplicate removal).
+//  * synthetic_graph  ogbn-shaped random graph with planted communities and a
+//                     power-law-ish degree profile (Phase B benchmarks; there is
+//                     no network access for the real datasets).
+//  * sample_neighbors GraphSAGE-style layer-wise uniform neighbour sampling
+//                     producing per-layer CSR blocks.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <omp.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <numeric>
+#include <random>
+#include <unordered_map>
+#include <cmath>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+using i32 = int32_t;
+using i64 = int64_t;
+
+namespace {
+
+constexpr int PROG_HDR = 4;
+constexpr int NODE_REC = 8;
+
+// splitmix64: cheap, well-mixed stateless hash used for deterministic sampling
+inline uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+std::vector<int> sweep_order(int n, const std::vector<std::vector<int>>& parents,
+                             const std::vector<int>& list_order) {
+  std::vector<char> done(n, 0);
+  std::vector<int> order;
+  order.reserve(n);
+  while ((int)order.size() < n) {
+    bool progressed = false;
+    for (int v : list_order) {
+      if (done[v]) continue;
+      bool ok = true;
+      for (int p : parents[v]) if (!done[p]) { ok = false; break; }
+      if (ok) { done[v] = 1; order.push_back(v); progressed = true; }
+    }
+    if (!progressed) throw std::invalid_argument("dag_program: graph is cyclic");
+  }
+  return order;
+}
+
+}  // namespace
+
+// parents[v]  : parent variable indices of v (in the order they feed the MLP)
+// kinds[v]    : 0 generated, 1 observed (clamped to data)
+// confs[v]    : confounder-noise ids appended after the own noise
+// list_order  : the variable order of the reference's sweep
+// returns (program int32[], n_params, max_in)
+py::tuple dag_program(int n_vars, const std::vector<std::vector<int>>& parents,
+                      const std::vector<int>& kinds, const std::vector<std::vector<int>>& confs,
+                      int H, std::vector<int> list_order, int n_conf) {
+  if ((int)parents.size() != n_vars || (int)kinds.size() != n_vars || (int)confs.size() != n_vars)
+    throw std::invalid_argument("dag_program: size mismatch");
+  if (list_order.empty()) { list_order.resize(n_vars); std::iota(list_order.begin(), list_order.end(), 0); }
+  for (int v = 0; v < n_vars; ++v)
+    for (int p : parents[v])
+      if (p < 0 || p >= n_vars) throw std::invalid_argument("dag_program: parent out of range");
+  const std::vector<int> order = sweep_order(n_vars, parents, list_order);
+  size_t pool = 0;
+  for (int v = 0; v < n_vars; ++v) pool += parents[v].size() + confs[v].size();
+  std::vector<i32> prog(PROG_HDR + (size_t)NODE_REC * n_vars + pool, 0);
+  int pool_off = PROG_HDR + NODE_REC * n_vars;
+  int param_off = 0, max_in = 0;
+  for (int k = 0; k < n_vars; ++k) {
+    const int v = order[k];
+    i32* rec = prog.data() + PROG_HDR + (size_t)k * NODE_REC;
+    const int npar = (int)parents[v].size(), ncf = (int)confs[v].size();
+    rec[0] = v;
+    rec[1] = kinds[v];
+    rec[2] = npar;
+    rec[3] = pool_off;
+    for (int j = 0; j < npar; ++j) prog[pool_off++] = parents[v][j];
+    rec[4] = ncf;
+    rec[5] = pool_off;
+    for (int j = 0; j < ncf; ++j) prog[pool_off++] = confs[v][j];
+    const int nin = npar + 1 + ncf;
+    rec[7] = nin;
+    if (kinds[v] == 0) {
+      rec[6] = param_off;
+      param_off += (nin + 2) * H + 1;
+      max_in = std::max(max_in, nin);
+    } else {
+      rec[6] = -1;
+    }
+  }
+  prog[0] = n_vars;
+  prog[1] = param_off;
+  prog[2] = n_conf;
+  prog[3] = max_in;
+  py::array_t<i32> arr(prog.size());
+  std::copy(prog.begin(), prog.end(), arr.mutable_data());
+  return py::make_tuple(arr, param_off, max_in);
+}
+
+bool is_acyclic(int n, const std::vector<std::pair<int, int>>& edges) {
+  std::vector<int> indeg(n, 0);
+  std::vector<std::vector<int>> succ(n);
+  for (auto& e : edges) { succ[e.first].push_back(e.second); indeg[e.second]++; }
+  std::vector<int> q;
+  for (int v = 0; v < n; ++v) if (!indeg[v]) q.push_back(v);
+  size_t seen = 0;
+  while (!q.empty()) {
+    int v = q.back(); q.pop_back(); ++seen;
+    for (int w : succ[v]) if (--indeg[w] == 0) q.push_back(w);
+  }
+  return seen == (size_t)n;
+}
+
+uint64_t canonical_hash(std::vector<std::pair<int, int>> edges) {
+  std::sort(edges.begin(), edges.end());
+  edges.erase(std::unique(edges.begin(), edges.end()), edges.end());
+  uint64_t h = 0x243F6A8885A308D3ull ^ edges.size();
+  for (auto& e : edges) h = mix64(h ^ (((uint64_t)(uint32_t)e.first << 32) | (uint32_t)e.second));
+  return h;
+}
+
+// CSR (rowptr int64? no: int32 indices, int64 rowptr when nnz >= 2^31)
+py::tuple csr_from_edges(i64 n, py::array_t<i64, py::array::c_style | py::array::forcecast> src_a,
+                         py::array_t<i64, py::array::c_style | py::array::forcecast> dst_a,
+                         bool symmetric, bool self_loops, bool dedup) {
+  const i64 m = src_a.size();
+  if (dst_a.size() != m) throw std::invalid_argument("csr_from_edges: size mismatch");
+  const i64* src = src_a.data();
+  const i64* dst = dst_a.data();
+  const int nt = omp_get_max_threads();
+  const i64 tot = (symmetric ? 2 * m : m);
+  std::vector<i64> deg(n + 1, 0);
+  {
+    std::vector<std::vector<i64>> local(nt, std::vector<i64>(n, 0));
+#pragma omp parallel for schedule(static)
+    for (i64 e = 0; e < m; ++e) {
+      auto& d = local[omp_get_thread_num()];
+      const i64 s = src[e], t = dst[e];
+      if (s < 0 || s >= n || t < 0 || t >= n) continue;
+      if (s == t) continue;   // self loops handled separately
+      d[s]++;
+      if (symmetric) d[t]++;
+    }
+    for (int t = 0; t < nt; ++t)
+      for (i64 v = 0; v < n; ++v) deg[v + 1] += local[t][v];
+  }
+  if (self_loops) for (i64 v = 0; v < n; ++v) deg[v + 1] += 1;
+  for (i64 v = 0; v < n; ++v) deg[v + 1] += deg[v];
+  std::vector<i64> fill(deg.begin(), deg.end() - 1);
+  std::vector<i32> col(deg[n]);
+  (void)tot;
+  // sequential scatter keeps the build deterministic
+  for (i64 e = 0; e < m; ++e) {
+    const i64 s = src[e], t = dst[e];
+    if (s < 0 || s >= n || t < 0 || t >= n || s == t) continue;
+    col[fill[s]++] = (i32)t;
+    if (symmetric) col[fill[t]++] = (i32)s;
+  }
+  if (self_loops) for (i64 v = 0; v < n; ++v) col[fill[v]++] = (i32)v;
+  // sort each row (locality) and optionally drop duplicates
+  std::vector<i64> newdeg(n + 1, 0);
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (i64 v = 0; v < n; ++v) {
+    auto b = col.begin() + deg[v], e = col.begin() + deg[v + 1];
+    std::sort(b, e);
+    newdeg[v + 1] = dedup ? (std::unique(b, e) - b) : (e - b);
+  }
+  for (i64 v = 0; v < n; ++v) newdeg[v + 1] += newdeg[v];
+  py::array_t<i64> rowptr(n + 1);
+  py::array_t<i32> colout(newdeg[n]);
+  i64* rp = rowptr.mutable_data();
+  i32* co = colout.mutable_data();
+  std::copy(newdeg.begin(), newdeg.end(), rp);
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (i64 v = 0; v < n; ++v)
+    std::copy(col.begin() + deg[v], col.begin() + deg[v] + (newdeg[v + 1] - newdeg[v]), co + newdeg[v]);
+  return py::make_tuple(rowptr, colout);
+}
+
+// Planted-partition graph with the shape of an OGB node-property dataset.
+//   n nodes, ~m undirected edges, c classes; node v's community = its class.
+//   Each node draws a degree from a truncated power law with mean 2m/n; each
+//   edge end goes to the same community with probability `homophily` (a
+//   window of nearby ids inside the community -> locality) and uniformly at
+//   random otherwise.  Features: class centroid + N(0,1) noise (bf16-ready
+//   fp32), so a 2-layer GCN reaches a non-trivial validation accuracy.
+py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophily,
+                          double feat_noise, uint64_t seed) {
+  py::array_t<i64> src_a(m), dst_a(m);
+  py::array_t<i32> label_a(n);
+  i64* src = src_a.mutable_data();
+  i64* dst = dst_a.mutable_data();
+  i32* lab = label_a.mutable_data();
+  // contiguous communities: class blocks of roughly equal size
+  const i64 block = (n + n_class - 1) / n_class;
+  for (i64 v = 0; v < n; ++v) lab[v] = (i32)std::min<i64>(v / block, n_class - 1);
+  const double mean_deg = (double)m / (double)n;   // edges per source node
+#pragma omp parallel for schedule(static)
+  for (i64 e = 0; e < m; ++e) {
+    uint64_t h = mix64(seed ^ mix64((uint64_t)e * 0x9E3779B97F4A7C15ull));
+    // source: power-law-ish popularity (inverse CDF of a Pareto-like law)
+    const double u = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+    h = mix64(h);
+    i64 s = (i64)((double)n * std::pow(u, 1.6)) % n;   // skew towards low ids ...
+    s = (i64)(mix64(s ^ seed) % (uint64_t)n);           // ... then scatter the hubs
+    const double u2 = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+    h = mix64(h);
+    i64 t;
+    if (u2 < homophily) {
+      const i64 c = lab[s];
+      const i64 lo = c * block, hi = std::min<i64>(n, lo + block);
+      const i64 win = std::max<i64>(16, (i64)(8 * mean_deg));
+      const i64 off = (i64)(h % (uint64_t)(2 * win + 1)) - win;
+      t = s + off;
+      if (t < lo) t += (hi - lo);
+      if (t >= hi) t -= (hi - lo);
+      if (t < lo || t >= hi) t = lo + (i64)(h % (uint64_t)(hi - lo));
+    } else {
+      t = (i64)(h % (uint64_t)n);
+    }
+    src[e] = s;
+    dst[e] = t;
+  }
+  py::array_t<float> feat_a({(py::ssize_t)n, (py::ssize_t)n_feat});
+  float* x = feat_a.mutable_data();
+  // class centroids
+  std::vector<float> cent((size_t)n_class * n_feat);
+  {
+    std::mt19937_64 g(seed ^ 0xC0FFEEull);
+    std::normal_distribution<float> nd(0.f, 1.f);
+    for (auto& c : cent) c = nd(g);
+  }
+#pragma omp parallel for schedule(static)
+  for (i64 v = 0; v < n; ++v) {
+    uint64_t h = mix64(seed ^ 0xFEEDull ^ mix64((uint64_t)v));
+    for (int f = 0; f < n_feat; f += 2) {
+      h = mix64(h);
+      const double u1 = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+      h = mix64(h);
+      const double u2 = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+      const double r = std::sqrt(-2.0 * std::log(u1));
+      const double z0 = r * std::cos(6.283185307179586 * u2), z1 = r * std::sin(6.283185307179586 * u2);
+      x[(size_t)v * n_feat + f] = (float)(cent[(size_t)lab[v] * n_feat + f] + feat_noise * z0);
+      if (f + 1 < n_feat)
+        x[(size_t)v * n_feat + f + 1] = (float)(cent[(size_t)lab[v] * n_feat + f + 1] + feat_noise * z1);
+    }
+  }
+  return py::make_tuple(src_a, dst_a, feat_a, label_a);
+}
+
+// Layer-wise uniform neighbour sampling (GraphSAGE).  For each layer (outermost
+// first) sample up to fanout[l] neighbours of the current frontier; returns, per
+// layer, (block_rowptr, block_col_local, frontier_nodes) with the destination
+// nodes first in each frontier (standard "dst nodes are a prefix of src nodes").
+py::list sample_neighbors(py::array_t<i64, py::array::c_style | py::array::forcecast> rowptr_a,
+                          py::array_t<i32, py::array::c_style | py::array::forcecast> col_a,
+                          py::array_t<i64, py::array::c_style | py::array::forcecast> seeds_a,
+                          std::vector<int> fanouts, uint64_t seed) {
+  const i64* rowptr = rowptr_a.data();
+  const i32* col = col_a.data();
+  std::vector<i64> frontier(seeds_a.data(), seeds_a.data() + seeds_a.size());
+  py::list out;
+  for (size_t l = 0; l < fanouts.size(); ++l) {
+    const int fo = fanouts[l];
+    const i64 nd = (i64)frontier.size();
+    std::vector<i64> cnt(nd + 1, 0);
+    for (i64 i = 0; i < nd; ++i) {
+      const i64 v = frontier[i];
+      const i64 deg = rowptr[v + 1] - rowptr[v];
+      cnt[i + 1] = fo < 0 ? deg : std::min<i64>(deg, fo);
+    }
+    for (i64 i = 0; i < nd; ++i) cnt[i + 1] += cnt[i];
+    std::vector<i64> picked(cnt[nd]);
+#pragma omp parallel for schedule(dynamic, 256)
+    for (i64 i = 0; i < nd; ++i) {
+      const i64 v = frontier[i];
+      const i64 b = rowptr[v], deg = rowptr[v + 1] - b, k = cnt[i + 1] - cnt[i];
+      i64* dstp = picked.data() + cnt[i];
+      if (k == deg) {
+        for (i64 q = 0; q < k; ++q) dstp[q] = col[b + q];
+      } else {   // Floyd's algorithm: k distinct positions out of deg
+        uint64_t h = mix64(seed ^ mix64((uint64_t)v * 131 + l));
+        std::vector<i64> pos;
+        pos.reserve(k);
+        for (i64 j = deg - k; j < deg; ++j) {
+          h = mix64(h);
+          i64 t = (i64)(h % (uint64_t)(j + 1));
+          if (std::find(pos.begin(), pos.end(), t) != pos.end()) t = j;
+          pos.push_back(t);
+        }
+        for (i64 q = 0; q < k; ++q) dstp[q] = col[b + pos[q]];
+      }
+    }
+    // relabel: destination nodes first, then new source nodes in first-seen order
+    std::vector<i64> nodes(frontier);
+    std::unordered_map<i64, i32> idx;
+    idx.reserve(frontier.size() * 2 + picked.size());
+    for (i64 i = 0; i < nd; ++i) idx.emplace(frontier[i], (i32)i);
+    py::array_t<i32> bcol(picked.size());
+    i32* bc = bcol.mutable_data();
+    for (size_t q = 0; q < picked.size(); ++q) {
+      auto it = idx.find(picked[q]);
+      if (it == idx.end()) {
+        it = idx.emplace(picked[q], (i32)nodes.size()).first;
+        nodes.push_back(picked[q]);
+      }
+      bc[q] = it->second;
+    }
+    py::array_t<i64> brow(nd + 1);
+    std::copy(cnt.begin(), cnt.end(), brow.mutable_data());
+    py::array_t<i64> nodes_a(nodes.size());
+    std::copy(nodes.begin(), nodes.end(), nodes_a.mutable_data());
+    out.append(py::make_tuple(brow, bcol, nodes_a));
+    frontier.swap(nodes);
+  }
+  return out;
+}
+
+PYBIND11_MODULE(_rt, m) {
+  m.doc() = "cgnn_amd host runtime (C++)";
+  m.def("dag_program", &dag_program, py::arg("n_vars"), py::arg("parents"), py::arg("kinds"),
+        py::arg("confs"), py::arg("H"), py::arg("list_order") = std::vector<int>(),
+        py::arg("n_conf") = 0);
+  m.def("is_acyclic", &is_acyclic);
+  m.def("canonical_hash", &canonical_hash);
+  m.def("csr_from_edges", &csr_from_edges, py::arg("n"), py::arg("src"), py::arg("dst"),
+        py::arg("symmetric") = true, py::arg("self_loops") = true, py::arg("dedup") = true);
+  m.def("synthetic_graph", &synthetic_graph, py::arg("n"), py::arg("m"), py::arg("n_feat"),
+        py::arg("n_class"), py::arg("homophily") = 0.8, py::arg("feat_noise") = 1.0,
+        py::arg("seed") = 0);
+  m.def("sample_neighbors", &sample_neighbors);
+  m.def("num_threads", []() { return omp_get_max_threads(); });
+}

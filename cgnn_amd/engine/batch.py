@@ -1,0 +1,155 @@
+"""Batched device trainer: R independent CGNN models in one set of kernels.
+
+The unit of GPU work is a *batch of models* (runs x candidates x pairs),
+not one TF session.  Buffers are PyTorch tensors on the target
+device; the step sequence is owned by the native ``CgnnEngine`` (C++), which
+replays chunks of steps through hipGraphs.  Nothing is copied back to the host
+until the final scores are read.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import native
+from .program import Program, pack_programs
+
+SUPPORTED_D = (1, 2, 3, 4, 6, 8, 12, 16, 20, 24, 32, 48, 64)
+MMD_TILE = 256
+TARGET_WGS = 2048
+
+
+def padded_dim(d: int) -> int:
+    for D in SUPPORTED_D:
+        if D >= d:
+            return D
+    raise ValueError("CGNN device path supports at most %d variables (got %d)" % (SUPPORTED_D[-1], d))
+
+
+def mmd_geometry(N: int, R: int):
+    row_tiles = (N + MMD_TILE - 1) // MMD_TILE
+    ct = 2 * row_tiles
+    n_chunks = min(ct, max(1, math.ceil(TARGET_WGS / (row_tiles * R))))
+    tpc = math.ceil(ct / n_chunks)
+    n_chunks = math.ceil(ct / tpc)
+    return row_tiles, n_chunks, tpc
+
+
+def _keys_tensor(keys, device):
+    arr = np.asarray(keys, dtype=np.uint64).astype(np.uint32).reshape(-1)
+    return torch.from_numpy(arr.view(np.int32).copy()).to(device)
+
+
+class DeviceTrainer:
+    """Train + evaluate R models on one GPU; returns per-model scores."""
+
+    def __init__(self, programs: Sequence[Program], datas: Sequence[np.ndarray],
+                 keys: Sequence[tuple], H: int, device, learning_rate=0.01, init_std=0.05,
+                 use_fast_mmd=False, nb_vectors=100, record_history=0, graph_chunk=50):
+        hip = native.hip()
+        self.hip = hip
+        if not hip.gen_supported_h(int(H)):
+            raise native.NativeExtensionError("h_layer_dim=%d has no compiled generator kernel" % H)
+        self.device = torch.device(device)
+        R = len(programs)
+        d = programs[0].n_vars
+        if any(p.n_vars != d for p in programs):
+            raise ValueError("all models in a device batch must share the variable count")
+        N = int(np.asarray(datas[0]).shape[1])
+        if any(np.asarray(x).shape != (d, N) for x in datas):
+            raise ValueError("all models in a device batch must share the data shape [d, N]")
+        D = padded_dim(d)
+        self.R, self.N, self.d, self.D, self.H = R, N, d, D, int(H)
+        prog, stride, P, max_in = pack_programs(programs)
+        self.P = P
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            self.prog = torch.from_numpy(prog).to(dev)
+            data = np.zeros((R, D, N), dtype=np.float32)
+            for r, x in enumerate(datas):
+                data[r, :d] = np.asarray(x, dtype=np.float32)
+            self.data = torch.from_numpy(data).to(dev)
+            self.keys = _keys_tensor(keys, dev)
+            self.params = torch.zeros(R, P, **f32)
+            self.m = torch.zeros(R, P, **f32)
+            self.v = torch.zeros(R, P, **f32)
+            self.xhat = torch.zeros(R, D, N, **f32)
+            self.dxhat = torch.zeros(R, D, N, **f32)
+            row_tiles, n_chunks, tpc = mmd_geometry(N, R)
+            self.geometry = (row_tiles, n_chunks, tpc)
+            self.rff_k = int(nb_vectors) if use_fast_mmd else 0
+            F = 7 * self.rff_k
+            n_parts = max(row_tiles * n_chunks, (F + 255) // 256 if F else 0)
+            self.gradp = torch.zeros(max(n_chunks, 1), R, D, N, **f32)
+            self.lpart = torch.zeros(R, n_parts, **f32)
+            G = hip.gen_bwd_blocks(N)
+            self.gpart = torch.zeros(R, G, P, **f32)
+            self.tt = torch.zeros(R, **f32)
+            self.loss_last = torch.zeros(R, **f32)
+            self.loss_acc = torch.zeros(R, **f32)
+            self.hist_len = int(record_history)
+            self.hist = torch.zeros(R, max(self.hist_len, 1), **f32)
+            self.step = torch.zeros(2, dtype=torch.int32, device=dev)
+            self.rff_w = torch.zeros(R, max(F, 1), D + 1, **f32)
+            self.rff_diff = torch.zeros(R, max(F, 1), **f32)
+            stream = torch.cuda.current_stream(dev)
+            icfg = [R, N, D, self.H, P, stride, max_in, row_tiles, n_chunks, tpc, self.hist_len,
+                    self.rff_k, d]
+            fcfg = [float(learning_rate), 0.9, 0.999, 1e-8, float(init_std)]
+            ptrs = [t.data_ptr() for t in (self.prog, self.params, self.m, self.v, self.data,
+                                           self.xhat, self.dxhat, self.gradp, self.lpart, self.gpart,
+                                           self.tt, self.loss_last, self.loss_acc)]
+            ptrs.append(self.hist.data_ptr() if self.hist_len else 0)
+            ptrs += [self.step.data_ptr(), self.keys.data_ptr(), self.rff_w.data_ptr(),
+                     self.rff_diff.data_ptr()]
+            self.engine = hip.CgnnEngine(icfg, fcfg, ptrs, stream.cuda_stream)
+        self.graph_chunk = int(graph_chunk)
+
+    def start(self):
+        """Initialise parameters and the constant true-true MMD block (async)."""
+        with torch.cuda.device(self.device):
+            self.step.zero_()
+            self.loss_acc.zero_()
+            self.engine.init()
+            self.engine.tt()
+
+    def train(self, epochs: int):
+        with torch.cuda.device(self.device):
+            self.engine.run(0, int(epochs), self.graph_chunk, self.hist_len > 0)
+
+    def evaluate(self, epochs: int):
+        with torch.cuda.device(self.device):
+            self.loss_acc.zero_()
+            self.engine.run(1, int(epochs), self.graph_chunk, False)
+
+    def launch(self, train_epochs: int, test_epochs: int):
+        """Enqueue the whole train+eval schedule without synchronising."""
+        self.start()
+        self.train(train_epochs)
+        self.evaluate(test_epochs)
+        self._test_epochs = max(int(test_epochs), 1)
+
+    def collect(self) -> np.ndarray:
+        scores = (self.loss_acc / float(self._test_epochs)).cpu().numpy().astype(np.float64)
+        return scores
+
+    def history(self) -> np.ndarray:
+        return self.hist[:, :self.hist_len].cpu().numpy()
+
+    def run(self, train_epochs: int, test_epochs: int, verbose=False) -> np.ndarray:
+        self.launch(train_epochs, test_epochs)
+        scores = self.collect()
+        if verbose and self.hist_len:
+            h = self.history()
+            for r in range(self.R):
+                for it in range(0, self.hist_len, 100):
+                    print('Run:{}, Iter:{}, score:{}'.format(r, it, h[r, it]))
+        return scores
+
+    def generated(self) -> np.ndarray:
+        """Last generated samples, [R, d, N]."""
+        return self.xhat[:, :self.d].cpu().numpy()

@@ -1,0 +1,141 @@
+"""Score many generative models at once.
+
+``score_jobs`` is the single execution entry point used by every model and
+search (replacing each ``Parallel(n_jobs=NB_JOBS)(delayed(run_fn)(...))`` call
+site listed in SURVEY §2.5): it takes a list of independent jobs (one job =
+one run of one candidate graph on one data matrix), packs them into device
+batches, spreads the batches over GPUs / ranks, and returns one score per job.
+
+Failure handling: a non-finite score is kept as NaN and dropped
+by :func:`finite_mean` exactly like the reference's ``np.isfinite`` filter;
+``max_retries`` optionally re-trains such a job with a fresh RNG stream, and
+``CGNN_FAULT=nan@job:k[,k...]`` injects failures for tests.
+"""
+from __future__ import annotations
+
+import dataclasses
+import logging
+import os
+import time
+from typing import Hashable, List, Optional, Sequence
+
+import numpy as np
+
+from ..parallel import dist as pdist
+from ..utils import philox
+from ..utils.metrics import METRICS
+from .program import Program
+
+log = logging.getLogger("cgnn_amd")
+
+
+@dataclasses.dataclass
+class Job:
+    program: Program
+    data: np.ndarray              # [d, N] float32, already subsampled
+    key: tuple                    # Philox key of this model
+
+
+def subsample(mat: np.ndarray, max_points: int, seed: int, *salt) -> np.ndarray:
+    """Per-run random subsample of the rows of [N, d] data (CGNN.py:183-185)."""
+    if mat.shape[0] <= max_points:
+        return mat
+    perm = philox.numpy_rng(seed, "subsample", *salt).permutation(mat.shape[0])
+    return mat[perm[:int(max_points)]]
+
+
+def finite_mean(values) -> float:
+    v = np.asarray(values, dtype=np.float64)
+    v = v[np.isfinite(v)]
+    return float(v.mean()) if v.size else float("nan")
+
+
+def _fault_indices():
+    spec = os.environ.get("CGNN_FAULT", "")
+    if not spec.startswith("nan@job:"):
+        return set()
+    return {int(x) for x in spec[len("nan@job:"):].split(",") if x.strip()}
+
+
+def _group_batches(jobs: Sequence[Job], batch: int):
+    """Group compatible jobs (same [d, N]) into batches of at most `batch`."""
+    groups = {}
+    for i, j in enumerate(jobs):
+        groups.setdefault((j.program.n_vars, j.data.shape[1]), []).append(i)
+    out = []
+    for idx in groups.values():
+        for s in range(0, len(idx), batch):
+            out.append(idx[s:s + batch])
+    return out
+
+
+def _run_local(jobs: Sequence[Job], cfg) -> np.ndarray:
+    import torch
+    n = len(jobs)
+    scores = np.full(n, np.nan)
+    if n == 0:
+        return scores
+    devices = pdist.devices_for(cfg)
+    t0 = time.perf_counter()
+    if devices:
+        from .batch import DeviceTrainer
+        batches = _group_batches(jobs, max(1, cfg.batch_models))
+        pending = []
+        for b, idx in enumerate(batches):
+            dev = devices[b % len(devices)]
+            tr = DeviceTrainer([jobs[i].program for i in idx], [jobs[i].data for i in idx],
+                               [jobs[i].key for i in idx], cfg.h_layer_dim, dev,
+                               learning_rate=cfg.learning_rate, init_std=cfg.init_std,
+                               use_fast_mmd=cfg.use_Fast_MMD, nb_vectors=cfg.nb_vectors_approx_MMD,
+                               record_history=cfg.train_epochs if cfg.verbose else 0)
+            tr.launch(cfg.train_epochs, cfg.test_epochs)
+            pending.append((idx, tr))
+            # bound the number of in-flight batches per device (memory)
+            if len(pending) >= 4 * len(devices):
+                i0, t = pending.pop(0)
+                scores[i0] = t.collect()
+        for idx, tr in pending:
+            scores[idx] = tr.collect()
+            if cfg.verbose and tr.hist_len:
+                h = tr.history()
+                for r in range(tr.R):
+                    for it in range(0, tr.hist_len, 100):
+                        log.info('Run:%d, Iter:%d, score:%s', idx[r], it, h[r, it])
+    else:
+        from .reference import ReferenceTrainer
+        for idx in _group_batches(jobs, max(1, cfg.batch_models)):
+            tr = ReferenceTrainer([jobs[i].program for i in idx], [jobs[i].data for i in idx],
+                                  [jobs[i].key for i in idx], cfg.h_layer_dim,
+                                  learning_rate=cfg.learning_rate, init_std=cfg.init_std,
+                                  use_fast_mmd=cfg.use_Fast_MMD, nb_vectors=cfg.nb_vectors_approx_MMD)
+            scores[idx] = tr.run(cfg.train_epochs, cfg.test_epochs, verbose=cfg.verbose)
+    dt = time.perf_counter() - t0
+    steps = n * (cfg.train_epochs + cfg.test_epochs)
+    METRICS.record("score_jobs", models=n, seconds=dt, model_steps=steps,
+                   steps_per_s=steps / dt if dt > 0 else 0.0, devices=len(devices) or 0)
+    return scores
+
+
+def score_jobs(jobs: Sequence[Job], cfg, max_retries: int = 0) -> np.ndarray:
+    """One score per job (mean test-phase loss); NaN for non-finite runs."""
+    n = len(jobs)
+    idx = pdist.shard_indices(n)
+    local = _run_local([jobs[i] for i in idx], cfg) if len(idx) else np.zeros(0)
+    faults = _fault_indices()
+    for k, i in enumerate(idx):
+        if int(i) in faults:
+            local[k] = np.nan
+    for attempt in range(max_retries):
+        bad = [k for k in range(len(idx)) if not np.isfinite(local[k])]
+        if not bad:
+            break
+        retry = []
+        for k in bad:
+            j = jobs[idx[k]]
+            retry.append(Job(j.program, j.data, philox.model_key(j.key[0], j.key[1], "retry", attempt)))
+        local[bad] = _run_local(retry, cfg)
+    scores = pdist.combine_scores(n, idx, local)
+    dropped = int((~np.isfinite(scores)).sum())
+    if dropped:
+        METRICS.record("dropped_runs", count=dropped, total=n)
+    return scores

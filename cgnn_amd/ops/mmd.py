@@ -1,0 +1,71 @@
+"""Differentiable MMD losses as PyTorch ops.
+
+On a GPU tensor the fused HIP kernel computes the loss AND its gradient in
+one pass (the backward only scales the saved gradient); on CPU the dense
+PyTorch formula of the reference is used (Loss.py:12-32).  Both accept a
+batch of independent problems ``[R, N, d]``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import native
+from ..engine.batch import mmd_geometry, padded_dim
+from ..engine.reference import GAMMAS, mmd_loss_dense
+
+
+def _to_feature_major(x: torch.Tensor, D: int) -> torch.Tensor:
+    R, N, d = x.shape
+    out = torch.zeros(R, D, N, dtype=torch.float32, device=x.device)
+    out[:, :d] = x.detach().float().transpose(1, 2)
+    return out
+
+
+class _MMDHip(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, true):
+        hip = native.hip()
+        R, N, d = pred.shape
+        D = padded_dim(d)
+        P = _to_feature_major(pred, D)
+        T = _to_feature_major(true, D)
+        row_tiles, n_chunks, tpc = mmd_geometry(N, R)
+        dev = pred.device
+        gradp = torch.empty(n_chunks, R, D, N, dtype=torch.float32, device=dev)
+        lpart = torch.empty(R, row_tiles * n_chunks, dtype=torch.float32, device=dev)
+        tt = torch.zeros(R, dtype=torch.float32, device=dev)
+        last = torch.zeros(R, dtype=torch.float32, device=dev)
+        acc = torch.zeros(R, dtype=torch.float32, device=dev)
+        step = torch.zeros(2, dtype=torch.int32, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        inv = 1.0 / (N * N)
+        hip.mmd(2, D, P.data_ptr(), T.data_ptr(), gradp.data_ptr(), lpart.data_ptr(), N, R,
+                row_tiles, n_chunks, tpc, 0.0, st)
+        hip.loss_finalize(lpart.data_ptr(), row_tiles * n_chunks, tt.data_ptr(), last.data_ptr(),
+                          acc.data_ptr(), inv, 2, 0, 0, step.data_ptr(), 0, R, st)
+        hip.mmd(0, D, P.data_ptr(), T.data_ptr(), gradp.data_ptr(), lpart.data_ptr(), N, R,
+                row_tiles, n_chunks, tpc, 4.0 * inv, st)
+        hip.loss_finalize(lpart.data_ptr(), row_tiles * n_chunks, tt.data_ptr(), last.data_ptr(),
+                          acc.data_ptr(), inv, 0, 0, 0, step.data_ptr(), 0, R, st)
+        g = gradp.sum(0)[:, :d].transpose(1, 2).contiguous()    # [R, N, d]
+        ctx.save_for_backward(g)
+        return last.to(pred.dtype)
+
+    @staticmethod
+    def backward(ctx, gout):
+        (g,) = ctx.saved_tensors
+        return (gout.view(-1, 1, 1).to(g.dtype) * g).to(gout.dtype), None
+
+
+def mmd_loss(pred: torch.Tensor, true: torch.Tensor) -> torch.Tensor:
+    """Biased multi-bandwidth MMD^2; ``[N,d]`` -> scalar or ``[R,N,d]`` -> ``[R]``."""
+    batched = pred.dim() == 3
+    p = pred if batched else pred.unsqueeze(0)
+    t = true if batched else true.unsqueeze(0)
+    if p.is_cuda:
+        out = _MMDHip.apply(p, t.detach())
+    else:
+        out = torch.stack([mmd_loss_dense(p[r], t[r]) for r in range(p.shape[0])])
+    return out if batched else out[0]

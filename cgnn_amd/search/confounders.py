@@ -1,0 +1,120 @@
+"""Hill climbing with hidden confounders (CGNN_confounders.py:219-383).
+
+Score = mean finite run score + ``complexity_graph_param * #edges``.  For every
+skeleton edge, in skeleton order:
+
+* oriented in the graph: try the reversal, then try removing the (possibly
+  reversed) edge; an edge whose removal improves the score is labelled a
+  possible confounder, otherwise its weight becomes the score increase its
+  removal would cause (:262-317);
+* absent (removed earlier): try adding u->v and v->u and keep the better one
+  if it improves the score (:320-381).
+
+Loop until a full pass brings no improvement.  Candidates that do not depend
+on each other's outcome are scored in one batch: the reversal and the removal
+of the current orientation, and the two additions.  The removal of the
+*reversed* edge is scored afterwards only if the reversal was accepted.
+"""
+from __future__ import annotations
+
+import copy
+import logging
+
+from ..utils.settings import SETTINGS
+from .hill_climbing import _say, make_evaluator
+
+log = logging.getLogger("cgnn_amd")
+
+
+def hill_climbing_confounders(graph, data, run_cgnn_function=None, **kwargs):
+    cfg = SETTINGS.snapshot(**kwargs)
+    skel = graph.skeleton
+    if not skel:
+        raise ValueError("hill_climbing_confounders needs DirectedGraph(skeleton=...)")
+    nodes = skel.get_list_nodes()
+    ev = kwargs.get("evaluator") or make_evaluator(data, run_cgnn_function, cfg, "confounders", nodes, kwargs)
+    tested = {graph.canonical_key()}
+    globalscore = float(ev([graph])[0])
+    _say(cfg, "Graph score : " + str(globalscore))
+    confounders = set()
+    improvement = True
+    while improvement:
+        improvement = False
+        for u, v in skel.get_list_edges_without_duplicate():
+            if graph.has_edge(u, v) or graph.has_edge(v, u):
+                n1, n2 = (u, v) if graph.has_edge(u, v) else (v, u)
+                # --- reversal and removal of the current orientation, together
+                rev = copy.deepcopy(graph)
+                rev.reverse_edge(n1, n2)
+                rem = copy.deepcopy(graph)
+                rem.remove_edge(n1, n2)
+                cands = []
+                rev_ok = not rev.is_cyclic() and rev.canonical_key() not in tested
+                rem_ok = rem.canonical_key() not in tested
+                if rev_ok:
+                    cands.append(("rev", rev))
+                if rem_ok:
+                    cands.append(("rem", rem))
+                scores = dict(zip([c[0] for c in cands], ev([c[1] for c in cands]))) if cands else {}
+                if rev_ok:
+                    tested.add(rev.canonical_key())
+                    s = float(scores["rev"])
+                    _say(cfg, "Reverse edge %s -> %s : %s (best %s)" % (n1, n2, s, globalscore))
+                    if s < globalscore:
+                        graph.reverse_edge(n1, n2)
+                        improvement = True
+                        globalscore = s
+                        n1, n2 = n2, n1
+                        _say(cfg, "Edge %s -> %s got reversed !" % (n2, n1))
+                        # the removal candidate above removed the old orientation;
+                        # removing either orientation gives the same graph
+                # removal of the (possibly reversed) edge: same graph either way
+                rem_key = rem.canonical_key()
+                if rem_ok:
+                    tested.add(rem_key)
+                    s = float(scores["rem"])
+                    if s < globalscore:
+                        graph.remove_edge(n1, n2)
+                        improvement = True
+                        globalscore = s
+                        confounders.add(frozenset((n1, n2)))
+                        _say(cfg, "Edge %s -> %s got removed, possible confounder !" % (n1, n2))
+                    else:
+                        graph.set_weight(n1, n2, s - globalscore)
+                        _say(cfg, "Edge %s -> %s not removed. Score edge : %s" % (n1, n2, s - globalscore))
+                else:
+                    _say(cfg, "Removing already evaluated for edge %s -> %s" % (n1, n2))
+            else:
+                a_g = copy.deepcopy(graph)
+                a_g.add(u, v)
+                b_g = copy.deepcopy(graph)
+                b_g.add(v, u)
+                cands = []
+                for tag, g in (("uv", a_g), ("vu", b_g)):
+                    if not g.is_cyclic() and g.canonical_key() not in tested:
+                        cands.append((tag, g))
+                s_uv = s_vu = 9999.0
+                if cands:
+                    res = dict(zip([c[0] for c in cands], ev([c[1] for c in cands])))
+                    for tag, g in cands:
+                        tested.add(g.canonical_key())
+                    s_uv = float(res.get("uv", 9999.0))
+                    s_vu = float(res.get("vu", 9999.0))
+                if s_uv < globalscore and s_uv < s_vu:
+                    graph.add(u, v, globalscore - s_uv)
+                    globalscore = s_uv
+                    improvement = True
+                    confounders.discard(frozenset((u, v)))
+                    _say(cfg, "Edge %s -> %s is added !" % (u, v))
+                elif s_vu < globalscore and s_vu < s_uv:
+                    graph.add(v, u, globalscore - s_vu)
+                    globalscore = s_vu
+                    improvement = True
+                    confounders.discard(frozenset((u, v)))
+                    _say(cfg, "Edge %s -> %s is added !" % (v, u))
+                else:
+                    _say(cfg, "Edge not added, possible confounder %s <-> %s" % (u, v))
+                    confounders.add(frozenset((u, v)))
+    graph.search_score = globalscore
+    graph.confounders = sorted(tuple(sorted(c, key=repr)) for c in confounders)
+    return graph
