@@ -1,0 +1,115 @@
+"""Headline benchmark (BASELINE.json): epochs/sec + val-acc of a 2-layer GCN on
+an ogbn-products-shaped graph, 1/2/4/8 MI355X.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one full-graph training epoch (forward + backward + Adam) over all
+2,449,029 nodes.  Data: synthetic graph of the ogbn-products shape (no network
+for the real dataset), random-init weights.  Multi-GPU: 1-D row partition of
+the graph over ranks (strong scaling: the whole job trains the same graph),
+RCCL all-gathers of the layer-2 activations / gradients and an all-reduce of
+the weight gradients.  W untimed warm-up epochs, then exactly K timed epochs
+bracketed by barrier + device synchronize; the MAX time over ranks is reported.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "epochs/sec + val-acc, 2-layer GCN ogbn-products, 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--dataset", default="ogbn-products")
+    ap.add_argument("--hidden", type=int, default=256)
+    ap.add_argument("--dropout", type=float, default=0.5)
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink the graph (debug only)")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--feat-noise", type=float, default=4.0)
+    ap.add_argument("--label-noise", type=float, default=0.25)
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from cgnn_amd.parallel import dist as pdist
+    from cgnn_amd.gnn.data import SHAPES, synthetic
+    from cgnn_amd.gnn.gcn import GCNTrainer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        pdist.init_process_group("nccl")
+    rank = pdist.rank()
+    local = pdist.local_rank()
+    torch.cuda.set_device(local % torch.cuda.device_count())
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    t_setup = time.perf_counter()
+    g = synthetic(a.dataset, seed=a.seed, device=dev, scale=a.scale, feat_noise=a.feat_noise,
+                  label_noise=a.label_noise)
+    tr = GCNTrainer(g, hidden=a.hidden, dropout=a.dropout, lr=a.lr, seed=a.seed)
+    n_nodes, nnz = g.n, g.nnz
+    del g
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup
+
+    for _ in range(a.warmup):
+        tr.train_step()
+    pdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        tr.train_step()
+    torch.cuda.synchronize()
+    pdist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    res = tr.evaluate()
+    train_loss = tr.train_loss()
+
+    n, m, F, C, _, _ = SHAPES[a.dataset]
+    if rank == 0:
+        eps = a.steps / dt
+        out = {
+            "metric": METRIC,
+            "value": round(eps, 4),
+            "unit": "epochs/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * dt / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic graph of the %s shape (%d nodes, %d undirected edges, %d features, "
+                    "%d classes; planted communities), random-init weights" % (a.dataset, n, m, F, C),
+            "config": {"model": "GCN-2layer-hidden%d" % a.hidden, "global_batch": n_nodes,
+                       "seq_len": None, "parallelism": "graph-rowpart%d" % world,
+                       "dataset": a.dataset, "nnz_with_self_loops": nnz, "dropout": a.dropout,
+                       "optimizer": "adam", "lr": a.lr},
+            "val_acc": round(res["val_acc"], 4),
+            "test_acc": round(res["test_acc"], 4),
+            "train_loss": round(train_loss, 5),
+            "epochs_trained": a.warmup + a.steps,
+            "setup_s": round(setup_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

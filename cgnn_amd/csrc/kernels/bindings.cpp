@@ -52,6 +52,10 @@ int gnn_launch_spmm_ce(const int*, const int*, const void*, const float*, const 
 int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, float, float, float,
                     const int*, hipStream_t);
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
+int gnn_spmm_ce_blocks(int);
+int gnn_launch_bias_relu_dropout(void*, const float*, long, int, int, float, uint32_t, uint32_t,
+                                 uint32_t, hipStream_t);
+int gnn_launch_relu_dropout_bwd(void*, const void*, long, float, hipStream_t);
 }
 
 static inline hipStream_t S(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -159,6 +163,15 @@ PYBIND11_MODULE(_hip, m) {
                        float eps, float wd, uint64_t step, uint64_t st) {
     chk(gnn_launch_adam(Pt<float>(p), Pt<float>(mm), Pt<float>(vv), Pt<const float>(g), n, lr, b1, b2, eps, wd,
                         Pt<const int>(step), S(st)), "gnn_adam");
+  });
+  m.def("gnn_spmm_ce_blocks", &gnn_spmm_ce_blocks);
+  m.def("gnn_bias_relu_dropout", [](uint64_t h, uint64_t bias, long rows, int F, int ld, float p, uint32_t k0,
+                                    uint32_t k1, uint32_t step, uint64_t st) {
+    chk(gnn_launch_bias_relu_dropout(Pt<void>(h), Pt<const float>(bias), rows, F, ld, p, k0, k1, step, S(st)),
+        "gnn_bias_relu_dropout");
+  });
+  m.def("gnn_relu_dropout_bwd", [](uint64_t dh, uint64_t h, long n, float p, uint64_t st) {
+    chk(gnn_launch_relu_dropout_bwd(Pt<void>(dh), Pt<const void>(h), n, p, S(st)), "gnn_relu_dropout_bwd");
   });
   m.def("gnn_cast_bf16", [](uint64_t src, uint64_t dst, long n, uint64_t st) {
     chk(gnn_launch_cast_bf16(Pt<const float>(src), Pt<void>(dst), n, S(st)), "gnn_cast_bf16");

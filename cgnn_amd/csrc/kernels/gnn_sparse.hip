@@ -18,6 +18,7 @@
 // broadcast inside the sub-group with ds_bpermute; four gathered rows are kept
 // in flight per lane.  Accumulation is fp32; storage is bf16.
 #include "cgnn_common.h"
+#include <algorithm>
 
 using namespace cgnn;
 
@@ -133,7 +134,8 @@ __global__ __launch_bounds__(256) void spmm_kernel(
 
 // Layer-2 aggregate + bias + log-softmax + NLL.  L = 8 lanes per row, C <= 64.
 //   mask[i]: 0 = unused, 1 = train, 2 = valid, 3 = test
-//   stats[block][4] = {sum train loss, #correct train, #correct valid, #correct test}
+//   stats[block][4 + 64] = {sum train loss, #correct train, #correct valid, #correct test,
+//                           per-class sum of dL/dlogits (= the b2 gradient, mode 0)}
 //   mode 0: also write G[i,:] = rscale[i] * (softmax - onehot) / n_train  (train rows)
 __global__ __launch_bounds__(256) void spmm_ce_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Z,
@@ -142,6 +144,7 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
     int n_rows, int C, int ld, int mode, float inv_count) {
   constexpr int L = 8, RPW = 8;
   __shared__ float s_red[4][4];
+  __shared__ float s_cls[4][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int sub = lane / L, sl = lane - sub * L;
   const int row = (blockIdx.x * (blockDim.x >> 6) + wid) * RPW + sub;
@@ -182,16 +185,30 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
 #pragma unroll
     for (int q = 0; q < 8; ++q) if (f0 + q == y) my_loss = lse - lg[q];
   }
+  float dl[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int c = f0 + q;
+    dl[q] = (rv && split == 1 && c < C) ? (__expf(lg[q] - lse) - (c == y ? 1.f : 0.f)) * inv_count : 0.f;
+  }
   if (mode == 0 && rv && f0 < ld) {
     float gq[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = f0 + q;
-      float g = 0.f;
-      if (split == 1 && c < C) g = (__expf(lg[q] - lse) - (c == y ? 1.f : 0.f)) * inv_count * rs;
-      gq[q] = g;
-    }
+    for (int q = 0; q < 8; ++q) gq[q] = dl[q] * rs;
     *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(G) + (size_t)row * ld + f0) = f32x8_to_bf16(gq);
+  }
+  // per-class sums over the 8 rows of this wave: lanes with equal sl hold the same classes
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float v = dl[q];
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    dl[q] = v;
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s_cls[wid][lane * 8 + q] = dl[q];
   }
   // statistics: one contribution per row (sub-group lane 0), fixed-order block reduce
   const bool lead = rv && sl == 0;
@@ -204,8 +221,58 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
   __syncthreads();
   if (threadIdx.x < 4) {
     const int k = threadIdx.x;
-    stats[(size_t)blockIdx.x * 4 + k] = (s_red[0][k] + s_red[1][k]) + (s_red[2][k] + s_red[3][k]);
+    stats[(size_t)blockIdx.x * 68 + k] = (s_red[0][k] + s_red[1][k]) + (s_red[2][k] + s_red[3][k]);
+  } else if (threadIdx.x >= 64 && threadIdx.x < 128) {
+    const int k = threadIdx.x - 64;
+    stats[(size_t)blockIdx.x * 68 + 4 + k] = (s_cls[0][k] + s_cls[1][k]) + (s_cls[2][k] + s_cls[3][k]);
   }
+}
+
+// H = dropout(relu(P + b)) in place on a bf16 [rows][ld] matrix (first F columns valid).
+// Dropout keeps with probability 1-p and scales by 1/(1-p); the keep bit of element
+// (row, col) is bit (col % 4) of a Philox draw keyed (row, col/4, step): reproducible
+// and independent of launch geometry.  One thread per 8 consecutive columns.
+__global__ __launch_bounds__(256) void bias_relu_dropout_kernel(
+    uint16_t* __restrict__ Hm, const float* __restrict__ bias, long rows, int F, int ld, float p,
+    uint32_t k0, uint32_t k1, uint32_t step) {
+  const int cpr = ld / 8;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * cpr) return;
+  const long row = idx / cpr;
+  const int c0 = (int)(idx - row * cpr) * 8;
+  uint4* ptr = reinterpret_cast<uint4*>(Hm + row * ld + c0);
+  float v[8];
+  bf16x8_to_f32(*ptr, v);
+  const float scale = 1.f / (1.f - p);
+  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    u32x4 rnd = {0, 0, 0, 0};
+    if (p > 0.f) rnd = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)((c0 >> 2) + h), step, RNG_DROPOUT}, k0, k1);
+    const uint32_t rr[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = h * 4 + q, c = c0 + j;
+      float x = (c < F) ? fmaxf(v[j] + bias[c], 0.f) : 0.f;
+      if (p > 0.f) x = (rr[q] >= thr) ? x * scale : 0.f;
+      v[j] = x;
+    }
+  }
+  *ptr = f32x8_to_bf16(v);
+}
+
+// dP = dH * [H > 0] * 1/(1-p)  (H already holds relu + dropout, so H > 0 iff the unit was
+// active and kept).  bf16 in/out, in place on dH.
+__global__ __launch_bounds__(256) void relu_dropout_bwd_kernel(
+    uint16_t* __restrict__ dH, const uint16_t* __restrict__ Hm, long n8, float scale) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n8) return;
+  float g[8], h[8];
+  bf16x8_to_f32(reinterpret_cast<const uint4*>(dH)[idx], g);
+  bf16x8_to_f32(reinterpret_cast<const uint4*>(Hm)[idx], h);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) g[q] = h[q] > 0.f ? g[q] * scale : 0.f;
+  reinterpret_cast<uint4*>(dH)[idx] = f32x8_to_bf16(g);
 }
 
 // PyTorch-semantics Adam (bias-corrected, eps inside) with optional decoupled
@@ -249,6 +316,17 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
                                const float* rscale, const float* bias, int n_rows, int F, int ldx,
                                int ldy, int xbf, int ybf, int relu, hipStream_t st) {
   if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
+  if (F > 512) {
+    // wide features: column slabs of 512 (16-byte aligned offsets), one launch each
+    const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;
+    for (int c0 = 0; c0 < F; c0 += 512) {
+      const int fc = std::min(512, F - c0);
+      const int rc = gnn_launch_spmm(rowptr, col, (const char*)X + c0 * xs, (char*)Y + c0 * ys, rscale,
+                                     bias ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu, st);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   if (F <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
   if (F <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
   if (F <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
@@ -257,6 +335,24 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
 }
 
 extern "C" int gnn_spmm_ce_blocks(int n_rows) { return (n_rows + 31) / 32; }
+
+extern "C" int gnn_launch_bias_relu_dropout(void* H, const float* bias, long rows, int F, int ld,
+                                            float p, uint32_t k0, uint32_t k1, uint32_t step,
+                                            hipStream_t st) {
+  if (ld % 8) return -3;
+  const long n = rows * (ld / 8);
+  hipLaunchKernelGGL(bias_relu_dropout_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     (uint16_t*)H, bias, rows, F, ld, p, k0, k1, step);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_launch_relu_dropout_bwd(void* dH, const void* H, long n, float p, hipStream_t st) {
+  if (n % 8) return -3;
+  const long n8 = n / 8;
+  hipLaunchKernelGGL(relu_dropout_bwd_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st,
+                     (uint16_t*)dH, (const uint16_t*)H, n8, 1.f / (1.f - p));
+  return (int)hipGetLastError();
+}
 
 extern "C" int gnn_launch_spmm_ce(const int* rowptr, const int* col, const void* Z,
                                   const float* rscale, const float* bias, const int* labels,

@@ -200,14 +200,15 @@ py::tuple csr_from_edges(i64 n, py::array_t<i64, py::array::c_style | py::array:
 }
 
 // Planted-partition graph with the shape of an OGB node-property dataset.
-//   n nodes, ~m undirected edges, c classes; node v's community = its class.
+//   n nodes, ~m undirected edges, c classes; communities are contiguous id blocks,
+//   node labels follow the community except for a `label_noise` fraction.
 //   Each node draws a degree from a truncated power law with mean 2m/n; each
 //   edge end goes to the same community with probability `homophily` (a
 //   window of nearby ids inside the community -> locality) and uniformly at
 //   random otherwise.  Features: class centroid + N(0,1) noise (bf16-ready
 //   fp32), so a 2-layer GCN reaches a non-trivial validation accuracy.
 py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophily,
-                          double feat_noise, uint64_t seed) {
+                          double feat_noise, uint64_t seed, double label_noise) {
   py::array_t<i64> src_a(m), dst_a(m);
   py::array_t<i32> label_a(n);
   i64* src = src_a.mutable_data();
@@ -215,7 +216,14 @@ py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophil
   i32* lab = label_a.mutable_data();
   // contiguous communities: class blocks of roughly equal size
   const i64 block = (n + n_class - 1) / n_class;
-  for (i64 v = 0; v < n; ++v) lab[v] = (i32)std::min<i64>(v / block, n_class - 1);
+  std::vector<i32> comm(n);
+  for (i64 v = 0; v < n; ++v) comm[v] = (i32)std::min<i64>(v / block, n_class - 1);
+  // node label = its community's class, except a `label_noise` fraction drawn uniformly
+  for (i64 v = 0; v < n; ++v) {
+    const uint64_t h = mix64(seed ^ 0x1AB3ull ^ mix64((uint64_t)v));
+    const double u = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+    lab[v] = u < label_noise ? (i32)(mix64(h) % (uint64_t)n_class) : comm[v];
+  }
   const double mean_deg = (double)m / (double)n;   // edges per source node
 #pragma omp parallel for schedule(static)
   for (i64 e = 0; e < m; ++e) {
@@ -229,7 +237,7 @@ py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophil
     h = mix64(h);
     i64 t;
     if (u2 < homophily) {
-      const i64 c = lab[s];
+      const i64 c = comm[s];
       const i64 lo = c * block, hi = std::min<i64>(n, lo + block);
       const i64 win = std::max<i64>(16, (i64)(8 * mean_deg));
       const i64 off = (i64)(h % (uint64_t)(2 * win + 1)) - win;
@@ -349,7 +357,7 @@ PYBIND11_MODULE(_rt, m) {
         py::arg("symmetric") = true, py::arg("self_loops") = true, py::arg("dedup") = true);
   m.def("synthetic_graph", &synthetic_graph, py::arg("n"), py::arg("m"), py::arg("n_feat"),
         py::arg("n_class"), py::arg("homophily") = 0.8, py::arg("feat_noise") = 1.0,
-        py::arg("seed") = 0);
+        py::arg("seed") = 0, py::arg("label_noise") = 0.0);
   m.def("sample_neighbors", &sample_neighbors);
   m.def("num_threads", []() { return omp_get_max_threads(); });
 }

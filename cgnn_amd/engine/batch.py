@@ -96,7 +96,10 @@ class DeviceTrainer:
             self.step = torch.zeros(2, dtype=torch.int32, device=dev)
             self.rff_w = torch.zeros(R, max(F, 1), D + 1, **f32)
             self.rff_diff = torch.zeros(R, max(F, 1), **f32)
-            stream = torch.cuda.current_stream(dev)
+            # a dedicated (non-default) stream: hipGraph capture is not allowed on
+            # the legacy null stream, and batches on different devices overlap
+            self.stream = torch.cuda.Stream(dev)
+            stream = self.stream
             icfg = [R, N, D, self.H, P, stride, max_in, row_tiles, n_chunks, tpc, self.hist_len,
                     self.rff_k, d]
             fcfg = [float(learning_rate), 0.9, 0.999, 1e-8, float(init_std)]
@@ -114,6 +117,7 @@ class DeviceTrainer:
         with torch.cuda.device(self.device):
             self.step.zero_()
             self.loss_acc.zero_()
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
             self.engine.init()
             self.engine.tt()
 
@@ -122,9 +126,12 @@ class DeviceTrainer:
             self.engine.run(0, int(epochs), self.graph_chunk, self.hist_len > 0)
 
     def evaluate(self, epochs: int):
-        with torch.cuda.device(self.device):
+        with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
             self.loss_acc.zero_()
             self.engine.run(1, int(epochs), self.graph_chunk, False)
+
+    def _join(self):
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
 
     def launch(self, train_epochs: int, test_epochs: int):
         """Enqueue the whole train+eval schedule without synchronising."""
@@ -134,10 +141,12 @@ class DeviceTrainer:
         self._test_epochs = max(int(test_epochs), 1)
 
     def collect(self) -> np.ndarray:
+        self._join()
         scores = (self.loss_acc / float(self._test_epochs)).cpu().numpy().astype(np.float64)
         return scores
 
     def history(self) -> np.ndarray:
+        self._join()
         return self.hist[:, :self.hist_len].cpu().numpy()
 
     def run(self, train_epochs: int, test_epochs: int, verbose=False) -> np.ndarray:
@@ -152,4 +161,5 @@ class DeviceTrainer:
 
     def generated(self) -> np.ndarray:
         """Last generated samples, [R, d, N]."""
+        self._join()
         return self.xhat[:, :self.d].cpu().numpy()

@@ -1,0 +1,124 @@
+"""Node-property-prediction datasets for the GNN track (not in the reference).
+
+There is no network access, so the OGB / Planetoid datasets are replaced by
+synthetic graphs *of the same shape* (nodes, undirected edges, feature width,
+classes, split sizes) from the C++ generator ``_rt.synthetic_graph``: planted
+communities (one per class, contiguous id blocks, as after a graph-partitioning
+reorder), homophilous edges drawn uniformly inside the community, the rest
+uniform over the graph; node labels follow the community except for a
+``label_noise`` fraction, and features = centroid of the node's label + Gaussian
+noise -- so neither the graph nor the features alone determine the label and
+a GCN reaches a realistic (not saturated) accuracy.
+
+The CSR holds A + I, symmetrised and de-duplicated; the GCN normalisation
+D^-1/2 (A+I) D^-1/2 is kept as the vector ``dinv``.  On a GPU the CSR is built
+with device sorts; on the CPU with the C++ runtime.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import native
+
+# name: (nodes, undirected edges, features, classes, train, valid)  -- public dataset shapes
+SHAPES = {
+    "cora": (2708, 5278, 1433, 7, 140, 500),
+    "citeseer": (3327, 4552, 3703, 6, 120, 500),
+    "pubmed": (19717, 44324, 500, 3, 60, 500),
+    "ogbn-arxiv": (169343, 1166243, 128, 40, 90941, 29799),
+    "ogbn-products": (2449029, 61859140, 100, 47, 196615, 39323),
+    "reddit": (232965, 57307946, 602, 41, 153431, 23831),
+    "ogbn-papers100M": (111059956, 1615685872, 128, 172, 1207179, 125265),
+}
+
+
+@dataclasses.dataclass
+class GraphData:
+    n: int
+    rowptr: torch.Tensor      # int32 [n+1] (A + I)
+    col: torch.Tensor         # int32 [nnz]
+    dinv: torch.Tensor        # fp32 [n]  (deg of A+I)^-1/2
+    x: torch.Tensor           # fp32 [n, F] raw features
+    y: torch.Tensor           # int32 [n]
+    mask: torch.Tensor        # uint8 [n]: 1 train, 2 valid, 3 test
+    n_classes: int
+    name: str = "synthetic"
+
+    @property
+    def nnz(self):
+        return int(self.col.numel())
+
+    @property
+    def n_features(self):
+        return int(self.x.shape[1])
+
+    def to(self, device):
+        f = {k: (v.to(device) if torch.is_tensor(v) else v) for k, v in dataclasses.asdict(self).items()}
+        return GraphData(**f)
+
+
+def build_csr(n: int, src: np.ndarray, dst: np.ndarray, device=None):
+    """A + I symmetrised, de-duplicated CSR (int32 rowptr / col) on ``device``."""
+    device = torch.device(device) if device is not None else torch.device("cpu")
+    if device.type == "cuda":
+        s = torch.as_tensor(src, device=device, dtype=torch.int64)
+        d = torch.as_tensor(dst, device=device, dtype=torch.int64)
+        keep = s != d
+        s, d = s[keep], d[keep]
+        loops = torch.arange(n, device=device, dtype=torch.int64)
+        rows = torch.cat([s, d, loops])
+        cols = torch.cat([d, s, loops])
+        del s, d
+        key = torch.unique(rows * n + cols)          # sorted + de-duplicated
+        del rows, cols
+        r = key // n
+        c = (key - r * n).to(torch.int32)
+        counts = torch.bincount(r, minlength=n)
+        rowptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+        rowptr[1:] = torch.cumsum(counts, 0)
+        if rowptr[-1] >= 2 ** 31:
+            raise ValueError("nnz >= 2^31 needs int64 CSR (graph must be sharded)")
+        return rowptr.to(torch.int32), c
+    rp, col = native.rt().csr_from_edges(n, np.asarray(src, np.int64), np.asarray(dst, np.int64),
+                                         True, True, True)
+    return torch.from_numpy(np.asarray(rp).astype(np.int32)), torch.from_numpy(np.asarray(col))
+
+
+def synthetic(name: str = "ogbn-products", seed: int = 0, device=None, scale: float = 1.0,
+              homophily: float = 0.8, feat_noise: float = 4.0, label_noise: float = 0.25) -> GraphData:
+    """Synthetic graph with the shape of ``name`` (``scale`` shrinks nodes and edges)."""
+    n, m, F, C, n_train, n_val = SHAPES[name]
+    n = max(int(n * scale), C * 4)
+    m = max(int(m * scale), n)
+    n_train = max(int(n_train * scale), C)
+    n_val = max(int(n_val * scale), C)
+    src, dst, x, y = native.rt().synthetic_graph(n, m, F, C, homophily, feat_noise, seed, label_noise)
+    rowptr, col = build_csr(n, np.asarray(src), np.asarray(dst), device)
+    del src, dst
+    device = rowptr.device
+    deg = (rowptr[1:] - rowptr[:-1]).to(torch.float32)
+    dinv = deg.clamp_min(1).rsqrt()
+    # split: a seeded permutation (train / valid / rest test), like OGB's fixed split sizes
+    perm = np.random.default_rng(seed + 1).permutation(n)
+    mask = np.full(n, 3, dtype=np.uint8)
+    mask[perm[:n_train]] = 1
+    mask[perm[n_train:n_train + n_val]] = 2
+    return GraphData(n=n, rowptr=rowptr, col=col, dinv=dinv.to(device),
+                     x=torch.from_numpy(np.asarray(x)).to(device),
+                     y=torch.from_numpy(np.asarray(y).astype(np.int32)).to(device),
+                     mask=torch.from_numpy(mask).to(device), n_classes=C, name=name + "-synthetic")
+
+
+def partition_rows(g: GraphData, rank: int, world: int):
+    """Contiguous row block of ``rank`` (equal sizes, last one padded): local CSR
+    with global column ids, plus the row range."""
+    per = (g.n + world - 1) // world
+    r0, r1 = rank * per, min(g.n, (rank + 1) * per)
+    rp = g.rowptr[r0:r1 + 1].to(torch.int64)
+    col = g.col[int(rp[0]): int(rp[-1])]
+    rp = (rp - rp[0]).to(torch.int32)
+    return r0, r1, per, rp, col
