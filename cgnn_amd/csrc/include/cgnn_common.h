@@ -108,4 +108,15 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return t;
 }
 
+// XCD-aware block remap (MI355X: 8 XCDs, each with its own L2; the dispatcher
+// deals blocks round-robin over XCDs).  Returns a logical block id such that the
+// blocks resident on one XCD process a CONTIGUOUS range of the work.  Bijective
+// for any grid size (q = n/8, r = n%8).  Speed only -- never correctness.
+__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nwg) {
+  const unsigned q = nwg >> 3, r = nwg & 7u;
+  const unsigned xcd = b & 7u, idx = b >> 3;
+  const unsigned base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + idx;
+}
+
 }  // namespace cgnn

@@ -45,7 +45,7 @@ int rff_launch_fwd_bwd(int, const float*, const float*, const float*, float*, fl
                        int, int, int, int, float, hipStream_t);
 // GNN track
 int gnn_launch_spmm(const int*, const int*, const void*, void*, const float*, const float*, int,
-                    int, int, int, int, int, int, hipStream_t);
+                    int, int, int, int, int, int, int, hipStream_t);
 int gnn_launch_spmm_ce(const int*, const int*, const void*, const float*, const float*,
                        const int*, const uint8_t*, float*, void*, float*, int, int, int, int, float,
                        hipStream_t);
@@ -56,6 +56,10 @@ int gnn_spmm_ce_blocks(int);
 int gnn_launch_bias_relu_dropout(void*, const float*, long, int, int, float, uint32_t, uint32_t,
                                  uint32_t, hipStream_t);
 int gnn_launch_relu_dropout_bwd(void*, const void*, long, float, hipStream_t);
+int gnn_launch_dense_fwd(const void*, const float*, const float*, const float*, const float*, void*, void*,
+                         int, int, int, int, int, int, float, uint32_t, uint32_t, uint32_t, hipStream_t);
+int gnn_launch_dense_bwd(const void*, const float*, const void*, void*, int, int, int, int, float,
+                         hipStream_t);
 }
 
 static inline hipStream_t S(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -146,10 +150,11 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("gnn_spmm", [](uint64_t rowptr, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, uint64_t bias,
-                       int n_rows, int F, int ld_x, int ld_y, int x_bf16, int y_bf16, int relu, uint64_t st) {
+                       int n_rows, int F, int ld_x, int ld_y, int x_bf16, int y_bf16, int relu, int unit_col,
+                       uint64_t st) {
     chk(gnn_launch_spmm(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(x), Pt<void>(y),
                         Pt<const float>(rscale), Pt<const float>(bias), n_rows, F, ld_x, ld_y, x_bf16,
-                        y_bf16, relu, S(st)), "gnn_spmm");
+                        y_bf16, relu, unit_col, S(st)), "gnn_spmm");
   });
   m.def("gnn_spmm_ce", [](uint64_t rowptr, uint64_t col, uint64_t z, uint64_t rscale, uint64_t bias,
                           uint64_t labels, uint64_t mask, uint64_t loss_part, uint64_t dlogits, uint64_t correct,
@@ -172,6 +177,18 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("gnn_relu_dropout_bwd", [](uint64_t dh, uint64_t h, long n, float p, uint64_t st) {
     chk(gnn_launch_relu_dropout_bwd(Pt<void>(dh), Pt<const void>(h), n, p, S(st)), "gnn_relu_dropout_bwd");
+  });
+  m.def("gnn_dense_fwd", [](uint64_t ax, uint64_t w1, uint64_t b1, uint64_t w2, uint64_t dinv, uint64_t h1,
+                            uint64_t z2, int n, int F, int ldx, int HD, int C, int ldc, float p, uint32_t k0,
+                            uint32_t k1, uint32_t step, uint64_t st) {
+    return gnn_launch_dense_fwd(Pt<const void>(ax), Pt<const float>(w1), Pt<const float>(b1), Pt<const float>(w2),
+                                Pt<const float>(dinv), Pt<void>(h1), Pt<void>(z2), n, F, ldx, HD, C, ldc, p, k0,
+                                k1, step, S(st));
+  });
+  m.def("gnn_dense_bwd", [](uint64_t dy2, uint64_t w2, uint64_t h1, uint64_t dp1, int n, int HD, int C, int ldc,
+                            float p, uint64_t st) {
+    return gnn_launch_dense_bwd(Pt<const void>(dy2), Pt<const float>(w2), Pt<const void>(h1), Pt<void>(dp1), n,
+                                HD, C, ldc, p, S(st));
   });
   m.def("gnn_cast_bf16", [](uint64_t src, uint64_t dst, long n, uint64_t st) {
     chk(gnn_launch_cast_bf16(Pt<const float>(src), Pt<void>(dst), n, S(st)), "gnn_cast_bf16");

@@ -19,6 +19,8 @@
 // in flight per lane.  Accumulation is fp32; storage is bf16.
 #include "cgnn_common.h"
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 
 using namespace cgnn;
 
@@ -61,7 +63,7 @@ __device__ __forceinline__ void load8(const void* X, size_t off, float* f) {
 }
 
 // Sum the rows X[col[e]] for e in [e0, e1) into acc (8 features at f0).
-template <int L, bool XBF>
+template <int L, bool XBF, int U = 4>
 __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const void* __restrict__ X,
                                            int e0, int e1, int ldx, int f0, bool fv, int sub_base,
                                            int sl, float* acc) {
@@ -69,6 +71,21 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
     const int myj = (e + sl < e1) ? col[e + sl] : 0;
     const int cnt = min(L, e1 - e);
     int k = 0;
+    if (U == 8 && L >= 8) {
+      for (; k + 8 <= cnt; k += 8) {
+        int j[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) j[u] = __shfl(myj, sub_base + k + u, 64);
+        if (fv) {
+          float a[8][8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) load8<XBF>(X, (size_t)j[u] * ldx + f0, a[u]);
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            acc[q] += ((a[0][q] + a[1][q]) + (a[2][q] + a[3][q])) + ((a[4][q] + a[5][q]) + (a[6][q] + a[7][q]));
+        }
+      }
+    }
     for (; k + 4 <= cnt; k += 4) {
       const int j0 = __shfl(myj, sub_base + k + 0, 64);
       const int j1 = __shfl(myj, sub_base + k + 1, 64);
@@ -98,21 +115,22 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
 
 }  // namespace
 
-template <int L, bool XBF, bool YBF>
+template <int L, bool XBF, bool YBF, int U>
 __global__ __launch_bounds__(256) void spmm_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
     void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
-    int n_rows, int F, int ldx, int ldy, int relu) {
+    int n_rows, int F, int ldx, int ldy, int relu, int unit_col) {
   constexpr int RPW = 64 / L;
   const int lane = threadIdx.x & 63;
   const int sub = lane / L, sl = lane - sub * L;
-  const int row = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
+  const unsigned blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = (blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
   const bool rv = row < n_rows;
   const int f0 = sl * 8;
   const bool fv = rv && f0 < F;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
-  gather_sum<L, XBF>(col, X, e0, e1, ldx, f0, fv, sub * L, sl, acc);
+  gather_sum<L, XBF, U>(col, X, e0, e1, ldx, f0, fv, sub * L, sl, acc);
   if (!rv || f0 >= ldy) return;
   const float rs = rscale ? rscale[row] : 1.f;
   float y[8];
@@ -121,7 +139,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     const int f = f0 + q;
     float v = acc[q] * rs + ((bias && f < F) ? bias[f] : 0.f);
     if (relu) v = fmaxf(v, 0.f);
-    y[q] = f < F ? v : 0.f;
+    y[q] = f < F ? v : (f == unit_col ? 1.f : 0.f);
   }
   if (YBF) {
     *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
@@ -145,9 +163,13 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
   constexpr int L = 8, RPW = 8;
   __shared__ float s_red[4][4];
   __shared__ float s_cls[4][64];
+  __shared__ int s_cnt;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();   // the only barrier: at entry, where the waves are still in step
   const int sub = lane / L, sl = lane - sub * L;
-  const int row = (blockIdx.x * (blockDim.x >> 6) + wid) * RPW + sub;
+  const unsigned blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = (blk * (blockDim.x >> 6) + wid) * RPW + sub;
   const bool rv = row < n_rows;
   const int f0 = sl * 8;
   const bool fv = rv && f0 < C;
@@ -218,47 +240,62 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
   float v2 = wave_sum(split == 2 ? hit : 0.f);
   float v3 = wave_sum(split == 3 ? hit : 0.f);
   if (lane == 0) { s_red[wid][0] = v0; s_red[wid][1] = v1; s_red[wid][2] = v2; s_red[wid][3] = v3; }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    const int k = threadIdx.x;
-    stats[(size_t)blockIdx.x * 68 + k] = (s_red[0][k] + s_red[1][k]) + (s_red[2][k] + s_red[3][k]);
-  } else if (threadIdx.x >= 64 && threadIdx.x < 128) {
-    const int k = threadIdx.x - 64;
-    stats[(size_t)blockIdx.x * 68 + 4 + k] = (s_cls[0][k] + s_cls[1][k]) + (s_cls[2][k] + s_cls[3][k]);
+  // The LAST wave of the block to finish sums the four partials in fixed order
+  // (deterministic) -- no end-of-block barrier, so short rows do not wait for the
+  // block's longest row (power-law degrees).
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  int prev = 0;
+  if (lane == 0) prev = atomicAdd(&s_cnt, 1);
+  prev = __shfl(prev, 0, 64);
+  if (prev == (int)(blockDim.x >> 6) - 1) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (lane < 4) {
+      stats[(size_t)blk * 68 + lane] = (s_red[0][lane] + s_red[1][lane]) + (s_red[2][lane] + s_red[3][lane]);
+    }
+    stats[(size_t)blk * 68 + 4 + lane] = (s_cls[0][lane] + s_cls[1][lane]) + (s_cls[2][lane] + s_cls[3][lane]);
   }
 }
 
-// H = dropout(relu(P + b)) in place on a bf16 [rows][ld] matrix (first F columns valid).
-// Dropout keeps with probability 1-p and scales by 1/(1-p); the keep bit of element
-// (row, col) is bit (col % 4) of a Philox draw keyed (row, col/4, step): reproducible
-// and independent of launch geometry.  One thread per 8 consecutive columns.
+// H = dropout(relu(P + b)) in place on a bf16 [rows][ld] matrix (F valid columns,
+// F % 32 == 0).  Dropout keeps with probability 1-p (p quantised to 1/256) and scales
+// kept units by 1/(1-p).  Mask of element (row, n): byte (n%4) + 4*((n%32)/8) of the
+// Philox4x32 draw keyed (row, 2*(n/32) + (n/4)%2, step) -- the layout in which the
+// fused MFMA kernel (gnn_dense.hip) holds the values, so both produce the same mask.
+// One thread per (row, 32-column group, half): 16 values, one draw.
 __global__ __launch_bounds__(256) void bias_relu_dropout_kernel(
     uint16_t* __restrict__ Hm, const float* __restrict__ bias, long rows, int F, int ld, float p,
-    uint32_t k0, uint32_t k1, uint32_t step) {
-  const int cpr = ld / 8;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * cpr) return;
-  const long row = idx / cpr;
-  const int c0 = (int)(idx - row * cpr) * 8;
-  uint4* ptr = reinterpret_cast<uint4*>(Hm + row * ld + c0);
-  float v[8];
-  bf16x8_to_f32(*ptr, v);
+    uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8) {
+  const int per_row = F / 16;                                // (F/32 groups) x 2 halves
+  const uint32_t tpr = (uint32_t)per_row;
+  const uint32_t rpb = blockDim.x / tpr;
+  const uint32_t rloc = threadIdx.x / tpr;
+  const long row = (long)blockIdx.y * rpb + rloc;
+  if (rloc >= rpb || row >= rows) return;
+  const int k = (int)(threadIdx.x - rloc * tpr);
+  const int t = k >> 1, h = k & 1;
   const float scale = 1.f / (1.f - p);
-  const uint32_t thr = (uint32_t)(p * 4294967296.0);
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    u32x4 rnd = {0, 0, 0, 0};
-    if (p > 0.f) rnd = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)((c0 >> 2) + h), step, RNG_DROPOUT}, k0, k1);
-    const uint32_t rr[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = h * 4 + q, c = c0 + j;
-      float x = (c < F) ? fmaxf(v[j] + bias[c], 0.f) : 0.f;
-      if (p > 0.f) x = (rr[q] >= thr) ? x * scale : 0.f;
-      v[j] = x;
-    }
+  uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  if (thr8 > 0) {
+    const u32x4 r = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
+    w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
   }
-  *ptr = f32x8_to_bf16(v);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int n0 = 32 * t + 8 * g + 4 * h;
+    uint2* ptr = reinterpret_cast<uint2*>(Hm + row * ld + n0);
+    const uint2 hv = *ptr;
+    float v[4] = {__uint_as_float(hv.x << 16), __uint_as_float(hv.x & 0xffff0000u),
+                  __uint_as_float(hv.y << 16), __uint_as_float(hv.y & 0xffff0000u)};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = i + 4 * g;
+      float x = fmaxf(v[i] + bias[n0 + i], 0.f);
+      if (thr8 > 0) x = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
+      v[i] = x;
+    }
+    *ptr = make_uint2(f32_to_bf16_rne(v[0]) | (f32_to_bf16_rne(v[1]) << 16),
+                      f32_to_bf16_rne(v[2]) | (f32_to_bf16_rne(v[3]) << 16));
+  }
 }
 
 // dP = dH * [H > 0] * 1/(1-p)  (H already holds relu + dropout, so H > 0 iff the unit was
@@ -299,22 +336,40 @@ __global__ void cast_bf16_kernel(const float* __restrict__ src, uint16_t* __rest
 }
 
 // ---------------------------------------------------------------- launchers
+static int spmm_unroll() {
+  static int u = -1;
+  if (u < 0) {
+    const char* e = getenv("CGNN_SPMM_UNROLL");
+    u = (e && atoi(e) == 4) ? 4 : 8;
+  }
+  return u;
+}
+
+template <int L, int U>
+static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
+                         const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
+                         int relu, int uc, hipStream_t st) {
+  constexpr int RPB = 4 * (64 / L);   // rows per 256-thread block
+  dim3 grid((n_rows + RPB - 1) / RPB), block(256);
+  if (xbf && ybf) hipLaunchKernelGGL((spmm_kernel<L, true, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc);
+  else if (xbf) hipLaunchKernelGGL((spmm_kernel<L, true, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc);
+  else if (ybf) hipLaunchKernelGGL((spmm_kernel<L, false, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc);
+  else hipLaunchKernelGGL((spmm_kernel<L, false, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc);
+  return (int)hipGetLastError();
+}
+
 template <int L>
 static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
-                         int relu, hipStream_t st) {
-  constexpr int RPB = 4 * (64 / L);   // rows per 256-thread block
-  dim3 grid((n_rows + RPB - 1) / RPB), block(256);
-  if (xbf && ybf) hipLaunchKernelGGL((spmm_kernel<L, true, true>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu);
-  else if (xbf) hipLaunchKernelGGL((spmm_kernel<L, true, false>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu);
-  else if (ybf) hipLaunchKernelGGL((spmm_kernel<L, false, true>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu);
-  else hipLaunchKernelGGL((spmm_kernel<L, false, false>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu);
-  return (int)hipGetLastError();
+                         int relu, int uc, hipStream_t st) {
+  if (spmm_unroll() == 8)
+    return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, st);
+  return spmm_dispatch_u<L, 4>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, st);
 }
 
 extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X, void* Y,
                                const float* rscale, const float* bias, int n_rows, int F, int ldx,
-                               int ldy, int xbf, int ybf, int relu, hipStream_t st) {
+                               int ldy, int xbf, int ybf, int relu, int unit_col, hipStream_t st) {
   if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
   if (F > 512) {
     // wide features: column slabs of 512 (16-byte aligned offsets), one launch each
@@ -322,15 +377,16 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
     for (int c0 = 0; c0 < F; c0 += 512) {
       const int fc = std::min(512, F - c0);
       const int rc = gnn_launch_spmm(rowptr, col, (const char*)X + c0 * xs, (char*)Y + c0 * ys, rscale,
-                                     bias ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu, st);
+                                     bias ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu,
+                                     unit_col - c0, st);
       if (rc) return rc;
     }
     return 0;
   }
-  if (F <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
-  if (F <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
-  if (F <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
-  if (F <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, st);
+  if (F <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, st);
+  if (F <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, st);
+  if (F <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, st);
+  if (F <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, st);
   return -1;
 }
 
@@ -339,10 +395,13 @@ extern "C" int gnn_spmm_ce_blocks(int n_rows) { return (n_rows + 31) / 32; }
 extern "C" int gnn_launch_bias_relu_dropout(void* H, const float* bias, long rows, int F, int ld,
                                             float p, uint32_t k0, uint32_t k1, uint32_t step,
                                             hipStream_t st) {
-  if (ld % 8) return -3;
-  const long n = rows * (ld / 8);
-  hipLaunchKernelGGL(bias_relu_dropout_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                     (uint16_t*)H, bias, rows, F, ld, p, k0, k1, step);
+  if (F % 32 || F > ld || ld % 8 || F / 16 > 256) return -3;
+  const int rpb = 256 / (F / 16);
+  const long gy = (rows + rpb - 1) / rpb;
+  if (gy > 2147483647L) return -4;
+  const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
+  hipLaunchKernelGGL(bias_relu_dropout_kernel, dim3(1, (unsigned)gy), dim3(256), 0, st,
+                     (uint16_t*)H, bias, rows, F, ld, p, k0, k1, step, thr8);
   return (int)hipGetLastError();
 }
 

@@ -145,7 +145,7 @@ class ReferenceTrainer:
                 theta = self.params[r].clone().requires_grad_(True)
                 L = self.loss(r, theta)
                 (g,) = torch.autograd.grad(L, theta)
-                self.loss_history[r].append(float(L))
+                self.loss_history[r].append(float(L.detach()))
                 ms[r] = b1 * ms[r] + (1 - b1) * g
                 vs[r] = b2 * vs[r] + (1 - b2) * g * g
                 self.params[r] = self.params[r] - lr_t * ms[r] / (vs[r].sqrt() + eps)

@@ -7,11 +7,15 @@ Adam.  Storage bf16, accumulation fp32, master weights fp32.
 One epoch = one full-graph forward + backward + optimizer step:
 
   1. AX   = spmm(Xs)                       Xs = D^-1/2 X  (normalised once, like a cached Â)
-  2. H1   = dropout(relu(AX W1 + b1))      GEMM (hipBLASLt) + fused HIP epilogue (Philox mask)
-  3. Z2   = D^-1/2 (H1 W2)                 (all-gathered across ranks)
+  2. H1   = dropout(relu(AX W1 + b1))      } one fused MFMA kernel (gnn_dense.hip): both GEMMs,
+  3. Z2   = D^-1/2 (H1 W2)                 } bias, ReLU, Philox dropout, row scale; Z2 all-gathered
   4. loss, G = spmm_ce(Z2)                 aggregate + bias + log-softmax + NLL + dlogits, fused
   5. dY2  = D^-1/2 spmm(G)                 (G all-gathered across ranks; Â symmetric)
-  6. dW2 = H1^T dY2, dH1 = dY2 W2^T, relu/dropout backward (fused), dW1 = AX^T dP1
+  6. dH1 = dY2 W2^T, relu/dropout backward (fused); the weight gradients
+     dW2 = H1^T dY2 and [dW1; db1] = [AX | 1]^T dP1 are contractions over millions
+     of rows with tiny outputs, so they run as split-K batched GEMMs (row chunks
+     of CHUNK rows -> one fp32 partial per chunk -> fixed-order sum); db1 comes
+     for free from the ones column the layer-1 SpMM writes next to AX
   7. gradients all-reduced (RCCL), fused Adam
 
 Multi-GPU: each rank owns a contiguous block of rows (1-D partition); the
@@ -38,6 +42,10 @@ def _ru8(x):
     return (x + 7) // 8 * 8
 
 
+def _ru(x, m):
+    return (x + m - 1) // m * m
+
+
 def _mm_f32(a, b):
     """bf16 x bf16 -> fp32 output (fp32 accumulation)."""
     if a.is_cuda:
@@ -45,16 +53,38 @@ def _mm_f32(a, b):
     return a.float() @ b.float()
 
 
+CHUNK = 8192
+
+
+def _tsgemm(A, B, chunk=CHUNK):
+    """A^T B for tall A [M, k1], B [M, k2] (M a multiple of ``chunk``): split-K over
+    row chunks as one batched GEMM with fp32 partials, then a fixed-order sum."""
+    M = A.shape[0]
+    S = M // chunk
+    a = A.view(S, chunk, A.shape[1]).transpose(1, 2)
+    b = B.view(S, chunk, B.shape[1])
+    if A.is_cuda:
+        part = torch.bmm(a, b, out_dtype=torch.float32)
+    else:
+        part = torch.bmm(a.float(), b.float())
+    return part.sum(0)
+
+
 class GCNTrainer:
     def __init__(self, g: GraphData, hidden: int = 256, dropout: float = 0.5, lr: float = 0.01,
                  weight_decay: float = 0.0, seed: int = 0, rank: Optional[int] = None,
-                 world: Optional[int] = None):
+                 world: Optional[int] = None, fused: bool = True, align_rows: bool = False):
         self.rank = pdist.rank() if rank is None else rank
         self.world = pdist.world_size() if world is None else world
         self.dev = g.rowptr.device
         dev = self.dev
         self.F, self.C, self.hidden = g.n_features, g.n_classes, hidden
-        self.ldx, self.ldc = _ru8(self.F), _ru8(self.C)
+        # gathered rows padded to whole 128-byte lines when align_rows (fewer lines touched per
+        # gathered row: a 208-B row straddles 2-3 lines, a 256-B aligned row exactly 2)
+        if align_rows:
+            self.ldx, self.ldc = _ru(self.F + 1, 64), _ru(self.C, 64)
+        else:
+            self.ldx, self.ldc = _ru8(self.F + 1), _ru8(self.C)    # +1: ones column of AX
         self.p, self.lr, self.wd = float(dropout), float(lr), float(weight_decay)
         self.key = model_key(seed, "gcn-dropout")
         r0, r1, per, rp, col = partition_rows(g, self.rank, self.world)
@@ -93,15 +123,17 @@ class GCNTrainer:
         self.gb1 = self.grads[o[1]:o[2]]
         self.gW2 = self.grads[o[2]:o[3]].view(hidden, self.C)
         self.gb2 = self.grads[o[3]:o[4]]
-        # activations / workspaces (rows of this rank; Z2/G padded to `per` rows for all-gather)
+        # activations / workspaces (rows of this rank; Z2/G padded to `per` rows for all-gather;
+        # AX/H1/dH1/dY2 padded with zero rows to a multiple of CHUNK for the split-K GEMMs)
         n = self.nloc
-        self.AX = torch.zeros(n, self.ldx, **bf)
-        self.H1 = torch.zeros(n, hidden, **bf)
-        self.dH1 = torch.zeros(n, hidden, **bf)
+        self.npad = (n + CHUNK - 1) // CHUNK * CHUNK
+        self.AX = torch.zeros(self.npad, self.ldx, **bf)
+        self.H1 = torch.zeros(self.npad, hidden, **bf)
+        self.dH1 = torch.zeros(self.npad, hidden, **bf)
         self.W2b = torch.zeros(hidden, self.ldc, **bf)
         self.Z2loc = torch.zeros(per, self.ldc, **bf)
         self.Gloc = torch.zeros(per, self.ldc, **bf)
-        self.dY2 = torch.zeros(n, self.ldc, **bf)
+        self.dY2 = torch.zeros(self.npad, self.ldc, **bf)
         if self.world > 1:
             self.Z2 = torch.zeros(per * self.world, self.ldc, **bf)
             self.G = torch.zeros(per * self.world, self.ldc, **bf)
@@ -109,6 +141,9 @@ class GCNTrainer:
             self.Z2, self.G = self.Z2loc, self.Gloc
         self.epoch = 0
         self.last_stats = None
+        # fused MFMA dense kernels (gnn_dense.hip); shapes they do not cover fall back to
+        # hipBLASLt GEMMs + the standalone epilogue kernels
+        self.fused = bool(fused) and hidden % 32 == 0 and self.C <= 64
 
     # ------------------------------------------------------------------ passes
     def _all_gather(self, out, inp):
@@ -117,17 +152,21 @@ class GCNTrainer:
 
     def forward(self, train: bool):
         n, F, C = self.nloc, self.F, self.C
-        ops.spmm(self.rowptr, self.col, self.Xs, F, rscale=self.dinv, out=self.AX)
-        W1b = self.W1.to(torch.bfloat16)
-        if self.AX.is_cuda:
-            torch.mm(self.AX[:, :F], W1b, out=self.H1)
-        else:
-            self.H1.copy_((self.AX[:, :F].float() @ W1b.float()).to(torch.bfloat16))
-        ops.bias_relu_dropout_(self.H1, self.b1, self.hidden, self.p if train else 0.0, self.key, self.epoch)
+        ops.spmm(self.rowptr, self.col, self.Xs, F, rscale=self.dinv, out=self.AX, unit_col=F)
+        H1 = self.H1[:n]
+        p = self.p if train else 0.0
         self.W2b[:, :C] = self.W2.to(torch.bfloat16)
-        y2 = _mm_f32(self.H1, self.W2b)
-        torch.mul(y2, self.dinv[:, None], out=y2)
-        self.Z2loc[:n] = y2.to(torch.bfloat16)
+        if not (self.fused and ops.dense_fwd(self.AX, self.W1, self.b1, self.W2, self.dinv, H1,
+                                             self.Z2loc[:n], F, p, self.key, self.epoch)):
+            W1b = self.W1.to(torch.bfloat16)
+            if self.AX.is_cuda:
+                torch.mm(self.AX[:n, :F], W1b, out=H1)
+            else:
+                H1.copy_((self.AX[:n, :F].float() @ W1b.float()).to(torch.bfloat16))
+            ops.bias_relu_dropout_(H1, self.b1, self.hidden, p, self.key, self.epoch)
+            y2 = _mm_f32(H1, self.W2b)
+            torch.mul(y2, self.dinv[:, None], out=y2)
+            self.Z2loc[:n] = y2.to(torch.bfloat16)
         self._all_gather(self.Z2, self.Z2loc)
         stats, _ = ops.spmm_ce(self.rowptr, self.col, self.Z2, C, self.dinv, self.b2, self.y, self.mask,
                                1.0 / max(self.n_train, 1), mode=0 if train else 1,
@@ -138,16 +177,18 @@ class GCNTrainer:
         n, F, C = self.nloc, self.F, self.C
         self._all_gather(self.G, self.Gloc)
         ops.spmm(self.rowptr, self.col, self.G, C, rscale=self.dinv, out=self.dY2)
-        dY2 = self.dY2[:, :C]
-        self.gW2.copy_(_mm_f32(self.H1.t(), dY2))
+        self.gW2.copy_(_tsgemm(self.H1, self.dY2)[:, :C])
         self.gb2.copy_(stats[4:4 + C])
-        if self.dH1.is_cuda:
-            torch.mm(dY2, self.W2b[:, :C].t(), out=self.dH1)
-        else:
-            self.dH1.copy_((dY2.float() @ self.W2b[:, :C].float().t()).to(torch.bfloat16))
-        ops.relu_dropout_bwd_(self.dH1, self.H1, self.p)
-        self.gW1.copy_(_mm_f32(self.AX[:, :F].t(), self.dH1))
-        torch.sum(self.dH1, 0, dtype=torch.float32, out=self.gb1)
+        dH1 = self.dH1[:n]
+        if not (self.fused and ops.dense_bwd(self.dY2, self.W2, self.H1, dH1, self.p)):
+            if dH1.is_cuda:
+                torch.mm(self.dY2[:n, :C], self.W2b[:, :C].t(), out=dH1)
+            else:
+                dH1.copy_((self.dY2[:n, :C].float() @ self.W2b[:, :C].float().t()).to(torch.bfloat16))
+            ops.relu_dropout_bwd_(dH1, self.H1[:n], self.p)
+        g1 = _tsgemm(self.AX, self.dH1)               # rows 0..F-1: dW1, row F: db1 (ones column)
+        self.gW1.copy_(g1[:F])
+        self.gb1.copy_(g1[F])
         if self.world > 1:
             torch.distributed.all_reduce(self.grads)
 

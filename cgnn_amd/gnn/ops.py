@@ -23,8 +23,10 @@ def _row_ids(rowptr):
 
 
 def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dtype=torch.bfloat16,
-         ld_out=None):
-    """Y[i,:F] = act(rscale[i] * sum_{j in N(i)} X[j,:F] + bias); X is [*, ldx]."""
+         ld_out=None, unit_col=-1):
+    """Y[i,:F] = act(rscale[i] * sum_{j in N(i)} X[j,:F] + bias); X is [*, ldx].
+    Padding columns of Y are written 0, except ``unit_col`` which is written 1
+    (a ones column that turns the bias gradient into one more GEMM row)."""
     n = rowptr.numel() - 1
     ldo = ld_out or X.shape[1]
     if out is None:
@@ -34,7 +36,8 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
         hip.gnn_spmm(rowptr.data_ptr(), col.data_ptr(), X.data_ptr(), out.data_ptr(),
                      rscale.data_ptr() if rscale is not None else 0,
                      bias.data_ptr() if bias is not None else 0, n, F, X.shape[1], out.shape[1],
-                     int(X.dtype == torch.bfloat16), int(out.dtype == torch.bfloat16), int(relu), _st(X))
+                     int(X.dtype == torch.bfloat16), int(out.dtype == torch.bfloat16), int(relu), int(unit_col),
+                     _st(X))
         return out
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, F, dtype=torch.float32)
@@ -45,8 +48,10 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
         acc = acc + bias[:F]
     if relu:
         acc = acc.clamp_min(0)
-    out.zero_()
-    out[:, :F] = acc.to(out.dtype)
+    out[:n].zero_()
+    out[:n, :F] = acc.to(out.dtype)
+    if unit_col >= 0:
+        out[:n, unit_col] = 1
     return out
 
 
@@ -88,26 +93,75 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
     return stats, G
 
 
+def dropout_keep_mask(rows: int, F: int, p: float, key, step) -> torch.Tensor:
+    """Keep mask of the fused dropout: element (row, n) uses byte (n%4) + 4*((n%32)//8)
+    of the Philox draw keyed (row, 2*(n//32) + (n//4)%2, step), kept if >= round(256 p)."""
+    import numpy as np
+    thr8 = min(255, int(np.floor(p * 256.0 + 0.5)))
+    if thr8 == 0:
+        return torch.ones(rows, F, dtype=torch.bool)
+    r = np.arange(rows, dtype=np.uint32)[:, None]
+    n = np.arange(F)
+    ctr = (2 * (n // 32) + (n // 4) % 2).astype(np.uint32)[None, :]
+    words = np.stack(philox.philox4x32_10(r, ctr, step, philox.RNG_DROPOUT, key[0], key[1]), -1)
+    q = (n % 4) + 4 * ((n % 32) // 8)
+    wsel = np.take_along_axis(words, (q // 4)[None, :, None].repeat(rows, 0), -1)[..., 0]
+    byte = (wsel >> (8 * (q % 4)).astype(np.uint32)[None, :]) & 0xFF
+    return torch.from_numpy(byte >= thr8)
+
+
 def bias_relu_dropout_(H, bias, F, p, key, step):
-    """In place: H = dropout(relu(H + bias)) (Philox mask keyed by (row, col/4, step))."""
+    """In place: H = dropout(relu(H + bias)) (Philox mask keyed by (row, col/16, step))."""
     if H.is_cuda:
         native.hip().gnn_bias_relu_dropout(H.data_ptr(), bias.data_ptr(), H.shape[0], F, H.shape[1],
                                            float(p), int(key[0]), int(key[1]), int(step), _st(H))
         return H
-    import numpy as np
     x = torch.relu(H[:, :F].float() + bias[:F])
     if p > 0:
-        rows = np.arange(H.shape[0], dtype=np.uint32)[:, None]
-        cols = np.arange(F)
-        words = philox.philox4x32_10(rows, (cols // 4).astype(np.uint32)[None, :], step,
-                                     philox.RNG_DROPOUT, key[0], key[1])
-        w = np.stack(words, -1)                       # [n, F, 4]
-        r = np.take_along_axis(w, (cols % 4)[None, :, None].repeat(H.shape[0], 0), -1)[..., 0]
-        keep = torch.from_numpy(r.astype(np.uint64) >= np.uint64(int(p * 4294967296.0)))
+        keep = dropout_keep_mask(H.shape[0], F, p, key, step)
         x = torch.where(keep, x / (1 - p), torch.zeros_like(x))
     H.zero_()
     H[:, :F] = x.to(H.dtype)
     return H
+
+
+def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step):
+    """H1 = dropout(relu(AX[:, :F] W1 + b1)), Z2 = dinv * (H1 W2) (fused MFMA kernel on GPU)."""
+    n = H1.shape[0]
+    HD, C = W1.shape[1], W2.shape[1]
+    if AX.is_cuda:
+        rc = native.hip().gnn_dense_fwd(AX.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
+                                        dinv.data_ptr(), H1.data_ptr(), Z2.data_ptr(), n, F, AX.shape[1],
+                                        HD, C, Z2.shape[1], float(p), int(key[0]), int(key[1]), int(step),
+                                        _st(AX))
+        if rc == 0:
+            return True
+        if rc != -1:
+            raise RuntimeError("gnn_dense_fwd failed (%d)" % rc)
+        return False          # shape not covered by a compiled variant
+    H1.copy_((AX[:n, :F].float() @ W1.to(torch.bfloat16).float()).to(torch.bfloat16))
+    bias_relu_dropout_(H1, b1, HD, p, key, step)
+    y2 = H1.float() @ W2.to(torch.bfloat16).float()
+    Z2.zero_()
+    Z2[:, :C] = (y2 * dinv[:n, None]).to(torch.bfloat16)
+    return True
+
+
+def dense_bwd(dY2, W2, H1, dP1, p):
+    """dP1 = (dY2 W2^T) * [H1 > 0] / (1-p)."""
+    n = dP1.shape[0]
+    HD, C = W2.shape
+    if dY2.is_cuda:
+        rc = native.hip().gnn_dense_bwd(dY2.data_ptr(), W2.data_ptr(), H1.data_ptr(), dP1.data_ptr(), n,
+                                        HD, C, dY2.shape[1], float(p), _st(dY2))
+        if rc == 0:
+            return True
+        if rc != -1:
+            raise RuntimeError("gnn_dense_bwd failed (%d)" % rc)
+        return False
+    g = dY2[:n, :C].float() @ W2.to(torch.bfloat16).float().t()
+    dP1.copy_(torch.where(H1[:n].float() > 0, g / (1 - p), torch.zeros_like(g)).to(torch.bfloat16))
+    return True
 
 
 def relu_dropout_bwd_(dH, H, p):

@@ -1,0 +1,189 @@
+"""Settings, formats, Philox RNG, DAG programs and the fp64 oracle (CPU)."""
+import math
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import cgnn
+from cgnn_amd.engine.program import (PROG_HDR, NODE_REC, program_for_confounders, program_for_dag,
+                                     program_for_pair, pack_programs)
+from cgnn_amd.engine.reference import (GAMMAS, ReferenceTrainer, mmd_loss_dense, rff_frequencies,
+                                       rff_mmd_loss)
+from cgnn_amd.utils import philox
+from cgnn_amd.utils.formats import CCEPC_PairsFileReader, standardize, write_cepc_pairs
+from cgnn_amd.utils.graph import DirectedGraph, UndirectedGraph
+from cgnn_amd.utils.settings import DefaultSettings
+
+from conftest import example, have_example
+
+
+# ------------------------------------------------------------------ settings
+def test_settings_defaults_and_slots():
+    s = DefaultSettings()
+    assert (s.NB_RUNS, s.NB_JOBS, s.GPU, s.NB_GPU, s.GPU_OFFSET) == (32, 1, True, 1, 0)
+    assert (s.learning_rate, s.init_weights, s.max_nb_points) == (0.01, 0.05, 1500)
+    assert (s.h_layer_dim, s.train_epochs, s.test_epochs) == (20, 1000, 500)
+    assert (s.use_Fast_MMD, s.nb_vectors_approx_MMD, s.complexity_graph_param) == (False, 100, 5e-5)
+    with pytest.raises(AttributeError):
+        s.nb_runs = 3      # typo'd attribute (lower case) must raise, as with __slots__
+
+
+def test_snapshot_kwargs_precedence():
+    s = DefaultSettings()
+    s.NB_RUNS = 8
+    c = s.snapshot(init_std=0.1, nb_runs=4, h_layer_dim=30)
+    assert c.init_std == 0.1 and c.nb_runs == 4 and c.h_layer_dim == 30
+    assert s.snapshot().nb_runs == 8
+
+
+def test_env_override(monkeypatch):
+    monkeypatch.setenv("CGNN_NB_RUNS", "5")
+    monkeypatch.setenv("CGNN_USE_FAST_MMD", "1")
+    s = DefaultSettings()
+    assert s.NB_RUNS == 5 and s.use_Fast_MMD is True
+
+
+# ------------------------------------------------------------------ formats
+def test_standardize_matches_population_scale():
+    x = np.random.default_rng(0).normal(3, 2, size=(100, 3))
+    z = standardize(x)
+    np.testing.assert_allclose(z.mean(0), 0, atol=1e-12)
+    np.testing.assert_allclose(z.std(0), 1, atol=1e-12)
+    assert np.all(standardize(np.ones(5)) == 0)
+
+
+def test_cepc_roundtrip(tmp_path):
+    a = [np.arange(5.0), np.array([1.5, -2.0, 3.0])]
+    b = [np.arange(5.0) ** 2, np.array([0.0, 1.0, 2.0])]
+    p = tmp_path / "pairs.csv"
+    write_cepc_pairs(p, ["p1", "p2"], a, b)
+    df = CCEPC_PairsFileReader(p, scale=False)
+    assert list(df.SampleID) == ["p1", "p2"]
+    np.testing.assert_allclose(df.A[1], a[1])
+    np.testing.assert_allclose(df.B[0], b[0])
+    dfs = CCEPC_PairsFileReader(p, scale=True)
+    np.testing.assert_allclose(dfs.A[0], standardize(a[0]))
+
+
+@pytest.mark.skipif(not have_example("Example_pairwise_pairs.csv"), reason="reference examples absent")
+def test_reads_reference_pairs_file():
+    df = CCEPC_PairsFileReader(example("Example_pairwise_pairs.csv"))
+    assert len(df) == 5 and all(len(a) == 1500 for a in df.A)
+
+
+# ------------------------------------------------------------------ philox
+def test_philox_known_answer():
+    # Random123 known-answer vectors for philox4x32-10
+    out = philox.philox4x32_10(0, 0, 0, 0, 0, 0)
+    assert [int(x) for x in out] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    out = philox.philox4x32_10(0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF)
+    assert [int(x) for x in out] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+
+
+def test_philox_normals_are_standard():
+    z = philox.normal(1, 2, np.arange(200000, dtype=np.uint32), 3, 4, philox.RNG_NODE_NOISE)
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+    z2 = philox.normal(1, 2, np.arange(10, dtype=np.uint32), 3, 5, philox.RNG_NODE_NOISE)
+    assert not np.allclose(z[:10], z2)          # a different step draws fresh noise
+
+
+def test_model_keys_are_stable():
+    assert philox.model_key(0, "a", 1) == philox.model_key(0, "a", 1)
+    assert philox.model_key(0, "a", 1) != philox.model_key(0, "a", 2)
+
+
+# ------------------------------------------------------------------ programs
+def test_program_layout_and_param_count():
+    g = DirectedGraph()
+    for a, b in [("x", "y"), ("x", "z"), ("y", "z")]:
+        g.add(a, b)
+    H = 20
+    p = program_for_dag(g, H)
+    recs = list(p.node_records())
+    assert [r[0] for r in recs] == [0, 1, 2]          # generation order x, y, z
+    assert [len(r[2]) for r in recs] == [0, 1, 2]     # parent counts
+    assert p.n_params == sum((len(r[2]) + 1 + 2) * H + 1 for r in recs)
+    assert p.max_in == 3
+
+
+def test_confounder_program_shares_edge_noise():
+    skel = UndirectedGraph()
+    skel.add("a", "b")
+    skel.add("b", "c")
+    g = DirectedGraph(skeleton=skel)
+    g.add("a", "b")
+    p = program_for_confounders(g, 5)
+    recs = {r[0]: r for r in p.node_records()}
+    # every node gets one confounder input per skeleton neighbour; b sees both edges
+    assert sorted(recs[1][3]) == [0, 1]
+    assert recs[0][3] == [0] and recs[2][3] == [1]
+    assert p.n_conf == 2
+
+
+def test_pair_program_clamps_cause():
+    p = program_for_pair(30)
+    recs = list(p.node_records())
+    assert recs[0][1] == 1 and recs[1][1] == 0 and recs[1][2] == [0]
+    assert p.n_params == (2 + 2) * 30 + 1
+
+
+def test_cyclic_graph_program_rejected():
+    g = DirectedGraph()
+    g.add("a", "b")
+    g.add("b", "a")
+    with pytest.raises(Exception):
+        program_for_dag(g, 5)
+
+
+# ------------------------------------------------------------------ oracle
+def test_mmd_dense_matches_brute_force():
+    rng = np.random.default_rng(1)
+    p, t = rng.normal(size=(7, 3)), rng.normal(size=(7, 3))
+    brute = 0.0
+    X = np.vstack([p, t])
+    s = np.r_[np.full(7, 1 / 7), np.full(7, -1 / 7)]
+    for i in range(14):
+        for j in range(14):
+            d2 = ((X[i] - X[j]) ** 2).sum()
+            brute += s[i] * s[j] * sum(math.exp(-g * d2) for g in GAMMAS)
+    got = float(mmd_loss_dense(torch.tensor(p), torch.tensor(t)))
+    assert abs(got - brute) < 1e-12
+
+
+def test_mmd_analytic_gradient_matches_finite_difference():
+    rng = np.random.default_rng(2)
+    p = torch.tensor(rng.normal(size=(9, 2)), requires_grad=True)
+    t = torch.tensor(rng.normal(size=(9, 2)))
+    L = mmd_loss_dense(p, t)
+    (g,) = torch.autograd.grad(L, p)
+    # the fused kernel's closed form: g_i = 4/N^2 sum_j sign_j w_ij (x_j - p_i)
+    N = 9
+    X = torch.cat([p.detach(), t])
+    sign = torch.cat([torch.ones(N), -torch.ones(N)]).double()
+    d2 = torch.cdist(p.detach(), X) ** 2
+    w = sum(gm * torch.exp(-gm * d2) for gm in GAMMAS)
+    closed = 4.0 / N ** 2 * ((sign[None, :] * w)[:, :, None] * (X[None, :, :] - p.detach()[:, None, :])).sum(1)
+    np.testing.assert_allclose(g.numpy(), closed.numpy(), rtol=1e-10, atol=1e-12)
+
+
+def test_rff_frequencies_shape_and_scale():
+    W = rff_frequencies((3, 4), 0, k=50, d=2)
+    assert W.shape == (3, 350)
+    assert torch.all((W[2] >= 0) & (W[2] <= 2 * math.pi))
+    # block b has std 2*gamma_b (reference scaling, B12)
+    assert abs(W[:2, 300:].std().item() / 100.0 - 1) < 0.25
+
+
+def test_reference_trainer_decreases_loss():
+    p = program_for_pair(20)
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=300)
+    y = np.tanh(2 * x) + 0.1 * rng.normal(size=300)
+    data = standardize(np.stack([x, y], 0).T).T.astype(np.float32)
+    tr = ReferenceTrainer([p], [data], [(1, 2)], 20, learning_rate=0.01)
+    tr.train(60)
+    h = tr.loss_history[0]
+    assert np.mean(h[-10:]) < 0.7 * np.mean(h[:5])

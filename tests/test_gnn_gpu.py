@@ -54,6 +54,36 @@ def test_spmm_ce_matches_reference():
     np.testing.assert_allclose(g_got.cpu().float().numpy(), g_ref.float().numpy(), atol=2e-5, rtol=2e-2)
 
 
+def test_fused_dense_matches_reference():
+    torch.manual_seed(5)
+    n, F, HD, C = 777, 100, 256, 47
+    AX = torch.zeros(n, 104, dtype=torch.bfloat16)
+    AX[:, :F] = torch.randn(n, F).to(torch.bfloat16)
+    AX[:, F] = 1
+    W1, b1 = torch.randn(F, HD) * 0.1, torch.randn(HD) * 0.1
+    W2 = torch.randn(HD, C) * 0.1
+    dinv = torch.rand(n) + 0.5
+    dY2 = torch.zeros(n, 48, dtype=torch.bfloat16)
+    dY2[:, :C] = (torch.randn(n, C) * 0.01).to(torch.bfloat16)
+    outs, h1_gpu = [], None
+    for dev in ("cuda:0", "cpu"):
+        H1 = torch.zeros(n, HD, dtype=torch.bfloat16, device=dev)
+        Z2 = torch.zeros(n, 48, dtype=torch.bfloat16, device=dev)
+        assert ops.dense_fwd(AX.to(dev), W1.to(dev), b1.to(dev), W2.to(dev), dinv.to(dev), H1, Z2, F, 0.5,
+                             (9, 10), 3)
+        # the backward of both paths uses the SAME H1 (the GPU one): its mask defines dP1
+        h1_gpu = H1.cpu() if h1_gpu is None else h1_gpu
+        dP1 = torch.zeros(n, HD, dtype=torch.bfloat16, device=dev)
+        assert ops.dense_bwd(dY2.to(dev), W2.to(dev), h1_gpu.to(dev), dP1, 0.5)
+        outs.append((H1.cpu().float(), Z2.cpu().float(), dP1.cpu().float()))
+    (h, z, d), (h_ref, z_ref, d_ref) = outs
+    # same dropout mask; bf16 rounding of the GEMM inputs/outputs only
+    assert ((h_ref > 0) != (h > 0)).float().mean() < 0.01
+    np.testing.assert_allclose(h.numpy(), h_ref.numpy(), atol=3e-2, rtol=3e-2)
+    np.testing.assert_allclose(z.numpy(), z_ref.numpy(), atol=3e-2, rtol=5e-2)
+    np.testing.assert_allclose(d.numpy(), d_ref.numpy(), atol=2e-3, rtol=5e-2)
+
+
 def test_dropout_mask_matches_reference():
     torch.manual_seed(2)
     H = torch.randn(300, 256).to(torch.bfloat16)
@@ -65,10 +95,12 @@ def test_dropout_mask_matches_reference():
     assert 0.2 < keep < 0.4   # relu (~1/2) x keep (1/2)
 
 
-def test_gcn_steps_match_cpu():
-    g = synthetic("cora", seed=3, device="cpu")
+@pytest.mark.parametrize("name,fused", [("cora", True), ("ogbn-arxiv", True), ("ogbn-products", True),
+                                        ("ogbn-products", False)])
+def test_gcn_steps_match_cpu(name, fused):
+    g = synthetic(name, seed=3, device="cpu", scale=1.0 if name == "cora" else 0.003)
     cpu = GCNTrainer(g, hidden=64, rank=0, world=1)
-    gpu = GCNTrainer(g.to("cuda:0"), hidden=64, rank=0, world=1)
+    gpu = GCNTrainer(g.to("cuda:0"), hidden=64, rank=0, world=1, fused=fused)
     for _ in range(3):
         cpu.train_step()
         gpu.train_step()
