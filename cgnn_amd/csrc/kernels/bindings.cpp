@@ -54,10 +54,11 @@ int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, flo
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
 int gnn_spmm_ce_blocks(int);
 int gnn_launch_bias_relu_dropout(void*, const float*, long, int, int, float, uint32_t, uint32_t,
-                                 uint32_t, hipStream_t);
+                                 uint32_t, uint32_t, hipStream_t);
 int gnn_launch_relu_dropout_bwd(void*, const void*, long, float, hipStream_t);
 int gnn_launch_dense_fwd(const void*, const float*, const float*, const float*, const float*, void*, void*,
-                         int, int, int, int, int, int, float, uint32_t, uint32_t, uint32_t, hipStream_t);
+                         int, int, int, int, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t,
+                         hipStream_t);
 int gnn_launch_dense_bwd(const void*, const float*, const void*, void*, int, int, int, int, float,
                          hipStream_t);
 }
@@ -171,8 +172,8 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("gnn_spmm_ce_blocks", &gnn_spmm_ce_blocks);
   m.def("gnn_bias_relu_dropout", [](uint64_t h, uint64_t bias, long rows, int F, int ld, float p, uint32_t k0,
-                                    uint32_t k1, uint32_t step, uint64_t st) {
-    chk(gnn_launch_bias_relu_dropout(Pt<void>(h), Pt<const float>(bias), rows, F, ld, p, k0, k1, step, S(st)),
+                                    uint32_t k1, uint32_t step, uint32_t row0, uint64_t st) {
+    chk(gnn_launch_bias_relu_dropout(Pt<void>(h), Pt<const float>(bias), rows, F, ld, p, k0, k1, step, row0, S(st)),
         "gnn_bias_relu_dropout");
   });
   m.def("gnn_relu_dropout_bwd", [](uint64_t dh, uint64_t h, long n, float p, uint64_t st) {
@@ -180,10 +181,10 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("gnn_dense_fwd", [](uint64_t ax, uint64_t w1, uint64_t b1, uint64_t w2, uint64_t dinv, uint64_t h1,
                             uint64_t z2, int n, int F, int ldx, int HD, int C, int ldc, float p, uint32_t k0,
-                            uint32_t k1, uint32_t step, uint64_t st) {
+                            uint32_t k1, uint32_t step, uint32_t row0, uint64_t st) {
     return gnn_launch_dense_fwd(Pt<const void>(ax), Pt<const float>(w1), Pt<const float>(b1), Pt<const float>(w2),
                                 Pt<const float>(dinv), Pt<void>(h1), Pt<void>(z2), n, F, ldx, HD, C, ldc, p, k0,
-                                k1, step, S(st));
+                                k1, step, row0, S(st));
   });
   m.def("gnn_dense_bwd", [](uint64_t dy2, uint64_t w2, uint64_t h1, uint64_t dp1, int n, int HD, int C, int ldc,
                             float p, uint64_t st) {

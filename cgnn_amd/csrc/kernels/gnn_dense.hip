@@ -61,7 +61,7 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
     const uint16_t* __restrict__ AX, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ dinv, uint16_t* __restrict__ H1,
     uint16_t* __restrict__ Z2, int n, int F, int ldx, int C, int ldc, float p, uint32_t k0,
-    uint32_t k1, uint32_t step, uint32_t thr8) {
+    uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0) {
   constexpr int KP = KS * 16;
   constexpr int W1S = KP + 8;          // padded row strides (bank-conflict-free b128 / b64 reads)
   constexpr int W2S = HD + 8;
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
       // epilogue: bias, relu, dropout (one Philox draw = this lane's 16 bytes)
       uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
       if (thr8 > 0) {
-        const u32x4 r = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
+        const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
         w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
       }
       float v[16];
@@ -232,26 +232,26 @@ template <int KS, int HD>
 static int fwd_launch(const uint16_t* AX, const float* W1, const float* b1, const float* W2,
                       const float* dinv, uint16_t* H1, uint16_t* Z2, int n, int F, int ldx, int C,
                       int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
-                      hipStream_t st) {
+                      uint32_t row0, hipStream_t st) {
   const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KS * 16 + 8) + 64 * (size_t)(HD + 8)) + sizeof(float) * HD;
   (void)hipFuncSetAttribute((const void*)gcn_dense_fwd_kernel<KS, HD>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((gcn_dense_fwd_kernel<KS, HD>), dim3(dense_grid(n)), dim3(WAVES * 64), lds, st, AX, W1,
-                     b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8);
+                     b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0);
   return (int)hipGetLastError();
 }
 
 extern "C" int gnn_launch_dense_fwd(const void* AX, const float* W1, const float* b1, const float* W2,
                                     const float* dinv, void* H1, void* Z2, int n, int F, int ldx,
                                     int HD, int C, int ldc, float p, uint32_t k0, uint32_t k1,
-                                    uint32_t step, hipStream_t st) {
+                                    uint32_t step, uint32_t row0, hipStream_t st) {
   if (C > 64 || ldc % 8 || ldx % 8 || ldc > 64) return -3;
   const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
   const int KS = (F + 15) / 16;
   auto* ax = (const uint16_t*)AX;
   auto* h1 = (uint16_t*)H1;
   auto* z2 = (uint16_t*)Z2;
-#define FWD(ks, hd) if (KS <= ks && HD == hd) return fwd_launch<ks, hd>(ax, W1, b1, W2, dinv, h1, z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, st);
+#define FWD(ks, hd) if (KS <= ks && HD == hd) return fwd_launch<ks, hd>(ax, W1, b1, W2, dinv, h1, z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, st);
   FWD(4, 256) FWD(7, 256) FWD(8, 256) FWD(4, 128) FWD(8, 128)
 #undef FWD
   return -1;

@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
 // One thread per (row, 32-column group, half): 16 values, one draw.
 __global__ __launch_bounds__(256) void bias_relu_dropout_kernel(
     uint16_t* __restrict__ Hm, const float* __restrict__ bias, long rows, int F, int ld, float p,
-    uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8) {
+    uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0) {
   const int per_row = F / 16;                                // (F/32 groups) x 2 halves
   const uint32_t tpr = (uint32_t)per_row;
   const uint32_t rpb = blockDim.x / tpr;
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void bias_relu_dropout_kernel(
   const float scale = 1.f / (1.f - p);
   uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
   if (thr8 > 0) {
-    const u32x4 r = philox4x32_10(u32x4{(uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
+    const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
     w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
   }
 #pragma unroll
@@ -394,14 +394,14 @@ extern "C" int gnn_spmm_ce_blocks(int n_rows) { return (n_rows + 31) / 32; }
 
 extern "C" int gnn_launch_bias_relu_dropout(void* H, const float* bias, long rows, int F, int ld,
                                             float p, uint32_t k0, uint32_t k1, uint32_t step,
-                                            hipStream_t st) {
+                                            uint32_t row0, hipStream_t st) {
   if (F % 32 || F > ld || ld % 8 || F / 16 > 256) return -3;
   const int rpb = 256 / (F / 16);
   const long gy = (rows + rpb - 1) / rpb;
   if (gy > 2147483647L) return -4;
   const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
   hipLaunchKernelGGL(bias_relu_dropout_kernel, dim3(1, (unsigned)gy), dim3(256), 0, st,
-                     (uint16_t*)H, bias, rows, F, ld, p, k0, k1, step, thr8);
+                     (uint16_t*)H, bias, rows, F, ld, p, k0, k1, step, thr8, row0);
   return (int)hipGetLastError();
 }
 

@@ -157,13 +157,13 @@ class GCNTrainer:
         p = self.p if train else 0.0
         self.W2b[:, :C] = self.W2.to(torch.bfloat16)
         if not (self.fused and ops.dense_fwd(self.AX, self.W1, self.b1, self.W2, self.dinv, H1,
-                                             self.Z2loc[:n], F, p, self.key, self.epoch)):
+                                             self.Z2loc[:n], F, p, self.key, self.epoch, self.r0)):
             W1b = self.W1.to(torch.bfloat16)
             if self.AX.is_cuda:
                 torch.mm(self.AX[:n, :F], W1b, out=H1)
             else:
                 H1.copy_((self.AX[:n, :F].float() @ W1b.float()).to(torch.bfloat16))
-            ops.bias_relu_dropout_(H1, self.b1, self.hidden, p, self.key, self.epoch)
+            ops.bias_relu_dropout_(H1, self.b1, self.hidden, p, self.key, self.epoch, self.r0)
             y2 = _mm_f32(H1, self.W2b)
             torch.mul(y2, self.dinv[:, None], out=y2)
             self.Z2loc[:n] = y2.to(torch.bfloat16)

@@ -93,14 +93,14 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
     return stats, G
 
 
-def dropout_keep_mask(rows: int, F: int, p: float, key, step) -> torch.Tensor:
+def dropout_keep_mask(rows: int, F: int, p: float, key, step, row0: int = 0) -> torch.Tensor:
     """Keep mask of the fused dropout: element (row, n) uses byte (n%4) + 4*((n%32)//8)
     of the Philox draw keyed (row, 2*(n//32) + (n//4)%2, step), kept if >= round(256 p)."""
     import numpy as np
     thr8 = min(255, int(np.floor(p * 256.0 + 0.5)))
     if thr8 == 0:
         return torch.ones(rows, F, dtype=torch.bool)
-    r = np.arange(rows, dtype=np.uint32)[:, None]
+    r = (row0 + np.arange(rows)).astype(np.uint32)[:, None]
     n = np.arange(F)
     ctr = (2 * (n // 32) + (n // 4) % 2).astype(np.uint32)[None, :]
     words = np.stack(philox.philox4x32_10(r, ctr, step, philox.RNG_DROPOUT, key[0], key[1]), -1)
@@ -110,22 +110,23 @@ def dropout_keep_mask(rows: int, F: int, p: float, key, step) -> torch.Tensor:
     return torch.from_numpy(byte >= thr8)
 
 
-def bias_relu_dropout_(H, bias, F, p, key, step):
-    """In place: H = dropout(relu(H + bias)) (Philox mask keyed by (row, col/16, step))."""
+def bias_relu_dropout_(H, bias, F, p, key, step, row0=0):
+    """In place: H = dropout(relu(H + bias)); the mask is keyed by the GLOBAL row
+    (row0 + local row), so it does not depend on how rows are partitioned."""
     if H.is_cuda:
         native.hip().gnn_bias_relu_dropout(H.data_ptr(), bias.data_ptr(), H.shape[0], F, H.shape[1],
-                                           float(p), int(key[0]), int(key[1]), int(step), _st(H))
+                                           float(p), int(key[0]), int(key[1]), int(step), int(row0), _st(H))
         return H
     x = torch.relu(H[:, :F].float() + bias[:F])
     if p > 0:
-        keep = dropout_keep_mask(H.shape[0], F, p, key, step)
+        keep = dropout_keep_mask(H.shape[0], F, p, key, step, row0)
         x = torch.where(keep, x / (1 - p), torch.zeros_like(x))
     H.zero_()
     H[:, :F] = x.to(H.dtype)
     return H
 
 
-def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step):
+def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step, row0=0):
     """H1 = dropout(relu(AX[:, :F] W1 + b1)), Z2 = dinv * (H1 W2) (fused MFMA kernel on GPU)."""
     n = H1.shape[0]
     HD, C = W1.shape[1], W2.shape[1]
@@ -133,14 +134,14 @@ def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step):
         rc = native.hip().gnn_dense_fwd(AX.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
                                         dinv.data_ptr(), H1.data_ptr(), Z2.data_ptr(), n, F, AX.shape[1],
                                         HD, C, Z2.shape[1], float(p), int(key[0]), int(key[1]), int(step),
-                                        _st(AX))
+                                        int(row0), _st(AX))
         if rc == 0:
             return True
         if rc != -1:
             raise RuntimeError("gnn_dense_fwd failed (%d)" % rc)
         return False          # shape not covered by a compiled variant
     H1.copy_((AX[:n, :F].float() @ W1.to(torch.bfloat16).float()).to(torch.bfloat16))
-    bias_relu_dropout_(H1, b1, HD, p, key, step)
+    bias_relu_dropout_(H1, b1, HD, p, key, step, row0)
     y2 = H1.float() @ W2.to(torch.bfloat16).float()
     Z2.zero_()
     Z2[:, :C] = (y2 * dinv[:n, None]).to(torch.bfloat16)

@@ -1,0 +1,113 @@
+"""Host C++ runtime (_rt), synthetic generators and the GNN track on CPU."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from cgnn_amd import native
+from cgnn_amd.generators import RandomGraphGenerator, functions_default as fd
+from cgnn_amd.gnn import ops
+from cgnn_amd.gnn.data import SHAPES, build_csr, partition_rows, synthetic
+from cgnn_amd.gnn.gcn import GCNTrainer
+from cgnn_amd.utils.formats import CCEPC_PairsFileReader
+
+
+def test_csr_builder_symmetric_dedup_self_loops():
+    rt = native.rt()
+    rp, col = rt.csr_from_edges(4, np.array([0, 0, 1, 2, 2]), np.array([1, 1, 2, 2, 3]), True, True, True)
+    rp, col = np.asarray(rp), np.asarray(col)
+    rows = {i: sorted(col[rp[i]:rp[i + 1]].tolist()) for i in range(4)}
+    assert rows == {0: [0, 1], 1: [0, 1, 2], 2: [1, 2, 3], 3: [2, 3]}
+
+
+def test_build_csr_matches_dense_adjacency():
+    rng = np.random.default_rng(0)
+    n = 50
+    src, dst = rng.integers(0, n, 300), rng.integers(0, n, 300)
+    rp, col = build_csr(n, src, dst, "cpu")
+    A = np.zeros((n, n), bool)
+    A[src, dst] = A[dst, src] = True
+    np.fill_diagonal(A, True)
+    B = np.zeros((n, n), bool)
+    for i in range(n):
+        B[i, col[rp[i]:rp[i + 1]].numpy()] = True
+    assert (A == B).all()
+
+
+def test_dag_acyclicity_and_hash():
+    rt = native.rt()
+    assert rt.is_acyclic(3, [(0, 1), (1, 2)]) and not rt.is_acyclic(2, [(0, 1), (1, 0)])
+    assert rt.canonical_hash([(0, 1), (2, 3)]) == rt.canonical_hash([(2, 3), (0, 1)])
+    assert rt.canonical_hash([(0, 1)]) != rt.canonical_hash([(1, 0)])
+
+
+def test_neighbor_sampler_blocks():
+    g = synthetic("cora", seed=0)
+    seeds = np.arange(10)
+    blocks = native.rt().sample_neighbors(g.rowptr.numpy().astype(np.int64), g.col.numpy(), seeds, [5, 3], 7)
+    assert len(blocks) == 2
+    rp, col, nodes = (np.asarray(x) for x in blocks[0])
+    assert len(rp) == 11 and np.all(np.diff(rp) <= 5)
+    assert list(nodes[:10]) == list(seeds)            # destination nodes are a prefix
+    assert col.max() < len(nodes)
+    # every sampled neighbour is a real neighbour
+    for i in range(10):
+        nb = set(g.col[g.rowptr[i]:g.rowptr[i + 1]].tolist())
+        assert set(nodes[col[rp[i]:rp[i + 1]]].tolist()) <= nb
+
+
+def test_synthetic_shapes_and_split():
+    g = synthetic("ogbn-arxiv", seed=1, scale=0.01)
+    n, m, F, C, ntr, nva = SHAPES["ogbn-arxiv"]
+    assert g.n_features == F and g.n_classes == C
+    assert int((g.mask == 1).sum()) == int(ntr * 0.01)
+    assert g.y.max() < C
+    r0, r1, per, rp, col = partition_rows(g, 1, 3)
+    assert r0 == per and rp[-1] == col.numel()
+
+
+def test_dropout_mask_is_partition_independent():
+    full = ops.dropout_keep_mask(40, 64, 0.5, (1, 2), 3)
+    part = ops.dropout_keep_mask(20, 64, 0.5, (1, 2), 3, row0=20)
+    assert torch.equal(full[20:], part)
+    assert 0.4 < full.float().mean() < 0.6
+
+
+def test_gcn_cpu_learns():
+    g = synthetic("ogbn-products", seed=0, scale=0.005)
+    tr = GCNTrainer(g, hidden=64)
+    first = None
+    for e in range(25):
+        tr.train_step()
+        if e == 0:
+            first = tr.train_loss()
+    res = tr.evaluate()
+    assert tr.train_loss() < first
+    assert res["val_acc"] > 0.4
+
+
+def test_random_graph_generator(tmp_path):
+    gen = RandomGraphGenerator(num_nodes=15, max_joint_causes=3, number_points=200, seed=3)
+    G, data, cat, cat_idx = gen.generate()
+    assert not G.is_cyclic()
+    assert set(G.get_list_nodes()) == set(data.columns)
+    effects = [c for c in data.columns if G.get_parents(c)]       # roots stay U(-1, 1)
+    np.testing.assert_allclose(data[effects].values.mean(0), 0, atol=1e-9)
+    roots = [c for c in data.columns if not G.get_parents(c)]
+    assert len(roots) >= 2 and np.abs(data[roots].values).max() <= 1
+    gen.save_data(str(tmp_path / "g"))
+    t = pd.read_csv(tmp_path / "g_target.csv")
+    assert list(t.columns) == ["Cause", "Effect"] and len(t) == len(G.get_list_edges())
+    pairs, targets = gen.generate_pairs(4, prefix=str(tmp_path / "p"))
+    df = CCEPC_PairsFileReader(str(tmp_path / "p_pairs.csv"))
+    assert len(df) == 4 and set(targets.Target) <= {1.0, -1.0}
+
+
+def test_mechanism_primitives():
+    rng = np.random.default_rng(0)
+    x = fd.cause(300, rng=rng)
+    assert x.min() >= -1 and x.max() <= 1
+    y = fd.effect(x, 300, 0.7, rng=rng)
+    assert abs(y.mean()) < 1e-9 and abs(y.std() - 1) < 1e-9
+    b = fd.rand_bin(y, rng=rng)
+    assert b.dtype.kind == "i" and len(np.unique(b)) >= 2
