@@ -111,3 +111,22 @@ def test_mechanism_primitives():
     assert abs(y.mean()) < 1e-9 and abs(y.std() - 1) < 1e-9
     b = fd.rand_bin(y, rng=rng)
     assert b.dtype.kind == "i" and len(np.unique(b)) >= 2
+
+
+def test_generators_module():
+    from cgnn_amd.generators import (CGNN_generator, full_graph_polynomial_generator, linear_regressor,
+                                     polynomial_regressor, support_vector_regressor)
+    from cgnn_amd.utils.graph import DirectedGraph
+    rng = np.random.default_rng(0)
+    a = rng.normal(size=150)
+    df = pd.DataFrame({"a": a, "b": a ** 2 + 0.1 * rng.normal(size=150)})
+    g = DirectedGraph()
+    g.add("a", "b")
+    out = full_graph_polynomial_generator(df, g, train_epochs=20, gpu=False)
+    assert out.shape == (150, 2) and np.isfinite(out.values).all()
+    out = CGNN_generator(df, g, train_epochs=10, test_epochs=1, gpu=False)
+    assert out.shape == (150, 2) and np.isfinite(out.values).all()
+    y = polynomial_regressor(df[["a"]].values, df.b.values, ["a"], train_epochs=30)
+    assert y.shape == (150,)
+    assert linear_regressor(df[["a"]].values, df.b.values, ["a"]).shape == (150,)
+    assert support_vector_regressor(df[["a"]].values, df.b.values, ["a"]).shape == (150,)
