@@ -17,16 +17,15 @@ extern "C" {
 int cgnn_mmd_supported_d(int);
 int cgnn_gen_supported_h(int);
 int cgnn_gen_bwd_blocks(int);
-size_t cgnn_gen_bwd_lds(int, int);
+size_t cgnn_gen_bwd_lds(int, int, int);
 int cgnn_launch_mmd(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
                     float, hipStream_t);
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
                               const int*, int, int, hipStream_t);
-int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, const uint32_t*,
-                        const int*, int, int, int, int, int, hipStream_t);
-int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int, int,
-                        float*, const uint32_t*, const int*, int, int, int, int, int, float*,
-                        hipStream_t);
+int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int,
+                        const uint32_t*, const int*, int, int, int, int, int, hipStream_t);
+int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
+                        const float*, int, int, int, int, int, int, float*, hipStream_t);
 int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
                      int, float, float, float, float, int, hipStream_t);
 int cgnn_launch_init(float*, float*, float*, const int*, int, int, const uint32_t*, float, int,
@@ -73,7 +72,7 @@ static void chk(int rc, const char* what) {
 class PyEngine {
  public:
   PyEngine(std::vector<int> icfg, std::vector<float> fcfg, std::vector<uint64_t> ptrs, uint64_t stream) {
-    if (icfg.size() < 13 || fcfg.size() < 5 || ptrs.size() < 18) throw std::invalid_argument("engine config size");
+    if (icfg.size() < 14 || fcfg.size() < 5 || ptrs.size() < 18) throw std::invalid_argument("engine config size");
     std::vector<const void*> p(ptrs.size());
     for (size_t k = 0; k < ptrs.size(); ++k) p[k] = reinterpret_cast<const void*>(ptrs[k]);
     h_ = cgnn_engine_create(icfg.data(), fcfg.data(), p.data(), S(stream));
@@ -109,18 +108,17 @@ PYBIND11_MODULE(_hip, m) {
                                   inv_n2, flags, Pt<float>(hist), hist_stride, Pt<const int>(step), step_off,
                                   R, S(st)), "loss_finalize");
   });
-  m.def("gen_fwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t data, uint64_t xhat, uint64_t keys,
-                      uint64_t step, int off, int N, int D, int H, int R, uint64_t st) {
+  m.def("gen_fwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t data, uint64_t xhat, uint64_t noise,
+                      int NS, uint64_t keys, uint64_t step, int off, int N, int D, int H, int R, uint64_t st) {
     chk(cgnn_launch_gen_fwd(Pt<const int>(prog), ps, Pt<const float>(params), P, Pt<const float>(data),
-                            Pt<float>(xhat), Pt<const uint32_t>(keys), Pt<const int>(step), off, N, D, H, R,
-                            S(st)), "gen_fwd");
+                            Pt<float>(xhat), Pt<float>(noise), NS, Pt<const uint32_t>(keys), Pt<const int>(step),
+                            off, N, D, H, R, S(st)), "gen_fwd");
   });
-  m.def("gen_bwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t xhat, uint64_t gradp, int nch,
-                      int R, uint64_t dxhat, uint64_t keys, uint64_t step, int off, int N, int D, int H,
-                      int max_in, uint64_t gpart, uint64_t st) {
+  m.def("gen_bwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t xhat, uint64_t noise, int NS,
+                      uint64_t gradp, int nch, int R, int N, int D, int H, int max_in, uint64_t gpart, uint64_t st) {
     chk(cgnn_launch_gen_bwd(Pt<const int>(prog), ps, Pt<const float>(params), P, Pt<const float>(xhat),
-                            Pt<const float>(gradp), nch, R, Pt<float>(dxhat), Pt<const uint32_t>(keys),
-                            Pt<const int>(step), off, N, D, H, max_in, Pt<float>(gpart), S(st)), "gen_bwd");
+                            Pt<const float>(noise), NS, Pt<const float>(gradp), nch, R, N, D, H, max_in,
+                            Pt<float>(gpart), S(st)), "gen_bwd");
   });
   m.def("adam", [](uint64_t params, uint64_t mm, uint64_t vv, uint64_t gpart, int G, uint64_t prog, int ps, int P,
                    uint64_t step, int off, float lr, float b1, float b2, float eps, int R, uint64_t st) {

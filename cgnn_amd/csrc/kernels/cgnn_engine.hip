@@ -22,11 +22,10 @@ int cgnn_launch_mmd(int, int, const float*, const float*, float*, float*, int, i
                     float, hipStream_t);
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
                               const int*, int, int, hipStream_t);
-int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, const uint32_t*,
-                        const int*, int, int, int, int, int, hipStream_t);
-int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int, int,
-                        float*, const uint32_t*, const int*, int, int, int, int, int, float*,
-                        hipStream_t);
+int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int,
+                        const uint32_t*, const int*, int, int, int, int, int, hipStream_t);
+int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
+                        const float*, int, int, int, int, int, int, float*, hipStream_t);
 int cgnn_gen_bwd_blocks(int);
 int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
                      int, float, float, float, float, int, hipStream_t);
@@ -47,6 +46,7 @@ struct EngineConfig {
   int hist_stride = 0;
   int rff_k = 0;     // > 0: random-Fourier-feature MMD with k features per bandwidth
   int d_true = 0;    // unpadded variable count (RFF draws must not depend on padding)
+  int NS = 0;        // noise streams per model = D + max #confounder streams
 };
 
 struct EngineBuffers {
@@ -56,7 +56,7 @@ struct EngineBuffers {
   float* v = nullptr;
   const float* data = nullptr;
   float* xhat = nullptr;
-  float* dxhat = nullptr;
+  float* noise = nullptr;    // [R][NS][N] noise draws of the forward, reused by the backward
   float* gradp = nullptr;   // [n_chunks][R][D][N]
   float* lpart = nullptr;   // [R][n_chunks*row_tiles]
   float* gpart = nullptr;   // [R][G][P]
@@ -129,23 +129,22 @@ class Engine {
 
   void enqueue_train_step(int off, bool record_hist) {
     const float inv = loss_scale();
-    check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.keys, b_.step,
-                              off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
+    check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
+                              b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
     enqueue_loss(off, true);
     check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 0,
                                     record_hist ? b_.loss_hist : nullptr, c_.hist_stride, b_.step, off,
                                     c_.R, st_), "finalize");
-    check(cgnn_launch_gen_bwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.xhat, b_.gradp, grad_chunks(),
-                              c_.R, b_.dxhat, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.max_in,
-                              b_.gpart, st_), "gen_bwd");
+    check(cgnn_launch_gen_bwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.xhat, b_.noise, c_.NS, b_.gradp,
+                              grad_chunks(), c_.R, c_.N, c_.D, c_.H, c_.max_in, b_.gpart, st_), "gen_bwd");
     check(cgnn_launch_adam(b_.params, b_.m, b_.v, b_.gpart, G_, b_.prog, c_.prog_stride, c_.P, b_.step,
                            off, c_.lr, c_.beta1, c_.beta2, c_.eps, c_.R, st_), "adam");
   }
 
   void enqueue_eval_step(int off) {
     const float inv = loss_scale();
-    check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.keys, b_.step,
-                              off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
+    check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
+                              b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
     enqueue_loss(off, false);
     check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 1,
                                     nullptr, 0, b_.step, off, c_.R, st_), "finalize(eval)");
@@ -211,12 +210,12 @@ extern "C" void* cgnn_engine_create(const int* icfg, const float* fcfg, const vo
   cgnn::EngineConfig c;
   c.R = icfg[0]; c.N = icfg[1]; c.D = icfg[2]; c.H = icfg[3]; c.P = icfg[4];
   c.prog_stride = icfg[5]; c.max_in = icfg[6]; c.row_tiles = icfg[7]; c.n_chunks = icfg[8];
-  c.tpc = icfg[9]; c.hist_stride = icfg[10]; c.rff_k = icfg[11]; c.d_true = icfg[12];
+  c.tpc = icfg[9]; c.hist_stride = icfg[10]; c.rff_k = icfg[11]; c.d_true = icfg[12]; c.NS = icfg[13];
   c.lr = fcfg[0]; c.beta1 = fcfg[1]; c.beta2 = fcfg[2]; c.eps = fcfg[3]; c.init_std = fcfg[4];
   cgnn::EngineBuffers b;
   b.prog = (const int*)ptrs[0]; b.params = (float*)ptrs[1]; b.m = (float*)ptrs[2];
   b.v = (float*)ptrs[3]; b.data = (const float*)ptrs[4]; b.xhat = (float*)ptrs[5];
-  b.dxhat = (float*)ptrs[6]; b.gradp = (float*)ptrs[7]; b.lpart = (float*)ptrs[8];
+  b.noise = (float*)ptrs[6]; b.gradp = (float*)ptrs[7]; b.lpart = (float*)ptrs[8];
   b.gpart = (float*)ptrs[9]; b.tt = (float*)ptrs[10]; b.loss_last = (float*)ptrs[11];
   b.loss_acc = (float*)ptrs[12]; b.loss_hist = (float*)ptrs[13]; b.step = (int*)ptrs[14];
   b.keys = (const uint32_t*)ptrs[15]; b.rff_w = (float*)ptrs[16]; b.rff_diff = (float*)ptrs[17];

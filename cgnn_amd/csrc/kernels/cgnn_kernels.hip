@@ -33,23 +33,6 @@ constexpr int KIND_GEN = 0;
 constexpr int KIND_OBS = 1;
 constexpr float MMD_SENTINEL = 1.0e17f;   // padded columns: exp(-g*d2) == 0 exactly
 
-// Seven bandwidths of Loss.py:10: {0.005, 0.05, 0.25, 0.5, 1, 5, 50}.
-// exp(-0.5 d2) and exp(-d2) are squares of exp(-0.25 d2); the others are one
-// v_exp_f32 each (a square costs 4 issue cycles, an exp 8 + its pre-scale 4,
-// so powering further would cost more than it saves and lose accuracy).
-__device__ __forceinline__ void rbf7(float d2, float& ks, float& w) {
-  const float L2E = 1.4426950408889634f;
-  float e1 = __builtin_amdgcn_exp2f(d2 * (-0.005f * L2E));
-  float e2 = __builtin_amdgcn_exp2f(d2 * (-0.05f * L2E));
-  float e3 = __builtin_amdgcn_exp2f(d2 * (-0.25f * L2E));
-  float e4 = e3 * e3;
-  float e5 = e4 * e4;
-  float e6 = __builtin_amdgcn_exp2f(d2 * (-5.0f * L2E));
-  float e7 = __builtin_amdgcn_exp2f(d2 * (-50.0f * L2E));
-  ks = ((e1 + e2) + (e3 + e4)) + ((e5 + e6) + e7);
-  w = ((0.005f * e1 + 0.05f * e2) + (0.25f * e3 + 0.5f * e4)) + ((e5 + 5.0f * e6) + 50.0f * e7);
-}
-
 }  // namespace
 
 // ============================================================================
@@ -59,18 +42,43 @@ __device__ __forceinline__ void rbf7(float d2, float& ks, float& w) {
 //   MODE 2: const  -> true-true block (rows and columns from `data`)
 // Each thread owns one row i of the generated block and streams 256-column
 // tiles of the joint [pred; true] column space through LDS (broadcast reads).
-// Per pair: 3D flops for distance + gradient, 5 exp + 2 squares for the kernel.
+// Columns are consumed in PAIRS with packed fp32 math (v_pk_add/mul/fma_f32 do
+// two lanes' worth of work per issue): the LDS tile is laid out
+// [T/2][D][2] so that one ds_read_b64 returns (x_j[k], x_{j+1}[k]) ready packed.
+// Per column pair: 3D packed ops for distance + gradient, 10 v_exp_f32 and
+// ~20 packed ops for the seven kernel values and their weights.
 //   grad_i += sign * w_ij * (x_j - p_i),  sign = +1 (pred col), -1 (true col)
 //   loss   += (+1 | -2) * sum_gamma exp(-gamma d2)
 // dL/dp_i = 4/N^2 * grad_i  (derivation in docs/KERNELS.md).
 // ============================================================================
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 exp2_2(f2 x) {
+  return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+}
+
+// seven bandwidths for two distances at once; returns ks (kernel sum) and w
+// (sum gamma * kernel) as packed pairs.
+__device__ __forceinline__ void rbf7x2(f2 d2, f2& ks, f2& w) {
+  const float L2E = 1.4426950408889634f;
+  const f2 e1 = exp2_2(d2 * (-0.005f * L2E));
+  const f2 e2 = exp2_2(d2 * (-0.05f * L2E));
+  const f2 e3 = exp2_2(d2 * (-0.25f * L2E));
+  const f2 e4 = e3 * e3;
+  const f2 e5 = e4 * e4;
+  const f2 e6 = exp2_2(d2 * (-5.0f * L2E));
+  const f2 e7 = exp2_2(d2 * (-50.0f * L2E));
+  ks = ((e1 + e2) + (e3 + e4)) + ((e5 + e6) + e7);
+  w = ((0.005f * e1 + 0.05f * e2) + (0.25f * e3 + 0.5f * e4)) + ((e5 + 5.0f * e6) + 50.0f * e7);
+}
+
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void mmd_rbf_kernel(
     const float* __restrict__ xhat, const float* __restrict__ data,
     float* __restrict__ grad_part, float* __restrict__ loss_part,
     int N, int R, int tiles_per_chunk, float grad_scale) {
   constexpr int T = 256;
-  __shared__ __attribute__((aligned(16))) float s_x[T * D];
+  __shared__ __attribute__((aligned(16))) float s_x[T * D];   // [T/2][D][2]
   __shared__ float s_red[4];
 
   const int rt = blockIdx.x, chunk = blockIdx.y, r = blockIdx.z;
@@ -82,11 +90,12 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
   const float* P = (MODE == 2 ? data : xhat) + mbase;
   const float* Tm = data + mbase;
 
-  float p[D], g[D];
+  f2 p[D], g[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
-    p[k] = valid ? P[(size_t)k * N + i] : 0.f;
-    g[k] = 0.f;
+    const float pk = valid ? P[(size_t)k * N + i] : 0.f;
+    p[k] = f2{pk, pk};
+    g[k] = f2{0.f, 0.f};
   }
   float lacc = 0.f;
 
@@ -94,6 +103,7 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
   const int n_tiles = (MODE == 2) ? ct : 2 * ct;
   const int tile_lo = chunk * tiles_per_chunk;
   const int tile_hi = min(n_tiles, tile_lo + tiles_per_chunk);
+  float* my = s_x + ((t >> 1) * D) * 2 + (t & 1);
 
   for (int tile = tile_lo; tile < tile_hi; ++tile) {
     const bool is_pred = (MODE != 2) && tile < ct;
@@ -101,37 +111,33 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
     const int col0 = (is_pred || MODE == 2 ? tile : tile - ct) * T;
     const int c = col0 + t;
     __syncthreads();
-    if (c < N) {
 #pragma unroll
-      for (int k = 0; k < D; ++k) s_x[t * D + k] = src[(size_t)k * N + c];
-    } else {
-#pragma unroll
-      for (int k = 0; k < D; ++k) s_x[t * D + k] = MMD_SENTINEL;
-    }
+    for (int k = 0; k < D; ++k) my[2 * k] = (c < N) ? src[(size_t)k * N + c] : MMD_SENTINEL;
     __syncthreads();
     const float lsign = (MODE == 2 || is_pred) ? 1.f : -2.f;
     const float gsign = is_pred ? 1.f : -1.f;
-    float tl = 0.f;
+    f2 tl = {0.f, 0.f};
+    const f2* xp = reinterpret_cast<const f2*>(s_x);
 #pragma unroll 2
-    for (int jj = 0; jj < T; ++jj) {
-      const float* xj = s_x + jj * D;
-      float diff[D];
-      float d2 = 0.f;
+    for (int jj = 0; jj < T / 2; ++jj) {
+      const f2* xj = xp + jj * D;
+      f2 diff[D];
+      f2 d2 = {0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         diff[k] = xj[k] - p[k];
-        d2 = fmaf(diff[k], diff[k], d2);
+        d2 = diff[k] * diff[k] + d2;
       }
-      float ks, w;
-      rbf7(d2, ks, w);
+      f2 ks, w;
+      rbf7x2(d2, ks, w);
       tl += ks;
       if (MODE == 0) {
-        const float sw = gsign * w;
+        const f2 sw = gsign * w;
 #pragma unroll
-        for (int k = 0; k < D; ++k) g[k] = fmaf(sw, diff[k], g[k]);
+        for (int k = 0; k < D; ++k) g[k] = sw * diff[k] + g[k];
       }
     }
-    lacc = fmaf(lsign, tl, lacc);
+    lacc = fmaf(lsign, tl.x + tl.y, lacc);
   }
 
   // deterministic block reduction of the loss partial
@@ -146,7 +152,7 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
   if (MODE == 0 && valid) {
     float* gp = grad_part + ((size_t)chunk * R + r) * D * N;
 #pragma unroll
-    for (int k = 0; k < D; ++k) gp[(size_t)k * N + i] = g[k] * grad_scale;
+    for (int k = 0; k < D; ++k) gp[(size_t)k * N + i] = (g[k].x + g[k].y) * grad_scale;
   }
 }
 
@@ -183,31 +189,38 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(
 
 // ============================================================================
 // K1: generator forward.  grid = (ceil(N/256), R), one thread per sample.
-// Weights are read with wave-uniform addresses (scalar loads / broadcast).
+// The sample's generated values live in LDS (s_x[var][thread]) for the whole DAG
+// sweep, so reading a parent is an LDS access instead of a dependent global
+// round trip; the draws of every noise stream are written to `noise`
+// ([R][NS][N], NS = D + #confounder streams) for the backward.  Weights are read
+// with wave-uniform addresses (scalar loads).
 // ============================================================================
 template <int H>
 __global__ __launch_bounds__(256) void gen_fwd_kernel(
     const int* __restrict__ prog, int prog_stride, const float* __restrict__ params, int P,
-    const float* __restrict__ data, float* __restrict__ xhat,
+    const float* __restrict__ data, float* __restrict__ xhat, float* __restrict__ noise, int NS,
     const uint32_t* __restrict__ keys, const int* __restrict__ step_base, int step_off,
     int N, int D, int Hrt) {
+  extern __shared__ __attribute__((aligned(16))) float s_x[];   // [D][blockDim]
   const int r = blockIdx.y;
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+  const int t = threadIdx.x, B = blockDim.x;
+  const int n = blockIdx.x * B + t;
+  const bool valid = n < N;
+  const int nc = valid ? n : 0;
   const int* pr = prog + (size_t)r * prog_stride;
   const int nn = pr[0];
   const uint32_t step = (uint32_t)(step_base[0] + step_off);
   const uint32_t k0 = keys[2 * r], k1 = keys[2 * r + 1];
   const float* th = params + (size_t)r * P;
-  float* xr = xhat + (size_t)r * D * N;
   const float* dr = data + (size_t)r * D * N;
+  float* nz = noise + (size_t)r * NS * N;
   const int Hh = (H > 0) ? H : Hrt;
 
   for (int kk = 0; kk < nn; ++kk) {
     const int* nd = pr + PROG_HDR + kk * NODE_REC;
     const int var = nd[0];
     if (nd[1] == KIND_OBS) {
-      xr[(size_t)var * N + n] = dr[(size_t)var * N + n];
+      s_x[var * B + t] = dr[(size_t)var * N + nc];
       continue;
     }
     const int npar = nd[2], paroff = nd[3], ncf = nd[4], cfoff = nd[5], poff = nd[6];
@@ -216,72 +229,83 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
     const float* b1 = W1 + (size_t)nin * Hh;
     const float* W2 = b1 + Hh;
     const float b2 = W2[Hh];
-    float pre[H > 0 ? H : 1];
+    const float e = rng_normal(k0, k1, (uint32_t)n, (uint32_t)var, step, RNG_NODE_NOISE);
+    if (valid) nz[(size_t)var * N + n] = e;
     if (H > 0) {
+      float pre[H > 0 ? H : 1];
 #pragma unroll
-      for (int q = 0; q < H; ++q) pre[q] = b1[q];
+      for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[npar * H + q], e, b1[q]);
       for (int j = 0; j < npar; ++j) {
-        const float x = xr[(size_t)pr[paroff + j] * N + n];
+        const float x = s_x[pr[paroff + j] * B + t];
 #pragma unroll
         for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[j * H + q], x, pre[q]);
       }
-      {
-        const float e = rng_normal(k0, k1, (uint32_t)n, (uint32_t)var, step, RNG_NODE_NOISE);
-#pragma unroll
-        for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[npar * H + q], e, pre[q]);
-      }
       for (int c = 0; c < ncf; ++c) {
-        const float e = rng_normal(k0, k1, (uint32_t)n, (uint32_t)pr[cfoff + c], step, RNG_CONF_NOISE);
+        const int cid = pr[cfoff + c];
+        const float ec = rng_normal(k0, k1, (uint32_t)n, (uint32_t)cid, step, RNG_CONF_NOISE);
+        if (valid) nz[(size_t)(D + cid) * N + n] = ec;
 #pragma unroll
-        for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[(npar + 1 + c) * H + q], e, pre[q]);
+        for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[(npar + 1 + c) * H + q], ec, pre[q]);
       }
       float out = b2;
 #pragma unroll
       for (int q = 0; q < H; ++q) out = fmaf(W2[q], fmaxf(pre[q], 0.f), out);
-      xr[(size_t)var * N + n] = out;
+      s_x[var * B + t] = out;
     } else {
       // generic hidden width: hidden unit outer loop (no register array)
       float out = b2;
-      const float e0 = rng_normal(k0, k1, (uint32_t)n, (uint32_t)var, step, RNG_NODE_NOISE);
+      for (int c = 0; c < ncf; ++c) {
+        const int cid = pr[cfoff + c];
+        if (valid)
+          nz[(size_t)(D + cid) * N + n] = rng_normal(k0, k1, (uint32_t)n, (uint32_t)cid, step, RNG_CONF_NOISE);
+      }
       for (int q = 0; q < Hh; ++q) {
-        float a = b1[q];
-        for (int j = 0; j < npar; ++j) a = fmaf(W1[j * Hh + q], xr[(size_t)pr[paroff + j] * N + n], a);
-        a = fmaf(W1[npar * Hh + q], e0, a);
+        float a = fmaf(W1[npar * Hh + q], e, b1[q]);
+        for (int j = 0; j < npar; ++j) a = fmaf(W1[j * Hh + q], s_x[pr[paroff + j] * B + t], a);
         for (int c = 0; c < ncf; ++c)
           a = fmaf(W1[(npar + 1 + c) * Hh + q],
                    rng_normal(k0, k1, (uint32_t)n, (uint32_t)pr[cfoff + c], step, RNG_CONF_NOISE), a);
         out = fmaf(W2[q], fmaxf(a, 0.f), out);
       }
-      xr[(size_t)var * N + n] = out;
+      s_x[var * B + t] = out;
+    }
+  }
+  if (valid) {
+    float* xr = xhat + (size_t)r * D * N;
+    for (int kk = 0; kk < nn; ++kk) {
+      const int var = pr[PROG_HDR + kk * NODE_REC];
+      xr[(size_t)var * N + n] = s_x[var * B + t];
     }
   }
 }
 
 // ============================================================================
 // K2: generator backward.  grid = (G, R), block = BS samples (one per thread).
+// The sample's generated values and running gradients live in LDS
+// (s_x / s_dx [D][BS]); the noise draws come from the forward's `noise` buffer.
 // Per node (reverse topological order):
-//   1. each thread recomputes inputs (parents from xhat, noise from Philox),
-//      the pre-activation and dh_q = g * W2_q * [pre_q > 0]; pushes
-//      dL/dparent = W1 dh into dxhat of the parents (own sample -> no race);
-//   2. the block reduces the per-sample outer products over its BS samples
-//      from LDS in a fixed order and writes one partial slab
-//      gpart[r][blk][param] -- no atomics, bitwise reproducible.
-// LDS: s_in [BS][MI+1] (inputs + bias column), s_dh/s_relu [BS][H+1], s_g [BS].
+//   1. each thread rebuilds the node inputs, the pre-activation and
+//      dh_q = g * W2_q * [pre_q > 0]; pushes dL/dparent = W1 dh into s_dx;
+//   2. the block reduces the per-sample outer products over its BS samples from
+//      LDS in a fixed order (4 independent partial sums per parameter) and writes
+//      one partial slab gpart[r][blk][param] -- no atomics, bitwise reproducible.
+// LDS: s_in [BS][MI+2], s_dh/s_relu [BS][H+1], s_g [BS], s_x/s_dx [D][BS].
 // ============================================================================
 template <int H, int BS>
 __global__ __launch_bounds__(BS) void gen_bwd_kernel(
     const int* __restrict__ prog, int prog_stride, const float* __restrict__ params, int P,
-    const float* __restrict__ xhat, const float* __restrict__ grad_part, int n_chunks, int R,
-    float* __restrict__ dxhat, const uint32_t* __restrict__ keys,
-    const int* __restrict__ step_base, int step_off, int N, int D, int max_in,
-    float* __restrict__ gpart) {
+    const float* __restrict__ xhat, const float* __restrict__ noise, int NS,
+    const float* __restrict__ grad_part, int n_chunks, int R,
+    int N, int D, int max_in, float* __restrict__ gpart) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int SI = max_in + 2;        // odd-ish stride -> conflict-free row access
+  const int SI = max_in + 2;
   const int SH = H + 1;
   float* s_in = smem;
   float* s_dh = s_in + BS * SI;
   float* s_relu = s_dh + BS * SH;
   float* s_g = s_relu + BS * SH;
+  float* s_x = s_g + BS;
+  float* s_dx = s_x + BS * D;
 
   const int r = blockIdx.y, blk = blockIdx.x, G = gridDim.x;
   const int t = threadIdx.x;
@@ -289,20 +313,20 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
   const bool valid = n < N;
   const int* pr = prog + (size_t)r * prog_stride;
   const int nn = pr[0];
-  const uint32_t step = (uint32_t)(step_base[0] + step_off);
-  const uint32_t k0 = keys[2 * r], k1 = keys[2 * r + 1];
   const float* th = params + (size_t)r * P;
   const float* xr = xhat + (size_t)r * D * N;
-  float* dx = dxhat + (size_t)r * D * N;
+  const float* nz = noise + (size_t)r * NS * N;
   float* gp = gpart + ((size_t)r * G + blk) * P;
 
-  // dL/dxhat from the MMD kernel: fixed-order sum over column chunks
-  if (valid) {
-    for (int v = 0; v < D; ++v) {
-      float s = 0.f;
+  // sample state into LDS; dL/dxhat = fixed-order sum of the MMD column chunks
+  for (int v = 0; v < D; ++v) {
+    float s = 0.f, x = 0.f;
+    if (valid) {
+      x = xr[(size_t)v * N + n];
       for (int c = 0; c < n_chunks; ++c) s += grad_part[(((size_t)c * R + r) * D + v) * N + n];
-      dx[(size_t)v * N + n] = s;
     }
+    s_x[v * BS + t] = x;
+    s_dx[v * BS + t] = s;
   }
 
   for (int kk = nn - 1; kk >= 0; --kk) {
@@ -320,20 +344,15 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
     for (int q = 0; q < H; ++q) pre[q] = b1[q];
     for (int j = 0; j < nin; ++j) {
       float x;
-      if (j < npar) {
-        x = valid ? xr[(size_t)pr[paroff + j] * N + n] : 0.f;
-      } else if (j == npar) {
-        x = rng_normal(k0, k1, (uint32_t)n, (uint32_t)var, step, RNG_NODE_NOISE);
-      } else {
-        x = rng_normal(k0, k1, (uint32_t)n, (uint32_t)pr[cfoff + (j - npar - 1)], step, RNG_CONF_NOISE);
-      }
-      if (!valid) x = 0.f;
+      if (j < npar) x = s_x[pr[paroff + j] * BS + t];
+      else if (j == npar) x = valid ? nz[(size_t)var * N + n] : 0.f;
+      else x = valid ? nz[(size_t)(D + pr[cfoff + (j - npar - 1)]) * N + n] : 0.f;
       my_in[j] = x;
 #pragma unroll
       for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[j * H + q], x, pre[q]);
     }
     my_in[nin] = valid ? 1.f : 0.f;   // bias column
-    const float gout = valid ? dx[(size_t)var * N + n] : 0.f;
+    const float gout = s_dx[var * BS + t];
     float dh[H];
 #pragma unroll
     for (int q = 0; q < H; ++q) {
@@ -343,29 +362,42 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
       s_relu[t * SH + q] = on ? pre[q] : 0.f;
     }
     s_g[t] = gout;
-    if (valid) {
-      for (int j = 0; j < npar; ++j) {
-        float s = 0.f;
+    for (int j = 0; j < npar; ++j) {
+      float s = 0.f;
 #pragma unroll
-        for (int q = 0; q < H; ++q) s = fmaf(W1[j * H + q], dh[q], s);
-        dx[(size_t)pr[paroff + j] * N + n] += s;
-      }
+      for (int q = 0; q < H; ++q) s = fmaf(W1[j * H + q], dh[q], s);
+      s_dx[pr[paroff + j] * BS + t] += s;
     }
     __syncthreads();
     const int n_w1b1 = (nin + 1) * H;
     const int np = n_w1b1 + H + 1;
     for (int pidx = t; pidx < np; pidx += BS) {
-      float acc = 0.f;
+      const float* a;
+      const float* b;
+      int sa, sb;
       if (pidx < n_w1b1) {
-        const int j = pidx / H, q = pidx - (pidx / H) * H;
-        for (int s = 0; s < BS; ++s) acc = fmaf(s_in[s * SI + j], s_dh[s * SH + q], acc);
+        const int j = pidx / H, q = pidx - j * H;
+        a = s_in + j; sa = SI; b = s_dh + q; sb = SH;
       } else if (pidx < n_w1b1 + H) {
-        const int q = pidx - n_w1b1;
-        for (int s = 0; s < BS; ++s) acc = fmaf(s_relu[s * SH + q], s_g[s], acc);
+        a = s_relu + (pidx - n_w1b1); sa = SH; b = s_g; sb = 1;
       } else {
-        for (int s = 0; s < BS; ++s) acc += s_g[s];
+        a = s_g; sa = 1; b = nullptr; sb = 0;
       }
-      gp[poff + pidx] = acc;
+      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+      if (b) {
+#pragma unroll 4
+        for (int s4 = 0; s4 < BS; s4 += 4) {
+          acc0 = fmaf(a[(s4 + 0) * sa], b[(s4 + 0) * sb], acc0);
+          acc1 = fmaf(a[(s4 + 1) * sa], b[(s4 + 1) * sb], acc1);
+          acc2 = fmaf(a[(s4 + 2) * sa], b[(s4 + 2) * sb], acc2);
+          acc3 = fmaf(a[(s4 + 3) * sa], b[(s4 + 3) * sb], acc3);
+        }
+      } else {
+        for (int s4 = 0; s4 < BS; s4 += 4) {
+          acc0 += a[s4]; acc1 += a[s4 + 1]; acc2 += a[s4 + 2]; acc3 += a[s4 + 3];
+        }
+      }
+      gp[poff + pidx] = (acc0 + acc1) + (acc2 + acc3);
     }
     __syncthreads();
   }
@@ -476,17 +508,18 @@ extern "C" int cgnn_gen_supported_h(int H) {
 }
 
 extern "C" int cgnn_launch_gen_fwd(const int* prog, int prog_stride, const float* params, int P,
-                                   const float* data, float* xhat, const uint32_t* keys,
-                                   const int* step_base, int step_off, int N, int D, int H, int R,
-                                   hipStream_t st) {
+                                   const float* data, float* xhat, float* noise, int NS,
+                                   const uint32_t* keys, const int* step_base, int step_off, int N,
+                                   int D, int H, int R, hipStream_t st) {
   dim3 grid((N + 255) / 256, R), block(256);
+  const size_t lds = sizeof(float) * (size_t)D * 256;
   switch (H) {
-#define CASE_H(h) case h: hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, 0, st, prog, prog_stride, params, P, data, xhat, keys, step_base, step_off, N, D, H); break;
+#define CASE_H(h) case h: hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, lds, st, prog, prog_stride, params, P, data, xhat, noise, NS, keys, step_base, step_off, N, D, H); break;
     CGNN_H_LIST(CASE_H)
 #undef CASE_H
     default:
-      hipLaunchKernelGGL((gen_fwd_kernel<0>), grid, block, 0, st, prog, prog_stride, params, P, data,
-                         xhat, keys, step_base, step_off, N, D, H);
+      hipLaunchKernelGGL((gen_fwd_kernel<0>), grid, block, lds, st, prog, prog_stride, params, P, data,
+                         xhat, noise, NS, keys, step_base, step_off, N, D, H);
   }
   return (int)hipGetLastError();
 }
@@ -495,21 +528,21 @@ constexpr int GEN_BWD_BS = 128;
 
 extern "C" int cgnn_gen_bwd_blocks(int N) { return (N + GEN_BWD_BS - 1) / GEN_BWD_BS; }
 
-extern "C" size_t cgnn_gen_bwd_lds(int H, int max_in) {
-  return sizeof(float) * ((size_t)GEN_BWD_BS * (max_in + 2) + 2 * (size_t)GEN_BWD_BS * (H + 1) + GEN_BWD_BS);
+extern "C" size_t cgnn_gen_bwd_lds(int H, int max_in, int D) {
+  return sizeof(float) * ((size_t)GEN_BWD_BS * (max_in + 2) + 2 * (size_t)GEN_BWD_BS * (H + 1) + GEN_BWD_BS +
+                          2 * (size_t)GEN_BWD_BS * D);
 }
 
 extern "C" int cgnn_launch_gen_bwd(const int* prog, int prog_stride, const float* params, int P,
-                                   const float* xhat, const float* gradp, int n_chunks, int R,
-                                   float* dxhat, const uint32_t* keys, const int* step_base,
-                                   int step_off, int N, int D, int H, int max_in, float* gpart,
+                                   const float* xhat, const float* noise, int NS, const float* gradp,
+                                   int n_chunks, int R, int N, int D, int H, int max_in, float* gpart,
                                    hipStream_t st) {
   const int G = cgnn_gen_bwd_blocks(N);
   dim3 grid(G, R), block(GEN_BWD_BS);
-  const size_t lds = cgnn_gen_bwd_lds(H, max_in);
+  const size_t lds = cgnn_gen_bwd_lds(H, max_in, D);
   if (lds > 160 * 1024) return -2;
   switch (H) {
-#define CASE_H(h) case h: hipLaunchKernelGGL((gen_bwd_kernel<h, GEN_BWD_BS>), grid, block, lds, st, prog, prog_stride, params, P, xhat, gradp, n_chunks, R, dxhat, keys, step_base, step_off, N, D, max_in, gpart); break;
+#define CASE_H(h) case h: hipLaunchKernelGGL((gen_bwd_kernel<h, GEN_BWD_BS>), grid, block, lds, st, prog, prog_stride, params, P, xhat, noise, NS, gradp, n_chunks, R, N, D, max_in, gpart); break;
     CGNN_H_LIST(CASE_H)
 #undef CASE_H
     default: return -1;

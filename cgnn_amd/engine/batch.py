@@ -78,7 +78,9 @@ class DeviceTrainer:
             self.m = torch.zeros(R, P, **f32)
             self.v = torch.zeros(R, P, **f32)
             self.xhat = torch.zeros(R, D, N, **f32)
-            self.dxhat = torch.zeros(R, D, N, **f32)
+            # forward noise draws, reused by the backward: [R][D + confounder streams][N]
+            self.NS = D + max(int(p.n_conf) for p in programs)
+            self.noise = torch.zeros(R, self.NS, N, **f32)
             row_tiles, n_chunks, tpc = mmd_geometry(N, R)
             self.geometry = (row_tiles, n_chunks, tpc)
             self.rff_k = int(nb_vectors) if use_fast_mmd else 0
@@ -101,10 +103,10 @@ class DeviceTrainer:
             self.stream = torch.cuda.Stream(dev)
             stream = self.stream
             icfg = [R, N, D, self.H, P, stride, max_in, row_tiles, n_chunks, tpc, self.hist_len,
-                    self.rff_k, d]
+                    self.rff_k, d, self.NS]
             fcfg = [float(learning_rate), 0.9, 0.999, 1e-8, float(init_std)]
             ptrs = [t.data_ptr() for t in (self.prog, self.params, self.m, self.v, self.data,
-                                           self.xhat, self.dxhat, self.gradp, self.lpart, self.gpart,
+                                           self.xhat, self.noise, self.gradp, self.lpart, self.gpart,
                                            self.tt, self.loss_last, self.loss_acc)]
             ptrs.append(self.hist.data_ptr() if self.hist_len else 0)
             ptrs += [self.step.data_ptr(), self.keys.data_ptr(), self.rff_w.data_ptr(),
