@@ -17,7 +17,7 @@ extern "C" {
 int cgnn_mmd_supported_d(int);
 int cgnn_gen_supported_h(int);
 int cgnn_gen_bwd_blocks(int);
-size_t cgnn_gen_bwd_lds(int, int, int);
+size_t cgnn_gen_bwd_lds(int, int, int, int);
 int cgnn_launch_mmd(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
                     float, hipStream_t);
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,

@@ -187,13 +187,16 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(
   }
 }
 
+// wave-uniform read of an LDS-resident program word (lands in an SGPR)
+__device__ __forceinline__ int uni(const int* p) { return __builtin_amdgcn_readfirstlane(*p); }
+
 // ============================================================================
 // K1: generator forward.  grid = (ceil(N/256), R), one thread per sample.
-// The sample's generated values live in LDS (s_x[var][thread]) for the whole DAG
-// sweep, so reading a parent is an LDS access instead of a dependent global
-// round trip; the draws of every noise stream are written to `noise`
-// ([R][NS][N], NS = D + #confounder streams) for the backward.  Weights are read
-// with wave-uniform addresses (scalar loads).
+// The model's DAG program is staged in LDS once, and the sample's generated
+// values live in LDS (s_x[var][thread]) for the whole sweep, so a parent read is
+// an LDS access rather than a dependent global round trip.  The draws of every
+// noise stream are written to `noise` ([R][NS][N], NS = D + #confounder
+// streams) for the backward.  Weights are read with wave-uniform (scalar) loads.
 // ============================================================================
 template <int H>
 __global__ __launch_bounds__(256) void gen_fwd_kernel(
@@ -201,14 +204,17 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
     const float* __restrict__ data, float* __restrict__ xhat, float* __restrict__ noise, int NS,
     const uint32_t* __restrict__ keys, const int* __restrict__ step_base, int step_off,
     int N, int D, int Hrt) {
-  extern __shared__ __attribute__((aligned(16))) float s_x[];   // [D][blockDim]
+  extern __shared__ __attribute__((aligned(16))) float s_x[];   // [D][blockDim], then program
   const int r = blockIdx.y;
   const int t = threadIdx.x, B = blockDim.x;
   const int n = blockIdx.x * B + t;
   const bool valid = n < N;
   const int nc = valid ? n : 0;
-  const int* pr = prog + (size_t)r * prog_stride;
-  const int nn = pr[0];
+  int* s_prog = reinterpret_cast<int*>(s_x + (size_t)D * B);
+  const int* pg = prog + (size_t)r * prog_stride;
+  for (int i = t; i < prog_stride; i += B) s_prog[i] = pg[i];
+  __syncthreads();
+  const int nn = uni(s_prog);
   const uint32_t step = (uint32_t)(step_base[0] + step_off);
   const uint32_t k0 = keys[2 * r], k1 = keys[2 * r + 1];
   const float* th = params + (size_t)r * P;
@@ -217,13 +223,14 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
   const int Hh = (H > 0) ? H : Hrt;
 
   for (int kk = 0; kk < nn; ++kk) {
-    const int* nd = pr + PROG_HDR + kk * NODE_REC;
-    const int var = nd[0];
-    if (nd[1] == KIND_OBS) {
+    const int* nd = s_prog + PROG_HDR + kk * NODE_REC;
+    const int var = uni(nd);
+    if (uni(nd + 1) == KIND_OBS) {
       s_x[var * B + t] = dr[(size_t)var * N + nc];
       continue;
     }
-    const int npar = nd[2], paroff = nd[3], ncf = nd[4], cfoff = nd[5], poff = nd[6];
+    const int npar = uni(nd + 2), paroff = uni(nd + 3), ncf = uni(nd + 4), cfoff = uni(nd + 5);
+    const int poff = uni(nd + 6);
     const int nin = npar + 1 + ncf;
     const float* W1 = th + poff;
     const float* b1 = W1 + (size_t)nin * Hh;
@@ -236,12 +243,12 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
 #pragma unroll
       for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[npar * H + q], e, b1[q]);
       for (int j = 0; j < npar; ++j) {
-        const float x = s_x[pr[paroff + j] * B + t];
+        const float x = s_x[uni(s_prog + paroff + j) * B + t];
 #pragma unroll
         for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[j * H + q], x, pre[q]);
       }
       for (int c = 0; c < ncf; ++c) {
-        const int cid = pr[cfoff + c];
+        const int cid = uni(s_prog + cfoff + c);
         const float ec = rng_normal(k0, k1, (uint32_t)n, (uint32_t)cid, step, RNG_CONF_NOISE);
         if (valid) nz[(size_t)(D + cid) * N + n] = ec;
 #pragma unroll
@@ -255,16 +262,16 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
       // generic hidden width: hidden unit outer loop (no register array)
       float out = b2;
       for (int c = 0; c < ncf; ++c) {
-        const int cid = pr[cfoff + c];
+        const int cid = uni(s_prog + cfoff + c);
         if (valid)
           nz[(size_t)(D + cid) * N + n] = rng_normal(k0, k1, (uint32_t)n, (uint32_t)cid, step, RNG_CONF_NOISE);
       }
       for (int q = 0; q < Hh; ++q) {
         float a = fmaf(W1[npar * Hh + q], e, b1[q]);
-        for (int j = 0; j < npar; ++j) a = fmaf(W1[j * Hh + q], s_x[pr[paroff + j] * B + t], a);
+        for (int j = 0; j < npar; ++j) a = fmaf(W1[j * Hh + q], s_x[uni(s_prog + paroff + j) * B + t], a);
         for (int c = 0; c < ncf; ++c)
           a = fmaf(W1[(npar + 1 + c) * Hh + q],
-                   rng_normal(k0, k1, (uint32_t)n, (uint32_t)pr[cfoff + c], step, RNG_CONF_NOISE), a);
+                   rng_normal(k0, k1, (uint32_t)n, (uint32_t)uni(s_prog + cfoff + c), step, RNG_CONF_NOISE), a);
         out = fmaf(W2[q], fmaxf(a, 0.f), out);
       }
       s_x[var * B + t] = out;
@@ -273,23 +280,30 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
   if (valid) {
     float* xr = xhat + (size_t)r * D * N;
     for (int kk = 0; kk < nn; ++kk) {
-      const int var = pr[PROG_HDR + kk * NODE_REC];
+      const int var = uni(s_prog + PROG_HDR + kk * NODE_REC);
       xr[(size_t)var * N + n] = s_x[var * B + t];
     }
   }
 }
 
 // ============================================================================
-// K2: generator backward.  grid = (G, R), block = BS samples (one per thread).
-// The sample's generated values and running gradients live in LDS
-// (s_x / s_dx [D][BS]); the noise draws come from the forward's `noise` buffer.
-// Per node (reverse topological order):
-//   1. each thread rebuilds the node inputs, the pre-activation and
-//      dh_q = g * W2_q * [pre_q > 0]; pushes dL/dparent = W1 dh into s_dx;
-//   2. the block reduces the per-sample outer products over its BS samples from
-//      LDS in a fixed order (4 independent partial sums per parameter) and writes
-//      one partial slab gpart[r][blk][param] -- no atomics, bitwise reproducible.
-// LDS: s_in [BS][MI+2], s_dh/s_relu [BS][H+1], s_g [BS], s_x/s_dx [D][BS].
+// K2: generator backward.  grid = (G, R), block = BS = 128 samples (2 waves).
+// LDS-resident per block: the DAG program, the samples' generated values s_x
+// and running gradients s_dx ([D][BS]).  Per node (reverse topological order):
+//   compute  each thread rebuilds its sample's node inputs and pre-activations
+//            (packed fp32), stores the input row s_in[s] = [x_0..x_{nin-1}, 1, g]
+//            and s_z[s] = [dh_0..dh_{H-1} | relu_0..relu_{H-1} | 1, 0] with
+//            dh = g W2 [pre > 0], and pushes dL/dparent = W1 dh into s_dx.
+//   reduce   the node's parameter gradients are the products
+//              dW1|db1[j][q] = sum_s s_in[s][j] dh[s][q]          (j <= nin)
+//              dW2[q] | db2  = sum_s g_s * (relu[s][q] | 1)        (row nin+1)
+//            computed as "items" (row j, column pair) so one v_pk_fma_f32 does
+//            two parameters per sample with a broadcast s_in read and one
+//            ds_read_b64 of s_z.  When a node has <= 64 items (the common case)
+//            each wave reduces half of the samples and wave 1 hands its partial
+//            to wave 0 through LDS; the fixed order keeps the slab
+//            gpart[r][blk][param] bitwise reproducible (no atomics).
+// Noise draws come from the forward's `noise` buffer, prefetched a node ahead.
 // ============================================================================
 template <int H, int BS>
 __global__ __launch_bounds__(BS) void gen_bwd_kernel(
@@ -297,28 +311,31 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
     const float* __restrict__ xhat, const float* __restrict__ noise, int NS,
     const float* __restrict__ grad_part, int n_chunks, int R,
     int N, int D, int max_in, float* __restrict__ gpart) {
+  static_assert(BS == 128, "two-wave reduction split assumes 128 samples per block");
+  constexpr int HE = (H + 1) & ~1;       // dh / relu segments padded to even width
+  constexpr int HP = HE / 2;             // column pairs per row
+  constexpr int SZ = 2 * HE + 2;         // s_z row: dh | relu | 1 0
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int SI = max_in + 2;
-  const int SH = H + 1;
-  float* s_in = smem;
-  float* s_dh = s_in + BS * SI;
-  float* s_relu = s_dh + BS * SH;
-  float* s_g = s_relu + BS * SH;
-  float* s_x = s_g + BS;
-  float* s_dx = s_x + BS * D;
+  const int SI = (max_in + 2) | 1;       // odd stride: conflict-free per-thread row writes
+  float* s_z = smem;                                   // [BS][SZ]   (8-byte aligned rows)
+  f2* s_red = reinterpret_cast<f2*>(s_z + BS * SZ);    // [64]       wave-1 partials
+  float* s_x = reinterpret_cast<float*>(s_red + 64);   // [D][BS]
+  float* s_dx = s_x + BS * D;                          // [D][BS]
+  float* s_in = s_dx + BS * D;                         // [BS][SI]
+  int* s_prog = reinterpret_cast<int*>(s_in + BS * SI);
 
   const int r = blockIdx.y, blk = blockIdx.x, G = gridDim.x;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n = blk * BS + t;
   const bool valid = n < N;
-  const int* pr = prog + (size_t)r * prog_stride;
-  const int nn = pr[0];
+  const int* pg = prog + (size_t)r * prog_stride;
+  for (int i = t; i < prog_stride; i += BS) s_prog[i] = pg[i];
   const float* th = params + (size_t)r * P;
   const float* xr = xhat + (size_t)r * D * N;
   const float* nz = noise + (size_t)r * NS * N;
   float* gp = gpart + ((size_t)r * G + blk) * P;
 
-  // sample state into LDS; dL/dxhat = fixed-order sum of the MMD column chunks
+  // sample state; dL/dxhat = fixed-order sum of the MMD column chunks (0 on padding rows)
   for (int v = 0; v < D; ++v) {
     float s = 0.f, x = 0.f;
     if (valid) {
@@ -328,76 +345,111 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
     s_x[v * BS + t] = x;
     s_dx[v * BS + t] = s;
   }
+  float* my_z = s_z + t * SZ;
+  if (HE != H) { my_z[H] = 0.f; my_z[HE + H] = 0.f; }
+  my_z[2 * HE] = 1.f;
+  my_z[2 * HE + 1] = 0.f;
+  float* my_in = s_in + t * SI;
+  __syncthreads();
+  const int nn = uni(s_prog);
+  float e_cur = (nn > 0 && valid) ? nz[(size_t)uni(s_prog + PROG_HDR + (nn - 1) * NODE_REC) * N + n] : 0.f;
 
   for (int kk = nn - 1; kk >= 0; --kk) {
-    const int* nd = pr + PROG_HDR + kk * NODE_REC;
-    if (nd[1] == KIND_OBS) continue;
-    const int var = nd[0], npar = nd[2], paroff = nd[3], ncf = nd[4], cfoff = nd[5], poff = nd[6];
+    const float e_next =
+        (kk > 0 && valid) ? nz[(size_t)uni(s_prog + PROG_HDR + (kk - 1) * NODE_REC) * N + n] : 0.f;
+    const int* nd = s_prog + PROG_HDR + kk * NODE_REC;
+    if (uni(nd + 1) == KIND_OBS) { e_cur = e_next; continue; }
+    const int var = uni(nd), npar = uni(nd + 2), paroff = uni(nd + 3), ncf = uni(nd + 4);
+    const int cfoff = uni(nd + 5), poff = uni(nd + 6);
     const int nin = npar + 1 + ncf;
     const float* W1 = th + poff;
     const float* b1 = W1 + (size_t)nin * H;
     const float* W2 = b1 + H;
 
-    float* my_in = s_in + t * SI;
+    // ---- compute phase (one sample per thread) ----
+    const float gout = s_dx[var * BS + t];      // 0 on padding rows
     float pre[H];
 #pragma unroll
     for (int q = 0; q < H; ++q) pre[q] = b1[q];
     for (int j = 0; j < nin; ++j) {
       float x;
-      if (j < npar) x = s_x[pr[paroff + j] * BS + t];
-      else if (j == npar) x = valid ? nz[(size_t)var * N + n] : 0.f;
-      else x = valid ? nz[(size_t)(D + pr[cfoff + (j - npar - 1)]) * N + n] : 0.f;
+      if (j < npar) x = s_x[uni(s_prog + paroff + j) * BS + t];
+      else if (j == npar) x = e_cur;
+      else x = valid ? nz[(size_t)(D + uni(s_prog + cfoff + (j - npar - 1))) * N + n] : 0.f;
       my_in[j] = x;
 #pragma unroll
       for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[j * H + q], x, pre[q]);
     }
-    my_in[nin] = valid ? 1.f : 0.f;   // bias column
-    const float gout = s_dx[var * BS + t];
+    my_in[nin] = 1.f;
+    my_in[nin + 1] = gout;
     float dh[H];
 #pragma unroll
     for (int q = 0; q < H; ++q) {
       const bool on = pre[q] > 0.f;
       dh[q] = on ? gout * W2[q] : 0.f;
-      s_dh[t * SH + q] = dh[q];
-      s_relu[t * SH + q] = on ? pre[q] : 0.f;
+      my_z[q] = dh[q];
+      my_z[HE + q] = on ? pre[q] : 0.f;
     }
-    s_g[t] = gout;
     for (int j = 0; j < npar; ++j) {
       float s = 0.f;
 #pragma unroll
       for (int q = 0; q < H; ++q) s = fmaf(W1[j * H + q], dh[q], s);
-      s_dx[pr[paroff + j] * BS + t] += s;
+      s_dx[uni(s_prog + paroff + j) * BS + t] += s;
     }
+    e_cur = e_next;
     __syncthreads();
-    const int n_w1b1 = (nin + 1) * H;
-    const int np = n_w1b1 + H + 1;
-    for (int pidx = t; pidx < np; pidx += BS) {
-      const float* a;
-      const float* b;
-      int sa, sb;
-      if (pidx < n_w1b1) {
-        const int j = pidx / H, q = pidx - j * H;
-        a = s_in + j; sa = SI; b = s_dh + q; sb = SH;
-      } else if (pidx < n_w1b1 + H) {
-        a = s_relu + (pidx - n_w1b1); sa = SH; b = s_g; sb = 1;
+
+    // ---- reduction phase ----
+    const int n_w1 = (nin + 1) * HP;           // items of rows 0..nin (dW1, db1)
+    const int n_items = n_w1 + HP + 1;         // + row nin+1 (dW2 pairs, db2)
+    const bool split = n_items <= 64;          // each wave takes half of the samples
+    // item -> (row j, column offset in s_z, output slots o0/o1) and its sum over
+    // samples [s_lo, s_lo + s_n)
+    auto item = [&](int it, int s_lo, int s_n, int& o0, int& o1) -> f2 {
+      int j, zoff;
+      if (it < n_w1) {
+        j = it / HP;
+        zoff = 2 * (it - j * HP);
+        o0 = j * H + zoff;
+        o1 = (zoff + 1 < H) ? o0 + 1 : -1;
       } else {
-        a = s_g; sa = 1; b = nullptr; sb = 0;
+        j = nin + 1;
+        const int q = 2 * (it - n_w1);
+        zoff = HE + q;
+        if (q < H) { o0 = (nin + 1) * H + q; o1 = (q + 1 < H) ? o0 + 1 : -1; }
+        else { o0 = (nin + 1) * H + H; o1 = -1; }        // db2 = sum_s g * 1
       }
-      float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-      if (b) {
+      const float* a = s_in + s_lo * SI + j;
+      const float* zb = s_z + s_lo * SZ + zoff;
+      f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
 #pragma unroll 4
-        for (int s4 = 0; s4 < BS; s4 += 4) {
-          acc0 = fmaf(a[(s4 + 0) * sa], b[(s4 + 0) * sb], acc0);
-          acc1 = fmaf(a[(s4 + 1) * sa], b[(s4 + 1) * sb], acc1);
-          acc2 = fmaf(a[(s4 + 2) * sa], b[(s4 + 2) * sb], acc2);
-          acc3 = fmaf(a[(s4 + 3) * sa], b[(s4 + 3) * sb], acc3);
-        }
-      } else {
-        for (int s4 = 0; s4 < BS; s4 += 4) {
-          acc0 += a[s4]; acc1 += a[s4 + 1]; acc2 += a[s4 + 2]; acc3 += a[s4 + 3];
-        }
+      for (int s2 = 0; s2 < s_n; s2 += 2) {
+        const float a0 = a[s2 * SI], a1 = a[(s2 + 1) * SI];
+        const f2 z0 = *reinterpret_cast<const f2*>(zb + s2 * SZ);
+        const f2 z1 = *reinterpret_cast<const f2*>(zb + (s2 + 1) * SZ);
+        acc0 = f2{a0, a0} * z0 + acc0;
+        acc1 = f2{a1, a1} * z1 + acc1;
       }
-      gp[poff + pidx] = (acc0 + acc1) + (acc2 + acc3);
+      return acc0 + acc1;
+    };
+    if (split) {
+      f2 acc = {0.f, 0.f};
+      int o0 = -1, o1 = -1;
+      if (lane < n_items) acc = item(lane, wave * 64, 64, o0, o1);
+      if (wave == 1) s_red[lane] = acc;
+      __syncthreads();
+      if (wave == 0 && lane < n_items) {
+        acc = acc + s_red[lane];
+        gp[poff + o0] = acc.x;
+        if (o1 >= 0) gp[poff + o1] = acc.y;
+      }
+    } else {
+      for (int it = t; it < n_items; it += BS) {
+        int o0, o1;
+        const f2 acc = item(it, 0, BS, o0, o1);
+        gp[poff + o0] = acc.x;
+        if (o1 >= 0) gp[poff + o1] = acc.y;
+      }
     }
     __syncthreads();
   }
@@ -498,6 +550,14 @@ extern "C" int cgnn_launch_loss_finalize(const float* lpart, int n_parts, float*
 #define CGNN_H_LIST(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(10) X(12) X(16) X(20) X(24) X(30) X(32) \
   X(40) X(48) X(50) X(64)
 
+// kernels whose dynamic LDS exceeds the default 64 KiB window must opt in
+template <typename K>
+static void allow_lds(K kernel, size_t lds) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
 extern "C" int cgnn_gen_supported_h(int H) {
   switch (H) {
 #define CASE_H(h) case h: return 1;
@@ -512,12 +572,14 @@ extern "C" int cgnn_launch_gen_fwd(const int* prog, int prog_stride, const float
                                    const uint32_t* keys, const int* step_base, int step_off, int N,
                                    int D, int H, int R, hipStream_t st) {
   dim3 grid((N + 255) / 256, R), block(256);
-  const size_t lds = sizeof(float) * (size_t)D * 256;
+  const size_t lds = sizeof(float) * (size_t)D * 256 + sizeof(int) * (size_t)prog_stride;
+  if (lds > 160 * 1024) return -2;
   switch (H) {
-#define CASE_H(h) case h: hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, lds, st, prog, prog_stride, params, P, data, xhat, noise, NS, keys, step_base, step_off, N, D, H); break;
+#define CASE_H(h) case h: allow_lds(gen_fwd_kernel<h>, lds); hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, lds, st, prog, prog_stride, params, P, data, xhat, noise, NS, keys, step_base, step_off, N, D, H); break;
     CGNN_H_LIST(CASE_H)
 #undef CASE_H
     default:
+      allow_lds(gen_fwd_kernel<0>, lds);
       hipLaunchKernelGGL((gen_fwd_kernel<0>), grid, block, lds, st, prog, prog_stride, params, P, data,
                          xhat, noise, NS, keys, step_base, step_off, N, D, H);
   }
@@ -528,9 +590,10 @@ constexpr int GEN_BWD_BS = 128;
 
 extern "C" int cgnn_gen_bwd_blocks(int N) { return (N + GEN_BWD_BS - 1) / GEN_BWD_BS; }
 
-extern "C" size_t cgnn_gen_bwd_lds(int H, int max_in, int D) {
-  return sizeof(float) * ((size_t)GEN_BWD_BS * (max_in + 2) + 2 * (size_t)GEN_BWD_BS * (H + 1) + GEN_BWD_BS +
-                          2 * (size_t)GEN_BWD_BS * D);
+extern "C" size_t cgnn_gen_bwd_lds(int H, int max_in, int D, int prog_stride) {
+  const size_t HE = (size_t)((H + 1) & ~1);
+  return sizeof(float) * ((size_t)GEN_BWD_BS * ((2 * HE + 2) + ((max_in + 2) | 1) + 2 * (size_t)D) + 128) +
+         sizeof(int) * (size_t)prog_stride;
 }
 
 extern "C" int cgnn_launch_gen_bwd(const int* prog, int prog_stride, const float* params, int P,
@@ -539,10 +602,10 @@ extern "C" int cgnn_launch_gen_bwd(const int* prog, int prog_stride, const float
                                    hipStream_t st) {
   const int G = cgnn_gen_bwd_blocks(N);
   dim3 grid(G, R), block(GEN_BWD_BS);
-  const size_t lds = cgnn_gen_bwd_lds(H, max_in, D);
+  const size_t lds = cgnn_gen_bwd_lds(H, max_in, D, prog_stride);
   if (lds > 160 * 1024) return -2;
   switch (H) {
-#define CASE_H(h) case h: hipLaunchKernelGGL((gen_bwd_kernel<h, GEN_BWD_BS>), grid, block, lds, st, prog, prog_stride, params, P, xhat, noise, NS, gradp, n_chunks, R, N, D, max_in, gpart); break;
+#define CASE_H(h) case h: allow_lds(gen_bwd_kernel<h, GEN_BWD_BS>, lds); hipLaunchKernelGGL((gen_bwd_kernel<h, GEN_BWD_BS>), grid, block, lds, st, prog, prog_stride, params, P, xhat, noise, NS, gradp, n_chunks, R, N, D, max_in, gpart); break;
     CGNN_H_LIST(CASE_H)
 #undef CASE_H
     default: return -1;

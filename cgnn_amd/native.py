@@ -6,12 +6,16 @@ a missing or stale extension raises :class:`NativeExtensionError`.  The CPU
 path (tests, tiny problems on machines without a GPU) is the PyTorch oracle in
 ``engine/reference.py`` and never touches ``_hip``.
 
+``CGNN_HIP_LIB`` / ``CGNN_RT_LIB`` point at another build of the same module
+(A/B kernel benchmarking in one process environment).
+
 ``rt()`` returns the host C++ runtime (``_rt``); it is built on first use if
 missing (g++ only, a few seconds).
 """
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import threading
 
@@ -28,6 +32,13 @@ def _load(name, builder):
         if name in _mods:
             return _mods[name]
         import torch  # noqa: F401  -- torch's HIP runtime must be loaded first (same SONAME)
+        alt = os.environ.get("CGNN%s_LIB" % name.upper())
+        if alt:   # A/B benchmarking: load another build of the same module
+            spec = importlib.util.spec_from_file_location("cgnn_amd." + name, alt)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            _mods[name] = mod
+            return mod
         try:
             mod = importlib.import_module("cgnn_amd." + name)
         except ImportError as first:
