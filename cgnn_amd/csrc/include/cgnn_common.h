@@ -119,4 +119,27 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nwg) {
   return base + idx;
 }
 
+// ---- packed-fp32 multi-bandwidth RBF (the seven gammas of Loss.py:10) ----
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 exp2_2(f2 x) {
+  return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+}
+
+// seven bandwidths for two distances at once; returns ks (kernel sum) and w
+// (sum gamma * kernel) as packed pairs.
+__device__ __forceinline__ void rbf7x2(f2 d2, f2& ks, f2& w) {
+  const float L2E = 1.4426950408889634f;
+  const f2 e1 = exp2_2(d2 * (-0.005f * L2E));
+  const f2 e2 = exp2_2(d2 * (-0.05f * L2E));
+  const f2 e3 = exp2_2(d2 * (-0.25f * L2E));
+  const f2 e4 = e3 * e3;
+  const f2 e5 = e4 * e4;
+  const f2 e6 = exp2_2(d2 * (-5.0f * L2E));
+  const f2 e7 = exp2_2(d2 * (-50.0f * L2E));
+  ks = ((e1 + e2) + (e3 + e4)) + ((e5 + e6) + e7);
+  w = ((0.005f * e1 + 0.05f * e2) + (0.25f * e3 + 0.5f * e4)) + ((e5 + 5.0f * e6) + 50.0f * e7);
+}
+
+
 }  // namespace cgnn

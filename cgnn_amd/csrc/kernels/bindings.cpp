@@ -15,6 +15,10 @@ namespace py = pybind11;
 
 extern "C" {
 int cgnn_mmd_supported_d(int);
+int cgnn_mmd_mfma_supported(int);
+int cgnn_mmd_mfma_row_blocks(int);
+int cgnn_launch_mmd_mfma(int, int, const float*, const float*, const float*, const float*, float*, float*,
+                         int, int, int, int, float, hipStream_t);
 int cgnn_gen_supported_h(int);
 int cgnn_gen_bwd_blocks(int);
 size_t cgnn_gen_bwd_lds(int, int, int, int);
@@ -22,7 +26,7 @@ int cgnn_launch_mmd(int, int, const float*, const float*, float*, float*, int, i
                     float, hipStream_t);
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
                               const int*, int, int, hipStream_t);
-int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int,
+int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
                         const float*, int, int, int, int, int, int, float*, hipStream_t);
@@ -72,7 +76,7 @@ static void chk(int rc, const char* what) {
 class PyEngine {
  public:
   PyEngine(std::vector<int> icfg, std::vector<float> fcfg, std::vector<uint64_t> ptrs, uint64_t stream) {
-    if (icfg.size() < 14 || fcfg.size() < 5 || ptrs.size() < 18) throw std::invalid_argument("engine config size");
+    if (icfg.size() < 17 || fcfg.size() < 5 || ptrs.size() < 20) throw std::invalid_argument("engine config size");
     std::vector<const void*> p(ptrs.size());
     for (size_t k = 0; k < ptrs.size(); ++k) p[k] = reinterpret_cast<const void*>(ptrs[k]);
     h_ = cgnn_engine_create(icfg.data(), fcfg.data(), p.data(), S(stream));
@@ -92,6 +96,14 @@ PYBIND11_MODULE(_hip, m) {
   m.def("arch", []() { return std::string("gfx950"); });
   m.def("device_count", []() { int n = 0; if (hipGetDeviceCount(&n) != hipSuccess) return 0; return n; });
   m.def("mmd_supported_d", &cgnn_mmd_supported_d);
+  m.def("mmd_mfma_supported", &cgnn_mmd_mfma_supported);
+  m.def("mmd_mfma_row_blocks", &cgnn_mmd_mfma_row_blocks);
+  m.def("mmd_mfma", [](int mode, int D, uint64_t xhat, uint64_t data, uint64_t xn, uint64_t yn, uint64_t gp,
+                       uint64_t lp, int N, int R, int n_chunks, int tpc, float gscale, uint64_t st) {
+    chk(cgnn_launch_mmd_mfma(mode, D, Pt<const float>(xhat), Pt<const float>(data), Pt<const float>(xn),
+                             Pt<const float>(yn), Pt<float>(gp), Pt<float>(lp), N, R, n_chunks, tpc, gscale,
+                             S(st)), "mmd_mfma");
+  });
   m.def("gen_supported_h", &cgnn_gen_supported_h);
   m.def("gen_bwd_blocks", &cgnn_gen_bwd_blocks);
   m.def("gen_bwd_lds", &cgnn_gen_bwd_lds);
@@ -109,9 +121,11 @@ PYBIND11_MODULE(_hip, m) {
                                   R, S(st)), "loss_finalize");
   });
   m.def("gen_fwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t data, uint64_t xhat, uint64_t noise,
-                      int NS, uint64_t keys, uint64_t step, int off, int N, int D, int H, int R, uint64_t st) {
+                      int NS, uint64_t xnorm, uint64_t keys, uint64_t step, int off, int N, int D, int H, int R,
+                      uint64_t st) {
     chk(cgnn_launch_gen_fwd(Pt<const int>(prog), ps, Pt<const float>(params), P, Pt<const float>(data),
-                            Pt<float>(xhat), Pt<float>(noise), NS, Pt<const uint32_t>(keys), Pt<const int>(step),
+                            Pt<float>(xhat), Pt<float>(noise), NS, Pt<float>(xnorm), Pt<const uint32_t>(keys),
+                            Pt<const int>(step),
                             off, N, D, H, R, S(st)), "gen_fwd");
   });
   m.def("gen_bwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t xhat, uint64_t noise, int NS,

@@ -20,9 +20,12 @@
 extern "C" {
 int cgnn_launch_mmd(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
                     float, hipStream_t);
+int cgnn_launch_mmd_mfma(int, int, const float*, const float*, const float*, const float*, float*, float*,
+                         int, int, int, int, float, hipStream_t);
+int cgnn_mmd_mfma_row_blocks(int);
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
                               const int*, int, int, hipStream_t);
-int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int,
+int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
                         const float*, int, int, int, int, int, int, float*, hipStream_t);
@@ -47,6 +50,8 @@ struct EngineConfig {
   int rff_k = 0;     // > 0: random-Fourier-feature MMD with k features per bandwidth
   int d_true = 0;    // unpadded variable count (RFF draws must not depend on padding)
   int NS = 0;        // noise streams per model = D + max #confounder streams
+  int mfma = 0;      // 1: train/eval MMD on the matrix cores (mmd_mfma.hip), D >= 8
+  int mf_chunks = 1, mf_tpc = 0;   // its column chunking (32-wide tiles per chunk)
 };
 
 struct EngineBuffers {
@@ -68,6 +73,8 @@ struct EngineBuffers {
   const uint32_t* keys = nullptr;
   float* rff_w = nullptr;       // [R][7k][D+1]
   float* rff_diff = nullptr;    // [R][7k]
+  float* xnorm = nullptr;       // [R][N] squared norms of xhat rows (written by gen_fwd)
+  const float* ynorm = nullptr; // [R][N] squared norms of the data rows
 };
 
 class Engine {
@@ -87,19 +94,29 @@ class Engine {
 
   static constexpr int kGammaCount = 7;
   int rff_features() const { return c_.rff_k * kGammaCount; }
+  // loss partials per model of a train/eval step, and of the constant true-true pass
   int n_parts() const {
-    return c_.rff_k > 0 ? (rff_features() + 255) / 256 : c_.n_chunks * c_.row_tiles;
+    if (c_.rff_k > 0) return (rff_features() + 255) / 256;
+    if (c_.mfma) return c_.mf_chunks * cgnn_mmd_mfma_row_blocks(c_.N);
+    return c_.n_chunks * c_.row_tiles;
   }
-  int grad_chunks() const { return c_.rff_k > 0 ? 1 : c_.n_chunks; }
+  int n_parts_tt() const { return c_.n_chunks * c_.row_tiles; }
+  int grad_chunks() const { return c_.rff_k > 0 ? 1 : (c_.mfma ? c_.mf_chunks : c_.n_chunks); }
 
-  // loss (+ gradient when train) of the current xhat
-  void enqueue_loss(int off, bool train) {
+  // loss (+ gradient when train) of the current xhat; `need_loss` false lets the
+  // matrix-core kernel skip the (unread) training loss
+  void enqueue_loss(int off, bool train, bool need_loss = true) {
     if (c_.rff_k > 0) {
       check(rff_launch_freqs(b_.rff_w, b_.keys, b_.step, off, c_.rff_k, c_.D, kGammaCount, c_.d_true,
                              c_.R, st_), "rff_freqs");
       check(rff_launch_fwd_bwd(train ? 0 : 1, b_.xhat, b_.data, b_.rff_w, b_.rff_diff, b_.lpart,
                                b_.gradp, c_.N, c_.D, rff_features(), c_.R, c_.rff_k,
                                sqrtf(2.f / (float)c_.rff_k), st_), "rff");
+    } else if (c_.mfma) {
+      const float inv = 1.f / ((float)c_.N * (float)c_.N);
+      check(cgnn_launch_mmd_mfma(train ? (need_loss ? 0 : 3) : 1, c_.D, b_.xhat, b_.data, b_.xnorm, b_.ynorm,
+                                 b_.gradp, b_.lpart, c_.N, c_.R,
+                                 c_.mf_chunks, c_.mf_tpc, train ? 4.f * inv : 0.f, st_), "mmd_mfma");
     } else {
       const float inv = 1.f / ((float)c_.N * (float)c_.N);
       check(cgnn_launch_mmd(train ? 0 : 1, c_.D, b_.xhat, b_.data, b_.gradp, b_.lpart, c_.N, c_.R,
@@ -123,18 +140,19 @@ class Engine {
     const float inv = 1.f / ((float)c_.N * (float)c_.N);
     check(cgnn_launch_mmd(2, c_.D, b_.xhat, b_.data, b_.gradp, b_.lpart, c_.N, c_.R, c_.row_tiles,
                           c_.n_chunks, c_.tpc, 0.f, st_), "mmd(tt)");
-    check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 2,
+    check(cgnn_launch_loss_finalize(b_.lpart, n_parts_tt(), b_.tt, b_.loss_last, b_.loss_acc, inv, 2,
                                     nullptr, 0, b_.step, 0, c_.R, st_), "finalize(tt)");
   }
 
   void enqueue_train_step(int off, bool record_hist) {
     const float inv = loss_scale();
     check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
-                              b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
-    enqueue_loss(off, true);
-    check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 0,
-                                    record_hist ? b_.loss_hist : nullptr, c_.hist_stride, b_.step, off,
-                                    c_.R, st_), "finalize");
+                              b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
+    enqueue_loss(off, true, record_hist);
+    // the training loss is only observable through the recorded history
+    if (record_hist)
+      check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 0,
+                                      b_.loss_hist, c_.hist_stride, b_.step, off, c_.R, st_), "finalize");
     check(cgnn_launch_gen_bwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.xhat, b_.noise, c_.NS, b_.gradp,
                               grad_chunks(), c_.R, c_.N, c_.D, c_.H, c_.max_in, b_.gpart, st_), "gen_bwd");
     check(cgnn_launch_adam(b_.params, b_.m, b_.v, b_.gpart, G_, b_.prog, c_.prog_stride, c_.P, b_.step,
@@ -144,7 +162,7 @@ class Engine {
   void enqueue_eval_step(int off) {
     const float inv = loss_scale();
     check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
-                              b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
+                              b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
     enqueue_loss(off, false);
     check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 1,
                                     nullptr, 0, b_.step, off, c_.R, st_), "finalize(eval)");
@@ -211,6 +229,7 @@ extern "C" void* cgnn_engine_create(const int* icfg, const float* fcfg, const vo
   c.R = icfg[0]; c.N = icfg[1]; c.D = icfg[2]; c.H = icfg[3]; c.P = icfg[4];
   c.prog_stride = icfg[5]; c.max_in = icfg[6]; c.row_tiles = icfg[7]; c.n_chunks = icfg[8];
   c.tpc = icfg[9]; c.hist_stride = icfg[10]; c.rff_k = icfg[11]; c.d_true = icfg[12]; c.NS = icfg[13];
+  c.mfma = icfg[14]; c.mf_chunks = icfg[15]; c.mf_tpc = icfg[16];
   c.lr = fcfg[0]; c.beta1 = fcfg[1]; c.beta2 = fcfg[2]; c.eps = fcfg[3]; c.init_std = fcfg[4];
   cgnn::EngineBuffers b;
   b.prog = (const int*)ptrs[0]; b.params = (float*)ptrs[1]; b.m = (float*)ptrs[2];
@@ -219,6 +238,7 @@ extern "C" void* cgnn_engine_create(const int* icfg, const float* fcfg, const vo
   b.gpart = (float*)ptrs[9]; b.tt = (float*)ptrs[10]; b.loss_last = (float*)ptrs[11];
   b.loss_acc = (float*)ptrs[12]; b.loss_hist = (float*)ptrs[13]; b.step = (int*)ptrs[14];
   b.keys = (const uint32_t*)ptrs[15]; b.rff_w = (float*)ptrs[16]; b.rff_diff = (float*)ptrs[17];
+  b.xnorm = (float*)ptrs[18]; b.ynorm = (const float*)ptrs[19];
   return new cgnn::Engine(c, b, st);
 }
 

@@ -51,26 +51,7 @@ constexpr float MMD_SENTINEL = 1.0e17f;   // padded columns: exp(-g*d2) == 0 exa
 //   loss   += (+1 | -2) * sum_gamma exp(-gamma d2)
 // dL/dp_i = 4/N^2 * grad_i  (derivation in docs/KERNELS.md).
 // ============================================================================
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f2 exp2_2(f2 x) {
-  return f2{__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-}
-
-// seven bandwidths for two distances at once; returns ks (kernel sum) and w
-// (sum gamma * kernel) as packed pairs.
-__device__ __forceinline__ void rbf7x2(f2 d2, f2& ks, f2& w) {
-  const float L2E = 1.4426950408889634f;
-  const f2 e1 = exp2_2(d2 * (-0.005f * L2E));
-  const f2 e2 = exp2_2(d2 * (-0.05f * L2E));
-  const f2 e3 = exp2_2(d2 * (-0.25f * L2E));
-  const f2 e4 = e3 * e3;
-  const f2 e5 = e4 * e4;
-  const f2 e6 = exp2_2(d2 * (-5.0f * L2E));
-  const f2 e7 = exp2_2(d2 * (-50.0f * L2E));
-  ks = ((e1 + e2) + (e3 + e4)) + ((e5 + e6) + e7);
-  w = ((0.005f * e1 + 0.05f * e2) + (0.25f * e3 + 0.5f * e4)) + ((e5 + 5.0f * e6) + 50.0f * e7);
-}
+// f2, exp2_2 and rbf7x2 live in cgnn_common.h (shared with mmd_mfma.hip)
 
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void mmd_rbf_kernel(
@@ -202,8 +183,8 @@ template <int H>
 __global__ __launch_bounds__(256) void gen_fwd_kernel(
     const int* __restrict__ prog, int prog_stride, const float* __restrict__ params, int P,
     const float* __restrict__ data, float* __restrict__ xhat, float* __restrict__ noise, int NS,
-    const uint32_t* __restrict__ keys, const int* __restrict__ step_base, int step_off,
-    int N, int D, int Hrt) {
+    float* __restrict__ xnorm, const uint32_t* __restrict__ keys, const int* __restrict__ step_base,
+    int step_off, int N, int D, int Hrt) {
   extern __shared__ __attribute__((aligned(16))) float s_x[];   // [D][blockDim], then program
   const int r = blockIdx.y;
   const int t = threadIdx.x, B = blockDim.x;
@@ -278,11 +259,17 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
     }
   }
   if (valid) {
+    // generated sample out, plus its squared norm (program order) for the
+    // matrix-core MMD's Gram-form distances
     float* xr = xhat + (size_t)r * D * N;
+    float nrm = 0.f;
     for (int kk = 0; kk < nn; ++kk) {
       const int var = uni(s_prog + PROG_HDR + kk * NODE_REC);
-      xr[(size_t)var * N + n] = s_x[var * B + t];
+      const float v = s_x[var * B + t];
+      xr[(size_t)var * N + n] = v;
+      nrm = fmaf(v, v, nrm);
     }
+    if (xnorm) xnorm[(size_t)r * N + n] = nrm;
   }
 }
 
@@ -568,20 +555,20 @@ extern "C" int cgnn_gen_supported_h(int H) {
 }
 
 extern "C" int cgnn_launch_gen_fwd(const int* prog, int prog_stride, const float* params, int P,
-                                   const float* data, float* xhat, float* noise, int NS,
+                                   const float* data, float* xhat, float* noise, int NS, float* xnorm,
                                    const uint32_t* keys, const int* step_base, int step_off, int N,
                                    int D, int H, int R, hipStream_t st) {
   dim3 grid((N + 255) / 256, R), block(256);
   const size_t lds = sizeof(float) * (size_t)D * 256 + sizeof(int) * (size_t)prog_stride;
   if (lds > 160 * 1024) return -2;
   switch (H) {
-#define CASE_H(h) case h: allow_lds(gen_fwd_kernel<h>, lds); hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, lds, st, prog, prog_stride, params, P, data, xhat, noise, NS, keys, step_base, step_off, N, D, H); break;
+#define CASE_H(h) case h: allow_lds(gen_fwd_kernel<h>, lds); hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, lds, st, prog, prog_stride, params, P, data, xhat, noise, NS, xnorm, keys, step_base, step_off, N, D, H); break;
     CGNN_H_LIST(CASE_H)
 #undef CASE_H
     default:
       allow_lds(gen_fwd_kernel<0>, lds);
       hipLaunchKernelGGL((gen_fwd_kernel<0>), grid, block, lds, st, prog, prog_stride, params, P, data,
-                         xhat, noise, NS, keys, step_base, step_off, N, D, H);
+                         xhat, noise, NS, xnorm, keys, step_base, step_off, N, D, H);
   }
   return (int)hipGetLastError();
 }

@@ -1,0 +1,340 @@
+// Matrix-core MMD for wide joints (D >= 8).  Both products of the fused MMD
+// run on v_mfma_f32_32x32x16_f16 with a three-pass hi/lo split of every f32
+// operand (x = hi + lo, both f16; hi*hi + hi*lo + lo*hi, ~22-bit operands, f32
+// accumulation), 16x the f32-MFMA rate; the seven-bandwidth exponential
+// epilogue runs on the vector ALUs (packed f32) and co-issues with the matrix
+// cores of the other waves.  Same outputs and partial layout as the vector
+// kernel (cgnn_kernels.hip, mmd_rbf_kernel); the squared distance is taken in
+// the Gram form |x|^2 + |z|^2 - 2 x.z that the reference computes
+// (Loss.py:17-19).
+//
+// Orientation (one wave = 32 generated rows i; the block's 4 waves share a
+// 32-column tile j of the joint [pred; true] staged in LDS):
+//   C'[j][i] = sum_d Z[j][d] X[i][d]      A = Z tile (LDS, [j][d]), B = X rows
+//                                         (registers, split once)
+//   -> lane l owns row i = l&31; accumulator r holds column
+//      j(r, h) = (r&3) + 8(r>>2) + 4h (h = l>>5).
+//   W[i][j] = s_j * sum_g g exp(-g d2_ij)  (s_j = +1 pred column, -1 true column)
+//   G[i][d] += sum_j W[i][j] Z[j][d]       A = W: accumulator registers 8s..8s+7
+//      are k-step s (element e <-> j = 16s + 8(e>>2) + 4h + (e&3)), B = Z read
+//      from the transposed LDS image [d][j] at those j -- no lane movement.
+//   dL/dp_i = 4/N^2 (G_i - p_i sum_j W_ij)
+#include "cgnn_common.h"
+
+using namespace cgnn;
+
+namespace {
+
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+
+constexpr int MT = 32;          // tile edge (rows per wave, columns per tile)
+constexpr int WAVES = 4;        // rows per block = 128
+
+// seven bandwidths for two distances, each kernel value folded into the sum
+// (ks) and the weighted sum (w) as soon as it exists.
+__device__ __forceinline__ void rbf7x2_chain(f2 d2, f2& ks, f2& w) {
+  const float L2E = 1.4426950408889634f;
+  f2 e = exp2_2(d2 * (-0.005f * L2E));
+  ks = e;
+  w = e * 0.005f;
+  e = exp2_2(d2 * (-0.05f * L2E));
+  ks += e;
+  w = e * 0.05f + w;
+  f2 e3 = exp2_2(d2 * (-0.25f * L2E));
+  ks += e3;
+  w = e3 * 0.25f + w;
+  e3 *= e3;                               // gamma 0.5
+  ks += e3;
+  w = e3 * 0.5f + w;
+  e3 *= e3;                               // gamma 1
+  ks += e3;
+  w += e3;
+  e = exp2_2(d2 * (-5.0f * L2E));
+  ks += e;
+  w = e * 5.0f + w;
+  e = exp2_2(d2 * (-50.0f * L2E));
+  ks += e;
+  w = e * 50.0f + w;
+}
+
+__device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+
+__device__ __forceinline__ h8 cat(h4 a, h4 b) {
+  return h8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+__device__ __forceinline__ f16v mma(h8 a, h8 b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <int KD, int MODE>
+__global__ __launch_bounds__(256) void mmd_mfma_kernel(
+    const float* __restrict__ xhat, const float* __restrict__ data,
+    const float* __restrict__ xnorm, const float* __restrict__ ynorm,
+    float* __restrict__ grad_part, float* __restrict__ loss_part,
+    int N, int R, int tiles_per_chunk, float grad_scale) {
+  // MODE 0 train (loss + gradient), 1 eval (loss), 3 train without the loss
+  // (nobody reads the training loss unless a history is recorded)
+  constexpr bool GRAD = MODE == 0 || MODE == 3;
+  constexpr bool LOSS = MODE != 3;
+  constexpr int KP = (KD + 15) / 16 * 16;   // distance K padded to the MFMA k-step
+  constexpr int KS = KP / 16;
+  constexpr int NT = (KD + 31) / 32;        // 32-wide output tiles of the gradient
+  constexpr int ZS = KP + 8;                // [j][d] image row stride (halfs): conflict-free b128
+  constexpr int ZT = MT + 4;                // [d][j] image row stride (halfs): conflict-free b64
+  constexpr int ZIMG = MT * ZS, TIMG = NT * 32 * ZT;
+  __shared__ __attribute__((aligned(16))) _Float16 s_zh[2][ZIMG];
+  __shared__ __attribute__((aligned(16))) _Float16 s_zl[2][ZIMG];
+  __shared__ __attribute__((aligned(16))) _Float16 s_th[2][TIMG];
+  __shared__ __attribute__((aligned(16))) _Float16 s_tl[2][TIMG];
+  __shared__ __attribute__((aligned(16))) float s_n[2][MT];
+  __shared__ float s_red[WAVES];
+
+  const int rb = blockIdx.x, chunk = blockIdx.y, r = blockIdx.z;
+  const int n_chunks = gridDim.y, n_rb = gridDim.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int h = lane >> 5, li = lane & 31;
+  const int i = rb * (WAVES * MT) + wave * MT + li;
+  const bool row_ok = i < N;
+  const size_t mbase = (size_t)r * KD * N;
+  const float* X = xhat + mbase;
+  const float* Y = data + mbase;
+
+  // this lane's B fragments of its row (dims 16s + 8h + e), split once; row norm
+  h8 xbh[KS], xbl[KS];
+  const float* XN = xnorm + (size_t)r * N;
+  const float* YN = ynorm + (size_t)r * N;
+  const float nx = row_ok ? XN[i] : 0.f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int d = 16 * s + 8 * h + e;
+      const float v = (row_ok && d < KD) ? X[d * N + i] : 0.f;
+      _Float16 hi, lo;
+      split16(v, hi, lo);
+      xbh[s][e] = hi;
+      xbl[s][e] = lo;
+    }
+  }
+
+  const int TX = (N + MT - 1) / MT;         // column tiles per part
+  const int ct = 2 * TX;
+  const int t_begin = chunk * tiles_per_chunk;
+  const int t_end = min(ct, t_begin + tiles_per_chunk);
+
+  // zero both buffers once: padded dims / rows are never written afterwards
+  for (int e = t; e < 2 * ZIMG; e += 256) { (&s_zh[0][0])[e] = (_Float16)0.f; (&s_zl[0][0])[e] = (_Float16)0.f; }
+  for (int e = t; e < 2 * TIMG; e += 256) { (&s_th[0][0])[e] = (_Float16)0.f; (&s_tl[0][0])[e] = (_Float16)0.f; }
+  __syncthreads();
+
+  constexpr int LR = (MT * KD + 255) / 256;
+  // staging registers: LR tile elements + (threads 0..31) the column norm
+  auto load_tile = [&](int tile, float* regs) {
+    const float* src = tile < TX ? X : Y;
+    const int c0 = (tile < TX ? tile : tile - TX) * MT;
+    regs[LR] = (t < MT && c0 + t < N) ? (tile < TX ? XN : YN)[c0 + t] : 0.f;
+#pragma unroll
+    for (int k = 0; k < LR; ++k) {
+      const int e = t + 256 * k;
+      const int d = e >> 5, jj = e & 31;
+      regs[k] = (e < MT * KD && c0 + jj < N) ? src[d * N + c0 + jj] : 0.f;
+    }
+  };
+  auto store_tile = [&](int buf, const float* regs) {
+    if (t < MT) s_n[buf][t] = regs[LR];
+#pragma unroll
+    for (int k = 0; k < LR; ++k) {
+      const int e = t + 256 * k;
+      const int d = e >> 5, jj = e & 31;
+      if (e < MT * KD) {
+        _Float16 hi, lo;
+        split16(regs[k], hi, lo);
+        s_zh[buf][jj * ZS + d] = hi;
+        s_zl[buf][jj * ZS + d] = lo;
+        s_th[buf][d * ZT + jj] = hi;
+        s_tl[buf][d * ZT + jj] = lo;
+      }
+    }
+  };
+  float stage[LR + 1];
+  if (t_begin < t_end) {
+    load_tile(t_begin, stage);
+    store_tile(0, stage);
+    if (t_begin + 1 < t_end) {
+      load_tile(t_begin + 1, stage);
+      store_tile(1, stage);
+    }
+  }
+  __syncthreads();
+
+  f16v acc_g[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) acc_g[q] = f16v{};
+  float rowsum = 0.f, lacc = 0.f;
+
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int buf = (tile - t_begin) & 1;
+    const bool pred_part = tile < TX;
+    const int c0 = (pred_part ? tile : tile - TX) * MT;
+    const bool more = tile + 2 < t_end;
+    if (more) load_tile(tile + 2, stage);          // prefetch while this tile computes
+
+    // ---- distance Gram C'[j][i], three passes per k-step ----
+    f16v c = f16v{};
+    const _Float16* zr = &s_zh[buf][li * ZS + 8 * h];
+    const _Float16* zl = &s_zl[buf][li * ZS + 8 * h];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const h8 ah = *reinterpret_cast<const h8*>(zr + 16 * s);
+      const h8 al = *reinterpret_cast<const h8*>(zl + 16 * s);
+      c = mma(ah, xbh[s], c);
+      c = mma(ah, xbl[s], c);
+      c = mma(al, xbh[s], c);
+    }
+
+    // ---- epilogue (packed pairs of accumulator registers): kernel sum for the
+    // loss and, when training, the signed weights W written over c in place ----
+    f2 tl2 = {0.f, 0.f};
+    f2 rs2 = {0.f, 0.f};
+    const float sg = pred_part ? 1.f : -1.f;
+    // columns j >= N - c0 are padding (only the last tile of each part): d2 -> huge
+    const int jlim = N - c0 - 4 * h;               // compare j - 4h against it
+    const bool ragged = N - c0 < MT;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float4 nz4 = *reinterpret_cast<const float4*>(&s_n[buf][8 * g4 + 4 * h]);
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const int rg = 4 * g4 + 2 * qq;
+        const f2 nzp = qq ? f2{nz4.z, nz4.w} : f2{nz4.x, nz4.y};
+        const f2 cc = {c[rg], c[rg + 1]};
+        f2 d2 = cc * -2.f + (nzp + nx);    // Gram form, unclamped like the reference
+        if (ragged) {
+          const int jr = 2 * qq + 8 * g4;
+          d2.x = jr < jlim ? d2.x : 1.0e30f;
+          d2.y = jr + 1 < jlim ? d2.y : 1.0e30f;
+        }
+        f2 ks, w;
+        if (GRAD) rbf7x2_chain(d2, ks, w);
+        else rbf7x2(d2, ks, w);
+        if (LOSS) tl2 += ks;
+        if (GRAD) {
+          w *= sg;
+          rs2 += w;
+          c[rg] = w.x;
+          c[rg + 1] = w.y;
+        }
+      }
+    }
+    if (LOSS) lacc = fmaf(pred_part ? 1.f : -2.f, tl2.x + tl2.y, lacc);
+
+    if (GRAD) {
+      rowsum += rs2.x + rs2.y;
+      // ---- gradient product G[i][d] += sum_j W[i][j] Z[j][d] ----
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        h8 wh, wl;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          _Float16 hi, lo;
+          split16(c[8 * s + e], hi, lo);
+          wh[e] = hi;
+          wl[e] = lo;
+        }
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+          const _Float16* th = &s_th[buf][(32 * q + li) * ZT + 16 * s + 4 * h];
+          const _Float16* tl = &s_tl[buf][(32 * q + li) * ZT + 16 * s + 4 * h];
+          const h8 bh = cat(*reinterpret_cast<const h4*>(th), *reinterpret_cast<const h4*>(th + 8));
+          const h8 bl = cat(*reinterpret_cast<const h4*>(tl), *reinterpret_cast<const h4*>(tl + 8));
+          acc_g[q] = mma(wh, bh, acc_g[q]);
+          acc_g[q] = mma(wh, bl, acc_g[q]);
+          acc_g[q] = mma(wl, bh, acc_g[q]);
+        }
+      }
+    }
+    __syncthreads();                     // everyone is done with buffer `buf`
+    if (more) store_tile(buf, stage);
+    __syncthreads();
+  }
+
+  // ---- loss partial: fixed-order wave then block reduction ----
+  float v = row_ok ? lacc : 0.f;
+  v = wave_sum(v);
+  if (lane == 0) s_red[wave] = v;
+  __syncthreads();
+  if (t == 0) {
+    const float sum = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+    loss_part[((size_t)r * n_chunks + chunk) * n_rb + rb] = sum;
+  }
+
+  if (GRAD) {
+    // sum_j W_ij: the two lane halves hold disjoint column sets of row i = l&31
+    rowsum += __shfl_xor(rowsum, 32);
+    float* gp = grad_part + ((size_t)chunk * R + r) * KD * N;
+    const int i0 = rb * (WAVES * MT) + wave * MT;
+#pragma unroll
+    for (int rg = 0; rg < 16; ++rg) {
+      const int il = (rg & 3) + 8 * (rg >> 2) + 4 * h;   // accumulator row -> local row
+      const float rs = __shfl(rowsum, il);
+      const int ii = i0 + il;
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const int d = 32 * q + li;
+        if (d < KD && ii < N) {
+          const float p = X[d * N + ii];
+          gp[d * N + ii] = (acc_g[q][rg] - p * rs) * grad_scale;
+        }
+      }
+    }
+  }
+}
+
+template <int KD>
+int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const float* xn, const float* yn,
+                      float* gpart, float* lpart, int N, int R, int n_chunks, int tpc, float gscale,
+                      hipStream_t st) {
+  const int n_rb = (N + WAVES * MT - 1) / (WAVES * MT);
+  dim3 grid(n_rb, n_chunks, R), block(256);
+  if (mode == 0)
+    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 0>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale);
+  else if (mode == 3)
+    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 3>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale);
+  else if (mode == 1)
+    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 1>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale);
+  else
+    return -3;
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Supported widths (the padded D of engine/batch.py SUPPORTED_D, >= 8)
+extern "C" int cgnn_mmd_mfma_supported(int D) {
+  switch (D) {
+    case 8: case 12: case 16: case 20: case 24: case 32: case 48: case 64: return 1;
+    default: return 0;
+  }
+}
+
+// Geometry: row blocks of 128 generated rows; `n_chunks` column chunks of
+// `tpc` 32-wide tiles of the joint [pred; true] column space.
+extern "C" int cgnn_mmd_mfma_row_blocks(int N) { return (N + WAVES * MT - 1) / (WAVES * MT); }
+
+// xnorm / ynorm: [R][N] squared norms of the generated / true samples
+extern "C" int cgnn_launch_mmd_mfma(int mode, int D, const float* xhat, const float* data, const float* xnorm,
+                                    const float* ynorm, float* gpart, float* lpart, int N, int R, int n_chunks,
+                                    int tpc, float gscale, hipStream_t st) {
+  switch (D) {
+#define CASE_D(d) case d: return launch_mmd_mfma_d<d>(mode, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale, st);
+    CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20) CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64)
+#undef CASE_D
+    default: return -1;
+  }
+}

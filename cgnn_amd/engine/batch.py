@@ -38,6 +38,38 @@ def mmd_geometry(N: int, R: int):
     return row_tiles, n_chunks, tpc
 
 
+MFMA_ROWS = 128     # generated rows per workgroup of the matrix-core MMD
+MFMA_TILE = 32      # joint columns per LDS tile
+
+
+def mmd_mfma_geometry(N: int, R: int):
+    """(row_blocks, n_chunks, tiles_per_chunk) of the matrix-core MMD: enough
+    column chunks that the launch has >= ~1024 workgroups."""
+    rb = (N + MFMA_ROWS - 1) // MFMA_ROWS
+    ct = 2 * ((N + MFMA_TILE - 1) // MFMA_TILE)
+    n_chunks = min(ct, max(1, math.ceil(1024 / (rb * R))))
+    tpc = math.ceil(ct / n_chunks)
+    n_chunks = math.ceil(ct / tpc)
+    return rb, n_chunks, tpc
+
+
+def mmd_kernel_choice(D: int, mmd_kernel: str = "auto") -> str:
+    """'mfma' (matrix cores, D >= 8) or 'valu' (packed-fp32 vector kernel).
+    ``CGNN_MMD_KERNEL=valu|mfma`` overrides 'auto'."""
+    import os
+    choice = mmd_kernel
+    if choice == "auto":
+        choice = os.environ.get("CGNN_MMD_KERNEL", "auto")
+    hip = native.hip()
+    if choice == "auto":
+        choice = "mfma" if hip.mmd_mfma_supported(D) else "valu"
+    if choice == "mfma" and not hip.mmd_mfma_supported(D):
+        raise ValueError("matrix-core MMD needs D in (8, 12, 16, 20, 24, 32, 48, 64), got %d" % D)
+    if choice not in ("mfma", "valu"):
+        raise ValueError("mmd_kernel must be auto|mfma|valu")
+    return choice
+
+
 def _keys_tensor(keys, device):
     arr = np.asarray(keys, dtype=np.uint64).astype(np.uint32).reshape(-1)
     return torch.from_numpy(arr.view(np.int32).copy()).to(device)
@@ -48,7 +80,8 @@ class DeviceTrainer:
 
     def __init__(self, programs: Sequence[Program], datas: Sequence[np.ndarray],
                  keys: Sequence[tuple], H: int, device, learning_rate=0.01, init_std=0.05,
-                 use_fast_mmd=False, nb_vectors=100, record_history=0, graph_chunk=50):
+                 use_fast_mmd=False, nb_vectors=100, record_history=0, graph_chunk=50,
+                 mmd_kernel="auto"):
         hip = native.hip()
         self.hip = hip
         if not hip.gen_supported_h(int(H)):
@@ -84,9 +117,11 @@ class DeviceTrainer:
             row_tiles, n_chunks, tpc = mmd_geometry(N, R)
             self.geometry = (row_tiles, n_chunks, tpc)
             self.rff_k = int(nb_vectors) if use_fast_mmd else 0
+            self.mmd_kernel = "rff" if self.rff_k else mmd_kernel_choice(D, mmd_kernel)
+            mf_rb, mf_chunks, mf_tpc = mmd_mfma_geometry(N, R)
             F = 7 * self.rff_k
-            n_parts = max(row_tiles * n_chunks, (F + 255) // 256 if F else 0)
-            self.gradp = torch.zeros(max(n_chunks, 1), R, D, N, **f32)
+            n_parts = max(row_tiles * n_chunks, mf_rb * mf_chunks, (F + 255) // 256 if F else 0)
+            self.gradp = torch.zeros(max(n_chunks, mf_chunks, 1), R, D, N, **f32)
             self.lpart = torch.zeros(R, n_parts, **f32)
             G = hip.gen_bwd_blocks(N)
             self.gpart = torch.zeros(R, G, P, **f32)
@@ -98,19 +133,22 @@ class DeviceTrainer:
             self.step = torch.zeros(2, dtype=torch.int32, device=dev)
             self.rff_w = torch.zeros(R, max(F, 1), D + 1, **f32)
             self.rff_diff = torch.zeros(R, max(F, 1), **f32)
+            # squared row norms for the Gram-form (matrix-core) MMD
+            self.xnorm = torch.zeros(R, N, **f32)
+            self.ynorm = (self.data * self.data).sum(1).contiguous()
             # a dedicated (non-default) stream: hipGraph capture is not allowed on
             # the legacy null stream, and batches on different devices overlap
             self.stream = torch.cuda.Stream(dev)
             stream = self.stream
             icfg = [R, N, D, self.H, P, stride, max_in, row_tiles, n_chunks, tpc, self.hist_len,
-                    self.rff_k, d, self.NS]
+                    self.rff_k, d, self.NS, int(self.mmd_kernel == "mfma"), mf_chunks, mf_tpc]
             fcfg = [float(learning_rate), 0.9, 0.999, 1e-8, float(init_std)]
             ptrs = [t.data_ptr() for t in (self.prog, self.params, self.m, self.v, self.data,
                                            self.xhat, self.noise, self.gradp, self.lpart, self.gpart,
                                            self.tt, self.loss_last, self.loss_acc)]
             ptrs.append(self.hist.data_ptr() if self.hist_len else 0)
             ptrs += [self.step.data_ptr(), self.keys.data_ptr(), self.rff_w.data_ptr(),
-                     self.rff_diff.data_ptr()]
+                     self.rff_diff.data_ptr(), self.xnorm.data_ptr(), self.ynorm.data_ptr()]
             self.engine = hip.CgnnEngine(icfg, fcfg, ptrs, stream.cuda_stream)
         self.graph_chunk = int(graph_chunk)
 

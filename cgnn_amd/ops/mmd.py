@@ -12,7 +12,7 @@ import math
 import torch
 
 from .. import native
-from ..engine.batch import mmd_geometry, padded_dim
+from ..engine.batch import mmd_geometry, mmd_kernel_choice, mmd_mfma_geometry, padded_dim
 from ..engine.reference import GAMMAS, mmd_loss_dense
 
 
@@ -25,16 +25,18 @@ def _to_feature_major(x: torch.Tensor, D: int) -> torch.Tensor:
 
 class _MMDHip(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pred, true):
+    def forward(ctx, pred, true, kernel="auto"):
         hip = native.hip()
         R, N, d = pred.shape
         D = padded_dim(d)
+        kernel = mmd_kernel_choice(D, kernel)
         P = _to_feature_major(pred, D)
         T = _to_feature_major(true, D)
         row_tiles, n_chunks, tpc = mmd_geometry(N, R)
         dev = pred.device
-        gradp = torch.empty(n_chunks, R, D, N, dtype=torch.float32, device=dev)
-        lpart = torch.empty(R, row_tiles * n_chunks, dtype=torch.float32, device=dev)
+        mf_rb, mf_chunks, mf_tpc = mmd_mfma_geometry(N, R)
+        gradp = torch.empty(max(n_chunks, mf_chunks), R, D, N, dtype=torch.float32, device=dev)
+        lpart = torch.empty(R, max(row_tiles * n_chunks, mf_rb * mf_chunks), dtype=torch.float32, device=dev)
         tt = torch.zeros(R, dtype=torch.float32, device=dev)
         last = torch.zeros(R, dtype=torch.float32, device=dev)
         acc = torch.zeros(R, dtype=torch.float32, device=dev)
@@ -45,27 +47,36 @@ class _MMDHip(torch.autograd.Function):
                 row_tiles, n_chunks, tpc, 0.0, st)
         hip.loss_finalize(lpart.data_ptr(), row_tiles * n_chunks, tt.data_ptr(), last.data_ptr(),
                           acc.data_ptr(), inv, 2, 0, 0, step.data_ptr(), 0, R, st)
-        hip.mmd(0, D, P.data_ptr(), T.data_ptr(), gradp.data_ptr(), lpart.data_ptr(), N, R,
-                row_tiles, n_chunks, tpc, 4.0 * inv, st)
-        hip.loss_finalize(lpart.data_ptr(), row_tiles * n_chunks, tt.data_ptr(), last.data_ptr(),
+        if kernel == "mfma":
+            pn = (P * P).sum(1).contiguous()
+            tn = (T * T).sum(1).contiguous()
+            hip.mmd_mfma(0, D, P.data_ptr(), T.data_ptr(), pn.data_ptr(), tn.data_ptr(), gradp.data_ptr(),
+                         lpart.data_ptr(), N, R, mf_chunks, mf_tpc, 4.0 * inv, st)
+            parts, chunks = mf_rb * mf_chunks, mf_chunks
+        else:
+            hip.mmd(0, D, P.data_ptr(), T.data_ptr(), gradp.data_ptr(), lpart.data_ptr(), N, R,
+                    row_tiles, n_chunks, tpc, 4.0 * inv, st)
+            parts, chunks = row_tiles * n_chunks, n_chunks
+        hip.loss_finalize(lpart.data_ptr(), parts, tt.data_ptr(), last.data_ptr(),
                           acc.data_ptr(), inv, 0, 0, 0, step.data_ptr(), 0, R, st)
-        g = gradp.sum(0)[:, :d].transpose(1, 2).contiguous()    # [R, N, d]
+        g = gradp[:chunks].sum(0)[:, :d].transpose(1, 2).contiguous()    # [R, N, d]
         ctx.save_for_backward(g)
         return last.to(pred.dtype)
 
     @staticmethod
     def backward(ctx, gout):
         (g,) = ctx.saved_tensors
-        return (gout.view(-1, 1, 1).to(g.dtype) * g).to(gout.dtype), None
+        return (gout.view(-1, 1, 1).to(g.dtype) * g).to(gout.dtype), None, None
 
 
-def mmd_loss(pred: torch.Tensor, true: torch.Tensor) -> torch.Tensor:
-    """Biased multi-bandwidth MMD^2; ``[N,d]`` -> scalar or ``[R,N,d]`` -> ``[R]``."""
+def mmd_loss(pred: torch.Tensor, true: torch.Tensor, kernel: str = "auto") -> torch.Tensor:
+    """Biased multi-bandwidth MMD^2; ``[N,d]`` -> scalar or ``[R,N,d]`` -> ``[R]``.
+    ``kernel``: 'auto' | 'mfma' (matrix cores, padded d >= 8) | 'valu'."""
     batched = pred.dim() == 3
     p = pred if batched else pred.unsqueeze(0)
     t = true if batched else true.unsqueeze(0)
     if p.is_cuda:
-        out = _MMDHip.apply(p, t.detach())
+        out = _MMDHip.apply(p, t.detach(), kernel)
     else:
         out = torch.stack([mmd_loss_dense(p[r], t[r]) for r in range(p.shape[0])])
     return out if batched else out[0]

@@ -19,8 +19,11 @@ def test_native_extension_is_loaded():
     assert hip.__file__.startswith(__import__("os").path.dirname(native.__file__))
 
 
-@pytest.mark.parametrize("N,d", [(2, 1), (63, 2), (64, 5), (257, 22), (1000, 22), (1500, 2)])
-def test_mmd_loss_and_grad_match_oracle(N, d):
+@pytest.mark.parametrize("N,d,kernel", [(2, 1, "valu"), (63, 2, "valu"), (64, 5, "valu"), (257, 22, "valu"),
+                                        (1000, 22, "valu"), (1500, 2, "valu"), (33, 8, "mfma"),
+                                        (257, 22, "mfma"), (1000, 22, "mfma"), (500, 40, "mfma"),
+                                        (130, 64, "mfma")])
+def test_mmd_loss_and_grad_match_oracle(N, d, kernel):
     from cgnn_amd.ops.mmd import mmd_loss
     torch.manual_seed(N * 7 + d)
     R = 3
@@ -35,7 +38,7 @@ def test_mmd_loss_and_grad_match_oracle(N, d):
         ref_l.append(float(L))
         ref_g.append(g)
     pg = pred.float().cuda().requires_grad_(True)
-    out = mmd_loss(pg, true.float().cuda())
+    out = mmd_loss(pg, true.float().cuda(), kernel=kernel)
     out.sum().backward()
     np.testing.assert_allclose(out.detach().cpu().numpy(), ref_l, rtol=2e-4, atol=2e-5)
     gref = torch.stack(ref_g).numpy()
@@ -90,6 +93,32 @@ def test_device_trainer_matches_oracle(kind, fast):
     hist = dev.history()
     np.testing.assert_allclose(hist, np.array(ref.loss_history), rtol=3e-3, atol=1e-5)
     np.testing.assert_allclose(scores, ref_scores, rtol=3e-3, atol=1e-5)
+
+
+def test_mfma_and_vector_mmd_trainers_agree():
+    """A 10-variable DAG (padded D = 12) trained with the matrix-core MMD and with
+    the vector MMD: the two differ only by the distance formula's rounding."""
+    H = 16
+    g = DirectedGraph()
+    for k in range(9):
+        g.add("V%d" % k, "V%d" % (k + 1))
+    g.add("V0", "V5")
+    prog = program_for_dag(g, H)
+    N = 400
+    datas = [_data(10, N, s) for s in range(3)]
+    keys = [model_key(5, "mf", r) for r in range(3)]
+    a = DeviceTrainer([prog] * 3, datas, keys, H, "cuda:0", record_history=8, mmd_kernel="mfma")
+    b = DeviceTrainer([prog] * 3, datas, keys, H, "cuda:0", record_history=8, mmd_kernel="valu")
+    assert a.mmd_kernel == "mfma" and b.mmd_kernel == "valu"
+    sa, sb = a.run(8, 4), b.run(8, 4)
+    np.testing.assert_allclose(a.history(), b.history(), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(sa, sb, rtol=1e-4, atol=1e-6)
+    # without a recorded history the training steps skip the (unread) loss:
+    # same gradients, same scores
+    c = DeviceTrainer([prog] * 3, datas, keys, H, "cuda:0", mmd_kernel="mfma").run(8, 4)
+    np.testing.assert_allclose(c, sa, rtol=1e-6)
+    ref = ReferenceTrainer([prog] * 3, datas, keys, H)
+    np.testing.assert_allclose(sa, ref.run(8, 4), rtol=3e-3, atol=1e-5)
 
 
 def test_graph_replay_equals_eager():
