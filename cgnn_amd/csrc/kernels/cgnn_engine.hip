@@ -119,7 +119,7 @@ class Engine {
                                  c_.mf_chunks, c_.mf_tpc, train ? 4.f * inv : 0.f, st_), "mmd_mfma");
     } else {
       const float inv = 1.f / ((float)c_.N * (float)c_.N);
-      check(cgnn_launch_mmd(train ? 0 : 1, c_.D, b_.xhat, b_.data, b_.gradp, b_.lpart, c_.N, c_.R,
+      check(cgnn_launch_mmd(train ? (need_loss ? 0 : 3) : 1, c_.D, b_.xhat, b_.data, b_.gradp, b_.lpart, c_.N, c_.R,
                             c_.row_tiles, c_.n_chunks, c_.tpc, train ? 4.f * inv : 0.f, st_), "mmd");
     }
   }

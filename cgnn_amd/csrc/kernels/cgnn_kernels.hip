@@ -58,6 +58,9 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
     const float* __restrict__ xhat, const float* __restrict__ data,
     float* __restrict__ grad_part, float* __restrict__ loss_part,
     int N, int R, int tiles_per_chunk, float grad_scale) {
+  // MODE 3: training step whose loss nobody reads (no history): gradient only
+  constexpr bool GRAD = MODE == 0 || MODE == 3;
+  constexpr bool LOSS = MODE != 3;
   constexpr int T = 256;
   __shared__ __attribute__((aligned(16))) float s_x[T * D];   // [T/2][D][2]
   __shared__ float s_red[4];
@@ -111,14 +114,14 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
       }
       f2 ks, w;
       rbf7x2(d2, ks, w);
-      tl += ks;
-      if (MODE == 0) {
+      if (LOSS) tl += ks;
+      if (GRAD) {
         const f2 sw = gsign * w;
 #pragma unroll
         for (int k = 0; k < D; ++k) g[k] = sw * diff[k] + g[k];
       }
     }
-    lacc = fmaf(lsign, tl.x + tl.y, lacc);
+    if (LOSS) lacc = fmaf(lsign, tl.x + tl.y, lacc);
   }
 
   // deterministic block reduction of the loss partial
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
     float s = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
     loss_part[((size_t)r * n_chunks + chunk) * row_tiles + rt] = s;
   }
-  if (MODE == 0 && valid) {
+  if (GRAD && valid) {
     float* gp = grad_part + ((size_t)chunk * R + r) * D * N;
 #pragma unroll
     for (int k = 0; k < D; ++k) gp[(size_t)k * N + i] = (g[k].x + g[k].y) * grad_scale;
@@ -503,6 +506,7 @@ static int launch_mmd_d(int mode, const float* xhat, const float* data, float* g
                         hipStream_t st) {
   dim3 grid(row_tiles, n_chunks, R), block(256);
   if (mode == 0) hipLaunchKernelGGL((mmd_rbf_kernel<D, 0>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
+  else if (mode == 3) hipLaunchKernelGGL((mmd_rbf_kernel<D, 3>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
   else if (mode == 1) hipLaunchKernelGGL((mmd_rbf_kernel<D, 1>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
   else hipLaunchKernelGGL((mmd_rbf_kernel<D, 2>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
   return (int)hipGetLastError();
