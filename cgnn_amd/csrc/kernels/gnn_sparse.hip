@@ -119,7 +119,9 @@ template <int L, bool XBF, bool YBF, int U>
 __global__ __launch_bounds__(256) void spmm_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
     void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
-    int n_rows, int F, int ldx, int ldy, int relu, int unit_col) {
+    int n_rows, int F, int ldx, int ldy, int relu, int unit_col, int wcols) {
+  // wcols: output columns this launch writes (from its base): the row stride ldy
+  // for a whole-row launch, the slab width for a column-slab launch
   constexpr int RPW = 64 / L;
   const int lane = threadIdx.x & 63;
   const int sub = lane / L, sl = lane - sub * L;
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
   gather_sum<L, XBF, U>(col, X, e0, e1, ldx, f0, fv, sub * L, sl, acc);
-  if (!rv || f0 >= ldy) return;
+  if (!rv || f0 >= wcols) return;
   const float rs = rscale ? rscale[row] : 1.f;
   float y[8];
 #pragma unroll
@@ -175,7 +177,7 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
   const bool fv = rv && f0 < C;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
-  gather_sum<L, true>(col, Z, e0, e1, ld, f0, fv, sub * L, sl, acc);
+  gather_sum<L, true, 8>(col, Z, e0, e1, ld, f0, fv, sub * L, sl, acc);
 
   const float rs = rv ? rscale[row] : 0.f;
   float lg[8];
@@ -348,46 +350,55 @@ static int spmm_unroll() {
 template <int L, int U>
 static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
-                         int relu, int uc, hipStream_t st) {
+                         int relu, int uc, int wc, hipStream_t st) {
   constexpr int RPB = 4 * (64 / L);   // rows per 256-thread block
   dim3 grid((n_rows + RPB - 1) / RPB), block(256);
-  if (xbf && ybf) hipLaunchKernelGGL((spmm_kernel<L, true, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc);
-  else if (xbf) hipLaunchKernelGGL((spmm_kernel<L, true, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc);
-  else if (ybf) hipLaunchKernelGGL((spmm_kernel<L, false, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc);
-  else hipLaunchKernelGGL((spmm_kernel<L, false, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc);
+  if (xbf && ybf) hipLaunchKernelGGL((spmm_kernel<L, true, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc);
+  else if (xbf) hipLaunchKernelGGL((spmm_kernel<L, true, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc);
+  else if (ybf) hipLaunchKernelGGL((spmm_kernel<L, false, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc);
+  else hipLaunchKernelGGL((spmm_kernel<L, false, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc);
   return (int)hipGetLastError();
 }
 
 template <int L>
 static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
-                         int relu, int uc, hipStream_t st) {
+                         int relu, int uc, int wc, hipStream_t st) {
   if (spmm_unroll() == 8)
-    return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, st);
-  return spmm_dispatch_u<L, 4>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, st);
+    return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
+  return spmm_dispatch_u<L, 4>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
+}
+
+// one launch writing output columns [0, wcols) of its base (wcols <= 512)
+static int spmm_launch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
+                       const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf, int relu,
+                       int uc, int wc, hipStream_t st) {
+  const int w = std::max(F, wc);
+  if (w <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
+  if (w <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
+  if (w <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
+  if (w <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
+  return -1;
 }
 
 extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X, void* Y,
                                const float* rscale, const float* bias, int n_rows, int F, int ldx,
                                int ldy, int xbf, int ybf, int relu, int unit_col, hipStream_t st) {
   if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
-  if (F > 512) {
-    // wide features: column slabs of 512 (16-byte aligned offsets), one launch each
-    const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;
-    for (int c0 = 0; c0 < F; c0 += 512) {
-      const int fc = std::min(512, F - c0);
-      const int rc = gnn_launch_spmm(rowptr, col, (const char*)X + c0 * xs, (char*)Y + c0 * ys, rscale,
-                                     bias ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu,
-                                     unit_col - c0, st);
-      if (rc) return rc;
-    }
-    return 0;
+  if (ldy <= 512 && F <= 512)
+    return spmm_launch(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, ldy, st);
+  // wide rows: column slabs of 512 output columns (16-byte aligned offsets), one
+  // launch each; the last slabs also write the padding / ones columns up to ldy
+  const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;
+  for (int c0 = 0; c0 < ldy; c0 += 512) {
+    const int fc = std::max(0, std::min(512, F - c0));
+    const int wc = std::min(512, ldy - c0);
+    const int rc = spmm_launch(rowptr, col, (const char*)X + (fc ? c0 * xs : 0), (char*)Y + c0 * ys, rscale,
+                               bias && fc ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu,
+                               unit_col >= 0 ? unit_col - c0 : -1, wc, st);
+    if (rc) return rc;
   }
-  if (F <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, st);
-  if (F <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, st);
-  if (F <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, st);
-  if (F <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, st);
-  return -1;
+  return 0;
 }
 
 extern "C" int gnn_spmm_ce_blocks(int n_rows) { return (n_rows + 31) / 32; }

@@ -35,6 +35,22 @@ def test_spmm_matches_reference(F, ld, xbf, ybf):
     np.testing.assert_allclose(got.float().numpy(), ref.float().numpy(), rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("F,ld", [(1433, 1440), (1024, 1032), (600, 608)])
+def test_spmm_wide_rows_with_ones_column(F, ld):
+    """Rows wider than one 512-column slab (Cora / Citeseer / Reddit widths): every
+    slab writes only its own columns, the last ones the padding and the ones column."""
+    n, rp, col = _graph(300, 2000, 2)
+    torch.manual_seed(1)
+    X = torch.randn(n, ld)
+    X[:, F:] = 0
+    X = X.to(torch.bfloat16)
+    rs = torch.rand(n) + 0.5
+    ref = ops.spmm(rp, col, X, F, rscale=rs, unit_col=F)
+    got = ops.spmm(rp.cuda(), col.cuda(), X.cuda(), F, rscale=rs.cuda(), unit_col=F).cpu()
+    np.testing.assert_allclose(got.float().numpy(), ref.float().numpy(), rtol=2e-2, atol=2e-2)
+    assert torch.all(got[:, F] == 1) and torch.all(got[:, F + 1:] == 0)
+
+
 def test_spmm_ce_matches_reference():
     n, rp, col = _graph(700, 5000, 1)
     C, ld = 47, 48
