@@ -62,6 +62,11 @@ int gnn_launch_relu_dropout_bwd(void*, const void*, long, float, hipStream_t);
 int gnn_launch_dense_fwd(const void*, const float*, const float*, const float*, const float*, void*, void*,
                          int, int, int, int, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t,
                          hipStream_t);
+int gnn_fused_bwd_blocks(int);
+int gnn_fused_bwd_width(int);
+int gnn_fused_bwd_supported(int, int, int);
+int gnn_launch_fused_bwd(const void*, const void*, const float*, const float*, const float*, float*, int, int,
+                         int, int, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
 int gnn_launch_dense_bwd(const void*, const float*, const void*, void*, int, int, int, int, float,
                          hipStream_t);
 }
@@ -202,6 +207,16 @@ PYBIND11_MODULE(_hip, m) {
                             float p, uint64_t st) {
     return gnn_launch_dense_bwd(Pt<const void>(dy2), Pt<const float>(w2), Pt<const void>(h1), Pt<void>(dp1), n,
                                 HD, C, ldc, p, S(st));
+  });
+  m.def("gnn_fused_bwd_blocks", &gnn_fused_bwd_blocks);
+  m.def("gnn_fused_bwd_width", &gnn_fused_bwd_width);
+  m.def("gnn_fused_bwd_supported", &gnn_fused_bwd_supported);
+  m.def("gnn_fused_bwd", [](uint64_t ax, uint64_t dy2, uint64_t w1, uint64_t b1, uint64_t w2, uint64_t gpart, int n,
+                            int F, int ldx, int HD, int C, int ldc, float p, uint32_t k0, uint32_t k1,
+                            uint32_t step, uint32_t row0, uint64_t st) {
+    return gnn_launch_fused_bwd(Pt<const void>(ax), Pt<const void>(dy2), Pt<const float>(w1), Pt<const float>(b1),
+                                Pt<const float>(w2), Pt<float>(gpart), n, F, ldx, HD, C, ldc, p, k0, k1, step,
+                                row0, S(st));
   });
   m.def("gnn_cast_bf16", [](uint64_t src, uint64_t dst, long n, uint64_t st) {
     chk(gnn_launch_cast_bf16(Pt<const float>(src), Pt<void>(dst), n, S(st)), "gnn_cast_bf16");

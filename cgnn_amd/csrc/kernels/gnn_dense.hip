@@ -118,7 +118,7 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
         if (thr8 > 0) x = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
         v[q] = x;
       }
-      if (rv) {
+      if (rv && H1) {          // H1 == nullptr: the fused backward recomputes it
 #pragma unroll
         for (int g = 0; g < 4; ++g)
           *reinterpret_cast<uint2*>(H1 + (size_t)row * HD + 32 * t + 8 * g + 4 * h) =
@@ -213,6 +213,195 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_bwd_kernel(
   }
 }
 
+
+// ============================================================================
+// Fused backward of the dense stages, H1 never stored (recomputed) and the two
+// weight-gradient contractions over the rows done in the same pass:
+//   P1^T = W1^T AX^T, H1 = dropout(relu(P1 + b1))      (as the forward, same Philox)
+//   dP1^T = (W2 dY2^T) * [H1 > 0] / (1-p)
+//   gW1^T[h][f] += sum_rows dP1^T[h][row] AX[row][f]     (f = F is the ones column: gb1)
+//   gW2[h][c]   += sum_rows H1^T[h][row] dY2[row][c]
+// Block = HD/32 waves, wave w owns hidden block w (32 units) for all three
+// products, so its weight-gradient tiles (KF/32 + 2 of 32x32) stay in its
+// accumulators for the whole persistent loop; the block walks 32-row tiles.
+// Per tile: stage AX / dY2 rows in LDS (row-major for the row-operand reads and
+// transposed [col][row] for the contraction over rows), recompute, write the
+// wave's H1^T / dP1^T block transposed ([hidden][row]) so the row contraction
+// reads 16 contiguous bytes per fragment; next tile's rows are prefetched into
+// registers meanwhile.  Output: one fp32 slab per block,
+// gpart[block][HD][KF + 64] = [gW1^T | gW2], summed in fixed order afterwards.
+// ============================================================================
+template <int KS, int KC, int HD>
+__global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
+    const uint16_t* __restrict__ AX, const uint16_t* __restrict__ dY2, const float* __restrict__ W1,
+    const float* __restrict__ b1, const float* __restrict__ W2, float* __restrict__ gpart, int n, int F,
+    int ldx, int C, int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
+    uint32_t row0) {
+  constexpr int NW = HD / 32;                 // waves per block = hidden blocks
+  constexpr int NT = NW * 64;
+  constexpr int KP = KS * 16;                 // layer-1 K (features + ones column), padded
+  constexpr int KF = (KP + 31) / 32 * 32;     // gW1^T columns (f), padded to whole tiles
+  constexpr int CP = KC * 16;                 // classes, padded
+  constexpr int W1S = KP + 8, W2S = CP + 8;
+  constexpr int AXS = KP + 8, DYS = CP + 8;
+  constexpr int TR = TILE + 8;                // transposed images: 32 rows + pad (80-B rows)
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* sW1T = lds;                       // [HD][W1S]
+  uint16_t* sW2 = sW1T + HD * W1S;            // [HD][W2S]   W2 rows (hidden-major)
+  uint16_t* sAX = sW2 + HD * W2S;             // [32][AXS]   row-major tile
+  uint16_t* sDY = sAX + TILE * AXS;           // [32][DYS]
+  uint16_t* sAXt = sDY + TILE * DYS;          // [KF][TR]    transposed tile
+  uint16_t* sDYt = sAXt + KF * TR;            // [64][TR]
+  uint16_t* sH1t = sDYt + 64 * TR;            // [HD][TR]
+  uint16_t* sDPt = sH1t + HD * TR;            // [HD][TR]
+  float* sB1 = reinterpret_cast<float*>(sDPt + HD * TR);   // [HD]
+
+  const int tid = threadIdx.x;
+  for (int i = tid; i < HD * KP; i += NT) {
+    const int k = i / HD, nn = i - k * HD;
+    sW1T[nn * W1S + k] = bf16_bits(k < F ? W1[(size_t)k * HD + nn] : 0.f);
+  }
+  for (int i = tid; i < HD * CP; i += NT) {
+    const int nn = i / CP, c = i - nn * CP;
+    sW2[nn * W2S + c] = bf16_bits(c < C ? W2[(size_t)nn * C + c] : 0.f);
+  }
+  for (int i = tid; i < HD; i += NT) sB1[i] = b1[i];
+  // zero the padding the per-tile staging never writes
+  for (int i = tid; i < TILE * AXS; i += NT) sAX[i] = 0;
+  for (int i = tid; i < TILE * DYS; i += NT) sDY[i] = 0;
+  for (int i = tid; i < KF * TR; i += NT) sAXt[i] = 0;
+  for (int i = tid; i < 64 * TR; i += NT) sDYt[i] = 0;
+
+  const int lane = tid & 63, h = lane >> 5, lr = lane & 31;
+  const int t = tid >> 6;                     // this wave's hidden block
+  const int n_tiles = (n + TILE - 1) / TILE;
+  const float scale = 1.f / (1.f - p);
+  const int xch = ldx / 8, ych = ldc / 8;     // 16-byte chunks per row
+
+  f32x16 g1[KF / 32], g2[2];
+#pragma unroll
+  for (int q = 0; q < KF / 32; ++q) g1[q] = f32x16{};
+  g2[0] = f32x16{};
+  g2[1] = f32x16{};
+
+  // prefetch registers: chunks tid, tid + NT, ... of the AX tile and of the dY2 tile
+  constexpr int PFX = (TILE * (KP / 8) + NT - 1) / NT, PFY = (TILE * (CP / 8) + NT - 1) / NT;
+  uint4 pax[PFX], pdy[PFY];
+  auto prefetch = [&](int tile) {
+    const int r0 = tile * TILE;
+#pragma unroll
+    for (int k = 0; k < PFX; ++k) {
+      const int i = tid + k * NT;
+      const int rr = i / xch, ch = i - rr * xch;
+      pax[k] = (i < TILE * xch && r0 + rr < n)
+                   ? *reinterpret_cast<const uint4*>(AX + (size_t)(r0 + rr) * ldx + 8 * ch)
+                   : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < PFY; ++k) {
+      const int i = tid + k * NT;
+      const int rr = i / ych, ch = i - rr * ych;
+      pdy[k] = (i < TILE * ych && r0 + rr < n)
+                   ? *reinterpret_cast<const uint4*>(dY2 + (size_t)(r0 + rr) * ldc + 8 * ch)
+                   : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  if ((int)blockIdx.x < n_tiles) prefetch(blockIdx.x);
+  __syncthreads();
+
+  for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    // ---- stage this tile (row-major + transposed), prefetch the next ----
+#pragma unroll
+    for (int k = 0; k < PFX; ++k) {
+      const int i = tid + k * NT;
+      if (i < TILE * xch) {
+        const int rr = i / xch, ch = i - rr * xch;
+        *reinterpret_cast<uint4*>(sAX + rr * AXS + 8 * ch) = pax[k];
+        const uint32_t w[4] = {pax[k].x, pax[k].y, pax[k].z, pax[k].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sAXt[(8 * ch + e) * TR + rr] = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PFY; ++k) {
+      const int i = tid + k * NT;
+      if (i < TILE * ych) {
+        const int rr = i / ych, ch = i - rr * ych;
+        *reinterpret_cast<uint4*>(sDY + rr * DYS + 8 * ch) = pdy[k];
+        const uint32_t w[4] = {pdy[k].x, pdy[k].y, pdy[k].z, pdy[k].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sDYt[(8 * ch + e) * TR + rr] = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
+      }
+    }
+    if (tile + (int)gridDim.x < n_tiles) prefetch(tile + gridDim.x);
+    __syncthreads();
+
+    // ---- recompute H1^T block t, dP1^T block t (lane = row, registers = hidden) ----
+    const int row = tile * TILE + lr;
+    f32x16 acc = {};
+    {
+      const uint16_t* arow = sW1T + (32 * t + lr) * W1S + 8 * h;
+      const uint16_t* xrow = sAX + lr * AXS + 8 * h;
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(load_bf16x8(arow + 16 * s2), load_bf16x8(xrow + 16 * s2),
+                                                      acc, 0, 0, 0);
+    }
+    f32x16 dh = {};
+    {
+      const uint16_t* arow = sW2 + (32 * t + lr) * W2S + 8 * h;
+      const uint16_t* yrow = sDY + lr * DYS + 8 * h;
+#pragma unroll
+      for (int s2 = 0; s2 < KC; ++s2)
+        dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(load_bf16x8(arow + 16 * s2), load_bf16x8(yrow + 16 * s2),
+                                                     dh, 0, 0, 0);
+    }
+    uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    if (thr8 > 0) {
+      const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
+      w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int nn = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+      float x = fmaxf(acc[q] + sB1[nn], 0.f);
+      if (thr8 > 0) x = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
+      const float d = x > 0.f ? dh[q] * scale : 0.f;
+      sH1t[nn * TR + lr] = bf16_bits(x);
+      sDPt[nn * TR + lr] = bf16_bits(d);
+    }
+    __syncthreads();
+
+    // ---- contractions over the tile's 32 rows (two k-steps of 16) ----
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 adp = load_bf16x8(sDPt + (32 * t + lr) * TR + 16 * s2 + 8 * h);
+      const bf16x8 ah1 = load_bf16x8(sH1t + (32 * t + lr) * TR + 16 * s2 + 8 * h);
+#pragma unroll
+      for (int q = 0; q < KF / 32; ++q)
+        g1[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            adp, load_bf16x8(sAXt + (32 * q + lr) * TR + 16 * s2 + 8 * h), g1[q], 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        g2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            ah1, load_bf16x8(sDYt + (32 * q + lr) * TR + 16 * s2 + 8 * h), g2[q], 0, 0, 0);
+    }
+    __syncthreads();      // images are rewritten by the next tile
+  }
+
+  // ---- this block's partial slab: rows = hidden 32t + m, columns [f | KF + c] ----
+  float* gp = gpart + (size_t)blockIdx.x * HD * (KF + 64);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int hrow = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+    float* dst = gp + (size_t)hrow * (KF + 64);
+#pragma unroll
+    for (int fb = 0; fb < KF / 32; ++fb) dst[32 * fb + lr] = g1[fb][q];
+    dst[KF + lr] = g2[0][q];
+    dst[KF + 32 + lr] = g2[1][q];
+  }
+}
+
 // ---------------------------------------------------------------- launchers
 static int dense_grid(int n) {
   static int cached_cus[64] = {0};
@@ -278,5 +467,70 @@ extern "C" int gnn_launch_dense_bwd(const void* dY2, const float* W2, const void
 #define BWD(kc, hd) if (KC <= kc && HD == hd) return bwd_launch<kc, hd>(dy, W2, h1, dp, n, C, ldc, p, st);
   BWD(3, 256) BWD(4, 256) BWD(3, 128) BWD(4, 128)
 #undef BWD
+  return -1;
+}
+
+// ---- fused backward launcher ----
+extern "C" int gnn_fused_bwd_blocks(int n) {
+  static int cached_cus[64] = {0};
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess && dev < 64) {
+    if (!cached_cus[dev]) {
+      hipDeviceProp_t prop;
+      cached_cus[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+    }
+    cus = cached_cus[dev];
+  }
+  const int tiles = (n + TILE - 1) / TILE;
+  return std::max(1, std::min(cus, tiles));
+}
+
+// width of one gpart row (gW1^T columns padded to whole 32-tiles, then 64 for gW2)
+extern "C" int gnn_fused_bwd_width(int ldx) {
+  const int KP = (ldx + 15) / 16 * 16;
+  return (KP + 31) / 32 * 32 + 64;
+}
+
+template <int KS, int KC, int HD>
+static int fused_bwd_launch(const uint16_t* AX, const uint16_t* dY2, const float* W1, const float* b1,
+                            const float* W2, float* gpart, int n, int F, int ldx, int C, int ldc, float p,
+                            uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0,
+                            hipStream_t st) {
+  constexpr int KP = KS * 16, KF = (KP + 31) / 32 * 32, CP = KC * 16, TR = TILE + 8;
+  const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KP + 8) + (size_t)HD * (CP + 8) + TILE * (KP + 8) +
+                                         TILE * (CP + 8) + (size_t)KF * TR + 64 * TR + 2 * (size_t)HD * TR) +
+                     sizeof(float) * HD;
+  if (lds > 160 * 1024) return -2;
+  (void)hipFuncSetAttribute((const void*)gcn_fused_bwd_kernel<KS, KC, HD>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((gcn_fused_bwd_kernel<KS, KC, HD>), dim3(gnn_fused_bwd_blocks(n)), dim3(HD * 2), lds, st,
+                     AX, dY2, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_fused_bwd_supported(int ldx, int HD, int ldc) {
+  const int KS = (ldx + 15) / 16, KC = (ldc + 15) / 16;
+  if (ldc % 8 || ldx % 8 || ldc > 64) return 0;
+  if (HD == 256) return (KS == 4 || KS == 7 || KS == 8) && (KC == 3 || KC == 4);
+  if (HD == 128) return ((KS == 7 || KS == 8 || KS == 4) && KC == 3) || (KS == 8 && KC == 4);
+  return 0;
+}
+
+// AX: [n][ldx] bf16 with the ones column at F (ldx covers F + 1); dY2: [n][ldc] bf16.
+// gpart: [gnn_fused_bwd_blocks(n)][HD][gnn_fused_bwd_width(ldx)] fp32.
+// Returns -1 when no compiled variant covers the shape.
+extern "C" int gnn_launch_fused_bwd(const void* AX, const void* dY2, const float* W1, const float* b1,
+                                    const float* W2, float* gpart, int n, int F, int ldx, int HD, int C,
+                                    int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t row0,
+                                    hipStream_t st) {
+  if (C > 64 || ldc % 8 || ldx % 8 || ldc > 64 || F + 1 > ldx) return -3;
+  const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
+  const int KS = (ldx + 15) / 16, KC = (ldc + 15) / 16;
+  auto* ax = (const uint16_t*)AX;
+  auto* dy = (const uint16_t*)dY2;
+#define FB(ks, kc, hd) if (KS == ks && KC == kc && HD == hd) return fused_bwd_launch<ks, kc, hd>(ax, dy, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, st);
+  FB(7, 3, 256) FB(7, 4, 256) FB(8, 3, 256) FB(8, 4, 256) FB(4, 3, 256) FB(4, 4, 256)
+  FB(7, 3, 128) FB(8, 3, 128) FB(4, 3, 128) FB(8, 4, 128)
+#undef FB
   return -1;
 }

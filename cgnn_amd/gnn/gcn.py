@@ -144,6 +144,11 @@ class GCNTrainer:
         # fused MFMA dense kernels (gnn_dense.hip); shapes they do not cover fall back to
         # hipBLASLt GEMMs + the standalone epilogue kernels
         self.fused = bool(fused) and hidden % 32 == 0 and self.C <= 64
+        # fully fused backward (H1 recomputed, weight gradients in the same pass): H1 is
+        # then never stored and the split-K GEMMs are not needed
+        self.fused_bwd = (self.fused and dev.type == "cuda" and
+                          ops.fused_bwd_supported(self.ldx, hidden, self.ldc))
+        self._gpart = None
 
     # ------------------------------------------------------------------ passes
     def _all_gather(self, out, inp):
@@ -156,7 +161,8 @@ class GCNTrainer:
         H1 = self.H1[:n]
         p = self.p if train else 0.0
         self.W2b[:, :C] = self.W2.to(torch.bfloat16)
-        if not (self.fused and ops.dense_fwd(self.AX, self.W1, self.b1, self.W2, self.dinv, H1,
+        if not (self.fused and ops.dense_fwd(self.AX, self.W1, self.b1, self.W2, self.dinv,
+                                             None if self.fused_bwd else H1,
                                              self.Z2loc[:n], F, p, self.key, self.epoch, self.r0)):
             W1b = self.W1.to(torch.bfloat16)
             if self.AX.is_cuda:
@@ -177,8 +183,17 @@ class GCNTrainer:
         n, F, C = self.nloc, self.F, self.C
         self._all_gather(self.G, self.Gloc)
         ops.spmm(self.rowptr, self.col, self.G, C, rscale=self.dinv, out=self.dY2)
-        self.gW2.copy_(_tsgemm(self.H1, self.dY2)[:, :C])
         self.gb2.copy_(stats[4:4 + C])
+        if self.fused_bwd:
+            gW1, gb1, gW2, self._gpart = ops.fused_bwd(self.AX, self.dY2, self.W1, self.b1, self.W2, n, F,
+                                                       self.p, self.key, self.epoch, self.r0, self._gpart)
+            self.gW1.copy_(gW1)
+            self.gb1.copy_(gb1)
+            self.gW2.copy_(gW2)
+            if self.world > 1:
+                torch.distributed.all_reduce(self.grads)
+            return
+        self.gW2.copy_(_tsgemm(self.H1, self.dY2)[:, :C])
         dH1 = self.dH1[:n]
         if not (self.fused and ops.dense_bwd(self.dY2, self.W2, self.H1, dH1, self.p)):
             if dH1.is_cuda:

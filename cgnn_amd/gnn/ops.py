@@ -127,12 +127,14 @@ def bias_relu_dropout_(H, bias, F, p, key, step, row0=0):
 
 
 def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step, row0=0):
-    """H1 = dropout(relu(AX[:, :F] W1 + b1)), Z2 = dinv * (H1 W2) (fused MFMA kernel on GPU)."""
-    n = H1.shape[0]
+    """H1 = dropout(relu(AX[:, :F] W1 + b1)), Z2 = dinv * (H1 W2) (fused MFMA kernel on GPU).
+    ``H1=None`` (GPU only): H1 is not stored -- the fused backward recomputes it."""
+    n = Z2.shape[0]
     HD, C = W1.shape[1], W2.shape[1]
     if AX.is_cuda:
         rc = native.hip().gnn_dense_fwd(AX.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
-                                        dinv.data_ptr(), H1.data_ptr(), Z2.data_ptr(), n, F, AX.shape[1],
+                                        dinv.data_ptr(), H1.data_ptr() if H1 is not None else 0,
+                                        Z2.data_ptr(), n, F, AX.shape[1],
                                         HD, C, Z2.shape[1], float(p), int(key[0]), int(key[1]), int(step),
                                         int(row0), _st(AX))
         if rc == 0:
@@ -163,6 +165,30 @@ def dense_bwd(dY2, W2, H1, dP1, p):
     g = dY2[:n, :C].float() @ W2.to(torch.bfloat16).float().t()
     dP1.copy_(torch.where(H1[:n].float() > 0, g / (1 - p), torch.zeros_like(g)).to(torch.bfloat16))
     return True
+
+
+def fused_bwd_supported(ldx, hidden, ldc):
+    return bool(native.hip().gnn_fused_bwd_supported(int(ldx), int(hidden), int(ldc)))
+
+
+def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None):
+    """Fused GCN dense backward (GPU): recomputes H1 from AX, then
+    dP1 = (dY2 W2^T) * [H1 > 0] / (1-p) and the weight gradients in one pass.
+    Returns (gW1 [F, HD], gb1 [HD], gW2 [HD, C], gpart)."""
+    hip = native.hip()
+    HD, C = W1.shape[1], W2.shape[1]
+    ldx = AX.shape[1]
+    nb, width = hip.gnn_fused_bwd_blocks(n), hip.gnn_fused_bwd_width(ldx)
+    if gpart is None or gpart.shape != (nb, HD, width):
+        gpart = torch.empty(nb, HD, width, dtype=torch.float32, device=AX.device)
+    rc = hip.gnn_fused_bwd(AX.data_ptr(), dY2.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
+                           gpart.data_ptr(), n, F, ldx, HD, C, dY2.shape[1], float(p), int(key[0]), int(key[1]),
+                           int(step), int(row0), _st(AX))
+    if rc != 0:
+        raise RuntimeError("gnn_fused_bwd failed (%d)" % rc)
+    g = gpart.sum(0)                     # fixed-order reduction over the block slabs
+    kf = width - 64
+    return g[:, :F].t(), g[:, F], g[:, kf:kf + C], gpart
 
 
 def relu_dropout_bwd_(dH, H, p):

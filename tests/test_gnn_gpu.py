@@ -132,3 +132,43 @@ def test_gcn_learns_products_shape_small():
         tr.train_step()
     res = tr.evaluate()
     assert res["val_acc"] > 0.3, res
+
+
+@pytest.mark.parametrize("HD,p,row0", [(256, 0.5, 0), (256, 0.0, 0), (128, 0.5, 4096)])
+def test_fused_backward_matches_reference(HD, p, row0):
+    """Fused dense backward (H1 recomputed from AX, weight gradients contracted over the
+    rows in the same pass) vs the unfused math on CPU with the same dropout mask."""
+    torch.manual_seed(3)
+    n, F, C = 1000, 100, 47
+    ldx, ldc = 104, 48
+    AX = torch.zeros(n, ldx)
+    AX[:, :F] = torch.randn(n, F) * 0.5
+    AX[:, F] = 1.0                                   # ones column -> gb1
+    AX = AX.to(torch.bfloat16)
+    dY2 = torch.zeros(n, ldc)
+    dY2[:, :C] = torch.randn(n, C) * 0.1
+    dY2 = dY2.to(torch.bfloat16)
+    W1 = torch.randn(F, HD) * 0.1
+    b1 = torch.randn(HD) * 0.1
+    W2 = torch.randn(HD, C) * 0.1
+    key, step = (123, 456), 7
+    assert ops.fused_bwd_supported(ldx, HD, ldc)
+    gW1, gb1, gW2, _ = ops.fused_bwd(AX.cuda(), dY2.cuda(), W1.cuda(), b1.cuda(), W2.cuda(), n, F, p, key, step,
+                                     row0)
+    # reference: same bf16 roundings as the kernel (operands, H1 and dP1 images)
+    P1 = AX[:, :F].float() @ W1.to(torch.bfloat16).float() + b1
+    H1 = torch.relu(P1)
+    if p > 0:
+        keep = ops.dropout_keep_mask(n, HD, p, key, step, row0)
+        H1 = torch.where(keep, H1 / (1 - p), torch.zeros_like(H1))
+    dH = dY2[:, :C].float() @ W2.to(torch.bfloat16).float().t()
+    dP1 = torch.where(H1 > 0, dH / (1 - p), torch.zeros_like(dH))
+    H1b, dP1b = H1.to(torch.bfloat16).double(), dP1.to(torch.bfloat16).double()
+    rW1 = AX[:, :F].double().t() @ dP1b
+    rb1 = dP1b.sum(0)
+    rW2 = H1b.t() @ dY2[:, :C].double()
+    for got, ref in ((gW1, rW1), (gb1, rb1), (gW2, rW2)):
+        got = got.double().cpu()
+        scale = ref.abs().max().item()
+        np.testing.assert_allclose(got.numpy(), ref.numpy(), atol=2e-2 * scale, rtol=0)
+        assert (got - ref).abs().mean().item() < 2e-3 * scale
