@@ -128,6 +128,11 @@ class GCNTrainer:
         n = self.nloc
         self.npad = (n + CHUNK - 1) // CHUNK * CHUNK
         self.AX = torch.zeros(self.npad, self.ldx, **bf)
+        # multi-GPU: the layer-1 aggregation of the NEXT epoch is computed into a second
+        # buffer while the backward all-gather is in flight (it does not depend on the
+        # parameters), then the buffers swap; every epoch still performs its own SpMM
+        self.AX_next = torch.zeros_like(self.AX) if self.world > 1 else None
+        self._ax_ready = False
         self.H1 = torch.zeros(self.npad, hidden, **bf)
         self.dH1 = torch.zeros(self.npad, hidden, **bf)
         self.W2b = torch.zeros(hidden, self.ldc, **bf)
@@ -155,9 +160,14 @@ class GCNTrainer:
         if self.world > 1:
             torch.distributed.all_gather_into_tensor(out, inp)
 
+    def _aggregate_features(self, out):
+        ops.spmm(self.rowptr, self.col, self.Xs, self.F, rscale=self.dinv, out=out, unit_col=self.F)
+
     def forward(self, train: bool):
         n, F, C = self.nloc, self.F, self.C
-        ops.spmm(self.rowptr, self.col, self.Xs, F, rscale=self.dinv, out=self.AX, unit_col=F)
+        if not self._ax_ready:
+            self._aggregate_features(self.AX)
+        self._ax_ready = False
         H1 = self.H1[:n]
         p = self.p if train else 0.0
         self.W2b[:, :C] = self.W2.to(torch.bfloat16)
@@ -181,7 +191,12 @@ class GCNTrainer:
 
     def backward(self, stats):
         n, F, C = self.nloc, self.F, self.C
-        self._all_gather(self.G, self.Gloc)
+        if self.world > 1:
+            work = torch.distributed.all_gather_into_tensor(self.G, self.Gloc, async_op=True)
+            self._aggregate_features(self.AX_next)     # overlaps the all-gather
+            work.wait()
+        else:
+            self._all_gather(self.G, self.Gloc)
         ops.spmm(self.rowptr, self.col, self.G, C, rscale=self.dinv, out=self.dY2)
         self.gb2.copy_(stats[4:4 + C])
         if self.fused_bwd:
@@ -211,6 +226,9 @@ class GCNTrainer:
         stats = self.forward(train=True)
         self.backward(stats)
         ops.adam_(self.params, self.grads, self.m, self.v, self.lr, self.step_t, wd=self.wd)
+        if self.AX_next is not None:
+            self.AX, self.AX_next = self.AX_next, self.AX
+            self._ax_ready = True
         self.last_stats = stats
         self.epoch += 1
         return stats
