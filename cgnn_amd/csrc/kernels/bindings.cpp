@@ -22,6 +22,7 @@ int cgnn_launch_mmd_mfma(int, int, const float*, const float*, const float*, con
 int cgnn_gen_supported_h(int);
 int cgnn_gen_bwd_blocks(int);
 size_t cgnn_gen_bwd_lds(int, int, int, int);
+int cgnn_read_stamps(unsigned long long*);
 int cgnn_launch_mmd(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
                     float, hipStream_t);
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
@@ -112,6 +113,14 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gen_supported_h", &cgnn_gen_supported_h);
   m.def("gen_bwd_blocks", &cgnn_gen_bwd_blocks);
   m.def("gen_bwd_lds", &cgnn_gen_bwd_lds);
+  m.def("read_stamps", []() {
+    unsigned long long v[16] = {0};
+    const int rc = cgnn_read_stamps(v);
+    py::list out;
+    if (rc == 0)
+      for (int k = 0; k < 16; ++k) out.append(v[k]);
+    return out;
+  });
 
   m.def("mmd", [](int mode, int D, uint64_t xhat, uint64_t data, uint64_t gp, uint64_t lp, int N, int R,
                   int row_tiles, int n_chunks, int tpc, float gscale, uint64_t st) {

@@ -253,10 +253,12 @@ class GCNTrainer:
 
 
 def smoke_step():
-    """One tiny GCN training step on cuda:0 (used by __graft_entry__.smoke)."""
+    """Two tiny GCN training steps on cuda:0 through the flagship fused kernels (a
+    0.1 % ogbn-products-shaped graph, hidden 256; used by __graft_entry__.smoke)."""
     from .data import synthetic
-    g = synthetic("cora", seed=0, device="cuda:0")
-    tr = GCNTrainer(g, hidden=64, rank=0, world=1)
+    g = synthetic("ogbn-products", seed=0, device="cuda:0", scale=0.001)
+    tr = GCNTrainer(g, hidden=256, rank=0, world=1)
+    assert tr.fused and tr.fused_bwd
     tr.train_step()
     tr.train_step()
     res = tr.evaluate()
