@@ -288,60 +288,73 @@ py::list sample_neighbors(py::array_t<i64, py::array::c_style | py::array::force
                           std::vector<int> fanouts, uint64_t seed) {
   const i64* rowptr = rowptr_a.data();
   const i32* col = col_a.data();
+  struct Block { std::vector<i64> rp; std::vector<i32> col; std::vector<i64> nodes; };
+  std::vector<Block> blocks(fanouts.size());
   std::vector<i64> frontier(seeds_a.data(), seeds_a.data() + seeds_a.size());
-  py::list out;
-  for (size_t l = 0; l < fanouts.size(); ++l) {
-    const int fo = fanouts[l];
-    const i64 nd = (i64)frontier.size();
-    std::vector<i64> cnt(nd + 1, 0);
-    for (i64 i = 0; i < nd; ++i) {
-      const i64 v = frontier[i];
-      const i64 deg = rowptr[v + 1] - rowptr[v];
-      cnt[i + 1] = fo < 0 ? deg : std::min<i64>(deg, fo);
-    }
-    for (i64 i = 0; i < nd; ++i) cnt[i + 1] += cnt[i];
-    std::vector<i64> picked(cnt[nd]);
+  {
+    // the sampling itself runs without the GIL (a data-loader thread overlaps it
+    // with the GPU step of the previous batch)
+    py::gil_scoped_release nogil;
+    for (size_t l = 0; l < fanouts.size(); ++l) {
+      const int fo = fanouts[l];
+      const i64 nd = (i64)frontier.size();
+      std::vector<i64>& cnt = blocks[l].rp;
+      cnt.assign(nd + 1, 0);
+      for (i64 i = 0; i < nd; ++i) {
+        const i64 v = frontier[i];
+        const i64 deg = rowptr[v + 1] - rowptr[v];
+        cnt[i + 1] = fo < 0 ? deg : std::min<i64>(deg, fo);
+      }
+      for (i64 i = 0; i < nd; ++i) cnt[i + 1] += cnt[i];
+      std::vector<i64> picked(cnt[nd]);
 #pragma omp parallel for schedule(dynamic, 256)
-    for (i64 i = 0; i < nd; ++i) {
-      const i64 v = frontier[i];
-      const i64 b = rowptr[v], deg = rowptr[v + 1] - b, k = cnt[i + 1] - cnt[i];
-      i64* dstp = picked.data() + cnt[i];
-      if (k == deg) {
-        for (i64 q = 0; q < k; ++q) dstp[q] = col[b + q];
-      } else {   // Floyd's algorithm: k distinct positions out of deg
-        uint64_t h = mix64(seed ^ mix64((uint64_t)v * 131 + l));
-        std::vector<i64> pos;
-        pos.reserve(k);
-        for (i64 j = deg - k; j < deg; ++j) {
-          h = mix64(h);
-          i64 t = (i64)(h % (uint64_t)(j + 1));
-          if (std::find(pos.begin(), pos.end(), t) != pos.end()) t = j;
-          pos.push_back(t);
+      for (i64 i = 0; i < nd; ++i) {
+        const i64 v = frontier[i];
+        const i64 b = rowptr[v], deg = rowptr[v + 1] - b, k = cnt[i + 1] - cnt[i];
+        i64* dstp = picked.data() + cnt[i];
+        if (k == deg) {
+          for (i64 q = 0; q < k; ++q) dstp[q] = col[b + q];
+        } else {   // Floyd's algorithm: k distinct positions out of deg
+          uint64_t h = mix64(seed ^ mix64((uint64_t)v * 131 + l));
+          std::vector<i64> pos;
+          pos.reserve(k);
+          for (i64 j = deg - k; j < deg; ++j) {
+            h = mix64(h);
+            i64 t = (i64)(h % (uint64_t)(j + 1));
+            if (std::find(pos.begin(), pos.end(), t) != pos.end()) t = j;
+            pos.push_back(t);
+          }
+          for (i64 q = 0; q < k; ++q) dstp[q] = col[b + pos[q]];
         }
-        for (i64 q = 0; q < k; ++q) dstp[q] = col[b + pos[q]];
       }
-    }
-    // relabel: destination nodes first, then new source nodes in first-seen order
-    std::vector<i64> nodes(frontier);
-    std::unordered_map<i64, i32> idx;
-    idx.reserve(frontier.size() * 2 + picked.size());
-    for (i64 i = 0; i < nd; ++i) idx.emplace(frontier[i], (i32)i);
-    py::array_t<i32> bcol(picked.size());
-    i32* bc = bcol.mutable_data();
-    for (size_t q = 0; q < picked.size(); ++q) {
-      auto it = idx.find(picked[q]);
-      if (it == idx.end()) {
-        it = idx.emplace(picked[q], (i32)nodes.size()).first;
-        nodes.push_back(picked[q]);
+      // relabel: destination nodes first, then new source nodes in first-seen order
+      std::vector<i64>& nodes = blocks[l].nodes;
+      nodes = frontier;
+      std::unordered_map<i64, i32> idx;
+      idx.reserve(frontier.size() * 2 + picked.size());
+      for (i64 i = 0; i < nd; ++i) idx.emplace(frontier[i], (i32)i);
+      std::vector<i32>& bc = blocks[l].col;
+      bc.resize(picked.size());
+      for (size_t q = 0; q < picked.size(); ++q) {
+        auto it = idx.find(picked[q]);
+        if (it == idx.end()) {
+          it = idx.emplace(picked[q], (i32)nodes.size()).first;
+          nodes.push_back(picked[q]);
+        }
+        bc[q] = it->second;
       }
-      bc[q] = it->second;
+      frontier = nodes;
     }
-    py::array_t<i64> brow(nd + 1);
-    std::copy(cnt.begin(), cnt.end(), brow.mutable_data());
-    py::array_t<i64> nodes_a(nodes.size());
-    std::copy(nodes.begin(), nodes.end(), nodes_a.mutable_data());
+  }
+  py::list out;
+  for (auto& b : blocks) {
+    py::array_t<i64> brow(b.rp.size());
+    std::copy(b.rp.begin(), b.rp.end(), brow.mutable_data());
+    py::array_t<i32> bcol(b.col.size());
+    std::copy(b.col.begin(), b.col.end(), bcol.mutable_data());
+    py::array_t<i64> nodes_a(b.nodes.size());
+    std::copy(b.nodes.begin(), b.nodes.end(), nodes_a.mutable_data());
     out.append(py::make_tuple(brow, bcol, nodes_a));
-    frontier.swap(nodes);
   }
   return out;
 }

@@ -1,0 +1,244 @@
+"""GraphSAGE (mean aggregator) on the HIP SpMM -- GNN track, not in the reference.
+
+Layer:  h_i' = act( W_self h_i + W_neigh mean_{j in N(i)} h_j + b )
+
+Two training modes:
+
+* **full graph** -- every layer aggregates over the whole CSR (A + I) with the
+  row scale 1/deg, like the GCN trainer;
+* **sampled mini-batches** -- the C++ neighbour sampler (``_rt.sample_neighbors``,
+  OpenMP, GIL released) draws a fan-out per layer for a batch of seed nodes and
+  returns one bipartite block per layer (destination nodes are a prefix of the
+  source nodes).  A background thread samples batch k+1 while the GPU trains on
+  batch k.
+
+The aggregation is the same CSR gather-sum kernel as the GCN (``spmm_kernel``);
+its backward is the transposed block SpMM, for which the transposed CSR is built
+on the device with a stable sort -- deterministic, no atomics.  Dense parts are
+hipBLASLt GEMMs through PyTorch autograd.
+"""
+from __future__ import annotations
+
+import math
+import queue
+import threading
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import native
+from . import ops
+from .data import GraphData
+
+
+def transpose_csr(rowptr: torch.Tensor, col: torch.Tensor, n_cols: int):
+    """CSR of the transpose (rows = former columns), deterministic (stable sort)."""
+    n_rows = rowptr.numel() - 1
+    rows = torch.repeat_interleave(torch.arange(n_rows, device=col.device, dtype=torch.int32),
+                                   (rowptr[1:] - rowptr[:-1]).long())
+    order = torch.sort(col.long(), stable=True).indices
+    col_t = rows[order].to(torch.int32)
+    counts = torch.bincount(col.long(), minlength=n_cols)
+    rp_t = torch.zeros(n_cols + 1, dtype=torch.int64, device=col.device)
+    rp_t[1:] = torch.cumsum(counts, 0)
+    return rp_t.to(torch.int32), col_t
+
+
+class Block:
+    """One bipartite aggregation block: ``n_dst`` destination rows over ``n_src``
+    source rows (the destinations are the first ``n_dst`` sources)."""
+
+    def __init__(self, rowptr, col, n_src, device):
+        self.rowptr = torch.as_tensor(np.asarray(rowptr), dtype=torch.int32).to(device)
+        self.col = torch.as_tensor(np.asarray(col), dtype=torch.int32).to(device)
+        self.n_dst = self.rowptr.numel() - 1
+        self.n_src = int(n_src)
+        deg = (self.rowptr[1:] - self.rowptr[:-1]).float()
+        self.inv_deg = torch.where(deg > 0, 1.0 / deg.clamp_min(1), torch.zeros_like(deg))
+        self._t = None
+
+    def transposed(self):
+        if self._t is None:
+            self._t = transpose_csr(self.rowptr, self.col, self.n_src)
+        return self._t
+
+
+class _MeanAggregate(torch.autograd.Function):
+    """agg[i] = inv_deg[i] * sum_{e in row i} h[col[e]]  (fp32, HIP SpMM on GPU)."""
+
+    @staticmethod
+    def forward(ctx, h, block: Block):
+        ctx.block = block
+        F = h.shape[1]
+        return ops.spmm(block.rowptr, block.col, h.contiguous(), F, rscale=block.inv_deg,
+                        out_dtype=torch.float32, ld_out=F)
+
+    @staticmethod
+    def backward(ctx, g):
+        b = ctx.block
+        rp_t, col_t = b.transposed()
+        gs = (g * b.inv_deg[:, None]).contiguous()
+        F = g.shape[1]
+        return ops.spmm(rp_t, col_t, gs, F, out_dtype=torch.float32, ld_out=F), None
+
+
+def mean_aggregate(h: torch.Tensor, block: Block) -> torch.Tensor:
+    if h.shape[1] % 8:
+        raise ValueError("feature width must be a multiple of 8 (pad the features)")
+    return _MeanAggregate.apply(h, block)
+
+
+class SAGE(torch.nn.Module):
+    def __init__(self, in_dim: int, hidden: int, out_dim: int, layers: int = 2, dropout: float = 0.5,
+                 seed: int = 0):
+        super().__init__()
+        g = torch.Generator().manual_seed(seed)
+        dims = [in_dim] + [hidden] * (layers - 1) + [out_dim]
+        self.w_self = torch.nn.ParameterList()
+        self.w_neigh = torch.nn.ParameterList()
+        self.bias = torch.nn.ParameterList()
+        for a, b in zip(dims[:-1], dims[1:]):
+            bound = math.sqrt(6.0 / (a + b))
+            self.w_self.append(torch.nn.Parameter((torch.rand(a, b, generator=g) * 2 - 1) * bound))
+            self.w_neigh.append(torch.nn.Parameter((torch.rand(a, b, generator=g) * 2 - 1) * bound))
+            self.bias.append(torch.nn.Parameter(torch.zeros(b)))
+        self.dropout = float(dropout)
+
+    def layer(self, k: int, h: torch.Tensor, block: Block, last: bool):
+        agg = mean_aggregate(h, block)
+        out = h[:block.n_dst] @ self.w_self[k] + agg @ self.w_neigh[k] + self.bias[k]
+        if not last:
+            out = torch.relu(out)
+            if self.training and self.dropout > 0:
+                out = torch.nn.functional.dropout(out, self.dropout)
+        return out
+
+    def forward(self, x: torch.Tensor, blocks: Sequence[Block]):
+        """``blocks`` ordered input layer first (the sampler's list reversed)."""
+        h = x
+        L = len(self.w_self)
+        for k in range(L):
+            h = self.layer(k, h, blocks[k], k == L - 1)
+            if k < L - 1 and h.shape[1] % 8:
+                h = torch.nn.functional.pad(h, (0, 8 - h.shape[1] % 8))
+        return h
+
+
+def _pad8(x: torch.Tensor) -> torch.Tensor:
+    F = x.shape[1]
+    return x if F % 8 == 0 else torch.nn.functional.pad(x, (0, 8 - F % 8))
+
+
+class SAGETrainer:
+    """Node classification with GraphSAGE; ``fanouts=None`` trains on the full graph."""
+
+    def __init__(self, g: GraphData, hidden: int = 256, layers: int = 2, dropout: float = 0.5,
+                 lr: float = 0.003, fanouts: Optional[List[int]] = (15, 10), batch_size: int = 1024,
+                 seed: int = 0, prefetch: bool = True, standardize: bool = True):
+        self.g = g
+        self.dev = g.rowptr.device
+        x = g.x.float()
+        if standardize:                       # column z-scores (standard preprocessing)
+            x = (x - x.mean(0)) / x.std(0).clamp_min(1e-6)
+        self.x = _pad8(x)
+        self.C = g.n_classes
+        F = self.x.shape[1]
+        # hidden width padded to a multiple of 8 (SpMM row alignment); output padded too
+        self.model = SAGE(F, hidden, self.C, layers, dropout, seed).to(self.dev)
+        self.model.w_self[0].data[g.n_features:] = 0
+        self.model.w_neigh[0].data[g.n_features:] = 0
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=lr)
+        self.fanouts = list(fanouts) if fanouts else None
+        self.layers = layers
+        self.batch_size = int(batch_size)
+        self.seed = int(seed)
+        self.train_idx = torch.nonzero(g.mask.cpu() == 1).flatten().numpy()
+        self._rp64 = g.rowptr.cpu().numpy().astype(np.int64)
+        self._col = g.col.cpu().numpy()
+        self._full = None
+        self.prefetch = bool(prefetch)
+        self.epoch = 0
+
+    # ----------------------------------------------------------- blocks
+    def full_blocks(self):
+        if self._full is None:
+            b = Block(self.g.rowptr.cpu().numpy(), self.g.col.cpu().numpy(), self.g.n, self.dev)
+            self._full = [b] * self.layers
+        return self._full
+
+    def sample(self, seeds: np.ndarray, salt: int):
+        raw = native.rt().sample_neighbors(self._rp64, self._col, seeds.astype(np.int64),
+                                           list(self.fanouts[:self.layers]), self.seed * 1000003 + salt)
+        return raw
+
+    def _to_device(self, raw):
+        blocks = []
+        for rp, col, nodes in raw:
+            blocks.append(Block(rp, col, len(nodes), self.dev))
+        nodes_in = torch.as_tensor(np.asarray(raw[-1][2]), device=self.dev)
+        return blocks[::-1], nodes_in
+
+    # ----------------------------------------------------------- training
+    def _step(self, blocks, nodes_in, seeds_t):
+        self.model.train()
+        out = self.model(self.x[nodes_in], blocks)
+        loss = torch.nn.functional.cross_entropy(out[:, :self.C], self.g.y[seeds_t].long())
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
+
+    def train_epoch(self):
+        """One epoch; returns the mean training loss (one host sync at the end)."""
+        if self.fanouts is None:
+            blocks = self.full_blocks()
+            self.model.train()
+            out = self.model(self.x, blocks)
+            tr = self.g.mask == 1
+            loss = torch.nn.functional.cross_entropy(out[tr][:, :self.C], self.g.y[tr].long())
+            self.opt.zero_grad(set_to_none=True)
+            loss.backward()
+            self.opt.step()
+            self.epoch += 1
+            return float(loss)
+        rng = np.random.default_rng(self.seed + self.epoch)
+        perm = rng.permutation(self.train_idx)
+        batches = [perm[i:i + self.batch_size] for i in range(0, len(perm), self.batch_size)]
+        losses = []
+        if self.prefetch and len(batches) > 1:
+            q: "queue.Queue" = queue.Queue(maxsize=2)
+
+            def producer():
+                for k, b in enumerate(batches):
+                    q.put((b, self.sample(b, self.epoch * 100003 + k)))
+                q.put(None)
+
+            th = threading.Thread(target=producer, daemon=True)
+            th.start()
+            while True:
+                item = q.get()
+                if item is None:
+                    break
+                seeds, raw = item
+                blocks, nodes_in = self._to_device(raw)
+                losses.append(self._step(blocks, nodes_in, torch.as_tensor(seeds, device=self.dev)))
+            th.join()
+        else:
+            for k, b in enumerate(batches):
+                blocks, nodes_in = self._to_device(self.sample(b, self.epoch * 100003 + k))
+                losses.append(self._step(blocks, nodes_in, torch.as_tensor(b, device=self.dev)))
+        self.epoch += 1
+        return float(torch.stack(losses).mean())
+
+    @torch.no_grad()
+    def evaluate(self):
+        """Full-graph (layer-wise exact) inference; accuracies per split."""
+        self.model.eval()
+        out = self.model(self.x, self.full_blocks())[:, :self.C]
+        pred = out.argmax(1)
+        res = {}
+        for name, k in (("train_acc", 1), ("val_acc", 2), ("test_acc", 3)):
+            m = self.g.mask == k
+            res[name] = float((pred[m] == self.g.y[m].long()).float().mean()) if bool(m.any()) else float("nan")
+        return res
