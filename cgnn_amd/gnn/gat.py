@@ -1,0 +1,190 @@
+"""Graph attention networks (GAT) -- GNN track, not in the reference.
+
+Attention aggregation over the CSR of A + I (multi-head):
+
+    e_ijk = LeakyReLU(a_dst_k . Wh_ik + a_src_k . Wh_jk),  alpha = softmax_j(e),
+    out_ik = sum_j alpha_ijk Wh_jk
+
+On a GPU the aggregation runs on three HIP kernels (``gnn_gat.hip``): a fused
+forward with an online softmax (edge scores never stored; per-(row, head)
+log-sum-exp kept), a row-wise backward doing the SDDMM ``<dout_i, Wh_j>`` and the
+softmax / LeakyReLU derivative, and a column-wise backward over the transposed
+CSR (stable device sort + edge permutation) that gathers ``dWh`` and the source
+score gradient -- no atomics anywhere.  The projections ``Wh = h W`` and the
+scores ``s = <Wh, a>`` are PyTorch ops (hipBLASLt), so autograd chains through.
+On the CPU the same math is written with PyTorch index ops (the reference the
+GPU kernels are tested against).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from .. import native
+from .data import GraphData
+from .sage import transpose_csr
+
+
+def _st(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+class GraphCSR:
+    """CSR (A + I) plus its lazily built transpose with the edge permutation."""
+
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n: int):
+        self.rowptr, self.col, self.n = rowptr.contiguous(), col.contiguous(), int(n)
+        self._t = None
+        self._rows = None
+
+    @property
+    def nnz(self):
+        return int(self.col.numel())
+
+    def transposed(self):
+        if self._t is None:
+            self._t = transpose_csr(self.rowptr, self.col, self.n, with_perm=True)
+        return self._t
+
+    def edge_rows(self):
+        if self._rows is None:
+            counts = (self.rowptr[1:] - self.rowptr[:-1]).long()
+            self._rows = torch.repeat_interleave(torch.arange(self.n, device=self.col.device), counts)
+        return self._rows
+
+
+class _GATAggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int):
+        hip = native.hip()
+        n = g.n
+        Wh, s_src, s_dst = Wh.contiguous(), s_src.contiguous(), s_dst.contiguous()
+        out = torch.empty(n, K * Fh, dtype=torch.float32, device=Wh.device)
+        lse = torch.empty(n, K, dtype=torch.float32, device=Wh.device)
+        hip.gnn_gat_fwd(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(),
+                        out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Wh))
+        ctx.save_for_backward(Wh, s_src, s_dst, out, lse)
+        ctx.g, ctx.K, ctx.Fh = g, K, Fh
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        hip = native.hip()
+        Wh, s_src, s_dst, out, lse = ctx.saved_tensors
+        g, K, Fh = ctx.g, ctx.K, ctx.Fh
+        n, dev = g.n, Wh.device
+        dout = dout.contiguous().float()
+        alpha_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+        dsc_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+        ds_dst = torch.empty(n, K, dtype=torch.float32, device=dev)
+        hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(),
+                            s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(),
+                            dsc_e.data_ptr(), ds_dst.data_ptr(), n, K, Fh, _st(Wh))
+        rp_t, col_t, perm = g.transposed()
+        dWh = torch.empty_like(Wh)
+        ds_src = torch.empty(n, K, dtype=torch.float32, device=dev)
+        hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
+                            dsc_e.data_ptr(), dout.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), n, K, Fh, _st(Wh))
+        return dWh, ds_src, ds_dst, None, None, None
+
+
+def _gat_aggregate_torch(Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int):
+    rows = g.edge_rows()
+    cols = g.col.long()
+    raw = s_dst[rows] + s_src[cols]                                   # [nnz, K]
+    e = torch.nn.functional.leaky_relu(raw, 0.2)
+    m = torch.full((g.n, K), -math.inf, dtype=e.dtype, device=e.device)
+    m = m.scatter_reduce(0, rows[:, None].expand(-1, K), e, "amax", include_self=True)
+    w = torch.exp(e - m[rows].detach())
+    den = torch.zeros(g.n, K, dtype=e.dtype, device=e.device).index_add(0, rows, w)
+    alpha = w / den[rows]
+    msg = alpha[:, :, None] * Wh.view(-1, K, Fh)[cols]
+    out = torch.zeros(g.n, K, Fh, dtype=Wh.dtype, device=Wh.device).index_add(0, rows, msg)
+    return out.view(g.n, K * Fh)
+
+
+def gat_aggregate(Wh: torch.Tensor, s_src: torch.Tensor, s_dst: torch.Tensor, g: GraphCSR, K: int, Fh: int):
+    """Multi-head attention aggregation; Wh [n, K*Fh] fp32, s_* [n, K]."""
+    if Wh.is_cuda:
+        if Fh % 8 or (Fh // 8) & (Fh // 8 - 1) or K * Fh > 512:
+            raise ValueError("HIP GAT needs Fh = 8 * 2^m and K * Fh <= 512")
+        return _GATAggregate.apply(Wh.float(), s_src.float(), s_dst.float(), g, K, Fh)
+    return _gat_aggregate_torch(Wh, s_src, s_dst, g, K, Fh)
+
+
+class GATLayer(torch.nn.Module):
+    def __init__(self, in_dim, heads, head_dim, generator=None):
+        super().__init__()
+        self.K, self.Fh = heads, head_dim
+        bound = math.sqrt(6.0 / (in_dim + heads * head_dim))
+        self.W = torch.nn.Parameter((torch.rand(in_dim, heads * head_dim, generator=generator) * 2 - 1) * bound)
+        ab = math.sqrt(6.0 / (head_dim + 1))
+        self.a_src = torch.nn.Parameter((torch.rand(heads, head_dim, generator=generator) * 2 - 1) * ab)
+        self.a_dst = torch.nn.Parameter((torch.rand(heads, head_dim, generator=generator) * 2 - 1) * ab)
+        self.bias = torch.nn.Parameter(torch.zeros(heads * head_dim))
+
+    def forward(self, h, g: GraphCSR):
+        Wh = h @ self.W
+        Whk = Wh.view(-1, self.K, self.Fh)
+        s_src = (Whk * self.a_src).sum(-1)
+        s_dst = (Whk * self.a_dst).sum(-1)
+        return gat_aggregate(Wh, s_src, s_dst, g, self.K, self.Fh) + self.bias
+
+
+class GAT(torch.nn.Module):
+    """2-layer GAT: K heads of width Fh (concatenated, ELU), then one output head
+    whose width is the class count padded to a power-of-two multiple of 8."""
+
+    def __init__(self, in_dim, n_classes, heads=8, head_dim=32, dropout=0.5, seed=0):
+        super().__init__()
+        gen = torch.Generator().manual_seed(seed)
+        out_w = 8
+        while out_w < n_classes:
+            out_w *= 2
+        self.C = n_classes
+        self.l1 = GATLayer(in_dim, heads, head_dim, gen)
+        self.l2 = GATLayer(heads * head_dim, 1, out_w, gen)
+        self.dropout = float(dropout)
+
+    def forward(self, x, g: GraphCSR):
+        h = torch.nn.functional.elu(self.l1(x, g))
+        if self.training and self.dropout > 0:
+            h = torch.nn.functional.dropout(h, self.dropout)
+        return self.l2(h, g)[:, :self.C]
+
+
+class GATTrainer:
+    """Full-graph GAT node classification (Adam, cross-entropy on the train split)."""
+
+    def __init__(self, gd: GraphData, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True):
+        self.gd = gd
+        self.dev = gd.rowptr.device
+        x = gd.x.float()
+        if standardize:
+            x = (x - x.mean(0)) / x.std(0).clamp_min(1e-6)
+        self.x = x
+        self.g = GraphCSR(gd.rowptr, gd.col, gd.n)
+        self.model = GAT(x.shape[1], gd.n_classes, heads, head_dim, dropout, seed).to(self.dev)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=lr)
+        self.tr = gd.mask == 1
+
+    def train_step(self):
+        self.model.train()
+        out = self.model(self.x, self.g)
+        loss = torch.nn.functional.cross_entropy(out[self.tr], self.gd.y[self.tr].long())
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
+
+    @torch.no_grad()
+    def evaluate(self):
+        self.model.eval()
+        pred = self.model(self.x, self.g).argmax(1)
+        res = {}
+        for name, k in (("train_acc", 1), ("val_acc", 2), ("test_acc", 3)):
+            m = self.gd.mask == k
+            res[name] = float((pred[m] == self.gd.y[m].long()).float().mean()) if bool(m.any()) else float("nan")
+        return res

@@ -32,8 +32,9 @@ from . import ops
 from .data import GraphData
 
 
-def transpose_csr(rowptr: torch.Tensor, col: torch.Tensor, n_cols: int):
-    """CSR of the transpose (rows = former columns), deterministic (stable sort)."""
+def transpose_csr(rowptr: torch.Tensor, col: torch.Tensor, n_cols: int, with_perm: bool = False):
+    """CSR of the transpose (rows = former columns), deterministic (stable sort);
+    ``with_perm`` also returns, per transposed edge, the original edge index."""
     n_rows = rowptr.numel() - 1
     rows = torch.repeat_interleave(torch.arange(n_rows, device=col.device, dtype=torch.int32),
                                    (rowptr[1:] - rowptr[:-1]).long())
@@ -42,6 +43,8 @@ def transpose_csr(rowptr: torch.Tensor, col: torch.Tensor, n_cols: int):
     counts = torch.bincount(col.long(), minlength=n_cols)
     rp_t = torch.zeros(n_cols + 1, dtype=torch.int64, device=col.device)
     rp_t[1:] = torch.cumsum(counts, 0)
+    if with_perm:
+        return rp_t.to(torch.int32), col_t, order.to(torch.int32)
     return rp_t.to(torch.int32), col_t
 
 
