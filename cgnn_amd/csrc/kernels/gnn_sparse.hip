@@ -196,12 +196,17 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
     const int oa = __shfl_xor(amax, off, 64);
     if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
   }
+  float ex[8];
   float se = 0.f;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) se += (f0 + q < C) ? __expf(lg[q] - mx) : 0.f;
+  for (int q = 0; q < 8; ++q) {
+    ex[q] = (f0 + q < C) ? __expf(lg[q] - mx) : 0.f;   // reused for the softmax below
+    se += ex[q];
+  }
 #pragma unroll
   for (int off = 1; off < L; off <<= 1) se += __shfl_xor(se, off, 64);
   const float lse = mx + __logf(se);
+  const float inv_se = 1.f / se;
   const int y = rv ? labels[row] : -1;
   const int split = rv ? (int)mask[row] : 0;
   float my_loss = 0.f;
@@ -213,7 +218,7 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int c = f0 + q;
-    dl[q] = (rv && split == 1 && c < C) ? (__expf(lg[q] - lse) - (c == y ? 1.f : 0.f)) * inv_count : 0.f;
+    dl[q] = (rv && split == 1 && c < C) ? (ex[q] * inv_se - (c == y ? 1.f : 0.f)) * inv_count : 0.f;
   }
   if (mode == 0 && rv && f0 < ld) {
     float gq[8];

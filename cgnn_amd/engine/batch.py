@@ -29,25 +29,27 @@ def padded_dim(d: int) -> int:
     raise ValueError("CGNN device path supports at most %d variables (got %d)" % (SUPPORTED_D[-1], d))
 
 
-def mmd_geometry(N: int, R: int):
+def mmd_geometry(N: int, R: int = 0):
+    """(row_tiles, n_chunks, tiles_per_chunk) of the vector MMD kernel.  A function
+    of N only -- never of the batch size R -- so the fixed-order sums (and hence every
+    score) are bitwise independent of how jobs are batched or sharded over GPUs:
+    one 256-column tile per chunk."""
     row_tiles = (N + MMD_TILE - 1) // MMD_TILE
     ct = 2 * row_tiles
-    n_chunks = min(ct, max(1, math.ceil(TARGET_WGS / (row_tiles * R))))
-    tpc = math.ceil(ct / n_chunks)
-    n_chunks = math.ceil(ct / tpc)
-    return row_tiles, n_chunks, tpc
+    return row_tiles, ct, 1
 
 
 MFMA_ROWS = 128     # generated rows per workgroup of the matrix-core MMD
 MFMA_TILE = 32      # joint columns per LDS tile
 
 
-def mmd_mfma_geometry(N: int, R: int):
-    """(row_blocks, n_chunks, tiles_per_chunk) of the matrix-core MMD: enough
-    column chunks that the launch has >= ~1024 workgroups."""
+def mmd_mfma_geometry(N: int, R: int = 0):
+    """(row_blocks, n_chunks, tiles_per_chunk) of the matrix-core MMD; like
+    ``mmd_geometry`` a function of N only (batch-independent sums): small N get a
+    few column chunks so that one model still spreads over >= 8 workgroups."""
     rb = (N + MFMA_ROWS - 1) // MFMA_ROWS
     ct = 2 * ((N + MFMA_TILE - 1) // MFMA_TILE)
-    n_chunks = min(ct, max(1, math.ceil(1024 / (rb * R))))
+    n_chunks = min(ct, max(1, math.ceil(8 / rb)))
     tpc = math.ceil(ct / n_chunks)
     n_chunks = math.ceil(ct / tpc)
     return rb, n_chunks, tpc
