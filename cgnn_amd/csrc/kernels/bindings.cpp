@@ -30,7 +30,7 @@ int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, 
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
-                        const float*, int, int, int, int, int, int, float*, hipStream_t);
+                        const float*, int, int, int, int, int, int, int, float*, hipStream_t);
 int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
                      int, float, float, float, float, int, hipStream_t);
 int cgnn_launch_init(float*, float*, float*, const int*, int, int, const uint32_t*, float, int,
@@ -149,9 +149,10 @@ PYBIND11_MODULE(_hip, m) {
                             off, N, D, H, R, S(st)), "gen_fwd");
   });
   m.def("gen_bwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t xhat, uint64_t noise, int NS,
-                      uint64_t gradp, int nch, int R, int N, int D, int H, int max_in, uint64_t gpart, uint64_t st) {
+                      uint64_t gradp, int nch, int R, int N, int D, int Dt, int H, int max_in, uint64_t gpart,
+                      uint64_t st) {
     chk(cgnn_launch_gen_bwd(Pt<const int>(prog), ps, Pt<const float>(params), P, Pt<const float>(xhat),
-                            Pt<const float>(noise), NS, Pt<const float>(gradp), nch, R, N, D, H, max_in,
+                            Pt<const float>(noise), NS, Pt<const float>(gradp), nch, R, N, D, Dt, H, max_in,
                             Pt<float>(gpart), S(st)), "gen_bwd");
   });
   m.def("adam", [](uint64_t params, uint64_t mm, uint64_t vv, uint64_t gpart, int G, uint64_t prog, int ps, int P,

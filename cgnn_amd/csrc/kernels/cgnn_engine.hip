@@ -28,7 +28,7 @@ int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, 
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
-                        const float*, int, int, int, int, int, int, float*, hipStream_t);
+                        const float*, int, int, int, int, int, int, int, float*, hipStream_t);
 int cgnn_gen_bwd_blocks(int);
 int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
                      int, float, float, float, float, int, hipStream_t);
@@ -154,7 +154,8 @@ class Engine {
       check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 0,
                                       b_.loss_hist, c_.hist_stride, b_.step, off, c_.R, st_), "finalize");
     check(cgnn_launch_gen_bwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.xhat, b_.noise, c_.NS, b_.gradp,
-                              grad_chunks(), c_.R, c_.N, c_.D, c_.H, c_.max_in, b_.gpart, st_), "gen_bwd");
+                              grad_chunks(), c_.R, c_.N, c_.D, c_.d_true, c_.H, c_.max_in, b_.gpart, st_),
+          "gen_bwd");
     check(cgnn_launch_adam(b_.params, b_.m, b_.v, b_.gpart, G_, b_.prog, c_.prog_stride, c_.P, b_.step,
                            off, c_.lr, c_.beta1, c_.beta2, c_.eps, c_.R, st_), "adam");
   }

@@ -306,48 +306,51 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
 
 // ============================================================================
 // K2: generator backward.  grid = (G, R), block = BS = 128 samples (2 waves).
-// LDS-resident per block: the DAG program, the samples' generated values s_x
-// and running gradients s_dx ([D][BS]).  Per node (reverse topological order):
+// LDS-resident per block: the samples' generated values s_x and running
+// gradients s_dx ([Dt][BS], Dt = unpadded variable count).  Per node (reverse
+// topological order):
 //   compute  each thread rebuilds its sample's node inputs and pre-activations
-//            (packed fp32), stores the input row s_in[s] = [x_0..x_{nin-1}, 1, g]
-//            and s_z[s] = [dh_0..dh_{H-1} | relu_0..relu_{H-1} | 1, 0] with
-//            dh = g W2 [pre > 0], and pushes dL/dparent = W1 dh into s_dx.
-//   reduce   the node's parameter gradients are the products
-//              dW1|db1[j][q] = sum_s s_in[s][j] dh[s][q]          (j <= nin)
-//              dW2[q] | db2  = sum_s g_s * (relu[s][q] | 1)        (row nin+1)
-//            computed as "items" (row j, column pair) so one v_pk_fma_f32 does
-//            two parameters per sample with a broadcast s_in read and one
-//            ds_read_b64 of s_z.  When a node has <= 64 items (the common case)
-//            each wave reduces half of the samples and wave 1 hands its partial
-//            to wave 0 through LDS; the fixed order keeps the slab
-//            gpart[r][blk][param] bitwise reproducible (no atomics).
-// Noise draws come from the forward's `noise` buffer, prefetched a node ahead.
+//            (packed fp32), stores its input row s_in[s] = [x_0..x_{nin-1}, 1, g]
+//            and mg[s][q] = g_s [pre_sq > 0] (the only per-unit value stored), and
+//            pushes dL/dparent = W1 (W2 * mg) into s_dx.
+//   reduce   one contraction over the block's samples gives everything:
+//              Gm[j][q] = sum_s s_in[s][j] mg[s][q]           (j <= nin)
+//              dW1|db1[j][q] = W2_q Gm[j][q]
+//              dW2[q] = sum_s relu_sq g_s = sum_j W1ext[j][q] Gm[j][q]
+//                       (relu = pre [pre > 0], pre = sum_j W1ext[j] s_in[j])
+//              db2 = sum_s g_s
+//            as "items" (row j, column pair): one v_pk_fma_f32 per two
+//            parameters and sample.  With <= 64 items (the common case) each wave
+//            takes half of the samples and hands its partial to wave 0 through LDS.
+//            Fixed orders throughout: gpart[r][blk][param] is bitwise reproducible.
+// Storing only mg (not dh and relu) keeps the footprint at ~300 B per sample, so
+// four blocks fit per CU and the whole grid of a 256-model batch is resident at
+// once.  Noise draws come from the forward's `noise` buffer, prefetched a node
+// ahead; program words are wave-uniform scalar loads.
 // ============================================================================
 template <int H, int BS>
 __global__ __launch_bounds__(BS) void gen_bwd_kernel(
     const int* __restrict__ prog, int prog_stride, const float* __restrict__ params, int P,
     const float* __restrict__ xhat, const float* __restrict__ noise, int NS,
     const float* __restrict__ grad_part, int n_chunks, int R,
-    int N, int D, int max_in, float* __restrict__ gpart) {
+    int N, int D, int Dt, int max_in, float* __restrict__ gpart) {
   static_assert(BS == 128, "two-wave reduction split assumes 128 samples per block");
-  constexpr int HE = (H + 1) & ~1;       // dh / relu segments padded to even width
+  constexpr int HE = (H + 1) & ~1;       // mg rows padded to even width (pairs)
   constexpr int HP = HE / 2;             // column pairs per row
-  constexpr int SZ = 2 * HE + 2;         // s_z row: dh | relu | 1 0
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int SI = (max_in + 2) | 1;       // odd stride: conflict-free per-thread row writes
-  float* s_z = smem;                                   // [BS][SZ]   (8-byte aligned rows)
-  f2* s_red = reinterpret_cast<f2*>(s_z + BS * SZ);    // [64]       wave-1 partials
-  float* s_x = reinterpret_cast<float*>(s_red + 64);   // [D][BS]
-  float* s_dx = s_x + BS * D;                          // [D][BS]
-  float* s_in = s_dx + BS * D;                         // [BS][SI]
-  int* s_prog = reinterpret_cast<int*>(s_in + BS * SI);
+  float* s_z = smem;                                   // [BS][HE]   mg rows (8-byte aligned)
+  f2* s_red = reinterpret_cast<f2*>(s_z + BS * HE);    // [64]       wave-1 partials
+  f2* s_g = s_red + 64;                                // [(max_in+1) * HP]  Gm pairs
+  float* s_x = reinterpret_cast<float*>(s_g + (max_in + 1) * HP);   // [Dt][BS]
+  float* s_dx = s_x + BS * Dt;                         // [Dt][BS]
+  float* s_in = s_dx + BS * Dt;                        // [BS][SI]
+  const int* s_prog = prog + (size_t)blockIdx.y * prog_stride;      // scalar (K$) reads
 
   const int r = blockIdx.y, blk = blockIdx.x, G = gridDim.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int n = blk * BS + t;
   const bool valid = n < N;
-  const int* pg = prog + (size_t)r * prog_stride;
-  for (int i = t; i < prog_stride; i += BS) s_prog[i] = pg[i];
   const float* th = params + (size_t)r * P;
   const float* xr = xhat + (size_t)r * D * N;
   const float* nz = noise + (size_t)r * NS * N;
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
 #endif
 
   // sample state; dL/dxhat = fixed-order sum of the MMD column chunks (0 on padding rows)
-  for (int v = 0; v < D; ++v) {
+  for (int v = 0; v < Dt; ++v) {
     float s = 0.f, x = 0.f;
     if (valid) {
       x = xr[(size_t)v * N + n];
@@ -368,10 +371,7 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
     s_x[v * BS + t] = x;
     s_dx[v * BS + t] = s;
   }
-  float* my_z = s_z + t * SZ;
-  if (HE != H) { my_z[H] = 0.f; my_z[HE + H] = 0.f; }
-  my_z[2 * HE] = 1.f;
-  my_z[2 * HE + 1] = 0.f;
+  float* my_z = s_z + t * HE;
   float* my_in = s_in + t * SI;
   __syncthreads();
   STAMP(0, st_t);
@@ -406,18 +406,16 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
     }
     my_in[nin] = 1.f;
     my_in[nin + 1] = gout;
-    float dh[H];
+    float mg[HE];
 #pragma unroll
-    for (int q = 0; q < H; ++q) {
-      const bool on = pre[q] > 0.f;
-      dh[q] = on ? gout * W2[q] : 0.f;
-      my_z[q] = dh[q];
-      my_z[HE + q] = on ? pre[q] : 0.f;
-    }
+    for (int q = 0; q < HE; ++q) mg[q] = (q < H && pre[q < H ? q : 0] > 0.f) ? gout : 0.f;
+#pragma unroll
+    for (int qp = 0; qp < HP; ++qp)
+      *reinterpret_cast<f2*>(my_z + 2 * qp) = f2{mg[2 * qp], mg[2 * qp + 1]};
     for (int j = 0; j < npar; ++j) {
       float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < H; ++q) s = fmaf(W1[j * H + q], dh[q], s);
+      for (int q = 0; q < H; ++q) s = fmaf(W1[j * H + q] * W2[q], mg[q], s);
       s_dx[uni(s_prog + paroff + j) * BS + t] += s;
     }
     e_cur = e_next;
@@ -426,57 +424,68 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
     STAMP(2, st_t);
 
     // ---- reduction phase ----
-    const int n_w1 = (nin + 1) * HP;           // items of rows 0..nin (dW1, db1)
-    const int n_items = n_w1 + HP + 1;         // + row nin+1 (dW2 pairs, db2)
+    const int n_w1 = (nin + 1) * HP;           // Gm items: rows 0..nin, column pairs
+    const int n_items = n_w1 + 1;              // + db2 = sum_s g
     const bool split = n_items <= 64;          // each wave takes half of the samples
-    // item -> (row j, column offset in s_z, output slots o0/o1) and its sum over
-    // samples [s_lo, s_lo + s_n)
-    auto item = [&](int it, int s_lo, int s_n, int& o0, int& o1) -> f2 {
-      int j, zoff;
-      if (it < n_w1) {
-        j = it / HP;
-        zoff = 2 * (it - j * HP);
-        o0 = j * H + zoff;
-        o1 = (zoff + 1 < H) ? o0 + 1 : -1;
-      } else {
-        j = nin + 1;
-        const int q = 2 * (it - n_w1);
-        zoff = HE + q;
-        if (q < H) { o0 = (nin + 1) * H + q; o1 = (q + 1 < H) ? o0 + 1 : -1; }
-        else { o0 = (nin + 1) * H + H; o1 = -1; }        // db2 = sum_s g * 1
-      }
-      const float* a = s_in + s_lo * SI + j;
-      const float* zb = s_z + s_lo * SZ + zoff;
+    auto item = [&](int it, int s_lo, int s_n) -> f2 {
       f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
+      if (it < n_w1) {
+        const int j = it / HP, qp = it - j * HP;
+        const float* a = s_in + s_lo * SI + j;
+        const float* zb = s_z + s_lo * HE + 2 * qp;
 #pragma unroll 4
-      for (int s2 = 0; s2 < s_n; s2 += 2) {
-        const float a0 = a[s2 * SI], a1 = a[(s2 + 1) * SI];
-        const f2 z0 = *reinterpret_cast<const f2*>(zb + s2 * SZ);
-        const f2 z1 = *reinterpret_cast<const f2*>(zb + (s2 + 1) * SZ);
-        acc0 = f2{a0, a0} * z0 + acc0;
-        acc1 = f2{a1, a1} * z1 + acc1;
+        for (int s2 = 0; s2 < s_n; s2 += 2) {
+          const float a0 = a[s2 * SI], a1 = a[(s2 + 1) * SI];
+          const f2 z0 = *reinterpret_cast<const f2*>(zb + s2 * HE);
+          const f2 z1 = *reinterpret_cast<const f2*>(zb + (s2 + 1) * HE);
+          acc0 = f2{a0, a0} * z0 + acc0;
+          acc1 = f2{a1, a1} * z1 + acc1;
+        }
+      } else {
+        const float* a = s_in + s_lo * SI + (nin + 1);
+        for (int s2 = 0; s2 < s_n; s2 += 2) {
+          acc0.x += a[s2 * SI];
+          acc1.x += a[(s2 + 1) * SI];
+        }
       }
       return acc0 + acc1;
     };
+    // item -> outputs: dW1/db1 pair (scaled by W2) or db2; Gm pair kept in s_g
+    auto emit = [&](int it, f2 acc) {
+      if (it < n_w1) {
+        const int j = it / HP, qp = it - j * HP, q = 2 * qp;
+        s_g[it] = acc;
+        gp[poff + j * H + q] = W2[q] * acc.x;
+        if (q + 1 < H) gp[poff + j * H + q + 1] = W2[q + 1] * acc.y;
+      } else {
+        gp[poff + (nin + 1) * H + H] = acc.x;      // db2
+      }
+    };
+    // dW2[q] = sum_j W1ext[j][q] Gm[j][q]  (W1ext row nin = b1), from s_g
+    auto emit_w2 = [&](int q) {
+      float s = 0.f;
+      for (int j = 0; j <= nin; ++j) {
+        const f2 gm = s_g[j * HP + (q >> 1)];
+        s = fmaf(j < nin ? W1[j * H + q] : b1[q], (q & 1) ? gm.y : gm.x, s);
+      }
+      gp[poff + (nin + 1) * H + q] = s;
+    };
     if (split) {
       f2 acc = {0.f, 0.f};
-      int o0 = -1, o1 = -1;
-      if (lane < n_items) acc = item(lane, wave * 64, 64, o0, o1);
+      if (lane < n_items) acc = item(lane, wave * 64, 64);
       STAMP(3, st_t);
       if (wave == 1) s_red[lane] = acc;
       __syncthreads();
-      if (wave == 0 && lane < n_items) {
-        acc = acc + s_red[lane];
-        gp[poff + o0] = acc.x;
-        if (o1 >= 0) gp[poff + o1] = acc.y;
+      if (wave == 0) {
+        if (lane < n_items) emit(lane, acc + s_red[lane]);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // s_g written by this wave
+        __builtin_amdgcn_wave_barrier();
+        if (lane < H) emit_w2(lane);
       }
     } else {
-      for (int it = t; it < n_items; it += BS) {
-        int o0, o1;
-        const f2 acc = item(it, 0, BS, o0, o1);
-        gp[poff + o0] = acc.x;
-        if (o1 >= 0) gp[poff + o1] = acc.y;
-      }
+      for (int it = t; it < n_items; it += BS) emit(it, item(it, 0, BS));
+      __syncthreads();
+      if (t < H) emit_w2(t);
     }
     STAMP(4, st_t);
     __syncthreads();
@@ -626,22 +635,24 @@ constexpr int GEN_BWD_BS = 128;
 
 extern "C" int cgnn_gen_bwd_blocks(int N) { return (N + GEN_BWD_BS - 1) / GEN_BWD_BS; }
 
+// D here is the unpadded variable count (the LDS arrays hold only real variables)
 extern "C" size_t cgnn_gen_bwd_lds(int H, int max_in, int D, int prog_stride) {
   const size_t HE = (size_t)((H + 1) & ~1);
-  return sizeof(float) * ((size_t)GEN_BWD_BS * ((2 * HE + 2) + ((max_in + 2) | 1) + 2 * (size_t)D) + 128) +
-         sizeof(int) * (size_t)prog_stride;
+  (void)prog_stride;
+  return sizeof(float) * ((size_t)GEN_BWD_BS * (HE + ((max_in + 2) | 1) + 2 * (size_t)D) + 128 +
+                          (size_t)(max_in + 1) * HE);
 }
 
 extern "C" int cgnn_launch_gen_bwd(const int* prog, int prog_stride, const float* params, int P,
                                    const float* xhat, const float* noise, int NS, const float* gradp,
-                                   int n_chunks, int R, int N, int D, int H, int max_in, float* gpart,
-                                   hipStream_t st) {
+                                   int n_chunks, int R, int N, int D, int Dt, int H, int max_in,
+                                   float* gpart, hipStream_t st) {
   const int G = cgnn_gen_bwd_blocks(N);
   dim3 grid(G, R), block(GEN_BWD_BS);
-  const size_t lds = cgnn_gen_bwd_lds(H, max_in, D, prog_stride);
+  const size_t lds = cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride);
   if (lds > 160 * 1024) return -2;
   switch (H) {
-#define CASE_H(h) case h: allow_lds(gen_bwd_kernel<h, GEN_BWD_BS>, lds); hipLaunchKernelGGL((gen_bwd_kernel<h, GEN_BWD_BS>), grid, block, lds, st, prog, prog_stride, params, P, xhat, noise, NS, gradp, n_chunks, R, N, D, max_in, gpart); break;
+#define CASE_H(h) case h: allow_lds(gen_bwd_kernel<h, GEN_BWD_BS>, lds); hipLaunchKernelGGL((gen_bwd_kernel<h, GEN_BWD_BS>), grid, block, lds, st, prog, prog_stride, params, P, xhat, noise, NS, gradp, n_chunks, R, N, D, Dt, max_in, gpart); break;
     CGNN_H_LIST(CASE_H)
 #undef CASE_H
     default: return -1;
