@@ -119,7 +119,10 @@ template <int L, bool XBF, bool YBF, int U>
 __global__ __launch_bounds__(256) void spmm_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
     void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
-    int n_rows, int F, int ldx, int ldy, int relu, int unit_col, int wcols) {
+    int n_rows, int F, int ldx, int ldy, int relu, int unit_col, int wcols,
+    const float* __restrict__ init, int ldi) {
+  // init (optional, fp32 [n_rows][ldi]): partial sums of earlier edges (e.g. the
+  // rank-local part of a split aggregation), added before the row scale
   // wcols: output columns this launch writes (from its base): the row stride ldy
   // for a whole-row launch, the slab width for a column-slab launch
   constexpr int RPW = 64 / L;
@@ -134,6 +137,11 @@ __global__ __launch_bounds__(256) void spmm_kernel(
   const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
   gather_sum<L, XBF, U>(col, X, e0, e1, ldx, f0, fv, sub * L, sl, acc);
   if (!rv || f0 >= wcols) return;
+  if (init && fv) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (f0 + q < F) acc[q] += init[(size_t)row * ldi + f0 + q];
+  }
   const float rs = rscale ? rscale[row] : 1.f;
   float y[8];
 #pragma unroll
@@ -161,7 +169,7 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Z,
     const float* __restrict__ rscale, const float* __restrict__ bias, const int* __restrict__ labels,
     const uint8_t* __restrict__ mask, float* __restrict__ stats, void* __restrict__ G,
-    int n_rows, int C, int ld, int mode, float inv_count) {
+    int n_rows, int C, int ld, int mode, float inv_count, const float* __restrict__ init, int ldi) {
   constexpr int L = 8, RPW = 8;
   __shared__ float s_red[4][4];
   __shared__ float s_cls[4][64];
@@ -178,6 +186,11 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
   gather_sum<L, true, 8>(col, Z, e0, e1, ld, f0, fv, sub * L, sl, acc);
+  if (init && fv) {              // partial sums of earlier edges (split aggregation)
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (f0 + q < C) acc[q] += init[(size_t)row * ldi + f0 + q];
+  }
 
   const float rs = rv ? rscale[row] : 0.f;
   float lg[8];
@@ -355,43 +368,47 @@ static int spmm_unroll() {
 template <int L, int U>
 static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
-                         int relu, int uc, int wc, hipStream_t st) {
+                         int relu, int uc, int wc, const float* init, int ldi, hipStream_t st) {
   constexpr int RPB = 4 * (64 / L);   // rows per 256-thread block
   dim3 grid((n_rows + RPB - 1) / RPB), block(256);
-  if (xbf && ybf) hipLaunchKernelGGL((spmm_kernel<L, true, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc);
-  else if (xbf) hipLaunchKernelGGL((spmm_kernel<L, true, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc);
-  else if (ybf) hipLaunchKernelGGL((spmm_kernel<L, false, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc);
-  else hipLaunchKernelGGL((spmm_kernel<L, false, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc);
+  if (xbf && ybf) hipLaunchKernelGGL((spmm_kernel<L, true, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi);
+  else if (xbf) hipLaunchKernelGGL((spmm_kernel<L, true, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi);
+  else if (ybf) hipLaunchKernelGGL((spmm_kernel<L, false, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi);
+  else hipLaunchKernelGGL((spmm_kernel<L, false, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi);
   return (int)hipGetLastError();
 }
 
 template <int L>
 static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
-                         int relu, int uc, int wc, hipStream_t st) {
+                         int relu, int uc, int wc, const float* init, int ldi, hipStream_t st) {
   if (spmm_unroll() == 8)
-    return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
-  return spmm_dispatch_u<L, 4>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
+    return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
+                                 ldi, st);
+  return spmm_dispatch_u<L, 4>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
+                               ldi, st);
 }
 
 // one launch writing output columns [0, wcols) of its base (wcols <= 512)
 static int spmm_launch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                        const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf, int relu,
-                       int uc, int wc, hipStream_t st) {
+                       int uc, int wc, const float* init, int ldi, hipStream_t st) {
   const int w = std::max(F, wc);
-  if (w <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
-  if (w <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
-  if (w <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
-  if (w <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, st);
+  if (w <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, st);
+  if (w <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, st);
+  if (w <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, st);
+  if (w <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, st);
   return -1;
 }
 
 extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X, void* Y,
                                const float* rscale, const float* bias, int n_rows, int F, int ldx,
-                               int ldy, int xbf, int ybf, int relu, int unit_col, hipStream_t st) {
+                               int ldy, int xbf, int ybf, int relu, int unit_col, const float* init, int ldi,
+                               hipStream_t st) {
   if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
   if (ldy <= 512 && F <= 512)
-    return spmm_launch(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, ldy, st);
+    return spmm_launch(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, ldy, init,
+                       ldi, st);
   // wide rows: column slabs of 512 output columns (16-byte aligned offsets), one
   // launch each; the last slabs also write the padding / ones columns up to ldy
   const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;
@@ -400,7 +417,8 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
     const int wc = std::min(512, ldy - c0);
     const int rc = spmm_launch(rowptr, col, (const char*)X + (fc ? c0 * xs : 0), (char*)Y + c0 * ys, rscale,
                                bias && fc ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu,
-                               unit_col >= 0 ? unit_col - c0 : -1, wc, st);
+                               unit_col >= 0 ? unit_col - c0 : -1, wc, init && fc ? init + c0 : nullptr, ldi,
+                               st);
     if (rc) return rc;
   }
   return 0;
@@ -431,13 +449,12 @@ extern "C" int gnn_launch_relu_dropout_bwd(void* dH, const void* H, long n, floa
 
 extern "C" int gnn_launch_spmm_ce(const int* rowptr, const int* col, const void* Z,
                                   const float* rscale, const float* bias, const int* labels,
-                                  const uint8_t* mask, float* stats, void* G, float* unused,
+                                  const uint8_t* mask, float* stats, void* G, const float* init, int ldi,
                                   int n_rows, int C, int ld, int mode, float inv_count,
                                   hipStream_t st) {
-  (void)unused;
   if (C > 64 || (ld % 8) || C > ld) return -3;
   hipLaunchKernelGGL(spmm_ce_kernel, dim3(gnn_spmm_ce_blocks(n_rows)), dim3(256), 0, st, rowptr, col,
-                     Z, rscale, bias, labels, mask, stats, G, n_rows, C, ld, mode, inv_count);
+                     Z, rscale, bias, labels, mask, stats, G, n_rows, C, ld, mode, inv_count, init, ldi);
   return (int)hipGetLastError();
 }
 

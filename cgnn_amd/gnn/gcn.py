@@ -22,7 +22,10 @@ Multi-GPU: each rank owns a contiguous block of rows (1-D partition); the
 static features are replicated (0.5 GB for ogbn-products, trivial against
 288 GB of HBM), so layer 1 needs no communication; layer 2 needs one
 all-gather of Z2 in the forward and one of G in the backward ([n, 48] bf16
-each), plus one all-reduce of the ~40k gradient floats.
+each), plus one all-reduce of the ~40k gradient floats.  Both all-gathers run
+asynchronously on RCCL's stream while the rank aggregates the edges whose
+source rows it owns (and, in the backward, the next epoch's layer-1 SpMM);
+the remaining edges are added afterwards through an fp32 partial.
 """
 from __future__ import annotations
 
@@ -133,6 +136,12 @@ class GCNTrainer:
         # parameters), then the buffers swap; every epoch still performs its own SpMM
         self.AX_next = torch.zeros_like(self.AX) if self.world > 1 else None
         self._ax_ready = False
+        if self.world > 1:
+            # layer-2 aggregations split into edges whose source row this rank owns
+            # (computed while the all-gather of the other ranks' rows is in flight) and
+            # the remaining edges (after it), summed through an fp32 partial
+            self.rp_loc, self.col_loc, self.rp_rem, self.col_rem = self._split_local(r0, r1)
+            self.part = torch.zeros(self.nloc, self.ldc, dtype=torch.float32, device=dev)
         self.H1 = torch.zeros(self.npad, hidden, **bf)
         self.dH1 = torch.zeros(self.npad, hidden, **bf)
         self.W2b = torch.zeros(hidden, self.ldc, **bf)
@@ -154,6 +163,22 @@ class GCNTrainer:
         self.fused_bwd = (self.fused and dev.type == "cuda" and
                           ops.fused_bwd_supported(self.ldx, hidden, self.ldc))
         self._gpart = None
+
+    def _split_local(self, r0, r1):
+        rp, col = self.rowptr.long(), self.col.long()
+        n = rp.numel() - 1
+        rows = torch.repeat_interleave(torch.arange(n, device=col.device), rp[1:] - rp[:-1])
+        loc = (col >= r0) & (col < r1)
+
+        def csr(sel, shift):
+            counts = torch.bincount(rows[sel], minlength=n)
+            out_rp = torch.zeros(n + 1, dtype=torch.int64, device=col.device)
+            out_rp[1:] = torch.cumsum(counts, 0)
+            return out_rp.to(torch.int32), (col[sel] - shift).to(torch.int32)
+
+        a, b = csr(loc, r0)
+        c, d = csr(~loc, 0)
+        return a, b, c, d
 
     # ------------------------------------------------------------------ passes
     def _all_gather(self, out, inp):
@@ -183,10 +208,16 @@ class GCNTrainer:
             y2 = _mm_f32(H1, self.W2b)
             torch.mul(y2, self.dinv[:, None], out=y2)
             self.Z2loc[:n] = y2.to(torch.bfloat16)
-        self._all_gather(self.Z2, self.Z2loc)
-        stats, _ = ops.spmm_ce(self.rowptr, self.col, self.Z2, C, self.dinv, self.b2, self.y, self.mask,
+        if self.world > 1:
+            work = torch.distributed.all_gather_into_tensor(self.Z2, self.Z2loc, async_op=True)
+            ops.spmm(self.rp_loc, self.col_loc, self.Z2loc, C, out=self.part, out_dtype=torch.float32)
+            work.wait()
+            rp, col, init = self.rp_rem, self.col_rem, self.part
+        else:
+            rp, col, init = self.rowptr, self.col, None
+        stats, _ = ops.spmm_ce(rp, col, self.Z2, C, self.dinv, self.b2, self.y, self.mask,
                                1.0 / max(self.n_train, 1), mode=0 if train else 1,
-                               G=self.Gloc[:n] if train else None)
+                               G=self.Gloc[:n] if train else None, init=init)
         return stats
 
     def backward(self, stats):
@@ -194,10 +225,11 @@ class GCNTrainer:
         if self.world > 1:
             work = torch.distributed.all_gather_into_tensor(self.G, self.Gloc, async_op=True)
             self._aggregate_features(self.AX_next)     # overlaps the all-gather
+            ops.spmm(self.rp_loc, self.col_loc, self.Gloc, C, out=self.part, out_dtype=torch.float32)
             work.wait()
+            ops.spmm(self.rp_rem, self.col_rem, self.G, C, rscale=self.dinv, out=self.dY2, init=self.part)
         else:
-            self._all_gather(self.G, self.Gloc)
-        ops.spmm(self.rowptr, self.col, self.G, C, rscale=self.dinv, out=self.dY2)
+            ops.spmm(self.rowptr, self.col, self.G, C, rscale=self.dinv, out=self.dY2)
         self.gb2.copy_(stats[4:4 + C])
         if self.fused_bwd:
             gW1, gb1, gW2, self._gpart = ops.fused_bwd(self.AX, self.dY2, self.W1, self.b1, self.W2, n, F,

@@ -23,10 +23,11 @@ def _row_ids(rowptr):
 
 
 def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dtype=torch.bfloat16,
-         ld_out=None, unit_col=-1):
-    """Y[i,:F] = act(rscale[i] * sum_{j in N(i)} X[j,:F] + bias); X is [*, ldx].
+         ld_out=None, unit_col=-1, init=None):
+    """Y[i,:F] = act(rscale[i] * (init[i] + sum_{j in N(i)} X[j,:F]) + bias); X is [*, ldx].
     Padding columns of Y are written 0, except ``unit_col`` which is written 1
-    (a ones column that turns the bias gradient into one more GEMM row)."""
+    (a ones column that turns the bias gradient into one more GEMM row).
+    ``init`` (optional fp32 [n, >=F]): partial sums of other edges (split aggregation)."""
     n = rowptr.numel() - 1
     ldo = ld_out or X.shape[1]
     if out is None:
@@ -37,11 +38,14 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
                      rscale.data_ptr() if rscale is not None else 0,
                      bias.data_ptr() if bias is not None else 0, n, F, X.shape[1], out.shape[1],
                      int(X.dtype == torch.bfloat16), int(out.dtype == torch.bfloat16), int(relu), int(unit_col),
-                     _st(X))
+                     _st(X), init.data_ptr() if init is not None else 0,
+                     init.shape[1] if init is not None else 0)
         return out
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, F, dtype=torch.float32)
     acc.index_add_(0, rows, X[col.long(), :F].float())
+    if init is not None:
+        acc = acc + init[:n, :F].float()
     if rscale is not None:
         acc = acc * rscale[:, None]
     if bias is not None:
@@ -55,8 +59,9 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
     return out
 
 
-def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=None):
-    """Layer-2 aggregate + log-softmax + NLL.  Returns (stats[68] summed, G)."""
+def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=None, init=None):
+    """Layer-2 aggregate + log-softmax + NLL.  Returns (stats[68] summed, G).
+    ``init`` (optional fp32 [n, >=C]): partial sums of other edges."""
     n = rowptr.numel() - 1
     ld = Z.shape[1]
     if Z.is_cuda:
@@ -67,11 +72,14 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
             G = torch.empty(n, ld, dtype=torch.bfloat16, device=Z.device)
         hip.gnn_spmm_ce(rowptr.data_ptr(), col.data_ptr(), Z.data_ptr(), rscale.data_ptr(), bias.data_ptr(),
                         labels.data_ptr(), mask.data_ptr(), stats.data_ptr(), G.data_ptr() if G is not None else 0,
-                        0, n, C, ld, mode, float(inv_count), _st(Z))
+                        init.data_ptr() if init is not None else 0, init.shape[1] if init is not None else 0,
+                        n, C, ld, mode, float(inv_count), _st(Z))
         return stats.sum(0), G
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, C, dtype=torch.float32)
     acc.index_add_(0, rows, Z[col.long(), :C].float())
+    if init is not None:
+        acc = acc + init[:n, :C].float()
     logits = acc * rscale[:, None] + bias[:C]
     lsm = torch.log_softmax(logits, 1)
     y = labels.long()

@@ -238,3 +238,38 @@ def test_gat_trainer_learns_gpu():
         last = float(tr.train_step())
     res = tr.evaluate()
     assert last < first and res["val_acc"] > 0.3, (first, last, res)
+
+
+def test_split_aggregation_with_init_matches_full():
+    """Edges split into two CSRs (rank-local / remote): the second pass adds the
+    first pass's fp32 partial -- equals one pass over all edges (SpMM and SpMM-CE)."""
+    n, rp, col = _graph(600, 5000, 7)
+    torch.manual_seed(2)
+    C, ld = 47, 48
+    Z = torch.zeros(n, ld)
+    Z[:, :C] = torch.randn(n, C)
+    Z = Z.to(torch.bfloat16)
+    rs = torch.rand(n) + 0.5
+    rows = torch.repeat_interleave(torch.arange(n), (rp[1:] - rp[:-1]).long())
+    sel = (col.long() % 3) == 0
+
+    def sub(m):
+        counts = torch.bincount(rows[m], minlength=n)
+        r = torch.zeros(n + 1, dtype=torch.int64)
+        r[1:] = torch.cumsum(counts, 0)
+        return r.to(torch.int32), col[m]
+
+    (ra, ca), (rb, cb) = sub(sel), sub(~sel)
+    d = "cuda:0"
+    full = ops.spmm(rp.to(d), col.to(d), Z.to(d), C, rscale=rs.to(d)).float().cpu()
+    part = ops.spmm(ra.to(d), ca.to(d), Z.to(d), C, out_dtype=torch.float32)
+    two = ops.spmm(rb.to(d), cb.to(d), Z.to(d), C, rscale=rs.to(d), init=part).float().cpu()
+    np.testing.assert_allclose(two.numpy(), full.numpy(), rtol=2e-2, atol=2e-2)
+    y = torch.randint(0, C, (n,), dtype=torch.int32)
+    mask = torch.randint(0, 4, (n,), dtype=torch.uint8)
+    b2 = torch.randn(C)
+    s_full, g_full = ops.spmm_ce(rp.to(d), col.to(d), Z.to(d), C, rs.to(d), b2.to(d), y.to(d), mask.to(d), 0.01)
+    s_two, g_two = ops.spmm_ce(rb.to(d), cb.to(d), Z.to(d), C, rs.to(d), b2.to(d), y.to(d), mask.to(d), 0.01,
+                               init=part)
+    np.testing.assert_allclose(s_two.cpu().numpy(), s_full.cpu().numpy(), rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(g_two.float().cpu().numpy(), g_full.float().cpu().numpy(), rtol=2e-2, atol=1e-4)
