@@ -17,14 +17,14 @@ extern "C" {
 int cgnn_mmd_supported_d(int);
 int cgnn_mmd_mfma_supported(int);
 int cgnn_mmd_mfma_row_blocks(int);
-int cgnn_launch_mmd_mfma(int, int, const float*, const float*, const float*, const float*, float*, float*,
-                         int, int, int, int, float, hipStream_t);
+int cgnn_launch_mmd_mfma_rows(int, int, const float*, const float*, const float*, const float*, float*, float*,
+                              int, int, int, int, float, int, int, hipStream_t);
 int cgnn_gen_supported_h(int);
 int cgnn_gen_bwd_blocks(int);
 size_t cgnn_gen_bwd_lds(int, int, int, int);
 int cgnn_read_stamps(unsigned long long*);
-int cgnn_launch_mmd(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
-                    float, hipStream_t);
+int cgnn_launch_mmd_rows(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
+                         float, int, int, hipStream_t);
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
                               const int*, int, int, hipStream_t);
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
@@ -111,11 +111,14 @@ PYBIND11_MODULE(_hip, m) {
   m.def("mmd_mfma_supported", &cgnn_mmd_mfma_supported);
   m.def("mmd_mfma_row_blocks", &cgnn_mmd_mfma_row_blocks);
   m.def("mmd_mfma", [](int mode, int D, uint64_t xhat, uint64_t data, uint64_t xn, uint64_t yn, uint64_t gp,
-                       uint64_t lp, int N, int R, int n_chunks, int tpc, float gscale, uint64_t st) {
-    chk(cgnn_launch_mmd_mfma(mode, D, Pt<const float>(xhat), Pt<const float>(data), Pt<const float>(xn),
-                             Pt<const float>(yn), Pt<float>(gp), Pt<float>(lp), N, R, n_chunks, tpc, gscale,
-                             S(st)), "mmd_mfma");
-  });
+                       uint64_t lp, int N, int R, int n_chunks, int tpc, float gscale, uint64_t st,
+                       int row_begin, int n_rows) {
+    chk(cgnn_launch_mmd_mfma_rows(mode, D, Pt<const float>(xhat), Pt<const float>(data), Pt<const float>(xn),
+                                  Pt<const float>(yn), Pt<float>(gp), Pt<float>(lp), N, R, n_chunks, tpc, gscale,
+                                  row_begin, n_rows < 0 ? N : n_rows, S(st)), "mmd_mfma");
+  }, py::arg("mode"), py::arg("D"), py::arg("xhat"), py::arg("data"), py::arg("xn"), py::arg("yn"), py::arg("gp"),
+     py::arg("lp"), py::arg("N"), py::arg("R"), py::arg("n_chunks"), py::arg("tpc"), py::arg("gscale"),
+     py::arg("st"), py::arg("row_begin") = 0, py::arg("n_rows") = -1);
   m.def("gen_supported_h", &cgnn_gen_supported_h);
   m.def("gen_bwd_blocks", &cgnn_gen_bwd_blocks);
   m.def("gen_bwd_lds", &cgnn_gen_bwd_lds);
@@ -129,10 +132,13 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("mmd", [](int mode, int D, uint64_t xhat, uint64_t data, uint64_t gp, uint64_t lp, int N, int R,
-                  int row_tiles, int n_chunks, int tpc, float gscale, uint64_t st) {
-    chk(cgnn_launch_mmd(mode, D, Pt<const float>(xhat), Pt<const float>(data), Pt<float>(gp), Pt<float>(lp),
-                        N, R, row_tiles, n_chunks, tpc, gscale, S(st)), "mmd");
-  });
+                  int row_tiles, int n_chunks, int tpc, float gscale, uint64_t st, int row_begin, int n_rows) {
+    chk(cgnn_launch_mmd_rows(mode, D, Pt<const float>(xhat), Pt<const float>(data), Pt<float>(gp),
+                             Pt<float>(lp), N, R, row_tiles, n_chunks, tpc, gscale, row_begin,
+                             n_rows < 0 ? N : n_rows, S(st)), "mmd");
+  }, py::arg("mode"), py::arg("D"), py::arg("xhat"), py::arg("data"), py::arg("gp"), py::arg("lp"), py::arg("N"),
+     py::arg("R"), py::arg("row_tiles"), py::arg("n_chunks"), py::arg("tpc"), py::arg("gscale"), py::arg("st"),
+     py::arg("row_begin") = 0, py::arg("n_rows") = -1);
   m.def("loss_finalize", [](uint64_t lp, int n_parts, uint64_t tt, uint64_t last, uint64_t acc, float inv_n2,
                             int flags, uint64_t hist, int hist_stride, uint64_t step, int step_off, int R,
                             uint64_t st) {

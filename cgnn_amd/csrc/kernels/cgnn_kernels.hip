@@ -53,11 +53,14 @@ constexpr float MMD_SENTINEL = 1.0e17f;   // padded columns: exp(-g*d2) == 0 exa
 // ============================================================================
 // f2, exp2_2 and rbf7x2 live in cgnn_common.h (shared with mmd_mfma.hip)
 
+// Rows: generated samples [row_begin, row_begin + n_rows) of the N columns (a
+// sample-sharded MMD evaluates only its own rows against all columns); gradient
+// partials are written with the local row stride n_rows.
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void mmd_rbf_kernel(
     const float* __restrict__ xhat, const float* __restrict__ data,
     float* __restrict__ grad_part, float* __restrict__ loss_part,
-    int N, int R, int tiles_per_chunk, float grad_scale) {
+    int N, int R, int tiles_per_chunk, float grad_scale, int row_begin, int n_rows) {
   // MODE 3: training step whose loss nobody reads (no history): gradient only
   constexpr bool GRAD = MODE == 0 || MODE == 3;
   constexpr bool LOSS = MODE != 3;
@@ -68,8 +71,9 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
   const int rt = blockIdx.x, chunk = blockIdx.y, r = blockIdx.z;
   const int n_chunks = gridDim.y, row_tiles = gridDim.x;
   const int t = threadIdx.x;
-  const int i = rt * T + t;
-  const bool valid = i < N;
+  const int il = rt * T + t;                 // local row
+  const int i = row_begin + il;              // column index of this row's sample
+  const bool valid = il < n_rows;
   const size_t mbase = (size_t)r * D * N;
   const float* P = (MODE == 2 ? data : xhat) + mbase;
   const float* Tm = data + mbase;
@@ -134,9 +138,9 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
     loss_part[((size_t)r * n_chunks + chunk) * row_tiles + rt] = s;
   }
   if (GRAD && valid) {
-    float* gp = grad_part + ((size_t)chunk * R + r) * D * N;
+    float* gp = grad_part + ((size_t)chunk * R + r) * D * n_rows;
 #pragma unroll
-    for (int k = 0; k < D; ++k) gp[(size_t)k * N + i] = (g[k].x + g[k].y) * grad_scale;
+    for (int k = 0; k < D; ++k) gp[(size_t)k * n_rows + il] = (g[k].x + g[k].y) * grad_scale;
   }
 }
 
@@ -556,13 +560,13 @@ __global__ void advance_step_kernel(int* step_base, int d_rng, int d_opt) {
 
 template <int D>
 static int launch_mmd_d(int mode, const float* xhat, const float* data, float* gpart, float* lpart,
-                        int N, int R, int row_tiles, int n_chunks, int tpc, float gscale,
+                        int row_begin, int n_rows, int N, int R, int row_tiles, int n_chunks, int tpc, float gscale,
                         hipStream_t st) {
   dim3 grid(row_tiles, n_chunks, R), block(256);
-  if (mode == 0) hipLaunchKernelGGL((mmd_rbf_kernel<D, 0>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
-  else if (mode == 3) hipLaunchKernelGGL((mmd_rbf_kernel<D, 3>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
-  else if (mode == 1) hipLaunchKernelGGL((mmd_rbf_kernel<D, 1>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
-  else hipLaunchKernelGGL((mmd_rbf_kernel<D, 2>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale);
+  if (mode == 0) hipLaunchKernelGGL((mmd_rbf_kernel<D, 0>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
+  else if (mode == 3) hipLaunchKernelGGL((mmd_rbf_kernel<D, 3>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
+  else if (mode == 1) hipLaunchKernelGGL((mmd_rbf_kernel<D, 1>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
+  else hipLaunchKernelGGL((mmd_rbf_kernel<D, 2>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
   return (int)hipGetLastError();
 }
 
@@ -571,16 +575,25 @@ extern "C" int cgnn_mmd_supported_d(int D) {
     case 32: case 48: case 64: return 1; default: return 0; }
 }
 
-extern "C" int cgnn_launch_mmd(int mode, int D, const float* xhat, const float* data, float* gpart,
-                               float* lpart, int N, int R, int row_tiles, int n_chunks, int tpc,
-                               float gscale, hipStream_t st) {
+// row_begin / n_rows: the rows (generated samples) this launch evaluates; (0, N)
+// for the whole set.  row_tiles must cover n_rows.
+extern "C" int cgnn_launch_mmd_rows(int mode, int D, const float* xhat, const float* data, float* gpart,
+                                    float* lpart, int N, int R, int row_tiles, int n_chunks, int tpc,
+                                    float gscale, int row_begin, int n_rows, hipStream_t st) {
+  if (row_begin < 0 || n_rows < 1 || row_begin + n_rows > N || (long)row_tiles * 256 < n_rows) return -2;
   switch (D) {
-#define CASE_D(d) case d: return launch_mmd_d<d>(mode, xhat, data, gpart, lpart, N, R, row_tiles, n_chunks, tpc, gscale, st);
+#define CASE_D(d) case d: return launch_mmd_d<d>(mode, xhat, data, gpart, lpart, row_begin, n_rows, N, R, row_tiles, n_chunks, tpc, gscale, st);
     CASE_D(1) CASE_D(2) CASE_D(3) CASE_D(4) CASE_D(6) CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20)
     CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64)
 #undef CASE_D
     default: return -1;
   }
+}
+
+extern "C" int cgnn_launch_mmd(int mode, int D, const float* xhat, const float* data, float* gpart,
+                               float* lpart, int N, int R, int row_tiles, int n_chunks, int tpc,
+                               float gscale, hipStream_t st) {
+  return cgnn_launch_mmd_rows(mode, D, xhat, data, gpart, lpart, N, R, row_tiles, n_chunks, tpc, gscale, 0, N, st);
 }
 
 extern "C" int cgnn_launch_loss_finalize(const float* lpart, int n_parts, float* tt, float* last,

@@ -77,7 +77,9 @@ __global__ __launch_bounds__(256) void mmd_mfma_kernel(
     const float* __restrict__ xhat, const float* __restrict__ data,
     const float* __restrict__ xnorm, const float* __restrict__ ynorm,
     float* __restrict__ grad_part, float* __restrict__ loss_part,
-    int N, int R, int tiles_per_chunk, float grad_scale) {
+    int N, int R, int tiles_per_chunk, float grad_scale, int row_begin, int n_rows) {
+  // rows: generated samples [row_begin, row_begin + n_rows) (a sample-sharded
+  // MMD owns a row range, columns are all N); gradient rows use stride n_rows.
   // MODE 0 train (loss + gradient), 1 eval (loss), 3 train without the loss
   // (nobody reads the training loss unless a history is recorded)
   constexpr bool GRAD = MODE == 0 || MODE == 3;
@@ -99,8 +101,8 @@ __global__ __launch_bounds__(256) void mmd_mfma_kernel(
   const int n_chunks = gridDim.y, n_rb = gridDim.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int h = lane >> 5, li = lane & 31;
-  const int i = rb * (WAVES * MT) + wave * MT + li;
-  const bool row_ok = i < N;
+  const int i = row_begin + rb * (WAVES * MT) + wave * MT + li;
+  const bool row_ok = i - row_begin < n_rows;
   const size_t mbase = (size_t)r * KD * N;
   const float* X = xhat + mbase;
   const float* Y = data + mbase;
@@ -277,8 +279,8 @@ __global__ __launch_bounds__(256) void mmd_mfma_kernel(
   if (GRAD) {
     // sum_j W_ij: the two lane halves hold disjoint column sets of row i = l&31
     rowsum += __shfl_xor(rowsum, 32);
-    float* gp = grad_part + ((size_t)chunk * R + r) * KD * N;
-    const int i0 = rb * (WAVES * MT) + wave * MT;
+    float* gp = grad_part + ((size_t)chunk * R + r) * KD * n_rows;
+    const int i0 = rb * (WAVES * MT) + wave * MT;           // local row
 #pragma unroll
     for (int rg = 0; rg < 16; ++rg) {
       const int il = (rg & 3) + 8 * (rg >> 2) + 4 * h;   // accumulator row -> local row
@@ -287,9 +289,9 @@ __global__ __launch_bounds__(256) void mmd_mfma_kernel(
 #pragma unroll
       for (int q = 0; q < NT; ++q) {
         const int d = 32 * q + li;
-        if (d < KD && ii < N) {
-          const float p = X[d * N + ii];
-          gp[d * N + ii] = (acc_g[q][rg] - p * rs) * grad_scale;
+        if (d < KD && ii < n_rows) {
+          const float p = X[d * N + row_begin + ii];
+          gp[d * n_rows + ii] = (acc_g[q][rg] - p * rs) * grad_scale;
         }
       }
     }
@@ -299,15 +301,15 @@ __global__ __launch_bounds__(256) void mmd_mfma_kernel(
 template <int KD>
 int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const float* xn, const float* yn,
                       float* gpart, float* lpart, int N, int R, int n_chunks, int tpc, float gscale,
-                      hipStream_t st) {
-  const int n_rb = (N + WAVES * MT - 1) / (WAVES * MT);
+                      int row_begin, int n_rows, hipStream_t st) {
+  const int n_rb = (n_rows + WAVES * MT - 1) / (WAVES * MT);
   dim3 grid(n_rb, n_chunks, R), block(256);
   if (mode == 0)
-    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 0>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale);
+    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 0>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
   else if (mode == 3)
-    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 3>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale);
+    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 3>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
   else if (mode == 1)
-    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 1>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale);
+    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 1>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
   else
     return -3;
   return (int)hipGetLastError();
@@ -328,13 +330,21 @@ extern "C" int cgnn_mmd_mfma_supported(int D) {
 extern "C" int cgnn_mmd_mfma_row_blocks(int N) { return (N + WAVES * MT - 1) / (WAVES * MT); }
 
 // xnorm / ynorm: [R][N] squared norms of the generated / true samples
-extern "C" int cgnn_launch_mmd_mfma(int mode, int D, const float* xhat, const float* data, const float* xnorm,
+extern "C" int cgnn_launch_mmd_mfma_rows(int mode, int D, const float* xhat, const float* data, const float* xnorm,
                                     const float* ynorm, float* gpart, float* lpart, int N, int R, int n_chunks,
-                                    int tpc, float gscale, hipStream_t st) {
+                                    int tpc, float gscale, int row_begin, int n_rows, hipStream_t st) {
+  if (row_begin < 0 || n_rows < 1 || row_begin + n_rows > N) return -2;
   switch (D) {
-#define CASE_D(d) case d: return launch_mmd_mfma_d<d>(mode, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale, st);
+#define CASE_D(d) case d: return launch_mmd_mfma_d<d>(mode, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale, row_begin, n_rows, st);
     CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20) CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64)
 #undef CASE_D
     default: return -1;
   }
+}
+
+extern "C" int cgnn_launch_mmd_mfma(int mode, int D, const float* xhat, const float* data, const float* xnorm,
+                                    const float* ynorm, float* gpart, float* lpart, int N, int R, int n_chunks,
+                                    int tpc, float gscale, hipStream_t st) {
+  return cgnn_launch_mmd_mfma_rows(mode, D, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale,
+                                   0, N, st);
 }

@@ -158,3 +158,25 @@ def test_batch_composition_bitwise_wide_joint():
     full = DeviceTrainer([prog] * 3, datas, keys, H, "cuda:0").run(6, 3)
     one = DeviceTrainer([prog], [datas[2]], [keys[2]], H, "cuda:0").run(6, 3)
     np.testing.assert_array_equal(one, full[2:3])
+
+
+@pytest.mark.parametrize("d,kernel", [(3, "valu"), (20, "valu"), (20, "mfma")])
+def test_row_range_mmd_tiles_the_full_mmd(d, kernel):
+    """Sample-sharded MMD building block: row ranges [b, b+n) of the HIP kernels
+    against all columns sum to the full loss and give exactly those rows of the
+    full gradient (parallel/sharded_mmd.py)."""
+    from cgnn_amd.parallel.sharded_mmd import row_partials
+    g = torch.Generator().manual_seed(5)
+    R, N = 3, 700
+    pred = torch.randn(R, N, d, generator=g, dtype=torch.float64)
+    true = torch.randn(R, N, d, generator=g, dtype=torch.float64) * 1.2 + 0.1
+    p = pred.clone().requires_grad_(True)
+    ref = torch.stack([mmd_loss_dense(p[r], true[r]) for r in range(R)])
+    ref.sum().backward()
+    P, T = pred.float().cuda(), true.float().cuda()
+    total = torch.zeros(R, dtype=torch.float64)
+    for b, e in [(0, 300), (300, 513), (513, 700)]:
+        loss, grad = row_partials(P[:, b:e], T[:, b:e], P, T, b, kernel)
+        total += loss.double().cpu()
+        np.testing.assert_allclose(grad.double().cpu().numpy(), p.grad[:, b:e].numpy(), rtol=2e-3, atol=2e-7)
+    np.testing.assert_allclose((total / N**2).numpy(), ref.detach().numpy(), rtol=2e-4, atol=1e-7)

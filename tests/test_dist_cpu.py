@@ -100,3 +100,39 @@ def test_gcn_row_partition_matches_single_process():
         assert abs(res["val_acc"] - ref["val_acc"]) < 0.06
     # the two ranks hold bitwise-identical replicated parameters
     np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+def _mmd_data():
+    g = torch.Generator().manual_seed(3)
+    pred = torch.randn(2, 60, 3, generator=g, dtype=torch.float64)
+    true = torch.randn(2, 60, 3, generator=g, dtype=torch.float64) * 1.3 + 0.2
+    return pred, true
+
+
+def _mmd_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from cgnn_amd.parallel.sharded_mmd import mmd_loss_sharded
+    pred, true = _mmd_data()
+    lo, hi = (0, 37) if rank == 0 else (37, 60)       # unequal shards
+    p = pred[:, lo:hi].clone().requires_grad_(True)
+    loss = mmd_loss_sharded(p, true[:, lo:hi])
+    loss.sum().backward()
+    out[rank] = (loss.detach().numpy().tolist(), p.grad.numpy().tolist())
+    dist.destroy_process_group()
+
+
+def test_sharded_mmd_matches_full_mmd():
+    """Sample-sharded MMD over 2 gloo ranks: every rank sees the global loss and
+    gets exactly its rows of the full gradient."""
+    from cgnn_amd.engine.reference import mmd_loss_dense
+    pred, true = _mmd_data()
+    p = pred.clone().requires_grad_(True)
+    ref = torch.stack([mmd_loss_dense(p[r], true[r]) for r in range(2)])
+    ref.sum().backward()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_mmd_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for rank, (lo, hi) in enumerate([(0, 37), (37, 60)]):
+        loss, grad = out[rank]
+        np.testing.assert_allclose(loss, ref.detach().numpy(), rtol=1e-10)
+        np.testing.assert_allclose(np.array(grad), p.grad[:, lo:hi].numpy(), rtol=1e-8, atol=1e-12)
