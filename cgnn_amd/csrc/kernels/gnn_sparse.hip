@@ -50,11 +50,18 @@ __device__ __forceinline__ uint4 f32x8_to_bf16(const float* f) {
   return o;
 }
 
-template <bool XBF>
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// element types of the gathered / written matrices: 0 = fp32, 1 = bf16, 2 = fp16
+template <int XT>
 __device__ __forceinline__ void load8(const void* X, size_t off, float* f) {
-  if (XBF) {
+  if (XT == 1) {
     const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(X) + off);
     bf16x8_to_f32(v, f);
+  } else if (XT == 2) {
+    const f16x8 v = *reinterpret_cast<const f16x8*>(reinterpret_cast<const uint16_t*>(X) + off);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) f[q] = (float)v[q];
   } else {
     const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + off);
     const float4 a = p[0], b = p[1];
@@ -63,7 +70,7 @@ __device__ __forceinline__ void load8(const void* X, size_t off, float* f) {
 }
 
 // Sum the rows X[col[e]] for e in [e0, e1) into acc (8 features at f0).
-template <int L, bool XBF, int U = 4>
+template <int L, int XBF, int U = 4>
 __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const void* __restrict__ X,
                                            int e0, int e1, int ldx, int f0, bool fv, int sub_base,
                                            int sl, float* acc) {
@@ -115,7 +122,7 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
 
 }  // namespace
 
-template <int L, bool XBF, bool YBF, int U>
+template <int L, int XBF, int YBF, int U>
 __global__ __launch_bounds__(256) void spmm_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
     void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
@@ -151,8 +158,13 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     if (relu) v = fmaxf(v, 0.f);
     y[q] = f < F ? v : (f == unit_col ? 1.f : 0.f);
   }
-  if (YBF) {
+  if (YBF == 1) {
     *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
+  } else if (YBF == 2) {
+    f16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (_Float16)y[q];
+    *reinterpret_cast<f16x8*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0) = o;
   } else {
     float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(Y) + (size_t)row * ldy + f0);
     p[0] = make_float4(y[0], y[1], y[2], y[3]);
@@ -185,7 +197,7 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
   const bool fv = rv && f0 < C;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
-  gather_sum<L, true, 8>(col, Z, e0, e1, ld, f0, fv, sub * L, sl, acc);
+  gather_sum<L, 1, 8>(col, Z, e0, e1, ld, f0, fv, sub * L, sl, acc);
   if (init && fv) {              // partial sums of earlier edges (split aggregation)
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -371,10 +383,17 @@ static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, voi
                          int relu, int uc, int wc, const float* init, int ldi, hipStream_t st) {
   constexpr int RPB = 4 * (64 / L);   // rows per 256-thread block
   dim3 grid((n_rows + RPB - 1) / RPB), block(256);
-  if (xbf && ybf) hipLaunchKernelGGL((spmm_kernel<L, true, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi);
-  else if (xbf) hipLaunchKernelGGL((spmm_kernel<L, true, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi);
-  else if (ybf) hipLaunchKernelGGL((spmm_kernel<L, false, true, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi);
-  else hipLaunchKernelGGL((spmm_kernel<L, false, false, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi);
+#define CGNN_SPMM(XT, YT) hipLaunchKernelGGL((spmm_kernel<L, XT, YT, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi)
+  // element-type codes: 0 fp32, 1 bf16, 2 fp16 (fp16 pairs with itself or with fp32)
+  if (xbf == 1 && ybf == 1) CGNN_SPMM(1, 1);
+  else if (xbf == 1 && ybf == 0) CGNN_SPMM(1, 0);
+  else if (xbf == 0 && ybf == 1) CGNN_SPMM(0, 1);
+  else if (xbf == 0 && ybf == 0) CGNN_SPMM(0, 0);
+  else if (xbf == 2 && ybf == 2) CGNN_SPMM(2, 2);
+  else if (xbf == 2 && ybf == 0) CGNN_SPMM(2, 0);
+  else if (xbf == 0 && ybf == 2) CGNN_SPMM(0, 2);
+  else return -5;
+#undef CGNN_SPMM
   return (int)hipGetLastError();
 }
 
@@ -411,7 +430,7 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
                        ldi, st);
   // wide rows: column slabs of 512 output columns (16-byte aligned offsets), one
   // launch each; the last slabs also write the padding / ones columns up to ldy
-  const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;
+  const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;   // bf16 and fp16 are both 2 bytes
   for (int c0 = 0; c0 < ldy; c0 += 512) {
     const int fc = std::max(0, std::min(512, F - c0));
     const int wc = std::min(512, ldy - c0);

@@ -32,10 +32,13 @@ def _st(t):
 
 
 class GraphCSR:
-    """CSR (A + I) plus its lazily built transpose with the edge permutation."""
+    """CSR (A + I) plus its lazily built transpose with the edge permutation.
+    ``n`` destination rows; ``n_cols`` source rows (default ``n``; a row block of a
+    partitioned graph keeps global source ids, so ``n_cols`` is the global count)."""
 
-    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n: int):
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n: int, n_cols: Optional[int] = None):
         self.rowptr, self.col, self.n = rowptr.contiguous(), col.contiguous(), int(n)
+        self.n_cols = int(n) if n_cols is None else int(n_cols)
         self._t = None
         self._rows = None
 
@@ -45,7 +48,7 @@ class GraphCSR:
 
     def transposed(self):
         if self._t is None:
-            self._t = transpose_csr(self.rowptr, self.col, self.n, with_perm=True)
+            self._t = transpose_csr(self.rowptr, self.col, self.n_cols, with_perm=True)
         return self._t
 
     def edge_rows(self):
@@ -83,10 +86,11 @@ class _GATAggregate(torch.autograd.Function):
                             s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(),
                             dsc_e.data_ptr(), ds_dst.data_ptr(), n, K, Fh, _st(Wh))
         rp_t, col_t, perm = g.transposed()
-        dWh = torch.empty_like(Wh)
-        ds_src = torch.empty(n, K, dtype=torch.float32, device=dev)
+        dWh = torch.empty_like(Wh)                      # [n_cols, K*Fh]: one row per source
+        ds_src = torch.empty(g.n_cols, K, dtype=torch.float32, device=dev)
         hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
-                            dsc_e.data_ptr(), dout.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), n, K, Fh, _st(Wh))
+                            dsc_e.data_ptr(), dout.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh,
+                            _st(Wh))
         return dWh, ds_src, ds_dst, None, None, None
 
 
@@ -106,7 +110,10 @@ def _gat_aggregate_torch(Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int):
 
 
 def gat_aggregate(Wh: torch.Tensor, s_src: torch.Tensor, s_dst: torch.Tensor, g: GraphCSR, K: int, Fh: int):
-    """Multi-head attention aggregation; Wh [n, K*Fh] fp32, s_* [n, K]."""
+    """Multi-head attention aggregation; Wh [n_cols, K*Fh] fp32, s_src [n_cols, K],
+    s_dst [n, K]; returns [n, K*Fh]."""
+    if Wh.shape[0] != g.n_cols or s_src.shape[0] != g.n_cols or s_dst.shape[0] != g.n:
+        raise ValueError("gat_aggregate: operand rows do not match the graph (%d x %d)" % (g.n, g.n_cols))
     if Wh.is_cuda:
         if Fh % 8 or (Fh // 8) & (Fh // 8 - 1) or K * Fh > 512:
             raise ValueError("HIP GAT needs Fh = 8 * 2^m and K * Fh <= 512")
@@ -125,11 +132,16 @@ class GATLayer(torch.nn.Module):
         self.a_dst = torch.nn.Parameter((torch.rand(heads, head_dim, generator=generator) * 2 - 1) * ab)
         self.bias = torch.nn.Parameter(torch.zeros(heads * head_dim))
 
-    def forward(self, h, g: GraphCSR):
+    def forward(self, h, g: GraphCSR, gather=None):
+        """``gather`` (graph-sharded training): maps this rank's rows to all rows;
+        the source-side [Wh | s_src] goes through ONE collective."""
         Wh = h @ self.W
         Whk = Wh.view(-1, self.K, self.Fh)
         s_src = (Whk * self.a_src).sum(-1)
         s_dst = (Whk * self.a_dst).sum(-1)
+        if gather is not None:
+            both = gather(torch.cat([Wh, s_src], 1))
+            Wh, s_src = both[:, :self.K * self.Fh], both[:, self.K * self.Fh:]
         return gat_aggregate(Wh, s_src, s_dst, g, self.K, self.Fh) + self.bias
 
 
@@ -148,11 +160,11 @@ class GAT(torch.nn.Module):
         self.l2 = GATLayer(heads * head_dim, 1, out_w, gen)
         self.dropout = float(dropout)
 
-    def forward(self, x, g: GraphCSR):
-        h = torch.nn.functional.elu(self.l1(x, g))
+    def forward(self, x, g: GraphCSR, gather=None):
+        h = torch.nn.functional.elu(self.l1(x, g, gather))
         if self.training and self.dropout > 0:
             h = torch.nn.functional.dropout(h, self.dropout)
-        return self.l2(h, g)[:, :self.C]
+        return self.l2(h, g, gather)[:, :self.C]
 
 
 class GATTrainer:
@@ -188,3 +200,84 @@ class GATTrainer:
             m = self.gd.mask == k
             res[name] = float((pred[m] == self.gd.y[m].long()).float().mean()) if bool(m.any()) else float("nan")
         return res
+
+
+class ShardedGATTrainer:
+    """Graph-sharded full-graph GAT (BASELINE config "ogbn-papers100M 2-layer GAT,
+    graph sharded across 8 x 288 GB HBM"): rank r owns a contiguous block of
+    destination rows -- its CSR rows (global source ids), features, labels and
+    all activations of those rows.  Per layer one all-gather of the source-side
+    [Wh | s_src] rows (RCCL ring over xGMI) and, in the backward, one
+    reduce-scatter of their gradients back to the owners; parameters are
+    replicated and their gradients averaged by the bucketed all-reduce.  Feature
+    standardisation uses globally all-reduced moments, so the model equals the
+    single-GPU one for any rank count."""
+
+    def __init__(self, gd: GraphData, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True,
+                 bucket_mb: float = 16.0):
+        import torch.distributed as dist
+        from ..parallel import dist as pdist
+        from ..parallel.collectives import gather_rows
+        from ..parallel.ddp import GradBucketer
+        from .data import partition_rows
+        self.rank, self.world = pdist.rank(), pdist.world_size()
+        self.dev = gd.rowptr.device
+        self.n = gd.n
+        r0, r1, per, rp, col = partition_rows(gd, self.rank, self.world)
+        self.r0, self.r1, self.per = r0, r1, per
+        self.g = GraphCSR(rp, col, r1 - r0, n_cols=gd.n)
+        x = gd.x[r0:r1].float()
+        if standardize:
+            mom = torch.stack([x.sum(0), (x * x).sum(0)]).double()
+            if self.world > 1:
+                dist.all_reduce(mom)
+            mean = mom[0] / gd.n
+            var = (mom[1] / gd.n - mean * mean) * gd.n / max(gd.n - 1, 1)
+            x = ((x - mean.float()) / var.clamp_min(1e-12).sqrt().float().clamp_min(1e-6))
+        self.x = x.contiguous()
+        self.y = gd.y[r0:r1].long()
+        self.mask = gd.mask[r0:r1]
+        self.tr = self.mask == 1
+        n_train = torch.tensor([float(self.tr.sum())], dtype=torch.float64, device=self.dev)
+        if self.world > 1:
+            dist.all_reduce(n_train)
+        self.n_train = float(n_train.item())
+        self.model = GAT(x.shape[1], gd.n_classes, heads, head_dim, dropout, seed).to(self.dev)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=lr)
+        self.ddp = None
+        self.gather = None
+        if self.world > 1:
+            self.ddp = GradBucketer(list(self.model.parameters()), bucket_mb)
+            self.ddp.broadcast_parameters(0)
+            self.gather = lambda t: gather_rows(t, per, gd.n)
+        self.epoch = 0
+
+    def train_step(self):
+        self.model.train()
+        out = self.model(self.x, self.g, self.gather)
+        # sum over this rank's train rows scaled so that the rank-average of the
+        # gradients is the gradient of the global mean loss
+        loss = torch.nn.functional.cross_entropy(out[self.tr], self.y[self.tr], reduction="sum")
+        (loss * (self.world / self.n_train)).backward()
+        if self.ddp is not None:
+            self.ddp.finish()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        self.epoch += 1
+        return loss.detach() / self.n_train        # this rank's share of the global mean loss
+
+    @torch.no_grad()
+    def evaluate(self):
+        import torch.distributed as dist
+        self.model.eval()
+        pred = self.model(self.x, self.g, self.gather).argmax(1)
+        cnt = torch.zeros(6, dtype=torch.float64, device=self.dev)
+        for i, k in enumerate((1, 2, 3)):
+            m = self.mask == k
+            cnt[2 * i] = float((pred[m] == self.y[m]).sum())
+            cnt[2 * i + 1] = float(m.sum())
+        if self.world > 1:
+            dist.all_reduce(cnt)
+        c = cnt.cpu().numpy()
+        return {name: float(c[2 * i] / c[2 * i + 1]) if c[2 * i + 1] else float("nan")
+                for i, name in enumerate(("train_acc", "val_acc", "test_acc"))}

@@ -277,6 +277,25 @@ class GCNTrainer:
                 "val_acc": float(s[2]) / max(self.n_val, 1),
                 "test_acc": float(s[3]) / max(self.n_test, 1)}
 
+    # ---------------------------------------------------------------- checkpoint
+    def state_tensors(self):
+        """Flat fp32 parameters, Adam moments and step, dropout RNG key (identical on
+        every rank; the dropout stream position is the epoch, kept in the metadata)."""
+        key = torch.tensor([int(self.key[0]), int(self.key[1])], dtype=torch.int64)
+        return {"params": self.params, "adam_m": self.m, "adam_v": self.v, "adam_step": self.step_t,
+                "rng_key": key}
+
+    def load_state_tensors(self, t):
+        if "rng_key" in t:
+            self.key = (int(t["rng_key"][0]), int(t["rng_key"][1]))
+        for name, dst in (("params", self.params), ("adam_m", self.m), ("adam_v", self.v),
+                          ("adam_step", self.step_t)):
+            if t[name].shape != dst.shape:
+                raise ValueError("checkpoint %s has shape %s, trainer %s" % (name, tuple(t[name].shape),
+                                                                              tuple(dst.shape)))
+            dst.copy_(t[name].to(dst.device))
+        self._ax_ready = False
+
     def train_loss(self):
         s = self.last_stats.clone()
         if self.world > 1:

@@ -22,6 +22,16 @@ def _row_ids(rowptr):
     return torch.repeat_interleave(torch.arange(n, device=rowptr.device), counts)
 
 
+_DT_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def dtype_code(dt) -> int:
+    """Element-type code of the sparse kernels (0 fp32, 1 bf16, 2 fp16)."""
+    if dt not in _DT_CODE:
+        raise TypeError("sparse kernels take fp32 / bf16 / fp16, got %s" % dt)
+    return _DT_CODE[dt]
+
+
 def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dtype=torch.bfloat16,
          ld_out=None, unit_col=-1, init=None):
     """Y[i,:F] = act(rscale[i] * (init[i] + sum_{j in N(i)} X[j,:F]) + bias); X is [*, ldx].
@@ -37,7 +47,7 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
         hip.gnn_spmm(rowptr.data_ptr(), col.data_ptr(), X.data_ptr(), out.data_ptr(),
                      rscale.data_ptr() if rscale is not None else 0,
                      bias.data_ptr() if bias is not None else 0, n, F, X.shape[1], out.shape[1],
-                     int(X.dtype == torch.bfloat16), int(out.dtype == torch.bfloat16), int(relu), int(unit_col),
+                     dtype_code(X.dtype), dtype_code(out.dtype), int(relu), int(unit_col),
                      _st(X), init.data_ptr() if init is not None else 0,
                      init.shape[1] if init is not None else 0)
         return out

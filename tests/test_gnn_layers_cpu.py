@@ -1,0 +1,91 @@
+"""CPU tests of the depth-generic GCN layers, the L-layer trainer (Cora-shaped
+CPU reference path of BASELINE.json), the inference engine and GNN checkpoints."""
+import numpy as np
+import pytest
+import torch
+
+from cgnn_amd.gnn.data import build_csr, synthetic
+from cgnn_amd.gnn.gcn_deep import DeepGCNTrainer, GCNInference
+from cgnn_amd.gnn.layers import GCN, NormGraph, norm_aggregate
+
+
+def _dense_norm_adj(rp, col, n):
+    A = torch.zeros(n, n, dtype=torch.float64)
+    rows = torch.repeat_interleave(torch.arange(n), (rp[1:] - rp[:-1]).long())
+    A[rows, col.long()] = 1.0
+    deg = A.sum(1)
+    d = deg.rsqrt()
+    return d[:, None] * A * d[None, :], d
+
+
+def test_norm_aggregate_forward_backward_match_dense():
+    n = 120
+    rng = np.random.default_rng(0)
+    rp, col = build_csr(n, rng.integers(0, n, 500), rng.integers(0, n, 500), "cpu")
+    Ahat, d = _dense_norm_adj(rp, col, n)
+    g = NormGraph(rp, col, d.float())
+    x = torch.randn(n, 13, dtype=torch.float32, requires_grad=True)     # width not a multiple of 8
+    y = norm_aggregate(x, g)
+    ref = Ahat @ x.detach().double()
+    np.testing.assert_allclose(y.detach().double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+    gy = torch.randn(n, 13)
+    y.backward(gy)
+    np.testing.assert_allclose(x.grad.double().numpy(), (Ahat.t() @ gy.double()).numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_deep_gcn_cora_cpu_learns():
+    g = synthetic("cora", seed=0, device="cpu")
+    tr = DeepGCNTrainer(g, hidden=64, layers=3, dropout=0.5, lr=0.01)
+    first = float(tr.train_step())
+    for _ in range(30):
+        last = float(tr.train_step())
+    res = tr.evaluate()
+    assert last < first
+    assert res["val_acc"] > 2.0 / g.n_classes, res
+
+
+def test_inference_matches_model_forward():
+    g = synthetic("cora", seed=1, device="cpu")
+    tr = DeepGCNTrainer(g, hidden=32, layers=2)
+    for _ in range(3):
+        tr.train_step()
+    tr.model.eval()
+    with torch.no_grad():
+        ref = tr.model(tr.x, tr.ng)
+    inf = GCNInference.from_model(g, tr.model)
+    got = inf()
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_deep_gcn_checkpoint_roundtrip(tmp_path):
+    from cgnn_amd.gnn.checkpoint import load_trainer, save_trainer
+    g = synthetic("cora", seed=2, device="cpu")
+    a = DeepGCNTrainer(g, hidden=32, layers=3, seed=5, dropout=0.0)
+    for _ in range(3):
+        a.train_step()
+    path = str(tmp_path / "gcn.safetensors")
+    save_trainer(a, path, config={"hidden": 32, "layers": 3})
+    b = DeepGCNTrainer(g, hidden=32, layers=3, seed=9, dropout=0.0)
+    meta = load_trainer(b, path)
+    assert meta["epoch"] == "3" and meta["config"]["layers"] == 3
+    for _ in range(2):
+        la, lb = float(a.train_step()), float(b.train_step())
+        assert la == pytest.approx(lb, rel=1e-6)
+    for pa, pb in zip(a.model.parameters(), b.model.parameters()):
+        np.testing.assert_allclose(pa.detach().numpy(), pb.detach().numpy(), rtol=1e-6, atol=1e-7)
+
+
+def test_fused_gcn_checkpoint_roundtrip(tmp_path):
+    from cgnn_amd.gnn.checkpoint import load_trainer, save_trainer
+    from cgnn_amd.gnn.gcn import GCNTrainer
+    g = synthetic("ogbn-products", seed=0, scale=0.001)
+    a = GCNTrainer(g, hidden=32, rank=0, world=1)
+    for _ in range(2):
+        a.train_step()
+    path = str(tmp_path / "gcn2.safetensors")
+    save_trainer(a, path)
+    b = GCNTrainer(g, hidden=32, rank=0, world=1, seed=3)
+    load_trainer(b, path)
+    a.train_step()
+    b.train_step()
+    np.testing.assert_array_equal(a.params.numpy(), b.params.numpy())

@@ -1,0 +1,182 @@
+"""Benchmarks of the BASELINE.json GNN configs other than the headline one
+(``bench.py``: 2-layer GCN on ogbn-products).  Synthetic graphs of the named
+shapes (no network for the datasets), random-init weights; one JSON line per
+run on rank 0.
+
+    python tools/bench_gnn_configs.py --config cora-cpu
+    python tools/bench_gnn_configs.py --config arxiv-gcn3
+    python tools/bench_gnn_configs.py --config reddit-infer
+    python tools/bench_gnn_configs.py --config products-sage3            # 1 GPU
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
+        tools/bench_gnn_configs.py --config products-sage3                # DP over 8 GPUs
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
+        tools/bench_gnn_configs.py --config papers-gat2                   # graph sharded over 8 GPUs
+
+Timing: W untimed warm-up steps, then K steps bracketed by barrier + device
+synchronize; the MAX over ranks is reported.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _timed(fn, steps, warmup, dev):
+    from cgnn_amd.parallel import dist as pdist
+    for _ in range(warmup):
+        fn()
+    pdist.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    _sync(dev)
+    pdist.barrier()
+    dt = time.perf_counter() - t0
+    if pdist.world_size() > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", required=True,
+                    choices=["cora-cpu", "arxiv-gcn3", "reddit-infer", "products-sage3", "papers-gat2"])
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink the graph (nodes and edges)")
+    ap.add_argument("--hidden", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-capture", action="store_true", help="eager launches instead of hipGraph replay")
+    a = ap.parse_args()
+
+    from cgnn_amd.gnn.data import SHAPES, synthetic
+    from cgnn_amd.parallel import dist as pdist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    cpu = a.config == "cora-cpu" or not torch.cuda.is_available()
+    if world > 1:
+        pdist.init_process_group("gloo" if cpu else "nccl")
+    rank = pdist.rank()
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(pdist.local_rank() % torch.cuda.device_count())
+        dev = torch.device("cuda", torch.cuda.current_device())
+    capture = None if not a.no_capture else False
+    res = {"n_gpus": 0 if cpu else world, "scale": a.scale}
+    t_setup = time.perf_counter()
+
+    if a.config in ("cora-cpu", "arxiv-gcn3"):
+        from cgnn_amd.gnn.gcn_deep import DeepGCNTrainer
+        name, layers = ("cora", 2) if a.config == "cora-cpu" else ("ogbn-arxiv", 3)
+        hidden = a.hidden or (16 if name == "cora" else 256)
+        steps, warmup = a.steps or (100 if cpu else 200), a.warmup or 10
+        g = synthetic(name, seed=a.seed, device=dev, scale=a.scale)
+        dtype = torch.float32 if cpu else torch.bfloat16
+        tr = DeepGCNTrainer(g, hidden=hidden, layers=layers, dropout=0.5, lr=0.01, dtype=dtype, seed=a.seed,
+                            capture=capture)
+        setup = time.perf_counter() - t_setup
+        dt = _timed(tr.train_step, steps, warmup, dev)
+        ev = tr.evaluate()
+        res.update(metric="epochs/sec + val-acc, %d-layer GCN %s full-graph" % (layers, name),
+                   value=round(steps / dt, 3), unit="epochs/s", ms_per_step=round(1e3 * dt / steps, 4),
+                   val_acc=round(ev["val_acc"], 4), test_acc=round(ev["test_acc"], 4),
+                   dtype=str(dtype).replace("torch.", ""), hipgraph=bool(tr._step_graph.graph is not None),
+                   config={"model": "GCN-%dlayer-hidden%d" % (layers, hidden), "dataset": name, "nodes": g.n,
+                           "nnz_with_self_loops": g.nnz})
+    elif a.config == "reddit-infer":
+        from cgnn_amd.gnn.gcn_deep import GCNInference
+        from cgnn_amd.gnn.layers import GCN
+        hidden = a.hidden or 256
+        steps, warmup = a.steps or 100, a.warmup or 5
+        g = synthetic("reddit", seed=a.seed, device=dev, scale=a.scale)
+        model = GCN([g.n_features, hidden, g.n_classes], seed=a.seed).to(dev).eval()
+        inf = GCNInference.from_model(g, model, dtype=torch.float16, capture=capture)
+        setup = time.perf_counter() - t_setup
+        for _ in range(warmup):
+            inf()
+        _sync(dev)
+        lat = []
+        if dev.type == "cuda":
+            st = torch.cuda.current_stream()
+            for _ in range(steps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                inf()
+                e1.record(st)
+                e1.synchronize()
+                lat.append(e0.elapsed_time(e1))
+        else:
+            for _ in range(steps):
+                t0 = time.perf_counter()
+                inf()
+                lat.append(1e3 * (time.perf_counter() - t0))
+        lat = np.array(lat)
+        dt = lat.sum() / 1e3
+        res.update(metric="latency, 2-layer GCN reddit full-graph inference", value=round(float(np.median(lat)), 4),
+                   unit="ms", higher_is_better=False, p99_ms=round(float(np.percentile(lat, 99)), 4),
+                   mean_ms=round(float(lat.mean()), 4), dtype=str(inf.dtype).replace("torch.", ""),
+                   hipgraph=bool(inf._graph.graph is not None),
+                   config={"model": "GCN-2layer-hidden%d" % hidden, "dataset": "reddit", "nodes": g.n,
+                           "nnz_with_self_loops": g.nnz})
+    elif a.config == "products-sage3":
+        from cgnn_amd.gnn.sage import SAGETrainer
+        hidden = a.hidden or 256
+        steps, warmup = a.steps or 2, a.warmup or 1
+        g = synthetic("ogbn-products", seed=a.seed, device=dev, scale=a.scale)
+        tr = SAGETrainer(g, hidden=hidden, layers=3, dropout=0.5, lr=0.003, fanouts=(15, 10, 5),
+                         batch_size=1024, seed=a.seed)
+        setup = time.perf_counter() - t_setup
+        per_epoch = len(tr._batches())
+        dt = _timed(tr.train_epoch, steps, warmup, dev)
+        ev = tr.evaluate()
+        seeds = len(tr.train_idx) * steps
+        res.update(metric="epochs/sec + val-acc, 3-layer GraphSAGE ogbn-products mini-batch DP",
+                   value=round(steps / dt, 4), unit="epochs/s", ms_per_step=round(1e3 * dt / steps, 3),
+                   seeds_per_s=round(seeds / dt, 1), iterations_per_epoch=per_epoch,
+                   val_acc=round(ev["val_acc"], 4), test_acc=round(ev["test_acc"], 4), dtype="fp32",
+                   scaling="strong (fixed global epoch; per-rank batch 1024)",
+                   config={"model": "SAGE-3layer-hidden%d" % hidden, "fanouts": [15, 10, 5],
+                           "batch_per_rank": 1024, "parallelism": "dp%d" % world, "nodes": g.n})
+    else:
+        from cgnn_amd.gnn.gat import ShardedGATTrainer
+        steps, warmup = a.steps or 10, a.warmup or 2
+        g = synthetic("ogbn-papers100M", seed=a.seed, device=dev, scale=a.scale)
+        tr = ShardedGATTrainer(g, heads=4, head_dim=32, dropout=0.5, lr=0.005, seed=a.seed)
+        n_nodes, nnz = g.n, g.nnz
+        del g
+        setup = time.perf_counter() - t_setup
+        dt = _timed(tr.train_step, steps, warmup, dev)
+        ev = tr.evaluate()
+        res.update(metric="epochs/sec + val-acc, 2-layer GAT ogbn-papers100M, graph sharded",
+                   value=round(steps / dt, 4), unit="epochs/s", ms_per_step=round(1e3 * dt / steps, 3),
+                   val_acc=round(ev["val_acc"], 4), test_acc=round(ev["test_acc"], 4), dtype="fp32",
+                   config={"model": "GAT-2layer-4x32", "parallelism": "graph-rowpart%d" % world, "nodes": n_nodes,
+                           "nnz_with_self_loops": nnz})
+    res.update(steps=steps, warmup=warmup, setup_s=round(setup, 2), data="synthetic graph of the named shape "
+               "(planted communities), random-init weights")
+    res.setdefault("higher_is_better", True)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
