@@ -74,6 +74,7 @@ enum RngPurpose : uint32_t {
   RNG_PARAM_INIT = 3u,   // parameter init            N(0,s^2) (param, 0, 0)
   RNG_RFF_FREQ   = 4u,   // Fourier-MMD frequencies            (feat, dim, step)
   RNG_DROPOUT    = 5u,   // GNN dropout masks                  (row, col/4, step)
+  RNG_SAMPLE     = 6u,   // GNN neighbour sampling             (node, salt, draw/4)
 };
 
 __device__ __forceinline__ float rng_normal(uint32_t k0, uint32_t k1, uint32_t a, uint32_t b,

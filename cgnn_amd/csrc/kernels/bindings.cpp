@@ -57,6 +57,8 @@ int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, flo
                     const int*, hipStream_t);
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
 int gnn_spmm_ce_blocks(int);
+int gnn_launch_sample_neighbors(const int*, const int*, const int*, int, int, const int*, int*, uint32_t, uint32_t,
+                                uint32_t, hipStream_t);
 int gnn_launch_bias_relu_dropout(void*, const float*, long, int, int, float, uint32_t, uint32_t,
                                  uint32_t, uint32_t, hipStream_t);
 int gnn_launch_relu_dropout_bwd(void*, const void*, long, float, hipStream_t);
@@ -212,6 +214,12 @@ PYBIND11_MODULE(_hip, m) {
                         Pt<const int>(step), S(st)), "gnn_adam");
   });
   m.def("gnn_spmm_ce_blocks", &gnn_spmm_ce_blocks);
+  m.def("gnn_sample_neighbors", [](uint64_t rowptr, uint64_t col, uint64_t nodes, int n, int fanout, uint64_t out_ptr,
+                                   uint64_t out_col, uint32_t k0, uint32_t k1, uint32_t salt, uint64_t st) {
+    chk(gnn_launch_sample_neighbors(Pt<const int>(rowptr), Pt<const int>(col), Pt<const int>(nodes), n, fanout,
+                                    Pt<const int>(out_ptr), Pt<int>(out_col), k0, k1, salt, S(st)),
+        "gnn_sample_neighbors");
+  });
   m.def("gnn_bias_relu_dropout", [](uint64_t h, uint64_t bias, long rows, int F, int ld, float p, uint32_t k0,
                                     uint32_t k1, uint32_t step, uint32_t row0, uint64_t st) {
     chk(gnn_launch_bias_relu_dropout(Pt<void>(h), Pt<const float>(bias), rows, F, ld, p, k0, k1, step, row0, S(st)),

@@ -145,7 +145,8 @@ class SAGETrainer:
 
     def __init__(self, g: GraphData, hidden: int = 256, layers: int = 2, dropout: float = 0.5,
                  lr: float = 0.003, fanouts: Optional[List[int]] = (15, 10), batch_size: int = 1024,
-                 seed: int = 0, prefetch: bool = True, standardize: bool = True, bucket_mb: float = 16.0):
+                 seed: int = 0, prefetch: bool = True, standardize: bool = True, bucket_mb: float = 16.0,
+                 sampler: Optional[str] = None):
         from ..parallel import dist as pdist
         self.rank, self.world = pdist.rank(), pdist.world_size()
         self.g = g
@@ -175,6 +176,12 @@ class SAGETrainer:
         self._col = g.col.cpu().numpy()
         self._full = None
         self.prefetch = bool(prefetch)
+        # "device": HIP sampler on the resident CSR (default on a GPU); "host": C++/OpenMP
+        self.sampler = sampler or ("device" if self.dev.type == "cuda" else "host")
+        self._dsampler = None
+        if self.fanouts and self.sampler == "device":
+            from .sampler import DeviceSampler
+            self._dsampler = DeviceSampler(g.rowptr, g.col, self.fanouts[:layers], seed)
         self.epoch = 0
 
     # ----------------------------------------------------------- blocks
@@ -239,7 +246,12 @@ class SAGETrainer:
             return float(loss)
         batches = self._batches()
         losses = []
-        if self.prefetch and len(batches) > 1:
+        if self._dsampler is not None:
+            for k, b in enumerate(batches):
+                seeds_t = torch.as_tensor(b, device=self.dev)
+                blocks, nodes_in = self._dsampler.sample(seeds_t, (self.epoch * 100003 + k) * self.world + self.rank)
+                losses.append(self._step(blocks, nodes_in, seeds_t))
+        elif self.prefetch and len(batches) > 1:
             q: "queue.Queue" = queue.Queue(maxsize=2)
 
             def producer():

@@ -23,6 +23,7 @@ RNG_CONF_NOISE = 2
 RNG_PARAM_INIT = 3
 RNG_RFF_FREQ = 4
 RNG_DROPOUT = 5
+RNG_SAMPLE = 6
 
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):
