@@ -70,12 +70,15 @@ __device__ __forceinline__ void load8(const void* X, size_t off, float* f) {
 }
 
 // Sum the rows X[col[e]] for e in [e0, e1) into acc (8 features at f0).
-template <int L, int XBF, int U = 4>
+// CS: gathered row j is scaled by cscale[j] (the column half of a symmetric
+// normalisation, when the producer of X did not fold it in)
+template <int L, int XBF, int U = 4, bool CS = false>
 __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const void* __restrict__ X,
                                            int e0, int e1, int ldx, int f0, bool fv, int sub_base,
-                                           int sl, float* acc) {
+                                           int sl, float* acc, const float* __restrict__ cscale = nullptr) {
   for (int e = e0; e < e1; e += L) {
     const int myj = (e + sl < e1) ? col[e + sl] : 0;
+    const float mycs = CS ? cscale[myj] : 1.f;
     const int cnt = min(L, e1 - e);
     int k = 0;
     if (U == 8 && L >= 8) {
@@ -83,13 +86,23 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
         int j[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) j[u] = __shfl(myj, sub_base + k + u, 64);
+        float c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c[u] = CS ? __shfl(mycs, sub_base + k + u, 64) : 1.f;
         if (fv) {
           float a[8][8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) load8<XBF>(X, (size_t)j[u] * ldx + f0, a[u]);
+          if (CS) {
 #pragma unroll
-          for (int q = 0; q < 8; ++q)
-            acc[q] += ((a[0][q] + a[1][q]) + (a[2][q] + a[3][q])) + ((a[4][q] + a[5][q]) + (a[6][q] + a[7][q]));
+            for (int q = 0; q < 8; ++q)
+              acc[q] += (fmaf(c[0], a[0][q], c[1] * a[1][q]) + fmaf(c[2], a[2][q], c[3] * a[3][q])) +
+                        (fmaf(c[4], a[4][q], c[5] * a[5][q]) + fmaf(c[6], a[6][q], c[7] * a[7][q]));
+          } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              acc[q] += ((a[0][q] + a[1][q]) + (a[2][q] + a[3][q])) + ((a[4][q] + a[5][q]) + (a[6][q] + a[7][q]));
+          }
         }
       }
     }
@@ -98,23 +111,33 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
       const int j1 = __shfl(myj, sub_base + k + 1, 64);
       const int j2 = __shfl(myj, sub_base + k + 2, 64);
       const int j3 = __shfl(myj, sub_base + k + 3, 64);
+      const float c0 = CS ? __shfl(mycs, sub_base + k + 0, 64) : 1.f;
+      const float c1 = CS ? __shfl(mycs, sub_base + k + 1, 64) : 1.f;
+      const float c2 = CS ? __shfl(mycs, sub_base + k + 2, 64) : 1.f;
+      const float c3 = CS ? __shfl(mycs, sub_base + k + 3, 64) : 1.f;
       if (fv) {
         float a[8], b[8], c[8], d[8];
         load8<XBF>(X, (size_t)j0 * ldx + f0, a);
         load8<XBF>(X, (size_t)j1 * ldx + f0, b);
         load8<XBF>(X, (size_t)j2 * ldx + f0, c);
         load8<XBF>(X, (size_t)j3 * ldx + f0, d);
+        if (CS) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] += (a[q] + b[q]) + (c[q] + d[q]);
+          for (int q = 0; q < 8; ++q) acc[q] += fmaf(c0, a[q], c1 * b[q]) + fmaf(c2, c[q], c3 * d[q]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] += (a[q] + b[q]) + (c[q] + d[q]);
+        }
       }
     }
     for (; k < cnt; ++k) {
       const int j = __shfl(myj, sub_base + k, 64);
+      const float cj = CS ? __shfl(mycs, sub_base + k, 64) : 1.f;
       if (fv) {
         float a[8];
         load8<XBF>(X, (size_t)j * ldx + f0, a);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] += a[q];
+        for (int q = 0; q < 8; ++q) acc[q] = CS ? fmaf(cj, a[q], acc[q]) : acc[q] + a[q];
       }
     }
   }
@@ -122,12 +145,12 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
 
 }  // namespace
 
-template <int L, int XBF, int YBF, int U>
+template <int L, int XBF, int YBF, int U, bool CS>
 __global__ __launch_bounds__(256) void spmm_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
     void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
     int n_rows, int F, int ldx, int ldy, int relu, int unit_col, int wcols,
-    const float* __restrict__ init, int ldi) {
+    const float* __restrict__ init, int ldi, const float* __restrict__ cscale) {
   // init (optional, fp32 [n_rows][ldi]): partial sums of earlier edges (e.g. the
   // rank-local part of a split aggregation), added before the row scale
   // wcols: output columns this launch writes (from its base): the row stride ldy
@@ -142,7 +165,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
   const bool fv = rv && f0 < F;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
-  gather_sum<L, XBF, U>(col, X, e0, e1, ldx, f0, fv, sub * L, sl, acc);
+  gather_sum<L, XBF, U, CS>(col, X, e0, e1, ldx, f0, fv, sub * L, sl, acc, cscale);
   if (!rv || f0 >= wcols) return;
   if (init && fv) {
 #pragma unroll
@@ -380,18 +403,24 @@ static int spmm_unroll() {
 template <int L, int U>
 static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
-                         int relu, int uc, int wc, const float* init, int ldi, hipStream_t st) {
+                         int relu, int uc, int wc, const float* init, int ldi, const float* cs, hipStream_t st) {
   constexpr int RPB = 4 * (64 / L);   // rows per 256-thread block
   dim3 grid((n_rows + RPB - 1) / RPB), block(256);
-#define CGNN_SPMM(XT, YT) hipLaunchKernelGGL((spmm_kernel<L, XT, YT, U>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi)
-  // element-type codes: 0 fp32, 1 bf16, 2 fp16 (fp16 pairs with itself or with fp32)
-  if (xbf == 1 && ybf == 1) CGNN_SPMM(1, 1);
-  else if (xbf == 1 && ybf == 0) CGNN_SPMM(1, 0);
-  else if (xbf == 0 && ybf == 1) CGNN_SPMM(0, 1);
-  else if (xbf == 0 && ybf == 0) CGNN_SPMM(0, 0);
-  else if (xbf == 2 && ybf == 2) CGNN_SPMM(2, 2);
-  else if (xbf == 2 && ybf == 0) CGNN_SPMM(2, 0);
-  else if (xbf == 0 && ybf == 2) CGNN_SPMM(0, 2);
+#define CGNN_SPMM(XT, YT, C) hipLaunchKernelGGL((spmm_kernel<L, XT, YT, U, C>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi, cs)
+  // element-type codes: 0 fp32, 1 bf16, 2 fp16 (fp16 pairs with itself or with fp32);
+  // a column scale is compiled for the same-type pairs only
+  if (cs) {
+    if (xbf == 1 && ybf == 1) CGNN_SPMM(1, 1, true);
+    else if (xbf == 2 && ybf == 2) CGNN_SPMM(2, 2, true);
+    else if (xbf == 0 && ybf == 0) CGNN_SPMM(0, 0, true);
+    else return -5;
+  } else if (xbf == 1 && ybf == 1) CGNN_SPMM(1, 1, false);
+  else if (xbf == 1 && ybf == 0) CGNN_SPMM(1, 0, false);
+  else if (xbf == 0 && ybf == 1) CGNN_SPMM(0, 1, false);
+  else if (xbf == 0 && ybf == 0) CGNN_SPMM(0, 0, false);
+  else if (xbf == 2 && ybf == 2) CGNN_SPMM(2, 2, false);
+  else if (xbf == 2 && ybf == 0) CGNN_SPMM(2, 0, false);
+  else if (xbf == 0 && ybf == 2) CGNN_SPMM(0, 2, false);
   else return -5;
 #undef CGNN_SPMM
   return (int)hipGetLastError();
@@ -400,34 +429,34 @@ static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, voi
 template <int L>
 static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
-                         int relu, int uc, int wc, const float* init, int ldi, hipStream_t st) {
+                         int relu, int uc, int wc, const float* init, int ldi, const float* cs, hipStream_t st) {
   if (spmm_unroll() == 8)
     return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
-                                 ldi, st);
+                                 ldi, cs, st);
   return spmm_dispatch_u<L, 4>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
-                               ldi, st);
+                               ldi, cs, st);
 }
 
 // one launch writing output columns [0, wcols) of its base (wcols <= 512)
 static int spmm_launch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                        const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf, int relu,
-                       int uc, int wc, const float* init, int ldi, hipStream_t st) {
+                       int uc, int wc, const float* init, int ldi, const float* cs, hipStream_t st) {
   const int w = std::max(F, wc);
-  if (w <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, st);
-  if (w <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, st);
-  if (w <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, st);
-  if (w <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, st);
+  if (w <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, st);
+  if (w <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, st);
+  if (w <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, st);
+  if (w <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, st);
   return -1;
 }
 
 extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X, void* Y,
                                const float* rscale, const float* bias, int n_rows, int F, int ldx,
                                int ldy, int xbf, int ybf, int relu, int unit_col, const float* init, int ldi,
-                               hipStream_t st) {
+                               const float* cscale, hipStream_t st) {
   if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
   if (ldy <= 512 && F <= 512)
     return spmm_launch(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, ldy, init,
-                       ldi, st);
+                       ldi, cscale, st);
   // wide rows: column slabs of 512 output columns (16-byte aligned offsets), one
   // launch each; the last slabs also write the padding / ones columns up to ldy
   const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;   // bf16 and fp16 are both 2 bytes
@@ -437,7 +466,7 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
     const int rc = spmm_launch(rowptr, col, (const char*)X + (fc ? c0 * xs : 0), (char*)Y + c0 * ys, rscale,
                                bias && fc ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu,
                                unit_col >= 0 ? unit_col - c0 : -1, wc, init && fc ? init + c0 : nullptr, ldi,
-                               st);
+                               cscale, st);
     if (rc) return rc;
   }
   return 0;

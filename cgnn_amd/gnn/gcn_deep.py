@@ -25,6 +25,13 @@ from .data import GraphData
 from .layers import GCN, NormGraph, aggregate, pad_cols
 
 
+def cross_entropy(logits: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """Mean softmax cross-entropy in fp32 as log-sum-exp minus the target logit
+    (two row reductions; PyTorch's nll_loss reduces with a single workgroup)."""
+    o = logits.float()
+    return (torch.logsumexp(o, 1) - o.gather(1, y[:, None]).squeeze(1)).mean()
+
+
 def _splits(g: GraphData):
     return {k: torch.nonzero(g.mask == v).flatten() for k, v in (("train", 1), ("val", 2), ("test", 3))}
 
@@ -57,7 +64,7 @@ class DeepGCNTrainer:
     def _step(self):
         self.model.train()
         out = self.model(self.x, self.ng)
-        loss = torch.nn.functional.cross_entropy(out[self.idx["train"]].float(), self.y_train)
+        loss = cross_entropy(out[self.idx["train"]], self.y_train)
         self.opt.zero_grad(set_to_none=False)
         loss.backward()
         self.opt.step()
@@ -136,6 +143,8 @@ class GCNInference:
         for k in range(L):
             z = h @ self.W[k]
             if k > 0:
+                # one elementwise pass over the narrow Z is cheaper than a per-edge
+                # column-scale load in the gather (measured: 4.97 vs 5.47 ms on reddit)
                 z = z * self.ng.dinv[:, None].to(z.dtype)
             h = aggregate(z, self.ng, prescaled=True, bias=self.b[k], relu=k < L - 1)
         return h

@@ -2,12 +2,13 @@
 track, not in the reference.
 
 * ``norm_aggregate`` -- ``Y = D^-1/2 (A+I) D^-1/2 X`` on the CSR of A + I.  The
-  column scale is applied to the operand before the gather, the row scale in
-  the SpMM epilogue, so no per-edge value is read.  The normalised adjacency is
+  column scale is applied in the gather (one float per gathered row), the row
+  scale in the SpMM epilogue, so no per-edge value is read.  The normalised adjacency is
   symmetric, so the backward is the same SpMM on the incoming gradient (no
   transposed CSR).
-* ``GCNConv`` -- ``Â (H W) + b`` (transform first: the gathered rows are the
-  narrower of the two widths).
+* ``gcn_layer`` / ``GCNConv`` -- ``act(Â (H W) + b)`` (transform first: the
+  gathered rows are the narrower of the two widths) with the normalisation,
+  bias and ReLU inside the SpMM and a split-K weight gradient.
 * ``GCN`` -- L layers with ReLU + dropout between them.
 
 Everything runs on the same ``ops.spmm`` as the fused 2-layer trainer (HIP on
@@ -46,10 +47,9 @@ def aggregate(x: torch.Tensor, g: NormGraph, prescaled: bool = False, bias=None,
     """act(dinv * (A+I) (dinv * x) + bias) in the storage dtype of x; ``prescaled``:
     x already carries the column scale.  Bias / ReLU run in the SpMM epilogue."""
     F = x.shape[1]
-    xs = x if prescaled else x * g.dinv[:, None].to(x.dtype)
-    xs = pad_cols(xs).contiguous()
+    xs = pad_cols(x).contiguous()
     out = ops.spmm(g.rowptr, g.col, xs, F, rscale=g.dinv, bias=bias, relu=relu, out_dtype=x.dtype,
-                   ld_out=xs.shape[1])
+                   ld_out=xs.shape[1], cscale=None if prescaled else g.dinv)
     return out[:, :F] if out.shape[1] != F else out
 
 
@@ -68,6 +68,49 @@ def norm_aggregate(x: torch.Tensor, g: NormGraph) -> torch.Tensor:
     return _NormAggregate.apply(x, g)
 
 
+class _GCNLayer(torch.autograd.Function):
+    """``act(Â (H W) + b)`` with the normalisation, bias and ReLU inside the SpMM
+    (column scale in the gather, row scale + bias + ReLU in the epilogue).
+    Backward: ReLU mask, ``db = sum dY``, ``dZ = Â dY`` (same SpMM, Â symmetric),
+    ``dW = H^T dZ`` as a split-K batched GEMM (``ops.tall_gemm_tn``), ``dH = dZ W^T``."""
+
+    @staticmethod
+    def forward(ctx, h, W, b, g: NormGraph, relu: bool):
+        Wc = W.to(h.dtype)
+        z = h @ Wc
+        out_dim = z.shape[1]
+        zp = pad_cols(z).contiguous()
+        y = ops.spmm(g.rowptr, g.col, zp, out_dim, rscale=g.dinv, cscale=g.dinv, bias=b.float().contiguous(),
+                     relu=relu, out_dtype=h.dtype, ld_out=zp.shape[1])
+        if y.shape[1] != out_dim:
+            y = y[:, :out_dim]
+        ctx.g, ctx.relu = g, relu
+        ctx.save_for_backward(h, Wc, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, Wc, y = ctx.saved_tensors
+        g = ctx.g
+        dy = dy.contiguous()
+        if ctx.relu:
+            dy = torch.ops.aten.threshold_backward(dy, y, 0)
+        db = dy.float().sum(0)
+        out_dim = dy.shape[1]
+        dyp = pad_cols(dy).contiguous()
+        dz = ops.spmm(g.rowptr, g.col, dyp, out_dim, rscale=g.dinv, cscale=g.dinv, out_dtype=dy.dtype,
+                      ld_out=dyp.shape[1])
+        if dz.shape[1] != out_dim:
+            dz = dz[:, :out_dim]
+        dW = ops.tall_gemm_tn(h, dz)
+        dh = dz @ Wc.t() if ctx.needs_input_grad[0] else None
+        return dh, dW, db, None, None
+
+
+def gcn_layer(h: torch.Tensor, W: torch.Tensor, b: torch.Tensor, g: NormGraph, relu: bool) -> torch.Tensor:
+    return _GCNLayer.apply(h, W, b, g, relu)
+
+
 class GCNConv(torch.nn.Module):
     """``Â (H W) + b``; glorot-uniform W, zero b (the PyG GCNConv initialisation)."""
 
@@ -77,9 +120,8 @@ class GCNConv(torch.nn.Module):
         self.weight = torch.nn.Parameter((torch.rand(in_dim, out_dim, generator=generator) * 2 - 1) * bound)
         self.bias = torch.nn.Parameter(torch.zeros(out_dim))
 
-    def forward(self, h: torch.Tensor, g: NormGraph) -> torch.Tensor:
-        z = h @ self.weight.to(h.dtype)
-        return norm_aggregate(z, g) + self.bias.to(h.dtype)
+    def forward(self, h: torch.Tensor, g: NormGraph, relu: bool = False) -> torch.Tensor:
+        return gcn_layer(h, self.weight, self.bias, g, relu)
 
 
 class GCN(torch.nn.Module):
@@ -96,9 +138,7 @@ class GCN(torch.nn.Module):
         h = x
         L = len(self.convs)
         for k, conv in enumerate(self.convs):
-            h = conv(h, g)
-            if k < L - 1:
-                h = torch.relu(h)
-                if self.training and self.dropout > 0:
-                    h = torch.nn.functional.dropout(h, self.dropout)
+            h = conv(h, g, relu=k < L - 1)
+            if k < L - 1 and self.training and self.dropout > 0:
+                h = torch.nn.functional.dropout(h, self.dropout)
         return h

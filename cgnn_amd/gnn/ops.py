@@ -33,11 +33,12 @@ def dtype_code(dt) -> int:
 
 
 def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dtype=torch.bfloat16,
-         ld_out=None, unit_col=-1, init=None):
-    """Y[i,:F] = act(rscale[i] * (init[i] + sum_{j in N(i)} X[j,:F]) + bias); X is [*, ldx].
+         ld_out=None, unit_col=-1, init=None, cscale=None):
+    """Y[i,:F] = act(rscale[i] * (init[i] + sum_{j in N(i)} cscale[j] X[j,:F]) + bias); X is [*, ldx].
     Padding columns of Y are written 0, except ``unit_col`` which is written 1
     (a ones column that turns the bias gradient into one more GEMM row).
-    ``init`` (optional fp32 [n, >=F]): partial sums of other edges (split aggregation)."""
+    ``init`` (optional fp32 [n, >=F]): partial sums of other edges (split aggregation).
+    ``cscale`` (optional fp32 per source row): a column scale applied in the gather."""
     n = rowptr.numel() - 1
     ldo = ld_out or X.shape[1]
     if out is None:
@@ -49,11 +50,15 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
                      bias.data_ptr() if bias is not None else 0, n, F, X.shape[1], out.shape[1],
                      dtype_code(X.dtype), dtype_code(out.dtype), int(relu), int(unit_col),
                      _st(X), init.data_ptr() if init is not None else 0,
-                     init.shape[1] if init is not None else 0)
+                     init.shape[1] if init is not None else 0,
+                     cscale.data_ptr() if cscale is not None else 0)
         return out
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, F, dtype=torch.float32)
-    acc.index_add_(0, rows, X[col.long(), :F].float())
+    src = X[col.long(), :F].float()
+    if cscale is not None:
+        src = src * cscale[col.long()][:, None]
+    acc.index_add_(0, rows, src)
     if init is not None:
         acc = acc + init[:n, :F].float()
     if rscale is not None:
@@ -109,6 +114,32 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
         G.zero_()
         G[:, :C] = (dl * rscale[:, None]).to(G.dtype)
     return stats, G
+
+
+def tall_gemm_tn(A: torch.Tensor, B: torch.Tensor, chunk: int = 8192) -> torch.Tensor:
+    """A^T B (fp32) for tall A [M, k1], B [M, k2] with tiny k1 x k2: a plain GEMM
+    would give the whole M-long reduction to k1*k2/tile^2 workgroups (16 for
+    256 x 256 on 64 x 64 tiles -- 6 % of the CUs); instead split K into row
+    chunks as ONE batched GEMM with fp32 partials and sum them in fixed order."""
+    M = A.shape[0]
+    S = M // chunk
+    cuda = A.is_cuda
+    out = None
+    if S:
+        a = A[:S * chunk].reshape(S, chunk, A.shape[1]).transpose(1, 2)
+        b = B[:S * chunk].reshape(S, chunk, B.shape[1])
+        if cuda and A.dtype != torch.float32:
+            out = torch.bmm(a, b, out_dtype=torch.float32).sum(0)
+        else:
+            out = torch.bmm(a.float(), b.float()).sum(0)
+    if M > S * chunk:
+        a, b = A[S * chunk:], B[S * chunk:]
+        if cuda and A.dtype != torch.float32:
+            tail = torch.mm(a.t(), b, out_dtype=torch.float32)
+        else:
+            tail = a.float().t() @ b.float()
+        out = tail if out is None else out + tail
+    return out
 
 
 def dropout_keep_mask(rows: int, F: int, p: float, key, step, row0: int = 0) -> torch.Tensor:
