@@ -200,11 +200,15 @@ __global__ __launch_bounds__(256) void spmm_kernel(
 //   stats[block][4 + 64] = {sum train loss, #correct train, #correct valid, #correct test,
 //                           per-class sum of dL/dlogits (= the b2 gradient, mode 0)}
 //   mode 0: also write G[i,:] = rscale[i] * (softmax - onehot) / n_train  (train rows)
+//   gslot (optional): G is COMPACT -- only rows with gslot[i] >= 0 (the train rows, the
+//   only non-zero rows of dL/dlogits) are written, to G[gslot[i]]; the backward then
+//   aggregates over the train columns of the adjacency only
 __global__ __launch_bounds__(256) void spmm_ce_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Z,
     const float* __restrict__ rscale, const float* __restrict__ bias, const int* __restrict__ labels,
     const uint8_t* __restrict__ mask, float* __restrict__ stats, void* __restrict__ G,
-    int n_rows, int C, int ld, int mode, float inv_count, const float* __restrict__ init, int ldi) {
+    int n_rows, int C, int ld, int mode, float inv_count, const float* __restrict__ init, int ldi,
+    const int* __restrict__ gslot) {
   constexpr int L = 8, RPW = 8;
   __shared__ float s_red[4][4];
   __shared__ float s_cls[4][64];
@@ -268,11 +272,12 @@ __global__ __launch_bounds__(256) void spmm_ce_kernel(
     const int c = f0 + q;
     dl[q] = (rv && split == 1 && c < C) ? (ex[q] * inv_se - (c == y ? 1.f : 0.f)) * inv_count : 0.f;
   }
-  if (mode == 0 && rv && f0 < ld) {
+  const int gr = (mode == 0 && rv) ? (gslot ? gslot[row] : row) : -1;
+  if (gr >= 0 && f0 < ld) {
     float gq[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) gq[q] = dl[q] * rs;
-    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(G) + (size_t)row * ld + f0) = f32x8_to_bf16(gq);
+    *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(G) + (size_t)gr * ld + f0) = f32x8_to_bf16(gq);
   }
   // per-class sums over the 8 rows of this wave: lanes with equal sl hold the same classes
 #pragma unroll
@@ -394,6 +399,11 @@ __global__ void cast_bf16_kernel(const float* __restrict__ src, uint16_t* __rest
 static int spmm_unroll() {
   static int u = -1;
   if (u < 0) {
+    // Measured alternative, kept out: a software-pipelined gather (next chunk's column
+    // indices requested early, non-temporal index loads / output stores, 16 raw rows in
+    // flight per lane) ran 30 % SLOWER on the ogbn-products shape (F = 100: 3.43 vs
+    // 2.64 ms; F = 256: 5.49 vs 4.10 ms; F = 47 unchanged) -- the gather is bound by
+    // cache throughput, not by the index round trip.
     const char* e = getenv("CGNN_SPMM_UNROLL");
     u = (e && atoi(e) == 4) ? 4 : 8;
   }
@@ -498,11 +508,11 @@ extern "C" int gnn_launch_relu_dropout_bwd(void* dH, const void* H, long n, floa
 extern "C" int gnn_launch_spmm_ce(const int* rowptr, const int* col, const void* Z,
                                   const float* rscale, const float* bias, const int* labels,
                                   const uint8_t* mask, float* stats, void* G, const float* init, int ldi,
-                                  int n_rows, int C, int ld, int mode, float inv_count,
+                                  int n_rows, int C, int ld, int mode, float inv_count, const int* gslot,
                                   hipStream_t st) {
   if (C > 64 || (ld % 8) || C > ld) return -3;
   hipLaunchKernelGGL(spmm_ce_kernel, dim3(gnn_spmm_ce_blocks(n_rows)), dim3(256), 0, st, rowptr, col,
-                     Z, rscale, bias, labels, mask, stats, G, n_rows, C, ld, mode, inv_count, init, ldi);
+                     Z, rscale, bias, labels, mask, stats, G, n_rows, C, ld, mode, inv_count, init, ldi, gslot);
   return (int)hipGetLastError();
 }
 

@@ -74,9 +74,11 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
     return out
 
 
-def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=None, init=None):
+def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=None, init=None, gslot=None):
     """Layer-2 aggregate + log-softmax + NLL.  Returns (stats[68] summed, G).
-    ``init`` (optional fp32 [n, >=C]): partial sums of other edges."""
+    ``init`` (optional fp32 [n, >=C]): partial sums of other edges.
+    ``gslot`` (optional int32 [n]): G is compact -- row i (a train row, gslot[i] >= 0)
+    goes to G[gslot[i]], other rows (whose dlogits are zero) are not written."""
     n = rowptr.numel() - 1
     ld = Z.shape[1]
     if Z.is_cuda:
@@ -84,11 +86,16 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
         nb = hip.gnn_spmm_ce_blocks(n)
         stats = torch.empty(nb, 68, dtype=torch.float32, device=Z.device)
         if G is None and mode == 0:
+            if gslot is not None:
+                raise ValueError("a compact G (gslot) must be allocated by the caller")
             G = torch.empty(n, ld, dtype=torch.bfloat16, device=Z.device)
+        if gslot is not None and gslot.dtype != torch.int32:
+            raise TypeError("gslot must be int32")
         hip.gnn_spmm_ce(rowptr.data_ptr(), col.data_ptr(), Z.data_ptr(), rscale.data_ptr(), bias.data_ptr(),
                         labels.data_ptr(), mask.data_ptr(), stats.data_ptr(), G.data_ptr() if G is not None else 0,
                         init.data_ptr() if init is not None else 0, init.shape[1] if init is not None else 0,
-                        n, C, ld, mode, float(inv_count), _st(Z))
+                        n, C, ld, mode, float(inv_count), _st(Z),
+                        gslot.data_ptr() if gslot is not None else 0)
         return stats.sum(0), G
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, C, dtype=torch.float32)
@@ -109,10 +116,16 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
     dl = dl * (tr[:, None].float() * inv_count)
     stats[4:4 + C] = dl.sum(0)
     if mode == 0:
-        if G is None:
-            G = torch.zeros(n, ld, dtype=Z.dtype)
-        G.zero_()
-        G[:, :C] = (dl * rscale[:, None]).to(G.dtype)
+        gval = (dl * rscale[:, None]).to(Z.dtype)
+        if gslot is not None:
+            sel = gslot >= 0
+            G[gslot[sel].long(), :C] = gval[sel].to(G.dtype)
+            G[gslot[sel].long(), C:] = 0
+        else:
+            if G is None:
+                G = torch.zeros(n, ld, dtype=Z.dtype)
+            G.zero_()
+            G[:, :C] = gval.to(G.dtype)
     return stats, G
 
 

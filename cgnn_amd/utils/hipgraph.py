@@ -14,6 +14,7 @@ step counters from device memory.
 """
 from __future__ import annotations
 
+import gc
 from typing import Any, Callable, Optional
 
 import torch
@@ -31,9 +32,19 @@ class StepGraph:
         self.out: Any = None
 
     def _capture(self):
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = self.fn()
+        # no garbage collection while capturing: a collected object that owns device
+        # state (an older captured graph and its memory pool, an event) would make a
+        # HIP call that is illegal inside a stream capture and abort the process
+        gc.collect()
+        was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = self.fn()
+        finally:
+            if was_enabled:
+                gc.enable()
 
     def __call__(self):
         if not self.enabled:

@@ -1,0 +1,55 @@
+"""SpMM micro-benchmark on the ogbn-products shape (the three sparse passes of
+the headline GCN epoch): gathered-row widths 100 (layer-1 features) and 47
+(layer-2 logits / their gradient), bf16, with the row pitch either packed to
+8 elements or padded to whole 128-B lines.  Prints one JSON line per variant:
+time per launch and the effective gather rate nnz * row_bytes / t.
+
+    python tools/bench_spmm.py [--scale 1.0] [--reps 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--dataset", default="ogbn-products")
+    a = ap.parse_args()
+    from cgnn_amd.gnn import ops
+    from cgnn_amd.gnn.data import synthetic
+    dev = torch.device("cuda", 0)
+    g = synthetic(a.dataset, seed=0, device=dev, scale=a.scale)
+    n, nnz = g.n, g.nnz
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for F, ld in ((100, 104), (100, 128), (47, 48), (47, 64), (256, 256)):
+        X = torch.randn(n, ld, device=dev).to(torch.bfloat16)
+        Y = torch.empty(n, ld, device=dev, dtype=torch.bfloat16)
+
+        def run():
+            ops.spmm(g.rowptr, g.col, X, F, rscale=g.dinv, out=Y)
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        ev0.record()
+        for _ in range(a.reps):
+            run()
+        ev1.record()
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / a.reps
+        row_b = F * 2
+        print(json.dumps({"F": F, "ld": ld, "ms": round(ms, 4), "nnz": nnz,
+                          "gather_TBps": round(nnz * row_b / ms / 1e9, 3),
+                          "line_TBps": round(nnz * ld * 2 / ms / 1e9, 3),
+                          "x_MB": round(n * ld * 2 / 1e6, 1)}), flush=True)
+        del X, Y
+
+
+if __name__ == "__main__":
+    main()
