@@ -32,7 +32,7 @@ backward (train rows only, padded to the largest rank's count: 1/12 of Z2's
 bytes), plus one all-reduce of the ~40k gradient floats.  The Z2 all-gather
 runs asynchronously on RCCL's stream while the rank aggregates the edges whose
 source rows it owns, the remaining edges are added afterwards through an fp32
-partial; the G all-gather overlaps the next epoch's layer-1 SpMM.
+partial, and so does the next epoch's layer-1 SpMM (parameter-independent).
 """
 from __future__ import annotations
 
@@ -139,7 +139,7 @@ class GCNTrainer:
         self.npad = (n + CHUNK - 1) // CHUNK * CHUNK
         self.AX = torch.zeros(self.npad, self.ldx, **bf)
         # multi-GPU: the layer-1 aggregation of the NEXT epoch is computed into a second
-        # buffer while the backward all-gather is in flight (it does not depend on the
+        # buffer while the forward all-gather of Z2 is in flight (it does not depend on the
         # parameters), then the buffers swap; every epoch still performs its own SpMM
         self.AX_next = torch.zeros_like(self.AX) if self.world > 1 else None
         self._ax_ready = False
@@ -245,8 +245,13 @@ class GCNTrainer:
             torch.mul(y2, self.dinv[:, None], out=y2)
             self.Z2loc[:n] = y2.to(torch.bfloat16)
         if self.world > 1:
+            # the Z2 all-gather is the epoch's one large transfer ([n, 48] bf16, 7/8 of it
+            # inbound at 8 ranks): the rank-local layer-2 edges and, in training, the next
+            # epoch's layer-1 aggregation (parameter-independent) run while it is in flight
             work = torch.distributed.all_gather_into_tensor(self.Z2, self.Z2loc, async_op=True)
             ops.spmm(self.rp_loc, self.col_loc, self.Z2loc, C, out=self.part, out_dtype=torch.float32)
+            if train:
+                self._aggregate_features(self.AX_next)
             work.wait()
             rp, col, init = self.rp_rem, self.col_rem, self.part
         else:
@@ -260,9 +265,7 @@ class GCNTrainer:
     def backward(self, stats):
         n, F, C = self.nloc, self.F, self.C
         if self.world > 1:
-            work = torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc, async_op=True)
-            self._aggregate_features(self.AX_next)     # overlaps the all-gather
-            work.wait()
+            torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc)
         ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
         self.gb2.copy_(stats[4:4 + C])
         if self.fused_bwd:
