@@ -24,6 +24,10 @@
 
 using namespace cgnn;
 
+#ifndef CGNN_SPMM_MINW
+#define CGNN_SPMM_MINW 1
+#endif
+
 namespace {
 
 struct bf16x8 { uint32_t w[4]; };
@@ -51,6 +55,26 @@ __device__ __forceinline__ uint4 f32x8_to_bf16(const float* f) {
 }
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// acc[0..7] += a[0..7] + b[0..7] for two raw bf16x8 rows, two instructions per feature
+// pair instead of four: v_perm_b32 pairs feature f of both rows into one dword, then
+// v_dot2c_f32_bf16 against (1, 1) adds both into the fp32 accumulator
+__device__ __forceinline__ void acc_bf16_pair(float* acc, const uint4 a, const uint4 b) {
+  const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
+  const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t lo = __builtin_amdgcn_perm(bw[w], aw[w], 0x05040100u);   // (a.f, b.f)
+    const uint32_t hi = __builtin_amdgcn_perm(bw[w], aw[w], 0x07060302u);   // (a.f+1, b.f+1)
+    acc[2 * w] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, lo), one, acc[2 * w], false);
+    acc[2 * w + 1] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, hi), one, acc[2 * w + 1], false);
+  }
+}
+
+__device__ __forceinline__ uint4 load_raw16(const void* X, size_t off) {
+  return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(X) + off);
+}
 
 // element types of the gathered / written matrices: 0 = fp32, 1 = bf16, 2 = fp16
 template <int XT>
@@ -89,7 +113,13 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
         float c[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) c[u] = CS ? __shfl(mycs, sub_base + k + u, 64) : 1.f;
-        if (fv) {
+        if (fv && XBF == 1 && !CS) {
+          uint4 r[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) r[u] = load_raw16(X, (size_t)j[u] * ldx + f0);
+#pragma unroll
+          for (int u = 0; u < 8; u += 2) acc_bf16_pair(acc, r[u], r[u + 1]);
+        } else if (fv) {
           float a[8][8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) load8<XBF>(X, (size_t)j[u] * ldx + f0, a[u]);
@@ -115,7 +145,12 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
       const float c1 = CS ? __shfl(mycs, sub_base + k + 1, 64) : 1.f;
       const float c2 = CS ? __shfl(mycs, sub_base + k + 2, 64) : 1.f;
       const float c3 = CS ? __shfl(mycs, sub_base + k + 3, 64) : 1.f;
-      if (fv) {
+      if (fv && XBF == 1 && !CS) {
+        const uint4 r0 = load_raw16(X, (size_t)j0 * ldx + f0), r1 = load_raw16(X, (size_t)j1 * ldx + f0);
+        const uint4 r2 = load_raw16(X, (size_t)j2 * ldx + f0), r3 = load_raw16(X, (size_t)j3 * ldx + f0);
+        acc_bf16_pair(acc, r0, r1);
+        acc_bf16_pair(acc, r2, r3);
+      } else if (fv) {
         float a[8], b[8], c[8], d[8];
         load8<XBF>(X, (size_t)j0 * ldx + f0, a);
         load8<XBF>(X, (size_t)j1 * ldx + f0, b);
@@ -146,7 +181,7 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
 }  // namespace
 
 template <int L, int XBF, int YBF, int U, bool CS>
-__global__ __launch_bounds__(256) void spmm_kernel(
+__global__ __launch_bounds__(256, CGNN_SPMM_MINW) void spmm_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
     void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
     int n_rows, int F, int ldx, int ldy, int relu, int unit_col, int wcols,
@@ -203,7 +238,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
 //   gslot (optional): G is COMPACT -- only rows with gslot[i] >= 0 (the train rows, the
 //   only non-zero rows of dL/dlogits) are written, to G[gslot[i]]; the backward then
 //   aggregates over the train columns of the adjacency only
-__global__ __launch_bounds__(256) void spmm_ce_kernel(
+__global__ __launch_bounds__(256, 8) void spmm_ce_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Z,
     const float* __restrict__ rscale, const float* __restrict__ bias, const int* __restrict__ labels,
     const uint8_t* __restrict__ mask, float* __restrict__ stats, void* __restrict__ G,
