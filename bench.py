@@ -37,7 +37,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--feat-noise", type=float, default=4.0)
     ap.add_argument("--label-noise", type=float, default=0.25)
-    ap.add_argument("--align", action="store_true", help="pad gathered rows to 128 B lines")
+    ap.add_argument("--rows", choices=["auto", "aligned", "packed"], default="auto",
+                    help="row pitch of gathered matrices: whole 128-B lines, packed to 8 elements, "
+                         "or auto (features aligned; layer-2 rows aligned on one GPU only)")
     ap.add_argument("--no-fused", action="store_true", help="hipBLASLt GEMMs + separate epilogues")
     a = ap.parse_args()
 
@@ -59,7 +61,7 @@ def main():
     g = synthetic(a.dataset, seed=a.seed, device=dev, scale=a.scale, feat_noise=a.feat_noise,
                   label_noise=a.label_noise)
     tr = GCNTrainer(g, hidden=a.hidden, dropout=a.dropout, lr=a.lr, seed=a.seed,
-                    fused=not a.no_fused, align_rows=a.align)
+                    fused=not a.no_fused, align_rows={'auto': None, 'aligned': True, 'packed': False}[a.rows])
     n_nodes, nnz = g.n, g.nnz
     del g
     torch.cuda.synchronize()

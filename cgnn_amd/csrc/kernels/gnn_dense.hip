@@ -32,7 +32,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int WAVES = 8;            // 512-thread blocks: 2 waves per SIMD share the LDS weights
+constexpr int WAVES = 16;           // 1024-thread blocks: 4 waves per SIMD share the LDS weights
 constexpr int TILE = 32;
 
 __device__ __forceinline__ bf16x8 load_bf16x8(const uint16_t* p) {
@@ -276,7 +276,9 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
   const int t = tid >> 6;                     // this wave's hidden block
   const int n_tiles = (n + TILE - 1) / TILE;
   const float scale = 1.f / (1.f - p);
-  const int xch = ldx / 8, ych = ldc / 8;     // 16-byte chunks per row
+  // 16-byte chunks staged per row: the K columns the products read (a row pitch wider
+  // than that -- rows padded to whole cache lines -- is not staged)
+  const int xch = min(ldx, KP) / 8, ych = min(ldc, CP) / 8;
 
   f32x16 g1[KF / 32], g2[2];
 #pragma unroll
@@ -485,9 +487,10 @@ extern "C" int gnn_fused_bwd_blocks(int n) {
   return std::max(1, std::min(cus, tiles));
 }
 
-// width of one gpart row (gW1^T columns padded to whole 32-tiles, then 64 for gW2)
-extern "C" int gnn_fused_bwd_width(int ldx) {
-  const int KP = (ldx + 15) / 16 * 16;
+// width of one gpart row (gW1^T columns padded to whole 32-tiles, then 64 for gW2);
+// K = F + 1 (features and the ones column)
+extern "C" int gnn_fused_bwd_width(int K) {
+  const int KP = (K + 15) / 16 * 16;
   return (KP + 31) / 32 * 32 + 64;
 }
 
@@ -508,9 +511,11 @@ static int fused_bwd_launch(const uint16_t* AX, const uint16_t* dY2, const float
   return (int)hipGetLastError();
 }
 
-extern "C" int gnn_fused_bwd_supported(int ldx, int HD, int ldc) {
-  const int KS = (ldx + 15) / 16, KC = (ldc + 15) / 16;
-  if (ldc % 8 || ldx % 8 || ldc > 64) return 0;
+// K = F + 1 (features and the ones column), C classes; the row pitches only need to
+// cover them (multiples of 8)
+extern "C" int gnn_fused_bwd_supported(int K, int HD, int C) {
+  const int KS = (K + 15) / 16, KC = (C + 15) / 16;
+  if (C > 64) return 0;
   if (HD == 256) return (KS == 4 || KS == 7 || KS == 8) && (KC == 3 || KC == 4);
   if (HD == 128) return ((KS == 7 || KS == 8 || KS == 4) && KC == 3) || (KS == 8 && KC == 4);
   return 0;
@@ -523,9 +528,9 @@ extern "C" int gnn_launch_fused_bwd(const void* AX, const void* dY2, const float
                                     const float* W2, float* gpart, int n, int F, int ldx, int HD, int C,
                                     int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t row0,
                                     hipStream_t st) {
-  if (C > 64 || ldc % 8 || ldx % 8 || ldc > 64 || F + 1 > ldx) return -3;
+  if (C > 64 || ldc % 8 || ldx % 8 || C > ldc || F + 1 > ldx) return -3;
   const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
-  const int KS = (ldx + 15) / 16, KC = (ldc + 15) / 16;
+  const int KS = (F + 1 + 15) / 16, KC = (C + 15) / 16;
   auto* ax = (const uint16_t*)AX;
   auto* dy = (const uint16_t*)dY2;
 #define FB(ks, kc, hd) if (KS == ks && KC == kc && HD == hd) return fused_bwd_launch<ks, kc, hd>(ax, dy, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, st);

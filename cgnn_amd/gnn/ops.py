@@ -229,8 +229,10 @@ def dense_bwd(dY2, W2, H1, dP1, p):
     return True
 
 
-def fused_bwd_supported(ldx, hidden, ldc):
-    return bool(native.hip().gnn_fused_bwd_supported(int(ldx), int(hidden), int(ldc)))
+def fused_bwd_supported(F, hidden, C):
+    """Whether a compiled fused-backward variant covers F features (+ the ones column),
+    ``hidden`` units and C classes (the row pitches only need to cover them)."""
+    return bool(native.hip().gnn_fused_bwd_supported(int(F) + 1, int(hidden), int(C)))
 
 
 def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None):
@@ -240,7 +242,7 @@ def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None):
     hip = native.hip()
     HD, C = W1.shape[1], W2.shape[1]
     ldx = AX.shape[1]
-    nb, width = hip.gnn_fused_bwd_blocks(n), hip.gnn_fused_bwd_width(ldx)
+    nb, width = hip.gnn_fused_bwd_blocks(n), hip.gnn_fused_bwd_width(F + 1)
     if gpart is None or gpart.shape != (nb, HD, width):
         gpart = torch.empty(nb, HD, width, dtype=torch.float32, device=AX.device)
     rc = hip.gnn_fused_bwd(AX.data_ptr(), dY2.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),

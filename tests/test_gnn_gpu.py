@@ -134,13 +134,14 @@ def test_gcn_learns_products_shape_small():
     assert res["val_acc"] > 0.3, res
 
 
-@pytest.mark.parametrize("HD,p,row0", [(256, 0.5, 0), (256, 0.0, 0), (128, 0.5, 4096)])
-def test_fused_backward_matches_reference(HD, p, row0):
+@pytest.mark.parametrize("HD,p,row0,ldx,ldc", [(256, 0.5, 0, 104, 48), (256, 0.0, 0, 104, 48),
+                                              (128, 0.5, 4096, 104, 48), (256, 0.5, 0, 128, 64)])
+def test_fused_backward_matches_reference(HD, p, row0, ldx, ldc):
     """Fused dense backward (H1 recomputed from AX, weight gradients contracted over the
-    rows in the same pass) vs the unfused math on CPU with the same dropout mask."""
+    rows in the same pass) vs the unfused math on CPU with the same dropout mask; row
+    pitches packed to 8 elements or padded to whole 128-B lines."""
     torch.manual_seed(3)
     n, F, C = 1000, 100, 47
-    ldx, ldc = 104, 48
     AX = torch.zeros(n, ldx)
     AX[:, :F] = torch.randn(n, F) * 0.5
     AX[:, F] = 1.0                                   # ones column -> gb1
@@ -152,7 +153,7 @@ def test_fused_backward_matches_reference(HD, p, row0):
     b1 = torch.randn(HD) * 0.1
     W2 = torch.randn(HD, C) * 0.1
     key, step = (123, 456), 7
-    assert ops.fused_bwd_supported(ldx, HD, ldc)
+    assert ops.fused_bwd_supported(F, HD, C)
     gW1, gb1, gW2, _ = ops.fused_bwd(AX.cuda(), dY2.cuda(), W1.cuda(), b1.cuda(), W2.cuda(), n, F, p, key, step,
                                      row0)
     # reference: same bf16 roundings as the kernel (operands, H1 and dP1 images)
