@@ -72,6 +72,26 @@ __device__ __forceinline__ void acc_bf16_pair(float* acc, const uint4 a, const u
   }
 }
 
+// the same for fp16 rows (v_dot2_f32_f16)
+__device__ __forceinline__ void acc_f16_pair(float* acc, const uint4 a, const uint4 b) {
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  const f16x2 one = {(_Float16)1.0f, (_Float16)1.0f};
+  const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t lo = __builtin_amdgcn_perm(bw[w], aw[w], 0x05040100u);
+    const uint32_t hi = __builtin_amdgcn_perm(bw[w], aw[w], 0x07060302u);
+    acc[2 * w] = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, lo), one, acc[2 * w], false);
+    acc[2 * w + 1] = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, hi), one, acc[2 * w + 1], false);
+  }
+}
+
+template <int XT>
+__device__ __forceinline__ void acc_pair(float* acc, const uint4 a, const uint4 b) {
+  if (XT == 1) acc_bf16_pair(acc, a, b);
+  else acc_f16_pair(acc, a, b);
+}
+
 __device__ __forceinline__ uint4 load_raw16(const void* X, size_t off) {
   return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(X) + off);
 }
@@ -113,12 +133,12 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
         float c[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) c[u] = CS ? __shfl(mycs, sub_base + k + u, 64) : 1.f;
-        if (fv && XBF == 1 && !CS) {
+        if (fv && XBF != 0 && !CS) {
           uint4 r[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) r[u] = load_raw16(X, (size_t)j[u] * ldx + f0);
 #pragma unroll
-          for (int u = 0; u < 8; u += 2) acc_bf16_pair(acc, r[u], r[u + 1]);
+          for (int u = 0; u < 8; u += 2) acc_pair<XBF>(acc, r[u], r[u + 1]);
         } else if (fv) {
           float a[8][8];
 #pragma unroll
@@ -145,11 +165,11 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
       const float c1 = CS ? __shfl(mycs, sub_base + k + 1, 64) : 1.f;
       const float c2 = CS ? __shfl(mycs, sub_base + k + 2, 64) : 1.f;
       const float c3 = CS ? __shfl(mycs, sub_base + k + 3, 64) : 1.f;
-      if (fv && XBF == 1 && !CS) {
+      if (fv && XBF != 0 && !CS) {
         const uint4 r0 = load_raw16(X, (size_t)j0 * ldx + f0), r1 = load_raw16(X, (size_t)j1 * ldx + f0);
         const uint4 r2 = load_raw16(X, (size_t)j2 * ldx + f0), r3 = load_raw16(X, (size_t)j3 * ldx + f0);
-        acc_bf16_pair(acc, r0, r1);
-        acc_bf16_pair(acc, r2, r3);
+        acc_pair<XBF>(acc, r0, r1);
+        acc_pair<XBF>(acc, r2, r3);
       } else if (fv) {
         float a[8], b[8], c[8], d[8];
         load8<XBF>(X, (size_t)j0 * ldx + f0, a);
