@@ -286,7 +286,11 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
   g2[0] = f32x16{};
   g2[1] = f32x16{};
 
-  // prefetch registers: chunks tid, tid + NT, ... of the AX tile and of the dY2 tile
+  // prefetch registers: chunks tid, tid + NT, ... of the AX tile and of the dY2 tile.
+  // Chunk i is row i % 32, 16-byte column chunk i / 32: consecutive lanes take
+  // consecutive rows, so the transposed image writes ([column][row], 2 bytes) of a
+  // wave land in consecutive bytes -- with row-major chunk order every lane of a wave
+  // hit the same LDS bank (32-way conflicts, 18 % of the kernel's wave cycles)
   constexpr int PFX = (TILE * (KP / 8) + NT - 1) / NT, PFY = (TILE * (CP / 8) + NT - 1) / NT;
   uint4 pax[PFX], pdy[PFY];
   auto prefetch = [&](int tile) {
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < PFX; ++k) {
       const int i = tid + k * NT;
-      const int rr = i / xch, ch = i - rr * xch;
+      const int rr = i % TILE, ch = i / TILE;
       pax[k] = (i < TILE * xch && r0 + rr < n)
                    ? *reinterpret_cast<const uint4*>(AX + (size_t)(r0 + rr) * ldx + 8 * ch)
                    : make_uint4(0u, 0u, 0u, 0u);
@@ -302,7 +306,7 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < PFY; ++k) {
       const int i = tid + k * NT;
-      const int rr = i / ych, ch = i - rr * ych;
+      const int rr = i % TILE, ch = i / TILE;
       pdy[k] = (i < TILE * ych && r0 + rr < n)
                    ? *reinterpret_cast<const uint4*>(dY2 + (size_t)(r0 + rr) * ldc + 8 * ch)
                    : make_uint4(0u, 0u, 0u, 0u);
@@ -317,7 +321,7 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
     for (int k = 0; k < PFX; ++k) {
       const int i = tid + k * NT;
       if (i < TILE * xch) {
-        const int rr = i / xch, ch = i - rr * xch;
+        const int rr = i % TILE, ch = i / TILE;
         *reinterpret_cast<uint4*>(sAX + rr * AXS + 8 * ch) = pax[k];
         const uint32_t w[4] = {pax[k].x, pax[k].y, pax[k].z, pax[k].w};
 #pragma unroll
@@ -328,7 +332,7 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
     for (int k = 0; k < PFY; ++k) {
       const int i = tid + k * NT;
       if (i < TILE * ych) {
-        const int rr = i / ych, ch = i - rr * ych;
+        const int rr = i % TILE, ch = i / TILE;
         *reinterpret_cast<uint4*>(sDY + rr * DYS + 8 * ch) = pdy[k];
         const uint32_t w[4] = {pdy[k].x, pdy[k].y, pdy[k].z, pdy[k].w};
 #pragma unroll
