@@ -14,8 +14,9 @@ Two training modes:
 
 The aggregation is the same CSR gather-sum kernel as the GCN (``spmm_kernel``);
 its backward is the transposed block SpMM, for which the transposed CSR is built
-on the device with a stable sort -- deterministic, no atomics.  Dense parts are
-hipBLASLt GEMMs through PyTorch autograd.
+on the device with a stable sort -- deterministic, no atomics.  The two linear
+maps of a layer are one hipBLASLt GEMM on bf16 operands (fp32 accumulation) and
+the weight gradient runs split-K (``_SageLinear``).
 """
 from __future__ import annotations
 
@@ -36,11 +37,13 @@ def transpose_csr(rowptr: torch.Tensor, col: torch.Tensor, n_cols: int, with_per
     """CSR of the transpose (rows = former columns), deterministic (stable sort);
     ``with_perm`` also returns, per transposed edge, the original edge index."""
     n_rows = rowptr.numel() - 1
+    # sizes known on the host (nnz, n_cols): no device-to-host synchronisation
     rows = torch.repeat_interleave(torch.arange(n_rows, device=col.device, dtype=torch.int32),
-                                   (rowptr[1:] - rowptr[:-1]).long())
+                                   (rowptr[1:] - rowptr[:-1]).long(), output_size=col.numel())
     order = torch.sort(col.long(), stable=True).indices
     col_t = rows[order].to(torch.int32)
-    counts = torch.bincount(col.long(), minlength=n_cols)
+    counts = torch.zeros(n_cols, dtype=torch.int64, device=col.device)
+    counts.index_add_(0, col.long(), torch.ones_like(col, dtype=torch.int64))
     rp_t = torch.zeros(n_cols + 1, dtype=torch.int64, device=col.device)
     rp_t[1:] = torch.cumsum(counts, 0)
     if with_perm:
@@ -92,6 +95,39 @@ def mean_aggregate(h: torch.Tensor, block: Block) -> torch.Tensor:
     return _MeanAggregate.apply(h, block)
 
 
+class _SageLinear(torch.autograd.Function):
+    """out = [h_dst | agg] @ [W_self; W_neigh] + b as ONE GEMM (K = 2F).
+
+    On a GPU the operands are bf16 (MFMA) with fp32 accumulation and output; the
+    weight gradient [h_dst | agg]^T g is a contraction over all the block's
+    destination rows into a tiny [2F, out] matrix, so it runs split-K
+    (``ops.tall_gemm_tn``: row chunks as one batched GEMM, fixed-order sum) -- as a
+    plain GEMM it gave the whole reduction to a few dozen workgroups (the largest
+    kernel of the mini-batch epoch, 341 us a call).  On the CPU everything is fp32."""
+
+    @staticmethod
+    def forward(ctx, h_dst, agg, w_self, w_neigh, b):
+        lowp = h_dst.is_cuda
+        dt = torch.bfloat16 if lowp else torch.float32
+        X = torch.cat([h_dst.to(dt), agg.to(dt)], 1)
+        W = torch.cat([w_self, w_neigh], 0).to(dt)
+        out = torch.mm(X, W, out_dtype=torch.float32) if lowp else X @ W
+        out += b
+        ctx.save_for_backward(X, W)
+        ctx.F = h_dst.shape[1]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        X, W = ctx.saved_tensors
+        F = ctx.F
+        lowp = X.is_cuda
+        gl = g.to(X.dtype).contiguous()
+        gW = ops.tall_gemm_tn(X, gl, chunk=4096)
+        gX = torch.mm(gl, W.t(), out_dtype=torch.float32) if lowp else gl @ W.t()
+        return gX[:, :F], gX[:, F:], gW[:F], gW[F:], g.sum(0)
+
+
 class SAGE(torch.nn.Module):
     def __init__(self, in_dim: int, hidden: int, out_dim: int, layers: int = 2, dropout: float = 0.5,
                  seed: int = 0):
@@ -110,7 +146,7 @@ class SAGE(torch.nn.Module):
 
     def layer(self, k: int, h: torch.Tensor, block: Block, last: bool):
         agg = mean_aggregate(h, block)
-        out = h[:block.n_dst] @ self.w_self[k] + agg @ self.w_neigh[k] + self.bias[k]
+        out = _SageLinear.apply(h[:block.n_dst], agg, self.w_self[k], self.w_neigh[k], self.bias[k])
         if not last:
             out = torch.relu(out)
             if self.training and self.dropout > 0:
@@ -125,6 +161,8 @@ class SAGE(torch.nn.Module):
             h = self.layer(k, h, blocks[k], k == L - 1)
             if k < L - 1 and h.shape[1] % 8:
                 h = torch.nn.functional.pad(h, (0, 8 - h.shape[1] % 8))
+            if k < L - 1 and h.is_cuda:
+                h = h.to(torch.bfloat16)      # the next SpMM gathers bf16 rows (fp32 sums)
         return h
 
 
@@ -155,6 +193,8 @@ class SAGETrainer:
         if standardize:                       # column z-scores (standard preprocessing)
             x = (x - x.mean(0)) / x.std(0).clamp_min(1e-6)
         self.x = _pad8(x)
+        if self.x.is_cuda:        # gathered features stored bf16 (the GEMMs take bf16 anyway)
+            self.x = self.x.to(torch.bfloat16)
         self.C = g.n_classes
         F = self.x.shape[1]
         # hidden width padded to a multiple of 8 (SpMM row alignment); output padded too

@@ -60,13 +60,20 @@ class DeviceSampler:
         self.rowptr, self.col = rowptr.contiguous(), col.contiguous()
         self.n = rowptr.numel() - 1
         self.fanouts = [int(f) for f in fanouts]
-        if any(f > 64 for f in self.fanouts):
-            raise ValueError("fanout > 64 not supported by the device sampler")
+        if any(f > 64 or f < 1 for f in self.fanouts):
+            raise ValueError("device sampler fanouts must be in 1..64")
         self.key = model_key(seed, "neighbour-sampler")
-        self.map = torch.full((self.n,), -1, dtype=torch.int32, device=rowptr.device)
+        # one spare entry (id n) absorbs the unused tail of the over-allocated pick buffer
+        self.map = torch.full((self.n + 1,), -1, dtype=torch.int32, device=rowptr.device)
+        self.flag = torch.zeros(self.n + 1, dtype=torch.bool, device=rowptr.device)
 
     def sample(self, seeds: torch.Tensor, salt: int) -> Tuple[List[DeviceBlock], torch.Tensor]:
-        """Blocks ordered input layer first, and the input node ids (int64)."""
+        """Blocks ordered input layer first, and the input node ids (int64).
+
+        One host synchronisation per layer (the number of new source nodes): the
+        pick buffer is sized by the fanout bound and its unused tail points at the
+        spare id n; the new sources are the set flags of a node bitmap, read back in
+        increasing id order by ``nonzero`` -- a sort-free unique."""
         hip = native.hip()
         dev = self.rowptr.device
         nodes = seeds.to(device=dev, dtype=torch.int32).contiguous()
@@ -75,22 +82,25 @@ class DeviceSampler:
             nd = nodes.numel()
             nl = nodes.long()
             deg = self.rowptr[nl + 1] - self.rowptr[nl]
-            cnt = deg if fo < 0 else deg.clamp(max=fo)
+            cnt = deg.clamp(max=fo)
             optr = torch.zeros(nd + 1, dtype=torch.int32, device=dev)
             optr[1:] = torch.cumsum(cnt, 0)
-            total = int(optr[-1])
-            out = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+            out = torch.full((max(nd * fo, 1),), self.n, dtype=torch.int32, device=dev)
             lsalt = (int(salt) * 16 + layer) & 0xFFFFFFFF
             hip.gnn_sample_neighbors(self.rowptr.data_ptr(), self.col.data_ptr(), nodes.data_ptr(), nd, fo,
                                      optr.data_ptr(), out.data_ptr(), int(self.key[0]), int(self.key[1]), lsalt,
                                      _st(nodes))
-            out = out[:total]
-            # relabel: destinations keep 0..nd-1, new sources follow in sorted-id order
-            self.map[nl] = torch.arange(nd, dtype=torch.int32, device=dev)
             ol = out.long()
-            new = torch.unique(ol[self.map[ol] < 0])
+            # relabel: destinations keep 0..nd-1, new sources follow in increasing id order
+            self.flag[ol] = True
+            self.flag[nl] = False
+            self.flag[self.n] = False
+            new = torch.nonzero(self.flag).flatten()        # the layer's one host sync
+            total = int(optr[-1])                            # (queue already drained)
+            self.flag[new] = False
+            self.map[nl] = torch.arange(nd, dtype=torch.int32, device=dev)
             self.map[new] = torch.arange(nd, nd + new.numel(), dtype=torch.int32, device=dev)
-            local = self.map[ol]
+            local = self.map[ol[:total]]
             src = torch.cat([nodes, new.to(torch.int32)])
             self.map[src.long()] = -1
             blocks.append(DeviceBlock(optr, local, src.numel()))

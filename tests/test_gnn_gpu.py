@@ -380,3 +380,4 @@ def test_device_sampler_matches_reference():
         nb = set(col[rp[v]:rp[v + 1]].tolist())
         assert len(set(picks.tolist())) == len(picks) and set(picks.tolist()) <= nb
     assert int(ds.map.max()) == -1                   # the relabel map is reset
+    assert not bool(ds.flag.any())                   # and so is the new-source bitmap

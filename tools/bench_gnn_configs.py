@@ -149,7 +149,8 @@ def main():
         res.update(metric="epochs/sec + val-acc, 3-layer GraphSAGE ogbn-products mini-batch DP",
                    value=round(steps / dt, 4), unit="epochs/s", ms_per_step=round(1e3 * dt / steps, 3),
                    seeds_per_s=round(seeds / dt, 1), iterations_per_epoch=per_epoch,
-                   val_acc=round(ev["val_acc"], 4), test_acc=round(ev["test_acc"], 4), dtype="fp32",
+                   val_acc=round(ev["val_acc"], 4), test_acc=round(ev["test_acc"], 4),
+                   dtype="bf16 (fp32 accumulation, fp32 master weights)" if dev.type == "cuda" else "fp32",
                    scaling="strong (fixed global epoch; per-rank batch 1024)",
                    config={"model": "SAGE-3layer-hidden%d" % hidden, "fanouts": [15, 10, 5],
                            "batch_per_rank": 1024, "parallelism": "dp%d" % world, "nodes": g.n})
