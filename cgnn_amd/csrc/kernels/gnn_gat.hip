@@ -44,6 +44,8 @@ __device__ __forceinline__ float leaky(float x) { return x > 0.f ? x : 0.2f * x;
 }  // namespace
 
 // L lanes per row (L * 8 >= K * Fh), G = Fh / 8 lanes per head.
+constexpr int EB = 4;   // edges per online-softmax step (gat_fwd_kernel)
+
 template <int L, int G>
 __global__ __launch_bounds__(256) void gat_fwd_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ Wh,
@@ -62,17 +64,40 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(
   for (int e = e0; e < e1; e += L) {
     const int myj = (e + sl < e1) ? col[e + sl] : 0;
     const int cnt = min(L, e1 - e);
-    for (int q = 0; q < cnt; ++q) {
-      const int j = __shfl(myj, sub * L + q, 64);
-      if (fv) {
-        const float sc = leaky(sd + s_src[(size_t)j * K + k]);
-        float w[8];
-        ld8(Wh + (size_t)j * HF + f0, w);
-        const float mn = fmaxf(m, sc);
-        const float a = __expf(m - mn), b = __expf(sc - mn);
+    // EB edges per step: their rows are requested together, and the online softmax
+    // rescales once per step (EB + 1 exponentials instead of 2 EB)
+    for (int q = 0; q < cnt; q += EB) {
+      int j[EB];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc[u] = fmaf(acc[u], a, b * w[u]);
-        l = fmaf(l, a, b);
+      for (int u = 0; u < EB; ++u) j[u] = __shfl(myj, sub * L + min(q + u, L - 1), 64);
+      if (fv) {
+        float w[EB][8], sc[EB];
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          ld8(Wh + (size_t)j[u] * HF + f0, w[u]);
+          sc[u] = s_src[(size_t)j[u] * K + k];
+        }
+        float mn = m;
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          sc[u] = (q + u < cnt) ? leaky(sd + sc[u]) : -INFINITY;
+          mn = fmaxf(mn, sc[u]);
+        }
+        const float a = __expf(m - mn);
+        float b[EB];
+#pragma unroll
+        for (int u = 0; u < EB; ++u) b[u] = __expf(sc[u] - mn);
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+          float t = acc[f] * a;
+#pragma unroll
+          for (int u = 0; u < EB; ++u) t = fmaf(b[u], w[u][f], t);
+          acc[f] = t;
+        }
+        float ls = l * a;
+#pragma unroll
+        for (int u = 0; u < EB; ++u) ls += b[u];
+        l = ls;
         m = mn;
       }
     }
@@ -116,25 +141,47 @@ __global__ __launch_bounds__(256) void gat_bwd_row_kernel(
   for (int e = e0; e < e1; e += L) {
     const int myj = (e + sl < e1) ? col[e + sl] : 0;
     const int cnt = min(L, e1 - e);
-    for (int q = 0; q < cnt; ++q) {
-      const int j = __shfl(myj, sub * L + q, 64);
-      float w[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      float raw = 0.f;
-      if (fv) {
-        ld8(Wh + (size_t)j * HF + f0, w);
-        raw = sd + s_src[(size_t)j * K + k];
-      }
-      float da = 0.f;
+    for (int q = 0; q < cnt; q += EB) {          // EB edges' rows requested together
+      int j[EB];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) da = fmaf(go[u], w[u], da);
-      da = group_sum<G>(da);                   // SDDMM: dalpha_ij = <dout_i, Wh_j>
+      for (int u = 0; u < EB; ++u) j[u] = __shfl(myj, sub * L + min(q + u, L - 1), 64);
+      float w[EB][8], raw[EB];
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        if (fv) {
+          ld8(Wh + (size_t)j[u] * HF + f0, w[u]);
+          raw[u] = sd + s_src[(size_t)j[u] * K + k];
+        } else {
+#pragma unroll
+          for (int f = 0; f < 8; ++f) w[u][f] = 0.f;
+          raw[u] = 0.f;
+        }
+      }
+      float da[EB];
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        float d = 0.f;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) d = fmaf(go[f], w[u][f], d);
+        da[u] = d;
+      }
+#pragma unroll
+      for (int off = 1; off < G; off <<= 1) {   // SDDMM: dalpha_ij = <dout_i, Wh_j>
+#pragma unroll
+        for (int u = 0; u < EB; ++u) da[u] += __shfl_xor(da[u], off, 64);
+      }
       if (fv) {
-        const float al = __expf(leaky(raw) - ls);
-        const float ds = al * (da - dd) * (raw > 0.f ? 1.f : 0.2f);
-        dsd += ds;
-        if (lead) {
-          alpha_e[(size_t)(e + q) * K + k] = al;
-          dsc_e[(size_t)(e + q) * K + k] = ds;
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          if (q + u < cnt) {
+            const float al = __expf(leaky(raw[u]) - ls);
+            const float ds = al * (da[u] - dd) * (raw[u] > 0.f ? 1.f : 0.2f);
+            dsd += ds;
+            if (lead) {
+              alpha_e[(size_t)(e + q + u) * K + k] = al;
+              dsc_e[(size_t)(e + q + u) * K + k] = ds;
+            }
+          }
         }
       }
     }
@@ -161,16 +208,29 @@ __global__ __launch_bounds__(256) void gat_bwd_col_kernel(
     const int myi = (e + sl < e1) ? col_t[e + sl] : 0;
     const int mye = (e + sl < e1) ? perm[e + sl] : 0;
     const int cnt = min(L, e1 - e);
-    for (int q = 0; q < cnt; ++q) {
-      const int i = __shfl(myi, sub * L + q, 64);
-      const int eo = __shfl(mye, sub * L + q, 64);
-      if (fv) {
-        const float al = alpha_e[(size_t)eo * K + k];
-        float g[8];
-        ld8(dout + (size_t)i * HF + f0, g);
+    for (int q = 0; q < cnt; q += EB) {          // EB edges' rows requested together
+      int i[EB], eo[EB];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc[u] = fmaf(al, g[u], acc[u]);
-        dss += dsc_e[(size_t)eo * K + k];
+      for (int u = 0; u < EB; ++u) {
+        const int src = sub * L + min(q + u, L - 1);
+        i[u] = __shfl(myi, src, 64);
+        eo[u] = __shfl(mye, src, 64);
+      }
+      if (fv) {
+        float g[EB][8], al[EB], dsc[EB];
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          ld8(dout + (size_t)i[u] * HF + f0, g[u]);
+          al[u] = alpha_e[(size_t)eo[u] * K + k];
+          dsc[u] = dsc_e[(size_t)eo[u] * K + k];
+        }
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+          const float a = (q + u < cnt) ? al[u] : 0.f;
+#pragma unroll
+          for (int f = 0; f < 8; ++f) acc[f] = fmaf(a, g[u][f], acc[f]);
+          dss += (q + u < cnt) ? dsc[u] : 0.f;
+        }
       }
     }
   }
@@ -191,7 +251,8 @@ int lanes_for(int HF) {
 
 #define GAT_DISPATCH(KERNEL, ...)                                                                  \
   do {                                                                                             \
-    const int L = lanes_for(HF), G = Fh / 8;                                                       \
+    /* one head: its group is the row's whole sub-group (lanes past HF add 0) */                  \
+    const int L = lanes_for(HF), G = K == 1 ? L : Fh / 8;                                          \
     if (L < 0 || Fh % 8 || HF != K * Fh) return -3;                                                \
     const int rpb = 4 * (64 / L);                                                                  \
     dim3 grid((n + rpb - 1) / rpb), block(256);                                                    \
@@ -213,6 +274,7 @@ int lanes_for(int HF) {
       case 6404: hipLaunchKernelGGL((KERNEL<64, 4>), grid, block, 0, st, __VA_ARGS__); break;      \
       case 6408: hipLaunchKernelGGL((KERNEL<64, 8>), grid, block, 0, st, __VA_ARGS__); break;      \
       case 6416: hipLaunchKernelGGL((KERNEL<64, 16>), grid, block, 0, st, __VA_ARGS__); break;    \
+      case 6464: hipLaunchKernelGGL((KERNEL<64, 64>), grid, block, 0, st, __VA_ARGS__); break;    \
       default: return -1;                                                                          \
     }                                                                                              \
     return (int)hipGetLastError();                                                                 \

@@ -115,8 +115,8 @@ def gat_aggregate(Wh: torch.Tensor, s_src: torch.Tensor, s_dst: torch.Tensor, g:
     if Wh.shape[0] != g.n_cols or s_src.shape[0] != g.n_cols or s_dst.shape[0] != g.n:
         raise ValueError("gat_aggregate: operand rows do not match the graph (%d x %d)" % (g.n, g.n_cols))
     if Wh.is_cuda:
-        if Fh % 8 or (Fh // 8) & (Fh // 8 - 1) or K * Fh > 512:
-            raise ValueError("HIP GAT needs Fh = 8 * 2^m and K * Fh <= 512")
+        if Fh % 8 or (K > 1 and (Fh // 8) & (Fh // 8 - 1)) or K * Fh > 512:
+            raise ValueError("HIP GAT needs Fh % 8 == 0 (8 * 2^m with several heads) and K * Fh <= 512")
         return _GATAggregate.apply(Wh.float(), s_src.float(), s_dst.float(), g, K, Fh)
     return _gat_aggregate_torch(Wh, s_src, s_dst, g, K, Fh)
 
@@ -135,10 +135,14 @@ class GATLayer(torch.nn.Module):
     def forward(self, h, g: GraphCSR, gather=None):
         """``gather`` (graph-sharded training): maps this rank's rows to all rows;
         the source-side [Wh | s_src] goes through ONE collective."""
-        Wh = h @ self.W
-        Whk = Wh.view(-1, self.K, self.Fh)
-        s_src = (Whk * self.a_src).sum(-1)
-        s_dst = (Whk * self.a_dst).sum(-1)
+        # the attention logits are linear in h: fold a_src / a_dst into the weight,
+        # s = h (W a), so [Wh | s_src | s_dst] is ONE GEMM (no [n, K, Fh] temporary,
+        # no broadcast multiply + reduction over all rows)
+        K, KF = self.K, self.K * self.Fh
+        Wk = self.W.view(-1, K, self.Fh)
+        Wcat = torch.cat([self.W, (Wk * self.a_src).sum(-1), (Wk * self.a_dst).sum(-1)], 1)
+        y = h @ Wcat
+        Wh, s_src, s_dst = y[:, :KF], y[:, KF:KF + K], y[:, KF + K:]
         if gather is not None:
             both = gather(torch.cat([Wh, s_src], 1))
             Wh, s_src = both[:, :self.K * self.Fh], both[:, self.K * self.Fh:]
@@ -147,14 +151,13 @@ class GATLayer(torch.nn.Module):
 
 class GAT(torch.nn.Module):
     """2-layer GAT: K heads of width Fh (concatenated, ELU), then one output head
-    whose width is the class count padded to a power-of-two multiple of 8."""
+    whose width is the class count padded to a multiple of 8 (a single head is
+    reduced over the whole row's lanes, so its width need not be a power of two)."""
 
     def __init__(self, in_dim, n_classes, heads=8, head_dim=32, dropout=0.5, seed=0):
         super().__init__()
         gen = torch.Generator().manual_seed(seed)
-        out_w = 8
-        while out_w < n_classes:
-            out_w *= 2
+        out_w = (n_classes + 7) // 8 * 8
         self.C = n_classes
         self.l1 = GATLayer(in_dim, heads, head_dim, gen)
         self.l2 = GATLayer(heads * head_dim, 1, out_w, gen)

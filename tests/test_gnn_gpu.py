@@ -206,7 +206,7 @@ def test_sage_minibatch_learns_gpu():
     assert last < first and res["val_acc"] > 0.3, (first, last, res)
 
 
-@pytest.mark.parametrize("K,Fh", [(4, 16), (1, 64), (8, 32), (3, 8)])
+@pytest.mark.parametrize("K,Fh", [(4, 16), (1, 64), (8, 32), (3, 8), (1, 176), (1, 40)])
 def test_gat_kernels_match_torch_autograd(K, Fh):
     from cgnn_amd.gnn.gat import GraphCSR, gat_aggregate
     n = 700
