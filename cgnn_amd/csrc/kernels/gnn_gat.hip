@@ -28,6 +28,21 @@ __device__ __forceinline__ void ld8(const float* p, float* f) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
 }
+// 8 gathered values of a row stored fp32 (WT = 0) or bf16 (WT = 1), returned as fp32
+template <int WT>
+__device__ __forceinline__ void ldg8(const void* base, size_t off, float* f) {
+  if (WT == 1) {
+    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(base) + off);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f[2 * q] = __uint_as_float(w[q] << 16);
+      f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  } else {
+    ld8(reinterpret_cast<const float*>(base) + off, f);
+  }
+}
 __device__ __forceinline__ void st8(float* p, const float* f) {
   *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
   *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
@@ -46,9 +61,9 @@ __device__ __forceinline__ float leaky(float x) { return x > 0.f ? x : 0.2f * x;
 // L lanes per row (L * 8 >= K * Fh), G = Fh / 8 lanes per head.
 constexpr int EB = 4;   // edges per online-softmax step (gat_fwd_kernel)
 
-template <int L, int G>
+template <int L, int G, int WT>
 __global__ __launch_bounds__(256) void gat_fwd_kernel(
-    const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ Wh,
+    const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Wh,
     const float* __restrict__ s_src, const float* __restrict__ s_dst, float* __restrict__ out,
     float* __restrict__ lse, int n, int K, int HF) {
   constexpr int RPW = 64 / L;
@@ -74,7 +89,7 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(
         float w[EB][8], sc[EB];
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-          ld8(Wh + (size_t)j[u] * HF + f0, w[u]);
+          ldg8<WT>(Wh, (size_t)j[u] * HF + f0, w[u]);
           sc[u] = s_src[(size_t)j[u] * K + k];
         }
         float mn = m;
@@ -110,9 +125,9 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(
   if (f0 % (8 * G) == 0) lse[(size_t)row * K + k] = l > 0.f ? m + __logf(l) : 0.f;
 }
 
-template <int L, int G>
+template <int L, int G, int WT>
 __global__ __launch_bounds__(256) void gat_bwd_row_kernel(
-    const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ Wh,
+    const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Wh,
     const float* __restrict__ s_src, const float* __restrict__ s_dst, const float* __restrict__ out,
     const float* __restrict__ lse, const float* __restrict__ dout, float* __restrict__ alpha_e,
     float* __restrict__ dsc_e, float* __restrict__ ds_dst, int n, int K, int HF) {
@@ -149,7 +164,7 @@ __global__ __launch_bounds__(256) void gat_bwd_row_kernel(
 #pragma unroll
       for (int u = 0; u < EB; ++u) {
         if (fv) {
-          ld8(Wh + (size_t)j[u] * HF + f0, w[u]);
+          ldg8<WT>(Wh, (size_t)j[u] * HF + f0, w[u]);
           raw[u] = sd + s_src[(size_t)j[u] * K + k];
         } else {
 #pragma unroll
@@ -189,10 +204,10 @@ __global__ __launch_bounds__(256) void gat_bwd_row_kernel(
   if (lead) ds_dst[(size_t)row * K + k] = dsd;
 }
 
-template <int L, int G>
+template <int L, int G, int WT>
 __global__ __launch_bounds__(256) void gat_bwd_col_kernel(
     const int* __restrict__ rowptr_t, const int* __restrict__ col_t, const int* __restrict__ perm,
-    const float* __restrict__ alpha_e, const float* __restrict__ dsc_e, const float* __restrict__ dout,
+    const float* __restrict__ alpha_e, const float* __restrict__ dsc_e, const void* __restrict__ dout,
     float* __restrict__ dWh, float* __restrict__ ds_src, int n, int K, int HF) {
   constexpr int RPW = 64 / L;
   const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
@@ -220,7 +235,7 @@ __global__ __launch_bounds__(256) void gat_bwd_col_kernel(
         float g[EB][8], al[EB], dsc[EB];
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-          ld8(dout + (size_t)i[u] * HF + f0, g[u]);
+          ldg8<WT>(dout, (size_t)i[u] * HF + f0, g[u]);
           al[u] = alpha_e[(size_t)eo[u] * K + k];
           dsc[u] = dsc_e[(size_t)eo[u] * K + k];
         }
@@ -249,7 +264,7 @@ int lanes_for(int HF) {
 }
 }  // namespace
 
-#define GAT_DISPATCH(KERNEL, ...)                                                                  \
+#define GAT_DISPATCH(KERNEL, WT, ...)                                                                  \
   do {                                                                                             \
     /* one head: its group is the row's whole sub-group (lanes past HF add 0) */                  \
     const int L = lanes_for(HF), G = K == 1 ? L : Fh / 8;                                          \
@@ -257,49 +272,58 @@ int lanes_for(int HF) {
     const int rpb = 4 * (64 / L);                                                                  \
     dim3 grid((n + rpb - 1) / rpb), block(256);                                                    \
     switch (L * 100 + G) {                                                                         \
-      case 801: hipLaunchKernelGGL((KERNEL<8, 1>), grid, block, 0, st, __VA_ARGS__); break;        \
-      case 802: hipLaunchKernelGGL((KERNEL<8, 2>), grid, block, 0, st, __VA_ARGS__); break;        \
-      case 804: hipLaunchKernelGGL((KERNEL<8, 4>), grid, block, 0, st, __VA_ARGS__); break;        \
-      case 808: hipLaunchKernelGGL((KERNEL<8, 8>), grid, block, 0, st, __VA_ARGS__); break;        \
-      case 1601: hipLaunchKernelGGL((KERNEL<16, 1>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 1602: hipLaunchKernelGGL((KERNEL<16, 2>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 1604: hipLaunchKernelGGL((KERNEL<16, 4>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 1608: hipLaunchKernelGGL((KERNEL<16, 8>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 1616: hipLaunchKernelGGL((KERNEL<16, 16>), grid, block, 0, st, __VA_ARGS__); break;    \
-      case 3202: hipLaunchKernelGGL((KERNEL<32, 2>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 3204: hipLaunchKernelGGL((KERNEL<32, 4>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 3208: hipLaunchKernelGGL((KERNEL<32, 8>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 3216: hipLaunchKernelGGL((KERNEL<32, 16>), grid, block, 0, st, __VA_ARGS__); break;    \
-      case 3232: hipLaunchKernelGGL((KERNEL<32, 32>), grid, block, 0, st, __VA_ARGS__); break;    \
-      case 6404: hipLaunchKernelGGL((KERNEL<64, 4>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 6408: hipLaunchKernelGGL((KERNEL<64, 8>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 6416: hipLaunchKernelGGL((KERNEL<64, 16>), grid, block, 0, st, __VA_ARGS__); break;    \
-      case 6464: hipLaunchKernelGGL((KERNEL<64, 64>), grid, block, 0, st, __VA_ARGS__); break;    \
+      case 801: hipLaunchKernelGGL((KERNEL<8, 1, WT>), grid, block, 0, st, __VA_ARGS__); break;        \
+      case 802: hipLaunchKernelGGL((KERNEL<8, 2, WT>), grid, block, 0, st, __VA_ARGS__); break;        \
+      case 804: hipLaunchKernelGGL((KERNEL<8, 4, WT>), grid, block, 0, st, __VA_ARGS__); break;        \
+      case 808: hipLaunchKernelGGL((KERNEL<8, 8, WT>), grid, block, 0, st, __VA_ARGS__); break;        \
+      case 1601: hipLaunchKernelGGL((KERNEL<16, 1, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
+      case 1602: hipLaunchKernelGGL((KERNEL<16, 2, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
+      case 1604: hipLaunchKernelGGL((KERNEL<16, 4, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
+      case 1608: hipLaunchKernelGGL((KERNEL<16, 8, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
+      case 1616: hipLaunchKernelGGL((KERNEL<16, 16, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
+      case 3202: hipLaunchKernelGGL((KERNEL<32, 2, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
+      case 3204: hipLaunchKernelGGL((KERNEL<32, 4, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
+      case 3208: hipLaunchKernelGGL((KERNEL<32, 8, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
+      case 3216: hipLaunchKernelGGL((KERNEL<32, 16, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
+      case 3232: hipLaunchKernelGGL((KERNEL<32, 32, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
+      case 6404: hipLaunchKernelGGL((KERNEL<64, 4, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
+      case 6408: hipLaunchKernelGGL((KERNEL<64, 8, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
+      case 6416: hipLaunchKernelGGL((KERNEL<64, 16, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
+      case 6464: hipLaunchKernelGGL((KERNEL<64, 64, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
       default: return -1;                                                                          \
     }                                                                                              \
     return (int)hipGetLastError();                                                                 \
   } while (0)
 
 // Wh [n][HF], s_src / s_dst / lse [n][K], HF = K * Fh, Fh % 8 == 0; HF <= 512.
-extern "C" int gnn_launch_gat_fwd(const int* rowptr, const int* col, const float* Wh, const float* s_src,
-                                  const float* s_dst, float* out, float* lse, int n, int K, int Fh,
+// wbf: the gathered matrix (Wh in the forward and the row backward, dout in the
+// column backward) is stored bf16 -- half the bytes of the edge gathers, values
+// widened to fp32 in registers (all arithmetic and every other operand fp32).
+extern "C" int gnn_launch_gat_fwd(const int* rowptr, const int* col, const void* Wh, const float* s_src,
+                                  const float* s_dst, float* out, float* lse, int n, int K, int Fh, int wbf,
                                   hipStream_t st) {
   const int HF = K * Fh;
-  GAT_DISPATCH(gat_fwd_kernel, rowptr, col, Wh, s_src, s_dst, out, lse, n, K, HF);
+  if (wbf) GAT_DISPATCH(gat_fwd_kernel, 1, rowptr, col, Wh, s_src, s_dst, out, lse, n, K, HF);
+  GAT_DISPATCH(gat_fwd_kernel, 0, rowptr, col, Wh, s_src, s_dst, out, lse, n, K, HF);
 }
 
-extern "C" int gnn_launch_gat_bwd_row(const int* rowptr, const int* col, const float* Wh, const float* s_src,
+extern "C" int gnn_launch_gat_bwd_row(const int* rowptr, const int* col, const void* Wh, const float* s_src,
                                       const float* s_dst, const float* out, const float* lse,
                                       const float* dout, float* alpha_e, float* dsc_e, float* ds_dst, int n,
-                                      int K, int Fh, hipStream_t st) {
+                                      int K, int Fh, int wbf, hipStream_t st) {
   const int HF = K * Fh;
-  GAT_DISPATCH(gat_bwd_row_kernel, rowptr, col, Wh, s_src, s_dst, out, lse, dout, alpha_e, dsc_e, ds_dst, n,
+  if (wbf)
+    GAT_DISPATCH(gat_bwd_row_kernel, 1, rowptr, col, Wh, s_src, s_dst, out, lse, dout, alpha_e, dsc_e, ds_dst,
+                 n, K, HF);
+  GAT_DISPATCH(gat_bwd_row_kernel, 0, rowptr, col, Wh, s_src, s_dst, out, lse, dout, alpha_e, dsc_e, ds_dst, n,
                K, HF);
 }
 
 extern "C" int gnn_launch_gat_bwd_col(const int* rowptr_t, const int* col_t, const int* perm,
-                                      const float* alpha_e, const float* dsc_e, const float* dout, float* dWh,
-                                      float* ds_src, int n, int K, int Fh, hipStream_t st) {
+                                      const float* alpha_e, const float* dsc_e, const void* dout, float* dWh,
+                                      float* ds_src, int n, int K, int Fh, int wbf, hipStream_t st) {
   const int HF = K * Fh;
-  GAT_DISPATCH(gat_bwd_col_kernel, rowptr_t, col_t, perm, alpha_e, dsc_e, dout, dWh, ds_src, n, K, HF);
+  if (wbf)
+    GAT_DISPATCH(gat_bwd_col_kernel, 1, rowptr_t, col_t, perm, alpha_e, dsc_e, dout, dWh, ds_src, n, K, HF);
+  GAT_DISPATCH(gat_bwd_col_kernel, 0, rowptr_t, col_t, perm, alpha_e, dsc_e, dout, dWh, ds_src, n, K, HF);
 }

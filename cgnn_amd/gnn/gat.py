@@ -59,39 +59,46 @@ class GraphCSR:
 
 
 class _GATAggregate(torch.autograd.Function):
+    """HIP attention aggregation.  ``lowp``: the edge-gathered matrices (Wh in the
+    forward and the row backward, dout in the column backward) are stored bf16,
+    halving the bytes of every gathered row; scores, softmax statistics, the
+    accumulation and all gradients stay fp32."""
+
     @staticmethod
-    def forward(ctx, Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int):
+    def forward(ctx, Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool):
         hip = native.hip()
         n = g.n
-        Wh, s_src, s_dst = Wh.contiguous(), s_src.contiguous(), s_dst.contiguous()
+        Whg = Wh.to(torch.bfloat16).contiguous() if lowp else Wh.contiguous()
+        s_src, s_dst = s_src.contiguous(), s_dst.contiguous()
         out = torch.empty(n, K * Fh, dtype=torch.float32, device=Wh.device)
         lse = torch.empty(n, K, dtype=torch.float32, device=Wh.device)
-        hip.gnn_gat_fwd(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(),
-                        out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Wh))
-        ctx.save_for_backward(Wh, s_src, s_dst, out, lse)
-        ctx.g, ctx.K, ctx.Fh = g, K, Fh
+        hip.gnn_gat_fwd(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(),
+                        out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Wh), int(lowp))
+        ctx.save_for_backward(Whg, s_src, s_dst, out, lse)
+        ctx.g, ctx.K, ctx.Fh, ctx.lowp = g, K, Fh, lowp
         return out
 
     @staticmethod
     def backward(ctx, dout):
         hip = native.hip()
-        Wh, s_src, s_dst, out, lse = ctx.saved_tensors
-        g, K, Fh = ctx.g, ctx.K, ctx.Fh
-        n, dev = g.n, Wh.device
+        Whg, s_src, s_dst, out, lse = ctx.saved_tensors
+        g, K, Fh, lowp = ctx.g, ctx.K, ctx.Fh, ctx.lowp
+        n, dev = g.n, Whg.device
         dout = dout.contiguous().float()
         alpha_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
         dsc_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
         ds_dst = torch.empty(n, K, dtype=torch.float32, device=dev)
-        hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(),
+        hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(),
                             s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(),
-                            dsc_e.data_ptr(), ds_dst.data_ptr(), n, K, Fh, _st(Wh))
+                            dsc_e.data_ptr(), ds_dst.data_ptr(), n, K, Fh, _st(Whg), int(lowp))
         rp_t, col_t, perm = g.transposed()
-        dWh = torch.empty_like(Wh)                      # [n_cols, K*Fh]: one row per source
+        doutg = dout.to(torch.bfloat16) if lowp else dout
+        dWh = torch.empty(g.n_cols, K * Fh, dtype=torch.float32, device=dev)   # one row per source
         ds_src = torch.empty(g.n_cols, K, dtype=torch.float32, device=dev)
         hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
-                            dsc_e.data_ptr(), dout.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh,
-                            _st(Wh))
-        return dWh, ds_src, ds_dst, None, None, None
+                            dsc_e.data_ptr(), doutg.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh,
+                            _st(Whg), int(lowp))
+        return dWh, ds_src, ds_dst, None, None, None, None
 
 
 def _gat_aggregate_torch(Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int):
@@ -109,15 +116,17 @@ def _gat_aggregate_torch(Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int):
     return out.view(g.n, K * Fh)
 
 
-def gat_aggregate(Wh: torch.Tensor, s_src: torch.Tensor, s_dst: torch.Tensor, g: GraphCSR, K: int, Fh: int):
+def gat_aggregate(Wh: torch.Tensor, s_src: torch.Tensor, s_dst: torch.Tensor, g: GraphCSR, K: int, Fh: int,
+                  lowp: bool = True):
     """Multi-head attention aggregation; Wh [n_cols, K*Fh] fp32, s_src [n_cols, K],
-    s_dst [n, K]; returns [n, K*Fh]."""
+    s_dst [n, K]; returns [n, K*Fh] fp32.  On a GPU ``lowp`` stores the
+    edge-gathered rows bf16 (see ``_GATAggregate``); the CPU path is fp32."""
     if Wh.shape[0] != g.n_cols or s_src.shape[0] != g.n_cols or s_dst.shape[0] != g.n:
         raise ValueError("gat_aggregate: operand rows do not match the graph (%d x %d)" % (g.n, g.n_cols))
     if Wh.is_cuda:
         if Fh % 8 or (K > 1 and (Fh // 8) & (Fh // 8 - 1)) or K * Fh > 512:
             raise ValueError("HIP GAT needs Fh % 8 == 0 (8 * 2^m with several heads) and K * Fh <= 512")
-        return _GATAggregate.apply(Wh.float(), s_src.float(), s_dst.float(), g, K, Fh)
+        return _GATAggregate.apply(Wh.float(), s_src.float(), s_dst.float(), g, K, Fh, bool(lowp))
     return _gat_aggregate_torch(Wh, s_src, s_dst, g, K, Fh)
 
 
