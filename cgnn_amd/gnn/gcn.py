@@ -83,7 +83,8 @@ def _tsgemm(A, B, chunk=CHUNK):
 class GCNTrainer:
     def __init__(self, g: GraphData, hidden: int = 256, dropout: float = 0.5, lr: float = 0.01,
                  weight_decay: float = 0.0, seed: int = 0, rank: Optional[int] = None,
-                 world: Optional[int] = None, fused: bool = True, align_rows: Optional[bool] = None):
+                 world: Optional[int] = None, fused: bool = True, align_rows: Optional[bool] = None,
+                 halo: Optional[bool] = None):
         self.rank = pdist.rank() if rank is None else rank
         self.world = pdist.world_size() if world is None else world
         self.dev = g.rowptr.device
@@ -161,7 +162,19 @@ class GCNTrainer:
         self.W2b = torch.zeros(hidden, self.ldc, **bf)
         self.Z2loc = torch.zeros(per, self.ldc, **bf)
         self.dY2 = torch.zeros(self.npad, self.ldc, **bf)
-        self.Z2 = torch.zeros(per * self.world, self.ldc, **bf) if self.world > 1 else self.Z2loc
+        # Layer-2 source rows of other ranks: a halo exchange (all-to-all of exactly the
+        # rows this rank's edges read) or an all-gather of every row.  On the synthetic
+        # ogbn-products graph the halo is 97 % of the all-gather's rows at 2 ranks, 86 %
+        # at 4 and 66 % at 8, so by default it is used from 4 ranks on.  Needs an
+        # initialised process group (the exchange plan is negotiated at setup).
+        if halo is None:
+            halo = self.world >= 4
+        self.halo = bool(halo) and self.world > 1 and torch.distributed.is_initialized()
+        if self.halo:
+            self._setup_halo(r0, r1, per)
+            self.Z2 = None
+        else:
+            self.Z2 = torch.zeros(per * self.world, self.ldc, **bf) if self.world > 1 else self.Z2loc
         self.epoch = 0
         self.last_stats = None
         # fused MFMA dense kernels (gnn_dense.hip); shapes they do not cover fall back to
@@ -188,6 +201,41 @@ class GCNTrainer:
         a, b = csr(loc, r0)
         c, d = csr(~loc, 0)
         return a, b, c, d
+
+    def _setup_halo(self, r0, r1, per):
+        """Exchange plan of the layer-2 halo: the distinct remote source rows this rank
+        reads (sorted global ids, hence grouped by owner in rank order) are requested
+        from their owners once; each epoch every rank sends the requested rows of its Z2
+        with one all-to-all, and the remote edges index the received buffer."""
+        dist = torch.distributed
+        dev = self.dev
+        col_rem = self.col_rem.long()
+        need = torch.unique(col_rem)                                  # sorted global ids
+        recv_counts = torch.bincount(need // per, minlength=self.world).to(torch.int64)
+        send_counts = torch.empty_like(recv_counts)
+        dist.all_to_all_single(send_counts, recv_counts)
+        rc, sc = [int(v) for v in recv_counts.tolist()], [int(v) for v in send_counts.tolist()]
+        req = torch.empty(sum(sc), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(req, need, output_split_sizes=sc, input_split_sizes=rc)
+        if req.numel() and (int(req.min()) < r0 or int(req.max()) >= r1):
+            raise RuntimeError("halo plan: a peer requested a row this rank does not own")
+        self.send_idx = (req - r0).contiguous()
+        self.recv_splits, self.send_splits = rc, sc
+        self.col_rem = torch.searchsorted(need, col_rem).to(torch.int32).contiguous()
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.Zrecv = torch.zeros(max(sum(rc), 1), self.ldc, **bf)
+        self.Zsend = torch.zeros(max(sum(sc), 1), self.ldc, **bf)
+
+    def _exchange_z2(self):
+        """Start the transfer of the other ranks' layer-2 rows; returns (work, buffer the
+        remote edges index)."""
+        if not self.halo:
+            return torch.distributed.all_gather_into_tensor(self.Z2, self.Z2loc, async_op=True), self.Z2
+        S, R = sum(self.send_splits), sum(self.recv_splits)
+        torch.index_select(self.Z2loc, 0, self.send_idx, out=self.Zsend[:S])
+        work = torch.distributed.all_to_all_single(self.Zrecv[:R], self.Zsend[:S], self.recv_splits,
+                                                   self.send_splits, async_op=True)
+        return work, self.Zrecv
 
     def _train_columns(self, g: GraphData, per: int):
         """Slots of the compact gradient and the local CSR restricted to train columns.
@@ -248,18 +296,18 @@ class GCNTrainer:
             torch.mul(y2, self.dinv[:, None], out=y2)
             self.Z2loc[:n] = y2.to(torch.bfloat16)
         if self.world > 1:
-            # the Z2 all-gather is the epoch's one large transfer ([n, 48] bf16, 7/8 of it
-            # inbound at 8 ranks): the rank-local layer-2 edges and, in training, the next
-            # epoch's layer-1 aggregation (parameter-independent) run while it is in flight
-            work = torch.distributed.all_gather_into_tensor(self.Z2, self.Z2loc, async_op=True)
+            # the Z2 exchange is the epoch's one large transfer (up to [n, 48] bf16, 7/8
+            # of it inbound at 8 ranks): the rank-local layer-2 edges and, in training, the
+            # next epoch's layer-1 aggregation (parameter-independent) run while it is in flight
+            work, zsrc = self._exchange_z2()
             ops.spmm(self.rp_loc, self.col_loc, self.Z2loc, C, out=self.part, out_dtype=torch.float32)
             if train:
                 self._aggregate_features(self.AX_next)
             work.wait()
             rp, col, init = self.rp_rem, self.col_rem, self.part
         else:
-            rp, col, init = self.rowptr, self.col, None
-        stats, _ = ops.spmm_ce(rp, col, self.Z2, C, self.dinv, self.b2, self.y, self.mask,
+            rp, col, init, zsrc = self.rowptr, self.col, None, self.Z2
+        stats, _ = ops.spmm_ce(rp, col, zsrc, C, self.dinv, self.b2, self.y, self.mask,
                                1.0 / max(self.n_train, 1), mode=0 if train else 1,
                                G=self.Gc_loc if train else None, init=init,
                                gslot=self.gslot if train else None)

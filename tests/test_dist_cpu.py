@@ -63,12 +63,13 @@ def test_score_jobs_sharded_equals_single_process():
         np.testing.assert_allclose(out[r], single, rtol=1e-12)   # same noise: exact
 
 
-def _gcn_worker(rank, world, port, out):
+def _gcn_worker(rank, world, port, out, halo=None):
     _init(rank, world, port)
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
     g = synthetic("ogbn-products", seed=0, scale=0.002)
-    tr = GCNTrainer(g, hidden=64)
+    tr = GCNTrainer(g, hidden=64, halo=halo)
+    assert tr.halo == (halo if halo is not None else world >= 4)
     tr.train_step()
     p1 = tr.params.clone().numpy().tolist()
     for _ in range(3):
@@ -78,7 +79,10 @@ def _gcn_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_gcn_row_partition_matches_single_process():
+@pytest.mark.parametrize("world,halo", [(2, False), (2, True), (4, None)])
+def test_gcn_row_partition_matches_single_process(world, halo):
+    """Row-partitioned GCN over gloo ranks == one process; layer-2 rows of other
+    ranks by all-gather or by the halo all-to-all (the default from 4 ranks)."""
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
     g = synthetic("ogbn-products", seed=0, scale=0.002)
@@ -90,16 +94,17 @@ def test_gcn_row_partition_matches_single_process():
     ref = tr.evaluate()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_gcn_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    for r in range(2):
+    mp.spawn(_gcn_worker, args=(world, _free_port(), out, halo), nprocs=world, join=True)
+    for r in range(world):
         res, params, q1 = out[r]
         # after one step the partitioned run equals the single-process one up to the
         # summation order of the split gradients (bf16 activations, fp32 sums)
         np.testing.assert_allclose(np.array(q1), p1, atol=2e-3)
         assert abs(res["train_loss"] - ref["train_loss"]) < 0.02 * ref["train_loss"]
         assert abs(res["val_acc"] - ref["val_acc"]) < 0.06
-    # the two ranks hold bitwise-identical replicated parameters
-    np.testing.assert_array_equal(out[0][1], out[1][1])
+    # the ranks hold bitwise-identical replicated parameters
+    for r in range(1, world):
+        np.testing.assert_array_equal(out[0][1], out[r][1])
 
 
 def _mmd_data():
