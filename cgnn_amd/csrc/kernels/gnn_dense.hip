@@ -376,7 +376,11 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
       sH1t[nn * TR + lr] = bf16_bits(x);
       sDPt[nn * TR + lr] = bf16_bits(d);
     }
-    __syncthreads();
+    // the contraction below reads only this wave's own hidden rows of the H1^T / dP1^T
+    // images: a wave-local ordering of the LDS writes and reads suffices (no block barrier)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 
     // ---- contractions over the tile's 32 rows (two k-steps of 16) ----
 #pragma unroll
