@@ -191,7 +191,7 @@ class GATTrainer:
         self.x = x
         self.g = GraphCSR(gd.rowptr, gd.col, gd.n)
         self.model = GAT(x.shape[1], gd.n_classes, heads, head_dim, dropout, seed).to(self.dev)
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=lr)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=lr, fused=self.dev.type == "cuda")
         self.tr = gd.mask == 1
 
     def train_step(self):
@@ -255,7 +255,7 @@ class ShardedGATTrainer:
             dist.all_reduce(n_train)
         self.n_train = float(n_train.item())
         self.model = GAT(x.shape[1], gd.n_classes, heads, head_dim, dropout, seed).to(self.dev)
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=lr)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=lr, fused=self.dev.type == "cuda")
         self.ddp = None
         self.gather = None
         if self.world > 1:

@@ -84,9 +84,11 @@ class _MeanAggregate(torch.autograd.Function):
     def backward(ctx, g):
         b = ctx.block
         rp_t, col_t = b.transposed()
-        gs = (g * b.inv_deg[:, None]).contiguous()
         F = g.shape[1]
-        return ops.spmm(rp_t, col_t, gs, F, out_dtype=torch.float32, ld_out=F), None
+        # d h_j = sum_{i: j in N(i)} inv_deg[i] g_i: the row scale of the forward becomes
+        # the column scale of the transposed SpMM (applied in the gather)
+        return ops.spmm(rp_t, col_t, g.contiguous(), F, out_dtype=torch.float32, ld_out=F,
+                        cscale=b.inv_deg), None
 
 
 def mean_aggregate(h: torch.Tensor, block: Block) -> torch.Tensor:
@@ -201,7 +203,7 @@ class SAGETrainer:
         self.model = SAGE(F, hidden, self.C, layers, dropout, seed).to(self.dev)
         self.model.w_self[0].data[g.n_features:] = 0
         self.model.w_neigh[0].data[g.n_features:] = 0
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=lr)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=lr, fused=self.dev.type == "cuda")
         self.ddp = None
         if self.world > 1:
             from ..parallel.ddp import GradBucketer
