@@ -41,6 +41,8 @@ def main():
                     help="row pitch of gathered matrices: whole 128-B lines, packed to 8 elements, "
                          "or auto (features aligned; layer-2 rows aligned on one GPU only)")
     ap.add_argument("--no-fused", action="store_true", help="hipBLASLt GEMMs + separate epilogues")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: gloo ranks on the PyTorch path (tests the script's distributed logic only)")
     a = ap.parse_args()
 
     import torch
@@ -49,13 +51,21 @@ def main():
     from cgnn_amd.gnn.data import SHAPES, synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
 
+    cuda = a.device == "cuda"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
-        pdist.init_process_group("nccl")
+        pdist.init_process_group("nccl" if cuda else "gloo")
     rank = pdist.rank()
     local = pdist.local_rank()
-    torch.cuda.set_device(local % torch.cuda.device_count())
-    dev = torch.device("cuda", torch.cuda.current_device())
+    if cuda:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
 
     t_setup = time.perf_counter()
     g = synthetic(a.dataset, seed=a.seed, device=dev, scale=a.scale, feat_noise=a.feat_noise,
@@ -64,17 +74,17 @@ def main():
                     fused=not a.no_fused, align_rows={'auto': None, 'aligned': True, 'packed': False}[a.rows])
     n_nodes, nnz = g.n, g.nnz
     del g
-    torch.cuda.synchronize()
+    sync()
     setup_s = time.perf_counter() - t_setup
 
     for _ in range(a.warmup):
         tr.train_step()
     pdist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         tr.train_step()
-    torch.cuda.synchronize()
+    sync()
     pdist.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -98,7 +108,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if cuda else "fp32 (CPU reference path)",
             "data": "synthetic graph of the %s shape (%d nodes, %d undirected edges, %d features, "
                     "%d classes; planted communities), random-init weights" % (a.dataset, n, m, F, C),
             "config": {"model": "GCN-2layer-hidden%d" % a.hidden, "global_batch": n_nodes,

@@ -1,0 +1,38 @@
+"""bench.py's distributed logic end to end on CPU: gloo ranks launched by
+torch.distributed.run, a tiny graph on the PyTorch path; rank 0 prints the one
+JSON line of the driver contract (the GPU run differs only in device/backend)."""
+import json
+import os
+
+import pytest
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("nproc", [2, 4])      # 4 ranks: the layer-2 halo exchange path
+def test_bench_gloo_ranks_print_one_json_line(nproc):
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(nproc),
+           "--steps", "2", "--warmup", "1", "--device", "cpu", "--scale", "0.002", "--hidden", "64"]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         timeout=600)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    out = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "val_acc"):
+        assert key in out, key
+    assert out["n_gpus"] == nproc and out["steps"] == 2 and out["warmup"] == 1
+    assert out["value"] > 0 and abs(out["value"] * out["ms_per_step"] / 1000.0 - 1.0) < 1e-3
+    assert out["config"]["parallelism"] == "graph-rowpart%d" % nproc
