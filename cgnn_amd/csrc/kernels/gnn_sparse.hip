@@ -334,26 +334,31 @@ __global__ __launch_bounds__(256, 8) void spmm_ce_kernel(
     for (int q = 0; q < 8; ++q) gq[q] = dl[q] * rs;
     *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(G) + (size_t)gr * ld + f0) = f32x8_to_bf16(gq);
   }
-  // per-class sums over the 8 rows of this wave: lanes with equal sl hold the same classes
+  // Loss and per-class dL/dlogits sums are non-zero only on train rows (8 % of
+  // ogbn-products): a wave with none of its 8 rows in the train split skips both
+  // reductions (wave-uniform branch; dl is already zero there).
+  float v0 = 0.f;
+  if (__ballot(rv && split == 1)) {
+    // per-class sums over the 8 rows of this wave: lanes with equal sl hold the same classes
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    float v = dl[q];
-    v += __shfl_xor(v, 8, 64);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    dl[q] = v;
+    for (int q = 0; q < 8; ++q) {
+      float v = dl[q];
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      dl[q] = v;
+    }
+    v0 = wave_sum(my_loss);
   }
   if (lane < 8) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) s_cls[wid][lane * 8 + q] = dl[q];
   }
-  // statistics: one contribution per row (sub-group lane 0), fixed-order block reduce
-  const bool lead = rv && sl == 0;
-  const float hit = (lead && amax == y) ? 1.f : 0.f;
-  float v0 = wave_sum(my_loss);
-  float v1 = wave_sum(split == 1 ? hit : 0.f);
-  float v2 = wave_sum(split == 2 ? hit : 0.f);
-  float v3 = wave_sum(split == 3 ? hit : 0.f);
+  // accuracy counts: one vote per row (sub-group lane 0), counted by ballot + popcount
+  const bool hit = rv && sl == 0 && amax == y;
+  const float v1 = (float)__popcll(__ballot(hit && split == 1));
+  const float v2 = (float)__popcll(__ballot(hit && split == 2));
+  const float v3 = (float)__popcll(__ballot(hit && split == 3));
   if (lane == 0) { s_red[wid][0] = v0; s_red[wid][1] = v1; s_red[wid][2] = v2; s_red[wid][3] = v3; }
   // The LAST wave of the block to finish sums the four partials in fixed order
   // (deterministic) -- no end-of-block barrier, so short rows do not wait for the
