@@ -41,6 +41,7 @@ def main():
                     help="row pitch of gathered matrices: whole 128-B lines, packed to 8 elements, "
                          "or auto (features aligned; layer-2 rows aligned on one GPU only)")
     ap.add_argument("--no-fused", action="store_true", help="hipBLASLt GEMMs + separate epilogues")
+    ap.add_argument("--capture", action="store_true", help="replay the epoch from a hipGraph (one GPU)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: gloo ranks on the PyTorch path (tests the script's distributed logic only)")
     a = ap.parse_args()
@@ -71,7 +72,8 @@ def main():
     g = synthetic(a.dataset, seed=a.seed, device=dev, scale=a.scale, feat_noise=a.feat_noise,
                   label_noise=a.label_noise)
     tr = GCNTrainer(g, hidden=a.hidden, dropout=a.dropout, lr=a.lr, seed=a.seed,
-                    fused=not a.no_fused, align_rows={'auto': None, 'aligned': True, 'packed': False}[a.rows])
+                    fused=not a.no_fused, align_rows={'auto': None, 'aligned': True, 'packed': False}[a.rows],
+                    capture=a.capture)
     n_nodes, nnz = g.n, g.nnz
     del g
     sync()

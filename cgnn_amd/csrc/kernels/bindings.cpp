@@ -64,7 +64,7 @@ int gnn_launch_bias_relu_dropout(void*, const float*, long, int, int, float, uin
 int gnn_launch_relu_dropout_bwd(void*, const void*, long, float, hipStream_t);
 int gnn_launch_dense_fwd(const void*, const float*, const float*, const float*, const float*, void*, void*,
                          int, int, int, int, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t,
-                         hipStream_t);
+                         const int*, hipStream_t);
 int gnn_launch_gat_fwd(const int*, const int*, const void*, const float*, const float*, float*, float*, int,
                        int, int, int, hipStream_t);
 int gnn_launch_gat_bwd_row(const int*, const int*, const void*, const float*, const float*, const float*,
@@ -75,7 +75,8 @@ int gnn_fused_bwd_blocks(int);
 int gnn_fused_bwd_width(int);
 int gnn_fused_bwd_supported(int, int, int);
 int gnn_launch_fused_bwd(const void*, const void*, const float*, const float*, const float*, float*, int, int,
-                         int, int, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, hipStream_t);
+                         int, int, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, const int*,
+                         hipStream_t);
 int gnn_launch_dense_bwd(const void*, const float*, const void*, void*, int, int, int, int, float,
                          hipStream_t);
 }
@@ -234,11 +235,13 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("gnn_dense_fwd", [](uint64_t ax, uint64_t w1, uint64_t b1, uint64_t w2, uint64_t dinv, uint64_t h1,
                             uint64_t z2, int n, int F, int ldx, int HD, int C, int ldc, float p, uint32_t k0,
-                            uint32_t k1, uint32_t step, uint32_t row0, uint64_t st) {
+                            uint32_t k1, uint32_t step, uint32_t row0, uint64_t st, uint64_t stepp) {
     return gnn_launch_dense_fwd(Pt<const void>(ax), Pt<const float>(w1), Pt<const float>(b1), Pt<const float>(w2),
                                 Pt<const float>(dinv), Pt<void>(h1), Pt<void>(z2), n, F, ldx, HD, C, ldc, p, k0,
-                                k1, step, row0, S(st));
-  });
+                                k1, step, row0, Pt<const int>(stepp), S(st));
+  }, py::arg("ax"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("dinv"), py::arg("h1"), py::arg("z2"),
+     py::arg("n"), py::arg("F"), py::arg("ldx"), py::arg("HD"), py::arg("C"), py::arg("ldc"), py::arg("p"),
+     py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"), py::arg("step_ptr") = 0);
   m.def("gnn_dense_bwd", [](uint64_t dy2, uint64_t w2, uint64_t h1, uint64_t dp1, int n, int HD, int C, int ldc,
                             float p, uint64_t st) {
     return gnn_launch_dense_bwd(Pt<const void>(dy2), Pt<const float>(w2), Pt<const void>(h1), Pt<void>(dp1), n,
@@ -273,11 +276,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gnn_fused_bwd_supported", &gnn_fused_bwd_supported);
   m.def("gnn_fused_bwd", [](uint64_t ax, uint64_t dy2, uint64_t w1, uint64_t b1, uint64_t w2, uint64_t gpart, int n,
                             int F, int ldx, int HD, int C, int ldc, float p, uint32_t k0, uint32_t k1,
-                            uint32_t step, uint32_t row0, uint64_t st) {
+                            uint32_t step, uint32_t row0, uint64_t st, uint64_t stepp) {
     return gnn_launch_fused_bwd(Pt<const void>(ax), Pt<const void>(dy2), Pt<const float>(w1), Pt<const float>(b1),
                                 Pt<const float>(w2), Pt<float>(gpart), n, F, ldx, HD, C, ldc, p, k0, k1, step,
-                                row0, S(st));
-  });
+                                row0, Pt<const int>(stepp), S(st));
+  }, py::arg("ax"), py::arg("dy2"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("gpart"), py::arg("n"),
+     py::arg("F"), py::arg("ldx"), py::arg("HD"), py::arg("C"), py::arg("ldc"), py::arg("p"), py::arg("k0"),
+     py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"), py::arg("step_ptr") = 0);
   m.def("gnn_cast_bf16", [](uint64_t src, uint64_t dst, long n, uint64_t st) {
     chk(gnn_launch_cast_bf16(Pt<const float>(src), Pt<void>(dst), n, S(st)), "gnn_cast_bf16");
   });

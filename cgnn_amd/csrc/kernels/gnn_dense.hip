@@ -61,7 +61,10 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
     const uint16_t* __restrict__ AX, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ dinv, uint16_t* __restrict__ H1,
     uint16_t* __restrict__ Z2, int n, int F, int ldx, int C, int ldc, float p, uint32_t k0,
-    uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0) {
+    uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0, const int* __restrict__ stepp) {
+  // stepp (optional): the dropout step read from device memory, so a captured hipGraph
+  // replays with the current epoch's mask
+  if (stepp) step = (uint32_t)*stepp;
   constexpr int KP = KS * 16;
   constexpr int W1S = KP + 8;          // padded row strides (bank-conflict-free b128 / b64 reads)
   constexpr int W2S = HD + 8;
@@ -236,7 +239,8 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
     const uint16_t* __restrict__ AX, const uint16_t* __restrict__ dY2, const float* __restrict__ W1,
     const float* __restrict__ b1, const float* __restrict__ W2, float* __restrict__ gpart, int n, int F,
     int ldx, int C, int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
-    uint32_t row0) {
+    uint32_t row0, const int* __restrict__ stepp) {
+  if (stepp) step = (uint32_t)*stepp;         // device-resident dropout step (graph replays)
   constexpr int NW = HD / 32;                 // waves per block = hidden blocks
   constexpr int NT = NW * 64;
   constexpr int KP = KS * 16;                 // layer-1 K (features + ones column), padded
@@ -431,26 +435,26 @@ template <int KS, int HD>
 static int fwd_launch(const uint16_t* AX, const float* W1, const float* b1, const float* W2,
                       const float* dinv, uint16_t* H1, uint16_t* Z2, int n, int F, int ldx, int C,
                       int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
-                      uint32_t row0, hipStream_t st) {
+                      uint32_t row0, const int* stepp, hipStream_t st) {
   const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KS * 16 + 8) + 64 * (size_t)(HD + 8)) + sizeof(float) * HD;
   (void)hipFuncSetAttribute((const void*)gcn_dense_fwd_kernel<KS, HD>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((gcn_dense_fwd_kernel<KS, HD>), dim3(dense_grid(n)), dim3(WAVES * 64), lds, st, AX, W1,
-                     b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0);
+                     b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp);
   return (int)hipGetLastError();
 }
 
 extern "C" int gnn_launch_dense_fwd(const void* AX, const float* W1, const float* b1, const float* W2,
                                     const float* dinv, void* H1, void* Z2, int n, int F, int ldx,
                                     int HD, int C, int ldc, float p, uint32_t k0, uint32_t k1,
-                                    uint32_t step, uint32_t row0, hipStream_t st) {
+                                    uint32_t step, uint32_t row0, const int* stepp, hipStream_t st) {
   if (C > 64 || ldc % 8 || ldx % 8 || ldc > 64) return -3;
   const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
   const int KS = (F + 15) / 16;
   auto* ax = (const uint16_t*)AX;
   auto* h1 = (uint16_t*)H1;
   auto* z2 = (uint16_t*)Z2;
-#define FWD(ks, hd) if (KS <= ks && HD == hd) return fwd_launch<ks, hd>(ax, W1, b1, W2, dinv, h1, z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, st);
+#define FWD(ks, hd) if (KS <= ks && HD == hd) return fwd_launch<ks, hd>(ax, W1, b1, W2, dinv, h1, z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp, st);
   FWD(4, 256) FWD(7, 256) FWD(8, 256) FWD(4, 128) FWD(8, 128)
 #undef FWD
   return -1;
@@ -506,7 +510,7 @@ template <int KS, int KC, int HD>
 static int fused_bwd_launch(const uint16_t* AX, const uint16_t* dY2, const float* W1, const float* b1,
                             const float* W2, float* gpart, int n, int F, int ldx, int C, int ldc, float p,
                             uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0,
-                            hipStream_t st) {
+                            const int* stepp, hipStream_t st) {
   constexpr int KP = KS * 16, KF = (KP + 31) / 32 * 32, CP = KC * 16, TR = TILE + 8;
   const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KP + 8) + (size_t)HD * (CP + 8) + TILE * (KP + 8) +
                                          TILE * (CP + 8) + (size_t)KF * TR + 64 * TR + 2 * (size_t)HD * TR) +
@@ -515,7 +519,7 @@ static int fused_bwd_launch(const uint16_t* AX, const uint16_t* dY2, const float
   (void)hipFuncSetAttribute((const void*)gcn_fused_bwd_kernel<KS, KC, HD>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((gcn_fused_bwd_kernel<KS, KC, HD>), dim3(gnn_fused_bwd_blocks(n)), dim3(HD * 2), lds, st,
-                     AX, dY2, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0);
+                     AX, dY2, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp);
   return (int)hipGetLastError();
 }
 
@@ -535,13 +539,13 @@ extern "C" int gnn_fused_bwd_supported(int K, int HD, int C) {
 extern "C" int gnn_launch_fused_bwd(const void* AX, const void* dY2, const float* W1, const float* b1,
                                     const float* W2, float* gpart, int n, int F, int ldx, int HD, int C,
                                     int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t row0,
-                                    hipStream_t st) {
+                                    const int* stepp, hipStream_t st) {
   if (C > 64 || ldc % 8 || ldx % 8 || C > ldc || F + 1 > ldx) return -3;
   const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
   const int KS = (F + 1 + 15) / 16, KC = (C + 15) / 16;
   auto* ax = (const uint16_t*)AX;
   auto* dy = (const uint16_t*)dY2;
-#define FB(ks, kc, hd) if (KS == ks && KC == kc && HD == hd) return fused_bwd_launch<ks, kc, hd>(ax, dy, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, st);
+#define FB(ks, kc, hd) if (KS == ks && KC == kc && HD == hd) return fused_bwd_launch<ks, kc, hd>(ax, dy, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp, st);
   FB(7, 3, 256) FB(7, 4, 256) FB(8, 3, 256) FB(8, 4, 256) FB(4, 3, 256) FB(4, 4, 256)
   FB(7, 3, 128) FB(8, 3, 128) FB(4, 3, 128) FB(8, 4, 128)
 #undef FB

@@ -188,24 +188,38 @@ def bias_relu_dropout_(H, bias, F, p, key, step, row0=0):
     return H
 
 
+def _step_args(step):
+    """(scalar step, device pointer): a device int32 tensor is read by the kernel at
+    launch time (hipGraph replays see the current value), an int is passed by value."""
+    if isinstance(step, torch.Tensor):
+        return 0, step.data_ptr()
+    return int(step), 0
+
+
+def _step_value(step):
+    return int(step.item()) if isinstance(step, torch.Tensor) else int(step)
+
+
 def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step, row0=0):
     """H1 = dropout(relu(AX[:, :F] W1 + b1)), Z2 = dinv * (H1 W2) (fused MFMA kernel on GPU).
-    ``H1=None`` (GPU only): H1 is not stored -- the fused backward recomputes it."""
+    ``H1=None`` (GPU only): H1 is not stored -- the fused backward recomputes it.
+    ``step``: the dropout step, an int or a device int32[1] tensor."""
     n = Z2.shape[0]
     HD, C = W1.shape[1], W2.shape[1]
     if AX.is_cuda:
+        sv, sp = _step_args(step)
         rc = native.hip().gnn_dense_fwd(AX.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
                                         dinv.data_ptr(), H1.data_ptr() if H1 is not None else 0,
                                         Z2.data_ptr(), n, F, AX.shape[1],
-                                        HD, C, Z2.shape[1], float(p), int(key[0]), int(key[1]), int(step),
-                                        int(row0), _st(AX))
+                                        HD, C, Z2.shape[1], float(p), int(key[0]), int(key[1]), sv,
+                                        int(row0), _st(AX), step_ptr=sp)
         if rc == 0:
             return True
         if rc != -1:
             raise RuntimeError("gnn_dense_fwd failed (%d)" % rc)
         return False          # shape not covered by a compiled variant
     H1.copy_((AX[:n, :F].float() @ W1.to(torch.bfloat16).float()).to(torch.bfloat16))
-    bias_relu_dropout_(H1, b1, HD, p, key, step, row0)
+    bias_relu_dropout_(H1, b1, HD, p, key, _step_value(step), row0)
     y2 = H1.float() @ W2.to(torch.bfloat16).float()
     Z2.zero_()
     Z2[:, :C] = (y2 * dinv[:n, None]).to(torch.bfloat16)
@@ -245,9 +259,10 @@ def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None):
     nb, width = hip.gnn_fused_bwd_blocks(n), hip.gnn_fused_bwd_width(F + 1)
     if gpart is None or gpart.shape != (nb, HD, width):
         gpart = torch.empty(nb, HD, width, dtype=torch.float32, device=AX.device)
+    sv, sp = _step_args(step)
     rc = hip.gnn_fused_bwd(AX.data_ptr(), dY2.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
                            gpart.data_ptr(), n, F, ldx, HD, C, dY2.shape[1], float(p), int(key[0]), int(key[1]),
-                           int(step), int(row0), _st(AX))
+                           sv, int(row0), _st(AX), step_ptr=sp)
     if rc != 0:
         raise RuntimeError("gnn_fused_bwd failed (%d)" % rc)
     g = gpart.sum(0)                     # fixed-order reduction over the block slabs

@@ -389,3 +389,21 @@ def test_device_sampler_matches_reference():
         assert len(set(picks.tolist())) == len(picks) and set(picks.tolist()) <= nb
     assert int(ds.map.max()) == -1                   # the relabel map is reset
     assert not bool(ds.flag.any())                   # and so is the new-source bitmap
+
+
+def test_gcn_hipgraph_epochs_equal_eager():
+    """The captured one-GPU epoch (replayed hipGraph; dropout step read from the device
+    step counter) is bitwise equal to eager launches, epoch after epoch -- in
+    particular every replay draws a fresh dropout mask."""
+    g = synthetic("ogbn-products", seed=1, device="cuda:0", scale=0.003)
+    eager = GCNTrainer(g, hidden=256, capture=False)
+    graph = GCNTrainer(g, hidden=256, capture=True)
+    assert graph._graph.enabled and not eager._graph.enabled
+    for _ in range(7):                       # 3 warm-up calls, the capture, then replays
+        eager.train_step()
+        graph.train_step()
+    torch.cuda.synchronize()
+    assert graph._graph.graph is not None
+    assert torch.equal(eager.params, graph.params)
+    assert torch.equal(eager.last_stats, graph.last_stats)
+    assert int(graph.step_t.item()) == 7 == graph.epoch
