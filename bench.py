@@ -1,7 +1,7 @@
 """Headline benchmark (BASELINE.json): epochs/sec + val-acc of a 2-layer GCN on
 an ogbn-products-shaped graph, 1/2/4/8 MI355X.
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W          (starts N ranks itself)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -14,12 +14,24 @@ the weight gradients.  W untimed warm-up epochs, then exactly K timed epochs
 bracketed by barrier + device synchronize; the MAX time over ranks is reported.
 """
 import argparse
+import importlib.util
 import json
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def _launcher():
+    """cgnn_amd/parallel/launch.py loaded standalone: the launching parent imports
+    neither torch nor the package, so it cannot initialise a device."""
+    spec = importlib.util.spec_from_file_location(
+        "_cgnn_launch", os.path.join(ROOT, "cgnn_amd", "parallel", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
 
 METRIC = "epochs/sec + val-acc, 2-layer GCN ogbn-products, 1/2/4/8 MI355X"
 
@@ -45,6 +57,11 @@ def main():
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: gloo ranks on the PyTorch path (tests the script's distributed logic only)")
     a = ap.parse_args()
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: start the N ranks here (children re-run this script)
+        sys.exit(_launcher().spawn_ranks(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
@@ -54,12 +71,18 @@ def main():
 
     cuda = a.device == "cuda"
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        sys.exit("bench.py: --gpus %d but the launcher started %d ranks" % (a.gpus, world))
+    if cuda and torch.cuda.device_count() < world:
+        sys.exit("bench.py: --gpus %d but only %d GPUs are visible" % (world, torch.cuda.device_count()))
     if world > 1:
         pdist.init_process_group("nccl" if cuda else "gloo")
+        if pdist.world_size() != world:
+            sys.exit("bench.py: process group has %d ranks, expected %d" % (pdist.world_size(), world))
     rank = pdist.rank()
     local = pdist.local_rank()
     if cuda:
-        torch.cuda.set_device(local % torch.cuda.device_count())
+        torch.cuda.set_device(local)
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")

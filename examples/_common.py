@@ -1,5 +1,5 @@
 """Shared helpers of the example scripts: locate the reference example CSVs
-(the read-only reference checkout, or the untracked .refdata/ staging copy)."""
+(tracked copies in tests/data/, else the read-only reference checkout)."""
 import os
 import sys
 
@@ -11,7 +11,8 @@ if ROOT not in sys.path:
 def data_path(name, override=None):
     if override:
         return override
-    for d in (os.path.join(ROOT, ".refdata"), "/root/reference", os.getcwd()):
+    for d in (os.path.join(ROOT, "tests", "data"), os.path.join(ROOT, ".refdata"), "/root/reference",
+              os.getcwd()):
         p = os.path.join(d, name)
         if os.path.exists(p):
             return p

@@ -8,8 +8,8 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 REF = "/root/reference"
-# reference example CSVs: staged (untracked) into .refdata/ so they reach the GPU box
-DATA = os.path.join(ROOT, ".refdata")
+# reference example CSVs (Example_*.csv, data only), shipped as tracked fixtures
+DATA = os.path.join(ROOT, "tests", "data")
 
 
 def pytest_configure(config):
@@ -28,11 +28,12 @@ def pytest_collection_modifyitems(config, items):
 
 
 def example(name):
-    """Path of an example CSV shipped with the reference (copied into tests/data)."""
-    p = os.path.join(DATA, name)
-    if os.path.exists(p):
-        return p
-    return os.path.join(REF, name)
+    """Path of an example CSV of the reference (tracked copy in tests/data/)."""
+    for d in (DATA, os.path.join(ROOT, ".refdata"), REF):
+        p = os.path.join(d, name)
+        if os.path.exists(p):
+            return p
+    return os.path.join(DATA, name)
 
 
 def have_example(name):
