@@ -31,22 +31,19 @@
 #include <string>
 #include <vector>
 
+#include "rt_common.h"
+
 namespace py = pybind11;
 using i32 = int32_t;
 using i64 = int64_t;
+using cgnn_rt::mix64;
+
+void register_reorder(py::module& m);   // reorder.cpp
 
 namespace {
 
 constexpr int PROG_HDR = 4;
 constexpr int NODE_REC = 8;
-
-// splitmix64: cheap, well-mixed stateless hash used for deterministic sampling
-inline uint64_t mix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
 
 std::vector<int> sweep_order(int n, const std::vector<std::vector<int>>& parents,
                              const std::vector<int>& list_order) {
@@ -204,25 +201,35 @@ py::tuple csr_from_edges(i64 n, py::array_t<i64, py::array::c_style | py::array:
 //   node labels follow the community except for a `label_noise` fraction.
 //   Each node draws a degree from a truncated power law with mean 2m/n; each
 //   edge end goes to the same community with probability `homophily` (a
-//   window of nearby ids inside the community -> locality) and uniformly at
-//   random otherwise.  Features: class centroid + N(0,1) noise (bf16-ready
-//   fp32), so a 2-layer GCN reaches a non-trivial validation accuracy.
+//   window of nearby ids inside the community) and uniformly at random
+//   otherwise.  Features: class centroid + N(0,1) noise (bf16-ready fp32), so a
+//   2-layer GCN reaches a non-trivial validation accuracy.
+//   id_order 0 ("banded") returns the generator's ids, whose homophilous edges
+//   join nearby ids -- locality a real dataset's ids do not hand out for free;
+//   id_order 1 ("shuffled") relabels every node through a seeded bijection of
+//   [0, n) (IdPermutation), so ids carry no information and any locality must be
+//   earned by a reordering pass (reorder.cpp).
 py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophily,
-                          double feat_noise, uint64_t seed, double label_noise) {
+                          double feat_noise, uint64_t seed, double label_noise, int id_order) {
   py::array_t<i64> src_a(m), dst_a(m);
   py::array_t<i32> label_a(n);
   i64* src = src_a.mutable_data();
   i64* dst = dst_a.mutable_data();
   i32* lab = label_a.mutable_data();
+  const cgnn_rt::IdPermutation perm(n, seed ^ 0x5A17ull);
+  auto pid = [&](i64 v) -> i64 { return id_order ? (i64)perm((uint64_t)v) : v; };
   // contiguous communities: class blocks of roughly equal size
   const i64 block = (n + n_class - 1) / n_class;
   std::vector<i32> comm(n);
   for (i64 v = 0; v < n; ++v) comm[v] = (i32)std::min<i64>(v / block, n_class - 1);
   // node label = its community's class, except a `label_noise` fraction drawn uniformly
+  std::vector<i32> lab0(n);
+#pragma omp parallel for schedule(static)
   for (i64 v = 0; v < n; ++v) {
     const uint64_t h = mix64(seed ^ 0x1AB3ull ^ mix64((uint64_t)v));
     const double u = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-    lab[v] = u < label_noise ? (i32)(mix64(h) % (uint64_t)n_class) : comm[v];
+    lab0[v] = u < label_noise ? (i32)(mix64(h) % (uint64_t)n_class) : comm[v];
+    lab[pid(v)] = lab0[v];
   }
   const double mean_deg = (double)m / (double)n;   // edges per source node
 #pragma omp parallel for schedule(static)
@@ -248,8 +255,8 @@ py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophil
     } else {
       t = (i64)(h % (uint64_t)n);
     }
-    src[e] = s;
-    dst[e] = t;
+    src[e] = pid(s);
+    dst[e] = pid(t);
   }
   py::array_t<float> feat_a({(py::ssize_t)n, (py::ssize_t)n_feat});
   float* x = feat_a.mutable_data();
@@ -263,6 +270,7 @@ py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophil
 #pragma omp parallel for schedule(static)
   for (i64 v = 0; v < n; ++v) {
     uint64_t h = mix64(seed ^ 0xFEEDull ^ mix64((uint64_t)v));
+    float* xr = x + (size_t)pid(v) * n_feat;
     for (int f = 0; f < n_feat; f += 2) {
       h = mix64(h);
       const double u1 = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
@@ -270,9 +278,9 @@ py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophil
       const double u2 = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
       const double r = std::sqrt(-2.0 * std::log(u1));
       const double z0 = r * std::cos(6.283185307179586 * u2), z1 = r * std::sin(6.283185307179586 * u2);
-      x[(size_t)v * n_feat + f] = (float)(cent[(size_t)lab[v] * n_feat + f] + feat_noise * z0);
+      xr[f] = (float)(cent[(size_t)lab0[v] * n_feat + f] + feat_noise * z0);
       if (f + 1 < n_feat)
-        x[(size_t)v * n_feat + f + 1] = (float)(cent[(size_t)lab[v] * n_feat + f + 1] + feat_noise * z1);
+        xr[f + 1] = (float)(cent[(size_t)lab0[v] * n_feat + f + 1] + feat_noise * z1);
     }
   }
   return py::make_tuple(src_a, dst_a, feat_a, label_a);
@@ -370,7 +378,16 @@ PYBIND11_MODULE(_rt, m) {
         py::arg("symmetric") = true, py::arg("self_loops") = true, py::arg("dedup") = true);
   m.def("synthetic_graph", &synthetic_graph, py::arg("n"), py::arg("m"), py::arg("n_feat"),
         py::arg("n_class"), py::arg("homophily") = 0.8, py::arg("feat_noise") = 1.0,
-        py::arg("seed") = 0, py::arg("label_noise") = 0.0);
+        py::arg("seed") = 0, py::arg("label_noise") = 0.0, py::arg("id_order") = 0);
   m.def("sample_neighbors", &sample_neighbors);
   m.def("num_threads", []() { return omp_get_max_threads(); });
+  m.def("id_permutation", [](i64 n, uint64_t seed, py::array_t<i64, py::array::c_style | py::array::forcecast> v) {
+    const cgnn_rt::IdPermutation p(n, seed);
+    py::array_t<i64> out(v.size());
+    const i64* a = v.data();
+    i64* o = out.mutable_data();
+    for (py::ssize_t i = 0; i < v.size(); ++i) o[i] = (i64)p((uint64_t)a[i]);
+    return out;
+  }, py::arg("n"), py::arg("seed"), py::arg("ids"));
+  register_reorder(m);
 }

@@ -3,12 +3,20 @@
 There is no network access, so the OGB / Planetoid datasets are replaced by
 synthetic graphs *of the same shape* (nodes, undirected edges, feature width,
 classes, split sizes) from the C++ generator ``_rt.synthetic_graph``: planted
-communities (one per class, contiguous id blocks, as after a graph-partitioning
-reorder), homophilous edges drawn uniformly inside the community, the rest
-uniform over the graph; node labels follow the community except for a
-``label_noise`` fraction, and features = centroid of the node's label + Gaussian
-noise -- so neither the graph nor the features alone determine the label and
-a GCN reaches a realistic (not saturated) accuracy.
+communities (one per class), homophilous edges joining nearby members of the
+community, the rest uniform over the graph; node labels follow the community
+except for a ``label_noise`` fraction, and features = centroid of the node's
+label + Gaussian noise -- so neither the graph nor the features alone determine
+the label and a GCN reaches a non-saturated accuracy (a synthetic-task number,
+not comparable with any real-dataset accuracy).
+
+Node ids: ``id_order="shuffled"`` (default) relabels every node through a seeded
+bijection, so -- as with a real dataset -- ids carry no locality; ``"banded"``
+keeps the generator's ids, whose homophilous edges join nearby ids (locality
+handed out for free, kept only for A/B measurements).  :func:`reorder` is the
+framework's own locality pass (label-propagation clusters laid out by a walk of
+the cluster graph, Cuthill-McKee inside each cluster; ``csrc/runtime/reorder.cpp``)
+that trainers run at setup.
 
 The CSR holds A + I, symmetrised and de-duplicated; the GCN normalisation
 D^-1/2 (A+I) D^-1/2 is kept as the vector ``dinv``.  On a GPU the CSR is built
@@ -88,15 +96,20 @@ def build_csr(n: int, src: np.ndarray, dst: np.ndarray, device=None):
     return torch.from_numpy(np.asarray(rp).astype(np.int32)), torch.from_numpy(np.asarray(col))
 
 
+ID_ORDERS = {"banded": 0, "shuffled": 1}
+
+
 def synthetic(name: str = "ogbn-products", seed: int = 0, device=None, scale: float = 1.0,
-              homophily: float = 0.8, feat_noise: float = 4.0, label_noise: float = 0.25) -> GraphData:
+              homophily: float = 0.8, feat_noise: float = 4.0, label_noise: float = 0.25,
+              id_order: str = "shuffled") -> GraphData:
     """Synthetic graph with the shape of ``name`` (``scale`` shrinks nodes and edges)."""
     n, m, F, C, n_train, n_val = SHAPES[name]
     n = max(int(n * scale), C * 4)
     m = max(int(m * scale), n)
     n_train = max(int(n_train * scale), C)
     n_val = max(int(n_val * scale), C)
-    src, dst, x, y = native.rt().synthetic_graph(n, m, F, C, homophily, feat_noise, seed, label_noise)
+    src, dst, x, y = native.rt().synthetic_graph(n, m, F, C, homophily, feat_noise, seed, label_noise,
+                                                 ID_ORDERS[id_order])
     rowptr, col = build_csr(n, np.asarray(src), np.asarray(dst), device)
     del src, dst
     device = rowptr.device
@@ -122,3 +135,40 @@ def partition_rows(g: GraphData, rank: int, world: int):
     col = g.col[int(rp[0]): int(rp[-1])]
     rp = (rp - rp[0]).to(torch.int32)
     return r0, r1, per, rp, col
+
+
+def locality(g: GraphData, windows=(64, 256, 1024, 4096, 65536), new_id=None):
+    """Fraction of the (non-loop) CSR entries whose endpoints are within w ids, per
+    window w: the reuse a row-ordered gather can find in L2 / the Infinity Cache."""
+    rp = g.rowptr.cpu().numpy().astype(np.int64)
+    col = g.col.cpu().numpy()
+    nid = np.zeros(0, np.int64) if new_id is None else np.asarray(new_id, np.int64)
+    return dict(zip(windows, native.rt().locality_stats(g.n, rp, col, nid, list(windows))))
+
+
+def reorder(g: GraphData, rounds: int = 8, max_cluster: int = 4096, seed: int = 0):
+    """Relabel the nodes of ``g`` for gather locality (``csrc/runtime/reorder.cpp``).
+
+    Returns ``(g2, new_id)``: ``g2`` is the same graph with node ``v`` renamed
+    ``new_id[v]`` (CSR rows, features, labels, split and normalisation permuted
+    alike, so losses and accuracies are unchanged), ``new_id`` an int64 tensor on
+    the CPU.  Deterministic for any thread count, so every rank of a multi-GPU job
+    computes the same order independently."""
+    rt = native.rt()
+    rp = g.rowptr.cpu().numpy().astype(np.int64)
+    col = g.col.cpu().numpy()
+    new_id = rt.locality_order(g.n, rp, col, rounds, max_cluster, seed)
+    rp2, col2 = rt.permute_csr(g.n, rp, col, new_id)
+    del rp, col
+    dev = g.rowptr.device
+    nid = torch.from_numpy(np.asarray(new_id))
+    old_of = torch.empty_like(nid)
+    old_of[nid] = torch.arange(g.n, dtype=torch.int64)
+    o = old_of.to(dev)
+    rp2 = np.asarray(rp2)
+    if rp2[-1] >= 2 ** 31:
+        raise ValueError("nnz >= 2^31 needs int64 CSR (graph must be sharded)")
+    g2 = GraphData(n=g.n, rowptr=torch.from_numpy(rp2.astype(np.int32)).to(dev),
+                   col=torch.from_numpy(np.asarray(col2)).to(dev), dinv=g.dinv[o], x=g.x[o], y=g.y[o],
+                   mask=g.mask[o], n_classes=g.n_classes, name=g.name + "-reordered")
+    return g2, nid

@@ -1,0 +1,77 @@
+"""Shuffled synthetic ids and the locality reordering pass (csrc/runtime/reorder.cpp)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from cgnn_amd import native
+from cgnn_amd.gnn.data import locality, reorder, synthetic
+from cgnn_amd.gnn.gcn import GCNTrainer
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 1000, 65537])
+def test_id_permutation_is_a_bijection(n):
+    p = np.asarray(native.rt().id_permutation(n, 7, np.arange(n)))
+    assert np.array_equal(np.sort(p), np.arange(n))
+    if n > 100:
+        assert np.mean(p == np.arange(n)) < 0.01
+
+
+def test_shuffled_graph_is_the_banded_graph_relabelled():
+    rt = native.rt()
+    n, m = 5000, 40000
+    s0, d0, x0, y0 = (np.asarray(a) for a in rt.synthetic_graph(n, m, 8, 5, 0.8, 1.0, 3, 0.1, 0))
+    s1, d1, x1, y1 = (np.asarray(a) for a in rt.synthetic_graph(n, m, 8, 5, 0.8, 1.0, 3, 0.1, 1))
+    # the bijection the generator used, recovered from the labels + features of every node
+    perm = np.asarray(rt.id_permutation(n, 3 ^ 0x5A17, np.arange(n)))
+    assert np.array_equal(s1, perm[s0]) and np.array_equal(d1, perm[d0])
+    assert np.array_equal(y1[perm], y0) and np.array_equal(x1[perm], x0)
+
+
+def test_reorder_restores_locality_and_is_a_permutation():
+    g = synthetic("ogbn-products", seed=0, scale=0.01)           # shuffled ids (default)
+    before = locality(g)
+    g2, nid = reorder(g)
+    assert torch.equal(torch.sort(nid).values, torch.arange(g.n))
+    after = locality(g2)
+    assert before[256] < 0.05 and after[1024] > 0.6, (before, after)
+    banded = locality(synthetic("ogbn-products", seed=0, scale=0.01, id_order="banded"))
+    assert after[4096] > banded[4096] - 0.05
+    # same graph: edge (u, v) of g is edge (nid[u], nid[v]) of g2; node data follows
+    rp, col = g.rowptr.long(), g.col.long()
+    rows = torch.repeat_interleave(torch.arange(g.n), rp[1:] - rp[:-1])
+    e1 = set((nid[rows] * g.n + nid[col]).tolist())
+    rp2, col2 = g2.rowptr.long(), g2.col.long()
+    rows2 = torch.repeat_interleave(torch.arange(g.n), rp2[1:] - rp2[:-1])
+    assert e1 == set((rows2 * g.n + col2).tolist())
+    assert torch.equal(g2.x[nid], g.x) and torch.equal(g2.y[nid], g.y) and torch.equal(g2.mask[nid], g.mask)
+    assert torch.equal(g2.dinv[nid], g.dinv)
+
+
+def test_reorder_is_independent_of_thread_count():
+    code = ("import numpy as np; from cgnn_amd.gnn.data import synthetic, reorder; "
+            "g = synthetic('ogbn-products', seed=1, scale=0.003); print(int(np.asarray(reorder(g)[1]) @ "
+            "np.arange(g.n, dtype=np.int64) % 1000000007))")
+    outs = []
+    for t in ("1", "5"):
+        env = dict(os.environ, OMP_NUM_THREADS=t, PYTHONPATH=ROOT)
+        outs.append(subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                                   check=True).stdout.strip())
+    assert outs[0] == outs[1]
+
+
+def test_gcn_loss_is_invariant_under_reorder():
+    g = synthetic("ogbn-products", seed=2, scale=0.002)
+    a = GCNTrainer(g, hidden=32, dropout=0.0, seed=0, rank=0, world=1)
+    b = GCNTrainer(g, hidden=32, dropout=0.0, seed=0, rank=0, world=1, reorder=True)
+    for _ in range(3):
+        a.train_step()
+        b.train_step()
+    ra, rb = a.evaluate(), b.evaluate()
+    for k in ra:
+        assert abs(ra[k] - rb[k]) < 2e-3, (k, ra, rb)
