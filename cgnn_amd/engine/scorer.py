@@ -8,8 +8,10 @@ batches, spreads the batches over GPUs / ranks, and returns one score per job.
 
 Failure handling: a non-finite score is kept as NaN and dropped
 by :func:`finite_mean` exactly like the reference's ``np.isfinite`` filter;
-``max_retries`` optionally re-trains such a job with a fresh RNG stream, and
-``CGNN_FAULT=nan@job:k[,k...]`` injects failures for tests.
+``max_retries`` (``SETTINGS.max_retries`` / the ``max_retries`` kwarg of every
+model and search entry point) re-trains such a job with a fresh RNG stream, and
+``CGNN_FAULT=nan@job:k[,k...]`` injects failures (first attempt only) for tests.
+With ``CGNN_PROFILE=1`` every call records a ``phase`` event ``score_jobs``.
 """
 from __future__ import annotations
 
@@ -23,7 +25,7 @@ import numpy as np
 
 from ..parallel import dist as pdist
 from ..utils import philox
-from ..utils.metrics import METRICS
+from ..utils.metrics import METRICS, timer
 from .program import Program
 
 log = logging.getLogger("cgnn_amd")
@@ -116,8 +118,13 @@ def _run_local(jobs: Sequence[Job], cfg) -> np.ndarray:
     return scores
 
 
-def score_jobs(jobs: Sequence[Job], cfg, max_retries: int = 0) -> np.ndarray:
+def score_jobs(jobs: Sequence[Job], cfg, max_retries: Optional[int] = None) -> np.ndarray:
     """One score per job (mean test-phase loss); NaN for non-finite runs."""
+    with timer("score_jobs"):
+        return _score_jobs(jobs, cfg, cfg.max_retries if max_retries is None else int(max_retries))
+
+
+def _score_jobs(jobs: Sequence[Job], cfg, max_retries: int) -> np.ndarray:
     n = len(jobs)
     idx = pdist.shard_indices(n)
     local = _run_local([jobs[i] for i in idx], cfg) if len(idx) else np.zeros(0)
@@ -134,6 +141,8 @@ def score_jobs(jobs: Sequence[Job], cfg, max_retries: int = 0) -> np.ndarray:
             j = jobs[idx[k]]
             retry.append(Job(j.program, j.data, philox.model_key(j.key[0], j.key[1], "retry", attempt)))
         local[bad] = _run_local(retry, cfg)
+        METRICS.record("retried_runs", attempt=attempt + 1, count=len(bad),
+                       recovered=int(np.isfinite(local[bad]).sum()))
     scores = pdist.combine_scores(n, idx, local)
     dropped = int((~np.isfinite(scores)).sum())
     if dropped:

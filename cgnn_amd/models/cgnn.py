@@ -25,6 +25,7 @@ from ..search.confounders import hill_climbing_confounders
 from ..search.hill_climbing import exploratory_hill_climbing, hill_climbing, tabu_search
 from ..utils.formats import standardize
 from ..utils.philox import model_key
+from ..utils.metrics import timer
 from ..utils.settings import SETTINGS
 from .base import GraphModel
 from .gnn import GNN
@@ -151,7 +152,8 @@ class CGNN(GraphModel):
     def orient_directed_graph(self, data, dag, alg='HC', **kwargs):
         data = pd.DataFrame(standardize(np.asarray(data.values, dtype=np.float64)), columns=data.columns)
         alg_dic = {'HC': hill_climbing, 'tabu': tabu_search, 'EHC': exploratory_hill_climbing}
-        return alg_dic[alg](dag, data, self.infer_graph, **self._kw(kwargs))
+        with timer("search:" + alg):
+            return alg_dic[alg](dag, data, self.infer_graph, **self._kw(kwargs))
 
     def orient_undirected_graph(self, data, umg, **kwargs):
         warnings.warn("The pairwise GNN model is computed on each edge of the UMG "
@@ -172,7 +174,8 @@ class CGNN_confounders(CGNN):
     def orient_directed_graph(self, data, dag, alg='HC', **kwargs):
         data = pd.DataFrame(standardize(np.asarray(data.values, dtype=np.float64)), columns=data.columns)
         alg_dic = {'HC': hill_climbing_confounders, 'tabu': tabu_search, 'EHC': exploratory_hill_climbing}
-        return alg_dic[alg](dag, data, self.infer_graph, **self._kw(kwargs))
+        with timer("search:confounders-" + alg):
+            return alg_dic[alg](dag, data, self.infer_graph, **self._kw(kwargs))
 
     def orient_undirected_graph(self, data, umg, **kwargs):
         warnings.warn("The pairwise GNN model is computed on each edge of the UMG "

@@ -18,6 +18,7 @@ import numpy as np
 
 from ..engine.program import program_for_pair
 from ..engine.scorer import Job, finite_mean, score_jobs, subsample
+from ..utils.metrics import timer
 from ..utils.philox import model_key
 from ..utils.settings import SETTINGS
 from .base import Pairwise_Model
@@ -66,7 +67,8 @@ class GNN(Pairwise_Model):
             js = pair_jobs(a, b, idx, cfg)
             spans.append((len(jobs), len(jobs) + len(js)))
             jobs.extend(js)
-        scores = score_jobs(jobs, cfg)
+        with timer("pairwise"):
+            scores = score_jobs(jobs, cfg)
         out, self.last_run_scores = [], []
         for s, e in spans:
             ab, ba, p = pair_score(scores[s:e])

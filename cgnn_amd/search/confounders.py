@@ -14,12 +14,19 @@ Loop until a full pass brings no improvement.  Candidates that do not depend
 on each other's outcome are scored in one batch: the reversal and the removal
 of the current orientation, and the two additions.  The removal of the
 *reversed* edge is scored afterwards only if the reversal was accepted.
+
+``checkpoint=<path>``: the search state (graph, tested configurations, best
+score, confounder labels, pass number and position in the skeleton) is written
+atomically after every skeleton edge; a later call with the same path resumes
+at the next edge (the reference's 95-candidate example run restarts from zero).
 """
 from __future__ import annotations
 
 import copy
 import logging
 
+from ..utils.checkpoint import SearchCheckpoint
+from ..utils.metrics import timer
 from ..utils.settings import SETTINGS
 from .hill_climbing import _say, make_evaluator
 
@@ -33,14 +40,25 @@ def hill_climbing_confounders(graph, data, run_cgnn_function=None, **kwargs):
         raise ValueError("hill_climbing_confounders needs DirectedGraph(skeleton=...)")
     nodes = skel.get_list_nodes()
     ev = kwargs.get("evaluator") or make_evaluator(data, run_cgnn_function, cfg, "confounders", nodes, kwargs)
-    tested = {graph.canonical_key()}
-    globalscore = float(ev([graph])[0])
-    _say(cfg, "Graph score : " + str(globalscore))
-    confounders = set()
-    improvement = True
-    while improvement:
-        improvement = False
-        for u, v in skel.get_list_edges_without_duplicate():
+    ck = SearchCheckpoint(kwargs.get("checkpoint"), "HC-confounders")
+    state = ck.load()
+    skel_edges = skel.get_list_edges_without_duplicate()
+    if state:
+        graph, tested, globalscore = state["graph"], state["tested"], state["best"]
+        confounders = {frozenset(c) for c in state["confounders"]}
+        loop, start, improvement = state["loop"], state["position"], state["improvement"]
+        skel = graph.skeleton
+        _say(cfg, "Resuming confounder HC at pass %d, skeleton edge %d, score %s" % (loop, start, globalscore))
+    else:
+        tested = {graph.canonical_key()}
+        with timer("search:initial_score"):
+            globalscore = float(ev([graph])[0])
+        _say(cfg, "Graph score : " + str(globalscore))
+        confounders = set()
+        loop, start, improvement = 1, 0, False
+    while True:
+        for pos in range(start, len(skel_edges)):
+            u, v = skel_edges[pos]
             if graph.has_edge(u, v) or graph.has_edge(v, u):
                 n1, n2 = (u, v) if graph.has_edge(u, v) else (v, u)
                 # --- reversal and removal of the current orientation, together
@@ -115,6 +133,13 @@ def hill_climbing_confounders(graph, data, run_cgnn_function=None, **kwargs):
                 else:
                     _say(cfg, "Edge not added, possible confounder %s <-> %s" % (u, v))
                     confounders.add(frozenset((u, v)))
+            ck.save(graph, tested, best=globalscore, loop=loop, position=pos + 1, improvement=improvement,
+                    confounders=sorted([sorted(c, key=repr) for c in confounders], key=repr))
+        if not improvement:
+            break
+        loop, start, improvement = loop + 1, 0, False
+        ck.save(graph, tested, best=globalscore, loop=loop, position=0, improvement=False,
+                confounders=sorted([sorted(c, key=repr) for c in confounders], key=repr))
     graph.search_score = globalscore
     graph.confounders = sorted(tuple(sorted(c, key=repr)) for c in confounders)
     return graph

@@ -18,6 +18,11 @@ at a time, like the reference's joblib plug-in).
   quadratically over ``nb_loops`` loops, accept if the score improves.
 * ``tabu_search`` (a stub raising in the reference, B3): best-admissible-move
   search over single reversals with a tabu list, aspiration and patience.
+
+Every search takes ``checkpoint=<path>``: its state is written atomically (JSON)
+after every evaluated batch / loop / iteration, and a later call with the same
+path resumes from it (EHC draws loop ``k``'s random edge set from a stream keyed
+by ``k``, so a resumed run makes the same draws as an uninterrupted one).
 """
 from __future__ import annotations
 
@@ -28,7 +33,8 @@ from typing import Callable, Optional
 import numpy as np
 
 from ..engine.evaluator import GraphEvaluator
-from ..utils.checkpoint import SearchCheckpoint
+from ..utils.checkpoint import SearchCheckpoint, graph_from_dict, graph_to_dict, key_from_json, key_to_json
+from ..utils.metrics import timer
 from ..utils.philox import numpy_rng
 from ..utils.settings import SETTINGS
 
@@ -65,7 +71,8 @@ def hill_climbing(graph, data, run_cgnn_function=None, **kwargs):
         _say(cfg, "Resuming HC at loop %d, edge %d, score %s" % (loop, i, globalscore))
     else:
         tested = {graph.canonical_key()}
-        globalscore = float(ev([graph])[0])
+        with timer("search:initial_score"):
+            globalscore = float(ev([graph])[0])
         loop, i, improvement, list_edges = 0, 0, False, []
         resume_pass = False
         _say(cfg, "Graph score : " + str(globalscore))
@@ -91,7 +98,8 @@ def hill_climbing(graph, data, run_cgnn_function=None, **kwargs):
             if not batch:
                 i = j
                 continue
-            scores = ev([b[2] for b in batch])
+            with timer("search:candidates"):
+                scores = ev([b[2] for b in batch])
             nxt = j
             for (jj, edge, tg, key), s in zip(batch, scores):
                 tested.add(key)
@@ -121,12 +129,20 @@ def exploratory_hill_climbing(graph, data, run_cgnn_function=None, **kwargs):
         exploration_factor = max(1, len(edges0) - 1)
     nodes = kwargs.get("nodes") or sorted(graph.get_list_nodes(), key=repr)
     ev = kwargs.get("evaluator") or make_evaluator(data, run_cgnn_function, cfg, "dag", nodes, kwargs, graph)
-    rng = numpy_rng(cfg.seed, "EHC")
-    tested = {graph.canonical_key()}
-    globalscore = float(ev([graph])[0])
-    _say(cfg, "Graph score : " + str(globalscore))
+    ck = SearchCheckpoint(kwargs.get("checkpoint"), "EHC")
+    state = ck.load()
+    if state:
+        graph, tested, globalscore, first = state["graph"], state["tested"], state["best"], state["loop"] + 1
+        _say(cfg, "Resuming EHC at loop %d, score %s" % (first, globalscore))
+    else:
+        tested = {graph.canonical_key()}
+        with timer("search:initial_score"):
+            globalscore = float(ev([graph])[0])
+        first = 1
+        _say(cfg, "Graph score : " + str(globalscore))
     max_tries = int(kwargs.get("max_tries", 200))
-    for loop in range(1, nb_loops + 1):
+    for loop in range(first, nb_loops + 1):
+        rng = numpy_rng(cfg.seed, "EHC", loop)
         list_edges = graph.get_list_edges()
         m = max(int(exploration_factor * ((nb_loops - loop) / nb_loops) ** 2), 1)
         cand = None
@@ -139,16 +155,18 @@ def exploratory_hill_climbing(graph, data, run_cgnn_function=None, **kwargs):
             if not tg.is_cyclic() and key not in tested:
                 cand = (sel, tg, key)
                 break
-        if cand is None:
-            continue
-        sel, tg, key = cand
-        tested.add(key)
-        s = float(ev([tg])[0])
-        _say(cfg, 'Reversed Edges {} : score {} (best {})'.format([list_edges[k][:2] for k in sel], s, globalscore))
-        if s < globalscore:
-            for k in sel:
-                graph.reverse_edge(list_edges[k][0], list_edges[k][1])
-            globalscore = s
+        if cand is not None:
+            sel, tg, key = cand
+            tested.add(key)
+            with timer("search:candidates"):
+                s = float(ev([tg])[0])
+            _say(cfg, 'Reversed Edges {} : score {} (best {})'.format([list_edges[k][:2] for k in sel], s,
+                                                                      globalscore))
+            if s < globalscore:
+                for k in sel:
+                    graph.reverse_edge(list_edges[k][0], list_edges[k][1])
+                globalscore = s
+        ck.save(graph, tested, best=globalscore, loop=loop)
     graph.search_score = globalscore
     return graph
 
@@ -168,13 +186,24 @@ def tabu_search(graph, data, run_cgnn_function=None, **kwargs):
     patience = int(kwargs.get("patience", 5))
     nodes = kwargs.get("nodes") or sorted(graph.get_list_nodes(), key=repr)
     ev = kwargs.get("evaluator") or make_evaluator(data, run_cgnn_function, cfg, "dag", nodes, kwargs, graph)
-    current = copy.deepcopy(graph)
-    cur_score = float(ev([current])[0])
-    best, best_score = copy.deepcopy(current), cur_score
-    tabu = {}
-    cache = {current.canonical_key(): cur_score}
-    stale = 0
-    for it in range(max_iter):
+    ck = SearchCheckpoint(kwargs.get("checkpoint"), "tabu")
+    state = ck.load()
+    if state:
+        current, cur_score = state["graph"], state["current_score"]
+        best, best_score = graph_from_dict(state["best_graph"]), state["best"]
+        tabu = {frozenset(p): int(t) for p, t in state["tabu"]}
+        cache = {key_from_json(k): float(v) for k, v in state["cache"]}
+        stale, first = state["stale"], state["iteration"] + 1
+        _say(cfg, "Resuming tabu search at iteration %d, best %s" % (first, best_score))
+    else:
+        current = copy.deepcopy(graph)
+        with timer("search:initial_score"):
+            cur_score = float(ev([current])[0])
+        best, best_score = copy.deepcopy(current), cur_score
+        tabu = {}
+        cache = {current.canonical_key(): cur_score}
+        stale, first = 0, 0
+    for it in range(first, max_iter):
         moves = []
         for a, b, w in current.get_list_edges():
             tg = copy.deepcopy(current)
@@ -184,7 +213,9 @@ def tabu_search(graph, data, run_cgnn_function=None, **kwargs):
             moves.append(((a, b), tg, tg.canonical_key()))
         todo = [m for m in moves if m[2] not in cache]
         if todo:
-            for m, s in zip(todo, ev([m[1] for m in todo])):
+            with timer("search:candidates"):
+                res = ev([m[1] for m in todo])
+            for m, s in zip(todo, res):
                 cache[m[2]] = float(s)
         choice = None
         for (a, b), tg, key in sorted(moves, key=lambda m: cache[m[2]]):
@@ -199,12 +230,18 @@ def tabu_search(graph, data, run_cgnn_function=None, **kwargs):
         (a, b), current, cur_score, pair = choice
         tabu[pair] = it + tenure
         _say(cfg, "tabu iter %d: reverse %s -> score %s" % (it, (a, b), cur_score))
+        done = False
         if cur_score < best_score:
             best, best_score, stale = copy.deepcopy(current), cur_score, 0
         else:
             stale += 1
-            if stale >= patience:
-                break
+            done = stale >= patience
+        ck.save(current, set(), current_score=cur_score, best=best_score, best_graph=graph_to_dict(best),
+                tabu=[[sorted(p, key=repr), t] for p, t in tabu.items()],
+                cache=[[key_to_json(k), v] for k, v in cache.items()], stale=stale,
+                iteration=max_iter if done else it)
+        if done:
+            break
     # write the result into the caller's graph object, like the other searches
     for a, b, w in list(graph.get_list_edges(order_by_weight=False)):
         graph.remove_edge(a, b)

@@ -12,6 +12,11 @@ New (not in the reference):
   * ``batch_models``         -- how many independent models (runs x candidates)
                                 one device launch trains together
   * ``verbose``              -- default verbosity of training / search logs
+  * ``max_retries``          -- re-train a run whose score is non-finite up to this
+                                many times with a fresh RNG stream before it is
+                                dropped (0 = the reference's drop-only behaviour;
+                                the reference re-runs only its polynomial generator,
+                                generators.py:165-178)
 
 Every field can also be overridden from the environment as ``CGNN_<NAME>``
 (e.g. ``CGNN_NB_RUNS=8``) when the singleton is created.
@@ -47,7 +52,8 @@ class DefaultSettings(object):
                  "device_ids",
                  "compat_remove_cycles",
                  "batch_models",
-                 "verbose")
+                 "verbose",
+                 "max_retries")
 
     def __init__(self):
         self.NB_RUNS = 32
@@ -73,6 +79,7 @@ class DefaultSettings(object):
         self.compat_remove_cycles = False
         self.batch_models = 256
         self.verbose = False
+        self.max_retries = 0
         self._apply_env()
 
     def _apply_env(self):
@@ -122,6 +129,7 @@ class DefaultSettings(object):
             compat_remove_cycles=bool(g("compat_remove_cycles", self.compat_remove_cycles)),
             batch_models=int(g("batch_models", self.batch_models)),
             verbose=bool(g("verbose", self.verbose)),
+            max_retries=int(g("max_retries", self.max_retries)),
         )
 
     def __repr__(self):
@@ -159,6 +167,7 @@ class RunConfig:
     compat_remove_cycles: bool = False
     batch_models: int = 256
     verbose: bool = False
+    max_retries: int = 0
 
     def replace(self, **kw) -> "RunConfig":
         return dataclasses.replace(self, **kw)
