@@ -33,30 +33,24 @@ constexpr int MT = 32;          // tile edge (rows per wave, columns per tile)
 constexpr int WAVES = 4;        // rows per block = 128
 
 // seven bandwidths for two distances, each kernel value folded into the sum
-// (ks) and the weighted sum (w) as soon as it exists.
+// (ks) and the weighted sum (w) as soon as it exists (values: rbf7_values).
 __device__ __forceinline__ void rbf7x2_chain(f2 d2, f2& ks, f2& w) {
-  const float L2E = 1.4426950408889634f;
-  f2 e = exp2_2(d2 * (-0.005f * L2E));
-  ks = e;
-  w = e * 0.005f;
-  e = exp2_2(d2 * (-0.05f * L2E));
-  ks += e;
-  w = e * 0.05f + w;
-  f2 e3 = exp2_2(d2 * (-0.25f * L2E));
-  ks += e3;
-  w = e3 * 0.25f + w;
-  e3 *= e3;                               // gamma 0.5
-  ks += e3;
-  w = e3 * 0.5f + w;
-  e3 *= e3;                               // gamma 1
-  ks += e3;
-  w += e3;
-  e = exp2_2(d2 * (-5.0f * L2E));
-  ks += e;
-  w = e * 5.0f + w;
-  e = exp2_2(d2 * (-50.0f * L2E));
-  ks += e;
-  w = e * 50.0f + w;
+  f2 e[7];
+  rbf7_values(d2, e);
+  ks = e[0];
+  w = e[0] * 0.005f;
+  ks += e[1];
+  w = e[1] * 0.05f + w;
+  ks += e[2];
+  w = e[2] * 0.25f + w;
+  ks += e[3];
+  w = e[3] * 0.5f + w;
+  ks += e[4];
+  w += e[4];
+  ks += e[5];
+  w = e[5] * 5.0f + w;
+  ks += e[6];
+  w = e[6] * 50.0f + w;
 }
 
 __device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {

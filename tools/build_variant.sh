@@ -1,10 +1,16 @@
 #!/bin/bash
-# usage: build_variant.sh OUTDIR -DFLAGS...  (rebuilds gnn_sparse.hip with flags, links a variant _hip.so)
+# usage: build_variant.sh OUTDIR "a.hip b.hip" -DFLAGS...
+#   rebuilds the named kernel sources with extra flags and links a variant _hip.so
+#   with the other in-tree objects (A/B in one environment: CGNN_HIP_LIB=OUTDIR/_hip...so)
 set -e
 out=$1; shift
+srcs=$1; shift
 mkdir -p $out
 R=/root/repo
 INC="-I$R/cgnn_amd/csrc/include $(python3 -c 'import pybind11,sysconfig;print("-I"+pybind11.get_include(),"-I"+sysconfig.get_paths()["include"])')"
-/opt/rocm/bin/hipcc -c -fPIC -std=c++17 -O3 -x hip --offload-arch=gfx950 $INC -Wno-unused-result -fvisibility=hidden "$@" $R/cgnn_amd/csrc/kernels/gnn_sparse.hip -o $out/gnn_sparse.hip.o
-objs=$(ls $R/build/hip/*.o | grep -v gnn_sparse.hip.o)
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $objs $out/gnn_sparse.hip.o -o $out/_hip.cpython-310-x86_64-linux-gnu.so
+objs=$(ls $R/build/hip/*.o)
+for base in $srcs; do
+  /opt/rocm/bin/hipcc -c -fPIC -std=c++17 -O3 -x hip --offload-arch=gfx950 $INC -Wno-unused-result -fvisibility=hidden "$@" $R/cgnn_amd/csrc/kernels/$base -o $out/$base.o
+  objs=$(echo "$objs" | grep -v "/$base.o")
+done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $objs $(for b in $srcs; do echo $out/$b.o; done) -o $out/_hip.cpython-310-x86_64-linux-gnu.so
