@@ -79,6 +79,14 @@ int gnn_launch_fused_bwd(const void*, const void*, const float*, const float*, c
                          hipStream_t);
 int gnn_launch_dense_bwd(const void*, const float*, const void*, void*, int, int, int, int, float,
                          hipStream_t);
+int gnn_launch_lin_fwd(const void*, int, int, const void*, int, int, const float*, int, const float*, void*, int,
+                       int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, const int*, const float*,
+                       hipStream_t);
+int gnn_launch_lin_bwd_data(const void*, int, const void*, int, float, int, const float*, int, int, void*, int,
+                            void*, int, const float*, int, hipStream_t);
+int gnn_lin_wgrad_chunks(int, int);
+int gnn_launch_lin_bwd_weight(const void*, int, int, const void*, int, int, const void*, int, const void*, int,
+                              float, int, float*, float*, float*, int, hipStream_t);
 }
 
 static inline hipStream_t S(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -283,6 +291,28 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("ax"), py::arg("dy2"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("gpart"), py::arg("n"),
      py::arg("F"), py::arg("ldx"), py::arg("HD"), py::arg("C"), py::arg("ldc"), py::arg("p"), py::arg("k0"),
      py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"), py::arg("step_ptr") = 0);
+  // generic fused dense layers (gnn_linear.hip); return codes: 0 ok, -1 no variant, -3 bad shape
+  m.def("gnn_lin_fwd", [](uint64_t x1, int ld1, int K1, uint64_t x2, int ld2, int K2, uint64_t w, int N, uint64_t b,
+                          uint64_t y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step,
+                          uint32_t row0, uint64_t stepp, uint64_t rscale, uint64_t st) {
+    return gnn_launch_lin_fwd(Pt<const void>(x1), ld1, K1, Pt<const void>(x2), ld2, K2, Pt<const float>(w), N,
+                              Pt<const float>(b), Pt<void>(y), ldy, n, relu, p, k0, k1, step, row0,
+                              Pt<const int>(stepp), Pt<const float>(rscale), S(st));
+  });
+  m.def("gnn_lin_bwd_data", [](uint64_t dy, int lddy, uint64_t ym, int ldym, float mscale, int N, uint64_t w, int K1,
+                               int K2, uint64_t dx1, int ldx1, uint64_t dx2, int ldx2, uint64_t rscale, int n,
+                               uint64_t st) {
+    return gnn_launch_lin_bwd_data(Pt<const void>(dy), lddy, Pt<const void>(ym), ldym, mscale, N, Pt<const float>(w),
+                                   K1, K2, Pt<void>(dx1), ldx1, Pt<void>(dx2), ldx2, Pt<const float>(rscale), n, S(st));
+  });
+  m.def("gnn_lin_wgrad_chunks", &gnn_lin_wgrad_chunks);
+  m.def("gnn_lin_bwd_weight", [](uint64_t x1, int ld1, int K1, uint64_t x2, int ld2, int K2, uint64_t dy, int lddy,
+                                 uint64_t ym, int ldym, float mscale, int N, uint64_t gpart, uint64_t dw, uint64_t db,
+                                 int n, uint64_t st) {
+    return gnn_launch_lin_bwd_weight(Pt<const void>(x1), ld1, K1, Pt<const void>(x2), ld2, K2, Pt<const void>(dy), lddy,
+                                     Pt<const void>(ym), ldym, mscale, N, Pt<float>(gpart), Pt<float>(dw),
+                                     Pt<float>(db), n, S(st));
+  });
   m.def("gnn_cast_bf16", [](uint64_t src, uint64_t dst, long n, uint64_t st) {
     chk(gnn_launch_cast_bf16(Pt<const float>(src), Pt<void>(dst), n, S(st)), "gnn_cast_bf16");
   });

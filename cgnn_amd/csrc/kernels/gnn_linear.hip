@@ -1,0 +1,517 @@
+// Generic fused dense layers of the GNN track on MFMA (gfx950, v_mfma_f32_32x32x16_bf16).
+//
+// The dense half of every message-passing layer is a tall-skinny product: millions
+// of rows, K and N of a few hundred.  Three kernels cover the forward and both
+// backward products of any such layer (GraphSAGE, the GAT projection, every layer of
+// the L-layer GCN), bf16 storage and fp32 accumulation throughout:
+//
+//   lin_fwd         Y = epi([X1 | X2] W + b)      epi: ReLU, Philox dropout, row scale
+//   lin_bwd_data    [dX1 | dX2] = rs * ((dY * m) W^T)     m = [Ym > 0] / (1 - p)
+//   lin_bwd_weight  [dW; db] = [X1 | X2 | 1]^T (dY * m)   split-K over row chunks
+//
+// [X1 | X2] is a VIRTUAL concatenation along the features (GraphSAGE's
+// [h_dst | mean-aggregate] without the copy); W is the fp32 master weight
+// [K1 + K2][N] (row-major), staged into LDS as bf16 once per persistent block.
+// The mask m of the backward kernels is applied while the gradient rows are
+// loaded: Ym is the layer's stored output (after ReLU and dropout), so Ym > 0
+// marks exactly the units that were kept and active -- neither the mask nor the
+// masked gradient is ever materialised.
+//
+// Forward / data-backward compute the output TRANSPOSED (tile = [feature][row]):
+// the A operand is a weight slab in LDS, the B operand is 16 contiguous bytes of
+// one row per lane, loaded from HBM in the natural row-major layout, and each
+// lane ends up owning 16 features of one row -- one Philox draw per lane and
+// 32-feature tile supplies exactly its 16 dropout bytes (the mask convention of
+// gnn_dense.hip / ops.dropout_keep_mask: draw (row, 2*(n/32) + (n/4)%2, step),
+// byte (n%4) + 4*((n%32)/8)).
+//
+// The weight gradient contracts over rows, so both operands must hold 8
+// consecutive ROWS per lane: each 32-row tile of [X1 | X2 | 1] and of the masked
+// gradient is staged in LDS transposed ([column][row]; chunks assigned
+// row-fastest so a wave's 2-byte transposed writes are contiguous, no bank
+// conflicts), the next tile is prefetched into registers meanwhile; every wave
+// keeps its [k-tile][n-tile] accumulators for the whole row chunk and the
+// per-chunk fp32 slabs are summed in a fixed order by lin_reduce (deterministic,
+// no atomics).
+#include "cgnn_common.h"
+#include <algorithm>
+#include <cmath>
+
+using namespace cgnn;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TILE = 32;
+// persistent blocks share one LDS weight slab: 16 waves (4 per SIMD, <= 128 VGPRs) up
+// to K = 256, 8 waves (<= 256 VGPRs) for the wider variants, whose B fragments alone
+// take 4 * KS registers
+template <int KS> struct FwdWaves { static constexpr int value = KS <= 16 ? 16 : 8; };
+constexpr int WGT_WAVES = 8;        // weight-gradient blocks
+constexpr int TR = TILE + 8;        // transposed image row: 32 rows + pad (80 B)
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+__device__ __forceinline__ uint16_t bf16_bits(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
+
+__device__ __forceinline__ float bf16_val(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+
+__device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
+  return make_uint2((uint32_t)bf16_bits(a) | ((uint32_t)bf16_bits(b) << 16),
+                    (uint32_t)bf16_bits(c) | ((uint32_t)bf16_bits(d) << 16));
+}
+
+// zero the elements [valid, 8) of a bf16x8 chunk (padding columns may hold anything,
+// and 0 * NaN would poison a product)
+__device__ __forceinline__ uint4 keep_first(uint4 v, int valid) {
+  if (valid >= 8) return v;
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int lo = 2 * e, hi = 2 * e + 1;
+    w[e] = (lo < valid ? (w[e] & 0xffffu) : 0u) | (hi < valid ? (w[e] & 0xffff0000u) : 0u);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// 8 features [f0, f0 + 8) of row `row` of the virtual concatenation [X1 | X2]
+// (K1 % 8 == 0 when X2 is given, so a chunk never straddles the two); zeros past K1 + K2
+__device__ __forceinline__ uint4 load_cat8(const uint16_t* __restrict__ x1, int ld1, int K1,
+                                           const uint16_t* __restrict__ x2, int ld2, int K2, int row, int f0) {
+  if (f0 < K1) return keep_first(*reinterpret_cast<const uint4*>(x1 + (size_t)row * ld1 + f0), K1 - f0);
+  const int g = f0 - K1;
+  if (x2 && g < K2) return keep_first(*reinterpret_cast<const uint4*>(x2 + (size_t)row * ld2 + g), K2 - g);
+  return make_uint4(0u, 0u, 0u, 0u);
+}
+
+// 8 gradient values [c0, c0 + 8) of row `row`, times the mask [Ym > 0] * mscale
+__device__ __forceinline__ uint4 load_masked8(const uint16_t* __restrict__ dY, int lddy,
+                                              const uint16_t* __restrict__ Ym, int ldym, float mscale,
+                                              int N, int row, int c0) {
+  if (c0 >= N) return make_uint4(0u, 0u, 0u, 0u);
+  uint4 g = keep_first(*reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + c0), N - c0);
+  if (!Ym && mscale == 1.f) return g;
+  const uint4 y = Ym ? *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + c0) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  uint32_t gw[4] = {g.x, g.y, g.z, g.w};
+  const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const uint32_t yb = (yw[w] >> (16 * half)) & 0xffffu;
+      // kept and active: y > 0 (positive, non-zero); the all-ones pattern = no mask
+      const bool keep = !Ym || ((yb & 0x7fffu) != 0 && !(yb & 0x8000u));
+      const float v = keep ? bf16_val((gw[w] >> (16 * half)) & 0xffffu) * mscale : 0.f;
+      o |= (uint32_t)bf16_bits(v) << (16 * half);
+    }
+    gw[w] = o;
+  }
+  return make_uint4(gw[0], gw[1], gw[2], gw[3]);
+}
+
+int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev >= 64) return 256;
+  if (!cached[dev]) {
+    hipDeviceProp_t prop;
+    cached[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
+  return cached[dev];
+}
+
+}  // namespace
+
+// ============================================================================
+// lin_fwd: Y[row][c] = epi(sum_k [X1 | X2][row][k] W[k][c] + b[c]) for the column
+// slab c in [blockIdx.y * ncols, +ncols); KS k-steps of 16 cover K1 + K2.
+// ============================================================================
+template <int KS, int FWD_WAVES = FwdWaves<KS>::value>
+__global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
+    const uint16_t* __restrict__ x1, int ld1, int K1, const uint16_t* __restrict__ x2, int ld2, int K2,
+    const float* __restrict__ W, int N, const float* __restrict__ bias, uint16_t* __restrict__ Y, int ldy,
+    int n, int ncols, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
+    uint32_t row0, const int* __restrict__ stepp, const float* __restrict__ rscale) {
+  if (stepp) step = (uint32_t)*stepp;
+  constexpr int KP = KS * 16;
+  constexpr int WS = KP + 8;                     // padded row stride of the W^T slab
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* sWT = lds;                           // [ncols][WS]
+  float* sB = reinterpret_cast<float*>(sWT + (size_t)ncols * WS);   // [ncols]
+  const int c0 = blockIdx.y * ncols;
+  const int K = K1 + K2;
+  for (int i = threadIdx.x; i < ncols * KP; i += blockDim.x) {
+    const int k = i / ncols, c = i - k * ncols;            // consecutive threads: consecutive c (coalesced W)
+    sWT[c * WS + k] = bf16_bits(k < K && c0 + c < N ? W[(size_t)k * N + c0 + c] : 0.f);
+  }
+  for (int c = threadIdx.x; c < ncols; c += blockDim.x) sB[c] = (bias && c0 + c < N) ? bias[c0 + c] : 0.f;
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31;
+  const int wave = blockIdx.x * FWD_WAVES + (threadIdx.x >> 6);
+  const int n_waves = gridDim.x * FWD_WAVES;
+  const int n_tiles = (n + TILE - 1) / TILE;
+  const float scale = thr8 > 0 ? 1.f / (1.f - p) : 1.f;
+  const int nt = ncols / 32;
+
+  for (int tile = wave; tile < n_tiles; tile += n_waves) {
+    const int row = tile * TILE + lr;
+    const bool rv = row < n;
+    bf16x8 bx[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      bx[s] = as_bf16x8(rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h) : make_uint4(0u, 0u, 0u, 0u));
+    const float rs = (rv && rscale) ? rscale[row] : 1.f;
+#pragma unroll 1
+    for (int t = 0; t < nt; ++t) {
+      f32x16 acc = {};
+      const uint16_t* arow = sWT + (32 * t + lr) * WS + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(*reinterpret_cast<const uint4*>(arow + 16 * s)),
+                                                      bx[s], acc, 0, 0, 0);
+      if (!rv) continue;
+      const int cg = c0 + 32 * t;                // global column of this tile
+      uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+      if (thr8 > 0) {
+        const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * (cg / 32) + h), step, RNG_DROPOUT},
+                                      k0, k1);
+        w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
+      }
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int cl = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+        float x = acc[q] + sB[cl];
+        if (relu) x = fmaxf(x, 0.f);
+        if (thr8 > 0) x = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
+        v[q] = x * rs;
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = cg + 8 * g + 4 * h;
+        if (c < ldy)
+          *reinterpret_cast<uint2*>(Y + (size_t)row * ldy + c) = pack4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+      }
+    }
+  }
+}
+
+// ============================================================================
+// lin_bwd_data: dX^T[k][row] = sum_c W[k][c] (dY * m)[row][c] for the k slab
+// [blockIdx.y * kcols, +kcols); KN k-steps of 16 cover the N gradient columns.
+// Output k < K1 -> dX1, K1 <= k < K1 + K2 -> dX2; times rscale[row] (optional).
+// ============================================================================
+template <int KN, int FWD_WAVES = FwdWaves<KN>::value>
+__global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
+    const uint16_t* __restrict__ dY, int lddy, const uint16_t* __restrict__ Ym, int ldym, float mscale, int N,
+    const float* __restrict__ W, int K1, int K2, uint16_t* __restrict__ dX1, int ldx1, uint16_t* __restrict__ dX2,
+    int ldx2, const float* __restrict__ rscale, int n, int kcols) {
+  constexpr int NP = KN * 16;
+  constexpr int WS = NP + 8;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* sW = lds;                            // [kcols][WS]: rows of W
+  const int kb = blockIdx.y * kcols;
+  const int K = K1 + K2;
+  for (int i = threadIdx.x; i < kcols * NP; i += blockDim.x) {
+    const int kk = i / NP, c = i - kk * NP;
+    sW[kk * WS + c] = bf16_bits(kb + kk < K && c < N ? W[(size_t)(kb + kk) * N + c] : 0.f);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31;
+  const int wave = blockIdx.x * FWD_WAVES + (threadIdx.x >> 6);
+  const int n_waves = gridDim.x * FWD_WAVES;
+  const int n_tiles = (n + TILE - 1) / TILE;
+  const int nt = kcols / 32;
+  for (int tile = wave; tile < n_tiles; tile += n_waves) {
+    const int row = tile * TILE + lr;
+    const bool rv = row < n;
+    bf16x8 by[KN];
+#pragma unroll
+    for (int s = 0; s < KN; ++s)
+      by[s] = as_bf16x8(rv ? load_masked8(dY, lddy, Ym, ldym, mscale, N, row, 16 * s + 8 * h) : make_uint4(0u, 0u, 0u, 0u));
+    const float rs = (rv && rscale) ? rscale[row] : 1.f;
+#pragma unroll 1
+    for (int t = 0; t < nt; ++t) {
+      f32x16 acc = {};
+      const uint16_t* arow = sW + (32 * t + lr) * WS + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KN; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(*reinterpret_cast<const uint4*>(arow + 16 * s)),
+                                                      by[s], acc, 0, 0, 0);
+      if (!rv) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int k = kb + 32 * t + 8 * g + 4 * h;          // 4 consecutive k, never straddling K1 (K1 % 8 == 0)
+        const uint2 o = pack4(acc[4 * g] * rs, acc[4 * g + 1] * rs, acc[4 * g + 2] * rs, acc[4 * g + 3] * rs);
+        if (k < K1) {
+          if (k < ldx1) *reinterpret_cast<uint2*>(dX1 + (size_t)row * ldx1 + k) = o;
+        } else if (dX2 && k - K1 < ldx2 && k < K1 + ldx2) {
+          *reinterpret_cast<uint2*>(dX2 + (size_t)row * ldx2 + (k - K1)) = o;
+        }
+      }
+    }
+  }
+}
+
+// ============================================================================
+// lin_bwd_weight: gpart[chunk][k][c] = sum_{rows of chunk} [X1 | X2 | 1][row][k] (dY * m)[row][c]
+// for the 64-column slab c in [blockIdx.y * 64, +64); k = K1 + K2 is the ones column
+// (the bias gradient).  KT = k-tiles of 32 covering K1 + K2 + 1; wave w owns the
+// k-tiles w, w + 8, ...
+// ============================================================================
+template <int KT>
+__global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
+    const uint16_t* __restrict__ x1, int ld1, int K1, const uint16_t* __restrict__ x2, int ld2, int K2,
+    const uint16_t* __restrict__ dY, int lddy, const uint16_t* __restrict__ Ym, int ldym, float mscale, int N,
+    float* __restrict__ gpart, int n, int rows_per_chunk) {
+  constexpr int NT = WGT_WAVES * 64;
+  constexpr int KROWS = KT * 32;
+  constexpr int KPW = (KT + WGT_WAVES - 1) / WGT_WAVES;     // k-tiles per wave
+  constexpr int XCH = KROWS / 8;                            // 16-byte chunks per staged X row
+  constexpr int PFX = (TILE * XCH + NT - 1) / NT;
+  constexpr int PFY = (TILE * 8 + NT - 1) / NT;             // 64 gradient columns = 8 chunks
+  __shared__ __attribute__((aligned(16))) uint16_t sXt[KROWS * TR];
+  __shared__ __attribute__((aligned(16))) uint16_t sDt[64 * TR];
+  const int tid = threadIdx.x;
+  const int K = K1 + K2;
+  const int c0 = blockIdx.y * 64;
+  const int r_begin = blockIdx.x * rows_per_chunk, r_end = min(n, r_begin + rows_per_chunk);
+  const int lane = tid & 63, h = lane >> 5, lr = lane & 31, wv = tid >> 6;
+  const int xch = (K + 7) / 8;                              // chunks that carry features
+
+  f32x16 acc[KPW][2];
+#pragma unroll
+  for (int a = 0; a < KPW; ++a) { acc[a][0] = f32x16{}; acc[a][1] = f32x16{}; }
+
+  uint4 px[PFX], py[PFY];
+  auto prefetch = [&](int r0) {
+#pragma unroll
+    for (int q = 0; q < PFX; ++q) {
+      const int i = tid + q * NT;
+      const int rr = i % TILE, ch = i / TILE;
+      px[q] = (ch < xch && r0 + rr < r_end) ? load_cat8(x1, ld1, K1, x2, ld2, K2, r0 + rr, 8 * ch)
+                                            : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int q = 0; q < PFY; ++q) {
+      const int i = tid + q * NT;
+      const int rr = i % TILE, ch = i / TILE;
+      py[q] = (i < TILE * 8 && r0 + rr < r_end) ? load_masked8(dY, lddy, Ym, ldym, mscale, N, r0 + rr, c0 + 8 * ch)
+                                                : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  if (r_begin < r_end) prefetch(r_begin);
+  for (int r0 = r_begin; r0 < r_end; r0 += TILE) {
+    __syncthreads();                                       // previous tile's images consumed
+#pragma unroll
+    for (int q = 0; q < PFX; ++q) {
+      const int i = tid + q * NT;
+      const int rr = i % TILE, ch = i / TILE;
+      if (ch < XCH) {
+        const uint32_t w[4] = {px[q].x, px[q].y, px[q].z, px[q].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = 8 * ch + e;
+          uint16_t v = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
+          if (k == K) v = (r0 + rr < r_end) ? (uint16_t)0x3f80u : (uint16_t)0;   // ones column (bf16 1.0)
+          sXt[k * TR + rr] = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PFY; ++q) {
+      const int i = tid + q * NT;
+      const int rr = i % TILE, ch = i / TILE;
+      if (i < TILE * 8) {
+        const uint32_t w[4] = {py[q].x, py[q].y, py[q].z, py[q].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sDt[(8 * ch + e) * TR + rr] = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
+      }
+    }
+    if (r0 + TILE < r_end) prefetch(r0 + TILE);
+    __syncthreads();
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 b0 = as_bf16x8(*reinterpret_cast<const uint4*>(sDt + lr * TR + 16 * s2 + 8 * h));
+      const bf16x8 b1 = as_bf16x8(*reinterpret_cast<const uint4*>(sDt + (32 + lr) * TR + 16 * s2 + 8 * h));
+#pragma unroll
+      for (int a = 0; a < KPW; ++a) {
+        const int kt = wv + WGT_WAVES * a;
+        if (kt < KT) {
+          const bf16x8 ax = as_bf16x8(*reinterpret_cast<const uint4*>(sXt + (32 * kt + lr) * TR + 16 * s2 + 8 * h));
+          acc[a][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b0, acc[a][0], 0, 0, 0);
+          acc[a][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, b1, acc[a][1], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // slab of this chunk: rows k in [0, K], columns c0 + [0, 64) (lane = column: coalesced)
+  float* gp = gpart + (size_t)blockIdx.x * (K + 1) * N;
+#pragma unroll
+  for (int a = 0; a < KPW; ++a) {
+    const int kt = wv + WGT_WAVES * a;
+    if (kt >= KT) continue;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = 32 * kt + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (k > K) continue;
+      if (c0 + lr < N) gp[(size_t)k * N + c0 + lr] = acc[a][0][q];
+      if (c0 + 32 + lr < N) gp[(size_t)k * N + c0 + 32 + lr] = acc[a][1][q];
+    }
+  }
+}
+
+// out[i] = sum_{c < chunks} gpart[c][i] (fixed order), i < count; the first k_rows * N
+// go to dW, the last N (the ones row) to db when db != nullptr
+__global__ __launch_bounds__(256) void lin_reduce_kernel(const float* __restrict__ gpart, int chunks, long count,
+                                                         int N, float* __restrict__ dW, float* __restrict__ db) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += gpart[(size_t)c * count + i];
+  const long kw = count - N;
+  if (i < kw) dW[i] = s;
+  else if (db) db[i - kw] = s;
+}
+
+// ---------------------------------------------------------------- launchers
+static int grid_rows(int n, int waves) {
+  const int tiles = (n + TILE - 1) / TILE;
+  return std::max(1, std::min(device_cus(), (tiles + waves - 1) / waves));
+}
+
+static int pick_ks(int K) {
+  const int ks = (K + 15) / 16;
+  for (int c : {4, 8, 16, 24, 32}) if (ks <= c) return c;
+  return -1;
+}
+
+// widest slab (multiple of 32 columns) whose bf16 weight image fits the LDS budget
+static int slab_cols(int N, int KP) {
+  const size_t budget = 144 * 1024;
+  int cols = (N + 31) / 32 * 32;
+  while (cols > 32 && (size_t)cols * (KP + 8) * 2 + (size_t)cols * 4 > budget) cols -= 32;
+  return cols;
+}
+
+template <int KS>
+static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const float* W, int N,
+                      const float* bias, uint16_t* Y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1,
+                      uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
+                      hipStream_t st) {
+  constexpr int KP = KS * 16;
+  const int ncols = slab_cols(std::max(N, ldy), KP);
+  const size_t lds = (size_t)ncols * (KP + 8) * 2 + (size_t)ncols * 4;
+  constexpr int WV = FwdWaves<KS>::value;
+  (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
+  hipLaunchKernelGGL((lin_fwd_kernel<KS>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
+                     x1, ld1, K1, x2, ld2, K2, W, N, bias, Y, ldy, n, ncols, relu, p, k0, k1, step, thr8, row0,
+                     stepp, rscale);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2, const float* W,
+                                  int N, const float* bias, void* Y, int ldy, int n, int relu, float p, uint32_t k0,
+                                  uint32_t k1, uint32_t step, uint32_t row0, const int* stepp, const float* rscale,
+                                  hipStream_t st) {
+  if (n <= 0) return 0;
+  if ((x2 && K1 % 8) || ld1 % 8 || (x2 && (ld2 % 8)) || ldy % 8 || K1 > ld1 || (x2 && K2 > ld2) || N > ldy)
+    return -3;
+  if (!x2) K2 = 0;
+  const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
+  const int ks = pick_ks(K1 + K2);
+  auto a = (const uint16_t*)x1;
+  auto b = (const uint16_t*)x2;
+  auto y = (uint16_t*)Y;
+#define LF(c) if (ks == c) return fwd_launch<c>(a, ld1, K1, b, ld2, K2, W, N, bias, y, ldy, n, relu, p, k0, k1, step, thr8, row0, stepp, rscale, st);
+  LF(4) LF(8) LF(16) LF(24) LF(32)
+#undef LF
+  return -1;
+}
+
+template <int KN>
+static int bwd_data_launch(const uint16_t* dY, int lddy, const uint16_t* Ym, int ldym, float mscale, int N,
+                           const float* W, int K1, int K2, uint16_t* dX1, int ldx1, uint16_t* dX2, int ldx2,
+                           const float* rscale, int n, hipStream_t st) {
+  constexpr int NP = KN * 16;
+  const int K = K1 + K2;
+  const int kcols = slab_cols(K, NP);
+  const size_t lds = (size_t)kcols * (NP + 8) * 2;
+  constexpr int WV = FwdWaves<KN>::value;
+  (void)hipFuncSetAttribute((const void*)lin_bwd_data_kernel<KN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
+  const int slabs = (K + kcols - 1) / kcols;
+  hipLaunchKernelGGL((lin_bwd_data_kernel<KN>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
+                     dY, lddy, Ym, ldym, mscale, N, W, K1, K2, dX1, ldx1, dX2, ldx2, rscale, n, kcols);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_launch_lin_bwd_data(const void* dY, int lddy, const void* Ym, int ldym, float mscale, int N,
+                                       const float* W, int K1, int K2, void* dX1, int ldx1, void* dX2, int ldx2,
+                                       const float* rscale, int n, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (lddy % 8 || (Ym && ldym % 8) || (dX2 && K1 % 8) || ldx1 % 8 || (dX2 && ldx2 % 8) || N > lddy) return -3;
+  if (!dX2) K2 = 0;
+  const int kn = pick_ks(N);
+  auto d = (const uint16_t*)dY;
+  auto m = (const uint16_t*)Ym;
+  auto o1 = (uint16_t*)dX1;
+  auto o2 = (uint16_t*)dX2;
+#define LB(c) if (kn == c) return bwd_data_launch<c>(d, lddy, m, ldym, mscale, N, W, K1, K2, o1, ldx1, o2, ldx2, rscale, n, st);
+  LB(4) LB(8) LB(16) LB(24) LB(32)
+#undef LB
+  return -1;
+}
+
+// chunk count of the split-K weight gradient for n rows and N columns (fills the chip)
+extern "C" int gnn_lin_wgrad_chunks(int n, int N) {
+  const int tiles = std::max(1, (n + TILE - 1) / TILE);
+  const int slabs = std::max(1, (N + 63) / 64);
+  const int want = std::max(1, 2 * device_cus() / slabs);
+  return std::min(tiles, want);
+}
+
+template <int KT>
+static int wgt_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const uint16_t* dY,
+                      int lddy, const uint16_t* Ym, int ldym, float mscale, int N, float* gpart, int n, int chunks,
+                      hipStream_t st) {
+  const int tiles = (n + TILE - 1) / TILE;
+  const int rpc = (tiles + chunks - 1) / chunks * TILE;
+  hipLaunchKernelGGL((lin_bwd_weight_kernel<KT>), dim3(chunks, (N + 63) / 64), dim3(WGT_WAVES * 64), 0, st, x1, ld1,
+                     K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, rpc);
+  return (int)hipGetLastError();
+}
+
+// gpart: [chunks][K1 + K2 + 1][N] fp32 scratch (chunks = gnn_lin_wgrad_chunks(n, N));
+// dW: [K1 + K2][N] fp32, db: [N] fp32 (optional)
+extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2,
+                                         const void* dY, int lddy, const void* Ym, int ldym, float mscale, int N,
+                                         float* gpart, float* dW, float* db, int n, hipStream_t st) {
+  if ((x2 && K1 % 8) || ld1 % 8 || (x2 && ld2 % 8) || lddy % 8 || (Ym && ldym % 8) || N > lddy) return -3;
+  if (!x2) K2 = 0;
+  const int K = K1 + K2;
+  const int chunks = gnn_lin_wgrad_chunks(std::max(n, 1), N);
+  if (n > 0) {
+    const int kt = (K + 1 + 31) / 32;
+    auto a = (const uint16_t*)x1;
+    auto b = (const uint16_t*)x2;
+    auto d = (const uint16_t*)dY;
+    auto m = (const uint16_t*)Ym;
+    int rc = -1;
+#define LW(c) if (rc == -1 && kt <= c) rc = wgt_launch<c>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, st);
+    LW(2) LW(4) LW(5) LW(8) LW(9) LW(12) LW(17)
+#undef LW
+    if (rc != 0) return rc;
+  } else {
+    (void)hipMemsetAsync(gpart, 0, sizeof(float) * (size_t)(K + 1) * N * chunks, st);
+  }
+  const long count = (long)(K + 1) * N;
+  hipLaunchKernelGGL(lin_reduce_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, gpart,
+                     n > 0 ? chunks : 1, count, N, dW, db);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,149 @@
+"""Fused dense layers of the GNN track (``csrc/kernels/gnn_linear.hip``).
+
+Three ops cover the dense half of every message-passing layer (GraphSAGE, the GAT
+projection, each layer of the L-layer GCN), bf16 storage / fp32 accumulation:
+
+* :func:`lin_fwd`         ``Y = epi([X1 | X2] W + b)``, epi = ReLU, Philox dropout
+                          (the fused-kernel mask convention, keyed by global row and
+                          a device step counter), row scale;
+* :func:`lin_bwd_data`    ``[dX1 | dX2] = rs * ((dY * m) W^T)``;
+* :func:`lin_bwd_weight`  ``dW, db = [X1 | X2]^T (dY * m), colsum(dY * m)``.
+
+``m = [Ym > 0] / (1 - p)``: the mask is recovered from the layer's stored output
+``Ym`` (after ReLU and dropout), so no mask tensor exists.  ``[X1 | X2]`` is a
+virtual concatenation (no copy).  Every op has a CPU branch that is the fp32
+reference of the same arithmetic (operands rounded to bf16 as the kernels see
+them) -- the numerics oracle of the GPU tests.  On a GPU the HIP kernels are
+mandatory: a shape no compiled variant covers raises.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import native
+from .ops import _st, _step_args, _step_value, dropout_keep_mask
+
+_GPART = {}
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else 0
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError("%s: no HIP variant / bad shape (code %d)" % (what, rc))
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _cat(x1, K1, x2, K2):
+    a = x1[:, :K1].float()
+    return a if x2 is None else torch.cat([a, x2[:, :K2].float()], 1)
+
+
+def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None,
+            K1: Optional[int] = None, K2: Optional[int] = None, relu: bool = False, p: float = 0.0, key=(0, 0),
+            step=0, row0: int = 0, rscale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+            ldy: Optional[int] = None) -> torch.Tensor:
+    """``out[:, :N] = epi([x1[:, :K1] | x2[:, :K2]] @ W + bias)`` in bf16 (columns N..ldy zero).
+
+    ``W``: fp32 [K1 + K2, N]; ``step``: int or device int32[1] (read at launch time)."""
+    n = x1.shape[0]
+    K1 = x1.shape[1] if K1 is None else int(K1)
+    K2 = 0 if x2 is None else (x2.shape[1] if K2 is None else int(K2))
+    N = W.shape[1]
+    if W.shape[0] != K1 + K2:
+        raise ValueError("W has %d rows, inputs give K = %d" % (W.shape[0], K1 + K2))
+    if out is None:
+        ldy = ldy or (N + 7) // 8 * 8
+        out = torch.empty(n, ldy, dtype=torch.bfloat16, device=x1.device)
+    if x1.is_cuda:
+        sv, sp = _step_args(step)
+        rc = native.hip().gnn_lin_fwd(x1.data_ptr(), x1.stride(0), K1, _ptr(x2), x2.stride(0) if x2 is not None else 0,
+                                      K2, W.data_ptr(), N, _ptr(bias), out.data_ptr(), out.stride(0), n, int(relu),
+                                      float(p), int(key[0]), int(key[1]), sv, int(row0), sp, _ptr(rscale), _st(x1))
+        _check(rc, "lin_fwd")
+        return out
+    y = _cat(x1, K1, x2, K2) @ _bf(W)
+    if bias is not None:
+        y = y + bias.float()
+    if relu:
+        y = torch.relu(y)
+    if p > 0:
+        keep = dropout_keep_mask(n, N, p, key, _step_value(step), row0)
+        y = torch.where(keep, y / (1 - p), torch.zeros_like(y))
+    if rscale is not None:
+        y = y * rscale[:, None].float()
+    out.zero_()
+    out[:, :N] = y.to(torch.bfloat16)
+    return out
+
+
+def _masked(dY, N, Ym, mscale):
+    g = dY[:, :N].float()
+    if Ym is not None:
+        g = torch.where(Ym[:, :N].float() > 0, g, torch.zeros_like(g))
+    return _bf(g * mscale) if (Ym is not None or mscale != 1.0) else g
+
+
+def lin_bwd_data(dY: torch.Tensor, W: torch.Tensor, K1: int, K2: int = 0, Ym: Optional[torch.Tensor] = None,
+                 mscale: float = 1.0, rscale: Optional[torch.Tensor] = None, out1: Optional[torch.Tensor] = None,
+                 out2: Optional[torch.Tensor] = None):
+    """``[out1 | out2] = rscale * ((dY[:, :N] * m) @ W^T)``, ``m = [Ym > 0] * mscale``; bf16.
+    Returns (out1, out2) (out2 None when K2 == 0)."""
+    n, N = dY.shape[0], W.shape[1]
+    if out1 is None:
+        out1 = torch.empty(n, (K1 + 7) // 8 * 8, dtype=torch.bfloat16, device=dY.device)
+    if K2 and out2 is None:
+        out2 = torch.empty(n, (K2 + 7) // 8 * 8, dtype=torch.bfloat16, device=dY.device)
+    if dY.is_cuda:
+        rc = native.hip().gnn_lin_bwd_data(dY.data_ptr(), dY.stride(0), _ptr(Ym), Ym.stride(0) if Ym is not None else 0,
+                                           float(mscale), N, W.data_ptr(), int(K1), int(K2), out1.data_ptr(),
+                                           out1.stride(0), _ptr(out2) if K2 else 0,
+                                           out2.stride(0) if K2 else 0, _ptr(rscale), n, _st(dY))
+        _check(rc, "lin_bwd_data")
+        return out1, (out2 if K2 else None)
+    d = _masked(dY, N, Ym, mscale) @ _bf(W).t()
+    if rscale is not None:
+        d = d * rscale[:, None].float()
+    out1[:, :K1] = d[:, :K1].to(torch.bfloat16)
+    if K2:
+        out2[:, :K2] = d[:, K1:].to(torch.bfloat16)
+    return out1, (out2 if K2 else None)
+
+
+def lin_bwd_weight(x1: torch.Tensor, dY: torch.Tensor, N: int, x2: Optional[torch.Tensor] = None,
+                   K1: Optional[int] = None, K2: Optional[int] = None, Ym: Optional[torch.Tensor] = None,
+                   mscale: float = 1.0, dW: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None):
+    """``dW = [x1 | x2]^T (dY * m)`` (fp32 [K1 + K2, N]) and ``db = colsum(dY * m)`` (fp32 [N]);
+    split-K over row chunks, fixed-order reduction (deterministic)."""
+    n = x1.shape[0]
+    K1 = x1.shape[1] if K1 is None else int(K1)
+    K2 = 0 if x2 is None else (x2.shape[1] if K2 is None else int(K2))
+    dev = x1.device
+    if dW is None:
+        dW = torch.empty(K1 + K2, N, dtype=torch.float32, device=dev)
+    if db is None:
+        db = torch.empty(N, dtype=torch.float32, device=dev)
+    if x1.is_cuda:
+        hip = native.hip()
+        chunks = hip.gnn_lin_wgrad_chunks(max(n, 1), N)
+        shape = (chunks, K1 + K2 + 1, N)
+        key = (dev.index, shape)
+        gp = _GPART.get(key)
+        if gp is None:
+            gp = _GPART[key] = torch.empty(shape, dtype=torch.float32, device=dev)
+        rc = hip.gnn_lin_bwd_weight(x1.data_ptr(), x1.stride(0), K1, _ptr(x2), x2.stride(0) if x2 is not None else 0,
+                                    K2, dY.data_ptr(), dY.stride(0), _ptr(Ym), Ym.stride(0) if Ym is not None else 0,
+                                    float(mscale), N, gp.data_ptr(), dW.data_ptr(), db.data_ptr(), n, _st(x1))
+        _check(rc, "lin_bwd_weight")
+        return dW, db
+    g = _masked(dY, N, Ym, mscale)
+    dW.copy_(_cat(x1, K1, x2, K2).t() @ g)
+    db.copy_(g.sum(0))
+    return dW, db

@@ -89,3 +89,33 @@ def test_fused_gcn_checkpoint_roundtrip(tmp_path):
     a.train_step()
     b.train_step()
     np.testing.assert_array_equal(a.params.numpy(), b.params.numpy())
+
+
+def test_linear_reference_ops_match_autograd():
+    """CPU branch of gnn/linear.py (the GPU kernels' numerics oracle) = autograd of
+    relu([x1 | x2] W + b) on bf16-rounded operands."""
+    from cgnn_amd.gnn.linear import lin_bwd_data, lin_bwd_weight, lin_fwd
+    g = torch.Generator().manual_seed(0)
+    n, K1, K2, N = 64, 16, 8, 24
+    x1 = torch.randn(n, K1, generator=g).to(torch.bfloat16)
+    x2 = torch.randn(n, K2, generator=g).to(torch.bfloat16)
+    W = torch.randn(K1 + K2, N, generator=g)
+    b = torch.randn(N, generator=g)
+    dY = torch.randn(n, N, generator=g).to(torch.bfloat16)
+    y = lin_fwd(x1, W, b, x2=x2, relu=True)
+    d1, d2 = lin_bwd_data(dY, W, K1, K2, Ym=y)
+    dW, db = lin_bwd_weight(x1, dY, N, x2=x2, Ym=y)
+    xr = torch.cat([x1, x2], 1).float().requires_grad_()
+    Wr = W.to(torch.bfloat16).float().requires_grad_()
+    br = b.clone().requires_grad_()
+    yr = torch.relu(xr @ Wr + br)
+    yr.backward(dY.float())
+    assert torch.allclose(y[:, :N].float(), yr.detach(), rtol=1e-2, atol=1e-2)
+    assert torch.allclose(torch.cat([d1[:, :K1], d2[:, :K2]], 1).float(), xr.grad, rtol=1e-2, atol=2e-2)
+    assert torch.allclose(dW, Wr.grad, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(db, br.grad, rtol=1e-4, atol=1e-4)
+    # dropout: the mask of ops.dropout_keep_mask, scaled by 1/(1-p)
+    yd = lin_fwd(x1, W, b, x2=x2, relu=True, p=0.5, key=(1, 2), step=3)
+    from cgnn_amd.gnn.ops import dropout_keep_mask
+    keep = dropout_keep_mask(n, N, 0.5, (1, 2), 3)
+    assert torch.equal(yd[:, :N].float() == 0, (~keep) | (y[:, :N].float() == 0))

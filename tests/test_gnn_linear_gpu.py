@@ -1,0 +1,124 @@
+"""Fused dense-layer kernels (gnn_linear.hip) against their fp32 PyTorch reference
+(the CPU branch of gnn/linear.py: the same arithmetic on bf16-rounded operands)."""
+import pytest
+import torch
+
+from cgnn_amd.gnn.linear import lin_bwd_data, lin_bwd_weight, lin_fwd
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _bf(n, ld, K, gen, scale=1.0):
+    x = torch.zeros(n, ld, dtype=torch.bfloat16)
+    x[:, :K] = (torch.randn(n, K, generator=gen) * scale).to(torch.bfloat16)
+    return x
+
+
+def _close(a, b, rtol, atol):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), rtol=rtol, atol=atol)
+
+
+@pytest.mark.parametrize("n,K,ld,N,ldy,relu,p,rs", [
+    (5000, 100, 128, 256, 256, True, 0.5, True),     # layer 1 of GCN / SAGE on ogbn-products features
+    (4133, 256, 256, 40, 40, False, 0.0, False),     # last layer to 40 classes (arxiv)
+    (777, 47, 48, 256, 264, True, 0.0, True),        # odd K, padded output pitch
+    (3, 128, 128, 96, 96, True, 0.3, False),         # fewer rows than one tile
+])
+def test_lin_fwd_matches_reference(n, K, ld, N, ldy, relu, p, rs):
+    g = torch.Generator().manual_seed(n)
+    x = _bf(n, ld, K, g)
+    W = torch.randn(K, N, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g) * 0.1
+    r = torch.rand(n, generator=g) + 0.5 if rs else None
+    key = (123, 456)
+    ref = lin_fwd(x, W, b, K1=K, relu=relu, p=p, key=key, step=7, row0=11, rscale=r, ldy=ldy)
+    out = lin_fwd(x.to(DEV), W.to(DEV), b.to(DEV), K1=K, relu=relu, p=p, key=key,
+                  step=torch.tensor([7], dtype=torch.int32, device=DEV), row0=11,
+                  rscale=r.to(DEV) if rs else None, ldy=ldy)
+    torch.cuda.synchronize()
+    _close(out, ref, 2e-2, 2e-2)
+    if p > 0:   # identical dropout masks
+        assert torch.equal(out.cpu()[:, :N] == 0, ref[:, :N] == 0) or \
+            (out.cpu()[:, :N] == 0).ne(ref[:, :N] == 0).float().mean() < 1e-3
+    assert torch.all(out.cpu()[:, N:] == 0)
+
+
+def test_lin_fwd_two_inputs_is_the_concatenation():
+    g = torch.Generator().manual_seed(1)
+    n, K1, K2, N = 3000, 256, 256, 256
+    x1, x2 = _bf(n, K1, K1, g), _bf(n, K2, K2, g)
+    W = torch.randn(K1 + K2, N, generator=g) / 20
+    b = torch.randn(N, generator=g)
+    out = lin_fwd(x1.to(DEV), W.to(DEV), b.to(DEV), x2=x2.to(DEV), relu=True)
+    cat = lin_fwd(torch.cat([x1, x2], 1).to(DEV), W.to(DEV), b.to(DEV), relu=True)
+    ref = lin_fwd(x1, W, b, x2=x2, relu=True)
+    _close(out, ref, 2e-2, 3e-2)
+    assert torch.equal(out, cat)
+
+
+@pytest.mark.parametrize("n,N,K1,K2,mask,ms,rs", [
+    (5000, 256, 100, 0, True, 2.0, True),
+    (3001, 256, 256, 256, True, 1.0, False),
+    (700, 47, 256, 0, False, 1.0, True),
+])
+def test_lin_bwd_data_matches_reference(n, N, K1, K2, mask, ms, rs):
+    g = torch.Generator().manual_seed(n + N)
+    ldd = (N + 7) // 8 * 8
+    dY = _bf(n, ldd, N, g)
+    Ym = torch.relu(_bf(n, ldd, N, g).float()).to(torch.bfloat16) if mask else None
+    W = torch.randn(K1 + K2, N, generator=g) / N ** 0.5
+    r = torch.rand(n, generator=g) + 0.5 if rs else None
+    ref1, ref2 = lin_bwd_data(dY, W, K1, K2, Ym=Ym, mscale=ms, rscale=r)
+    o1, o2 = lin_bwd_data(dY.to(DEV), W.to(DEV), K1, K2, Ym=Ym.to(DEV) if mask else None, mscale=ms,
+                          rscale=r.to(DEV) if rs else None)
+    torch.cuda.synchronize()
+    _close(o1[:, :K1], ref1[:, :K1], 2e-2, 2e-2)
+    if K2:
+        _close(o2[:, :K2], ref2[:, :K2], 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("n,K1,K2,N,mask", [
+    (10007, 128, 0, 256, True),       # arxiv hidden layer
+    (5000, 100, 0, 47, False),        # odd widths
+    (4100, 256, 256, 256, True),      # SAGE [h_dst | agg]
+    (17, 64, 0, 64, True),            # a single partial tile
+])
+def test_lin_bwd_weight_matches_reference(n, K1, K2, N, mask):
+    g = torch.Generator().manual_seed(n)
+    ld1 = (K1 + 7) // 8 * 8
+    ldd = (N + 7) // 8 * 8
+    x1 = _bf(n, ld1, K1, g)
+    x2 = _bf(n, K2, K2, g) if K2 else None
+    dY = _bf(n, ldd, N, g, 0.01)
+    Ym = torch.relu(_bf(n, ldd, N, g).float()).to(torch.bfloat16) if mask else None
+    dW_ref, db_ref = lin_bwd_weight(x1, dY, N, x2=x2, K1=K1, Ym=Ym, mscale=2.0 if mask else 1.0)
+    args = dict(x2=x2.to(DEV) if K2 else None, K1=K1, Ym=Ym.to(DEV) if mask else None, mscale=2.0 if mask else 1.0)
+    dW, db = lin_bwd_weight(x1.to(DEV), dY.to(DEV), N, **args)
+    dW2, db2 = lin_bwd_weight(x1.to(DEV), dY.to(DEV), N, **args)
+    torch.cuda.synchronize()
+    scale = dW_ref.abs().max().item()
+    _close(dW, dW_ref, 1e-3, 1e-4 * scale)
+    _close(db, db_ref, 1e-3, 1e-4 * db_ref.abs().max().item())
+    assert torch.equal(dW, dW2) and torch.equal(db, db2)          # deterministic (no atomics)
+
+
+def test_lin_layer_gradients_match_autograd():
+    """fwd + both backward kernels = autograd of relu(x W + b) (dropout off), fp32 reference."""
+    g = torch.Generator().manual_seed(3)
+    n, K, N = 2048, 128, 256
+    x = _bf(n, K, K, g)
+    W = torch.randn(K, N, generator=g) / 12
+    b = torch.randn(N, generator=g) * 0.1
+    dY = _bf(n, N, N, g, 0.1)
+    y = lin_fwd(x.to(DEV), W.to(DEV), b.to(DEV), relu=True)
+    dX, _ = lin_bwd_data(dY.to(DEV), W.to(DEV), K, Ym=y)
+    dW, db = lin_bwd_weight(x.to(DEV), dY.to(DEV), N, Ym=y)
+    xr = x.float().requires_grad_()
+    Wr = W.to(torch.bfloat16).float().requires_grad_()
+    br = b.clone().requires_grad_()
+    yr = torch.relu(xr @ Wr + br)
+    yr.backward(dY.float())
+    _close(dX, xr.grad, 3e-2, 3e-2)
+    _close(dW, Wr.grad, 2e-2, 2e-2 * Wr.grad.abs().max().item())
+    _close(db, br.grad, 2e-2, 2e-2 * br.grad.abs().max().item())
