@@ -49,7 +49,7 @@ int rff_launch_fwd_bwd(int, const float*, const float*, const float*, float*, fl
                        int, int, int, int, float, hipStream_t);
 // GNN track
 int gnn_launch_spmm(const int*, const int*, const void*, void*, const float*, const float*, int,
-                    int, int, int, int, int, int, int, const float*, int, const float*, hipStream_t);
+                    int, int, int, int, int, int, int, const float*, int, const float*, int, hipStream_t);
 int gnn_launch_spmm_ce(const int*, const int*, const void*, const float*, const float*,
                        const int*, const uint8_t*, float*, void*, const float*, int, int, int, int, int, float,
                        const int*, hipStream_t);
@@ -81,12 +81,14 @@ int gnn_launch_dense_bwd(const void*, const float*, const void*, void*, int, int
                          hipStream_t);
 int gnn_launch_lin_fwd(const void*, int, int, const void*, int, int, const float*, int, const float*, void*, int,
                        int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, const int*, const float*,
-                       hipStream_t);
+                       const int*, void*, hipStream_t);
 int gnn_launch_lin_bwd_data(const void*, int, const void*, int, float, int, const float*, int, int, void*, int,
-                            void*, int, const float*, int, hipStream_t);
+                            void*, int, const float*, int, int, void*, hipStream_t);
+long gnn_lin_fwd_image_bytes(int, int, int);
+long gnn_lin_bwd_image_bytes(int, int);
 int gnn_lin_wgrad_chunks(int, int);
 int gnn_launch_lin_bwd_weight(const void*, int, int, const void*, int, int, const void*, int, const void*, int,
-                              float, int, float*, float*, float*, int, hipStream_t);
+                              float, int, float*, float*, float*, int, const int*, hipStream_t);
 }
 
 static inline hipStream_t S(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
@@ -202,15 +204,16 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("gnn_spmm", [](uint64_t rowptr, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, uint64_t bias,
                        int n_rows, int F, int ld_x, int ld_y, int x_bf16, int y_bf16, int relu, int unit_col,
-                       uint64_t st, uint64_t init, int ldi, uint64_t cscale) {
+                       uint64_t st, uint64_t init, int ldi, uint64_t cscale, int init_rows) {
     chk(gnn_launch_spmm(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(x), Pt<void>(y),
                         Pt<const float>(rscale), Pt<const float>(bias), n_rows, F, ld_x, ld_y, x_bf16,
-                        y_bf16, relu, unit_col, Pt<const float>(init), ldi, Pt<const float>(cscale), S(st)),
+                        y_bf16, relu, unit_col, Pt<const float>(init), ldi, Pt<const float>(cscale), init_rows,
+                        S(st)),
         "gnn_spmm");
   }, py::arg("rowptr"), py::arg("col"), py::arg("x"), py::arg("y"), py::arg("rscale"), py::arg("bias"),
      py::arg("n_rows"), py::arg("F"), py::arg("ld_x"), py::arg("ld_y"), py::arg("x_bf16"), py::arg("y_bf16"),
      py::arg("relu"), py::arg("unit_col"), py::arg("st"), py::arg("init") = 0, py::arg("ldi") = 0,
-     py::arg("cscale") = 0);
+     py::arg("cscale") = 0, py::arg("init_rows") = -1);
   m.def("gnn_spmm_ce", [](uint64_t rowptr, uint64_t col, uint64_t z, uint64_t rscale, uint64_t bias,
                           uint64_t labels, uint64_t mask, uint64_t stats, uint64_t dlogits, uint64_t init, int ldi,
                           int n_rows, int C, int ld, int mode, float inv_count, uint64_t st, uint64_t gslot) {
@@ -294,25 +297,36 @@ PYBIND11_MODULE(_hip, m) {
   // generic fused dense layers (gnn_linear.hip); return codes: 0 ok, -1 no variant, -3 bad shape
   m.def("gnn_lin_fwd", [](uint64_t x1, int ld1, int K1, uint64_t x2, int ld2, int K2, uint64_t w, int N, uint64_t b,
                           uint64_t y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step,
-                          uint32_t row0, uint64_t stepp, uint64_t rscale, uint64_t st) {
+                          uint32_t row0, uint64_t stepp, uint64_t rscale, uint64_t st, uint64_t idx1, uint64_t wimg) {
     return gnn_launch_lin_fwd(Pt<const void>(x1), ld1, K1, Pt<const void>(x2), ld2, K2, Pt<const float>(w), N,
                               Pt<const float>(b), Pt<void>(y), ldy, n, relu, p, k0, k1, step, row0,
-                              Pt<const int>(stepp), Pt<const float>(rscale), S(st));
-  });
+                              Pt<const int>(stepp), Pt<const float>(rscale), Pt<const int>(idx1), Pt<void>(wimg),
+                              S(st));
+  }, py::arg("x1"), py::arg("ld1"), py::arg("K1"), py::arg("x2"), py::arg("ld2"), py::arg("K2"), py::arg("w"),
+     py::arg("N"), py::arg("b"), py::arg("y"), py::arg("ldy"), py::arg("n"), py::arg("relu"), py::arg("p"),
+     py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("stepp"), py::arg("rscale"),
+     py::arg("st"), py::arg("idx1") = 0, py::arg("wimg") = 0);
+  m.def("gnn_lin_fwd_image_bytes", &gnn_lin_fwd_image_bytes);
+  m.def("gnn_lin_bwd_image_bytes", &gnn_lin_bwd_image_bytes);
   m.def("gnn_lin_bwd_data", [](uint64_t dy, int lddy, uint64_t ym, int ldym, float mscale, int N, uint64_t w, int K1,
                                int K2, uint64_t dx1, int ldx1, uint64_t dx2, int ldx2, uint64_t rscale, int n,
-                               uint64_t st) {
+                               uint64_t st, int dx1_f32, uint64_t wimg) {
     return gnn_launch_lin_bwd_data(Pt<const void>(dy), lddy, Pt<const void>(ym), ldym, mscale, N, Pt<const float>(w),
-                                   K1, K2, Pt<void>(dx1), ldx1, Pt<void>(dx2), ldx2, Pt<const float>(rscale), n, S(st));
-  });
+                                   K1, K2, Pt<void>(dx1), ldx1, Pt<void>(dx2), ldx2, Pt<const float>(rscale), n,
+                                   dx1_f32, Pt<void>(wimg), S(st));
+  }, py::arg("dy"), py::arg("lddy"), py::arg("ym"), py::arg("ldym"), py::arg("mscale"), py::arg("N"), py::arg("w"),
+     py::arg("K1"), py::arg("K2"), py::arg("dx1"), py::arg("ldx1"), py::arg("dx2"), py::arg("ldx2"),
+     py::arg("rscale"), py::arg("n"), py::arg("st"), py::arg("dx1_f32") = 0, py::arg("wimg") = 0);
   m.def("gnn_lin_wgrad_chunks", &gnn_lin_wgrad_chunks);
   m.def("gnn_lin_bwd_weight", [](uint64_t x1, int ld1, int K1, uint64_t x2, int ld2, int K2, uint64_t dy, int lddy,
                                  uint64_t ym, int ldym, float mscale, int N, uint64_t gpart, uint64_t dw, uint64_t db,
-                                 int n, uint64_t st) {
+                                 int n, uint64_t st, uint64_t idx1) {
     return gnn_launch_lin_bwd_weight(Pt<const void>(x1), ld1, K1, Pt<const void>(x2), ld2, K2, Pt<const void>(dy), lddy,
                                      Pt<const void>(ym), ldym, mscale, N, Pt<float>(gpart), Pt<float>(dw),
-                                     Pt<float>(db), n, S(st));
-  });
+                                     Pt<float>(db), n, Pt<const int>(idx1), S(st));
+  }, py::arg("x1"), py::arg("ld1"), py::arg("K1"), py::arg("x2"), py::arg("ld2"), py::arg("K2"), py::arg("dy"),
+     py::arg("lddy"), py::arg("ym"), py::arg("ldym"), py::arg("mscale"), py::arg("N"), py::arg("gpart"),
+     py::arg("dw"), py::arg("db"), py::arg("n"), py::arg("st"), py::arg("idx1") = 0);
   m.def("gnn_cast_bf16", [](uint64_t src, uint64_t dst, long n, uint64_t st) {
     chk(gnn_launch_cast_bf16(Pt<const float>(src), Pt<void>(dst), n, S(st)), "gnn_cast_bf16");
   });

@@ -78,9 +78,15 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, int valid) {
 
 // 8 features [f0, f0 + 8) of row `row` of the virtual concatenation [X1 | X2]
 // (K1 % 8 == 0 when X2 is given, so a chunk never straddles the two); zeros past K1 + K2
+// idx1 (optional): X1 row of output row r is idx1[r] (gather-on-load: GraphSAGE's
+// first layer reads the seed / frontier rows straight out of the resident features)
 __device__ __forceinline__ uint4 load_cat8(const uint16_t* __restrict__ x1, int ld1, int K1,
-                                           const uint16_t* __restrict__ x2, int ld2, int K2, int row, int f0) {
-  if (f0 < K1) return keep_first(*reinterpret_cast<const uint4*>(x1 + (size_t)row * ld1 + f0), K1 - f0);
+                                           const uint16_t* __restrict__ x2, int ld2, int K2, int row, int f0,
+                                           const int* __restrict__ idx1) {
+  if (f0 < K1) {
+    const size_t r1 = idx1 ? (size_t)idx1[row] : (size_t)row;
+    return keep_first(*reinterpret_cast<const uint4*>(x1 + r1 * ld1 + f0), K1 - f0);
+  }
   const int g = f0 - K1;
   if (x2 && g < K2) return keep_first(*reinterpret_cast<const uint4*>(x2 + (size_t)row * ld2 + g), K2 - g);
   return make_uint4(0u, 0u, 0u, 0u);
@@ -134,7 +140,10 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     const uint16_t* __restrict__ x1, int ld1, int K1, const uint16_t* __restrict__ x2, int ld2, int K2,
     const float* __restrict__ W, int N, const float* __restrict__ bias, uint16_t* __restrict__ Y, int ldy,
     int n, int ncols, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
-    uint32_t row0, const int* __restrict__ stepp, const float* __restrict__ rscale) {
+    uint32_t row0, const int* __restrict__ stepp, const float* __restrict__ rscale, const int* __restrict__ idx1,
+    const uint16_t* __restrict__ wimg) {
+  // wimg: the bf16 LDS image of every column slab ([slabs][ncols][WS], lin_prep_fwd_kernel):
+  // one vectorised copy per block instead of converting / transposing the fp32 weights
   if (stepp) step = (uint32_t)*stepp;
   constexpr int KP = KS * 16;
   constexpr int WS = KP + 8;                     // padded row stride of the W^T slab
@@ -142,10 +151,11 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
   uint16_t* sWT = lds;                           // [ncols][WS]
   float* sB = reinterpret_cast<float*>(sWT + (size_t)ncols * WS);   // [ncols]
   const int c0 = blockIdx.y * ncols;
-  const int K = K1 + K2;
-  for (int i = threadIdx.x; i < ncols * KP; i += blockDim.x) {
-    const int k = i / ncols, c = i - k * ncols;            // consecutive threads: consecutive c (coalesced W)
-    sWT[c * WS + k] = bf16_bits(k < K && c0 + c < N ? W[(size_t)k * N + c0 + c] : 0.f);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(wimg + (size_t)blockIdx.y * ncols * WS);
+    uint4* dst = reinterpret_cast<uint4*>(sWT);
+    const int n16 = ncols * WS / 8;
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
   }
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) sB[c] = (bias && c0 + c < N) ? bias[c0 + c] : 0.f;
   __syncthreads();
@@ -163,7 +173,7 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     bf16x8 bx[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      bx[s] = as_bf16x8(rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h) : make_uint4(0u, 0u, 0u, 0u));
+      bx[s] = as_bf16x8(rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h, idx1) : make_uint4(0u, 0u, 0u, 0u));
     const float rs = (rv && rscale) ? rscale[row] : 1.f;
 #pragma unroll 1
     for (int t = 0; t < nt; ++t) {
@@ -209,16 +219,20 @@ template <int KN, int FWD_WAVES = FwdWaves<KN>::value>
 __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
     const uint16_t* __restrict__ dY, int lddy, const uint16_t* __restrict__ Ym, int ldym, float mscale, int N,
     const float* __restrict__ W, int K1, int K2, uint16_t* __restrict__ dX1, int ldx1, uint16_t* __restrict__ dX2,
-    int ldx2, const float* __restrict__ rscale, int n, int kcols) {
+    int ldx2, const float* __restrict__ rscale, int n, int kcols, int dx1_f32, const uint16_t* __restrict__ wimg) {
+  // dx1_f32: dX1 is fp32 (e.g. the init partial of a following SpMM) instead of bf16;
+  // wimg: bf16 LDS image of every k slab ([slabs][kcols][WS], lin_prep_bwd_kernel)
   constexpr int NP = KN * 16;
   constexpr int WS = NP + 8;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* sW = lds;                            // [kcols][WS]: rows of W
   const int kb = blockIdx.y * kcols;
   const int K = K1 + K2;
-  for (int i = threadIdx.x; i < kcols * NP; i += blockDim.x) {
-    const int kk = i / NP, c = i - kk * NP;
-    sW[kk * WS + c] = bf16_bits(kb + kk < K && c < N ? W[(size_t)(kb + kk) * N + c] : 0.f);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(wimg + (size_t)blockIdx.y * kcols * WS);
+    uint4* dst = reinterpret_cast<uint4*>(sW);
+    const int n16 = kcols * WS / 8;
+    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31;
@@ -248,7 +262,13 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
         const int k = kb + 32 * t + 8 * g + 4 * h;          // 4 consecutive k, never straddling K1 (K1 % 8 == 0)
         const uint2 o = pack4(acc[4 * g] * rs, acc[4 * g + 1] * rs, acc[4 * g + 2] * rs, acc[4 * g + 3] * rs);
         if (k < K1) {
-          if (k < ldx1) *reinterpret_cast<uint2*>(dX1 + (size_t)row * ldx1 + k) = o;
+          if (k < ldx1) {
+            if (dx1_f32)
+              *reinterpret_cast<float4*>(reinterpret_cast<float*>(dX1) + (size_t)row * ldx1 + k) =
+                  make_float4(acc[4 * g] * rs, acc[4 * g + 1] * rs, acc[4 * g + 2] * rs, acc[4 * g + 3] * rs);
+            else
+              *reinterpret_cast<uint2*>(dX1 + (size_t)row * ldx1 + k) = o;
+          }
         } else if (dX2 && k - K1 < ldx2 && k < K1 + ldx2) {
           *reinterpret_cast<uint2*>(dX2 + (size_t)row * ldx2 + (k - K1)) = o;
         }
@@ -258,16 +278,17 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
 }
 
 // ============================================================================
-// lin_bwd_weight: gpart[chunk][k][c] = sum_{rows of chunk} [X1 | X2 | 1][row][k] (dY * m)[row][c]
-// for the 64-column slab c in [blockIdx.y * 64, +64); k = K1 + K2 is the ones column
-// (the bias gradient).  KT = k-tiles of 32 covering K1 + K2 + 1; wave w owns the
-// k-tiles w, w + 8, ...
+// lin_bwd_weight: gpart[chunk][k][c] = sum_{rows of chunk} [X1 | X2][row][k] (dY * m)[row][c]
+// for the 64-column slab c in [blockIdx.y * 64, +64), and gpart[chunk][K1 + K2][c] =
+// sum_rows (dY * m)[row][c] (the bias gradient, accumulated on the VALU by the threads
+// that stage the gradient tile, so K = 256 is exactly 8 balanced k-tiles).  KT = k-tiles
+// of 32 covering K1 + K2; wave w owns the k-tiles w, w + 8, ...
 // ============================================================================
 template <int KT>
 __global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
     const uint16_t* __restrict__ x1, int ld1, int K1, const uint16_t* __restrict__ x2, int ld2, int K2,
     const uint16_t* __restrict__ dY, int lddy, const uint16_t* __restrict__ Ym, int ldym, float mscale, int N,
-    float* __restrict__ gpart, int n, int rows_per_chunk) {
+    float* __restrict__ gpart, int n, int rows_per_chunk, const int* __restrict__ idx1) {
   constexpr int NT = WGT_WAVES * 64;
   constexpr int KROWS = KT * 32;
   constexpr int KPW = (KT + WGT_WAVES - 1) / WGT_WAVES;     // k-tiles per wave
@@ -276,6 +297,7 @@ __global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
   constexpr int PFY = (TILE * 8 + NT - 1) / NT;             // 64 gradient columns = 8 chunks
   __shared__ __attribute__((aligned(16))) uint16_t sXt[KROWS * TR];
   __shared__ __attribute__((aligned(16))) uint16_t sDt[64 * TR];
+  __shared__ float sdb[64 * 33];
   const int tid = threadIdx.x;
   const int K = K1 + K2;
   const int c0 = blockIdx.y * 64;
@@ -286,6 +308,11 @@ __global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
   f32x16 acc[KPW][2];
 #pragma unroll
   for (int a = 0; a < KPW; ++a) { acc[a][0] = f32x16{}; acc[a][1] = f32x16{}; }
+  float dsum[PFY][8];                                       // bias-gradient partials (staging threads)
+#pragma unroll
+  for (int q = 0; q < PFY; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dsum[q][e] = 0.f;
 
   uint4 px[PFX], py[PFY];
   auto prefetch = [&](int r0) {
@@ -293,7 +320,7 @@ __global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
     for (int q = 0; q < PFX; ++q) {
       const int i = tid + q * NT;
       const int rr = i % TILE, ch = i / TILE;
-      px[q] = (ch < xch && r0 + rr < r_end) ? load_cat8(x1, ld1, K1, x2, ld2, K2, r0 + rr, 8 * ch)
+      px[q] = (ch < xch && r0 + rr < r_end) ? load_cat8(x1, ld1, K1, x2, ld2, K2, r0 + rr, 8 * ch, idx1)
                                             : make_uint4(0u, 0u, 0u, 0u);
     }
 #pragma unroll
@@ -314,12 +341,7 @@ __global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
       if (ch < XCH) {
         const uint32_t w[4] = {px[q].x, px[q].y, px[q].z, px[q].w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int k = 8 * ch + e;
-          uint16_t v = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
-          if (k == K) v = (r0 + rr < r_end) ? (uint16_t)0x3f80u : (uint16_t)0;   // ones column (bf16 1.0)
-          sXt[k * TR + rr] = v;
-        }
+        for (int e = 0; e < 8; ++e) sXt[(8 * ch + e) * TR + rr] = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
       }
     }
 #pragma unroll
@@ -329,7 +351,11 @@ __global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
       if (i < TILE * 8) {
         const uint32_t w[4] = {py[q].x, py[q].y, py[q].z, py[q].w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) sDt[(8 * ch + e) * TR + rr] = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t b16 = (w[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+          sDt[(8 * ch + e) * TR + rr] = (uint16_t)b16;
+          dsum[q][e] += bf16_val(b16);
+        }
       }
     }
     if (r0 + TILE < r_end) prefetch(r0 + TILE);
@@ -349,7 +375,7 @@ __global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
       }
     }
   }
-  // slab of this chunk: rows k in [0, K], columns c0 + [0, 64) (lane = column: coalesced)
+  // slab of this chunk: rows k in [0, K), columns c0 + [0, 64) (lane = column: coalesced)
   float* gp = gpart + (size_t)blockIdx.x * (K + 1) * N;
 #pragma unroll
   for (int a = 0; a < KPW; ++a) {
@@ -358,24 +384,76 @@ __global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int k = 32 * kt + (q & 3) + 8 * (q >> 2) + 4 * h;
-      if (k > K) continue;
+      if (k >= K) continue;
       if (c0 + lr < N) gp[(size_t)k * N + c0 + lr] = acc[a][0][q];
       if (c0 + 32 + lr < N) gp[(size_t)k * N + c0 + 32 + lr] = acc[a][1][q];
     }
   }
+  // bias-gradient row K: the staging threads' per-(row slot, column) partials, summed over
+  // the 32 row slots in a fixed order
+#pragma unroll
+  for (int q = 0; q < PFY; ++q) {
+    const int i = tid + q * NT;
+    if (i < TILE * 8) {
+      const int rr = i % TILE, ch = i / TILE;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sdb[(8 * ch + e) * 33 + rr] = dsum[q][e];
+    }
+  }
+  __syncthreads();
+  if (tid < 64 && c0 + tid < N) {
+    float t = 0.f;
+    for (int r = 0; r < TILE; ++r) t += sdb[tid * 33 + r];
+    gp[(size_t)K * N + c0 + tid] = t;
+  }
 }
 
 // out[i] = sum_{c < chunks} gpart[c][i] (fixed order), i < count; the first k_rows * N
-// go to dW, the last N (the ones row) to db when db != nullptr
+// go to dW, the last N (the ones row) to db when db != nullptr.  32 consecutive
+// outputs per block, the chunks split over 8 lane groups (8 independent load streams
+// per output instead of one serial chain), then a fixed-order sum of the 8 partials.
 __global__ __launch_bounds__(256) void lin_reduce_kernel(const float* __restrict__ gpart, int chunks, long count,
                                                          int N, float* __restrict__ dW, float* __restrict__ db) {
+  __shared__ float s[8][33];
+  const int e = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const long i = (long)blockIdx.x * 32 + e;
+  float acc = 0.f;
+  if (i < count)
+    for (int c = grp; c < chunks; c += 8) acc += gpart[(size_t)c * count + i];
+  s[grp][e] = acc;
+  __syncthreads();
+  if (grp == 0 && i < count) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += s[q][e];
+    const long kw = count - N;
+    if (i < kw) dW[i] = t;
+    else if (db) db[i - kw] = t;
+  }
+}
+
+// bf16 LDS images of the weights, written once per step (the blocks of the main
+// kernels then copy them with 16-byte loads):
+//   fwd: img[slab][c][k]  = W[k][slab * ncols + c]   (W^T, row stride WS = KP + 8)
+//   bwd: img[slab][kk][c] = W[slab * kcols + kk][c]  (W rows, row stride WS = NP + 8)
+// zero outside the matrix and in the pad columns
+__global__ __launch_bounds__(256) void lin_prep_fwd_kernel(const float* __restrict__ W, int K, int N, int ncols,
+                                                           int KP, int WS, long total, uint16_t* __restrict__ img) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  float s = 0.f;
-  for (int c = 0; c < chunks; ++c) s += gpart[(size_t)c * count + i];
-  const long kw = count - N;
-  if (i < kw) dW[i] = s;
-  else if (db) db[i - kw] = s;
+  if (i >= total) return;
+  const int k = (int)(i % WS);
+  const long rc = i / WS;                       // slab * ncols + c = global column
+  const int c = (int)rc;
+  img[i] = bf16_bits(k < K && k < KP && c < N ? W[(size_t)k * N + c] : 0.f);
+}
+
+__global__ __launch_bounds__(256) void lin_prep_bwd_kernel(const float* __restrict__ W, int K, int N, int NP, int WS,
+                                                           long total, uint16_t* __restrict__ img) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % WS);
+  const int k = (int)(i / WS);                  // slab * kcols + kk = global row of W
+  img[i] = bf16_bits(k < K && c < N && c < NP ? W[(size_t)k * N + c] : 0.f);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -402,23 +480,29 @@ template <int KS>
 static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const float* W, int N,
                       const float* bias, uint16_t* Y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1,
                       uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
-                      hipStream_t st) {
+                      const int* idx1, uint16_t* wimg, hipStream_t st) {
   constexpr int KP = KS * 16;
   const int ncols = slab_cols(std::max(N, ldy), KP);
   const size_t lds = (size_t)ncols * (KP + 8) * 2 + (size_t)ncols * 4;
+  {
+    const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
+    const long total = (long)slabs * ncols * (KP + 8);
+    hipLaunchKernelGGL(lin_prep_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2, N,
+                       ncols, KP, KP + 8, total, wimg);
+  }
   constexpr int WV = FwdWaves<KS>::value;
   (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
   hipLaunchKernelGGL((lin_fwd_kernel<KS>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
                      x1, ld1, K1, x2, ld2, K2, W, N, bias, Y, ldy, n, ncols, relu, p, k0, k1, step, thr8, row0,
-                     stepp, rscale);
+                     stepp, rscale, idx1, wimg);
   return (int)hipGetLastError();
 }
 
 extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2, const float* W,
                                   int N, const float* bias, void* Y, int ldy, int n, int relu, float p, uint32_t k0,
                                   uint32_t k1, uint32_t step, uint32_t row0, const int* stepp, const float* rscale,
-                                  hipStream_t st) {
+                                  const int* idx1, void* wimg, hipStream_t st) {
   if (n <= 0) return 0;
   if ((x2 && K1 % 8) || ld1 % 8 || (x2 && (ld2 % 8)) || ldy % 8 || K1 > ld1 || (x2 && K2 > ld2) || N > ldy)
     return -3;
@@ -428,7 +512,7 @@ extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x
   auto a = (const uint16_t*)x1;
   auto b = (const uint16_t*)x2;
   auto y = (uint16_t*)Y;
-#define LF(c) if (ks == c) return fwd_launch<c>(a, ld1, K1, b, ld2, K2, W, N, bias, y, ldy, n, relu, p, k0, k1, step, thr8, row0, stepp, rscale, st);
+#define LF(c) if (ks == c) return fwd_launch<c>(a, ld1, K1, b, ld2, K2, W, N, bias, y, ldy, n, relu, p, k0, k1, step, thr8, row0, stepp, rscale, idx1, (uint16_t*)wimg, st);
   LF(4) LF(8) LF(16) LF(24) LF(32)
 #undef LF
   return -1;
@@ -437,23 +521,28 @@ extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x
 template <int KN>
 static int bwd_data_launch(const uint16_t* dY, int lddy, const uint16_t* Ym, int ldym, float mscale, int N,
                            const float* W, int K1, int K2, uint16_t* dX1, int ldx1, uint16_t* dX2, int ldx2,
-                           const float* rscale, int n, hipStream_t st) {
+                           const float* rscale, int n, int dx1_f32, uint16_t* wimg, hipStream_t st) {
   constexpr int NP = KN * 16;
   const int K = K1 + K2;
   const int kcols = slab_cols(K, NP);
   const size_t lds = (size_t)kcols * (NP + 8) * 2;
+  {
+    const long total = (long)((K + kcols - 1) / kcols) * kcols * (NP + 8);
+    hipLaunchKernelGGL(lin_prep_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K, N, NP,
+                       NP + 8, total, wimg);
+  }
   constexpr int WV = FwdWaves<KN>::value;
   (void)hipFuncSetAttribute((const void*)lin_bwd_data_kernel<KN>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const int slabs = (K + kcols - 1) / kcols;
   hipLaunchKernelGGL((lin_bwd_data_kernel<KN>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
-                     dY, lddy, Ym, ldym, mscale, N, W, K1, K2, dX1, ldx1, dX2, ldx2, rscale, n, kcols);
+                     dY, lddy, Ym, ldym, mscale, N, W, K1, K2, dX1, ldx1, dX2, ldx2, rscale, n, kcols, dx1_f32, wimg);
   return (int)hipGetLastError();
 }
 
 extern "C" int gnn_launch_lin_bwd_data(const void* dY, int lddy, const void* Ym, int ldym, float mscale, int N,
                                        const float* W, int K1, int K2, void* dX1, int ldx1, void* dX2, int ldx2,
-                                       const float* rscale, int n, hipStream_t st) {
+                                       const float* rscale, int n, int dx1_f32, void* wimg, hipStream_t st) {
   if (n <= 0) return 0;
   if (lddy % 8 || (Ym && ldym % 8) || (dX2 && K1 % 8) || ldx1 % 8 || (dX2 && ldx2 % 8) || N > lddy) return -3;
   if (!dX2) K2 = 0;
@@ -462,10 +551,26 @@ extern "C" int gnn_launch_lin_bwd_data(const void* dY, int lddy, const void* Ym,
   auto m = (const uint16_t*)Ym;
   auto o1 = (uint16_t*)dX1;
   auto o2 = (uint16_t*)dX2;
-#define LB(c) if (kn == c) return bwd_data_launch<c>(d, lddy, m, ldym, mscale, N, W, K1, K2, o1, ldx1, o2, ldx2, rscale, n, st);
+#define LB(c) if (kn == c) return bwd_data_launch<c>(d, lddy, m, ldym, mscale, N, W, K1, K2, o1, ldx1, o2, ldx2, rscale, n, dx1_f32, (uint16_t*)wimg, st);
   LB(4) LB(8) LB(16) LB(24) LB(32)
 #undef LB
   return -1;
+}
+
+// bytes of the weight images the launchers write (the caller provides the scratch)
+extern "C" long gnn_lin_fwd_image_bytes(int K, int N, int ldy) {
+  const int ks = pick_ks(K);
+  if (ks < 0) return -1;
+  const int KP = ks * 16, ncols = slab_cols(std::max(N, ldy), KP);
+  const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
+  return 2L * slabs * ncols * (KP + 8);
+}
+
+extern "C" long gnn_lin_bwd_image_bytes(int K, int N) {
+  const int kn = pick_ks(N);
+  if (kn < 0) return -1;
+  const int NP = kn * 16, kcols = slab_cols(K, NP);
+  return 2L * ((K + kcols - 1) / kcols) * kcols * (NP + 8);
 }
 
 // chunk count of the split-K weight gradient for n rows and N columns (fills the chip)
@@ -479,11 +584,11 @@ extern "C" int gnn_lin_wgrad_chunks(int n, int N) {
 template <int KT>
 static int wgt_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const uint16_t* dY,
                       int lddy, const uint16_t* Ym, int ldym, float mscale, int N, float* gpart, int n, int chunks,
-                      hipStream_t st) {
+                      const int* idx1, hipStream_t st) {
   const int tiles = (n + TILE - 1) / TILE;
   const int rpc = (tiles + chunks - 1) / chunks * TILE;
   hipLaunchKernelGGL((lin_bwd_weight_kernel<KT>), dim3(chunks, (N + 63) / 64), dim3(WGT_WAVES * 64), 0, st, x1, ld1,
-                     K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, rpc);
+                     K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, rpc, idx1);
   return (int)hipGetLastError();
 }
 
@@ -491,27 +596,27 @@ static int wgt_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
 // dW: [K1 + K2][N] fp32, db: [N] fp32 (optional)
 extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2,
                                          const void* dY, int lddy, const void* Ym, int ldym, float mscale, int N,
-                                         float* gpart, float* dW, float* db, int n, hipStream_t st) {
+                                         float* gpart, float* dW, float* db, int n, const int* idx1, hipStream_t st) {
   if ((x2 && K1 % 8) || ld1 % 8 || (x2 && ld2 % 8) || lddy % 8 || (Ym && ldym % 8) || N > lddy) return -3;
   if (!x2) K2 = 0;
   const int K = K1 + K2;
   const int chunks = gnn_lin_wgrad_chunks(std::max(n, 1), N);
   if (n > 0) {
-    const int kt = (K + 1 + 31) / 32;
+    const int kt = (K + 31) / 32;
     auto a = (const uint16_t*)x1;
     auto b = (const uint16_t*)x2;
     auto d = (const uint16_t*)dY;
     auto m = (const uint16_t*)Ym;
     int rc = -1;
-#define LW(c) if (rc == -1 && kt <= c) rc = wgt_launch<c>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, st);
-    LW(2) LW(4) LW(5) LW(8) LW(9) LW(12) LW(17)
+#define LW(c) if (rc == -1 && kt <= c) rc = wgt_launch<c>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, idx1, st);
+    LW(2) LW(4) LW(5) LW(8) LW(9) LW(12) LW(16) LW(17)
 #undef LW
     if (rc != 0) return rc;
   } else {
     (void)hipMemsetAsync(gpart, 0, sizeof(float) * (size_t)(K + 1) * N * chunks, st);
   }
   const long count = (long)(K + 1) * N;
-  hipLaunchKernelGGL(lin_reduce_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, gpart,
+  hipLaunchKernelGGL(lin_reduce_kernel, dim3((unsigned)((count + 31) / 32)), dim3(256), 0, st, gpart,
                      n > 0 ? chunks : 1, count, N, dW, db);
   return (int)hipGetLastError();
 }

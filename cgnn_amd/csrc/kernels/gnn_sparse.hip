@@ -205,9 +205,10 @@ __global__ __launch_bounds__(256, CGNN_SPMM_MINW) void spmm_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
     void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
     int n_rows, int F, int ldx, int ldy, int relu, int unit_col, int wcols,
-    const float* __restrict__ init, int ldi, const float* __restrict__ cscale) {
-  // init (optional, fp32 [n_rows][ldi]): partial sums of earlier edges (e.g. the
-  // rank-local part of a split aggregation), added before the row scale
+    const float* __restrict__ init, int ldi, const float* __restrict__ cscale, int init_rows) {
+  // init (optional, fp32 [init_rows][ldi]): partial sums of earlier edges (e.g. the
+  // rank-local part of a split aggregation, or GraphSAGE's self-path gradient of the
+  // destination rows, a prefix of the sources), added before the row scale
   // wcols: output columns this launch writes (from its base): the row stride ldy
   // for a whole-row launch, the slab width for a column-slab launch
   constexpr int RPW = 64 / L;
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(256, CGNN_SPMM_MINW) void spmm_kernel(
   const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
   gather_sum<L, XBF, U, CS>(col, X, e0, e1, ldx, f0, fv, sub * L, sl, acc, cscale);
   if (!rv || f0 >= wcols) return;
-  if (init && fv) {
+  if (init && fv && row < init_rows) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       if (f0 + q < F) acc[q] += init[(size_t)row * ldi + f0 + q];
@@ -473,10 +474,10 @@ static int spmm_unroll() {
 template <int L, int U>
 static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
-                         int relu, int uc, int wc, const float* init, int ldi, const float* cs, hipStream_t st) {
+                         int relu, int uc, int wc, const float* init, int ldi, const float* cs, int ir, hipStream_t st) {
   constexpr int RPB = 4 * (64 / L);   // rows per 256-thread block
   dim3 grid((n_rows + RPB - 1) / RPB), block(256);
-#define CGNN_SPMM(XT, YT, C) hipLaunchKernelGGL((spmm_kernel<L, XT, YT, U, C>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi, cs)
+#define CGNN_SPMM(XT, YT, C) hipLaunchKernelGGL((spmm_kernel<L, XT, YT, U, C>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi, cs, ir)
   // element-type codes: 0 fp32, 1 bf16, 2 fp16 (fp16 pairs with itself or with fp32);
   // a column scale is compiled for the same-type pairs only
   if (cs) {
@@ -499,34 +500,36 @@ static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, voi
 template <int L>
 static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
-                         int relu, int uc, int wc, const float* init, int ldi, const float* cs, hipStream_t st) {
+                         int relu, int uc, int wc, const float* init, int ldi, const float* cs, int ir,
+                         hipStream_t st) {
   if (spmm_unroll() == 8)
     return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
-                                 ldi, cs, st);
+                                 ldi, cs, ir, st);
   return spmm_dispatch_u<L, 4>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
-                               ldi, cs, st);
+                               ldi, cs, ir, st);
 }
 
 // one launch writing output columns [0, wcols) of its base (wcols <= 512)
 static int spmm_launch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                        const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf, int relu,
-                       int uc, int wc, const float* init, int ldi, const float* cs, hipStream_t st) {
+                       int uc, int wc, const float* init, int ldi, const float* cs, int ir, hipStream_t st) {
   const int w = std::max(F, wc);
-  if (w <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, st);
-  if (w <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, st);
-  if (w <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, st);
-  if (w <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, st);
+  if (w <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, st);
+  if (w <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, st);
+  if (w <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, st);
+  if (w <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, st);
   return -1;
 }
 
 extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X, void* Y,
                                const float* rscale, const float* bias, int n_rows, int F, int ldx,
                                int ldy, int xbf, int ybf, int relu, int unit_col, const float* init, int ldi,
-                               const float* cscale, hipStream_t st) {
+                               const float* cscale, int init_rows, hipStream_t st) {
   if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
+  if (init_rows < 0) init_rows = n_rows;
   if (ldy <= 512 && F <= 512)
     return spmm_launch(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, ldy, init,
-                       ldi, cscale, st);
+                       ldi, cscale, init_rows, st);
   // wide rows: column slabs of 512 output columns (16-byte aligned offsets), one
   // launch each; the last slabs also write the padding / ones columns up to ldy
   const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;   // bf16 and fp16 are both 2 bytes
@@ -536,7 +539,7 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
     const int rc = spmm_launch(rowptr, col, (const char*)X + (fc ? c0 * xs : 0), (char*)Y + c0 * ys, rscale,
                                bias && fc ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu,
                                unit_col >= 0 ? unit_col - c0 : -1, wc, init && fc ? init + c0 : nullptr, ldi,
-                               cscale, st);
+                               cscale, init_rows, st);
     if (rc) return rc;
   }
   return 0;

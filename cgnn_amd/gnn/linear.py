@@ -26,6 +26,19 @@ from .. import native
 from .ops import _st, _step_args, _step_value, dropout_keep_mask
 
 _GPART = {}
+_WIMG = {}
+
+
+def _wimg(dev, nbytes):
+    """Scratch for the bf16 LDS image of a weight (written by the launcher each call;
+    cached per device and size, so a captured hipGraph keeps its address)."""
+    if nbytes < 0:
+        raise RuntimeError("no HIP variant for this weight shape")
+    key = (dev.index, int(nbytes))
+    buf = _WIMG.get(key)
+    if buf is None:
+        buf = _WIMG[key] = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
+    return buf
 
 
 def _ptr(t):
@@ -49,11 +62,14 @@ def _cat(x1, K1, x2, K2):
 def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None,
             K1: Optional[int] = None, K2: Optional[int] = None, relu: bool = False, p: float = 0.0, key=(0, 0),
             step=0, row0: int = 0, rscale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-            ldy: Optional[int] = None) -> torch.Tensor:
+            ldy: Optional[int] = None, idx1: Optional[torch.Tensor] = None, n: Optional[int] = None) -> torch.Tensor:
     """``out[:, :N] = epi([x1[:, :K1] | x2[:, :K2]] @ W + bias)`` in bf16 (columns N..ldy zero).
 
-    ``W``: fp32 [K1 + K2, N]; ``step``: int or device int32[1] (read at launch time)."""
-    n = x1.shape[0]
+    ``W``: fp32 [K1 + K2, N]; ``step``: int or device int32[1] (read at launch time);
+    ``idx1`` (int32): row r reads ``x1[idx1[r]]`` (gather-on-load); ``n``: output rows
+    (default ``len(idx1)`` or the rows of x2 / x1)."""
+    if n is None:
+        n = idx1.shape[0] if idx1 is not None else (x2.shape[0] if x2 is not None else x1.shape[0])
     K1 = x1.shape[1] if K1 is None else int(K1)
     K2 = 0 if x2 is None else (x2.shape[1] if K2 is None else int(K2))
     N = W.shape[1]
@@ -64,12 +80,16 @@ def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = No
         out = torch.empty(n, ldy, dtype=torch.bfloat16, device=x1.device)
     if x1.is_cuda:
         sv, sp = _step_args(step)
-        rc = native.hip().gnn_lin_fwd(x1.data_ptr(), x1.stride(0), K1, _ptr(x2), x2.stride(0) if x2 is not None else 0,
+        hip = native.hip()
+        img = _wimg(x1.device, hip.gnn_lin_fwd_image_bytes(K1 + K2, N, out.stride(0)))
+        rc = hip.gnn_lin_fwd(x1.data_ptr(), x1.stride(0), K1, _ptr(x2), x2.stride(0) if x2 is not None else 0,
                                       K2, W.data_ptr(), N, _ptr(bias), out.data_ptr(), out.stride(0), n, int(relu),
-                                      float(p), int(key[0]), int(key[1]), sv, int(row0), sp, _ptr(rscale), _st(x1))
+                                      float(p), int(key[0]), int(key[1]), sv, int(row0), sp, _ptr(rscale), _st(x1),
+                                      idx1=_ptr(idx1), wimg=img.data_ptr())
         _check(rc, "lin_fwd")
         return out
-    y = _cat(x1, K1, x2, K2) @ _bf(W)
+    a = x1[idx1.long()] if idx1 is not None else x1[:n]
+    y = _cat(a, K1, None if x2 is None else x2[:n], K2) @ _bf(W)
     if bias is not None:
         y = y + bias.float()
     if relu:
@@ -79,8 +99,8 @@ def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = No
         y = torch.where(keep, y / (1 - p), torch.zeros_like(y))
     if rscale is not None:
         y = y * rscale[:, None].float()
-    out.zero_()
-    out[:, :N] = y.to(torch.bfloat16)
+    out[:n].zero_()
+    out[:n, :N] = y.to(torch.bfloat16)
     return out
 
 
@@ -94,24 +114,27 @@ def _masked(dY, N, Ym, mscale):
 def lin_bwd_data(dY: torch.Tensor, W: torch.Tensor, K1: int, K2: int = 0, Ym: Optional[torch.Tensor] = None,
                  mscale: float = 1.0, rscale: Optional[torch.Tensor] = None, out1: Optional[torch.Tensor] = None,
                  out2: Optional[torch.Tensor] = None):
-    """``[out1 | out2] = rscale * ((dY[:, :N] * m) @ W^T)``, ``m = [Ym > 0] * mscale``; bf16.
-    Returns (out1, out2) (out2 None when K2 == 0)."""
+    """``[out1 | out2] = rscale * ((dY[:, :N] * m) @ W^T)``, ``m = [Ym > 0] * mscale``; bf16
+    (``out1`` may be fp32).  Returns (out1, out2) (out2 None when K2 == 0)."""
     n, N = dY.shape[0], W.shape[1]
     if out1 is None:
         out1 = torch.empty(n, (K1 + 7) // 8 * 8, dtype=torch.bfloat16, device=dY.device)
     if K2 and out2 is None:
         out2 = torch.empty(n, (K2 + 7) // 8 * 8, dtype=torch.bfloat16, device=dY.device)
     if dY.is_cuda:
-        rc = native.hip().gnn_lin_bwd_data(dY.data_ptr(), dY.stride(0), _ptr(Ym), Ym.stride(0) if Ym is not None else 0,
+        hip = native.hip()
+        img = _wimg(dY.device, hip.gnn_lin_bwd_image_bytes(int(K1) + int(K2), N))
+        rc = hip.gnn_lin_bwd_data(dY.data_ptr(), dY.stride(0), _ptr(Ym), Ym.stride(0) if Ym is not None else 0,
                                            float(mscale), N, W.data_ptr(), int(K1), int(K2), out1.data_ptr(),
                                            out1.stride(0), _ptr(out2) if K2 else 0,
-                                           out2.stride(0) if K2 else 0, _ptr(rscale), n, _st(dY))
+                                           out2.stride(0) if K2 else 0, _ptr(rscale), n, _st(dY),
+                                           dx1_f32=int(out1.dtype == torch.float32), wimg=img.data_ptr())
         _check(rc, "lin_bwd_data")
         return out1, (out2 if K2 else None)
     d = _masked(dY, N, Ym, mscale) @ _bf(W).t()
     if rscale is not None:
         d = d * rscale[:, None].float()
-    out1[:, :K1] = d[:, :K1].to(torch.bfloat16)
+    out1[:n, :K1] = d[:, :K1].to(out1.dtype)
     if K2:
         out2[:, :K2] = d[:, K1:].to(torch.bfloat16)
     return out1, (out2 if K2 else None)
@@ -119,10 +142,13 @@ def lin_bwd_data(dY: torch.Tensor, W: torch.Tensor, K1: int, K2: int = 0, Ym: Op
 
 def lin_bwd_weight(x1: torch.Tensor, dY: torch.Tensor, N: int, x2: Optional[torch.Tensor] = None,
                    K1: Optional[int] = None, K2: Optional[int] = None, Ym: Optional[torch.Tensor] = None,
-                   mscale: float = 1.0, dW: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None):
+                   mscale: float = 1.0, dW: Optional[torch.Tensor] = None, db: Optional[torch.Tensor] = None,
+                   idx1: Optional[torch.Tensor] = None, n: Optional[int] = None):
     """``dW = [x1 | x2]^T (dY * m)`` (fp32 [K1 + K2, N]) and ``db = colsum(dY * m)`` (fp32 [N]);
-    split-K over row chunks, fixed-order reduction (deterministic)."""
-    n = x1.shape[0]
+    split-K over row chunks, fixed-order reduction (deterministic).  ``idx1`` / ``n`` as in
+    :func:`lin_fwd` (rows of dY by default)."""
+    if n is None:
+        n = dY.shape[0]
     K1 = x1.shape[1] if K1 is None else int(K1)
     K2 = 0 if x2 is None else (x2.shape[1] if K2 is None else int(K2))
     dev = x1.device
@@ -140,10 +166,12 @@ def lin_bwd_weight(x1: torch.Tensor, dY: torch.Tensor, N: int, x2: Optional[torc
             gp = _GPART[key] = torch.empty(shape, dtype=torch.float32, device=dev)
         rc = hip.gnn_lin_bwd_weight(x1.data_ptr(), x1.stride(0), K1, _ptr(x2), x2.stride(0) if x2 is not None else 0,
                                     K2, dY.data_ptr(), dY.stride(0), _ptr(Ym), Ym.stride(0) if Ym is not None else 0,
-                                    float(mscale), N, gp.data_ptr(), dW.data_ptr(), db.data_ptr(), n, _st(x1))
+                                    float(mscale), N, gp.data_ptr(), dW.data_ptr(), db.data_ptr(), n, _st(x1),
+                                    idx1=_ptr(idx1))
         _check(rc, "lin_bwd_weight")
         return dW, db
-    g = _masked(dY, N, Ym, mscale)
-    dW.copy_(_cat(x1, K1, x2, K2).t() @ g)
+    g = _masked(dY[:n], N, None if Ym is None else Ym[:n], mscale)
+    a = x1[idx1.long()] if idx1 is not None else x1[:n]
+    dW.copy_(_cat(a, K1, None if x2 is None else x2[:n], K2).t() @ g)
     db.copy_(g.sum(0))
     return dW, db

@@ -33,11 +33,12 @@ def dtype_code(dt) -> int:
 
 
 def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dtype=torch.bfloat16,
-         ld_out=None, unit_col=-1, init=None, cscale=None):
+         ld_out=None, unit_col=-1, init=None, cscale=None, init_rows=None):
     """Y[i,:F] = act(rscale[i] * (init[i] + sum_{j in N(i)} cscale[j] X[j,:F]) + bias); X is [*, ldx].
     Padding columns of Y are written 0, except ``unit_col`` which is written 1
     (a ones column that turns the bias gradient into one more GEMM row).
-    ``init`` (optional fp32 [n, >=F]): partial sums of other edges (split aggregation).
+    ``init`` (optional fp32 [init_rows, >=F], default all n rows): partial sums of other
+    edges (split aggregation) added to the first ``init_rows`` rows.
     ``cscale`` (optional fp32 per source row): a column scale applied in the gather."""
     n = rowptr.numel() - 1
     ldo = ld_out or X.shape[1]
@@ -50,8 +51,9 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
                      bias.data_ptr() if bias is not None else 0, n, F, X.shape[1], out.shape[1],
                      dtype_code(X.dtype), dtype_code(out.dtype), int(relu), int(unit_col),
                      _st(X), init.data_ptr() if init is not None else 0,
-                     init.shape[1] if init is not None else 0,
-                     cscale.data_ptr() if cscale is not None else 0)
+                     init.stride(0) if init is not None else 0,
+                     cscale.data_ptr() if cscale is not None else 0,
+                     -1 if init_rows is None else int(init_rows))
         return out
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, F, dtype=torch.float32)
@@ -60,7 +62,8 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
         src = src * cscale[col.long()][:, None]
     acc.index_add_(0, rows, src)
     if init is not None:
-        acc = acc + init[:n, :F].float()
+        r = n if init_rows is None else int(init_rows)
+        acc[:r] = acc[:r] + init[:r, :F].float()
     if rscale is not None:
         acc = acc * rscale[:, None]
     if bias is not None:

@@ -14,9 +14,21 @@ Two training modes:
 
 The aggregation is the same CSR gather-sum kernel as the GCN (``spmm_kernel``);
 its backward is the transposed block SpMM, for which the transposed CSR is built
-on the device with a stable sort -- deterministic, no atomics.  The two linear
-maps of a layer are one hipBLASLt GEMM on bf16 operands (fp32 accumulation) and
-the weight gradient runs split-K (``_SageLinear``).
+on the device with a stable sort -- deterministic, no atomics.
+
+``fused=True`` (default on a GPU; the CPU runs the same schedule through the ops'
+reference branches): a hand-scheduled step on the HIP kernels only.  A layer is
+``spmm`` (mean aggregate, bf16 out) + ``lin_fwd`` over the VIRTUAL concatenation
+``[h_dst | agg]`` with ``[W_self; W_neigh]`` stacked (bias, ReLU, Philox dropout in
+the epilogue; the first layer reads its ``h_dst`` rows straight out of the
+resident feature matrix through a row index, and its gather through the global
+column ids -- the batch's input features are never copied); the loss is the
+fused ``spmm_ce`` over a unit-diagonal CSR (softmax cross-entropy + gradient in
+one pass); the backward is ``lin_bwd_weight`` (split-K, mask-on-load) +
+``lin_bwd_data`` (``dh_dst`` in fp32 straight into the ``init`` of the
+transposed SpMM that scatters ``dagg``), then one RCCL all-reduce of the flat
+gradient buffer and the flat Adam kernel.  ``fused=False``: PyTorch autograd
+with hipBLASLt GEMMs (``_SageLinear``), the A/B baseline.
 """
 from __future__ import annotations
 
@@ -29,8 +41,10 @@ import numpy as np
 import torch
 
 from .. import native
+from ..utils.philox import model_key
 from . import ops
 from .data import GraphData
+from .linear import lin_bwd_data, lin_bwd_weight, lin_fwd
 
 
 def transpose_csr(rowptr: torch.Tensor, col: torch.Tensor, n_cols: int, with_perm: bool = False):
@@ -168,6 +182,130 @@ class SAGE(torch.nn.Module):
         return h
 
 
+class _FusedSAGE:
+    """Flat-parameter GraphSAGE on the HIP kernels (see the module docstring).
+    Parameters ``[W_0, b_0, ..., W_{L-1}, b_{L-1}]``, ``W_k = [W_self; W_neigh]``
+    initialised exactly like :class:`SAGE` (same generator sequence)."""
+
+    def __init__(self, x: torch.Tensor, n_features: int, hidden: int, n_classes: int, layers: int, dropout: float,
+                 lr: float, seed: int):
+        dev = x.device
+        self.dev, self.L, self.C, self.p, self.lr = dev, layers, n_classes, float(dropout), float(lr)
+        F = x.shape[1]
+        self.dims = [F] + [hidden] * (layers - 1) + [n_classes]
+        self.ld = [(d + 7) // 8 * 8 for d in self.dims]
+        self.x = x
+        g = torch.Generator().manual_seed(seed)
+        parts, self.offs = [], []
+        off = 0
+        for k, (a, b) in enumerate(zip(self.dims[:-1], self.dims[1:])):
+            bound = math.sqrt(6.0 / (a + b))
+            ws = (torch.rand(a, b, generator=g) * 2 - 1) * bound
+            wn = (torch.rand(a, b, generator=g) * 2 - 1) * bound
+            if k == 0:                       # padded feature rows stay 0 (as SAGETrainer does)
+                ws[n_features:] = 0
+                wn[n_features:] = 0
+            parts += [torch.cat([ws, wn], 0).reshape(-1), torch.zeros(b)]
+            self.offs.append((off, off + 2 * a * b, off + 2 * a * b + b))
+            off += 2 * a * b + b
+        self.params = torch.cat(parts).to(dev)
+        self.grads = torch.zeros_like(self.params)
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.W, self.b, self.gW, self.gb = [], [], [], []
+        for (o0, o1, o2), a, b in zip(self.offs, self.dims[:-1], self.dims[1:]):
+            self.W.append(self.params[o0:o1].view(2 * a, b))
+            self.b.append(self.params[o1:o2])
+            self.gW.append(self.grads[o0:o1].view(2 * a, b))
+            self.gb.append(self.grads[o1:o2])
+        self.keys = [model_key(seed, "sage-dropout", k) for k in range(layers)]
+        self.db_scratch = torch.zeros(n_classes, dtype=torch.float32, device=dev)
+        self._ident = None
+
+    def _identity(self, n):
+        """Unit-diagonal CSR, unit row scale, all-train mask of >= n rows (cached)."""
+        if self._ident is None or self._ident[0].numel() < n + 1:
+            m = max(n, 1024)
+            ar = torch.arange(m + 1, dtype=torch.int32, device=self.dev)
+            self._ident = (ar, ar[:m].clone(), torch.ones(m, dtype=torch.float32, device=self.dev),
+                           torch.ones(m, dtype=torch.uint8, device=self.dev))
+        rp, col, ones, tr = self._ident
+        return rp[:n + 1], col[:n], ones[:n], tr[:n]
+
+    def _step_arg(self):
+        return self.step_t if self.dev.type == "cuda" else int(self.step_t.item())
+
+    def forward(self, blocks, idx0: Optional[torch.Tensor], train: bool):
+        """Layers over ``blocks`` (input layer first); ``idx0`` (int32): global ids of the
+        first block's sources (None: the block's ids are global already).  Returns the
+        logits [n_dst_last, ldc] and the saved per-layer tensors."""
+        saved = []
+        h = self.x
+        step = self._step_arg()
+        for k, blk in enumerate(blocks):
+            F, nd = self.dims[k], blk.n_dst
+            last = k == self.L - 1
+            if k == 0 and idx0 is not None:
+                col = idx0[blk.col.long()]
+                x1, idx1 = self.x, idx0[:nd]
+            else:
+                col, x1, idx1 = blk.col, h, None
+            agg = ops.spmm(blk.rowptr, col, h, F, rscale=blk.inv_deg,
+                           out=torch.empty(nd, self.ld[k], dtype=torch.bfloat16, device=self.dev))
+            out = torch.empty(nd, self.ld[k + 1], dtype=torch.bfloat16, device=self.dev)
+            lin_fwd(x1, self.W[k], None if last else self.b[k], x2=agg, K1=F, K2=F, relu=not last,
+                    p=self.p if (train and not last) else 0.0, key=self.keys[k], step=step, idx1=idx1, n=nd, out=out)
+            saved.append((x1, idx1, agg, out, blk))
+            h = out
+        return h, saved
+
+    def loss_and_grad(self, logits, labels, inv_count, mask=None):
+        """Fused softmax cross-entropy (+ the last bias) over the rows with mask == 1 (all
+        rows by default): stats, dlogits."""
+        n = logits.shape[0]
+        rp, col, ones, tr = self._identity(n)
+        G = torch.empty_like(logits)
+        stats, G = ops.spmm_ce(rp, col, logits, self.C, ones, self.b[-1], labels, tr if mask is None else mask,
+                               inv_count, mode=0, G=G)
+        return stats, G
+
+    def backward(self, saved, G, stats):
+        dY = G
+        ms = 1.0 / (1.0 - self.p) if self.p > 0 else 1.0
+        for k in range(self.L - 1, -1, -1):
+            x1, idx1, agg, out, blk = saved[k]
+            F, N, nd = self.dims[k], self.dims[k + 1], blk.n_dst
+            last = k == self.L - 1
+            Ym, m = (None, 1.0) if last else (out, ms)
+            lin_bwd_weight(x1, dY, N, x2=agg, K1=F, K2=F, Ym=Ym, mscale=m, dW=self.gW[k],
+                           db=self.db_scratch if last else self.gb[k], idx1=idx1, n=nd)
+            if last:
+                self.gb[k].copy_(stats[4:4 + self.C])
+            if k == 0:
+                break
+            dhd = torch.empty(nd, self.ld[k], dtype=torch.float32, device=self.dev)
+            dagg = torch.empty(nd, self.ld[k], dtype=torch.bfloat16, device=self.dev)
+            lin_bwd_data(dY, self.W[k], F, F, Ym=Ym, mscale=m, out1=dhd, out2=dagg)
+            rp_t, col_t = blk.transposed()
+            dY = ops.spmm(rp_t, col_t, dagg, F, cscale=blk.inv_deg, init=dhd, init_rows=nd,
+                          out=torch.empty(blk.n_src, self.ld[k], dtype=torch.bfloat16, device=self.dev))
+
+    def step(self, blocks, idx0, labels, world: int = 1, mask=None, count=None):
+        """One optimisation step; returns the summed training loss (device scalar)."""
+        logits, saved = self.forward(blocks, idx0, train=True)
+        count = logits.shape[0] if count is None else count
+        stats, G = self.loss_and_grad(logits, labels, 1.0 / (count * world), mask)
+        self.backward(saved, G, stats)
+        if world > 1:
+            torch.distributed.all_reduce(self.grads)      # loss already scaled by 1/world: a SUM is the mean
+        ops.adam_(self.params, self.grads, self.m, self.v, self.lr, self.step_t)
+        return stats[0:1]
+
+    def state_tensors(self):
+        return {"params": self.params, "adam_m": self.m, "adam_v": self.v, "adam_step": self.step_t}
+
+
 def _pad8(x: torch.Tensor) -> torch.Tensor:
     F = x.shape[1]
     return x if F % 8 == 0 else torch.nn.functional.pad(x, (0, 8 - F % 8))
@@ -186,7 +324,7 @@ class SAGETrainer:
     def __init__(self, g: GraphData, hidden: int = 256, layers: int = 2, dropout: float = 0.5,
                  lr: float = 0.003, fanouts: Optional[List[int]] = (15, 10), batch_size: int = 1024,
                  seed: int = 0, prefetch: bool = True, standardize: bool = True, bucket_mb: float = 16.0,
-                 sampler: Optional[str] = None):
+                 sampler: Optional[str] = None, fused: Optional[bool] = None):
         from ..parallel import dist as pdist
         self.rank, self.world = pdist.rank(), pdist.world_size()
         self.g = g
@@ -199,6 +337,31 @@ class SAGETrainer:
             self.x = self.x.to(torch.bfloat16)
         self.C = g.n_classes
         F = self.x.shape[1]
+        self.fused = (self.dev.type == "cuda") if fused is None else bool(fused)
+        self.fanouts = list(fanouts) if fanouts else None
+        self.layers = layers
+        self.batch_size = int(batch_size)
+        self.seed = int(seed)
+        self.train_idx = torch.nonzero(g.mask.cpu() == 1).flatten().numpy()
+        self._rp64 = g.rowptr.cpu().numpy().astype(np.int64)
+        self._col = g.col.cpu().numpy()
+        self._full = None
+        self.prefetch = bool(prefetch)
+        self.sampler = sampler or ("device" if self.dev.type == "cuda" else "host")
+        self._dsampler = None
+        if self.fanouts and self.sampler == "device":
+            from .sampler import DeviceSampler
+            self._dsampler = DeviceSampler(g.rowptr, g.col, self.fanouts[:layers], seed)
+        self.epoch = 0
+        if self.fused:
+            if not self.x.dtype == torch.bfloat16:
+                self.x = self.x.to(torch.bfloat16)
+            self.y32 = g.y.to(torch.int32)
+            self._fused = _FusedSAGE(self.x, g.n_features, hidden, self.C, layers, dropout, lr, seed)
+            self.model, self.opt, self.ddp = None, None, None
+            if self.world > 1:       # identical initial parameters on every rank
+                torch.distributed.broadcast(self._fused.params, 0)
+            return
         # hidden width padded to a multiple of 8 (SpMM row alignment); output padded too
         self.model = SAGE(F, hidden, self.C, layers, dropout, seed).to(self.dev)
         self.model.w_self[0].data[g.n_features:] = 0
@@ -247,6 +410,9 @@ class SAGETrainer:
 
     # ----------------------------------------------------------- training
     def _step(self, blocks, nodes_in, seeds_t):
+        if self.fused:
+            loss = self._fused.step(blocks, nodes_in.to(torch.int32), self.y32[seeds_t.long()], self.world)
+            return loss[0] / max(int(seeds_t.numel()), 1)
         self.model.train()
         out = self.model(self.x[nodes_in], blocks)
         loss = torch.nn.functional.cross_entropy(out[:, :self.C], self.g.y[seeds_t].long())
@@ -275,6 +441,11 @@ class SAGETrainer:
         """One epoch; returns the mean training loss (one host sync at the end)."""
         if self.fanouts is None:
             blocks = self.full_blocks()
+            if self.fused:
+                n_tr = max(int((self.g.mask == 1).sum()), 1)
+                loss = self._fused.step(blocks, None, self.y32, self.world, mask=self.g.mask, count=n_tr)
+                self.epoch += 1
+                return float(loss) / n_tr
             self.model.train()
             out = self.model(self.x, blocks)
             tr = self.g.mask == 1
@@ -321,6 +492,15 @@ class SAGETrainer:
     @torch.no_grad()
     def evaluate(self):
         """Full-graph (layer-wise exact) inference; accuracies per split."""
+        if self.fused:
+            f = self._fused
+            logits, _ = f.forward(self.full_blocks(), None, train=False)
+            rp, col, ones, _ = f._identity(self.g.n)
+            stats, _ = ops.spmm_ce(rp, col, logits, self.C, ones, f.b[-1], self.y32, self.g.mask, 1.0, mode=1)
+            s = stats.cpu().numpy()
+            cnt = [max(int((self.g.mask == k).sum()), 1) for k in (1, 2, 3)]
+            return {"train_acc": float(s[1]) / cnt[0], "val_acc": float(s[2]) / cnt[1],
+                    "test_acc": float(s[3]) / cnt[2]}
         self.model.eval()
         out = self.model(self.x, self.full_blocks())[:, :self.C]
         pred = out.argmax(1)

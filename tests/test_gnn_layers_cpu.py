@@ -119,3 +119,47 @@ def test_linear_reference_ops_match_autograd():
     from cgnn_amd.gnn.ops import dropout_keep_mask
     keep = dropout_keep_mask(n, N, 0.5, (1, 2), 3)
     assert torch.equal(yd[:, :N].float() == 0, (~keep) | (y[:, :N].float() == 0))
+
+
+@pytest.mark.parametrize("layers", [2, 3])
+def test_fused_deep_gcn_matches_autograd_gcn(layers):
+    """The hand-scheduled fused epoch (manual backward through SpMM, lin_* and spmm_ce)
+    trains like the autograd GCN: same init, dropout off, bf16 storage vs fp32."""
+    from cgnn_amd.gnn.gcn_deep import DeepGCNTrainer
+    g = synthetic("ogbn-arxiv", seed=4, scale=0.004)
+    a = DeepGCNTrainer(g, hidden=64, layers=layers, dropout=0.0, lr=0.01, dtype=torch.float32, fused=False)
+    b = DeepGCNTrainer(g, hidden=64, layers=layers, dropout=0.0, lr=0.01, fused=True)
+    assert b.fused and not a.fused
+    ra0, rb0 = a.evaluate(), b.evaluate()
+    assert abs(ra0["train_loss"] - rb0["train_loss"]) < 0.02 * ra0["train_loss"], (ra0, rb0)
+    for _ in range(5):
+        a.train_step()
+        b.train_step()
+    ra, rb = a.evaluate(), b.evaluate()
+    assert rb["train_loss"] < rb0["train_loss"] - 0.05            # it learns
+    assert abs(ra["train_loss"] - rb["train_loss"]) < 0.03 * ra["train_loss"], (ra, rb)
+    # gradients of the first step agree layer by layer
+    a2 = DeepGCNTrainer(g, hidden=64, layers=layers, dropout=0.0, lr=0.01, dtype=torch.float32, fused=False)
+    b2 = DeepGCNTrainer(g, hidden=64, layers=layers, dropout=0.0, lr=0.01, fused=True)
+    a2.model.train()
+    from cgnn_amd.gnn.gcn_deep import cross_entropy
+    out = a2.model(a2.x, a2.ng)
+    cross_entropy(out[a2.idx["train"]], a2.y_train).backward()
+    f = b2._fused
+    f.backward(f.forward(train=True))
+    def rel(a, b):
+        return float((a - b).norm() / b.norm())
+    for l, conv in enumerate(a2.model.convs):
+        gw_ref = conv.weight.grad[:f.dims[l]]
+        assert rel(f.gW[l], gw_ref) < 0.02, (l, rel(f.gW[l], gw_ref))     # bf16 activations vs fp32
+        assert rel(f.gb[l], conv.bias.grad) < 0.02, (l, rel(f.gb[l], conv.bias.grad))
+
+
+def test_fused_deep_gcn_dropout_trains_on_cpu():
+    from cgnn_amd.gnn.gcn_deep import DeepGCNTrainer
+    g = synthetic("ogbn-arxiv", seed=5, scale=0.004)
+    t = DeepGCNTrainer(g, hidden=64, layers=3, dropout=0.5, lr=0.01, fused=True)
+    r0 = t.evaluate()
+    for _ in range(8):
+        t.train_step()
+    assert t.evaluate()["train_loss"] < r0["train_loss"]

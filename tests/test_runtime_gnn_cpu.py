@@ -272,3 +272,27 @@ def test_gat_learns_cpu():
         last = float(tr.train_step())
     res = tr.evaluate()
     assert last < first and res["val_acc"] > 0.3, (first, last, res)
+
+
+@pytest.mark.parametrize("fanouts", [(5, 5), None])
+def test_fused_sage_matches_autograd_sage_cpu(fanouts):
+    """The fused SAGE schedule (ops' CPU reference branches) computes the same step as the
+    autograd model: same init, dropout off, same sampled blocks; then it learns."""
+    from cgnn_amd.gnn.sage import SAGETrainer
+    g = synthetic("ogbn-arxiv", seed=2, scale=0.01, feat_noise=2.0, label_noise=0.1)
+    kw = dict(hidden=64, fanouts=fanouts, batch_size=256, lr=0.01, dropout=0.0, prefetch=False)
+    a = SAGETrainer(g, fused=False, **kw)
+    b = SAGETrainer(g, fused=True, **kw)
+    assert b.fused and not a.fused
+    # identical initial parameters
+    f = b._fused
+    for k in range(2):
+        ref = torch.cat([a.model.w_self[k].detach(), a.model.w_neigh[k].detach()], 0)
+        assert torch.equal(f.W[k], ref)
+    la, lb = a.train_epoch(), b.train_epoch()
+    assert lb == pytest.approx(la, rel=0.03), (la, lb)
+    for _ in range(8):
+        lb_last = b.train_epoch()
+    assert lb_last < lb
+    ra, rb = a.evaluate(), b.evaluate()
+    assert rb["val_acc"] > 0.3, rb

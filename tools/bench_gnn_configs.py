@@ -62,10 +62,19 @@ def main():
     ap.add_argument("--hidden", type=int, default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-capture", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--reorder", choices=["lp-cm", "none"], default="lp-cm",
+                    help="framework locality pass on the (shuffled-id) synthetic graph, timed in setup")
+    ap.add_argument("--unfused", action="store_true", help="arxiv-gcn3 / products-sage3: autograd + hipBLASLt path (A/B)")
     a = ap.parse_args()
 
-    from cgnn_amd.gnn.data import SHAPES, synthetic
+    from cgnn_amd.gnn.data import SHAPES, reorder, synthetic
     from cgnn_amd.parallel import dist as pdist
+
+    def _graph(name):
+        g = synthetic(name, seed=a.seed, device=dev, scale=a.scale)
+        if a.reorder != "none":
+            g, _ = reorder(g, seed=a.seed)
+        return g
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     cpu = a.config == "cora-cpu" or not torch.cuda.is_available()
@@ -86,10 +95,10 @@ def main():
         name, layers = ("cora", 2) if a.config == "cora-cpu" else ("ogbn-arxiv", 3)
         hidden = a.hidden or (16 if name == "cora" else 256)
         steps, warmup = a.steps or (100 if cpu else 200), a.warmup or 10
-        g = synthetic(name, seed=a.seed, device=dev, scale=a.scale)
+        g = _graph(name)
         dtype = torch.float32 if cpu else torch.bfloat16
         tr = DeepGCNTrainer(g, hidden=hidden, layers=layers, dropout=0.5, lr=0.01, dtype=dtype, seed=a.seed,
-                            capture=capture)
+                            capture=capture, fused=False if a.unfused else None)
         setup = time.perf_counter() - t_setup
         dt = _timed(tr.train_step, steps, warmup, dev)
         ev = tr.evaluate()
@@ -97,6 +106,7 @@ def main():
                    value=round(steps / dt, 3), unit="epochs/s", ms_per_step=round(1e3 * dt / steps, 4),
                    val_acc=round(ev["val_acc"], 4), test_acc=round(ev["test_acc"], 4),
                    dtype=str(dtype).replace("torch.", ""), hipgraph=bool(tr._step_graph.graph is not None),
+                   fused=bool(tr.fused),
                    config={"model": "GCN-%dlayer-hidden%d" % (layers, hidden), "dataset": name, "nodes": g.n,
                            "nnz_with_self_loops": g.nnz})
     elif a.config == "reddit-infer":
@@ -104,7 +114,7 @@ def main():
         from cgnn_amd.gnn.layers import GCN
         hidden = a.hidden or 256
         steps, warmup = a.steps or 100, a.warmup or 5
-        g = synthetic("reddit", seed=a.seed, device=dev, scale=a.scale)
+        g = _graph("reddit")
         model = GCN([g.n_features, hidden, g.n_classes], seed=a.seed).to(dev).eval()
         inf = GCNInference.from_model(g, model, dtype=torch.float16, capture=capture)
         setup = time.perf_counter() - t_setup
@@ -138,9 +148,9 @@ def main():
         from cgnn_amd.gnn.sage import SAGETrainer
         hidden = a.hidden or 256
         steps, warmup = a.steps or 2, a.warmup or 1
-        g = synthetic("ogbn-products", seed=a.seed, device=dev, scale=a.scale)
+        g = _graph("ogbn-products")
         tr = SAGETrainer(g, hidden=hidden, layers=3, dropout=0.5, lr=0.003, fanouts=(15, 10, 5),
-                         batch_size=1024, seed=a.seed)
+                         batch_size=1024, seed=a.seed, fused=False if a.unfused else None)
         setup = time.perf_counter() - t_setup
         per_epoch = len(tr._batches())
         dt = _timed(tr.train_epoch, steps, warmup, dev)
@@ -148,7 +158,7 @@ def main():
         seeds = len(tr.train_idx) * steps
         res.update(metric="epochs/sec + val-acc, 3-layer GraphSAGE ogbn-products mini-batch DP",
                    value=round(steps / dt, 4), unit="epochs/s", ms_per_step=round(1e3 * dt / steps, 3),
-                   seeds_per_s=round(seeds / dt, 1), iterations_per_epoch=per_epoch,
+                   seeds_per_s=round(seeds / dt, 1), iterations_per_epoch=per_epoch, fused=bool(tr.fused),
                    val_acc=round(ev["val_acc"], 4), test_acc=round(ev["test_acc"], 4),
                    dtype="bf16 (fp32 accumulation, fp32 master weights)" if dev.type == "cuda" else "fp32",
                    scaling="strong (fixed global epoch; per-rank batch 1024)",
@@ -171,7 +181,7 @@ def main():
                    config={"model": "GAT-2layer-4x32", "parallelism": "graph-rowpart%d" % world, "nodes": n_nodes,
                            "nnz_with_self_loops": nnz})
     res.update(steps=steps, warmup=warmup, setup_s=round(setup, 2), data="synthetic graph of the named shape "
-               "(planted communities), random-init weights")
+               "(planted communities, shuffled ids), random-init weights", reordered=a.reorder != "none")
     res.setdefault("higher_is_better", True)
     if rank == 0:
         print(json.dumps(res), flush=True)

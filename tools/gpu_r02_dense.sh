@@ -1,0 +1,11 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r02_dense
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gnn_linear_gpu.py tests/test_gnn_gpu.py -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+timeout -k 10 200 python tools/bench_gnn_configs.py --config arxiv-gcn3 > $O/arxiv_fused.log 2>&1 || exit 1
+timeout -k 10 300 python tools/bench_gnn_configs.py --config products-sage3 > $O/sage_fused.log 2>&1 || exit 1
+timeout -k 10 300 python tools/bench_gnn_configs.py --config products-sage3 --unfused > $O/sage_unfused.log 2>&1 || exit 1
+timeout -s KILL 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/arxiv_trace -o run -- python3 tools/bench_gnn_configs.py --config arxiv-gcn3 --no-capture --steps 50 > $O/arxiv_trace.log 2>&1 || exit 1
+timeout -s KILL 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sage_trace -o run -- python3 tools/bench_gnn_configs.py --config products-sage3 --steps 1 --warmup 1 > $O/sage_trace.log 2>&1 || exit 1
+echo done
