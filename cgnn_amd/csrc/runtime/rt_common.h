@@ -41,6 +41,19 @@ struct IdPermutation {
     do { v = once(v); } while (v >= n);
     return v;
   }
+  uint64_t inverse_once(uint64_t v) const {
+    uint64_t L = v >> half, R = v & mask;
+    for (int r = 3; r >= 0; --r) {
+      const uint64_t t = R ^ (mix64(L ^ key[r]) & mask);
+      R = L;
+      L = t;
+    }
+    return (L << half) | R;
+  }
+  uint64_t inverse(uint64_t v) const {
+    do { v = inverse_once(v); } while (v >= n);
+    return v;
+  }
 };
 
 }  // namespace cgnn_rt

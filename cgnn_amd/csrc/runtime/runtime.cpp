@@ -27,6 +27,7 @@
 #include <random>
 #include <unordered_map>
 #include <cmath>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -209,68 +210,55 @@ py::tuple csr_from_edges(i64 n, py::array_t<i64, py::array::c_style | py::array:
 //   id_order 1 ("shuffled") relabels every node through a seeded bijection of
 //   [0, n) (IdPermutation), so ids carry no information and any locality must be
 //   earned by a reordering pass (reorder.cpp).
-py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophily,
-                          double feat_noise, uint64_t seed, double label_noise, int id_order) {
-  py::array_t<i64> src_a(m), dst_a(m);
-  py::array_t<i32> label_a(n);
-  i64* src = src_a.mutable_data();
-  i64* dst = dst_a.mutable_data();
-  i32* lab = label_a.mutable_data();
-  const cgnn_rt::IdPermutation perm(n, seed ^ 0x5A17ull);
-  auto pid = [&](i64 v) -> i64 { return id_order ? (i64)perm((uint64_t)v) : v; };
-  // contiguous communities: class blocks of roughly equal size
-  const i64 block = (n + n_class - 1) / n_class;
-  std::vector<i32> comm(n);
-  for (i64 v = 0; v < n; ++v) comm[v] = (i32)std::min<i64>(v / block, n_class - 1);
-  // node label = its community's class, except a `label_noise` fraction drawn uniformly
-  std::vector<i32> lab0(n);
-#pragma omp parallel for schedule(static)
-  for (i64 v = 0; v < n; ++v) {
+//   Every quantity is a pure function of (seed, edge index) or (seed, node id), so
+//   any row range of the graph can be generated on its own (synthetic_shard).
+namespace {
+
+struct SynthSpec {
+  int64_t n, m;
+  int n_feat, n_class;
+  double homophily, feat_noise, label_noise;
+  uint64_t seed;
+  int id_order;
+  int64_t block;
+  double mean_deg;
+  cgnn_rt::IdPermutation perm;
+  SynthSpec(int64_t n_, int64_t m_, int nf, int nc, double hom, double fn, uint64_t sd, double ln, int io)
+      : n(n_), m(m_), n_feat(nf), n_class(nc), homophily(hom), feat_noise(fn), label_noise(ln), seed(sd),
+        id_order(io), block((n_ + nc - 1) / nc), mean_deg((double)m_ / (double)n_), perm(n_, sd ^ 0x5A17ull) {}
+  int64_t pid(int64_t v) const { return id_order ? (int64_t)perm((uint64_t)v) : v; }
+  int64_t gen_id(int64_t v) const { return id_order ? (int64_t)perm.inverse((uint64_t)v) : v; }
+  int32_t comm(int64_t v) const { return (int32_t)std::min<int64_t>(v / block, n_class - 1); }
+  int32_t label(int64_t v) const {                    // v in generator space
     const uint64_t h = mix64(seed ^ 0x1AB3ull ^ mix64((uint64_t)v));
     const double u = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-    lab0[v] = u < label_noise ? (i32)(mix64(h) % (uint64_t)n_class) : comm[v];
-    lab[pid(v)] = lab0[v];
+    return u < label_noise ? (int32_t)(mix64(h) % (uint64_t)n_class) : comm(v);
   }
-  const double mean_deg = (double)m / (double)n;   // edges per source node
-#pragma omp parallel for schedule(static)
-  for (i64 e = 0; e < m; ++e) {
+  // edge e in generator space
+  void edge(int64_t e, int64_t& s, int64_t& t) const {
     uint64_t h = mix64(seed ^ mix64((uint64_t)e * 0x9E3779B97F4A7C15ull));
-    // source: power-law-ish popularity (inverse CDF of a Pareto-like law)
     const double u = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
     h = mix64(h);
-    i64 s = (i64)((double)n * std::pow(u, 1.6)) % n;   // skew towards low ids ...
-    s = (i64)(mix64(s ^ seed) % (uint64_t)n);           // ... then scatter the hubs
+    s = (int64_t)((double)n * std::pow(u, 1.6)) % n;   // skew towards low ids ...
+    s = (int64_t)(mix64(s ^ seed) % (uint64_t)n);       // ... then scatter the hubs
     const double u2 = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
     h = mix64(h);
-    i64 t;
     if (u2 < homophily) {
-      const i64 c = comm[s];
-      const i64 lo = c * block, hi = std::min<i64>(n, lo + block);
-      const i64 win = std::max<i64>(16, (i64)(8 * mean_deg));
-      const i64 off = (i64)(h % (uint64_t)(2 * win + 1)) - win;
+      const int64_t c = comm(s);
+      const int64_t lo = c * block, hi = std::min<int64_t>(n, lo + block);
+      const int64_t win = std::max<int64_t>(16, (int64_t)(8 * mean_deg));
+      const int64_t off = (int64_t)(h % (uint64_t)(2 * win + 1)) - win;
       t = s + off;
       if (t < lo) t += (hi - lo);
       if (t >= hi) t -= (hi - lo);
-      if (t < lo || t >= hi) t = lo + (i64)(h % (uint64_t)(hi - lo));
+      if (t < lo || t >= hi) t = lo + (int64_t)(h % (uint64_t)(hi - lo));
     } else {
-      t = (i64)(h % (uint64_t)n);
+      t = (int64_t)(h % (uint64_t)n);
     }
-    src[e] = pid(s);
-    dst[e] = pid(t);
   }
-  py::array_t<float> feat_a({(py::ssize_t)n, (py::ssize_t)n_feat});
-  float* x = feat_a.mutable_data();
-  // class centroids
-  std::vector<float> cent((size_t)n_class * n_feat);
-  {
-    std::mt19937_64 g(seed ^ 0xC0FFEEull);
-    std::normal_distribution<float> nd(0.f, 1.f);
-    for (auto& c : cent) c = nd(g);
-  }
-#pragma omp parallel for schedule(static)
-  for (i64 v = 0; v < n; ++v) {
+  void features(int64_t v, const std::vector<float>& cent, float* xr) const {   // v in generator space
+    const int32_t lab = label(v);
     uint64_t h = mix64(seed ^ 0xFEEDull ^ mix64((uint64_t)v));
-    float* xr = x + (size_t)pid(v) * n_feat;
     for (int f = 0; f < n_feat; f += 2) {
       h = mix64(h);
       const double u1 = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
@@ -278,12 +266,145 @@ py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophil
       const double u2 = ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
       const double r = std::sqrt(-2.0 * std::log(u1));
       const double z0 = r * std::cos(6.283185307179586 * u2), z1 = r * std::sin(6.283185307179586 * u2);
-      xr[f] = (float)(cent[(size_t)lab0[v] * n_feat + f] + feat_noise * z0);
-      if (f + 1 < n_feat)
-        xr[f + 1] = (float)(cent[(size_t)lab0[v] * n_feat + f + 1] + feat_noise * z1);
+      xr[f] = (float)(cent[(size_t)lab * n_feat + f] + feat_noise * z0);
+      if (f + 1 < n_feat) xr[f + 1] = (float)(cent[(size_t)lab * n_feat + f + 1] + feat_noise * z1);
+    }
+  }
+  std::vector<float> centroids() const {
+    std::vector<float> cent((size_t)n_class * n_feat);
+    std::mt19937_64 g(seed ^ 0xC0FFEEull);
+    std::normal_distribution<float> nd(0.f, 1.f);
+    for (auto& c : cent) c = nd(g);
+    return cent;
+  }
+};
+
+}  // namespace
+
+py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophily,
+                          double feat_noise, uint64_t seed, double label_noise, int id_order) {
+  const SynthSpec sp(n, m, n_feat, n_class, homophily, feat_noise, seed, label_noise, id_order);
+  py::array_t<i64> src_a(m), dst_a(m);
+  py::array_t<i32> label_a(n);
+  i64* src = src_a.mutable_data();
+  i64* dst = dst_a.mutable_data();
+  i32* lab = label_a.mutable_data();
+  py::array_t<float> feat_a({(py::ssize_t)n, (py::ssize_t)n_feat});
+  float* x = feat_a.mutable_data();
+  {
+    py::gil_scoped_release nogil;
+#pragma omp parallel for schedule(static)
+    for (i64 e = 0; e < m; ++e) {
+      i64 s, t;
+      sp.edge(e, s, t);
+      src[e] = sp.pid(s);
+      dst[e] = sp.pid(t);
+    }
+    const std::vector<float> cent = sp.centroids();
+#pragma omp parallel for schedule(static)
+    for (i64 v = 0; v < n; ++v) {
+      const i64 pv = sp.pid(v);
+      lab[pv] = sp.label(v);
+      sp.features(v, cent, x + (size_t)pv * n_feat);
     }
   }
   return py::make_tuple(src_a, dst_a, feat_a, label_a);
+}
+
+// Rows [r0, r1) (final ids) of the same graph as synthetic_graph + csr_from_edges(n,
+// src, dst, symmetric, self loops, dedup): CSR with GLOBAL column ids, the rows'
+// features and labels -- generated without materialising the rest of the graph
+// (every rank of a graph-sharded job scans the edge hash space and keeps the edges
+// touching its rows: O(m) hashing, O(local nnz) memory).  rowptr is int64 (a shard
+// of a 10^9-edge graph may pass 2^31 entries), columns int32 (n < 2^31).
+py::tuple synthetic_shard(i64 n, i64 m, int n_feat, int n_class, double homophily, double feat_noise,
+                          uint64_t seed, double label_noise, int id_order, i64 r0, i64 r1) {
+  if (r0 < 0 || r1 > n || r0 > r1) throw std::invalid_argument("synthetic_shard: bad row range");
+  if (n >= (i64)1 << 31) throw std::invalid_argument("synthetic_shard: n >= 2^31 needs int64 columns");
+  const SynthSpec sp(n, m, n_feat, n_class, homophily, feat_noise, seed, label_noise, id_order);
+  const i64 nl = r1 - r0;
+  py::array_t<i64> rp_a(nl + 1);
+  i64* rp = rp_a.mutable_data();
+  py::array_t<float> feat_a({(py::ssize_t)nl, (py::ssize_t)n_feat});
+  py::array_t<i32> label_a(nl);
+  std::vector<i32> col;
+  {
+    py::gil_scoped_release nogil;
+    std::vector<i64> cnt(nl + 1, 0);
+    // pass 1: degree of every local row (both directions of every edge, self loops apart)
+#pragma omp parallel for schedule(static)
+    for (i64 e = 0; e < m; ++e) {
+      i64 s, t;
+      sp.edge(e, s, t);
+      const i64 ps = sp.pid(s), pt = sp.pid(t);
+      if (ps == pt) continue;
+      if (ps >= r0 && ps < r1) __atomic_fetch_add(&cnt[ps - r0 + 1], 1, __ATOMIC_RELAXED);
+      if (pt >= r0 && pt < r1) __atomic_fetch_add(&cnt[pt - r0 + 1], 1, __ATOMIC_RELAXED);
+    }
+    for (i64 v = 0; v < nl; ++v) cnt[v + 1] += cnt[v] + 1;    // + the self loop
+    std::vector<i64> cur(cnt.begin(), cnt.end() - 1);
+    col.resize(cnt[nl]);
+    for (i64 v = 0; v < nl; ++v) col[cur[v]++] = (i32)(r0 + v);
+    // pass 2: fill (order inside a row is fixed by the sort below)
+#pragma omp parallel for schedule(static)
+    for (i64 e = 0; e < m; ++e) {
+      i64 s, t;
+      sp.edge(e, s, t);
+      const i64 ps = sp.pid(s), pt = sp.pid(t);
+      if (ps == pt) continue;
+      if (ps >= r0 && ps < r1) col[__atomic_fetch_add(&cur[ps - r0], 1, __ATOMIC_RELAXED)] = (i32)pt;
+      if (pt >= r0 && pt < r1) col[__atomic_fetch_add(&cur[pt - r0], 1, __ATOMIC_RELAXED)] = (i32)ps;
+    }
+    // sort + de-duplicate every row, then compact
+    std::vector<i64> keep(nl + 1, 0);
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (i64 v = 0; v < nl; ++v) {
+      auto b = col.begin() + cnt[v], e = col.begin() + cnt[v + 1];
+      std::sort(b, e);
+      keep[v + 1] = std::unique(b, e) - b;
+    }
+    rp[0] = 0;
+    for (i64 v = 0; v < nl; ++v) rp[v + 1] = rp[v] + keep[v + 1];
+    i64 w = 0;
+    for (i64 v = 0; v < nl; ++v) {            // in place: rows only move left
+      const i64 b = cnt[v], k = keep[v + 1];
+      if (w != b) std::memmove(col.data() + w, col.data() + b, sizeof(i32) * (size_t)k);
+      w += k;
+    }
+    col.resize(w);
+    col.shrink_to_fit();
+    const std::vector<float> cent = sp.centroids();
+    float* x = feat_a.mutable_data();
+    i32* lab = label_a.mutable_data();
+#pragma omp parallel for schedule(static)
+    for (i64 v = 0; v < nl; ++v) {
+      const i64 gv = sp.gen_id(r0 + v);
+      lab[v] = sp.label(gv);
+      sp.features(gv, cent, x + (size_t)v * n_feat);
+    }
+  }
+  py::array_t<i32> col_a((py::ssize_t)col.size());
+  std::copy(col.begin(), col.end(), col_a.mutable_data());
+  return py::make_tuple(rp_a, col_a, feat_a, label_a);
+}
+
+// Train / valid / test split by a per-node hash: node v is train with probability
+// n_train / n, valid with n_val / n, else test (1 / 2 / 3) -- a pure function of
+// (seed, v), so every rank labels its own rows consistently without a global
+// permutation of 10^8 ids.
+py::array_t<uint8_t> split_mask(i64 n, i64 n_train, i64 n_val, uint64_t seed,
+                                py::array_t<i64, py::array::c_style | py::array::forcecast> ids) {
+  py::array_t<uint8_t> out(ids.size());
+  const i64* id = ids.data();
+  uint8_t* o = out.mutable_data();
+  const double pt = (double)n_train / (double)n, pv = (double)(n_train + n_val) / (double)n;
+  const i64 k = ids.size();
+#pragma omp parallel for schedule(static)
+  for (i64 i = 0; i < k; ++i) {
+    const double u = ((mix64(mix64(seed ^ 0x5B117ull) ^ (uint64_t)id[i]) >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+    o[i] = u < pt ? 1 : (u < pv ? 2 : 3);
+  }
+  return out;
 }
 
 // Layer-wise uniform neighbour sampling (GraphSAGE).  For each layer (outermost
@@ -379,15 +500,21 @@ PYBIND11_MODULE(_rt, m) {
   m.def("synthetic_graph", &synthetic_graph, py::arg("n"), py::arg("m"), py::arg("n_feat"),
         py::arg("n_class"), py::arg("homophily") = 0.8, py::arg("feat_noise") = 1.0,
         py::arg("seed") = 0, py::arg("label_noise") = 0.0, py::arg("id_order") = 0);
+  m.def("synthetic_shard", &synthetic_shard, py::arg("n"), py::arg("m"), py::arg("n_feat"), py::arg("n_class"),
+        py::arg("homophily"), py::arg("feat_noise"), py::arg("seed"), py::arg("label_noise"), py::arg("id_order"),
+        py::arg("r0"), py::arg("r1"));
+  m.def("split_mask", &split_mask, py::arg("n"), py::arg("n_train"), py::arg("n_val"), py::arg("seed"),
+        py::arg("ids"));
   m.def("sample_neighbors", &sample_neighbors);
   m.def("num_threads", []() { return omp_get_max_threads(); });
-  m.def("id_permutation", [](i64 n, uint64_t seed, py::array_t<i64, py::array::c_style | py::array::forcecast> v) {
+  m.def("id_permutation", [](i64 n, uint64_t seed, py::array_t<i64, py::array::c_style | py::array::forcecast> v,
+                             bool inverse) {
     const cgnn_rt::IdPermutation p(n, seed);
     py::array_t<i64> out(v.size());
     const i64* a = v.data();
     i64* o = out.mutable_data();
-    for (py::ssize_t i = 0; i < v.size(); ++i) o[i] = (i64)p((uint64_t)a[i]);
+    for (py::ssize_t i = 0; i < v.size(); ++i) o[i] = (i64)(inverse ? p.inverse((uint64_t)a[i]) : p((uint64_t)a[i]));
     return out;
-  }, py::arg("n"), py::arg("seed"), py::arg("ids"));
+  }, py::arg("n"), py::arg("seed"), py::arg("ids"), py::arg("inverse") = false);
   register_reorder(m);
 }

@@ -115,11 +115,9 @@ def synthetic(name: str = "ogbn-products", seed: int = 0, device=None, scale: fl
     device = rowptr.device
     deg = (rowptr[1:] - rowptr[:-1]).to(torch.float32)
     dinv = deg.clamp_min(1).rsqrt()
-    # split: a seeded permutation (train / valid / rest test), like OGB's fixed split sizes
-    perm = np.random.default_rng(seed + 1).permutation(n)
-    mask = np.full(n, 3, dtype=np.uint8)
-    mask[perm[:n_train]] = 1
-    mask[perm[n_train:n_train + n_val]] = 2
+    # split: train / valid / test by a per-node hash with OGB's split proportions (a pure
+    # function of the node id, so a graph shard labels its rows without the full graph)
+    mask = np.asarray(native.rt().split_mask(n, n_train, n_val, seed + 1, np.arange(n, dtype=np.int64)))
     return GraphData(n=n, rowptr=rowptr, col=col, dinv=dinv.to(device),
                      x=torch.from_numpy(np.asarray(x)).to(device),
                      y=torch.from_numpy(np.asarray(y).astype(np.int32)).to(device),
@@ -135,6 +133,66 @@ def partition_rows(g: GraphData, rank: int, world: int):
     col = g.col[int(rp[0]): int(rp[-1])]
     rp = (rp - rp[0]).to(torch.int32)
     return r0, r1, per, rp, col
+
+
+@dataclasses.dataclass
+class GraphShard:
+    """Rows [r0, r1) of an n-node graph (A + I, symmetric): CSR with GLOBAL column ids,
+    the rows' features / labels / split.  Built by :func:`synthetic_shard` without the
+    rest of the graph.  ``rowptr`` is int32 when the shard's nnz fits, else int64."""
+    n: int
+    r0: int
+    r1: int
+    rowptr: torch.Tensor
+    col: torch.Tensor
+    x: torch.Tensor
+    y: torch.Tensor
+    mask: torch.Tensor
+    n_classes: int
+    n_train_global: int = 0
+    name: str = "synthetic-shard"
+
+    @property
+    def n_local(self):
+        return self.r1 - self.r0
+
+    @property
+    def nnz(self):
+        return int(self.col.numel())
+
+
+def shard_rows(n: int, rank: int, world: int):
+    """Row block of ``rank``: contiguous, equal sizes (the last one shorter)."""
+    per = (n + world - 1) // world
+    return rank * per, min(n, (rank + 1) * per), per
+
+
+def synthetic_shard(name: str, rank: int, world: int, seed: int = 0, device=None, scale: float = 1.0,
+                    homophily: float = 0.8, feat_noise: float = 4.0, label_noise: float = 0.25,
+                    id_order: str = "shuffled", feature_dtype=torch.float32) -> GraphShard:
+    """This rank's rows of ``synthetic(name, ...)`` -- the same graph, generated shard-locally
+    (the C++ generator hashes every edge once and keeps those touching the shard; memory
+    is O(shard)).  ``feature_dtype`` bf16 halves the feature bytes of a 10^8-node graph."""
+    n, m, F, C, n_train, n_val = SHAPES[name]
+    n = max(int(n * scale), C * 4)
+    m = max(int(m * scale), n)
+    n_train = max(int(n_train * scale), C)
+    n_val = max(int(n_val * scale), C)
+    r0, r1, _ = shard_rows(n, rank, world)
+    rt = native.rt()
+    rp, col, x, y = rt.synthetic_shard(n, m, F, C, homophily, feat_noise, seed, label_noise, ID_ORDERS[id_order],
+                                       r0, r1)
+    rp = np.asarray(rp)
+    rp_t = torch.from_numpy(rp.astype(np.int32) if rp[-1] < 2 ** 31 else rp)
+    mask = np.asarray(rt.split_mask(n, n_train, n_val, seed + 1, np.arange(r0, r1, dtype=np.int64)))
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    xt = torch.from_numpy(np.asarray(x))
+    if feature_dtype != torch.float32:
+        xt = xt.to(feature_dtype)
+    return GraphShard(n=n, r0=r0, r1=r1, rowptr=rp_t.to(dev), col=torch.from_numpy(np.asarray(col)).to(dev),
+                      x=xt.to(dev), y=torch.from_numpy(np.asarray(y).astype(np.int32)).to(dev),
+                      mask=torch.from_numpy(mask).to(dev), n_classes=C, n_train_global=n_train,
+                      name="%s-synthetic-shard%d/%d" % (name, rank, world))
 
 
 def locality(g: GraphData, windows=(64, 256, 1024, 4096, 65536), new_id=None):

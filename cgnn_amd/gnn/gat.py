@@ -58,6 +58,36 @@ class GraphCSR:
         return self._rows
 
 
+def _gat_forward_kernels(Whg, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool):
+    n = g.n
+    out = torch.empty(n, K * Fh, dtype=torch.float32, device=Whg.device)
+    lse = torch.empty(n, K, dtype=torch.float32, device=Whg.device)
+    native.hip().gnn_gat_fwd(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(),
+                             s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Whg), int(lowp))
+    return out, lse
+
+
+def _gat_backward_kernels(Whg, s_src, s_dst, out, lse, dout, g: GraphCSR, K: int, Fh: int, lowp: bool):
+    """(dWh [n_cols, K*Fh] fp32, ds_src [n_cols, K], ds_dst [n, K])."""
+    hip = native.hip()
+    n, dev = g.n, Whg.device
+    dout = dout.contiguous().float()
+    alpha_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+    dsc_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+    ds_dst = torch.empty(n, K, dtype=torch.float32, device=dev)
+    hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(),
+                        s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(),
+                        dsc_e.data_ptr(), ds_dst.data_ptr(), n, K, Fh, _st(Whg), int(lowp))
+    rp_t, col_t, perm = g.transposed()
+    doutg = dout.to(torch.bfloat16) if lowp else dout
+    dWh = torch.empty(g.n_cols, K * Fh, dtype=torch.float32, device=dev)   # one row per source
+    ds_src = torch.empty(g.n_cols, K, dtype=torch.float32, device=dev)
+    hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
+                        dsc_e.data_ptr(), doutg.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh,
+                        _st(Whg), int(lowp))
+    return dWh, ds_src, ds_dst
+
+
 class _GATAggregate(torch.autograd.Function):
     """HIP attention aggregation.  ``lowp``: the edge-gathered matrices (Wh in the
     forward and the row backward, dout in the column backward) are stored bf16,
@@ -66,39 +96,63 @@ class _GATAggregate(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool):
-        hip = native.hip()
-        n = g.n
         Whg = Wh.to(torch.bfloat16).contiguous() if lowp else Wh.contiguous()
         s_src, s_dst = s_src.contiguous(), s_dst.contiguous()
-        out = torch.empty(n, K * Fh, dtype=torch.float32, device=Wh.device)
-        lse = torch.empty(n, K, dtype=torch.float32, device=Wh.device)
-        hip.gnn_gat_fwd(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(),
-                        out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Wh), int(lowp))
+        out, lse = _gat_forward_kernels(Whg, s_src, s_dst, g, K, Fh, lowp)
         ctx.save_for_backward(Whg, s_src, s_dst, out, lse)
         ctx.g, ctx.K, ctx.Fh, ctx.lowp = g, K, Fh, lowp
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        hip = native.hip()
         Whg, s_src, s_dst, out, lse = ctx.saved_tensors
-        g, K, Fh, lowp = ctx.g, ctx.K, ctx.Fh, ctx.lowp
-        n, dev = g.n, Whg.device
-        dout = dout.contiguous().float()
-        alpha_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
-        dsc_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
-        ds_dst = torch.empty(n, K, dtype=torch.float32, device=dev)
-        hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(),
-                            s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(),
-                            dsc_e.data_ptr(), ds_dst.data_ptr(), n, K, Fh, _st(Whg), int(lowp))
-        rp_t, col_t, perm = g.transposed()
-        doutg = dout.to(torch.bfloat16) if lowp else dout
-        dWh = torch.empty(g.n_cols, K * Fh, dtype=torch.float32, device=dev)   # one row per source
-        ds_src = torch.empty(g.n_cols, K, dtype=torch.float32, device=dev)
-        hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
-                            dsc_e.data_ptr(), doutg.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh,
-                            _st(Whg), int(lowp))
+        dWh, ds_src, ds_dst = _gat_backward_kernels(Whg, s_src, s_dst, out, lse, dout, ctx.g, ctx.K, ctx.Fh,
+                                                    ctx.lowp)
         return dWh, ds_src, ds_dst, None, None, None, None
+
+
+class _HaloGAT(torch.autograd.Function):
+    """Graph-sharded attention aggregation: the source-side ``[Wh | s_src]`` of this
+    rank's rows goes through ONE halo all-to-all (Wh as bf16 on the wire when ``lowp``,
+    the attention scores exactly as fp32), the HIP kernels (or the CPU reference)
+    aggregate over the extended rows ``[own | received]``, and the backward returns
+    the gradients of the received rows to their owners (fp32) through the transposed
+    exchange."""
+
+    @staticmethod
+    def forward(ctx, Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool, halo,
+                grad_wire=torch.float32):
+        wdt = torch.bfloat16 if (lowp and Wh.is_cuda) else torch.float32
+        ctx.grad_wire = grad_wire
+        buf = halo.exchange(halo.pack([Wh.to(wdt), s_src.float()]))
+        Wh_ext, s_ext = halo.unpack(buf, [(K * Fh, wdt), (K, torch.float32)])
+        del buf
+        ctx.g, ctx.K, ctx.Fh, ctx.lowp, ctx.halo = g, K, Fh, lowp, halo
+        s_dst = s_dst.contiguous()
+        if Wh.is_cuda:
+            out, lse = _gat_forward_kernels(Wh_ext, s_ext, s_dst, g, K, Fh, wdt == torch.bfloat16)
+            ctx.save_for_backward(Wh_ext, s_ext, s_dst, out, lse)
+            return out
+        ctx.save_for_backward(Wh_ext, s_ext, s_dst)
+        return _gat_aggregate_torch(Wh_ext, s_ext, s_dst, g, K, Fh)
+
+    @staticmethod
+    def backward(ctx, dout):
+        g, K, Fh, halo = ctx.g, ctx.K, ctx.Fh, ctx.halo
+        if dout.is_cuda:
+            Wh_ext, s_ext, s_dst, out, lse = ctx.saved_tensors
+            dWh, ds_src, ds_dst = _gat_backward_kernels(Wh_ext, s_ext, s_dst, out, lse, dout, g, K, Fh,
+                                                        Wh_ext.dtype == torch.bfloat16)
+        else:
+            Wh_ext, s_ext, s_dst = ctx.saved_tensors
+            with torch.enable_grad():
+                a = Wh_ext.detach().requires_grad_()
+                b = s_ext.detach().requires_grad_()
+                c = s_dst.detach().requires_grad_()
+                o = _gat_aggregate_torch(a, b, c, g, K, Fh)
+                dWh, ds_src, ds_dst = torch.autograd.grad(o, (a, b, c), dout)
+        dWh_loc, ds_loc = halo.reduce_back([dWh.float(), ds_src.float()], ctx.grad_wire)
+        return dWh_loc, ds_loc, ds_dst, None, None, None, None, None, None
 
 
 def _gat_aggregate_torch(Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int):
@@ -141,9 +195,10 @@ class GATLayer(torch.nn.Module):
         self.a_dst = torch.nn.Parameter((torch.rand(heads, head_dim, generator=generator) * 2 - 1) * ab)
         self.bias = torch.nn.Parameter(torch.zeros(heads * head_dim))
 
-    def forward(self, h, g: GraphCSR, gather=None):
-        """``gather`` (graph-sharded training): maps this rank's rows to all rows;
-        the source-side [Wh | s_src] goes through ONE collective."""
+    def forward(self, h, g: GraphCSR, halo=None):
+        """``halo`` (graph-sharded training, ``parallel.halo.HaloExchange``): the
+        source-side [Wh | s_src] of this rank's rows goes through ONE all-to-all and the
+        aggregation runs over [own | received] rows (``g`` holds the extended columns)."""
         # the attention logits are linear in h: fold a_src / a_dst into the weight,
         # s = h (W a), so [Wh | s_src | s_dst] is ONE GEMM (no [n, K, Fh] temporary,
         # no broadcast multiply + reduction over all rows)
@@ -152,9 +207,9 @@ class GATLayer(torch.nn.Module):
         Wcat = torch.cat([self.W, (Wk * self.a_src).sum(-1), (Wk * self.a_dst).sum(-1)], 1)
         y = h @ Wcat
         Wh, s_src, s_dst = y[:, :KF], y[:, KF:KF + K], y[:, KF + K:]
-        if gather is not None:
-            both = gather(torch.cat([Wh, s_src], 1))
-            Wh, s_src = both[:, :self.K * self.Fh], both[:, self.K * self.Fh:]
+        if halo is not None:
+            return _HaloGAT.apply(Wh, s_src, s_dst, g, self.K, self.Fh, True, halo,
+                                  getattr(halo, "grad_wire", torch.float32)) + self.bias
         return gat_aggregate(Wh, s_src, s_dst, g, self.K, self.Fh) + self.bias
 
 
@@ -172,11 +227,11 @@ class GAT(torch.nn.Module):
         self.l2 = GATLayer(heads * head_dim, 1, out_w, gen)
         self.dropout = float(dropout)
 
-    def forward(self, x, g: GraphCSR, gather=None):
-        h = torch.nn.functional.elu(self.l1(x, g, gather))
+    def forward(self, x, g: GraphCSR, halo=None):
+        h = torch.nn.functional.elu(self.l1(x, g, halo))
         if self.training and self.dropout > 0:
             h = torch.nn.functional.dropout(h, self.dropout)
-        return self.l2(h, g, gather)[:, :self.C]
+        return self.l2(h, g, halo)[:, :self.C]
 
 
 class GATTrainer:
@@ -216,57 +271,90 @@ class GATTrainer:
 
 class ShardedGATTrainer:
     """Graph-sharded full-graph GAT (BASELINE config "ogbn-papers100M 2-layer GAT,
-    graph sharded across 8 x 288 GB HBM"): rank r owns a contiguous block of
-    destination rows -- its CSR rows (global source ids), features, labels and
-    all activations of those rows.  Per layer one all-gather of the source-side
-    [Wh | s_src] rows (RCCL ring over xGMI) and, in the backward, one
-    reduce-scatter of their gradients back to the owners; parameters are
-    replicated and their gradients averaged by the bucketed all-reduce.  Feature
-    standardisation uses globally all-reduced moments, so the model equals the
-    single-GPU one for any rank count."""
+    graph sharded across 8 x 288 GB HBM").
 
-    def __init__(self, gd: GraphData, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True,
-                 bucket_mb: float = 16.0):
+    Rank r owns a contiguous block of rows: its CSR rows (global source ids), features,
+    labels and every activation of those rows -- built by ``data.synthetic_shard``
+    from rank-local generation (no rank ever holds the whole graph; 10^8 nodes and
+    3.2 x 10^9 CSR entries at full size).  Per layer the source-side [Wh | s_src] rows
+    a rank's edges read -- and only those -- arrive through one halo all-to-all
+    (``parallel.halo``: bf16 activations + exact fp32 scores on the wire); the
+    backward returns their gradients to the owners.  Parameters are replicated and
+    their gradients averaged by the bucketed all-reduce; feature standardisation
+    uses globally all-reduced moments, so for any rank count the model equals the
+    single-GPU one (``tests/test_dist_cpu.py``).
+
+    ``emulate=(rank, world)``: one rank of a larger job in a single process (the
+    halo plan and buffers of that rank, received rows left zero) -- a memory /
+    compute dry run of a full-size shard on one GPU, not a numerics run.
+    """
+
+    def __init__(self, shard, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True,
+                 bucket_mb: float = 16.0, emulate=None):
         import torch.distributed as dist
         from ..parallel import dist as pdist
-        from ..parallel.collectives import gather_rows
         from ..parallel.ddp import GradBucketer
-        from .data import partition_rows
-        self.rank, self.world = pdist.rank(), pdist.world_size()
-        self.dev = gd.rowptr.device
-        self.n = gd.n
-        r0, r1, per, rp, col = partition_rows(gd, self.rank, self.world)
+        from ..parallel.halo import HaloExchange
+        from .data import GraphShard, shard_rows
+        if not isinstance(shard, GraphShard):          # a full graph: take this rank's rows of it
+            shard = shard_of(shard, pdist.rank(), pdist.world_size())
+        self.emulate = emulate
+        if emulate is not None:
+            self.rank, self.world = int(emulate[0]), int(emulate[1])
+        else:
+            self.rank, self.world = pdist.rank(), pdist.world_size()
+        self.dev = shard.rowptr.device
+        self.n = shard.n
+        r0, r1, per = shard_rows(shard.n, self.rank, self.world)
+        if (r0, r1) != (shard.r0, shard.r1):
+            raise ValueError("shard rows [%d, %d) are not rank %d/%d's block" % (shard.r0, shard.r1, self.rank,
+                                                                                 self.world))
         self.r0, self.r1, self.per = r0, r1, per
-        self.g = GraphCSR(rp, col, r1 - r0, n_cols=gd.n)
-        x = gd.x[r0:r1].float()
+        nloc = r1 - r0
+        distributed = self.world > 1 and emulate is None
+        self.halo = None
+        if self.world > 1:
+            self.halo = HaloExchange(shard.col, r0, r1, per, shard.n, emulate=emulate)
+            self.g = GraphCSR(shard.rowptr, self.halo.col_ext, nloc, n_cols=self.halo.n_ext)
+        else:
+            self.g = GraphCSR(shard.rowptr, shard.col, nloc, n_cols=shard.n)
+        x = shard.x.float()
         if standardize:
             mom = torch.stack([x.sum(0), (x * x).sum(0)]).double()
-            if self.world > 1:
+            if distributed:
                 dist.all_reduce(mom)
-            mean = mom[0] / gd.n
-            var = (mom[1] / gd.n - mean * mean) * gd.n / max(gd.n - 1, 1)
+            mean = mom[0] / shard.n
+            var = (mom[1] / shard.n - mean * mean) * shard.n / max(shard.n - 1, 1)
             x = ((x - mean.float()) / var.clamp_min(1e-12).sqrt().float().clamp_min(1e-6))
         self.x = x.contiguous()
-        self.y = gd.y[r0:r1].long()
-        self.mask = gd.mask[r0:r1]
+        self.y = shard.y.long()
+        self.mask = shard.mask
         self.tr = self.mask == 1
         n_train = torch.tensor([float(self.tr.sum())], dtype=torch.float64, device=self.dev)
-        if self.world > 1:
+        if distributed:
             dist.all_reduce(n_train)
-        self.n_train = float(n_train.item())
-        self.model = GAT(x.shape[1], gd.n_classes, heads, head_dim, dropout, seed).to(self.dev)
+        self.n_train = float(n_train.item()) if emulate is None else float(shard.n_train_global or n_train.item())
+        self.model = GAT(x.shape[1], shard.n_classes, heads, head_dim, dropout, seed).to(self.dev)
         self.opt = torch.optim.Adam(self.model.parameters(), lr=lr, fused=self.dev.type == "cuda")
         self.ddp = None
-        self.gather = None
-        if self.world > 1:
+        if distributed:
             self.ddp = GradBucketer(list(self.model.parameters()), bucket_mb)
             self.ddp.broadcast_parameters(0)
-            self.gather = lambda t: gather_rows(t, per, gd.n)
         self.epoch = 0
+
+    def halo_stats(self):
+        """Rows / bytes this rank receives and sends per layer-1 exchange (Wh bf16 + fp32 scores)."""
+        if self.halo is None:
+            return {"recv_rows": 0, "send_rows": 0}
+        l1 = self.model.l1
+        w = 2 * l1.K * l1.Fh + 4 * l1.K
+        rb, sb = self.halo.bytes_per_exchange(w)
+        return {"recv_rows": self.halo.n_recv, "send_rows": self.halo.n_send, "local_rows": self.halo.nloc,
+                "layer1_recv_bytes": rb, "layer1_send_bytes": sb}
 
     def train_step(self):
         self.model.train()
-        out = self.model(self.x, self.g, self.gather)
+        out = self.model(self.x, self.g, self.halo)
         # sum over this rank's train rows scaled so that the rank-average of the
         # gradients is the gradient of the global mean loss
         loss = torch.nn.functional.cross_entropy(out[self.tr], self.y[self.tr], reduction="sum")
@@ -282,14 +370,27 @@ class ShardedGATTrainer:
     def evaluate(self):
         import torch.distributed as dist
         self.model.eval()
-        pred = self.model(self.x, self.g, self.gather).argmax(1)
+        pred = self.model(self.x, self.g, self.halo).argmax(1)
         cnt = torch.zeros(6, dtype=torch.float64, device=self.dev)
         for i, k in enumerate((1, 2, 3)):
             m = self.mask == k
             cnt[2 * i] = float((pred[m] == self.y[m]).sum())
             cnt[2 * i + 1] = float(m.sum())
-        if self.world > 1:
+        if self.world > 1 and self.emulate is None:
             dist.all_reduce(cnt)
         c = cnt.cpu().numpy()
         return {name: float(c[2 * i] / c[2 * i + 1]) if c[2 * i + 1] else float("nan")
                 for i, name in enumerate(("train_acc", "val_acc", "test_acc"))}
+
+
+def shard_of(gd: GraphData, rank: int, world: int):
+    """This rank's rows of an in-memory graph as a ``GraphShard`` (tests / small graphs;
+    large graphs are generated shard-locally by ``data.synthetic_shard``)."""
+    from .data import GraphShard, shard_rows
+    r0, r1, _ = shard_rows(gd.n, rank, world)
+    rp = gd.rowptr[r0:r1 + 1].to(torch.int64)
+    col = gd.col[int(rp[0]): int(rp[-1])]
+    rp = (rp - rp[0]).to(torch.int32)
+    return GraphShard(n=gd.n, r0=r0, r1=r1, rowptr=rp.contiguous(), col=col.contiguous(), x=gd.x[r0:r1],
+                      y=gd.y[r0:r1], mask=gd.mask[r0:r1], n_classes=gd.n_classes,
+                      n_train_global=int((gd.mask == 1).sum()), name=gd.name + "-shard%d/%d" % (rank, world))

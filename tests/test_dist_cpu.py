@@ -199,24 +199,28 @@ def test_sage_data_parallel_keeps_replicas_identical():
 
 def _gat_shard_worker(rank, world, port, out):
     _init(rank, world, port)
-    from cgnn_amd.gnn.data import synthetic
+    from cgnn_amd.gnn.data import synthetic_shard
     from cgnn_amd.gnn.gat import ShardedGATTrainer
-    g = synthetic("ogbn-products", seed=1, scale=0.0005)
-    tr = ShardedGATTrainer(g, heads=2, head_dim=8, dropout=0.0, lr=0.01, seed=rank)
+    # rank-local generation: this rank never builds the rest of the graph
+    shard = synthetic_shard("ogbn-products", rank, world, seed=1, scale=0.0005)
+    tr = ShardedGATTrainer(shard, heads=2, head_dim=8, dropout=0.0, lr=0.01, seed=rank)
     losses = []
     for _ in range(3):
         l = tr.train_step().clone()
         dist.all_reduce(l)
         losses.append(float(l))
     res = tr.evaluate()
-    out[rank] = (losses, res, torch.cat([p.detach().flatten() for p in tr.model.parameters()]).numpy())
+    out[rank] = (losses, res, torch.cat([p.detach().flatten() for p in tr.model.parameters()]).numpy(),
+                 tr.halo_stats())
     dist.destroy_process_group()
 
 
-def test_sharded_gat_matches_single_process():
-    """GAT with rows sharded over 2 gloo ranks (all-gather of [Wh | s_src], reduce-
-    scatter of their gradients, averaged parameter gradients) equals the
-    unsharded model: same global losses, accuracies and parameters."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_gat_matches_single_process(world):
+    """GAT with rows sharded over gloo ranks -- rank-local shard generation, halo
+    all-to-all of exactly the [Wh | s_src] rows each rank reads, gradients returned
+    to their owners, averaged parameter gradients -- equals the unsharded model:
+    same global losses, accuracies and parameters."""
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gat import ShardedGATTrainer
     g = synthetic("ogbn-products", seed=1, scale=0.0005)
@@ -226,10 +230,13 @@ def test_sharded_gat_matches_single_process():
     ref_params = torch.cat([p.detach().flatten() for p in ref.model.parameters()]).numpy()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_gat_shard_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    for r in range(2):
-        losses, res, params = out[r]
+    mp.spawn(_gat_shard_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        losses, res, params, hs = out[r]
         np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
         assert res == pytest.approx(ref_res, abs=1e-9)
-        np.testing.assert_allclose(params, ref_params, rtol=1e-4, atol=1e-6)
+        # (summation order of the returned halo gradients differs from the unsharded sum)
+        np.testing.assert_allclose(params, ref_params, rtol=1e-4, atol=3e-5)
+        assert 0 < hs["recv_rows"] < g.n - hs["local_rows"] or hs["recv_rows"] == g.n - hs["local_rows"]
+    assert sum(out[r][3]["recv_rows"] for r in range(world)) == sum(out[r][3]["send_rows"] for r in range(world))
     np.testing.assert_array_equal(out[0][2], out[1][2])

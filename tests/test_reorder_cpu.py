@@ -75,3 +75,26 @@ def test_gcn_loss_is_invariant_under_reorder():
     ra, rb = a.evaluate(), b.evaluate()
     for k in ra:
         assert abs(ra[k] - rb[k]) < 2e-3, (k, ra, rb)
+
+
+@pytest.mark.parametrize("world,id_order", [(3, "shuffled"), (2, "banded")])
+def test_shards_reassemble_the_full_graph(world, id_order):
+    """Rank-local shard generation gives exactly the rows of the full build."""
+    from cgnn_amd.gnn.data import synthetic_shard
+    full = synthetic("ogbn-products", seed=5, scale=0.002, id_order=id_order)
+    parts = [synthetic_shard("ogbn-products", r, world, seed=5, scale=0.002, id_order=id_order) for r in range(world)]
+    assert sum(p.n_local for p in parts) == full.n and all(p.n == full.n for p in parts)
+    rp = torch.cat([parts[0].rowptr.long()] + [p.rowptr.long()[1:] + sum(q.nnz for q in parts[:i])
+                                               for i, p in enumerate(parts) if i > 0])
+    assert torch.equal(rp, full.rowptr.long())
+    assert torch.equal(torch.cat([p.col for p in parts]), full.col)
+    assert torch.equal(torch.cat([p.x for p in parts]), full.x)
+    assert torch.equal(torch.cat([p.y for p in parts]), full.y)
+    assert torch.equal(torch.cat([p.mask for p in parts]), full.mask)
+
+
+def test_id_permutation_inverse():
+    rt = native.rt()
+    ids = np.arange(10007)
+    p = np.asarray(rt.id_permutation(10007, 9, ids))
+    assert np.array_equal(np.asarray(rt.id_permutation(10007, 9, p, True)), ids)

@@ -64,6 +64,11 @@ def main():
     ap.add_argument("--no-capture", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--reorder", choices=["lp-cm", "none"], default="lp-cm",
                     help="framework locality pass on the (shuffled-id) synthetic graph, timed in setup")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="papers-gat2: one process plays rank --emulate-rank of this many ranks (its "
+                         "rank-local shard, halo plan and buffers; received rows zero) -- memory / compute dry run")
+    ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--halo-grad-bf16", action="store_true", help="papers-gat2: gradients on the halo wire in bf16")
     ap.add_argument("--unfused", action="store_true", help="arxiv-gcn3 / products-sage3: autograd + hipBLASLt path (A/B)")
     a = ap.parse_args()
 
@@ -165,23 +170,41 @@ def main():
                    config={"model": "SAGE-3layer-hidden%d" % hidden, "fanouts": [15, 10, 5],
                            "batch_per_rank": 1024, "parallelism": "dp%d" % world, "nodes": g.n})
     else:
+        from cgnn_amd.gnn.data import synthetic_shard
         from cgnn_amd.gnn.gat import ShardedGATTrainer
         steps, warmup = a.steps or 10, a.warmup or 2
-        g = synthetic("ogbn-papers100M", seed=a.seed, device=dev, scale=a.scale)
-        tr = ShardedGATTrainer(g, heads=4, head_dim=32, dropout=0.5, lr=0.005, seed=a.seed)
-        n_nodes, nnz = g.n, g.nnz
-        del g
+        emu = (a.emulate_rank, a.emulate_world) if a.emulate_world > 1 else None
+        srank, sworld = emu if emu else (rank, world)
+        t0 = time.perf_counter()
+        shard = synthetic_shard("ogbn-papers100M", srank, sworld, seed=a.seed, device=dev, scale=a.scale)
+        gen_s = time.perf_counter() - t0
+        n_nodes, nnz_local, n_local = shard.n, shard.nnz, shard.n_local
+        tr = ShardedGATTrainer(shard, heads=4, head_dim=32, dropout=0.5, lr=0.005, seed=a.seed, emulate=emu)
+        if tr.halo is not None and a.halo_grad_bf16:
+            tr.halo.grad_wire = torch.bfloat16
+        del shard
         setup = time.perf_counter() - t_setup
+        if dev.type == "cuda":
+            torch.cuda.reset_peak_memory_stats(dev)
         dt = _timed(tr.train_step, steps, warmup, dev)
         ev = tr.evaluate()
+        peak = torch.cuda.max_memory_allocated(dev) / 2 ** 30 if dev.type == "cuda" else None
         res.update(metric="epochs/sec + val-acc, 2-layer GAT ogbn-papers100M, graph sharded",
                    value=round(steps / dt, 4), unit="epochs/s", ms_per_step=round(1e3 * dt / steps, 3),
                    val_acc=round(ev["val_acc"], 4), test_acc=round(ev["test_acc"], 4),
-                   dtype="fp32 compute, bf16 storage of the edge-gathered rows" if dev.type == "cuda" else "fp32",
-                   config={"model": "GAT-2layer-4x32", "parallelism": "graph-rowpart%d" % world, "nodes": n_nodes,
-                           "nnz_with_self_loops": nnz})
+                   dtype="bf16 storage of the edge-gathered / halo rows, fp32 scores, accumulation and gradients"
+                   if dev.type == "cuda" else "fp32",
+                   peak_gpu_mem_gib=round(peak, 2) if peak is not None else None,
+                   shard={"rank": srank, "world": sworld, "rows": n_local, "nnz": nnz_local, "gen_s": round(gen_s, 2),
+                          "rank_local_generation": True},
+                   halo=tr.halo_stats(), emulated=emu is not None, reordered=False,
+                   note=("DRY RUN: one rank of %d in one process; received halo rows are zero, so timing / memory "
+                         "are those of the rank's kernels and buffers without communication, accuracy is not "
+                         "meaningful" % sworld) if emu else None,
+                   config={"model": "GAT-2layer-4x32", "parallelism": "graph-rowpart%d" % sworld, "nodes": n_nodes})
     res.update(steps=steps, warmup=warmup, setup_s=round(setup, 2), data="synthetic graph of the named shape "
-               "(planted communities, shuffled ids), random-init weights", reordered=a.reorder != "none")
+               "(planted communities, shuffled ids), random-init weights")
+    res.setdefault("reordered", a.reorder != "none")
     res.setdefault("higher_is_better", True)
     if rank == 0:
         print(json.dumps(res), flush=True)
