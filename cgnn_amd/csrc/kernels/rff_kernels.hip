@@ -11,7 +11,11 @@
 //
 // Layouts: W [R][F][D+1] (D frequencies then the phase), diff [R][F],
 // data/xhat [R][D][N], grad -> chunk 0 of the MMD gradient buffer [1][R][D][N].
+//
+// Default: matrix-core kernels (below); the vector kernels (one feature / one sample
+// per thread) remain for CGNN_RFF_VALU=1 (A/B) and for W images too large for LDS.
 #include "cgnn_common.h"
+#include <cstdlib>
 
 using namespace cgnn;
 
@@ -117,6 +121,158 @@ __global__ __launch_bounds__(256) void rff_grad_kernel(const float* __restrict__
   for (int k = 0; k < D; ++k) gr[(size_t)k * N + n] = g[k];
 }
 
+// ============================================================================
+// Matrix-core K6: the projections theta = [x | 1] W^T run on the exact-fp32
+// matrix cores (v_mfma_f32_32x32x2_f32, the same bits as an fmaf chain), so the VALU
+// only evaluates the cos / sin epilogue while the next tile's MFMAs issue.
+//
+// Forward: wave w of the block owns the 32 features f0 + [0, 32) (8 waves = 256
+// features per block, the partial layout of rff_feat_kernel).  Per 32-sample tile:
+// C[n][f] = sum_k A[n][k] B[k][f], A = [x | 1] (lane: sample n = l & 31, k = 2s + l/32,
+// coalesced along n in the [D][N] layout), B = W^T held in registers for the whole
+// loop; the lane then owns 16 samples of ONE feature, so the column means are
+// in-register sums + one cross-half shuffle.
+// ============================================================================
+template <int D>
+__global__ __launch_bounds__(512) void rff_mfma_feat_kernel(const float* __restrict__ xhat,
+                                                            const float* __restrict__ data,
+                                                            const float* __restrict__ W,
+                                                            float* __restrict__ diff,
+                                                            float* __restrict__ loss_part, int N, int F,
+                                                            float norm) {
+  constexpr int KS = (D + 2) / 2;          // k-steps of 2 over the D + 1 columns of [x | 1]
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  __shared__ float s_red[8];
+  const int r = blockIdx.y;
+  const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31, wv = threadIdx.x >> 6;
+  const int f = (blockIdx.x * 8 + wv) * 32 + lr;
+  const bool fv = f < F;
+  const float* wf = W + ((size_t)r * F + (fv ? f : 0)) * (D + 1);
+  float bw[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    bw[s] = (fv && k <= D) ? wf[k] : 0.f;
+  }
+  float sums[2];
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+    const float* X = (part == 0 ? xhat : data) + (size_t)r * D * N;
+    float acc = 0.f;
+    for (int n0 = 0; n0 < N; n0 += 32) {
+      const int n = n0 + lr;
+      f32x16 c = {};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int k = 2 * s + h;
+        const float a = n < N ? (k < D ? X[(size_t)k * N + n] : (k == D ? 1.f : 0.f)) : 0.f;
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bw[s], c, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int nn = n0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        acc += nn < N ? cos_rev(c[q]) : 0.f;
+      }
+    }
+    sums[part] = acc + __shfl_xor(acc, 32, 64);
+  }
+  const float dlt = fv ? norm * (sums[0] - sums[1]) / (float)N : 0.f;
+  if (fv && h == 0) diff[(size_t)r * F + f] = dlt;
+  float v = (h == 0) ? dlt * dlt : 0.f;
+  v = wave_sum(v);
+  if (lane == 0) s_red[wv] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t += s_red[w];
+    loss_part[(size_t)r * gridDim.x + blockIdx.x] = t;
+  }
+}
+
+// Gradient: wave w owns the 32 samples n0 + [0, 32); over every 32-feature tile,
+//   C'[f][n] = sum_k W[f][k] [x | 1][k][n]        (A = W rows, B = this tile's samples)
+//   S'[f][n] = -coef diff_f sin(C'[f][n])          (in the accumulator registers)
+//   G[k][n] += sum_f W^T[k][f] S'[f][n]            (k-step q takes register q of every
+//                                                    lane as B: f = (q&3) + 8(q>>2) + 4(l/32)
+//                                                    -- the accumulator IS the operand)
+// W of the model is staged in LDS once per block.
+template <int D>
+__global__ __launch_bounds__(256) void rff_mfma_grad_kernel(const float* __restrict__ xhat,
+                                                            const float* __restrict__ W,
+                                                            const float* __restrict__ diff,
+                                                            float* __restrict__ grad, int N, int F,
+                                                            float coef) {
+  constexpr int KS = (D + 2) / 2;
+  constexpr int DT = (D + 31) / 32;        // 32-row tiles of the gradient's k (feature dim)
+  constexpr int WS = D + 1;
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  extern __shared__ float sW[];            // [F][WS] then diff [F]
+  float* sD = sW + (size_t)F * WS;
+  const int r = blockIdx.y;
+  const float* Wr = W + (size_t)r * F * WS;
+  for (int i = threadIdx.x; i < F * WS; i += blockDim.x) sW[i] = Wr[i];
+  for (int i = threadIdx.x; i < F; i += blockDim.x) sD[i] = -coef * diff[(size_t)r * F + i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31, wv = threadIdx.x >> 6;
+  const int n0 = (blockIdx.x * 4 + wv) * 32;
+  if (n0 >= N) return;                      // after the only barrier
+  const int n = n0 + lr;
+  const float* X = xhat + (size_t)r * D * N;
+  float xb[KS];                             // B of the first product: [x | 1][k = 2s + h][n]
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    xb[s] = n < N ? (k < D ? X[(size_t)k * N + n] : (k == D ? 1.f : 0.f)) : 0.f;
+  }
+  f32x16 g[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) g[t] = f32x16{};
+  for (int f0 = 0; f0 < F; f0 += 32) {
+    const int fa = f0 + lr;                 // this lane's A row of the first product
+    f32x16 c = {};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = 2 * s + h;
+      const float a = (fa < F && k <= D) ? sW[fa * WS + k] : 0.f;
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xb[s], c, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ff = f0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      c[q] = ff < F ? sD[ff] * sin_rev(c[q]) : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ff = f0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        const int k = 32 * t + lr;
+        const float a = (ff < F && k < D) ? sW[ff * WS + k] : 0.f;
+        g[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, c[q], g[t], 0, 0, 0);
+      }
+    }
+  }
+  if (n >= N) return;
+  float* gr = grad + (size_t)r * D * N;
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int k = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (k < D) gr[(size_t)k * N + n] = g[t][q];
+    }
+}
+
+// matrix-core path from this padded width on (CGNN_RFF_MFMA_MIN_D, default 1: every width); CGNN_RFF_VALU=1
+// forces the vector kernels.  Read at every enqueue (a captured hipGraph keeps its choice).
+static int rff_mfma_min_d() {
+  const char* v = getenv("CGNN_RFF_VALU");
+  if (v && atoi(v) == 1) return 1 << 30;
+  const char* e = getenv("CGNN_RFF_MFMA_MIN_D");
+  return e ? atoi(e) : 1;
+}
+
 extern "C" int rff_launch_freqs(float* W, const uint32_t* keys, const int* step_base, int step_off,
                                 int k, int D, int n_gamma, int d_true, int R, hipStream_t st) {
   const int tot = k * n_gamma * (D + 1);
@@ -129,6 +285,18 @@ template <int D>
 static int rff_fb_d(int mode, const float* xhat, const float* data, const float* W, float* diff,
                     float* loss_part, float* grad, int N, int F, int R, int k, float norm,
                     hipStream_t st) {
+  const size_t glds = sizeof(float) * ((size_t)F * (D + 1) + F);
+  if (D >= rff_mfma_min_d() && glds <= 160 * 1024) {
+    hipLaunchKernelGGL((rff_mfma_feat_kernel<D>), dim3((F + 255) / 256, R), dim3(512), 0, st, xhat, data, W, diff,
+                       loss_part, N, F, norm);
+    if (mode == 0) {
+      (void)hipFuncSetAttribute((const void*)rff_mfma_grad_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)glds);
+      hipLaunchKernelGGL((rff_mfma_grad_kernel<D>), dim3((N + 127) / 128, R), dim3(256), glds, st, xhat, W, diff,
+                         grad, N, F, 2.f * norm / (float)N);
+    }
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL((rff_feat_kernel<D>), dim3((F + 255) / 256, R), dim3(256), 0, st, xhat, data,
                      W, diff, loss_part, N, F, norm);
   if (mode == 0) {

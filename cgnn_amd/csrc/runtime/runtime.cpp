@@ -507,6 +507,7 @@ PYBIND11_MODULE(_rt, m) {
         py::arg("ids"));
   m.def("sample_neighbors", &sample_neighbors);
   m.def("num_threads", []() { return omp_get_max_threads(); });
+  m.def("set_num_threads", [](int k) { omp_set_num_threads(k > 0 ? k : 1); }, py::arg("k"));
   m.def("id_permutation", [](i64 n, uint64_t seed, py::array_t<i64, py::array::c_style | py::array::forcecast> v,
                              bool inverse) {
     const cgnn_rt::IdPermutation p(n, seed);

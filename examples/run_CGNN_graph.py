@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--train", type=int, default=None)
     ap.add_argument("--test", type=int, default=None)
     ap.add_argument("--checkpoint", default=None)
+    ap.add_argument("--fast-mmd", action="store_true", help="SETTINGS.use_Fast_MMD (random Fourier features)")
     a = ap.parse_args()
     datafile = _common.data_path("Example_graph_numdata.csv", a.data)
     skeletonfile = _common.data_path("Example_graph_skeleton.csv", a.skeleton)
@@ -34,6 +35,7 @@ def main():
         cgnn.SETTINGS.train_epochs = a.train
     if a.test:
         cgnn.SETTINGS.test_epochs = a.test
+    cgnn.SETTINGS.use_Fast_MMD = bool(a.fast_mmd)
     base = os.path.join(a.out_dir, os.path.basename(datafile))
     print("Processing " + datafile + "...")
     t0 = time.perf_counter()
@@ -50,7 +52,7 @@ def main():
     t2 = time.perf_counter()
     pd.DataFrame(directed_graph.get_list_edges(descending=True),
                  columns=['Cause', 'Effect', 'Score']).to_csv(base + "_predictions.csv")
-    res = {"workload": "graph", "alg": a.alg, "seconds_pairwise": round(t1 - t0, 3),
+    res = {"workload": "graph", "alg": a.alg, "fast_mmd": bool(a.fast_mmd), "seconds_pairwise": round(t1 - t0, 3),
            "seconds_search": round(t2 - t1, 3), "seconds_total": round(t2 - t0, 3),
            "candidates_evaluated": (METRICS.last("candidates") or {}).get("total")}
     tfile = datafile.replace("_numdata.csv", "_target.csv")

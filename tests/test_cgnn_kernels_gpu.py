@@ -180,3 +180,30 @@ def test_row_range_mmd_tiles_the_full_mmd(d, kernel):
         total += loss.double().cpu()
         np.testing.assert_allclose(grad.double().cpu().numpy(), p.grad[:, b:e].numpy(), rtol=2e-3, atol=2e-7)
     np.testing.assert_allclose((total / N**2).numpy(), ref.detach().numpy(), rtol=2e-4, atol=1e-7)
+
+
+@pytest.mark.parametrize("min_d", ["8", "1"])      # 8: the pair on the vector path, the DAG on MFMA
+def test_rff_matrix_core_matches_oracle_and_vector(monkeypatch, min_d):
+    """Fast MMD (random Fourier features) on the exact-fp32 matrix cores vs the fp64
+    oracle and vs the vector kernels, on a 10-variable DAG (padded D = 12) and a pair."""
+    H = 16
+    g = DirectedGraph()
+    for k in range(9):
+        g.add("V%d" % k, "V%d" % (k + 1))
+    for prog, d in ((program_for_dag(g, H), 10), (program_for_pair(H), 2)):
+        N = 350
+        datas = [_data(d, N, s) for s in range(3)]
+        keys = [model_key(11, "rff", r) for r in range(3)]
+        kw = dict(learning_rate=0.01, init_std=0.05, use_fast_mmd=True, nb_vectors=30)
+        ref = ReferenceTrainer([prog] * 3, datas, keys, H, **kw)
+        ref_scores = ref.run(6, 4)
+        monkeypatch.setenv("CGNN_RFF_MFMA_MIN_D", min_d)
+        a = DeviceTrainer([prog] * 3, datas, keys, H, "cuda:0", record_history=6, **kw)
+        sa = a.run(6, 4)
+        monkeypatch.setenv("CGNN_RFF_VALU", "1")
+        b = DeviceTrainer([prog] * 3, datas, keys, H, "cuda:0", record_history=6, **kw)
+        sb = b.run(6, 4)
+        monkeypatch.delenv("CGNN_RFF_VALU")
+        np.testing.assert_allclose(a.history(), np.array(ref.loss_history), rtol=3e-3, atol=1e-5)
+        np.testing.assert_allclose(sa, ref_scores, rtol=3e-3, atol=1e-5)
+        np.testing.assert_allclose(sa, sb, rtol=1e-4, atol=1e-6)
