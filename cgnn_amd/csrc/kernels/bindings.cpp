@@ -28,7 +28,7 @@ int cgnn_launch_mmd_rows(int, int, const float*, const float*, float*, float*, i
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
                               const int*, int, int, hipStream_t);
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
-                        const uint32_t*, const int*, int, int, int, int, int, hipStream_t);
+                        const uint32_t*, const int*, int, int, int, int, int, hipStream_t, int);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
                         const float*, int, int, int, int, int, int, int, float*, hipStream_t);
 int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
@@ -161,12 +161,14 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("gen_fwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t data, uint64_t xhat, uint64_t noise,
                       int NS, uint64_t xnorm, uint64_t keys, uint64_t step, int off, int N, int D, int H, int R,
-                      uint64_t st) {
+                      uint64_t st, int row0) {
     chk(cgnn_launch_gen_fwd(Pt<const int>(prog), ps, Pt<const float>(params), P, Pt<const float>(data),
                             Pt<float>(xhat), Pt<float>(noise), NS, Pt<float>(xnorm), Pt<const uint32_t>(keys),
                             Pt<const int>(step),
-                            off, N, D, H, R, S(st)), "gen_fwd");
-  });
+                            off, N, D, H, R, S(st), row0), "gen_fwd");
+  }, py::arg("prog"), py::arg("ps"), py::arg("params"), py::arg("P"), py::arg("data"), py::arg("xhat"),
+     py::arg("noise"), py::arg("NS"), py::arg("xnorm"), py::arg("keys"), py::arg("step"), py::arg("off"),
+     py::arg("N"), py::arg("D"), py::arg("H"), py::arg("R"), py::arg("st"), py::arg("row0") = 0);
   m.def("gen_bwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t xhat, uint64_t noise, int NS,
                       uint64_t gradp, int nch, int R, int N, int D, int Dt, int H, int max_in, uint64_t gpart,
                       uint64_t st) {

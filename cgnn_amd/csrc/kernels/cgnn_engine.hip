@@ -26,7 +26,7 @@ int cgnn_mmd_mfma_row_blocks(int);
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
                               const int*, int, int, hipStream_t);
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
-                        const uint32_t*, const int*, int, int, int, int, int, hipStream_t);
+                        const uint32_t*, const int*, int, int, int, int, int, hipStream_t, int);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
                         const float*, int, int, int, int, int, int, int, float*, hipStream_t);
 int cgnn_gen_bwd_blocks(int);
@@ -147,7 +147,7 @@ class Engine {
   void enqueue_train_step(int off, bool record_hist) {
     const float inv = loss_scale();
     check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
-                              b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
+                              b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_, 0), "gen_fwd");
     enqueue_loss(off, true, record_hist);
     // the training loss is only observable through the recorded history
     if (record_hist)
@@ -163,7 +163,7 @@ class Engine {
   void enqueue_eval_step(int off) {
     const float inv = loss_scale();
     check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
-                              b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_), "gen_fwd");
+                              b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_, 0), "gen_fwd");
     enqueue_loss(off, false);
     check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 1,
                                     nullptr, 0, b_.step, off, c_.R, st_), "finalize(eval)");

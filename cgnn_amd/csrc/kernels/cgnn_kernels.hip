@@ -219,7 +219,9 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
     const int* __restrict__ prog, int prog_stride, const float* __restrict__ params, int P,
     const float* __restrict__ data, float* __restrict__ xhat, float* __restrict__ noise, int NS,
     float* __restrict__ xnorm, const uint32_t* __restrict__ keys, const int* __restrict__ step_base,
-    int step_off, int N, int D, int Hrt) {
+    int step_off, int N, int D, int Hrt, int row0) {
+  // row0: global index of sample 0 (a sample-sharded job keys every noise draw by the
+  // GLOBAL sample, so the generated samples do not depend on the rank count)
   extern __shared__ __attribute__((aligned(16))) float s_x[];   // [D][blockDim], then program
   const int r = blockIdx.y;
   const int t = threadIdx.x, B = blockDim.x;
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
     const float* b1 = W1 + (size_t)nin * Hh;
     const float* W2 = b1 + Hh;
     const float b2 = W2[Hh];
-    const float e = rng_normal(k0, k1, (uint32_t)n, (uint32_t)var, step, RNG_NODE_NOISE);
+    const float e = rng_normal(k0, k1, (uint32_t)(row0 + n), (uint32_t)var, step, RNG_NODE_NOISE);
     if (valid) nz[(size_t)var * N + n] = e;
     if (H > 0) {
       float pre[H > 0 ? H : 1];
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
       }
       for (int c = 0; c < ncf; ++c) {
         const int cid = uni(s_prog + cfoff + c);
-        const float ec = rng_normal(k0, k1, (uint32_t)n, (uint32_t)cid, step, RNG_CONF_NOISE);
+        const float ec = rng_normal(k0, k1, (uint32_t)(row0 + n), (uint32_t)cid, step, RNG_CONF_NOISE);
         if (valid) nz[(size_t)(D + cid) * N + n] = ec;
 #pragma unroll
         for (int q = 0; q < H; ++q) pre[q] = fmaf(W1[(npar + 1 + c) * H + q], ec, pre[q]);
@@ -280,14 +282,16 @@ __global__ __launch_bounds__(256) void gen_fwd_kernel(
       for (int c = 0; c < ncf; ++c) {
         const int cid = uni(s_prog + cfoff + c);
         if (valid)
-          nz[(size_t)(D + cid) * N + n] = rng_normal(k0, k1, (uint32_t)n, (uint32_t)cid, step, RNG_CONF_NOISE);
+          nz[(size_t)(D + cid) * N + n] = rng_normal(k0, k1, (uint32_t)(row0 + n), (uint32_t)cid, step,
+                                                     RNG_CONF_NOISE);
       }
       for (int q = 0; q < Hh; ++q) {
         float a = fmaf(W1[npar * Hh + q], e, b1[q]);
         for (int j = 0; j < npar; ++j) a = fmaf(W1[j * Hh + q], s_x[uni(s_prog + paroff + j) * B + t], a);
         for (int c = 0; c < ncf; ++c)
           a = fmaf(W1[(npar + 1 + c) * Hh + q],
-                   rng_normal(k0, k1, (uint32_t)n, (uint32_t)uni(s_prog + cfoff + c), step, RNG_CONF_NOISE), a);
+                   rng_normal(k0, k1, (uint32_t)(row0 + n), (uint32_t)uni(s_prog + cfoff + c), step, RNG_CONF_NOISE),
+                   a);
         out = fmaf(W2[q], fmaxf(a, 0.f), out);
       }
       s_x[var * B + t] = out;
@@ -628,18 +632,18 @@ extern "C" int cgnn_gen_supported_h(int H) {
 extern "C" int cgnn_launch_gen_fwd(const int* prog, int prog_stride, const float* params, int P,
                                    const float* data, float* xhat, float* noise, int NS, float* xnorm,
                                    const uint32_t* keys, const int* step_base, int step_off, int N,
-                                   int D, int H, int R, hipStream_t st) {
+                                   int D, int H, int R, hipStream_t st, int row0) {
   dim3 grid((N + 255) / 256, R), block(256);
   const size_t lds = sizeof(float) * (size_t)D * 256 + sizeof(int) * (size_t)prog_stride;
   if (lds > 160 * 1024) return -2;
   switch (H) {
-#define CASE_H(h) case h: allow_lds(gen_fwd_kernel<h>, lds); hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, lds, st, prog, prog_stride, params, P, data, xhat, noise, NS, xnorm, keys, step_base, step_off, N, D, H); break;
+#define CASE_H(h) case h: allow_lds(gen_fwd_kernel<h>, lds); hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, lds, st, prog, prog_stride, params, P, data, xhat, noise, NS, xnorm, keys, step_base, step_off, N, D, H, row0); break;
     CGNN_H_LIST(CASE_H)
 #undef CASE_H
     default:
       allow_lds(gen_fwd_kernel<0>, lds);
       hipLaunchKernelGGL((gen_fwd_kernel<0>), grid, block, lds, st, prog, prog_stride, params, P, data,
-                         xhat, noise, NS, xnorm, keys, step_base, step_off, N, D, H);
+                         xhat, noise, NS, xnorm, keys, step_base, step_off, N, D, H, row0);
   }
   return (int)hipGetLastError();
 }

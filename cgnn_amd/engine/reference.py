@@ -91,9 +91,11 @@ class ReferenceTrainer:
         self.opt_step = 0
 
     # --------------------------------------------------------------- pieces
+    row0 = 0           # global index of sample 0 (sample-sharded training, engine/sharded.py)
+
     def noise(self, r, a_ids, b, purpose, N):
         k0, k1 = self.keys[r]
-        n = np.arange(N, dtype=np.uint32)
+        n = np.arange(N, dtype=np.uint32) + np.uint32(self.row0)
         return torch.as_tensor(philox.normal(k0, k1, n, b, self.rng_step, purpose, dtype=np.float64),
                                dtype=self.dtype)
 

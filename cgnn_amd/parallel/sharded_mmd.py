@@ -48,27 +48,30 @@ def _feature_major(x: torch.Tensor, D: int) -> torch.Tensor:
     return out
 
 
-def _row_partials_dense(p_loc, t_loc, P, T):
+def _row_partials_dense(p_loc, t_loc, P, T, chunk: int = 1024):
     """(loss partial, gradient·N²/4) of rows p_loc / t_loc against all columns
-    (CPU / oracle path).  Shapes [n, d] and [N, d]."""
+    (CPU / oracle path).  Shapes [n, d] and [N, d]; rows in chunks (memory O(chunk N))."""
     X = torch.cat([P, T], 0)
     N = P.shape[0]
     s = torch.cat([X.new_ones(N), -X.new_ones(N)])
     lw = torch.cat([X.new_ones(N), X.new_full((N,), -2.0)])
-    d2 = torch.cdist(p_loc, X).pow(2)
-    d2t = torch.cdist(t_loc, T).pow(2)
-    E = torch.zeros_like(d2)
-    W = torch.zeros_like(d2)
-    Lt = p_loc.new_zeros(())
-    for g in GAMMAS:
-        e = torch.exp(-g * d2)
-        E += e
-        W += g * e
-        Lt = Lt + torch.exp(-g * d2t).sum()
-    loss = (E * lw).sum() + Lt
-    Ws = W * s
-    grad = Ws @ X - p_loc * Ws.sum(1, keepdim=True)
-    return loss, grad
+    loss = p_loc.new_zeros(())
+    grads = []
+    for a in range(0, p_loc.shape[0], chunk):
+        pl, tl = p_loc[a:a + chunk], t_loc[a:a + chunk]
+        d2 = torch.cdist(pl, X).pow(2)
+        d2t = torch.cdist(tl, T).pow(2)
+        E = torch.zeros_like(d2)
+        W = torch.zeros_like(d2)
+        for g in GAMMAS:
+            e = torch.exp(-g * d2)
+            E += e
+            W += g * e
+            loss = loss + torch.exp(-g * d2t).sum()
+        loss = loss + (E * lw).sum()
+        Ws = W * s
+        grads.append(Ws @ X - pl * Ws.sum(1, keepdim=True))
+    return loss, torch.cat(grads, 0)
 
 
 def _valu_geometry(n_loc: int, N: int, R: int) -> Tuple[int, int, int]:

@@ -207,3 +207,22 @@ def test_rff_matrix_core_matches_oracle_and_vector(monkeypatch, min_d):
         np.testing.assert_allclose(a.history(), np.array(ref.loss_history), rtol=3e-3, atol=1e-5)
         np.testing.assert_allclose(sa, ref_scores, rtol=3e-3, atol=1e-5)
         np.testing.assert_allclose(sa, sb, rtol=1e-4, atol=1e-6)
+
+
+def test_sample_sharded_trainer_gpu_matches_oracle_and_engine():
+    """The long-N trainer (engine/sharded.py) on the HIP kernels, one rank: equals the
+    fp64 oracle and the hipGraph engine (DeviceTrainer) on the same job."""
+    from cgnn_amd.engine.sharded import SampleShardedTrainer
+    H = 16
+    g = DirectedGraph()
+    for k in range(9):
+        g.add("V%d" % k, "V%d" % (k + 1))
+    for prog, d in ((program_for_pair(H), 2), (program_for_dag(g, H), 10)):
+        N = 512
+        data = _data(d, N, 4)
+        key = [model_key(9, "long", 0)]
+        ref = ReferenceTrainer([prog], [data], key, H).run(5, 3)
+        sh = SampleShardedTrainer([prog], [data], key, H, "cuda:0", N).run(5, 3)
+        eng = DeviceTrainer([prog], [data], key, H, "cuda:0").run(5, 3)
+        np.testing.assert_allclose(sh, ref, rtol=3e-3, atol=1e-5)
+        np.testing.assert_allclose(sh, eng, rtol=1e-4, atol=1e-6)
