@@ -61,6 +61,9 @@ def main():
                     help="framework locality pass at setup (label-propagation clusters + Cuthill-McKee)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: gloo ranks on the PyTorch path (tests the script's distributed logic only)")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal: every rank on cuda:0 with gloo collectives (exercises the multi-rank "
+                         "HIP path on a one-GPU box; timings are not a scaling measurement)")
     a = ap.parse_args()
     if a.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -78,16 +81,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         sys.exit("bench.py: --gpus %d but the launcher started %d ranks" % (a.gpus, world))
-    if cuda and torch.cuda.device_count() < world:
+    shared = cuda and a.shared_gpu
+    if cuda and not shared and torch.cuda.device_count() < world:
         sys.exit("bench.py: --gpus %d but only %d GPUs are visible" % (world, torch.cuda.device_count()))
     if world > 1:
-        pdist.init_process_group("nccl" if cuda else "gloo")
+        pdist.init_process_group("nccl" if (cuda and not shared) else "gloo")
         if pdist.world_size() != world:
             sys.exit("bench.py: process group has %d ranks, expected %d" % (pdist.world_size(), world))
     rank = pdist.rank()
     local = pdist.local_rank()
     if cuda:
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(0 if shared else local)
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
@@ -145,6 +149,7 @@ def main():
             "data": "synthetic graph of the %s shape (%d nodes, %d undirected edges, %d features, "
                     "%d classes; planted communities; %s node ids), random-init weights"
                     % (a.dataset, n, m, F, C, a.id_order),
+            "shared_gpu_rehearsal": bool(shared),
             "config": {"model": "GCN-2layer-hidden%d" % a.hidden, "global_batch": n_nodes,
                        "seq_len": None, "parallelism": "graph-rowpart%d" % world,
                        "dataset": a.dataset, "nnz_with_self_loops": nnz, "dropout": a.dropout,

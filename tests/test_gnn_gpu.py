@@ -121,8 +121,16 @@ def test_gcn_steps_match_cpu(name, fused):
         cpu.train_step()
         gpu.train_step()
     a, b = cpu.evaluate(), gpu.evaluate()
-    assert abs(a["train_loss"] - b["train_loss"]) < 0.05 * max(a["train_loss"], 1e-3) + 1e-3
-    assert abs(a["val_acc"] - b["val_acc"]) < 0.05
+    # the CPU path is the fp32 reference of the same bf16-stored arithmetic with the same
+    # dropout masks: after 3 Adam steps only summation order separates the two
+    dp = (gpu.params.cpu() - cpu.params).abs().max().item()
+    print("gcn %s fused=%s: loss cpu %.6f gpu %.6f, val_acc %.4f / %.4f, max |dparam| %.2e"
+          % (name, fused, a["train_loss"], b["train_loss"], a["val_acc"], b["val_acc"], dp))
+    assert abs(a["train_loss"] - b["train_loss"]) < 5e-3 * max(a["train_loss"], 1e-3)
+    assert abs(a["val_acc"] - b["val_acc"]) < 0.01
+    # Adam moves each weight by <= lr = 0.01 per step; a wrong gradient sign or a
+    # dropped term shows up as a difference of order lr
+    assert dp < 2e-3, dp
 
 
 def test_gcn_learns_products_shape_small():
