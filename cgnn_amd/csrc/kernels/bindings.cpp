@@ -81,7 +81,7 @@ int gnn_launch_dense_bwd(const void*, const float*, const void*, void*, int, int
                          hipStream_t);
 int gnn_launch_lin_fwd(const void*, int, int, const void*, int, int, const float*, int, const float*, void*, int,
                        int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, const int*, const float*,
-                       const int*, void*, hipStream_t);
+                       const int*, void*, float*, int, int, hipStream_t);
 int gnn_launch_lin_bwd_data(const void*, int, const void*, int, float, int, const float*, int, int, void*, int,
                             void*, int, const float*, int, int, void*, hipStream_t);
 long gnn_lin_fwd_image_bytes(int, int, int);
@@ -299,15 +299,17 @@ PYBIND11_MODULE(_hip, m) {
   // generic fused dense layers (gnn_linear.hip); return codes: 0 ok, -1 no variant, -3 bad shape
   m.def("gnn_lin_fwd", [](uint64_t x1, int ld1, int K1, uint64_t x2, int ld2, int K2, uint64_t w, int N, uint64_t b,
                           uint64_t y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step,
-                          uint32_t row0, uint64_t stepp, uint64_t rscale, uint64_t st, uint64_t idx1, uint64_t wimg) {
+                          uint32_t row0, uint64_t stepp, uint64_t rscale, uint64_t st, uint64_t idx1, uint64_t wimg,
+                          uint64_t yf, int nsplit, int tk) {
     return gnn_launch_lin_fwd(Pt<const void>(x1), ld1, K1, Pt<const void>(x2), ld2, K2, Pt<const float>(w), N,
                               Pt<const float>(b), Pt<void>(y), ldy, n, relu, p, k0, k1, step, row0,
                               Pt<const int>(stepp), Pt<const float>(rscale), Pt<const int>(idx1), Pt<void>(wimg),
-                              S(st));
+                              Pt<float>(yf), nsplit, tk, S(st));
   }, py::arg("x1"), py::arg("ld1"), py::arg("K1"), py::arg("x2"), py::arg("ld2"), py::arg("K2"), py::arg("w"),
      py::arg("N"), py::arg("b"), py::arg("y"), py::arg("ldy"), py::arg("n"), py::arg("relu"), py::arg("p"),
      py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("stepp"), py::arg("rscale"),
-     py::arg("st"), py::arg("idx1") = 0, py::arg("wimg") = 0);
+     py::arg("st"), py::arg("idx1") = 0, py::arg("wimg") = 0, py::arg("yf") = 0, py::arg("nsplit") = 0,
+     py::arg("tk") = 1);
   m.def("gnn_lin_fwd_image_bytes", &gnn_lin_fwd_image_bytes);
   m.def("gnn_lin_bwd_image_bytes", &gnn_lin_bwd_image_bytes);
   m.def("gnn_lin_bwd_data", [](uint64_t dy, int lddy, uint64_t ym, int ldym, float mscale, int N, uint64_t w, int K1,

@@ -141,9 +141,12 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     const float* __restrict__ W, int N, const float* __restrict__ bias, uint16_t* __restrict__ Y, int ldy,
     int n, int ncols, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
     uint32_t row0, const int* __restrict__ stepp, const float* __restrict__ rscale, const int* __restrict__ idx1,
-    const uint16_t* __restrict__ wimg) {
+    const uint16_t* __restrict__ wimg, float* __restrict__ Yf, int nsplit, int tk) {
   // wimg: the bf16 LDS image of every column slab ([slabs][ncols][WS], lin_prep_fwd_kernel):
-  // one vectorised copy per block instead of converting / transposing the fp32 weights
+  // one vectorised copy per block instead of converting / transposing the fp32 weights.
+  // Yf (optional): columns c >= nsplit (nsplit % 4 == 0) are written EXACTLY, as fp32
+  // planes of tk columns -- Yf[(c - nsplit) / tk][row][(c - nsplit) % tk] -- instead of
+  // bf16 into Y (GAT: the attention scores s_src / s_dst folded into the projection)
   if (stepp) step = (uint32_t)*stepp;
   constexpr int KP = KS * 16;
   constexpr int WS = KP + 8;                     // padded row stride of the W^T slab
@@ -203,8 +206,15 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = cg + 8 * g + 4 * h;
-        if (c < ldy)
+        if (Yf && c >= nsplit) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int t = c + e - nsplit;
+            if (c + e < N) Yf[(size_t)(t / tk) * n * tk + (size_t)row * tk + t % tk] = v[4 * g + e];
+          }
+        } else if (c < ldy) {
           *reinterpret_cast<uint2*>(Y + (size_t)row * ldy + c) = pack4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+        }
       }
     }
   }
@@ -480,7 +490,7 @@ template <int KS>
 static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const float* W, int N,
                       const float* bias, uint16_t* Y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1,
                       uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
-                      const int* idx1, uint16_t* wimg, hipStream_t st) {
+                      const int* idx1, uint16_t* wimg, float* Yf, int nsplit, int tk, hipStream_t st) {
   constexpr int KP = KS * 16;
   const int ncols = slab_cols(std::max(N, ldy), KP);
   const size_t lds = (size_t)ncols * (KP + 8) * 2 + (size_t)ncols * 4;
@@ -495,24 +505,25 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
   const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
   hipLaunchKernelGGL((lin_fwd_kernel<KS>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
                      x1, ld1, K1, x2, ld2, K2, W, N, bias, Y, ldy, n, ncols, relu, p, k0, k1, step, thr8, row0,
-                     stepp, rscale, idx1, wimg);
+                     stepp, rscale, idx1, wimg, Yf, nsplit, tk);
   return (int)hipGetLastError();
 }
 
 extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2, const float* W,
                                   int N, const float* bias, void* Y, int ldy, int n, int relu, float p, uint32_t k0,
                                   uint32_t k1, uint32_t step, uint32_t row0, const int* stepp, const float* rscale,
-                                  const int* idx1, void* wimg, hipStream_t st) {
+                                  const int* idx1, void* wimg, float* Yf, int nsplit, int tk, hipStream_t st) {
   if (n <= 0) return 0;
-  if ((x2 && K1 % 8) || ld1 % 8 || (x2 && (ld2 % 8)) || ldy % 8 || K1 > ld1 || (x2 && K2 > ld2) || N > ldy)
+  if ((x2 && K1 % 8) || ld1 % 8 || (x2 && (ld2 % 8)) || ldy % 8 || K1 > ld1 || (x2 && K2 > ld2))
     return -3;
+  if (Yf ? (nsplit % 4 || nsplit > ldy || nsplit > N || tk <= 0 || (N - nsplit) % tk) : N > ldy) return -3;
   if (!x2) K2 = 0;
   const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
   const int ks = pick_ks(K1 + K2);
   auto a = (const uint16_t*)x1;
   auto b = (const uint16_t*)x2;
   auto y = (uint16_t*)Y;
-#define LF(c) if (ks == c) return fwd_launch<c>(a, ld1, K1, b, ld2, K2, W, N, bias, y, ldy, n, relu, p, k0, k1, step, thr8, row0, stepp, rscale, idx1, (uint16_t*)wimg, st);
+#define LF(c) if (ks == c) return fwd_launch<c>(a, ld1, K1, b, ld2, K2, W, N, bias, y, ldy, n, relu, p, k0, k1, step, thr8, row0, stepp, rscale, idx1, (uint16_t*)wimg, Yf, nsplit, tk, st);
   LF(4) LF(8) LF(16) LF(24) LF(32)
 #undef LF
   return -1;
