@@ -71,6 +71,15 @@ int gnn_launch_gat_bwd_row(const int*, const int*, const void*, const float*, co
                            const float*, const float*, float*, float*, float*, int, int, int, int, hipStream_t);
 int gnn_launch_gat_bwd_col(const int*, const int*, const int*, const float*, const float*, const void*, float*,
                            float*, int, int, int, int, hipStream_t);
+int gnn_launch_gat_act_fwd(const float*, const float*, void*, int, long, int, float, uint32_t, uint32_t, uint32_t,
+                           const int*, uint32_t, hipStream_t);
+int gnn_gat_act_bwd_blocks();
+int gnn_launch_gat_act_bwd(const void*, int, const float*, const float*, float*, void*, float*, float*, long, int,
+                           float, uint32_t, uint32_t, uint32_t, const int*, uint32_t, hipStream_t);
+int gnn_gat_row_ce_waves();
+int gnn_launch_gat_row_ce(const float*, int, const float*, int, const int*, const uint8_t*, float, float*, void*,
+                          float*, float*, float*, float*, long, hipStream_t);
+int gnn_launch_gat_pack_grad(const float*, const float*, const float*, int, int, void*, int, long, hipStream_t);
 int gnn_fused_bwd_blocks(int);
 int gnn_fused_bwd_width(int);
 int gnn_fused_bwd_supported(int, int, int);
@@ -284,6 +293,33 @@ PYBIND11_MODULE(_hip, m) {
                                Fh, wbf, S(st)), "gnn_gat_bwd_col");
   }, py::arg("rpt"), py::arg("colt"), py::arg("perm"), py::arg("ae"), py::arg("de"), py::arg("dout"),
      py::arg("dwh"), py::arg("dss"), py::arg("n"), py::arg("K"), py::arg("Fh"), py::arg("st"), py::arg("wbf") = 0);
+  // dense-side kernels of the fused GAT epoch (gnn_gat.hip)
+  m.def("gnn_gat_act_fwd", [](uint64_t out, uint64_t b, uint64_t h, int ldh, long n, int F, float p, uint32_t k0,
+                              uint32_t k1, uint32_t step, uint64_t stepp, uint32_t row0, uint64_t st) {
+    chk(gnn_launch_gat_act_fwd(Pt<const float>(out), Pt<const float>(b), Pt<void>(h), ldh, n, F, p, k0, k1, step,
+                               Pt<const int>(stepp), row0, S(st)), "gnn_gat_act_fwd");
+  });
+  m.def("gnn_gat_act_bwd_blocks", &gnn_gat_act_bwd_blocks);
+  m.def("gnn_gat_act_bwd", [](uint64_t dh, int ldh, uint64_t out, uint64_t b, uint64_t dout, uint64_t doutb,
+                              uint64_t bpart, uint64_t db, long n, int F, float p, uint32_t k0, uint32_t k1,
+                              uint32_t step, uint64_t stepp, uint32_t row0, uint64_t st) {
+    chk(gnn_launch_gat_act_bwd(Pt<const void>(dh), ldh, Pt<const float>(out), Pt<const float>(b), Pt<float>(dout),
+                               Pt<void>(doutb), Pt<float>(bpart), Pt<float>(db), n, F, p, k0, k1, step,
+                               Pt<const int>(stepp), row0, S(st)), "gnn_gat_act_bwd");
+  });
+  m.def("gnn_gat_row_ce_waves", &gnn_gat_row_ce_waves);
+  m.def("gnn_gat_row_ce", [](uint64_t z, int ldz, uint64_t b, int C, uint64_t y, uint64_t mask, float inv_count,
+                             uint64_t dz, uint64_t dzb, uint64_t spart, uint64_t bpart, uint64_t stats, uint64_t db,
+                             long n, uint64_t st) {
+    chk(gnn_launch_gat_row_ce(Pt<const float>(z), ldz, Pt<const float>(b), C, Pt<const int>(y),
+                              Pt<const uint8_t>(mask), inv_count, Pt<float>(dz), Pt<void>(dzb), Pt<float>(spart),
+                              Pt<float>(bpart), Pt<float>(stats), Pt<float>(db), n, S(st)), "gnn_gat_row_ce");
+  });
+  m.def("gnn_gat_pack_grad", [](uint64_t dwh, uint64_t dss, uint64_t dsd, int HF, int K, uint64_t dy, int ldy,
+                                long n, uint64_t st) {
+    chk(gnn_launch_gat_pack_grad(Pt<const float>(dwh), Pt<const float>(dss), Pt<const float>(dsd), HF, K,
+                                 Pt<void>(dy), ldy, n, S(st)), "gnn_gat_pack_grad");
+  });
   m.def("gnn_fused_bwd_blocks", &gnn_fused_bwd_blocks);
   m.def("gnn_fused_bwd_width", &gnn_fused_bwd_width);
   m.def("gnn_fused_bwd_supported", &gnn_fused_bwd_supported);

@@ -234,10 +234,27 @@ class GAT(torch.nn.Module):
         return self.l2(h, g, halo)[:, :self.C]
 
 
-class GATTrainer:
-    """Full-graph GAT node classification (Adam, cross-entropy on the train split)."""
+def _use_fused(fused, dev, F, heads, head_dim, n_classes):
+    """Default: the fused HIP epoch (gat_fused.py) on a GPU when its kernels cover the
+    shape, the autograd model otherwise; ``fused=True`` on a CPU runs its fp32
+    reference branches (tests)."""
+    from .gat_fused import FusedGAT
+    ok = FusedGAT.supported(F, heads, head_dim, n_classes)
+    if fused is None:
+        return ok and dev.type == "cuda"
+    if fused and not ok:
+        raise ValueError("fused GAT: no kernel variant for F=%d heads=%d head_dim=%d classes=%d"
+                         % (F, heads, head_dim, n_classes))
+    return bool(fused)
 
-    def __init__(self, gd: GraphData, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True):
+
+class GATTrainer:
+    """Full-graph GAT node classification (Adam, cross-entropy on the train split).
+    ``fused`` (default: on a GPU): the whole epoch on HIP kernels (``gat_fused``);
+    otherwise the autograd model over the HIP aggregation."""
+
+    def __init__(self, gd: GraphData, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True,
+                 fused: Optional[bool] = None):
         self.gd = gd
         self.dev = gd.rowptr.device
         x = gd.x.float()
@@ -245,11 +262,19 @@ class GATTrainer:
             x = (x - x.mean(0)) / x.std(0).clamp_min(1e-6)
         self.x = x
         self.g = GraphCSR(gd.rowptr, gd.col, gd.n)
+        self.tr = gd.mask == 1
+        self.fused = None
+        if _use_fused(fused, self.dev, x.shape[1], heads, head_dim, gd.n_classes):
+            from .gat_fused import FusedGAT
+            self.fused = FusedGAT(x, gd.y, gd.mask, gd.n_classes, self.g, heads, head_dim, dropout, lr, seed)
+            self.model = self.opt = None
+            return
         self.model = GAT(x.shape[1], gd.n_classes, heads, head_dim, dropout, seed).to(self.dev)
         self.opt = torch.optim.Adam(self.model.parameters(), lr=lr, fused=self.dev.type == "cuda")
-        self.tr = gd.mask == 1
 
     def train_step(self):
+        if self.fused is not None:
+            return self.fused.train_step()
         self.model.train()
         out = self.model(self.x, self.g)
         loss = torch.nn.functional.cross_entropy(out[self.tr], self.gd.y[self.tr].long())
@@ -260,6 +285,14 @@ class GATTrainer:
 
     @torch.no_grad()
     def evaluate(self):
+        if self.fused is not None:
+            c = self.fused.evaluate_counts().cpu().double().numpy()
+            m = self.gd.mask
+            res = {"train_loss": float(c[0]) / self.fused.n_train}
+            for i, name in ((1, "train_acc"), (2, "val_acc"), (3, "test_acc")):
+                cnt = int((m == i).sum())
+                res[name] = float(c[i]) / cnt if cnt else float("nan")
+            return res
         self.model.eval()
         pred = self.model(self.x, self.g).argmax(1)
         res = {}
@@ -290,7 +323,7 @@ class ShardedGATTrainer:
     """
 
     def __init__(self, shard, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True,
-                 bucket_mb: float = 16.0, emulate=None):
+                 bucket_mb: float = 16.0, emulate=None, fused: Optional[bool] = None):
         import torch.distributed as dist
         from ..parallel import dist as pdist
         from ..parallel.ddp import GradBucketer
@@ -334,9 +367,18 @@ class ShardedGATTrainer:
         if distributed:
             dist.all_reduce(n_train)
         self.n_train = float(n_train.item()) if emulate is None else float(shard.n_train_global or n_train.item())
+        self.ddp = None
+        self.fused = None
+        if _use_fused(fused, self.dev, x.shape[1], heads, head_dim, shard.n_classes):
+            # the whole epoch on HIP kernels; one all-reduce of the flat gradient buffer
+            from .gat_fused import FusedGAT
+            self.fused = FusedGAT(self.x, self.y, self.mask, shard.n_classes, self.g, heads, head_dim, dropout, lr,
+                                  seed, halo=self.halo, row0=r0, n_train=int(self.n_train), distributed=distributed)
+            self.model = self.opt = None
+            self.epoch = 0
+            return
         self.model = GAT(x.shape[1], shard.n_classes, heads, head_dim, dropout, seed).to(self.dev)
         self.opt = torch.optim.Adam(self.model.parameters(), lr=lr, fused=self.dev.type == "cuda")
-        self.ddp = None
         if distributed:
             self.ddp = GradBucketer(list(self.model.parameters()), bucket_mb)
             self.ddp.broadcast_parameters(0)
@@ -346,13 +388,16 @@ class ShardedGATTrainer:
         """Rows / bytes this rank receives and sends per layer-1 exchange (Wh bf16 + fp32 scores)."""
         if self.halo is None:
             return {"recv_rows": 0, "send_rows": 0}
-        l1 = self.model.l1
+        l1 = self.fused.layers[0] if self.fused is not None else self.model.l1
         w = 2 * l1.K * l1.Fh + 4 * l1.K
         rb, sb = self.halo.bytes_per_exchange(w)
         return {"recv_rows": self.halo.n_recv, "send_rows": self.halo.n_send, "local_rows": self.halo.nloc,
                 "layer1_recv_bytes": rb, "layer1_send_bytes": sb}
 
     def train_step(self):
+        if self.fused is not None:
+            self.epoch += 1
+            return self.fused.train_step()
         self.model.train()
         out = self.model(self.x, self.g, self.halo)
         # sum over this rank's train rows scaled so that the rank-average of the
@@ -369,13 +414,19 @@ class ShardedGATTrainer:
     @torch.no_grad()
     def evaluate(self):
         import torch.distributed as dist
-        self.model.eval()
-        pred = self.model(self.x, self.g, self.halo).argmax(1)
         cnt = torch.zeros(6, dtype=torch.float64, device=self.dev)
-        for i, k in enumerate((1, 2, 3)):
-            m = self.mask == k
-            cnt[2 * i] = float((pred[m] == self.y[m]).sum())
-            cnt[2 * i + 1] = float(m.sum())
+        if self.fused is not None:
+            c = self.fused.evaluate_counts().double()
+            for i, k in enumerate((1, 2, 3)):
+                cnt[2 * i] = c[k]
+                cnt[2 * i + 1] = float((self.mask == k).sum())
+        else:
+            self.model.eval()
+            pred = self.model(self.x, self.g, self.halo).argmax(1)
+            for i, k in enumerate((1, 2, 3)):
+                m = self.mask == k
+                cnt[2 * i] = float((pred[m] == self.y[m]).sum())
+                cnt[2 * i + 1] = float(m.sum())
         if self.world > 1 and self.emulate is None:
             dist.all_reduce(cnt)
         c = cnt.cpu().numpy()

@@ -1,0 +1,397 @@
+"""Fused GAT training epoch (GNN track, not in the reference): every dense op on
+hand-written HIP kernels, no autograd, no hipBLASLt, no ATen elementwise chain.
+
+Per layer (``gat.GATLayer`` semantics; the attention logits are linear in the
+input, so they fold into the projection ``Wc = [W | W a_src | W a_dst]``):
+
+  forward   [Wh | s_src | s_dst] = h Wc       lin_fwd (MFMA), Wh stored bf16 (the
+                                              edge-gathered operand), the scores as
+                                              exact fp32 planes (its ``tail`` output)
+            out, lse = GAT aggregation        gat_fwd (online softmax; sharded runs
+                                              first exchange [Wh | s_src] halo rows)
+            layer 1: h1 = bf16(dropout(elu(out + b1)))        gat_act_fwd
+            layer 2: loss, dlogits = CE(out + b2) (train rows) gat_row_ce
+  backward  dWh, ds_src, ds_dst               gat_bwd_row / gat_bwd_col (+ halo
+                                              reduce-back of the received rows)
+            dy = bf16([dWh | ds_src | ds_dst])                 gat_pack_grad
+            dWc = h^T dy                      lin_bwd_weight (split-K MFMA, fixed order)
+            dh = dy Wc^T                      lin_bwd_data (MFMA; layer 2 only)
+            dout1 = dh * mask * elu'(out1 + b1), db1           gat_act_bwd
+            dW, da_src, da_dst from dWc       (weight-sized tensors only)
+  update    gradients summed over ranks (one all-reduce of the flat buffer), Adam
+            on the flat fp32 parameter buffer (ops.adam_).
+
+Dropout is keyed by (seed, GLOBAL row, column, device step counter), so a
+sharded run draws exactly the masks of a one-GPU run; together with the
+rank-independent loss scale (1 / global train count) the model is the same for
+any rank count.  Every op has a CPU branch (the fp32 reference of the same
+bf16-stored arithmetic), so the sharded path is tested with gloo ranks on CPU.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from .. import native
+from ..utils.philox import model_key
+from . import ops
+from .linear import lin_bwd_data, lin_bwd_weight, lin_fwd
+
+
+def _st(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ru8(x):
+    return (x + 7) // 8 * 8
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else 0
+
+
+# ------------------------------------------------------------------ elementwise ops
+def act_fwd(out, bias, H, p, key, step, row0=0):
+    """H[:, :F] = bf16(dropout(elu(out + bias))), F = out.shape[1] (a multiple of 32)."""
+    n, F = out.shape
+    if out.is_cuda:
+        sv, sp = ops._step_args(step)
+        native.hip().gnn_gat_act_fwd(out.data_ptr(), bias.data_ptr(), H.data_ptr(), H.stride(0), n, F, float(p),
+                                     int(key[0]), int(key[1]), sv, sp, int(row0), _st(out))
+        return H
+    z = out.float() + bias.float()
+    e = torch.where(z > 0, z, torch.expm1(z))
+    if p > 0:
+        keep = ops.dropout_keep_mask(n, F, p, key, ops._step_value(step), row0)
+        e = torch.where(keep, e / (1 - p), torch.zeros_like(e))
+    H[:n, :F] = e.to(H.dtype)
+    return H
+
+
+_BPART = {}
+
+
+def _scratch(dev, shape):
+    key = (dev.type, dev.index, tuple(shape))
+    buf = _BPART.get(key)
+    if buf is None:
+        buf = _BPART[key] = torch.empty(shape, dtype=torch.float32, device=dev)
+    return buf
+
+
+def act_bwd(dH, out, bias, p, key, step, row0, dout, doutb, db):
+    """dout = dH * mask * elu'(out + bias) (fp32, plus a bf16 copy ``doutb``), db = colsum(dout)."""
+    n, F = out.shape
+    if out.is_cuda:
+        hip = native.hip()
+        bpart = _scratch(out.device, (hip.gnn_gat_act_bwd_blocks(), F))
+        sv, sp = ops._step_args(step)
+        hip.gnn_gat_act_bwd(dH.data_ptr(), dH.stride(0), out.data_ptr(), bias.data_ptr(), dout.data_ptr(),
+                            _ptr(doutb), bpart.data_ptr(), db.data_ptr(), n, F, float(p), int(key[0]), int(key[1]),
+                            sv, sp, int(row0), _st(out))
+        return dout
+    z = out.float() + bias.float()
+    d = dH[:n, :F].float() * torch.where(z > 0, torch.ones_like(z), torch.exp(z))
+    if p > 0:
+        keep = ops.dropout_keep_mask(n, F, p, key, ops._step_value(step), row0)
+        d = torch.where(keep, d / (1 - p), torch.zeros_like(d))
+    dout.copy_(d)
+    if doutb is not None:
+        doutb.copy_(d.to(torch.bfloat16))
+    db.copy_(d.sum(0))
+    return dout
+
+
+def row_ce(Z, bias, C, y, mask, inv_count, dZ=None, dZb=None, db=None):
+    """Cross-entropy of logits ``Z[:, :C] + bias`` on the train rows (mask == 1).
+    Returns [4] fp32 (sum of train NLL, correct train / valid / test); training
+    (``dZ`` given): dZ = (softmax - onehot) * inv_count on train rows, 0 elsewhere
+    (pad columns too), ``dZb`` its bf16 copy, ``db`` = colsum(dZ)."""
+    n, ldz = Z.shape
+    if Z.is_cuda:
+        hip = native.hip()
+        nw = hip.gnn_gat_row_ce_waves()
+        spart = _scratch(Z.device, (nw, 4))
+        bpart = _scratch(Z.device, (nw, C))
+        stats = torch.empty(4, dtype=torch.float32, device=Z.device)
+        hip.gnn_gat_row_ce(Z.data_ptr(), ldz, bias.data_ptr(), C, y.data_ptr(), mask.data_ptr(), float(inv_count),
+                           _ptr(dZ), _ptr(dZb), spart.data_ptr(), bpart.data_ptr(), stats.data_ptr(), _ptr(db), n,
+                           _st(Z))
+        return stats
+    logits = Z[:, :C].float() + bias[:C].float()
+    lse = torch.logsumexp(logits, 1)
+    yl = y.long()
+    zy = logits.gather(1, yl[:, None])[:, 0]
+    tr = mask == 1
+    pred = logits.argmax(1)
+    ok = pred == yl
+    stats = torch.stack([(lse - zy)[tr].sum(), ok[tr].sum().float(), ok[mask == 2].sum().float(),
+                         ok[mask == 3].sum().float()]).float()
+    if dZ is not None or dZb is not None:
+        d = torch.softmax(logits, 1)
+        d[torch.arange(n), yl] -= 1.0
+        d = torch.where(tr[:, None], d * inv_count, torch.zeros_like(d))
+        full = torch.zeros(n, ldz, dtype=torch.float32)
+        full[:, :C] = d
+        if dZ is not None:
+            dZ.copy_(full)
+        if dZb is not None:
+            dZb.copy_(full.to(torch.bfloat16))
+        if db is not None:
+            db[:C].copy_(d.sum(0))
+    return stats
+
+
+def pack_grad(dWh, ds_src, ds_dst, dy):
+    """dy[:, :HF + 2K] = bf16([dWh | ds_src | ds_dst]), zero pad columns."""
+    n, HF = dWh.shape
+    K = ds_src.shape[1]
+    if dWh.is_cuda:
+        native.hip().gnn_gat_pack_grad(dWh.data_ptr(), ds_src.data_ptr(), ds_dst.data_ptr(), HF, K, dy.data_ptr(),
+                                       dy.stride(0), n, _st(dWh))
+        return dy
+    dy.zero_()
+    dy[:n, :HF + 2 * K] = torch.cat([dWh.float(), ds_src.float(), ds_dst.float()], 1).to(dy.dtype)
+    return dy
+
+
+# ------------------------------------------------------------------ aggregation
+def _agg_fwd(Wh, s_src, s_dst, g, K, Fh):
+    n = g.n
+    if Wh.is_cuda:
+        out = torch.empty(n, K * Fh, dtype=torch.float32, device=Wh.device)
+        lse = torch.empty(n, K, dtype=torch.float32, device=Wh.device)
+        native.hip().gnn_gat_fwd(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(),
+                                 s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Wh),
+                                 int(Wh.dtype == torch.bfloat16))
+        return out, lse
+    from .gat import _gat_aggregate_torch
+    return _gat_aggregate_torch(Wh.float(), s_src, s_dst, g, K, Fh).float(), None
+
+
+def _agg_bwd(Wh, s_src, s_dst, out, lse, dout, doutb, g, K, Fh):
+    """(dWh [n_cols, K Fh] fp32, ds_src [n_cols, K], ds_dst [n, K])."""
+    n = g.n
+    if Wh.is_cuda:
+        hip = native.hip()
+        dev = Wh.device
+        alpha_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+        dsc_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+        ds_dst = torch.empty(n, K, dtype=torch.float32, device=dev)
+        wbf = int(Wh.dtype == torch.bfloat16)
+        hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(),
+                            out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(), dsc_e.data_ptr(),
+                            ds_dst.data_ptr(), n, K, Fh, _st(Wh), wbf)
+        rp_t, col_t, perm = g.transposed()
+        dWh = torch.empty(g.n_cols, K * Fh, dtype=torch.float32, device=dev)
+        ds_src = torch.empty(g.n_cols, K, dtype=torch.float32, device=dev)
+        hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
+                            dsc_e.data_ptr(), doutb.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh,
+                            _st(Wh), 1)
+        return dWh, ds_src, ds_dst
+    from .gat import _gat_aggregate_torch
+    with torch.enable_grad():
+        a = Wh.float().detach().requires_grad_()
+        b = s_src.detach().requires_grad_()
+        c = s_dst.detach().requires_grad_()
+        o = _gat_aggregate_torch(a, b, c, g, K, Fh)
+        return torch.autograd.grad(o, (a, b, c), dout)
+
+
+def wcat(W, a_src, a_dst, out):
+    """out = [W | W a_src | W a_dst] (per head: sum over the head's columns)."""
+    K, Fh = a_src.shape
+    Wk = W.view(-1, K, Fh)
+    torch.cat([W, (Wk * a_src).sum(-1), (Wk * a_dst).sum(-1)], 1, out=out)
+    return out
+
+
+def wcat_bwd(dWc, W, a_src, a_dst, gW, ga_src, ga_dst):
+    K, Fh = a_src.shape
+    KF = K * Fh
+    Wk = W.view(-1, K, Fh)
+    ds, dd = dWc[:, KF:KF + K, None], dWc[:, KF + K:KF + 2 * K, None]
+    gW.copy_(dWc[:, :KF] + (ds * a_src + dd * a_dst).reshape(-1, KF))
+    ga_src.copy_((Wk * ds).sum(0))
+    ga_dst.copy_((Wk * dd).sum(0))
+
+
+class _Layer:
+    pass
+
+
+class FusedGAT:
+    """The fused 2-layer GAT epoch over one rank's rows (the whole graph when
+    ``halo`` is None).  ``g``: GraphCSR over [own | received] source rows;
+    ``x``: fp32 [nloc, F] input features (already standardised); ``row0``: the
+    global id of the first own row (dropout keys); ``n_train``: GLOBAL train count.
+    Parameters are initialised exactly like ``gat.GAT(F, C, heads, head_dim, seed)``."""
+
+    def __init__(self, x, y, mask, n_classes, g, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0,
+                 halo=None, row0=0, n_train=None, distributed=False):
+        from .gat import GAT
+        dev = x.device
+        self.dev, self.g, self.halo = dev, g, halo
+        self.nloc, self.F = x.shape
+        self.C = int(n_classes)
+        self.p, self.lr = float(dropout), float(lr)
+        self.row0, self.distributed = int(row0), bool(distributed)
+        self.y = y.to(torch.int32).contiguous()
+        self.mask = mask.to(torch.uint8).contiguous()
+        if n_train is None:
+            n_train = int((self.mask == 1).sum())
+        self.n_train = max(int(n_train), 1)
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.xb = torch.zeros(self.nloc, _ru8(self.F), **bf)
+        self.xb[:, :self.F] = x.to(torch.bfloat16)
+        ref = GAT(self.F, self.C, heads, head_dim, dropout, seed)          # the init of the autograd model
+        mods = [ref.l1, ref.l2]
+        flat = torch.cat([t.detach().reshape(-1) for m in mods for t in (m.W, m.a_src, m.a_dst, m.bias)])
+        self.params = flat.to(dev)
+        self.grads = torch.zeros_like(self.params)
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.key = model_key(seed, "gat-dropout")
+        if self.distributed:
+            # replicas start from rank 0's parameters and dropout key
+            kt = torch.tensor([int(self.key[0]), int(self.key[1])], dtype=torch.int64, device=dev)
+            torch.distributed.broadcast(self.params, 0)
+            torch.distributed.broadcast(kt, 0)
+            self.key = (int(kt[0]), int(kt[1]))
+        off = 0
+        self.layers = []
+        kin = self.F
+        for m in mods:
+            L = _Layer()
+            L.K, L.Fh = m.K, m.Fh
+            L.KF = L.K * L.Fh
+            L.Kin = kin
+            views = []
+            for t in (m.W, m.a_src, m.a_dst, m.bias):
+                k = t.numel()
+                views.append((self.params[off:off + k].view(t.shape), self.grads[off:off + k].view(t.shape)))
+                off += k
+            (L.W, L.gW), (L.a_src, L.ga_src), (L.a_dst, L.ga_dst), (L.b, L.gb) = views
+            L.N = L.KF + 2 * L.K
+            L.Wc = torch.zeros(kin, L.N, dtype=torch.float32, device=dev)
+            L.dWc = torch.zeros_like(L.Wc)
+            L.db_scratch = torch.zeros(L.N, dtype=torch.float32, device=dev)
+            L.Wh = torch.zeros(self.nloc, L.KF, **bf)
+            L.s = torch.zeros(2, self.nloc, L.K, dtype=torch.float32, device=dev)
+            L.dy = torch.zeros(self.nloc, _ru8(L.N), **bf)
+            self.layers.append(L)
+            kin = L.KF
+        L1, L2 = self.layers
+        self.h1 = torch.zeros(self.nloc, L1.KF, **bf)
+        self.dh1 = torch.zeros(self.nloc, L1.KF, **bf)
+        self.dout1 = torch.zeros(self.nloc, L1.KF, dtype=torch.float32, device=dev)
+        self.dout1b = torch.zeros(self.nloc, L1.KF, **bf)
+        self.dout2 = torch.zeros(self.nloc, L2.KF, dtype=torch.float32, device=dev)
+        self.dout2b = torch.zeros(self.nloc, L2.KF, **bf)
+        self.epoch = 0
+        self.last_stats = None
+
+    @staticmethod
+    def supported(F, heads, head_dim, n_classes):
+        ow = _ru8(n_classes)
+        g1 = head_dim // 8
+        return (head_dim % 8 == 0 and (heads == 1 or (g1 & (g1 - 1)) == 0) and heads * head_dim <= 512
+                and (heads * head_dim) % 32 == 0 and ow <= 256 and F <= 512)
+
+    def _dropout_step(self):
+        return self.step_t if self.dev.type == "cuda" else int(self.step_t.item())
+
+    # ------------------------------------------------------------------ passes
+    def _project_aggregate(self, L, x, K1):
+        wcat(L.W, L.a_src, L.a_dst, L.Wc)
+        lin_fwd(x, L.Wc, None, K1=K1, out=L.Wh, tail=L.s, nsplit=L.KF, tk=L.K)
+        s_src, s_dst = L.s[0], L.s[1]
+        if self.halo is not None:
+            h = self.halo
+            buf = h.exchange(h.pack([L.Wh, s_src]))
+            Wh_ext, s_ext = h.unpack(buf, [(L.KF, torch.bfloat16), (L.K, torch.float32)])
+            del buf
+        else:
+            Wh_ext, s_ext = L.Wh, s_src
+        out, lse = _agg_fwd(Wh_ext, s_ext, s_dst, self.g, L.K, L.Fh)
+        L.saved = (Wh_ext, s_ext, s_dst, out, lse)
+        return out
+
+    def forward(self, train: bool):
+        L1, L2 = self.layers
+        p = self.p if train else 0.0
+        step = self._dropout_step()
+        out1 = self._project_aggregate(L1, self.xb, self.F)
+        act_fwd(out1, L1.b, self.h1, p, self.key, step, self.row0)
+        out2 = self._project_aggregate(L2, self.h1, L1.KF)
+        if train:
+            stats = row_ce(out2, L2.b, self.C, self.y, self.mask, 1.0 / self.n_train, dZ=self.dout2,
+                           dZb=self.dout2b, db=L2.gb)
+        else:
+            stats = row_ce(out2, L2.b, self.C, self.y, self.mask, 1.0 / self.n_train)
+        if not train:
+            for L in self.layers:
+                L.saved = None
+        return stats
+
+    def _layer_backward(self, L, dout, doutb, x, K1):
+        Wh_ext, s_ext, s_dst, out, lse = L.saved
+        dWh, ds_src, ds_dst = _agg_bwd(Wh_ext, s_ext, s_dst, out, lse, dout, doutb, self.g, L.K, L.Fh)
+        L.saved = None
+        if self.halo is not None:
+            dWh, ds_src = self.halo.reduce_back([dWh, ds_src])
+        pack_grad(dWh, ds_src, ds_dst, L.dy)
+        del dWh, ds_src, ds_dst
+        lin_bwd_weight(x, L.dy, L.N, K1=K1, dW=L.dWc, db=L.db_scratch)
+        wcat_bwd(L.dWc, L.W, L.a_src, L.a_dst, L.gW, L.ga_src, L.ga_dst)
+
+    def backward(self):
+        L1, L2 = self.layers
+        out1 = L1.saved[3]
+        self._layer_backward(L2, self.dout2, self.dout2b, self.h1, L1.KF)
+        lin_bwd_data(L2.dy, L2.Wc, L1.KF, out1=self.dh1)
+        act_bwd(self.dh1, out1, L1.b, self.p, self.key, self._dropout_step(), self.row0, self.dout1, self.dout1b,
+                L1.gb)
+        self._layer_backward(L1, self.dout1, self.dout1b, self.xb, self.F)
+
+    def train_step(self):
+        stats = self.forward(train=True)
+        self.backward()
+        if self.distributed:
+            torch.distributed.all_reduce(self.grads)
+        ops.adam_(self.params, self.grads, self.m, self.v, self.lr, self.step_t)
+        self.last_stats = stats
+        self.epoch += 1
+        return stats[0] / self.n_train          # this rank's share of the global mean loss
+
+    @torch.no_grad()
+    def evaluate_counts(self):
+        """[4] = (train NLL sum, correct train / valid / test) of this rank's rows."""
+        return self.forward(train=False)
+
+    def state_tensors(self):
+        return {"params": self.params, "adam_m": self.m, "adam_v": self.v, "adam_step": self.step_t}
+
+    def load_state_tensors(self, t):
+        for name, dst in (("params", self.params), ("adam_m", self.m), ("adam_v", self.v),
+                          ("adam_step", self.step_t)):
+            if t[name].shape != dst.shape:
+                raise ValueError("checkpoint %s has shape %s, trainer %s" % (name, tuple(t[name].shape),
+                                                                              tuple(dst.shape)))
+            dst.copy_(t[name].to(dst.device))
+
+    def to_module(self):
+        """The parameters as a ``gat.GAT`` module (CPU), e.g. for the autograd reference."""
+        from .gat import GAT
+        L1, L2 = self.layers
+        m = GAT(self.F, self.C, L1.K, L1.Fh, self.p, 0)
+        with torch.no_grad():
+            for mod, L in ((m.l1, L1), (m.l2, L2)):
+                mod.W.copy_(L.W.cpu())
+                mod.a_src.copy_(L.a_src.cpu())
+                mod.a_dst.copy_(L.a_dst.cpu())
+                mod.bias.copy_(L.b.cpu())
+        return m

@@ -62,12 +62,16 @@ def _cat(x1, K1, x2, K2):
 def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None,
             K1: Optional[int] = None, K2: Optional[int] = None, relu: bool = False, p: float = 0.0, key=(0, 0),
             step=0, row0: int = 0, rscale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-            ldy: Optional[int] = None, idx1: Optional[torch.Tensor] = None, n: Optional[int] = None) -> torch.Tensor:
+            ldy: Optional[int] = None, idx1: Optional[torch.Tensor] = None, n: Optional[int] = None,
+            tail: Optional[torch.Tensor] = None, nsplit: Optional[int] = None, tk: int = 1) -> torch.Tensor:
     """``out[:, :N] = epi([x1[:, :K1] | x2[:, :K2]] @ W + bias)`` in bf16 (columns N..ldy zero).
 
     ``W``: fp32 [K1 + K2, N]; ``step``: int or device int32[1] (read at launch time);
     ``idx1`` (int32): row r reads ``x1[idx1[r]]`` (gather-on-load); ``n``: output rows
-    (default ``len(idx1)`` or the rows of x2 / x1)."""
+    (default ``len(idx1)`` or the rows of x2 / x1).
+    ``tail`` (fp32, with ``nsplit``): the columns ``c >= nsplit`` are written exactly, as
+    planes of ``tk`` columns -- ``tail[(c - nsplit) // tk, row, (c - nsplit) % tk]`` --
+    instead of bf16 into ``out`` (whose columns then stop at ``nsplit``)."""
     if n is None:
         n = idx1.shape[0] if idx1 is not None else (x2.shape[0] if x2 is not None else x1.shape[0])
     K1 = x1.shape[1] if K1 is None else int(K1)
@@ -75,8 +79,11 @@ def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = No
     N = W.shape[1]
     if W.shape[0] != K1 + K2:
         raise ValueError("W has %d rows, inputs give K = %d" % (W.shape[0], K1 + K2))
+    if tail is not None:
+        if nsplit is None or nsplit % 4 or (N - nsplit) % tk or tail.numel() < (N - nsplit) * n:
+            raise ValueError("lin_fwd tail: nsplit %% 4 == 0 and [%d, n, %d] fp32 planes needed" % ((N - nsplit) // tk, tk))
     if out is None:
-        ldy = ldy or (N + 7) // 8 * 8
+        ldy = ldy or ((N if tail is None else nsplit) + 7) // 8 * 8
         out = torch.empty(n, ldy, dtype=torch.bfloat16, device=x1.device)
     if x1.is_cuda:
         sv, sp = _step_args(step)
@@ -85,7 +92,8 @@ def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = No
         rc = hip.gnn_lin_fwd(x1.data_ptr(), x1.stride(0), K1, _ptr(x2), x2.stride(0) if x2 is not None else 0,
                                       K2, W.data_ptr(), N, _ptr(bias), out.data_ptr(), out.stride(0), n, int(relu),
                                       float(p), int(key[0]), int(key[1]), sv, int(row0), sp, _ptr(rscale), _st(x1),
-                                      idx1=_ptr(idx1), wimg=img.data_ptr())
+                                      idx1=_ptr(idx1), wimg=img.data_ptr(), yf=_ptr(tail),
+                                      nsplit=int(nsplit or 0), tk=int(tk))
         _check(rc, "lin_fwd")
         return out
     a = x1[idx1.long()] if idx1 is not None else x1[:n]
@@ -100,6 +108,11 @@ def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = No
     if rscale is not None:
         y = y * rscale[:, None].float()
     out[:n].zero_()
+    if tail is not None:
+        out[:n, :nsplit] = y[:, :nsplit].to(torch.bfloat16)
+        P = (N - nsplit) // tk
+        tail.view(-1)[:P * n * tk].view(P, n, tk).copy_(y[:, nsplit:].reshape(n, P, tk).transpose(0, 1))
+        return out
     out[:n, :N] = y.to(torch.bfloat16)
     return out
 

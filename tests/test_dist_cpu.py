@@ -197,21 +197,29 @@ def test_sage_data_parallel_keeps_replicas_identical():
     assert np.isfinite(out[0][1]) and np.isfinite(out[1][2])
 
 
-def _gat_shard_worker(rank, world, port, out):
+def _gat_params(tr):
+    if tr.fused is not None:
+        return tr.fused.params.detach().clone().numpy()
+    return torch.cat([p.detach().flatten() for p in tr.model.parameters()]).numpy()
+
+
+def _gat_shard_worker(rank, world, port, out, fused=False, heads=2, dropout=0.0):
     _init(rank, world, port)
     from cgnn_amd.gnn.data import synthetic_shard
     from cgnn_amd.gnn.gat import ShardedGATTrainer
     # rank-local generation: this rank never builds the rest of the graph
     shard = synthetic_shard("ogbn-products", rank, world, seed=1, scale=0.0005)
-    tr = ShardedGATTrainer(shard, heads=2, head_dim=8, dropout=0.0, lr=0.01, seed=rank)
+    tr = ShardedGATTrainer(shard, heads=heads, head_dim=8, dropout=dropout, lr=0.01, seed=rank, fused=fused)
     losses = []
+    grads1 = None
     for _ in range(3):
         l = tr.train_step().clone()
         dist.all_reduce(l)
         losses.append(float(l))
+        if grads1 is None and tr.fused is not None:
+            grads1 = tr.fused.grads.clone().numpy()
     res = tr.evaluate()
-    out[rank] = (losses, res, torch.cat([p.detach().flatten() for p in tr.model.parameters()]).numpy(),
-                 tr.halo_stats())
+    out[rank] = (losses, res, _gat_params(tr), tr.halo_stats(), grads1)
     dist.destroy_process_group()
 
 
@@ -232,11 +240,46 @@ def test_sharded_gat_matches_single_process(world):
     out = mgr.dict()
     mp.spawn(_gat_shard_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     for r in range(world):
-        losses, res, params, hs = out[r]
+        losses, res, params, hs, _ = out[r]
         np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
         assert res == pytest.approx(ref_res, abs=1e-9)
         # (summation order of the returned halo gradients differs from the unsharded sum)
         np.testing.assert_allclose(params, ref_params, rtol=1e-4, atol=3e-5)
         assert 0 < hs["recv_rows"] < g.n - hs["local_rows"] or hs["recv_rows"] == g.n - hs["local_rows"]
     assert sum(out[r][3]["recv_rows"] for r in range(world)) == sum(out[r][3]["send_rows"] for r in range(world))
+    np.testing.assert_array_equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_fused_gat_matches_single_process(world):
+    """The fused GAT epoch (gat_fused: every dense op a HIP kernel on a GPU; its fp32
+    reference branches here) sharded over gloo ranks equals the one-process fused
+    model -- with dropout on, since the masks are keyed by the global row."""
+    from cgnn_amd.gnn.data import synthetic
+    from cgnn_amd.gnn.gat import ShardedGATTrainer
+    g = synthetic("ogbn-products", seed=1, scale=0.0005)
+    ref = ShardedGATTrainer(g, heads=4, head_dim=8, dropout=0.3, lr=0.01, seed=0, fused=True)
+    assert ref.fused is not None
+    ref_losses = [float(ref.train_step())]
+    ref_grads1 = ref.fused.grads.clone().numpy()
+    ref_losses += [float(ref.train_step()) for _ in range(2)]
+    ref_res = ref.evaluate()
+    ref_params = _gat_params(ref)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_gat_shard_worker, args=(world, _free_port(), out, True, 4, 0.3), nprocs=world, join=True)
+    for r in range(world):
+        losses, res, params, hs, grads1 = out[r]
+        # first-step gradients (rank-summed): equal up to the summation order of the
+        # halo-returned rows, which are then stored bf16 as the MFMA operand
+        assert np.abs(grads1 - ref_grads1).max() < 1e-3 * np.abs(ref_grads1).max()
+        # the gradient rows returned by the halo are summed in another order and then
+        # stored bf16 (as the MFMA weight-gradient operand), so a rounding can flip
+        np.testing.assert_allclose(losses, ref_losses, rtol=2e-4)
+        assert res == pytest.approx(ref_res, abs=2e-3)
+        # Adam normalises each gradient, so a near-zero gradient perturbed by such a
+        # rounding moves its weight by up to ~lr: bound the worst element by lr / 10
+        # and require (nearly) all of them to agree closely
+        d = np.abs(params - ref_params)
+        assert d.max() < 1e-3 and np.mean(d > 1e-4) < 0.05, (d.max(), np.mean(d > 1e-4))
     np.testing.assert_array_equal(out[0][2], out[1][2])

@@ -1,0 +1,118 @@
+"""HIP kernels of the fused GAT epoch (gnn_gat.hip dense-side kernels, lin_fwd's
+fp32 score planes) against their CPU reference branches, and the whole fused epoch
+on the GPU against the same epoch on the CPU."""
+import numpy as np
+import pytest
+import torch
+
+from cgnn_amd.gnn import ops
+from cgnn_amd.gnn.data import synthetic
+from cgnn_amd.gnn.gat import GATTrainer
+from cgnn_amd.gnn.gat_fused import act_bwd, act_fwd, pack_grad, row_ce
+from cgnn_amd.gnn.linear import lin_fwd
+
+pytestmark = pytest.mark.gpu
+
+
+def _cuda(*ts):
+    return [t.cuda() if t is not None else None for t in ts]
+
+
+@pytest.mark.parametrize("F,p,row0", [(128, 0.5, 0), (256, 0.3, 1000), (32, 0.0, 7)])
+def test_act_fwd_bwd_match_reference(F, p, row0):
+    torch.manual_seed(0)
+    n = 777
+    out = torch.randn(n, F) * 2
+    b = torch.randn(F) * 0.1
+    key, step = (11, 22), 5
+    H = torch.zeros(n, F, dtype=torch.bfloat16)
+    act_fwd(out, b, H, p, key, step, row0)
+    Hg = torch.zeros(n, F, dtype=torch.bfloat16, device="cuda")
+    act_fwd(out.cuda(), b.cuda(), Hg, p, key, torch.tensor([step], dtype=torch.int32, device="cuda"), row0)
+    np.testing.assert_allclose(Hg.cpu().float().numpy(), H.float().numpy(), rtol=8e-3, atol=1e-6)
+    dH = torch.randn(n, F).to(torch.bfloat16)
+    dout, doutb, db = torch.zeros(n, F), torch.zeros(n, F, dtype=torch.bfloat16), torch.zeros(F)
+    act_bwd(dH, out, b, p, key, step, row0, dout, doutb, db)
+    dg, dgb, dbg = torch.zeros(n, F, device="cuda"), torch.zeros(n, F, dtype=torch.bfloat16, device="cuda"), \
+        torch.zeros(F, device="cuda")
+    act_bwd(dH.cuda(), out.cuda(), b.cuda(), p, key, step, row0, dg, dgb, dbg)
+    np.testing.assert_allclose(dg.cpu().numpy(), dout.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(dgb.cpu().float().numpy(), doutb.float().numpy(), rtol=8e-3, atol=1e-6)
+    np.testing.assert_allclose(dbg.cpu().numpy(), db.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("C,ld", [(47, 48), (172, 176), (7, 8), (256, 256)])
+def test_row_ce_matches_reference(C, ld):
+    torch.manual_seed(1)
+    n = 5000
+    Z = torch.randn(n, ld) * 3
+    b = torch.randn(C)
+    y = torch.randint(0, C, (n,), dtype=torch.int32)
+    mask = torch.randint(0, 4, (n,), dtype=torch.uint8)
+    inv = 1.0 / max(int((mask == 1).sum()), 1)
+    dZ, dZb, db = torch.zeros(n, ld), torch.zeros(n, ld, dtype=torch.bfloat16), torch.zeros(C)
+    st = row_ce(Z, b, C, y, mask, inv, dZ=dZ, dZb=dZb, db=db)
+    g = _cuda(Z, b, y, mask)
+    dZg = torch.full((n, ld), 7.0, device="cuda")
+    dZbg = torch.zeros(n, ld, dtype=torch.bfloat16, device="cuda")
+    dbg = torch.zeros(C, device="cuda")
+    stg = row_ce(*g[:2], C, g[2], g[3], inv, dZ=dZg, dZb=dZbg, db=dbg)
+    np.testing.assert_allclose(stg.cpu().numpy(), st.numpy(), rtol=1e-4)
+    np.testing.assert_allclose(dZg.cpu().numpy(), dZ.numpy(), atol=1e-7)
+    np.testing.assert_allclose(dZbg.cpu().float().numpy(), dZb.float().numpy(), rtol=8e-3, atol=1e-9)
+    np.testing.assert_allclose(dbg.cpu().numpy(), db.numpy(), atol=1e-6)
+    ste = row_ce(*g[:2], C, g[2], g[3], inv)               # evaluation: statistics only
+    np.testing.assert_allclose(ste.cpu().numpy(), st.numpy(), rtol=1e-4)
+
+
+def test_pack_grad_and_lin_fwd_score_planes():
+    torch.manual_seed(2)
+    n, HF, K = 1000, 128, 4
+    dWh, ds, dd = torch.randn(n, HF), torch.randn(n, K), torch.randn(n, K)
+    dy = torch.zeros(n, 136, dtype=torch.bfloat16)
+    pack_grad(dWh, ds, dd, dy)
+    dyg = torch.full((n, 136), 3.0, dtype=torch.bfloat16, device="cuda")
+    pack_grad(*_cuda(dWh, ds, dd), dyg)
+    assert torch.equal(dyg.cpu(), dy)
+    # lin_fwd with the fp32 tail: [Wh (bf16) | s planes (fp32)]
+    x = torch.randn(n, 104).to(torch.bfloat16)
+    W = torch.randn(100, HF + 2 * K) * 0.1
+    Wh, s = torch.zeros(n, HF, dtype=torch.bfloat16), torch.zeros(2, n, K)
+    lin_fwd(x, W, None, K1=100, out=Wh, tail=s, nsplit=HF, tk=K)
+    Whg, sg = torch.zeros(n, HF, dtype=torch.bfloat16, device="cuda"), torch.zeros(2, n, K, device="cuda")
+    lin_fwd(x.cuda(), W.cuda(), None, K1=100, out=Whg, tail=sg, nsplit=HF, tk=K)
+    np.testing.assert_allclose(Whg.cpu().float().numpy(), Wh.float().numpy(), rtol=1e-2, atol=1e-2)
+    np.testing.assert_allclose(sg.cpu().numpy(), s.numpy(), rtol=1e-4, atol=1e-4)
+    ref = x[:, :100].float() @ W.to(torch.bfloat16).float()
+    np.testing.assert_allclose(sg[0].cpu().numpy(), ref[:, HF:HF + K].numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(sg[1].cpu().numpy(), ref[:, HF + K:].numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("heads,head_dim", [(4, 32), (8, 32), (4, 8)])
+def test_fused_gat_epoch_gpu_matches_cpu(heads, head_dim):
+    g = synthetic("ogbn-products", seed=3, scale=0.002)
+    cpu = GATTrainer(g, heads=heads, head_dim=head_dim, dropout=0.5, lr=0.01, seed=0, fused=True)
+    gpu = GATTrainer(g.to("cuda:0"), heads=heads, head_dim=head_dim, dropout=0.5, lr=0.01, seed=0)
+    assert gpu.fused is not None
+    lc, lg = [], []
+    for it in range(3):
+        lc.append(float(cpu.train_step()))
+        lg.append(float(gpu.train_step()))
+        if it == 0:
+            gc, gg = cpu.fused.grads.clone(), gpu.fused.grads.cpu()
+            assert (gg - gc).abs().max() < 3e-3 * gc.abs().max(), ((gg - gc).abs().max(), gc.abs().max())
+    np.testing.assert_allclose(lg, lc, rtol=2e-3)
+    d = (gpu.fused.params.cpu() - cpu.fused.params).abs()
+    assert d.max() < 2e-3 and (d > 2e-4).float().mean() < 0.05, (d.max(), (d > 2e-4).float().mean())
+    a, b = cpu.evaluate(), gpu.evaluate()
+    assert abs(a["val_acc"] - b["val_acc"]) < 0.01 and abs(a["train_loss"] - b["train_loss"]) < 2e-3 * a["train_loss"]
+
+
+def test_fused_gat_learns_products_shape_gpu():
+    g = synthetic("ogbn-products", seed=0, device="cuda:0", scale=0.01)
+    tr = GATTrainer(g, heads=4, head_dim=32, dropout=0.5, lr=0.01)
+    assert tr.fused is not None
+    for _ in range(30):
+        tr.train_step()
+    res = tr.evaluate()
+    assert res["val_acc"] > 0.3, res

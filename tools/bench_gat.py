@@ -21,12 +21,13 @@ def main():
     ap.add_argument("--head-dim", type=int, default=32)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--unfused", action="store_true", help="autograd model + hipBLASLt projections (A/B)")
     a = ap.parse_args()
     import torch
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gat import GATTrainer
     g = synthetic(a.dataset, seed=0, device="cuda:0", scale=a.scale)
-    tr = GATTrainer(g, heads=a.heads, head_dim=a.head_dim)
+    tr = GATTrainer(g, heads=a.heads, head_dim=a.head_dim, fused=False if a.unfused else None)
     for _ in range(a.warmup):
         tr.train_step()
     torch.cuda.synchronize()
@@ -38,7 +39,8 @@ def main():
     res = tr.evaluate()
     print(json.dumps({"bench": "gat_fullgraph", "dataset": a.dataset, "n": g.n, "nnz": g.nnz,
                       "heads": a.heads, "head_dim": a.head_dim, "ms_per_epoch": 1e3 * dt,
-                      "epochs_per_s": 1.0 / dt, "train_loss": float(loss), **res}))
+                      "epochs_per_s": 1.0 / dt, "train_loss": float(loss), "fused": tr.fused is not None,
+                      **res}))
 
 
 if __name__ == "__main__":

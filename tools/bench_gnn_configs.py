@@ -69,7 +69,7 @@ def main():
                          "rank-local shard, halo plan and buffers; received rows zero) -- memory / compute dry run")
     ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--halo-grad-bf16", action="store_true", help="papers-gat2: gradients on the halo wire in bf16")
-    ap.add_argument("--unfused", action="store_true", help="arxiv-gcn3 / products-sage3: autograd + hipBLASLt path (A/B)")
+    ap.add_argument("--unfused", action="store_true", help="arxiv-gcn3 / products-sage3 / papers-gat2: autograd + hipBLASLt path (A/B)")
     a = ap.parse_args()
 
     from cgnn_amd.gnn.data import SHAPES, reorder, synthetic
@@ -179,7 +179,8 @@ def main():
         shard = synthetic_shard("ogbn-papers100M", srank, sworld, seed=a.seed, device=dev, scale=a.scale)
         gen_s = time.perf_counter() - t0
         n_nodes, nnz_local, n_local = shard.n, shard.nnz, shard.n_local
-        tr = ShardedGATTrainer(shard, heads=4, head_dim=32, dropout=0.5, lr=0.005, seed=a.seed, emulate=emu)
+        tr = ShardedGATTrainer(shard, heads=4, head_dim=32, dropout=0.5, lr=0.005, seed=a.seed, emulate=emu,
+                               fused=False if a.unfused else None)
         if tr.halo is not None and a.halo_grad_bf16:
             tr.halo.grad_wire = torch.bfloat16
         del shard
@@ -197,7 +198,7 @@ def main():
                    peak_gpu_mem_gib=round(peak, 2) if peak is not None else None,
                    shard={"rank": srank, "world": sworld, "rows": n_local, "nnz": nnz_local, "gen_s": round(gen_s, 2),
                           "rank_local_generation": True},
-                   halo=tr.halo_stats(), emulated=emu is not None, reordered=False,
+                   halo=tr.halo_stats(), emulated=emu is not None, reordered=False, fused=tr.fused is not None,
                    note=("DRY RUN: one rank of %d in one process; received halo rows are zero, so timing / memory "
                          "are those of the rank's kernels and buffers without communication, accuracy is not "
                          "meaningful" % sworld) if emu else None,
