@@ -124,9 +124,7 @@ class _HaloGAT(torch.autograd.Function):
                 grad_wire=torch.float32):
         wdt = torch.bfloat16 if (lowp and Wh.is_cuda) else torch.float32
         ctx.grad_wire = grad_wire
-        buf = halo.exchange(halo.pack([Wh.to(wdt), s_src.float()]))
-        Wh_ext, s_ext = halo.unpack(buf, [(K * Fh, wdt), (K, torch.float32)])
-        del buf
+        Wh_ext, s_ext = halo.exchange_parts([Wh.to(wdt).contiguous(), s_src.float().contiguous()])
         ctx.g, ctx.K, ctx.Fh, ctx.lowp, ctx.halo = g, K, Fh, lowp, halo
         s_dst = s_dst.contiguous()
         if Wh.is_cuda:
@@ -323,7 +321,8 @@ class ShardedGATTrainer:
     """
 
     def __init__(self, shard, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True,
-                 bucket_mb: float = 16.0, emulate=None, fused: Optional[bool] = None):
+                 bucket_mb: float = 16.0, emulate=None, fused: Optional[bool] = None,
+                 halo_chunk_bytes: int = 4 << 30):
         import torch.distributed as dist
         from ..parallel import dist as pdist
         from ..parallel.ddp import GradBucketer
@@ -347,7 +346,12 @@ class ShardedGATTrainer:
         distributed = self.world > 1 and emulate is None
         self.halo = None
         if self.world > 1:
-            self.halo = HaloExchange(shard.col, r0, r1, per, shard.n, emulate=emulate)
+            # widest row on the wire: the fp32 layer gradients [dWh | ds_src] (exchange rounds
+            # are sized so that one round moves at most halo_chunk_bytes of it)
+            ow = (shard.n_classes + 7) // 8 * 8
+            wide = 4 * max(heads * head_dim + heads, ow + 1)
+            self.halo = HaloExchange(shard.col, r0, r1, per, shard.n, emulate=emulate, max_row_bytes=wide,
+                                     chunk_bytes=halo_chunk_bytes)
             self.g = GraphCSR(shard.rowptr, self.halo.col_ext, nloc, n_cols=self.halo.n_ext)
         else:
             self.g = GraphCSR(shard.rowptr, shard.col, nloc, n_cols=shard.n)

@@ -171,26 +171,30 @@ def _agg_fwd(Wh, s_src, s_dst, g, K, Fh):
     return _gat_aggregate_torch(Wh.float(), s_src, s_dst, g, K, Fh).float(), None
 
 
-def _agg_bwd(Wh, s_src, s_dst, out, lse, dout, doutb, g, K, Fh):
-    """(dWh [n_cols, K Fh] fp32, ds_src [n_cols, K], ds_dst [n, K])."""
-    n = g.n
-    if Wh.is_cuda:
-        hip = native.hip()
-        dev = Wh.device
-        alpha_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
-        dsc_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
-        ds_dst = torch.empty(n, K, dtype=torch.float32, device=dev)
-        wbf = int(Wh.dtype == torch.bfloat16)
-        hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(),
-                            out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(), dsc_e.data_ptr(),
-                            ds_dst.data_ptr(), n, K, Fh, _st(Wh), wbf)
-        rp_t, col_t, perm = g.transposed()
-        dWh = torch.empty(g.n_cols, K * Fh, dtype=torch.float32, device=dev)
-        ds_src = torch.empty(g.n_cols, K, dtype=torch.float32, device=dev)
-        hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
-                            dsc_e.data_ptr(), doutb.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh,
-                            _st(Wh), 1)
-        return dWh, ds_src, ds_dst
+def _agg_bwd_rows(Wh, s_src, s_dst, out, lse, dout, g, K, Fh):
+    """Row half of the aggregation backward: per edge the attention weight and the
+    score gradient (alpha_e, dsc_e [nnz, K]) and ds_dst [n, K] (GPU)."""
+    hip = native.hip()
+    dev = Wh.device
+    alpha_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+    dsc_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+    ds_dst = torch.empty(g.n, K, dtype=torch.float32, device=dev)
+    hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(),
+                        out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(), dsc_e.data_ptr(),
+                        ds_dst.data_ptr(), g.n, K, Fh, _st(Wh), int(Wh.dtype == torch.bfloat16))
+    return alpha_e, dsc_e, ds_dst
+
+
+def _agg_bwd_cols(alpha_e, dsc_e, doutb, g, K, Fh, lo, hi, dWh, ds_src):
+    """Column half for source rows [lo, hi) of the transposed CSR (rows are independent,
+    so a row range is a pointer offset): dWh [hi - lo, K Fh], ds_src [hi - lo, K] (GPU)."""
+    rp_t, col_t, perm = g.transposed()
+    native.hip().gnn_gat_bwd_col(rp_t.data_ptr() + 4 * lo, col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
+                                 dsc_e.data_ptr(), doutb.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), hi - lo, K,
+                                 Fh, _st(doutb), 1)
+
+
+def _agg_bwd_torch(Wh, s_src, s_dst, dout, g, K, Fh):
     from .gat import _gat_aggregate_torch
     with torch.enable_grad():
         a = Wh.float().detach().requires_grad_()
@@ -310,10 +314,7 @@ class FusedGAT:
         lin_fwd(x, L.Wc, None, K1=K1, out=L.Wh, tail=L.s, nsplit=L.KF, tk=L.K)
         s_src, s_dst = L.s[0], L.s[1]
         if self.halo is not None:
-            h = self.halo
-            buf = h.exchange(h.pack([L.Wh, s_src]))
-            Wh_ext, s_ext = h.unpack(buf, [(L.KF, torch.bfloat16), (L.K, torch.float32)])
-            del buf
+            Wh_ext, s_ext = self.halo.exchange_parts([L.Wh, s_src])
         else:
             Wh_ext, s_ext = L.Wh, s_src
         out, lse = _agg_fwd(Wh_ext, s_ext, s_dst, self.g, L.K, L.Fh)
@@ -339,10 +340,29 @@ class FusedGAT:
 
     def _layer_backward(self, L, dout, doutb, x, K1):
         Wh_ext, s_ext, s_dst, out, lse = L.saved
-        dWh, ds_src, ds_dst = _agg_bwd(Wh_ext, s_ext, s_dst, out, lse, dout, doutb, self.g, L.K, L.Fh)
         L.saved = None
-        if self.halo is not None:
-            dWh, ds_src = self.halo.reduce_back([dWh, ds_src])
+        g, K, Fh = self.g, L.K, L.Fh
+        if not self.dev.type == "cuda":
+            dWh, ds_src, ds_dst = _agg_bwd_torch(Wh_ext, s_ext, s_dst, dout, g, K, Fh)
+            del Wh_ext, s_ext
+            if self.halo is not None:
+                dWh, ds_src = self.halo.reduce_back([dWh, ds_src])
+        else:
+            alpha_e, dsc_e, ds_dst = _agg_bwd_rows(Wh_ext, s_ext, s_dst, out, lse, dout, g, K, Fh)
+            del Wh_ext, s_ext                        # the received rows are not needed any more
+            n = self.nloc
+            dWh = torch.empty(n, L.KF, dtype=torch.float32, device=self.dev)
+            ds_src = torch.empty(n, K, dtype=torch.float32, device=self.dev)
+            _agg_bwd_cols(alpha_e, dsc_e, doutb, g, K, Fh, 0, n, dWh, ds_src)
+            if self.halo is not None:
+                # the received rows' gradients are made one exchange round at a time
+                def produce(lo, hi):
+                    a = torch.empty(hi - lo, L.KF, dtype=torch.float32, device=self.dev)
+                    b = torch.empty(hi - lo, K, dtype=torch.float32, device=self.dev)
+                    _agg_bwd_cols(alpha_e, dsc_e, doutb, g, K, Fh, lo, hi, a, b)
+                    return [a, b]
+                self.halo.reduce_back_stream(produce, [dWh, ds_src], getattr(self.halo, "grad_wire", torch.float32))
+            del alpha_e, dsc_e
         pack_grad(dWh, ds_src, ds_dst, L.dy)
         del dWh, ds_src, ds_dst
         lin_bwd_weight(x, L.dy, L.N, K1=K1, dW=L.dWc, db=L.db_scratch)

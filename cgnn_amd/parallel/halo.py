@@ -9,33 +9,44 @@ each rank receives exactly the remote source rows its edges read:
   are sent to their owners with one all-to-all; every rank learns which of its rows
   each peer reads (``send_idx``), and the CSR columns are renumbered into the
   extended row space ``[own rows | received rows]`` (``col_ext``);
-* forward: one all-to-all of the requested rows, packed into ONE byte buffer
-  (bf16 activations and fp32 columns such as GAT's attention scores side by side
-  as raw bytes, so the scores cross the link exactly);
+* forward: all-to-alls of the requested rows, several column groups packed per row
+  as raw bytes (bf16 activations and fp32 attention scores side by side, so the
+  scores cross the link exactly);
 * backward: the transpose -- the gradient rows of the received rows go back to their
   owners (fp32 by default) and are summed into the owner's rows peer by peer (the
   rows one peer returns are distinct, so every accumulation is deterministic).
 
-xGMI sizing: a full-graph epoch moves the halo twice per layer; at 8 ranks with
-shuffled ids the halo is most of the graph (every node has ~30 neighbours), so the
-win over an fp32 all-gather is the bf16 payload and the rows nobody reads; a
-locality-preserving partition shrinks it further (``gnn.data.reorder``).
+**Bounded memory: the exchange runs in rounds.**  At the papers100M shape with
+shuffled ids a rank receives ~6x its own rows (every node has ~30 neighbours), so a
+one-shot exchange needs send / receive staging buffers of tens of GB per direction
+(89 M rows x 708 B of fp32 layer-2 gradient = 63 GB at 8 ranks) on top of the
+activations.  Every peer's slice is split into ``rounds`` equal parts (the same
+count on every rank: an all-reduce MAX at setup, sized so that one round moves at
+most ``chunk_bytes`` of the widest payload), and the received rows are laid out
+ROUND-MAJOR in the extended row space: round t's rows from all peers are one
+contiguous block ``ext_range(t)``.  So each round receives straight into its block,
+and in the backward a producer can compute only that block's gradient rows
+(:meth:`reduce_back_stream`, used by the fused GAT: the [n_ext, K Fh] fp32 gradient
+of the received rows is never materialised).
 
 ``emulate=(rank, world)`` builds the plan of one rank of a larger job inside a single
-process (no process group): the exchange then leaves the received rows at zero and
-returns no gradient to peers -- a dry run that has every buffer, kernel and byte
-count of that rank (memory and compute measurements), not its numerics.
+process (no process group): the send side is a symmetric stand-in (as many rows sent
+as received, to this rank's own rows), received rows are zero and returned gradients
+are zero -- a dry run with every buffer, kernel and byte count of that rank (memory
+and compute measurements), not its numerics.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+import math
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
 
 
 class HaloExchange:
     def __init__(self, col: torch.Tensor, r0: int, r1: int, per: int, n: int, group=None,
-                 emulate: Optional[Tuple[int, int]] = None):
+                 emulate: Optional[Tuple[int, int]] = None, max_row_bytes: int = 1024,
+                 chunk_bytes: int = 4 << 30):
         import torch.distributed as dist
         self.group = group
         self.dev = col.device
@@ -52,8 +63,9 @@ class HaloExchange:
         need = torch.unique(c[~local])                               # sorted global ids = grouped by owner
         recv_counts = torch.bincount(need // self.per, minlength=self.world).to(torch.int64)
         if self.emulate:
-            send_counts = torch.zeros_like(recv_counts)
-            req = torch.empty(0, dtype=torch.int64, device=self.dev)
+            send_counts = recv_counts.clone()
+            send_counts[self.rank] = 0
+            req = self.r0 + torch.arange(int(send_counts.sum()), dtype=torch.int64, device=self.dev) % max(self.nloc, 1)
         else:
             send_counts = torch.empty_like(recv_counts)
             dist.all_to_all_single(send_counts, recv_counts, group=group)
@@ -68,14 +80,55 @@ class HaloExchange:
         self.n_recv, self.n_send = sum(self.recv_splits), sum(self.send_splits)
         self.send_idx = (req - self.r0).contiguous()
         self.need = need
-        ext = torch.where(local, c - self.r0, self.nloc + torch.searchsorted(need, c))
+        # rounds: identical on every rank
+        rb = max(self.n_recv, self.n_send) * int(max_row_bytes)
+        rounds = max(1, math.ceil(rb / max(int(chunk_bytes), 1)))
+        if not self.emulate and dist.is_initialized():
+            t = torch.tensor([rounds], dtype=torch.int64, device=self.dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            rounds = int(t.item())
+        self.rounds = rounds
+        # per round: the rows of every peer slice in that round (equal split of each slice)
+        self._recv_r = [self._split(self.recv_splits, t) for t in range(rounds)]
+        self._send_r = [self._split(self.send_splits, t) for t in range(rounds)]
+        # round-major position of every needed row in the extended space
+        pos = torch.empty(self.n_recv, dtype=torch.int64, device=self.dev)
+        soff = [0]
+        for v in self.recv_splits:
+            soff.append(soff[-1] + v)
+        self._ext_base = []
+        base = 0
+        for t in range(rounds):
+            self._ext_base.append(base)
+            for p, (a, b) in enumerate(self._recv_r[t]):
+                if b > a:
+                    pos[soff[p] + a:soff[p] + b] = torch.arange(base, base + b - a, device=self.dev)
+                    base += b - a
+        self._ext_base.append(base)
+        j = torch.searchsorted(need, c.clamp_min(0))
+        ext = torch.where(local, c - self.r0, self.nloc + pos[j.clamp_max(max(self.n_recv - 1, 0))]
+                          if self.n_recv else c - self.r0)
         self.col_ext = ext.to(torch.int32).contiguous()
         self.n_ext = self.nloc + self.n_recv
-        # peer slices of send_idx (distinct rows within one slice: deterministic accumulation)
-        bounds = [0]
+        # per round: the own rows sent (peer order) and per-peer slices of them
+        self._send_idx_r = []
+        off = [0]
         for v in self.send_splits:
-            bounds.append(bounds[-1] + v)
-        self._slices = [(bounds[i], bounds[i + 1]) for i in range(self.world) if bounds[i + 1] > bounds[i]]
+            off.append(off[-1] + v)
+        for t in range(rounds):
+            parts = [self.send_idx[off[p] + a:off[p] + b] for p, (a, b) in enumerate(self._send_r[t])]
+            self._send_idx_r.append(torch.cat(parts) if parts else self.send_idx[:0])
+
+    def _split(self, splits: Sequence[int], t: int):
+        R = self.rounds
+        return [(L * t // R, L * (t + 1) // R) for L in splits]
+
+    def _sizes(self, ranges):
+        return [b - a for a, b in ranges]
+
+    def ext_range(self, t: int) -> Tuple[int, int]:
+        """Rows [lo, hi) of the extended space received in round t."""
+        return self.nloc + self._ext_base[t], self.nloc + self._ext_base[t + 1]
 
     # ------------------------------------------------------------------ packing
     @staticmethod
@@ -102,35 +155,73 @@ class HaloExchange:
         dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits,
                                group=self.group)
 
+    def exchange_parts(self, parts: Sequence[torch.Tensor]) -> List[torch.Tensor]:
+        """Rows [own | received] of column groups ``parts`` ([nloc, w_i], any dtypes):
+        one all-to-all per round, the groups packed side by side as raw bytes per row."""
+        ext = []
+        for p in parts:
+            e = torch.empty((self.n_ext,) + tuple(p.shape[1:]), dtype=p.dtype, device=self.dev)
+            e[:self.nloc] = p
+            ext.append(e)
+        nbytes = [p.shape[1] * p.element_size() for p in parts]
+        for t in range(self.rounds):
+            lo, hi = self.ext_range(t)
+            idx = self._send_idx_r[t]
+            send = torch.cat([p.index_select(0, idx).view(torch.uint8) for p in parts], 1) if idx.numel() else \
+                torch.empty(0, sum(nbytes), dtype=torch.uint8, device=self.dev)
+            recv = torch.empty(hi - lo, sum(nbytes), dtype=torch.uint8, device=self.dev)
+            self._all_to_all(recv, send, self._sizes(self._recv_r[t]), self._sizes(self._send_r[t]))
+            del send
+            c = 0
+            for e, p, nb in zip(ext, parts, nbytes):
+                e[lo:hi] = recv[:, c:c + nb].contiguous().view(p.dtype)
+                c += nb
+            del recv
+        return ext
+
     def exchange(self, payload_local: torch.Tensor) -> torch.Tensor:
         """Rows [own | received] of a packed local payload [nloc, W] (uint8)."""
-        W = payload_local.shape[1]
-        ext = torch.empty(self.n_ext, W, dtype=payload_local.dtype, device=self.dev)
-        ext[:self.nloc] = payload_local
-        send = payload_local.index_select(0, self.send_idx) if self.n_send else payload_local[:0]
-        self._all_to_all(ext[self.nloc:], send.contiguous(), self.recv_splits, self.send_splits)
-        return ext
+        return self.exchange_parts([payload_local])[0]
 
     def reduce_back(self, parts: Sequence[torch.Tensor], wire_dtype: torch.dtype = torch.float32):
         """Transpose of :meth:`exchange` for gradients given as column groups [n_ext, w_i]:
         the own rows of every group plus the gradients of the rows peers read, returned
-        to this rank (one all-to-all of only the received rows, in ``wire_dtype``) and
-        summed in peer order.  Returns one [nloc, w_i] tensor per group (in place on the
-        own-row slices of ``parts``, no full-size copy)."""
-        widths = [p.shape[1] for p in parts]
-        send = torch.cat([p[self.nloc:].to(wire_dtype) for p in parts], 1) if self.n_recv else \
-            torch.empty(0, sum(widths), dtype=wire_dtype, device=self.dev)
-        back = torch.empty(self.n_send, sum(widths), dtype=wire_dtype, device=self.dev)
-        self._all_to_all(back, send, self.send_splits, self.recv_splits)
-        del send
-        out, c = [], 0
-        for p, w in zip(parts, widths):
-            g = p[:self.nloc]
-            for a, b in self._slices:
-                g.index_put_((self.send_idx[a:b],), back[a:b, c:c + w].to(g.dtype), accumulate=True)
-            out.append(g)
-            c += w
-        return out
+        to this rank (in ``wire_dtype``) and summed in peer order.  Returns one
+        [nloc, w_i] tensor per group (in place on the own-row slices of ``parts``)."""
+        def produce(lo, hi):
+            return [p[lo:hi] for p in parts]
+        return self.reduce_back_stream(produce, [p[:self.nloc] for p in parts], wire_dtype)
+
+    def reduce_back_stream(self, produce: Callable[[int, int], Sequence[torch.Tensor]],
+                           own: Sequence[torch.Tensor], wire_dtype: torch.dtype = torch.float32):
+        """:meth:`reduce_back` with the received rows' gradients made on demand:
+        ``produce(lo, hi)`` returns the gradient groups of extended rows [lo, hi) (one
+        round's block); the peers' returns are added into ``own`` ([nloc, w_i], in
+        place), which is returned."""
+        widths = [o.shape[1] for o in own]
+        for t in range(self.rounds):
+            lo, hi = self.ext_range(t)
+            if hi > lo:
+                got = produce(lo, hi)
+                send = got[0].to(wire_dtype) if len(got) == 1 else torch.cat([g.to(wire_dtype) for g in got], 1)
+                del got
+            else:
+                send = torch.empty(0, sum(widths), dtype=wire_dtype, device=self.dev)
+            idx = self._send_idx_r[t]
+            back = torch.empty(idx.numel(), sum(widths), dtype=wire_dtype, device=self.dev)
+            self._all_to_all(back, send.contiguous(), self._sizes(self._send_r[t]), self._sizes(self._recv_r[t]))
+            del send
+            a = 0
+            for p, n_p in enumerate(self._sizes(self._send_r[t])):
+                if n_p:
+                    rows = idx[a:a + n_p]
+                    c = 0
+                    for g, w in zip(own, widths):
+                        g.index_put_((rows,), back[a:a + n_p, c:c + w].to(g.dtype), accumulate=True)
+                        c += w
+                a += n_p
+            del back
+        return list(own)
 
     def bytes_per_exchange(self, width_bytes: int) -> Tuple[int, int]:
         """(bytes received, bytes sent) by this rank for one exchange of ``width_bytes`` rows."""

@@ -203,13 +203,16 @@ def _gat_params(tr):
     return torch.cat([p.detach().flatten() for p in tr.model.parameters()]).numpy()
 
 
-def _gat_shard_worker(rank, world, port, out, fused=False, heads=2, dropout=0.0):
+def _gat_shard_worker(rank, world, port, out, fused=False, heads=2, dropout=0.0, chunk=4 << 30):
     _init(rank, world, port)
     from cgnn_amd.gnn.data import synthetic_shard
     from cgnn_amd.gnn.gat import ShardedGATTrainer
     # rank-local generation: this rank never builds the rest of the graph
     shard = synthetic_shard("ogbn-products", rank, world, seed=1, scale=0.0005)
-    tr = ShardedGATTrainer(shard, heads=heads, head_dim=8, dropout=dropout, lr=0.01, seed=rank, fused=fused)
+    tr = ShardedGATTrainer(shard, heads=heads, head_dim=8, dropout=dropout, lr=0.01, seed=rank, fused=fused,
+                           halo_chunk_bytes=chunk)
+    if chunk < (1 << 20):
+        assert tr.halo.rounds > 1
     losses = []
     grads1 = None
     for _ in range(3):
@@ -223,8 +226,8 @@ def _gat_shard_worker(rank, world, port, out, fused=False, heads=2, dropout=0.0)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_gat_matches_single_process(world):
+@pytest.mark.parametrize("world,chunk", [(2, 4 << 30), (4, 4 << 30), (4, 16 << 10)])
+def test_sharded_gat_matches_single_process(world, chunk):
     """GAT with rows sharded over gloo ranks -- rank-local shard generation, halo
     all-to-all of exactly the [Wh | s_src] rows each rank reads, gradients returned
     to their owners, averaged parameter gradients -- equals the unsharded model:
@@ -238,7 +241,7 @@ def test_sharded_gat_matches_single_process(world):
     ref_params = torch.cat([p.detach().flatten() for p in ref.model.parameters()]).numpy()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_gat_shard_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_gat_shard_worker, args=(world, _free_port(), out, False, 2, 0.0, chunk), nprocs=world, join=True)
     for r in range(world):
         losses, res, params, hs, _ = out[r]
         np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
@@ -250,8 +253,8 @@ def test_sharded_gat_matches_single_process(world):
     np.testing.assert_array_equal(out[0][2], out[1][2])
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_fused_gat_matches_single_process(world):
+@pytest.mark.parametrize("world,chunk", [(2, 4 << 30), (4, 4 << 30), (2, 16 << 10), (4, 16 << 10)])
+def test_sharded_fused_gat_matches_single_process(world, chunk):
     """The fused GAT epoch (gat_fused: every dense op a HIP kernel on a GPU; its fp32
     reference branches here) sharded over gloo ranks equals the one-process fused
     model -- with dropout on, since the masks are keyed by the global row."""
@@ -267,7 +270,8 @@ def test_sharded_fused_gat_matches_single_process(world):
     ref_params = _gat_params(ref)
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_gat_shard_worker, args=(world, _free_port(), out, True, 4, 0.3), nprocs=world, join=True)
+    # chunk 16 KB: the halo exchanges run in several rounds (bounded staging memory)
+    mp.spawn(_gat_shard_worker, args=(world, _free_port(), out, True, 4, 0.3, chunk), nprocs=world, join=True)
     for r in range(world):
         losses, res, params, hs, grads1 = out[r]
         # first-step gradients (rank-summed): equal up to the summation order of the
