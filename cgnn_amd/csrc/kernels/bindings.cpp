@@ -80,6 +80,7 @@ int gnn_gat_row_ce_waves();
 int gnn_launch_gat_row_ce(const float*, int, const float*, int, const int*, const uint8_t*, float, float*, void*,
                           float*, float*, float*, float*, long, hipStream_t);
 int gnn_launch_gat_pack_grad(const float*, const float*, const float*, int, int, void*, int, long, hipStream_t);
+int gnn_launch_halo_rows(const void*, long, const long*, void*, long, const long*, long, int, int, hipStream_t);
 int gnn_fused_bwd_blocks(int);
 int gnn_fused_bwd_width(int);
 int gnn_fused_bwd_supported(int, int, int);
@@ -319,6 +320,11 @@ PYBIND11_MODULE(_hip, m) {
                                 long n, uint64_t st) {
     chk(gnn_launch_gat_pack_grad(Pt<const float>(dwh), Pt<const float>(dss), Pt<const float>(dsd), HF, K,
                                  Pt<void>(dy), ldy, n, S(st)), "gnn_gat_pack_grad");
+  });
+  m.def("gnn_halo_rows", [](uint64_t src, long sp, uint64_t sidx, uint64_t dst, long dp, uint64_t didx, long rows,
+                            int words, int mode, uint64_t st) {
+    chk(gnn_launch_halo_rows(Pt<const void>(src), sp, Pt<const long>(sidx), Pt<void>(dst), dp, Pt<const long>(didx),
+                             rows, words, mode, S(st)), "gnn_halo_rows");
   });
   m.def("gnn_fused_bwd_blocks", &gnn_fused_bwd_blocks);
   m.def("gnn_fused_bwd_width", &gnn_fused_bwd_width);

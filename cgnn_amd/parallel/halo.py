@@ -43,6 +43,37 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import torch
 
 
+def _rows(src: torch.Tensor, dst: torch.Tensor, src_idx=None, dst_idx=None, mode: int = 0):
+    """``dst[dst_idx[r] or r] (op)= src[src_idx[r] or r]`` for r < rows (= len of the index, or
+    of src): mode 0 copies (same dtype, 4-byte multiple rows), 1 adds fp32 into fp32, 2 adds
+    bf16 into fp32 (accumulate modes: distinct dst rows).  2-D operands with unit column
+    stride (column slices of row-major buffers are fine).  GPU: one HIP launch
+    (csrc/kernels/gnn_halo.hip); CPU: the same with index ops."""
+    rows = (src_idx.numel() if src_idx is not None else
+            dst_idx.numel() if dst_idx is not None else src.shape[0])
+    if rows == 0:
+        return
+    if dst.is_cuda:
+        from .. import native
+        words = dst.shape[1] if mode else dst.shape[1] * dst.element_size() // 4
+        native.hip().gnn_halo_rows(src.data_ptr(), src.stride(0) * src.element_size(),
+                                   src_idx.data_ptr() if src_idx is not None else 0, dst.data_ptr(),
+                                   dst.stride(0) * dst.element_size(),
+                                   dst_idx.data_ptr() if dst_idx is not None else 0, rows, words, mode,
+                                   torch.cuda.current_stream(dst.device).cuda_stream)
+        return
+    v = src.index_select(0, src_idx) if src_idx is not None else src[:rows]
+    if mode == 0:
+        if dst_idx is not None:
+            dst[dst_idx] = v
+        else:
+            dst[:rows] = v
+    elif dst_idx is not None:
+        dst.index_put_((dst_idx,), v.to(dst.dtype), accumulate=True)
+    else:
+        dst[:rows] += v.to(dst.dtype)
+
+
 class HaloExchange:
     def __init__(self, col: torch.Tensor, r0: int, r1: int, per: int, n: int, group=None,
                  emulate: Optional[Tuple[int, int]] = None, max_row_bytes: int = 1024,
@@ -164,17 +195,21 @@ class HaloExchange:
             e[:self.nloc] = p
             ext.append(e)
         nbytes = [p.shape[1] * p.element_size() for p in parts]
+        W = sum(nbytes)
         for t in range(self.rounds):
             lo, hi = self.ext_range(t)
             idx = self._send_idx_r[t]
-            send = torch.cat([p.index_select(0, idx).view(torch.uint8) for p in parts], 1) if idx.numel() else \
-                torch.empty(0, sum(nbytes), dtype=torch.uint8, device=self.dev)
-            recv = torch.empty(hi - lo, sum(nbytes), dtype=torch.uint8, device=self.dev)
+            send = torch.empty(idx.numel(), W, dtype=torch.uint8, device=self.dev)
+            c = 0
+            for p, nb in zip(parts, nbytes):                   # gather the requested rows
+                _rows(p.view(torch.uint8), send[:, c:c + nb], src_idx=idx)
+                c += nb
+            recv = torch.empty(hi - lo, W, dtype=torch.uint8, device=self.dev)
             self._all_to_all(recv, send, self._sizes(self._recv_r[t]), self._sizes(self._send_r[t]))
             del send
             c = 0
-            for e, p, nb in zip(ext, parts, nbytes):
-                e[lo:hi] = recv[:, c:c + nb].contiguous().view(p.dtype)
+            for e, nb in zip(ext, nbytes):                     # unpack into this round's block
+                _rows(recv[:, c:c + nb], e.view(torch.uint8)[lo:hi])
                 c += nb
             del recv
         return ext
@@ -201,23 +236,32 @@ class HaloExchange:
         widths = [o.shape[1] for o in own]
         for t in range(self.rounds):
             lo, hi = self.ext_range(t)
+            send = torch.empty(hi - lo, sum(widths), dtype=wire_dtype, device=self.dev)
             if hi > lo:
                 got = produce(lo, hi)
-                send = got[0].to(wire_dtype) if len(got) == 1 else torch.cat([g.to(wire_dtype) for g in got], 1)
+                c = 0
+                for g, w in zip(got, widths):
+                    if g.dtype == wire_dtype:
+                        _rows(g, send[:, c:c + w])
+                    else:
+                        send[:, c:c + w].copy_(g)
+                    c += w
                 del got
-            else:
-                send = torch.empty(0, sum(widths), dtype=wire_dtype, device=self.dev)
             idx = self._send_idx_r[t]
             back = torch.empty(idx.numel(), sum(widths), dtype=wire_dtype, device=self.dev)
-            self._all_to_all(back, send.contiguous(), self._sizes(self._send_r[t]), self._sizes(self._recv_r[t]))
+            self._all_to_all(back, send, self._sizes(self._send_r[t]), self._sizes(self._recv_r[t]))
             del send
+            mode = 2 if wire_dtype == torch.bfloat16 else 1
             a = 0
             for p, n_p in enumerate(self._sizes(self._send_r[t])):
-                if n_p:
+                if n_p:                                   # one peer's rows are distinct: no conflicts
                     rows = idx[a:a + n_p]
                     c = 0
                     for g, w in zip(own, widths):
-                        g.index_put_((rows,), back[a:a + n_p, c:c + w].to(g.dtype), accumulate=True)
+                        if g.dtype != torch.float32:
+                            g.index_put_((rows,), back[a:a + n_p, c:c + w].to(g.dtype), accumulate=True)
+                        else:
+                            _rows(back[a:a + n_p, c:c + w], g, dst_idx=rows, mode=mode)
                         c += w
                 a += n_p
             del back
