@@ -81,6 +81,10 @@ int gnn_launch_gat_row_ce(const float*, int, const float*, int, const int*, cons
                           float*, float*, float*, float*, long, hipStream_t);
 int gnn_launch_gat_pack_grad(const float*, const float*, const float*, int, int, void*, int, long, hipStream_t);
 int gnn_launch_halo_rows(const void*, long, const long*, void*, long, const long*, long, int, int, hipStream_t);
+long gnn_sample_blocks_scratch(int, int, const int*, const int*);
+int gnn_launch_sample_blocks(const int*, const int*, int, const int*, int, int, const int*, const int*, int* const*,
+                             float* const*, int* const*, int* const*, int* const*, int* const*, int* const*,
+                             int* const*, int*, uint8_t*, int*, int*, uint32_t, uint32_t, uint32_t, hipStream_t);
 int gnn_fused_bwd_blocks(int);
 int gnn_fused_bwd_width(int);
 int gnn_fused_bwd_supported(int, int, int);
@@ -325,6 +329,34 @@ PYBIND11_MODULE(_hip, m) {
                             int words, int mode, uint64_t st) {
     chk(gnn_launch_halo_rows(Pt<const void>(src), sp, Pt<const long>(sidx), Pt<void>(dst), dp, Pt<const long>(didx),
                              rows, words, mode, S(st)), "gnn_halo_rows");
+  });
+  m.def("gnn_sample_blocks_scratch", [](int n, std::vector<int> fan, std::vector<int> nd_max) {
+    if (fan.size() != nd_max.size()) throw std::runtime_error("gnn_sample_blocks_scratch: list lengths differ");
+    return gnn_sample_blocks_scratch(n, (int)fan.size(), fan.data(), nd_max.data());
+  });
+  // whole mini-batch sampling pipeline (gnn_sampler.hip): per-level pointer lists
+  m.def("gnn_sample_blocks", [](uint64_t rowptr, uint64_t col, int n, uint64_t seeds, int n_seeds,
+                                std::vector<int> fan, std::vector<int> nd_max, std::vector<uint64_t> optr,
+                                std::vector<uint64_t> inv_deg, std::vector<uint64_t> picks, std::vector<uint64_t> local,
+                                std::vector<uint64_t> src, std::vector<uint64_t> rp_t, std::vector<uint64_t> col_t,
+                                std::vector<uint64_t> cnt_t, uint64_t counts, uint64_t flag, uint64_t map,
+                                uint64_t bscratch, uint32_t k0, uint32_t k1, uint32_t salt, uint64_t st) {
+    const size_t L = fan.size();
+    if (nd_max.size() != L || optr.size() != L || inv_deg.size() != L || picks.size() != L || local.size() != L ||
+        src.size() != L || rp_t.size() != L || col_t.size() != L || cnt_t.size() != L)
+      throw std::runtime_error("gnn_sample_blocks: per-level lists differ in length");
+    auto ip = [](const std::vector<uint64_t>& v) {
+      std::vector<int*> o(v.size());
+      for (size_t i = 0; i < v.size(); ++i) o[i] = reinterpret_cast<int*>(v[i]);
+      return o;
+    };
+    std::vector<float*> inv(L);
+    for (size_t i = 0; i < L; ++i) inv[i] = reinterpret_cast<float*>(inv_deg[i]);
+    auto a = ip(optr), b = ip(picks), c = ip(local), d = ip(src), e = ip(rp_t), f = ip(col_t), g = ip(cnt_t);
+    chk(gnn_launch_sample_blocks(Pt<const int>(rowptr), Pt<const int>(col), n, Pt<const int>(seeds), n_seeds,
+                                 (int)L, fan.data(), nd_max.data(), a.data(), inv.data(), b.data(), c.data(),
+                                 d.data(), e.data(), f.data(), g.data(), Pt<int>(counts), Pt<uint8_t>(flag),
+                                 Pt<int>(map), Pt<int>(bscratch), k0, k1, salt, S(st)), "gnn_sample_blocks");
   });
   m.def("gnn_fused_bwd_blocks", &gnn_fused_bwd_blocks);
   m.def("gnn_fused_bwd_width", &gnn_fused_bwd_width);

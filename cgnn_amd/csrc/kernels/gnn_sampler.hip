@@ -11,6 +11,7 @@
 //                             does not depend on the batch it is in or on the
 //                             thread that draws it).
 #include "cgnn_common.h"
+#include <algorithm>
 
 using namespace cgnn;
 
@@ -18,7 +19,9 @@ template <int MAXF>
 __global__ __launch_bounds__(256) void sample_neighbors_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ nodes, int n,
     int fanout, const int* __restrict__ out_ptr, int* __restrict__ out_col, uint32_t k0, uint32_t k1,
-    uint32_t salt) {
+    uint32_t salt, const int* __restrict__ n_dev) {
+  // n_dev (optional): the row count lives in device memory (the grid covers an upper bound)
+  if (n_dev) n = *n_dev;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int v = nodes[i];
@@ -49,11 +52,356 @@ extern "C" int gnn_launch_sample_neighbors(const int* rowptr, const int* col, co
   dim3 grid((n + 255) / 256), block(256);
   if (fanout <= 16)
     hipLaunchKernelGGL((sample_neighbors_kernel<16>), grid, block, 0, st, rowptr, col, nodes, n, fanout, out_ptr,
-                       out_col, k0, k1, salt);
+                       out_col, k0, k1, salt, (const int*)nullptr);
   else if (fanout <= 64)
     hipLaunchKernelGGL((sample_neighbors_kernel<64>), grid, block, 0, st, rowptr, col, nodes, n, fanout, out_ptr,
-                       out_col, k0, k1, salt);
+                       out_col, k0, k1, salt, (const int*)nullptr);
   else
     return -3;
+  return (int)hipGetLastError();
+}
+
+// ============================================================================
+// Whole mini-batch sampling pipeline without host synchronisation
+// (gnn_sample_blocks, driven from C++): for every level the row counts live in
+// device memory and every grid covers a host-known upper bound, so the host
+// enqueues all levels at once and learns the sizes with ONE copy at the end --
+// on a side stream, while the previous batch trains.
+//
+// Level l (destinations = seeds for l = 0, else the sources of level l - 1):
+//   count_scan    cnt = min(deg, fanout), exclusive scan -> rowptr, 1 / cnt,
+//                 total picks                                   (one block)
+//   sample        Floyd picks (sample_neighbors_kernel, device row count)
+//   mark          flag[pick] = 1
+//   dst_fix       flag[dst] = 0, map[dst] = i, src[i] = dst
+//   flag_scan     per 4096-id block counts, scan of the block counts (one
+//                 block; n_src = n_dst + new sources), then compaction: the new
+//                 sources in increasing id order -> src[n_dst + k], map, flag = 0
+//   relabel       local[e] = map[pick[e]]
+//   transpose     (blocks the backward scatters through) histogram, scan,
+//                 per-destination scatter, per-bucket insertion sort: the
+//                 transposed CSR in increasing destination order (deterministic)
+// No state needs resetting between levels or batches: every flag set is cleared
+// by dst_fix / compaction, and map entries are only read for ids set this level.
+// ============================================================================
+namespace {
+constexpr int SCAN_T = 1024;
+constexpr int FLAG_BLK = 4096;
+
+// exclusive scan of v(i), i < n, by one block (thread t owns a contiguous chunk);
+// out[i] = prefix, out[n] = total; returns nothing (total also in *total if given)
+template <class V>
+__device__ void block_scan(int n, V v, int* __restrict__ out, int* __restrict__ total) {
+  __shared__ int part[SCAN_T];
+  const int t = threadIdx.x;
+  const int chunk = (n + SCAN_T - 1) / SCAN_T;
+  const int a = min(n, t * chunk), b = min(n, a + chunk);
+  int s = 0;
+  for (int i = a; i < b; ++i) s += v(i);
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < SCAN_T; off <<= 1) {          // Hillis-Steele inclusive scan
+    const int x = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  int run = part[t] - s;                               // exclusive prefix of this chunk
+  for (int i = a; i < b; ++i) {
+    out[i] = run;
+    run += v(i);
+  }
+  if (t == SCAN_T - 1) {
+    out[n] = part[t];
+    if (total) *total = part[t];
+  }
+}
+}  // namespace
+
+// ---- multi-block exclusive scans with a device-side length (grid over an upper bound):
+// A: values of a 1024-element block -> vals[], block sum -> bsum[b]
+// B: one block scans the block sums -> boff[], total -> *total and out[n]
+// C: block-local scan of vals + boff[b] -> out[]
+constexpr int SB = 1024;          // elements per scan block (256 threads x 4)
+
+__device__ __forceinline__ int block_excl_scan4(int v0, int v1, int v2, int v3, int* tot, int* shw) {
+  // 256 threads x 4 consecutive items: returns the exclusive prefix of this thread's
+  // first item within the block; *tot = block total
+  const int s = v0 + v1 + v2 + v3;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) shw[w] = x;
+  __syncthreads();
+  int wo = 0;
+  for (int q = 0; q < w; ++q) wo += shw[q];
+  *tot = shw[0] + shw[1] + shw[2] + shw[3];
+  return wo + x - s;
+}
+
+// count values: cnt = min(deg(node), fanout) (also 1 / cnt) or an int array (reset to 0)
+__global__ __launch_bounds__(256) void sb_scanA_kernel(const int* __restrict__ rowptr, const int* __restrict__ nodes,
+                                                       int fanout, float* __restrict__ inv_deg, int* __restrict__ arr,
+                                                       int n_host, const int* __restrict__ n_dev,
+                                                       int* __restrict__ vals, int* __restrict__ bsum) {
+  __shared__ int shw[4];
+  const int n = n_dev ? *n_dev : n_host;
+  const int base = blockIdx.x * SB;
+  if (base >= n && blockIdx.x > 0) return;
+  int v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = base + 4 * threadIdx.x + q;
+    int x = 0;
+    if (i < n) {
+      if (nodes) {
+        const int nd = nodes[i];
+        const int d = rowptr[nd + 1] - rowptr[nd];
+        x = fanout < 0 ? d : min(d, fanout);
+        inv_deg[i] = x > 0 ? 1.f / (float)x : 0.f;
+      } else {
+        x = arr[i];
+        arr[i] = 0;                  // the histogram becomes the scatter cursor
+      }
+      vals[i] = x;
+    }
+    v[q] = x;
+  }
+  int tot;
+  (void)block_excl_scan4(v[0], v[1], v[2], v[3], &tot, shw);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_T) void sb_scanB_kernel(const int* __restrict__ bsum, int n_host,
+                                                          const int* __restrict__ n_dev, int* __restrict__ boff,
+                                                          int* __restrict__ out, int* __restrict__ total) {
+  __shared__ int tot;
+  const int n = n_dev ? *n_dev : n_host;
+  const int nb = (n + SB - 1) / SB;
+  auto v = [&](int i) { return bsum[i]; };
+  block_scan(nb, v, boff, &tot);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[n] = tot;
+    if (total) *total = tot;
+  }
+}
+
+__global__ __launch_bounds__(256) void sb_scanC_kernel(const int* __restrict__ vals, const int* __restrict__ boff,
+                                                       int n_host, const int* __restrict__ n_dev,
+                                                       int* __restrict__ out) {
+  __shared__ int shw[4];
+  const int n = n_dev ? *n_dev : n_host;
+  const int base = blockIdx.x * SB;
+  if (base >= n) return;
+  int v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = base + 4 * threadIdx.x + q;
+    v[q] = i < n ? vals[i] : 0;
+  }
+  int tot;
+  int run = boff[blockIdx.x] + block_excl_scan4(v[0], v[1], v[2], v[3], &tot, shw);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = base + 4 * threadIdx.x + q;
+    if (i < n) out[i] = run;
+    run += v[q];
+  }
+}
+
+__global__ __launch_bounds__(256) void sb_mark_kernel(const int* __restrict__ picks, const int* __restrict__ total,
+                                                      uint8_t* __restrict__ flag) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < *total) flag[picks[e]] = 1;
+}
+
+__global__ __launch_bounds__(256) void sb_dst_fix_kernel(const int* __restrict__ nodes, int n_host,
+                                                         const int* __restrict__ n_dev, uint8_t* __restrict__ flag,
+                                                         int* __restrict__ map, int* __restrict__ src) {
+  const int n = n_dev ? *n_dev : n_host;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int v = nodes[i];
+  flag[v] = 0;
+  map[v] = i;
+  src[i] = v;
+}
+
+__global__ __launch_bounds__(256) void sb_flag_count_kernel(const uint8_t* __restrict__ flag, int n,
+                                                            int* __restrict__ bcount) {
+  __shared__ int ws[4];
+  const int base = blockIdx.x * FLAG_BLK;
+  int s = 0;
+  for (int i = base + threadIdx.x; i < min(n, base + FLAG_BLK); i += 256) s += flag[i];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) bcount[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// exclusive scan of the block counts; n_src = n_dst + new sources
+__global__ __launch_bounds__(SCAN_T) void sb_block_scan_kernel(const int* __restrict__ bcount, int nb,
+                                                               int* __restrict__ boff, int n_dst_host,
+                                                               const int* __restrict__ n_dst_dev,
+                                                               int* __restrict__ n_src) {
+  __shared__ int tot;
+  auto v = [&](int i) { return bcount[i]; };
+  block_scan(nb, v, boff, &tot);
+  __syncthreads();
+  if (threadIdx.x == 0) *n_src = (n_dst_dev ? *n_dst_dev : n_dst_host) + tot;
+}
+
+// the new sources of each 4096-id block in increasing id order (wave ballots)
+__global__ __launch_bounds__(256) void sb_compact_kernel(uint8_t* __restrict__ flag, int n,
+                                                         const int* __restrict__ boff, int n_dst_host,
+                                                         const int* __restrict__ n_dst_dev, int* __restrict__ map,
+                                                         int* __restrict__ src) {
+  __shared__ int wsum[4];
+  const int nd = n_dst_dev ? *n_dst_dev : n_dst_host;
+  const int base = blockIdx.x * FLAG_BLK;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int run = boff[blockIdx.x];
+  for (int c0 = base; c0 < min(n, base + FLAG_BLK); c0 += 256) {
+    const int i = c0 + threadIdx.x;
+    const bool f = i < n && flag[i];
+    const unsigned long long bal = __ballot(f);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int woff = 0;
+    for (int q = 0; q < w; ++q) woff += wsum[q];
+    const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (f) {
+      const int k = run + woff + before;
+      map[i] = nd + k;
+      src[nd + k] = i;
+      flag[i] = 0;
+    }
+    run += tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void sb_relabel_kernel(const int* __restrict__ picks, const int* __restrict__ total,
+                                                         const int* __restrict__ map, int* __restrict__ local) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < *total) local[e] = map[picks[e]];
+}
+
+__global__ __launch_bounds__(256) void sb_hist_kernel(const int* __restrict__ local, const int* __restrict__ total,
+                                                      int* __restrict__ cnt) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < *total) atomicAdd(&cnt[local[e]], 1);
+}
+
+__global__ __launch_bounds__(256) void sb_scatter_kernel(const int* __restrict__ optr, const int* __restrict__ local,
+                                                         int n_host, const int* __restrict__ n_dev,
+                                                         const int* __restrict__ rp_t, int* __restrict__ cursor,
+                                                         int* __restrict__ col_t) {
+  const int n = n_dev ? *n_dev : n_host;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int e = optr[i]; e < optr[i + 1]; ++e) {
+    const int c = local[e];
+    col_t[rp_t[c] + atomicAdd(&cursor[c], 1)] = i;
+  }
+}
+
+__global__ __launch_bounds__(256) void sb_bucket_sort_kernel(const int* __restrict__ rp_t,
+                                                             const int* __restrict__ n_dev, int* __restrict__ col_t) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= *n_dev) return;
+  const int a = rp_t[c], b = rp_t[c + 1];
+  for (int i = a + 1; i < b; ++i) {
+    const int x = col_t[i];
+    int j = i - 1;
+    while (j >= a && col_t[j] > x) {
+      col_t[j + 1] = col_t[j];
+      --j;
+    }
+    col_t[j + 1] = x;
+  }
+}
+
+static unsigned blocks_for(long n, int t = 256) { return (unsigned)std::max(1L, (n + t - 1) / t); }
+
+// int32 scratch the pipeline needs (bscratch argument of gnn_launch_sample_blocks)
+extern "C" long gnn_sample_blocks_scratch(int n, int L, const int* fan, const int* nd_max) {
+  const long nb = (n + FLAG_BLK - 1) / FLAG_BLK;
+  long vmax = 1;
+  for (int l = 0; l < L; ++l) vmax = std::max(vmax, std::min<long>((long)nd_max[l] * (fan[l] + 1), (long)n) + 1);
+  const long sbmax = (vmax + SB - 1) / SB + 1;
+  return 2 * nb + 2 + 2 * sbmax + vmax;
+}
+
+// One level per entry of the arrays (L levels): nd_max[l] bounds the destinations,
+// fan[l] the fanout; dst of level 0 = seeds (n_seeds on the host), of level l > 0 =
+// src[l - 1] with its device count counts[2 (l - 1)].  counts[2 l] = n_src of level
+// l, counts[2 l + 1] = its picks.  Transposed CSR built for levels with rp_t[l] != 0.
+extern "C" int gnn_launch_sample_blocks(const int* rowptr, const int* col, int n, const int* seeds, int n_seeds,
+                                        int L, const int* fan, const int* nd_max, int* const* optr,
+                                        float* const* inv_deg, int* const* picks, int* const* local,
+                                        int* const* src, int* const* rp_t, int* const* col_t, int* const* cnt_t,
+                                        int* counts, uint8_t* flag, int* map, int* bscratch, uint32_t k0,
+                                        uint32_t k1, uint32_t salt, hipStream_t st) {
+  const int nb = (n + FLAG_BLK - 1) / FLAG_BLK;
+  // scan scratch after the flag-scan counts: block sums, block offsets, values
+  long vmax = 1;
+  for (int l = 0; l < L; ++l) vmax = std::max(vmax, std::min<long>((long)nd_max[l] * (fan[l] + 1), (long)n) + 1);
+  const long sbmax = (vmax + SB - 1) / SB + 1;
+  int* sbsum = bscratch + 2 * nb + 2;
+  int* sboff = sbsum + sbmax;
+  int* svals = sboff + sbmax;
+  for (int l = 0; l < L; ++l) {
+    const int fo = fan[l];
+    if (fo < 1 || fo > 64) return -3;
+    const int* nodes = l == 0 ? seeds : src[l - 1];
+    const int* nd_dev = l == 0 ? nullptr : counts + 2 * (l - 1);
+    const int ndh = l == 0 ? n_seeds : 0;
+    int* total = counts + 2 * l + 1;
+    int* nsrc = counts + 2 * l;
+    const long pmax = (long)nd_max[l] * fo;
+    // rowptr of the level: exclusive scan of min(deg, fanout) (+ 1 / cnt, total picks)
+    const unsigned nbs = blocks_for(nd_max[l], SB);
+    hipLaunchKernelGGL(sb_scanA_kernel, dim3(nbs), dim3(256), 0, st, rowptr, nodes, fo, inv_deg[l], (int*)nullptr,
+                       ndh, nd_dev, svals, sbsum);
+    hipLaunchKernelGGL(sb_scanB_kernel, dim3(1), dim3(SCAN_T), 0, st, sbsum, ndh, nd_dev, sboff, optr[l], total);
+    hipLaunchKernelGGL(sb_scanC_kernel, dim3(nbs), dim3(256), 0, st, svals, sboff, ndh, nd_dev, optr[l]);
+    const uint32_t lsalt = salt * 16u + (uint32_t)l;
+    if (fo <= 16)
+      hipLaunchKernelGGL((sample_neighbors_kernel<16>), dim3(blocks_for(nd_max[l])), dim3(256), 0, st, rowptr, col,
+                         nodes, ndh, fo, optr[l], picks[l], k0, k1, lsalt, nd_dev);
+    else
+      hipLaunchKernelGGL((sample_neighbors_kernel<64>), dim3(blocks_for(nd_max[l])), dim3(256), 0, st, rowptr, col,
+                         nodes, ndh, fo, optr[l], picks[l], k0, k1, lsalt, nd_dev);
+    hipLaunchKernelGGL(sb_mark_kernel, dim3(blocks_for(pmax)), dim3(256), 0, st, picks[l], total, flag);
+    hipLaunchKernelGGL(sb_dst_fix_kernel, dim3(blocks_for(nd_max[l])), dim3(256), 0, st, nodes, ndh, nd_dev, flag,
+                       map, src[l]);
+    hipLaunchKernelGGL(sb_flag_count_kernel, dim3(nb), dim3(256), 0, st, flag, n, bscratch);
+    hipLaunchKernelGGL(sb_block_scan_kernel, dim3(1), dim3(SCAN_T), 0, st, bscratch, nb, bscratch + nb + 1, ndh,
+                       nd_dev, nsrc);
+    hipLaunchKernelGGL(sb_compact_kernel, dim3(nb), dim3(256), 0, st, flag, n, bscratch + nb + 1, ndh, nd_dev, map,
+                       src[l]);
+    hipLaunchKernelGGL(sb_relabel_kernel, dim3(blocks_for(pmax)), dim3(256), 0, st, picks[l], total, map, local[l]);
+    if (rp_t[l]) {
+      const long smax = std::min<long>((long)nd_max[l] * (fo + 1), (long)n);
+      (void)hipMemsetAsync(cnt_t[l], 0, sizeof(int) * (size_t)smax, st);
+      hipLaunchKernelGGL(sb_hist_kernel, dim3(blocks_for(pmax)), dim3(256), 0, st, local[l], total, cnt_t[l]);
+      const unsigned nbt = blocks_for(smax, SB);
+      hipLaunchKernelGGL(sb_scanA_kernel, dim3(nbt), dim3(256), 0, st, (const int*)nullptr, (const int*)nullptr, 0,
+                         (float*)nullptr, cnt_t[l], 0, nsrc, svals, sbsum);
+      hipLaunchKernelGGL(sb_scanB_kernel, dim3(1), dim3(SCAN_T), 0, st, sbsum, 0, nsrc, sboff, rp_t[l],
+                         (int*)nullptr);
+      hipLaunchKernelGGL(sb_scanC_kernel, dim3(nbt), dim3(256), 0, st, svals, sboff, 0, nsrc, rp_t[l]);
+      hipLaunchKernelGGL(sb_scatter_kernel, dim3(blocks_for(nd_max[l])), dim3(256), 0, st, optr[l], local[l], ndh,
+                         nd_dev, rp_t[l], cnt_t[l], col_t[l]);
+      hipLaunchKernelGGL(sb_bucket_sort_kernel, dim3(blocks_for(smax)), dim3(256), 0, st, rp_t[l], nsrc, col_t[l]);
+    }
+  }
   return (int)hipGetLastError();
 }

@@ -347,11 +347,17 @@ class SAGETrainer:
         self._col = g.col.cpu().numpy()
         self._full = None
         self.prefetch = bool(prefetch)
-        self.sampler = sampler or ("device" if self.dev.type == "cuda" else "host")
+        # "pipelined" (default on a GPU): the native whole-batch sampler on a side stream,
+        # double-buffered; "device": the per-level HIP sampler; "host": C++/OpenMP
+        self.sampler = sampler or ("pipelined" if self.dev.type == "cuda" else "host")
         self._dsampler = None
+        self._psampler = None
         if self.fanouts and self.sampler == "device":
             from .sampler import DeviceSampler
             self._dsampler = DeviceSampler(g.rowptr, g.col, self.fanouts[:layers], seed)
+        if self.fanouts and self.sampler == "pipelined":
+            from .sampler import PipelinedSampler
+            self._psampler = PipelinedSampler(g.rowptr, g.col, self.fanouts[:layers], batch_size, seed)
         self.epoch = 0
         if self.fused:
             if not self.x.dtype == torch.bfloat16:
@@ -381,12 +387,6 @@ class SAGETrainer:
         self._col = g.col.cpu().numpy()
         self._full = None
         self.prefetch = bool(prefetch)
-        # "device": HIP sampler on the resident CSR (default on a GPU); "host": C++/OpenMP
-        self.sampler = sampler or ("device" if self.dev.type == "cuda" else "host")
-        self._dsampler = None
-        if self.fanouts and self.sampler == "device":
-            from .sampler import DeviceSampler
-            self._dsampler = DeviceSampler(g.rowptr, g.col, self.fanouts[:layers], seed)
         self.epoch = 0
 
     # ----------------------------------------------------------- blocks
@@ -414,7 +414,7 @@ class SAGETrainer:
             loss = self._fused.step(blocks, nodes_in.to(torch.int32), self.y32[seeds_t.long()], self.world)
             return loss[0] / max(int(seeds_t.numel()), 1)
         self.model.train()
-        out = self.model(self.x[nodes_in], blocks)
+        out = self.model(self.x[nodes_in.long()], blocks)
         loss = torch.nn.functional.cross_entropy(out[:, :self.C], self.g.y[seeds_t].long())
         self.opt.zero_grad(set_to_none=True)
         loss.backward()
@@ -459,7 +459,24 @@ class SAGETrainer:
             return float(loss)
         batches = self._batches()
         losses = []
-        if self._dsampler is not None:
+        if self._psampler is not None and batches:
+            ps = self._psampler
+            # the epoch's seeds uploaded once; batch k + 1 samples on the side stream while k trains
+            flat = torch.as_tensor(np.concatenate(batches).astype(np.int32), device=self.dev)
+            seeds, o = [], 0
+            for b in batches:
+                seeds.append(flat[o:o + len(b)])
+                o += len(b)
+            salt = lambda k: (self.epoch * 100003 + k) * self.world + self.rank
+            pend = ps.enqueue(seeds[0], salt(0))
+            for k in range(len(batches)):
+                nxt = ps.enqueue(seeds[k + 1], salt(k + 1)) if k + 1 < len(batches) else None
+                blocks, nodes_in = pend.resolve()
+                torch.cuda.current_stream(self.dev).wait_event(pend.slot.done)
+                losses.append(self._step(blocks, nodes_in, seeds[k]))
+                ps.consumed(pend)
+                pend = nxt
+        elif self._dsampler is not None:
             for k, b in enumerate(batches):
                 seeds_t = torch.as_tensor(b, device=self.dev)
                 blocks, nodes_in = self._dsampler.sample(seeds_t, (self.epoch * 100003 + k) * self.world + self.rank)

@@ -36,15 +36,19 @@ def _st(t):
 
 class DeviceBlock:
     """Bipartite block (GPU tensors): ``n_dst`` rows over ``n_src`` sources; the
-    destinations are the first ``n_dst`` sources.  Same interface as ``sage.Block``."""
+    destinations are the first ``n_dst`` sources.  Same interface as ``sage.Block``.
+    ``inv_deg`` / ``transposed`` may be given precomputed (the pipelined sampler
+    builds both on the device)."""
 
-    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n_src: int):
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n_src: int, inv_deg=None, transposed=None):
         self.rowptr, self.col = rowptr, col
         self.n_dst = rowptr.numel() - 1
         self.n_src = int(n_src)
-        deg = (rowptr[1:] - rowptr[:-1]).float()
-        self.inv_deg = torch.where(deg > 0, 1.0 / deg.clamp_min(1), torch.zeros_like(deg))
-        self._t = None
+        if inv_deg is None:
+            deg = (rowptr[1:] - rowptr[:-1]).float()
+            inv_deg = torch.where(deg > 0, 1.0 / deg.clamp_min(1), torch.zeros_like(deg))
+        self.inv_deg = inv_deg
+        self._t = transposed
 
     def transposed(self):
         if self._t is None:
@@ -146,3 +150,132 @@ def sample_reference(rowptr: np.ndarray, col: np.ndarray, seeds: np.ndarray, fan
         out_blocks.append((np.asarray(rp, dtype=np.int32), local, src))
         nodes = src
     return out_blocks
+
+
+class _Slot:
+    """Device buffers of one in-flight mini-batch (upper-bound sizes)."""
+
+    def __init__(self, dev, n, batch, fanouts, need_t):
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.nd_max = []
+        nd = batch
+        for fo in fanouts:
+            self.nd_max.append(nd)
+            nd = min(nd * (fo + 1), n)
+        self.optr, self.inv, self.picks, self.local, self.src = [], [], [], [], []
+        self.rp_t, self.col_t, self.cnt_t = [], [], []
+        for l, fo in enumerate(fanouts):
+            ndm = self.nd_max[l]
+            smax = min(ndm * (fo + 1), n)
+            self.optr.append(torch.zeros(ndm + 1, **i32))
+            self.inv.append(torch.zeros(ndm, dtype=torch.float32, device=dev))
+            self.picks.append(torch.zeros(max(ndm * fo, 1), **i32))
+            self.local.append(torch.zeros(max(ndm * fo, 1), **i32))
+            self.src.append(torch.zeros(smax, **i32))
+            if need_t[l]:
+                self.rp_t.append(torch.zeros(smax + 1, **i32))
+                self.col_t.append(torch.zeros(max(ndm * fo, 1), **i32))
+                self.cnt_t.append(torch.zeros(smax, **i32))
+            else:
+                self.rp_t.append(None)
+                self.col_t.append(None)
+                self.cnt_t.append(None)
+        self.counts = torch.zeros(2 * len(fanouts), **i32)
+        self.counts_host = torch.zeros(2 * len(fanouts), dtype=torch.int32).pin_memory()
+        self.done = None          # event: the sampling of this slot's batch finished
+        self.free = None          # event: the training that read this slot finished
+
+
+class SampledBatch:
+    """A mini-batch whose blocks are being sampled on the side stream; ``resolve()``
+    waits for that work only and returns (blocks input layer first, input node ids
+    int32) with host-known sizes."""
+
+    def __init__(self, slot, fanouts, n_seeds):
+        self.slot, self.fanouts, self.n_seeds = slot, fanouts, n_seeds
+        self._res = None
+
+    def resolve(self):
+        if self._res is None:
+            sl = self.slot
+            sl.done.synchronize()
+            c = sl.counts_host.tolist()
+            blocks = []
+            nd = self.n_seeds
+            for l in range(len(self.fanouts)):
+                n_src, total = int(c[2 * l]), int(c[2 * l + 1])
+                t = None
+                if sl.rp_t[l] is not None:
+                    t = (sl.rp_t[l][:n_src + 1], sl.col_t[l][:total])
+                blocks.append(DeviceBlock(sl.optr[l][:nd + 1], sl.local[l][:total], n_src,
+                                          inv_deg=sl.inv[l][:nd], transposed=t))
+                nd = n_src
+            self._res = (blocks[::-1], sl.src[-1][:nd])
+        return self._res
+
+
+class PipelinedSampler:
+    """The whole multi-level sampling of a mini-batch as ONE native call
+    (``gnn_sample_blocks``: ~10 HIP kernels per level, device-side row counts, no
+    host synchronisation) on a side stream, double-buffered: batch k + 1 is
+    sampled while batch k trains, and the host reads the level sizes with one
+    pinned copy.  Same draws and relabelling as :class:`DeviceSampler` (bitwise
+    equal blocks); the transposed CSRs the backward needs (every block but the
+    input layer's) are built on the device too, deterministically (histogram,
+    scan, scatter, per-bucket sort)."""
+
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, fanouts: Sequence[int], batch: int, seed: int = 0,
+                 slots: int = 2):
+        if not rowptr.is_cuda:
+            raise ValueError("PipelinedSampler needs the CSR on a GPU")
+        self.rowptr, self.col = rowptr.contiguous(), col.contiguous()
+        self.dev = rowptr.device
+        self.n = rowptr.numel() - 1
+        self.fanouts = [int(f) for f in fanouts]
+        if any(f > 64 or f < 1 for f in self.fanouts):
+            raise ValueError("device sampler fanouts must be in 1..64")
+        self.batch = int(batch)
+        self.key = model_key(seed, "neighbour-sampler")
+        L = len(self.fanouts)
+        need_t = [l < L - 1 for l in range(L)]
+        self.slots = [_Slot(self.dev, self.n, self.batch, self.fanouts, need_t) for _ in range(slots)]
+        self.flag = torch.zeros(self.n + 1, dtype=torch.uint8, device=self.dev)
+        self.map = torch.zeros(self.n + 1, dtype=torch.int32, device=self.dev)
+        ns = native.hip().gnn_sample_blocks_scratch(self.n, self.fanouts, self.slots[0].nd_max)
+        self.bscratch = torch.zeros(ns, dtype=torch.int32, device=self.dev)
+        self.stream = torch.cuda.Stream(device=self.dev)
+        self._next = 0
+
+    def enqueue(self, seeds: torch.Tensor, salt: int) -> SampledBatch:
+        """Start sampling ``seeds`` (int32 device tensor, <= batch) on the side stream."""
+        if seeds.numel() > self.batch:
+            raise ValueError("more seeds than the sampler's batch bound")
+        sl = self.slots[self._next]
+        self._next = (self._next + 1) % len(self.slots)
+        main = torch.cuda.current_stream(self.dev)
+        seeds = seeds.to(dtype=torch.int32).contiguous()
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_stream(main)            # the seeds were written on the main stream
+            if sl.free is not None:
+                self.stream.wait_event(sl.free)      # the slot's previous batch has trained
+            p = lambda ts: [t.data_ptr() if t is not None else 0 for t in ts]
+            native.hip().gnn_sample_blocks(
+                self.rowptr.data_ptr(), self.col.data_ptr(), self.n, seeds.data_ptr(), int(seeds.numel()),
+                self.fanouts, sl.nd_max, p(sl.optr), p(sl.inv), p(sl.picks), p(sl.local), p(sl.src), p(sl.rp_t),
+                p(sl.col_t), p(sl.cnt_t), sl.counts.data_ptr(), self.flag.data_ptr(), self.map.data_ptr(),
+                self.bscratch.data_ptr(), int(self.key[0]), int(self.key[1]), int(salt) & 0xFFFFFFFF,
+                self.stream.cuda_stream)
+            sl.counts_host.copy_(sl.counts, non_blocking=True)
+            sl.done = torch.cuda.Event()
+            sl.done.record(self.stream)
+            seeds.record_stream(self.stream)
+        return SampledBatch(sl, self.fanouts, int(seeds.numel()))
+
+    def consumed(self, batch: SampledBatch):
+        """Mark the end of the training that reads ``batch`` (enqueued on the current
+        stream): the slot may be refilled after it."""
+        main = torch.cuda.current_stream(self.dev)
+        main.wait_event(batch.slot.done)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        batch.slot.free = ev

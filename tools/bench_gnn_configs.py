@@ -68,6 +68,8 @@ def main():
                     help="papers-gat2: one process plays rank --emulate-rank of this many ranks (its "
                          "rank-local shard, halo plan and buffers; received rows zero) -- memory / compute dry run")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--sampler", choices=["pipelined", "device", "host"], default=None,
+                    help="products-sage3: neighbour sampler (default: pipelined on a GPU)")
     ap.add_argument("--halo-grad-bf16", action="store_true", help="papers-gat2: gradients on the halo wire in bf16")
     ap.add_argument("--unfused", action="store_true", help="arxiv-gcn3 / products-sage3 / papers-gat2: autograd + hipBLASLt path (A/B)")
     a = ap.parse_args()
@@ -155,7 +157,8 @@ def main():
         steps, warmup = a.steps or 2, a.warmup or 1
         g = _graph("ogbn-products")
         tr = SAGETrainer(g, hidden=hidden, layers=3, dropout=0.5, lr=0.003, fanouts=(15, 10, 5),
-                         batch_size=1024, seed=a.seed, fused=False if a.unfused else None)
+                         batch_size=1024, seed=a.seed, fused=False if a.unfused else None,
+                         sampler=a.sampler)
         setup = time.perf_counter() - t_setup
         per_epoch = len(tr._batches())
         dt = _timed(tr.train_epoch, steps, warmup, dev)
@@ -164,6 +167,7 @@ def main():
         res.update(metric="epochs/sec + val-acc, 3-layer GraphSAGE ogbn-products mini-batch DP",
                    value=round(steps / dt, 4), unit="epochs/s", ms_per_step=round(1e3 * dt / steps, 3),
                    seeds_per_s=round(seeds / dt, 1), iterations_per_epoch=per_epoch, fused=bool(tr.fused),
+                   sampler=tr.sampler,
                    val_acc=round(ev["val_acc"], 4), test_acc=round(ev["test_acc"], 4),
                    dtype="bf16 (fp32 accumulation, fp32 master weights)" if dev.type == "cuda" else "fp32",
                    scaling="strong (fixed global epoch; per-rank batch 1024)",

@@ -1,0 +1,11 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r02_sage
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_sampler_gpu.py tests/test_gnn_gpu.py -x -v -k "sampler or sage" --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/bench_gnn_configs.py --config products-sage3 --steps 3 --warmup 1 > $O/sage_pipelined.log 2>&1 || exit 1
+timeout -k 10 300 python -u tools/bench_gnn_configs.py --config products-sage3 --steps 3 --warmup 1 --sampler device > $O/sage_device.log 2>&1 || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/sprof -o run -- python -u tools/bench_gnn_configs.py --config products-sage3 --steps 1 --warmup 1 > $O/prof.log 2>&1 || exit 1
+python tools/prof_summary.py --top 40 /tmp/sprof/run_results.db > $O/sage_pipelined_kernel_stats.csv
+echo done
