@@ -10,10 +10,15 @@ skeleton edge, in skeleton order:
 * absent (removed earlier): try adding u->v and v->u and keep the better one
   if it improves the score (:320-381).
 
-Loop until a full pass brings no improvement.  Candidates that do not depend
-on each other's outcome are scored in one batch: the reversal and the removal
-of the current orientation, and the two additions.  The removal of the
-*reversed* edge is scored afterwards only if the reversal was accepted.
+Loop until a full pass brings no improvement.  Speculative batching: the
+candidates of the next skeleton edges (reversal + removal, or the two additions)
+are built against the current graph and scored in ONE device batch (up to the
+evaluator's speculation width, e.g. 256 models / 32 runs = 8 candidates); the
+decisions are replayed in skeleton order and the window stops at the first
+structural change.  Scores depend only on (seed, run) (common random numbers),
+so the accepted sequence is exactly the sequential one.  (Removing the reversed
+edge gives the same graph as removing the original orientation, so one removal
+candidate covers both outcomes of the reversal test.)
 
 ``checkpoint=<path>``: the search state (graph, tested configurations, best
 score, confounder labels, pass number and position in the skeleton) is written
@@ -56,90 +61,125 @@ def hill_climbing_confounders(graph, data, run_cgnn_function=None, **kwargs):
         _say(cfg, "Graph score : " + str(globalscore))
         confounders = set()
         loop, start, improvement = 1, 0, False
-    while True:
-        for pos in range(start, len(skel_edges)):
-            u, v = skel_edges[pos]
-            if graph.has_edge(u, v) or graph.has_edge(v, u):
-                n1, n2 = (u, v) if graph.has_edge(u, v) else (v, u)
-                # --- reversal and removal of the current orientation, together
-                rev = copy.deepcopy(graph)
-                rev.reverse_edge(n1, n2)
-                rem = copy.deepcopy(graph)
-                rem.remove_edge(n1, n2)
-                cands = []
-                rev_ok = not rev.is_cyclic() and rev.canonical_key() not in tested
-                rem_ok = rem.canonical_key() not in tested
-                if rev_ok:
-                    cands.append(("rev", rev))
-                if rem_ok:
-                    cands.append(("rem", rem))
-                scores = dict(zip([c[0] for c in cands], ev([c[1] for c in cands]))) if cands else {}
-                if rev_ok:
-                    tested.add(rev.canonical_key())
-                    s = float(scores["rev"])
-                    _say(cfg, "Reverse edge %s -> %s : %s (best %s)" % (n1, n2, s, globalscore))
-                    if s < globalscore:
-                        graph.reverse_edge(n1, n2)
-                        improvement = True
-                        globalscore = s
-                        n1, n2 = n2, n1
-                        _say(cfg, "Edge %s -> %s got reversed !" % (n2, n1))
-                        # the removal candidate above removed the old orientation;
-                        # removing either orientation gives the same graph
-                # removal of the (possibly reversed) edge: same graph either way
-                rem_key = rem.canonical_key()
-                if rem_ok:
-                    tested.add(rem_key)
-                    s = float(scores["rem"])
-                    if s < globalscore:
-                        graph.remove_edge(n1, n2)
-                        improvement = True
-                        globalscore = s
-                        confounders.add(frozenset((n1, n2)))
-                        _say(cfg, "Edge %s -> %s got removed, possible confounder !" % (n1, n2))
-                    else:
-                        graph.set_weight(n1, n2, s - globalscore)
-                        _say(cfg, "Edge %s -> %s not removed. Score edge : %s" % (n1, n2, s - globalscore))
+    width = int(kwargs.get("speculation", 0) or ev.speculation_width())
+
+    def plan(pos):
+        """Candidates of skeleton edge ``pos`` against the current graph."""
+        u, v = skel_edges[pos]
+        it = {"pos": pos, "u": u, "v": v, "cands": []}
+        if graph.has_edge(u, v) or graph.has_edge(v, u):
+            n1, n2 = (u, v) if graph.has_edge(u, v) else (v, u)
+            it.update(kind="present", n1=n1, n2=n2)
+            rev = copy.deepcopy(graph)
+            rev.reverse_edge(n1, n2)
+            rem = copy.deepcopy(graph)
+            rem.remove_edge(n1, n2)
+            it["rev_ok"] = not rev.is_cyclic() and rev.canonical_key() not in tested
+            it["rem_ok"] = rem.canonical_key() not in tested
+            it["rem_key"] = rem.canonical_key()
+            if it["rev_ok"]:
+                it["cands"].append(["rev", rev, rev.canonical_key(), None])
+            if it["rem_ok"]:
+                it["cands"].append(["rem", rem, it["rem_key"], None])
+        else:
+            it["kind"] = "absent"
+            a_g = copy.deepcopy(graph)
+            a_g.add(u, v)
+            b_g = copy.deepcopy(graph)
+            b_g.add(v, u)
+            for tag, g in (("uv", a_g), ("vu", b_g)):
+                if not g.is_cyclic() and g.canonical_key() not in tested:
+                    it["cands"].append([tag, g, g.canonical_key(), None])
+        return it
+
+    def process(it):
+        """The reference's sequential decision for one edge (scores precomputed);
+        returns whether the graph's structure changed."""
+        nonlocal globalscore, improvement
+        sc = {c[0]: c[3] for c in it["cands"]}
+        for c in it["cands"]:
+            tested.add(c[2])
+        changed = False
+        if it["kind"] == "present":
+            n1, n2 = it["n1"], it["n2"]
+            if it["rev_ok"]:
+                s = float(sc["rev"])
+                _say(cfg, "Reverse edge %s -> %s : %s (best %s)" % (n1, n2, s, globalscore))
+                if s < globalscore:
+                    graph.reverse_edge(n1, n2)
+                    improvement = changed = True
+                    globalscore = s
+                    n1, n2 = n2, n1
+                    _say(cfg, "Edge %s -> %s got reversed !" % (n2, n1))
+            # removal of the (possibly reversed) edge: the same graph either way
+            if it["rem_ok"]:
+                s = float(sc["rem"])
+                if s < globalscore:
+                    graph.remove_edge(n1, n2)
+                    improvement = changed = True
+                    globalscore = s
+                    confounders.add(frozenset((n1, n2)))
+                    _say(cfg, "Edge %s -> %s got removed, possible confounder !" % (n1, n2))
                 else:
-                    _say(cfg, "Removing already evaluated for edge %s -> %s" % (n1, n2))
+                    graph.set_weight(n1, n2, s - globalscore)
+                    _say(cfg, "Edge %s -> %s not removed. Score edge : %s" % (n1, n2, s - globalscore))
             else:
-                a_g = copy.deepcopy(graph)
-                a_g.add(u, v)
-                b_g = copy.deepcopy(graph)
-                b_g.add(v, u)
-                cands = []
-                for tag, g in (("uv", a_g), ("vu", b_g)):
-                    if not g.is_cyclic() and g.canonical_key() not in tested:
-                        cands.append((tag, g))
-                s_uv = s_vu = 9999.0
-                if cands:
-                    res = dict(zip([c[0] for c in cands], ev([c[1] for c in cands])))
-                    for tag, g in cands:
-                        tested.add(g.canonical_key())
-                    s_uv = float(res.get("uv", 9999.0))
-                    s_vu = float(res.get("vu", 9999.0))
-                if s_uv < globalscore and s_uv < s_vu:
-                    graph.add(u, v, globalscore - s_uv)
-                    globalscore = s_uv
-                    improvement = True
-                    confounders.discard(frozenset((u, v)))
-                    _say(cfg, "Edge %s -> %s is added !" % (u, v))
-                elif s_vu < globalscore and s_vu < s_uv:
-                    graph.add(v, u, globalscore - s_vu)
-                    globalscore = s_vu
-                    improvement = True
-                    confounders.discard(frozenset((u, v)))
-                    _say(cfg, "Edge %s -> %s is added !" % (v, u))
-                else:
-                    _say(cfg, "Edge not added, possible confounder %s <-> %s" % (u, v))
-                    confounders.add(frozenset((u, v)))
-            ck.save(graph, tested, best=globalscore, loop=loop, position=pos + 1, improvement=improvement,
-                    confounders=sorted([sorted(c, key=repr) for c in confounders], key=repr))
+                _say(cfg, "Removing already evaluated for edge %s -> %s" % (n1, n2))
+        else:
+            u, v = it["u"], it["v"]
+            s_uv = float(sc["uv"]) if "uv" in sc else 9999.0
+            s_vu = float(sc["vu"]) if "vu" in sc else 9999.0
+            if s_uv < globalscore and s_uv < s_vu:
+                graph.add(u, v, globalscore - s_uv)
+                globalscore = s_uv
+                improvement = changed = True
+                confounders.discard(frozenset((u, v)))
+                _say(cfg, "Edge %s -> %s is added !" % (u, v))
+            elif s_vu < globalscore and s_vu < s_uv:
+                graph.add(v, u, globalscore - s_vu)
+                globalscore = s_vu
+                improvement = changed = True
+                confounders.discard(frozenset((u, v)))
+                _say(cfg, "Edge %s -> %s is added !" % (v, u))
+            else:
+                _say(cfg, "Edge not added, possible confounder %s <-> %s" % (u, v))
+                confounders.add(frozenset((u, v)))
+        return changed
+
+    def save(position):
+        ck.save(graph, tested, best=globalscore, loop=loop, position=position, improvement=improvement,
+                confounders=sorted([sorted(c, key=repr) for c in confounders], key=repr))
+
+    while True:
+        pos = start
+        while pos < len(skel_edges):
+            # speculation: the candidates of the next edges against the current graph, scored
+            # in one batch (scores depend on (seed, run) only, not on the batch); decisions are
+            # then replayed in skeleton order, and the window ends at the first structural
+            # change -- later edges' candidates were built on the old graph
+            window, ncand = [], 0
+            j = pos
+            while j < len(skel_edges) and (not window or ncand + 2 <= width):
+                it = plan(j)
+                window.append(it)
+                ncand += len(it["cands"])
+                j += 1
+            flat = [c for it in window for c in it["cands"]]
+            if flat:
+                with timer("search:candidates"):
+                    scores = ev([c[1] for c in flat])
+                for c, s_ in zip(flat, scores):
+                    c[3] = s_
+            for it in window:
+                changed = process(it)
+                pos = it["pos"] + 1
+                save(pos)
+                if changed:
+                    break
         if not improvement:
             break
         loop, start, improvement = loop + 1, 0, False
-        ck.save(graph, tested, best=globalscore, loop=loop, position=0, improvement=False,
-                confounders=sorted([sorted(c, key=repr) for c in confounders], key=repr))
+        save(0)
     graph.search_score = globalscore
     graph.confounders = sorted(tuple(sorted(c, key=repr)) for c in confounders)
     return graph

@@ -79,7 +79,7 @@ def test_confounder_hill_climbing_resumes_after_crash(tmp_path):
         return g
 
     full, resumed, calls = _crash_then_resume(hill_climbing_confounders, make, data, tmp_path, 9, nb_runs=3,
-                                              gpu=False)
+                                              gpu=False, speculation=2)
     assert resumed.canonical_key() == full.canonical_key()
     assert resumed.search_score == full.search_score
     assert resumed.confounders == full.confounders
@@ -143,3 +143,27 @@ def test_profile_timers_record_phases(monkeypatch):
     METRICS.clear()
     cgnn.CGNN().orient_directed_graph(df, g, **TINY)
     assert not [e for e in METRICS.events if e["event"] == "phase"]
+
+
+def test_confounder_hill_climbing_speculation_keeps_the_sequential_result():
+    """Speculative windows (the candidates of several skeleton edges in one batch)
+    accept exactly the sequential sequence of changes."""
+    names = ["A", "B", "C", "D", "E", "F"]
+    data = _data(names)
+
+    def make():
+        skel = UndirectedGraph()
+        for a, b in [("A", "B"), ("B", "C"), ("C", "D"), ("D", "E"), ("A", "C"), ("B", "E"), ("E", "F"), ("A", "F")]:
+            skel.add(a, b)
+        g = DirectedGraph(skeleton=skel)
+        for a, b in [("A", "B"), ("C", "B"), ("C", "D"), ("E", "D"), ("A", "C"), ("F", "E")]:
+            g.add(a, b, 0.1)
+        return g
+
+    # the deterministic hash scorer accepts changes often: windows are cut frequently
+    seq = hill_climbing_confounders(make(), data, Scorer(), nb_runs=3, gpu=False, speculation=2)
+    for w in (4, 7, 64):
+        spec = hill_climbing_confounders(make(), data, Scorer(), nb_runs=3, gpu=False, speculation=w)
+        assert spec.canonical_key() == seq.canonical_key()
+        assert spec.search_score == seq.search_score
+        assert spec.confounders == seq.confounders
