@@ -252,7 +252,14 @@ class GATTrainer:
     otherwise the autograd model over the HIP aggregation."""
 
     def __init__(self, gd: GraphData, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True,
-                 fused: Optional[bool] = None):
+                 fused: Optional[bool] = None, reorder: bool = False):
+        # reorder=True: the framework's locality pass first (data.reorder; the attention
+        # kernels gather rows like the SpMM, so their L2 hit rate follows the order);
+        # accuracies are invariant, ``new_id`` maps caller ids to trainer rows
+        self.new_id = None
+        if reorder:
+            from .data import reorder as _reorder
+            gd, self.new_id = _reorder(gd, seed=seed)
         self.gd = gd
         self.dev = gd.rowptr.device
         x = gd.x.float()

@@ -226,3 +226,23 @@ def test_sample_sharded_trainer_gpu_matches_oracle_and_engine():
         eng = DeviceTrainer([prog], [data], key, H, "cuda:0").run(5, 3)
         np.testing.assert_allclose(sh, ref, rtol=3e-3, atol=1e-5)
         np.testing.assert_allclose(sh, eng, rtol=1e-4, atol=1e-6)
+
+
+def test_in_process_multi_device_round_robin_matches_one_device():
+    """score_jobs' in-process multi-GPU path (batches round-robin over the devices of
+    one process, a bounded window of in-flight batches per device) -- exercised on one
+    MI355X by listing it twice (device_ids=(0, 0)): more batches than the in-flight
+    window, scores bitwise equal to one device and to the per-batch ordering."""
+    from cgnn_amd.engine.program import program_for_pair
+    from cgnn_amd.engine.scorer import Job, score_jobs
+    from cgnn_amd.utils.settings import RunConfig
+    rng = np.random.default_rng(7)
+    jobs = [Job(program_for_pair(8), rng.normal(size=(2, 200)).astype(np.float32), model_key(3, r))
+            for r in range(22)]
+    base = dict(gpu=True, train_epochs=12, test_epochs=5, h_layer_dim=8, batch_models=2)
+    one = score_jobs(jobs, RunConfig(device_ids=(0,), **base))          # 11 batches, window 4
+    two = score_jobs(jobs, RunConfig(device_ids=(0, 0), **base))        # 11 batches, window 8
+    big = score_jobs(jobs, RunConfig(device_ids=(0,), **dict(base, batch_models=64)))
+    assert np.all(np.isfinite(one))
+    np.testing.assert_array_equal(one, two)
+    np.testing.assert_array_equal(one, big)
