@@ -49,8 +49,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--feat-noise", type=float, default=4.0)
     ap.add_argument("--label-noise", type=float, default=0.25)
-    ap.add_argument("--rows", choices=["auto", "aligned", "packed"], default="auto",
+    ap.add_argument("--rows", choices=["auto", "aligned", "packed", "mixed"], default="auto",
                     help="row pitch of gathered matrices: whole 128-B lines, packed to 8 elements, "
+                         "mixed (features aligned, layer-2 rows packed), "
                          "or auto (features aligned; layer-2 rows aligned on one GPU only)")
     ap.add_argument("--no-fused", action="store_true", help="hipBLASLt GEMMs + separate epilogues")
     ap.add_argument("--capture", action="store_true", help="replay the epoch from a hipGraph (one GPU)")
@@ -106,7 +107,9 @@ def main():
     sync()
     gen_s = time.perf_counter() - t_setup
     tr = GCNTrainer(g, hidden=a.hidden, dropout=a.dropout, lr=a.lr, seed=a.seed,
-                    fused=not a.no_fused, align_rows={'auto': None, 'aligned': True, 'packed': False}[a.rows],
+                    fused=not a.no_fused,
+                    align_rows={'auto': None, 'aligned': True, 'packed': False, 'mixed': None}[a.rows],
+                    align_c=False if a.rows == "mixed" else None,
                     capture=a.capture, reorder=a.reorder != "none")
     n_nodes, nnz = g.n, g.nnz
     del g

@@ -84,7 +84,8 @@ class GCNTrainer:
     def __init__(self, g: GraphData, hidden: int = 256, dropout: float = 0.5, lr: float = 0.01,
                  weight_decay: float = 0.0, seed: int = 0, rank: Optional[int] = None,
                  world: Optional[int] = None, fused: bool = True, align_rows: Optional[bool] = None,
-                 halo: Optional[bool] = None, capture: Optional[bool] = None, reorder: bool = False):
+                 halo: Optional[bool] = None, capture: Optional[bool] = None, reorder: bool = False,
+                 align_c: Optional[bool] = None):
         # reorder=True: relabel the nodes for gather locality first (data.reorder: LP
         # clusters + Cuthill-McKee, ~4-8 s of host C++ on the ogbn-products shape, part
         # of setup); the row partition of a multi-GPU run then cuts mostly between
@@ -105,6 +106,8 @@ class GCNTrainer:
         # layer-2 rows only on one GPU, since multi-GPU all-gathers them every epoch and
         # 64 columns instead of 48 would move a third more bytes.
         pad_c = (self.world == 1) if align_rows is None else bool(align_rows)
+        if align_c is not None:                  # layer-2 pitch chosen separately
+            pad_c = bool(align_c)
         pad_x = True if align_rows is None else bool(align_rows)
         self.ldx = _ru(self.F + 1, 64) if pad_x else _ru8(self.F + 1)    # +1: ones column of AX
         self.ldc = _ru(self.C, 64) if pad_c else _ru8(self.C)

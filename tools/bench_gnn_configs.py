@@ -68,6 +68,8 @@ def main():
                     help="papers-gat2: one process plays rank --emulate-rank of this many ranks (its "
                          "rank-local shard, halo plan and buffers; received rows zero) -- memory / compute dry run")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal: every rank on cuda:0 with gloo collectives (multi-rank path on one GPU)")
     ap.add_argument("--sampler", choices=["pipelined", "device", "host"], default=None,
                     help="products-sage3: neighbour sampler (default: pipelined on a GPU)")
     ap.add_argument("--halo-grad-bf16", action="store_true", help="papers-gat2: gradients on the halo wire in bf16")
@@ -86,12 +88,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     cpu = a.config == "cora-cpu" or not torch.cuda.is_available()
     if world > 1:
-        pdist.init_process_group("gloo" if cpu else "nccl")
+        pdist.init_process_group("gloo" if (cpu or a.shared_gpu) else "nccl")
     rank = pdist.rank()
     if cpu:
         dev = torch.device("cpu")
     else:
-        torch.cuda.set_device(pdist.local_rank() % torch.cuda.device_count())
+        torch.cuda.set_device(0 if a.shared_gpu else pdist.local_rank() % torch.cuda.device_count())
         dev = torch.device("cuda", torch.cuda.current_device())
     capture = None if not a.no_capture else False
     res = {"n_gpus": 0 if cpu else world, "scale": a.scale}
@@ -163,6 +165,13 @@ def main():
         per_epoch = len(tr._batches())
         dt = _timed(tr.train_epoch, steps, warmup, dev)
         ev = tr.evaluate()
+        if world > 1 and tr.fused:          # DP replicas must stay bitwise identical
+            import torch.distributed as dist
+            pr = tr._fused.params.clone()
+            pmax, pmin = pr.clone(), pr.clone()
+            dist.all_reduce(pmax, op=dist.ReduceOp.MAX)
+            dist.all_reduce(pmin, op=dist.ReduceOp.MIN)
+            res["replicas_identical"] = bool(torch.equal(pmax, pmin))
         seeds = len(tr.train_idx) * steps
         res.update(metric="epochs/sec + val-acc, 3-layer GraphSAGE ogbn-products mini-batch DP",
                    value=round(steps / dt, 4), unit="epochs/s", ms_per_step=round(1e3 * dt / steps, 3),
