@@ -80,17 +80,21 @@ def build_hip(force=False, verbose=False, debug=False):
     return target
 
 
-def build_rt(force=False, verbose=False, debug=False):
+def build_rt(force=False, verbose=False, debug=False, target=None):
+    """Host C++ runtime module ``_rt``.  ``debug``: -O1 -g with AddressSanitizer and
+    UndefinedBehaviorSanitizer (errors abort; load it with ``CGNN_RT_LIB=<target>`` and
+    ``LD_PRELOAD`` of the compiler's libasan -- ``tests/test_sanitizers_cpu.py``)."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     hdrs = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
-    target = rt_target()
+    target = target or rt_target()
     if not srcs:
         return None
     if not force and not _newer(target, srcs + hdrs + [__file__]):
         return target
     cxx = os.environ.get("CXX", "g++")
     inc = ["-I" + os.path.join(CSRC, "runtime")] + ["-I" + p for p in _pybind_includes()]
-    opt = ["-O0", "-g", "-fsanitize=address,undefined"] if debug else ["-O3"]
+    opt = (["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+            "-fno-sanitize-recover=undefined"] if debug else ["-O3"])
     cmd = [cxx, "-shared", "-fPIC", "-std=c++17", *opt, "-fopenmp", "-fvisibility=hidden",
            *inc, *srcs, "-o", target]
     _run(cmd, verbose)
