@@ -68,8 +68,8 @@ int gnn_launch_dense_fwd(const void*, const float*, const float*, const float*, 
 int gnn_launch_gat_fwd(const int*, const int*, const void*, const float*, const float*, float*, float*, int,
                        int, int, int, hipStream_t);
 int gnn_launch_gat_bwd_row(const int*, const int*, const void*, const float*, const float*, const float*,
-                           const float*, const float*, float*, float*, float*, int, int, int, int, hipStream_t);
-int gnn_launch_gat_bwd_col(const int*, const int*, const int*, const float*, const float*, const void*, float*,
+                           const float*, const float*, float*, float*, int, int, int, int, hipStream_t);
+int gnn_launch_gat_bwd_col(const int*, const int*, const void*, const float*, const float*, const void*, float*,
                            float*, int, int, int, int, hipStream_t);
 int gnn_launch_gat_act_fwd(const float*, const float*, void*, int, long, int, float, uint32_t, uint32_t, uint32_t,
                            const int*, uint32_t, hipStream_t);
@@ -282,21 +282,21 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("rp"), py::arg("col"), py::arg("wh"), py::arg("ss"), py::arg("sd"), py::arg("out"), py::arg("lse"),
      py::arg("n"), py::arg("K"), py::arg("Fh"), py::arg("st"), py::arg("wbf") = 0);
   m.def("gnn_gat_bwd_row", [](uint64_t rp, uint64_t col, uint64_t wh, uint64_t ss, uint64_t sd, uint64_t out,
-                              uint64_t lse, uint64_t dout, uint64_t ae, uint64_t de, uint64_t dsd, int n, int K,
-                              int Fh, uint64_t st, int wbf) {
+                              uint64_t lse, uint64_t dout, uint64_t rstat, uint64_t dsd, int n, int K, int Fh,
+                              uint64_t st, int wbf) {
     chk(gnn_launch_gat_bwd_row(Pt<const int>(rp), Pt<const int>(col), Pt<const void>(wh), Pt<const float>(ss),
                                Pt<const float>(sd), Pt<const float>(out), Pt<const float>(lse),
-                               Pt<const float>(dout), Pt<float>(ae), Pt<float>(de), Pt<float>(dsd), n, K, Fh,
-                               wbf, S(st)), "gnn_gat_bwd_row");
+                               Pt<const float>(dout), Pt<float>(rstat), Pt<float>(dsd), n, K, Fh, wbf, S(st)),
+        "gnn_gat_bwd_row");
   }, py::arg("rp"), py::arg("col"), py::arg("wh"), py::arg("ss"), py::arg("sd"), py::arg("out"), py::arg("lse"),
-     py::arg("dout"), py::arg("ae"), py::arg("de"), py::arg("dsd"), py::arg("n"), py::arg("K"), py::arg("Fh"),
-     py::arg("st"), py::arg("wbf") = 0);
-  m.def("gnn_gat_bwd_col", [](uint64_t rpt, uint64_t colt, uint64_t perm, uint64_t ae, uint64_t de, uint64_t dout,
+     py::arg("dout"), py::arg("rstat"), py::arg("dsd"), py::arg("n"), py::arg("K"), py::arg("Fh"), py::arg("st"),
+     py::arg("wbf") = 0);
+  m.def("gnn_gat_bwd_col", [](uint64_t rpt, uint64_t colt, uint64_t wh, uint64_t ss, uint64_t rstat, uint64_t dout,
                               uint64_t dwh, uint64_t dss, int n, int K, int Fh, uint64_t st, int wbf) {
-    chk(gnn_launch_gat_bwd_col(Pt<const int>(rpt), Pt<const int>(colt), Pt<const int>(perm), Pt<const float>(ae),
-                               Pt<const float>(de), Pt<const void>(dout), Pt<float>(dwh), Pt<float>(dss), n, K,
+    chk(gnn_launch_gat_bwd_col(Pt<const int>(rpt), Pt<const int>(colt), Pt<const void>(wh), Pt<const float>(ss),
+                               Pt<const float>(rstat), Pt<const void>(dout), Pt<float>(dwh), Pt<float>(dss), n, K,
                                Fh, wbf, S(st)), "gnn_gat_bwd_col");
-  }, py::arg("rpt"), py::arg("colt"), py::arg("perm"), py::arg("ae"), py::arg("de"), py::arg("dout"),
+  }, py::arg("rpt"), py::arg("colt"), py::arg("wh"), py::arg("ss"), py::arg("rstat"), py::arg("dout"),
      py::arg("dwh"), py::arg("dss"), py::arg("n"), py::arg("K"), py::arg("Fh"), py::arg("st"), py::arg("wbf") = 0);
   // dense-side kernels of the fused GAT epoch (gnn_gat.hip)
   m.def("gnn_gat_act_fwd", [](uint64_t out, uint64_t b, uint64_t h, int ldh, long n, int F, float p, uint32_t k0,

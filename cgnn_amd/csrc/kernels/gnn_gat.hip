@@ -11,11 +11,12 @@
 //   gat_bwd_row_kernel  per row i: alpha recomputed from the lse, the SDDMM
 //                       dalpha_ij = <dout_i, Wh_j> (head-group shuffle reduction),
 //                       de = alpha (dalpha - <dout_i, out_i>), LeakyReLU'; the row
-//                       term d s_dst[i] accumulates in registers; alpha and the
-//                       score gradient are written per edge (one lane per head).
-//   gat_bwd_col_kernel  per source row j over the TRANSPOSED CSR (edge permutation
-//                       from a stable device sort): dWh[j] = sum alpha_ij dout_i,
-//                       d s_src[j] = sum dscore_ij -- gathers only, no atomics.
+//                       term d s_dst[i] in registers; per (row, head) statistics
+//                       (s_dst, lse, D) for the column half -- nothing per edge.
+//   gat_bwd_col_kernel  per source row j over the TRANSPOSED CSR: alpha and the
+//                       score gradient recomputed from the gathered dout_i and row
+//                       statistics against the own row Wh_j: dWh[j] = sum alpha_ij
+//                       dout_i, d s_src[j] = sum dscore_ij -- gathers only, no atomics.
 // Everything fp32, fixed summation orders (deterministic).
 #include "cgnn_common.h"
 #include <algorithm>
@@ -126,12 +127,18 @@ __global__ __launch_bounds__(256) void gat_fwd_kernel(
   if (f0 % (8 * G) == 0) lse[(size_t)row * K + k] = l > 0.f ? m + __logf(l) : 0.f;
 }
 
+// Row half of the backward, per destination row i and head k: D_ik = <dout_ik, out_ik>,
+// and over the row's edges the SDDMM da_ij = <dout_i, Wh_j>, the attention weight
+// recomputed from the lse, ds_ij = alpha_ij (da_ij - D_ik) LeakyReLU'; their row sum is
+// d s_dst[i,k].  Nothing is stored per edge: the column half recomputes alpha and ds
+// from the row statistics rs[i][k] = (s_dst, lse, D, 0) (one 16-B gather per edge and
+// head) -- no [nnz, K] fp32 arrays, no edge permutation.
 template <int L, int G, int WT>
 __global__ __launch_bounds__(256) void gat_bwd_row_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Wh,
     const float* __restrict__ s_src, const float* __restrict__ s_dst, const float* __restrict__ out,
-    const float* __restrict__ lse, const float* __restrict__ dout, float* __restrict__ alpha_e,
-    float* __restrict__ dsc_e, float* __restrict__ ds_dst, int n, int K, int HF) {
+    const float* __restrict__ lse, const float* __restrict__ dout, float4* __restrict__ rstat,
+    float* __restrict__ ds_dst, int n, int K, int HF) {
   constexpr int RPW = 64 / L;
   const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
   const int row = (xcd_remap(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
@@ -191,24 +198,28 @@ __global__ __launch_bounds__(256) void gat_bwd_row_kernel(
         for (int u = 0; u < EB; ++u) {
           if (q + u < cnt) {
             const float al = __expf(leaky(raw[u]) - ls);
-            const float ds = al * (da[u] - dd) * (raw[u] > 0.f ? 1.f : 0.2f);
-            dsd += ds;
-            if (lead) {
-              alpha_e[(size_t)(e + q + u) * K + k] = al;
-              dsc_e[(size_t)(e + q + u) * K + k] = ds;
-            }
+            dsd += al * (da[u] - dd) * (raw[u] > 0.f ? 1.f : 0.2f);
           }
         }
       }
     }
   }
-  if (lead) ds_dst[(size_t)row * K + k] = dsd;
+  if (lead) {
+    ds_dst[(size_t)row * K + k] = dsd;
+    rstat[(size_t)row * K + k] = make_float4(sd, ls, dd, 0.f);
+  }
 }
 
+// Column half, per SOURCE row j of the transposed CSR (the destinations i that read j,
+// in increasing order) and head k: the own row Wh_j and s_src[j,k] stay in registers;
+// per edge the gathered dout_i and rs[i][k] give alpha_ij = exp(LeakyReLU(s_dst_i +
+// s_src_j) - lse_i) and ds_ij = alpha_ij (<dout_i, Wh_j> - D_i) LeakyReLU':
+// dWh_j = sum_i alpha_ij dout_i, d s_src[j,k] = sum_i ds_ij -- gathers only, no atomics,
+// fixed order.  Rows are independent, so a row range is a pointer offset (halo rounds).
 template <int L, int G, int WT>
 __global__ __launch_bounds__(256) void gat_bwd_col_kernel(
-    const int* __restrict__ rowptr_t, const int* __restrict__ col_t, const int* __restrict__ perm,
-    const float* __restrict__ alpha_e, const float* __restrict__ dsc_e, const void* __restrict__ dout,
+    const int* __restrict__ rowptr_t, const int* __restrict__ col_t, const void* __restrict__ Wh,
+    const float* __restrict__ s_src, const float4* __restrict__ rstat, const void* __restrict__ dout,
     float* __restrict__ dWh, float* __restrict__ ds_src, int n, int K, int HF) {
   constexpr int RPW = 64 / L;
   const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
@@ -217,35 +228,58 @@ __global__ __launch_bounds__(256) void gat_bwd_col_kernel(
   const int f0 = 8 * sl;
   const bool fv = rv && f0 < HF;
   const int k = fv ? f0 / (8 * G) : 0;
+  float wj[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float ss = 0.f;
+  if (fv) {
+    ldg8<WT>(Wh, (size_t)row * HF + f0, wj);
+    ss = s_src[(size_t)row * K + k];
+  }
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float dss = 0.f;
   const int e0 = rv ? rowptr_t[row] : 0, e1 = rv ? rowptr_t[row + 1] : 0;
   for (int e = e0; e < e1; e += L) {
     const int myi = (e + sl < e1) ? col_t[e + sl] : 0;
-    const int mye = (e + sl < e1) ? perm[e + sl] : 0;
     const int cnt = min(L, e1 - e);
     for (int q = 0; q < cnt; q += EB) {          // EB edges' rows requested together
-      int i[EB], eo[EB];
+      int i[EB];
+#pragma unroll
+      for (int u = 0; u < EB; ++u) i[u] = __shfl(myi, sub * L + min(q + u, L - 1), 64);
+      float g[EB][8];
+      float4 rs[EB];
 #pragma unroll
       for (int u = 0; u < EB; ++u) {
-        const int src = sub * L + min(q + u, L - 1);
-        i[u] = __shfl(myi, src, 64);
-        eo[u] = __shfl(mye, src, 64);
+        if (fv) {
+          ldg8<WT>(dout, (size_t)i[u] * HF + f0, g[u]);
+          rs[u] = rstat[(size_t)i[u] * K + k];
+        } else {
+#pragma unroll
+          for (int f = 0; f < 8; ++f) g[u][f] = 0.f;
+          rs[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+      float da[EB];
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        float d = 0.f;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) d = fmaf(g[u][f], wj[f], d);
+        da[u] = d;
+      }
+#pragma unroll
+      for (int off = 1; off < G; off <<= 1) {
+#pragma unroll
+        for (int u = 0; u < EB; ++u) da[u] += __shfl_xor(da[u], off, 64);
       }
       if (fv) {
-        float g[EB][8], al[EB], dsc[EB];
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-          ldg8<WT>(dout, (size_t)i[u] * HF + f0, g[u]);
-          al[u] = alpha_e[(size_t)eo[u] * K + k];
-          dsc[u] = dsc_e[(size_t)eo[u] * K + k];
-        }
+          if (q + u < cnt) {
+            const float raw = rs[u].x + ss;
+            const float al = __expf(leaky(raw) - rs[u].y);
+            dss += al * (da[u] - rs[u].z) * (raw > 0.f ? 1.f : 0.2f);
 #pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          const float a = (q + u < cnt) ? al[u] : 0.f;
-#pragma unroll
-          for (int f = 0; f < 8; ++f) acc[f] = fmaf(a, g[u][f], acc[f]);
-          dss += (q + u < cnt) ? dsc[u] : 0.f;
+            for (int f = 0; f < 8; ++f) acc[f] = fmaf(al, g[u][f], acc[f]);
+          }
         }
       }
     }
@@ -308,25 +342,27 @@ extern "C" int gnn_launch_gat_fwd(const int* rowptr, const int* col, const void*
   GAT_DISPATCH(gat_fwd_kernel, 0, rowptr, col, Wh, s_src, s_dst, out, lse, n, K, HF);
 }
 
+// rstat: [n][K] float4 (s_dst, lse, D, 0), written for the column half
 extern "C" int gnn_launch_gat_bwd_row(const int* rowptr, const int* col, const void* Wh, const float* s_src,
                                       const float* s_dst, const float* out, const float* lse,
-                                      const float* dout, float* alpha_e, float* dsc_e, float* ds_dst, int n,
-                                      int K, int Fh, int wbf, hipStream_t st) {
+                                      const float* dout, float* rstat, float* ds_dst, int n, int K, int Fh, int wbf,
+                                      hipStream_t st) {
   const int HF = K * Fh;
+  float4* rs = reinterpret_cast<float4*>(rstat);
   if (wbf)
-    GAT_DISPATCH(gat_bwd_row_kernel, 1, rowptr, col, Wh, s_src, s_dst, out, lse, dout, alpha_e, dsc_e, ds_dst,
-                 n, K, HF);
-  GAT_DISPATCH(gat_bwd_row_kernel, 0, rowptr, col, Wh, s_src, s_dst, out, lse, dout, alpha_e, dsc_e, ds_dst, n,
-               K, HF);
+    GAT_DISPATCH(gat_bwd_row_kernel, 1, rowptr, col, Wh, s_src, s_dst, out, lse, dout, rs, ds_dst, n, K, HF);
+  GAT_DISPATCH(gat_bwd_row_kernel, 0, rowptr, col, Wh, s_src, s_dst, out, lse, dout, rs, ds_dst, n, K, HF);
 }
 
-extern "C" int gnn_launch_gat_bwd_col(const int* rowptr_t, const int* col_t, const int* perm,
-                                      const float* alpha_e, const float* dsc_e, const void* dout, float* dWh,
-                                      float* ds_src, int n, int K, int Fh, int wbf, hipStream_t st) {
+// Wh / s_src / dWh / ds_src: rows of the launch's source range; rstat / dout: all
+// destination rows.  wbf: Wh and the gathered dout are bf16.
+extern "C" int gnn_launch_gat_bwd_col(const int* rowptr_t, const int* col_t, const void* Wh, const float* s_src,
+                                      const float* rstat, const void* dout, float* dWh, float* ds_src, int n, int K,
+                                      int Fh, int wbf, hipStream_t st) {
   const int HF = K * Fh;
-  if (wbf)
-    GAT_DISPATCH(gat_bwd_col_kernel, 1, rowptr_t, col_t, perm, alpha_e, dsc_e, dout, dWh, ds_src, n, K, HF);
-  GAT_DISPATCH(gat_bwd_col_kernel, 0, rowptr_t, col_t, perm, alpha_e, dsc_e, dout, dWh, ds_src, n, K, HF);
+  const float4* rs = reinterpret_cast<const float4*>(rstat);
+  if (wbf) GAT_DISPATCH(gat_bwd_col_kernel, 1, rowptr_t, col_t, Wh, s_src, rs, dout, dWh, ds_src, n, K, HF);
+  GAT_DISPATCH(gat_bwd_col_kernel, 0, rowptr_t, col_t, Wh, s_src, rs, dout, dWh, ds_src, n, K, HF);
 }
 
 // ============================================================================

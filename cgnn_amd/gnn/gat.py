@@ -8,9 +8,9 @@ Attention aggregation over the CSR of A + I (multi-head):
 On a GPU the aggregation runs on three HIP kernels (``gnn_gat.hip``): a fused
 forward with an online softmax (edge scores never stored; per-(row, head)
 log-sum-exp kept), a row-wise backward doing the SDDMM ``<dout_i, Wh_j>`` and the
-softmax / LeakyReLU derivative, and a column-wise backward over the transposed
-CSR (stable device sort + edge permutation) that gathers ``dWh`` and the source
-score gradient -- no atomics anywhere.  The projections ``Wh = h W`` and the
+softmax / LeakyReLU derivative (per-row statistics only, nothing per edge), and a
+column-wise backward over the transposed CSR that recomputes the attention
+weights and gathers ``dWh`` and the source score gradient -- no atomics anywhere.  The projections ``Wh = h W`` and the
 scores ``s = <Wh, a>`` are PyTorch ops (hipBLASLt), so autograd chains through.
 On the CPU the same math is written with PyTorch index ops (the reference the
 GPU kernels are tested against).
@@ -48,7 +48,7 @@ class GraphCSR:
 
     def transposed(self):
         if self._t is None:
-            self._t = transpose_csr(self.rowptr, self.col, self.n_cols, with_perm=True)
+            self._t = transpose_csr(self.rowptr, self.col, self.n_cols)
         return self._t
 
     def edge_rows(self):
@@ -68,23 +68,23 @@ def _gat_forward_kernels(Whg, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: 
 
 
 def _gat_backward_kernels(Whg, s_src, s_dst, out, lse, dout, g: GraphCSR, K: int, Fh: int, lowp: bool):
-    """(dWh [n_cols, K*Fh] fp32, ds_src [n_cols, K], ds_dst [n, K])."""
+    """(dWh [n_cols, K*Fh] fp32, ds_src [n_cols, K], ds_dst [n, K]): the row half (SDDMM,
+    d s_dst, per-(row, head) statistics) then the column half over the transposed CSR,
+    which recomputes the attention weights -- nothing is stored per edge."""
     hip = native.hip()
     n, dev = g.n, Whg.device
     dout = dout.contiguous().float()
-    alpha_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
-    dsc_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+    rstat = torch.empty(n, K, 4, dtype=torch.float32, device=dev)
     ds_dst = torch.empty(n, K, dtype=torch.float32, device=dev)
     hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(),
-                        s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(),
-                        dsc_e.data_ptr(), ds_dst.data_ptr(), n, K, Fh, _st(Whg), int(lowp))
-    rp_t, col_t, perm = g.transposed()
+                        s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), rstat.data_ptr(),
+                        ds_dst.data_ptr(), n, K, Fh, _st(Whg), int(lowp))
+    rp_t, col_t = g.transposed()
     doutg = dout.to(torch.bfloat16) if lowp else dout
     dWh = torch.empty(g.n_cols, K * Fh, dtype=torch.float32, device=dev)   # one row per source
     ds_src = torch.empty(g.n_cols, K, dtype=torch.float32, device=dev)
-    hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
-                        dsc_e.data_ptr(), doutg.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh,
-                        _st(Whg), int(lowp))
+    hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), Whg.data_ptr(), s_src.data_ptr(), rstat.data_ptr(),
+                        doutg.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh, _st(Whg), int(lowp))
     return dWh, ds_src, ds_dst
 
 

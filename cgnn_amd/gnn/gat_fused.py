@@ -172,26 +172,25 @@ def _agg_fwd(Wh, s_src, s_dst, g, K, Fh):
 
 
 def _agg_bwd_rows(Wh, s_src, s_dst, out, lse, dout, g, K, Fh):
-    """Row half of the aggregation backward: per edge the attention weight and the
-    score gradient (alpha_e, dsc_e [nnz, K]) and ds_dst [n, K] (GPU)."""
-    hip = native.hip()
+    """Row half of the aggregation backward: ds_dst [n, K] and the per-(row, head)
+    statistics (s_dst, lse, <dout, out>) the column half recomputes alpha from (GPU)."""
     dev = Wh.device
-    alpha_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
-    dsc_e = torch.empty(g.nnz, K, dtype=torch.float32, device=dev)
+    rstat = torch.empty(g.n, K, 4, dtype=torch.float32, device=dev)
     ds_dst = torch.empty(g.n, K, dtype=torch.float32, device=dev)
-    hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(), s_dst.data_ptr(),
-                        out.data_ptr(), lse.data_ptr(), dout.data_ptr(), alpha_e.data_ptr(), dsc_e.data_ptr(),
-                        ds_dst.data_ptr(), g.n, K, Fh, _st(Wh), int(Wh.dtype == torch.bfloat16))
-    return alpha_e, dsc_e, ds_dst
+    native.hip().gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(),
+                                 s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), rstat.data_ptr(),
+                                 ds_dst.data_ptr(), g.n, K, Fh, _st(Wh), int(Wh.dtype == torch.bfloat16))
+    return rstat, ds_dst
 
 
-def _agg_bwd_cols(alpha_e, dsc_e, doutb, g, K, Fh, lo, hi, dWh, ds_src):
+def _agg_bwd_cols(Wh, s_src, rstat, doutb, g, K, Fh, lo, hi, dWh, ds_src):
     """Column half for source rows [lo, hi) of the transposed CSR (rows are independent,
     so a row range is a pointer offset): dWh [hi - lo, K Fh], ds_src [hi - lo, K] (GPU)."""
-    rp_t, col_t, perm = g.transposed()
-    native.hip().gnn_gat_bwd_col(rp_t.data_ptr() + 4 * lo, col_t.data_ptr(), perm.data_ptr(), alpha_e.data_ptr(),
-                                 dsc_e.data_ptr(), doutb.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), hi - lo, K,
-                                 Fh, _st(doutb), 1)
+    rp_t, col_t = g.transposed()
+    KF = K * Fh
+    native.hip().gnn_gat_bwd_col(rp_t.data_ptr() + 4 * lo, col_t.data_ptr(), Wh.data_ptr() + Wh.element_size() * KF * lo,
+                                 s_src.data_ptr() + 4 * K * lo, rstat.data_ptr(), doutb.data_ptr(), dWh.data_ptr(),
+                                 ds_src.data_ptr(), hi - lo, K, Fh, _st(doutb), 1)
 
 
 def _agg_bwd_torch(Wh, s_src, s_dst, dout, g, K, Fh):
@@ -348,21 +347,20 @@ class FusedGAT:
             if self.halo is not None:
                 dWh, ds_src = self.halo.reduce_back([dWh, ds_src])
         else:
-            alpha_e, dsc_e, ds_dst = _agg_bwd_rows(Wh_ext, s_ext, s_dst, out, lse, dout, g, K, Fh)
-            del Wh_ext, s_ext                        # the received rows are not needed any more
+            rstat, ds_dst = _agg_bwd_rows(Wh_ext, s_ext, s_dst, out, lse, dout, g, K, Fh)
             n = self.nloc
             dWh = torch.empty(n, L.KF, dtype=torch.float32, device=self.dev)
             ds_src = torch.empty(n, K, dtype=torch.float32, device=self.dev)
-            _agg_bwd_cols(alpha_e, dsc_e, doutb, g, K, Fh, 0, n, dWh, ds_src)
+            _agg_bwd_cols(Wh_ext, s_ext, rstat, doutb, g, K, Fh, 0, n, dWh, ds_src)
             if self.halo is not None:
                 # the received rows' gradients are made one exchange round at a time
                 def produce(lo, hi):
                     a = torch.empty(hi - lo, L.KF, dtype=torch.float32, device=self.dev)
                     b = torch.empty(hi - lo, K, dtype=torch.float32, device=self.dev)
-                    _agg_bwd_cols(alpha_e, dsc_e, doutb, g, K, Fh, lo, hi, a, b)
+                    _agg_bwd_cols(Wh_ext, s_ext, rstat, doutb, g, K, Fh, lo, hi, a, b)
                     return [a, b]
                 self.halo.reduce_back_stream(produce, [dWh, ds_src], getattr(self.halo, "grad_wire", torch.float32))
-            del alpha_e, dsc_e
+            del rstat, Wh_ext, s_ext
         pack_grad(dWh, ds_src, ds_dst, L.dy)
         del dWh, ds_src, ds_dst
         lin_bwd_weight(x, L.dy, L.N, K1=K1, dW=L.dWc, db=L.db_scratch)
