@@ -93,8 +93,14 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
   const int tile_hi = min(n_tiles, tile_lo + tiles_per_chunk);
   float* my = s_x + ((t >> 1) * D) * 2 + (t & 1);
 
+  // evaluation over all rows: the pred-pred block is symmetric, so only column tiles at
+  // or right of the row tile are evaluated, those strictly right counting twice
+  // (25 % fewer distances per evaluation step; geometry fixed by N, so still bitwise
+  // reproducible and independent of the batch)
+  const bool sym = MODE == 1 && row_begin == 0 && n_rows == N;
   for (int tile = tile_lo; tile < tile_hi; ++tile) {
     const bool is_pred = (MODE != 2) && tile < ct;
+    if (sym && is_pred && tile < rt) continue;           // block-uniform: no barrier divergence
     const float* src = is_pred ? P : Tm;
     const int col0 = (is_pred || MODE == 2 ? tile : tile - ct) * T;
     const int c = col0 + t;
@@ -102,7 +108,7 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
 #pragma unroll
     for (int k = 0; k < D; ++k) my[2 * k] = (c < N) ? src[(size_t)k * N + c] : MMD_SENTINEL;
     __syncthreads();
-    const float lsign = (MODE == 2 || is_pred) ? 1.f : -2.f;
+    const float lsign = (MODE == 2 || is_pred) ? ((sym && tile > rt) ? 2.f : 1.f) : -2.f;
     const float gsign = is_pred ? 1.f : -1.f;
     f2 tl = {0.f, 0.f};
     const f2* xp = reinterpret_cast<const f2*>(s_x);
