@@ -118,6 +118,23 @@ __device__ __forceinline__ uint4 load_masked8(const uint16_t* __restrict__ dY, i
   return make_uint4(gw[0], gw[1], gw[2], gw[3]);
 }
 
+// block-wide copy of a weight image global -> LDS with 8 loads in flight per thread: a
+// plain strided loop waits on every load before its LDS store (a serial chain of L2
+// round trips, ~30 us per launch for a 133 KB image -- it dominated the small layers
+// of a GraphSAGE mini-batch)
+__device__ __forceinline__ void copy_image(uint4* __restrict__ dst, const uint4* __restrict__ src, int n16) {
+  const int bd = blockDim.x;
+  int i = threadIdx.x;
+  for (; i + 7 * bd < n16; i += 8 * bd) {
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[i + u * bd];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) dst[i + u * bd] = v[u];
+  }
+  for (; i < n16; i += bd) dst[i] = src[i];
+}
+
 int device_cus() {
   static int cached[64] = {0};
   int dev = 0;
@@ -157,8 +174,7 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
   {
     const uint4* src = reinterpret_cast<const uint4*>(wimg + (size_t)blockIdx.y * ncols * WS);
     uint4* dst = reinterpret_cast<uint4*>(sWT);
-    const int n16 = ncols * WS / 8;
-    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    copy_image(dst, src, ncols * WS / 8);
   }
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) sB[c] = (bias && c0 + c < N) ? bias[c0 + c] : 0.f;
   __syncthreads();
@@ -241,8 +257,7 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
   {
     const uint4* src = reinterpret_cast<const uint4*>(wimg + (size_t)blockIdx.y * kcols * WS);
     uint4* dst = reinterpret_cast<uint4*>(sW);
-    const int n16 = kcols * WS / 8;
-    for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+    copy_image(dst, src, kcols * WS / 8);
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31;
@@ -486,12 +501,15 @@ static int slab_cols(int N, int KP) {
   return cols;
 }
 
+
+
 template <int KS>
 static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const float* W, int N,
                       const float* bias, uint16_t* Y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1,
                       uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
                       const int* idx1, uint16_t* wimg, float* Yf, int nsplit, int tk, hipStream_t st) {
   constexpr int KP = KS * 16;
+  constexpr int WV = FwdWaves<KS>::value;
   const int ncols = slab_cols(std::max(N, ldy), KP);
   const size_t lds = (size_t)ncols * (KP + 8) * 2 + (size_t)ncols * 4;
   {
@@ -500,7 +518,6 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
     hipLaunchKernelGGL(lin_prep_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2, N,
                        ncols, KP, KP + 8, total, wimg);
   }
-  constexpr int WV = FwdWaves<KS>::value;
   (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
   hipLaunchKernelGGL((lin_fwd_kernel<KS>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
@@ -569,19 +586,20 @@ extern "C" int gnn_launch_lin_bwd_data(const void* dY, int lddy, const void* Ym,
 }
 
 // bytes of the weight images the launchers write (the caller provides the scratch)
+// (upper bounds over every slab width the launchers may pick for any row count:
+// slabs * width < columns + 256)
 extern "C" long gnn_lin_fwd_image_bytes(int K, int N, int ldy) {
   const int ks = pick_ks(K);
   if (ks < 0) return -1;
-  const int KP = ks * 16, ncols = slab_cols(std::max(N, ldy), KP);
-  const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
-  return 2L * slabs * ncols * (KP + 8);
+  const int KP = ks * 16;
+  return 2L * ((std::max(N, ldy) + 31) / 32 * 32 + 256) * (KP + 8);
 }
 
 extern "C" long gnn_lin_bwd_image_bytes(int K, int N) {
   const int kn = pick_ks(N);
   if (kn < 0) return -1;
-  const int NP = kn * 16, kcols = slab_cols(K, NP);
-  return 2L * ((K + kcols - 1) / kcols) * kcols * (NP + 8);
+  const int NP = kn * 16;
+  return 2L * ((K + 31) / 32 * 32 + 256) * (NP + 8);
 }
 
 // chunk count of the split-K weight gradient for n rows and N columns (fills the chip)
