@@ -91,6 +91,12 @@ def main():
             sys.exit("bench.py: process group has %d ranks, expected %d" % (pdist.world_size(), world))
     rank = pdist.rank()
     local = pdist.local_rank()
+    if world > 1 and os.environ.get("OMP_NUM_THREADS") == "1":
+        # torch.distributed.run pins OMP_NUM_THREADS=1: give the host C++ setup (graph
+        # generation, locality reorder) this rank's share of the node's cores instead
+        from cgnn_amd import native
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        native.rt().set_num_threads(max(1, (os.cpu_count() or 8) // max(lw, 1)))
     if cuda:
         torch.cuda.set_device(0 if shared else local)
         dev = torch.device("cuda", torch.cuda.current_device())
