@@ -23,6 +23,7 @@ from typing import Optional
 import torch
 
 from .. import native
+from ..utils import checks
 from .data import GraphData
 from .sage import transpose_csr
 
@@ -58,7 +59,22 @@ class GraphCSR:
         return self._rows
 
 
+def _check_graph(g: "GraphCSR", Wh, s_src, s_dst, what):
+    if checks.enabled():
+        checks.csr(g.rowptr, g.col, g.n_cols, what, n_rows=g.n)
+        checks.rows(Wh, g.n_cols, what + " Wh")
+        checks.rows(s_src, g.n_cols, what + " s_src")
+        checks.rows(s_dst, g.n, what + " s_dst")
+
+
+def _check_transposed(g: "GraphCSR", what):
+    if checks.enabled():
+        rp_t, col_t = g.transposed()
+        checks.csr(rp_t, col_t, g.n, what, n_rows=g.n_cols)
+
+
 def _gat_forward_kernels(Whg, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool):
+    _check_graph(g, Whg, s_src, s_dst, "gat_fwd")
     n = g.n
     out = torch.empty(n, K * Fh, dtype=torch.float32, device=Whg.device)
     lse = torch.empty(n, K, dtype=torch.float32, device=Whg.device)
@@ -73,6 +89,8 @@ def _gat_backward_kernels(Whg, s_src, s_dst, out, lse, dout, g: GraphCSR, K: int
     which recomputes the attention weights -- nothing is stored per edge."""
     hip = native.hip()
     n, dev = g.n, Whg.device
+    _check_graph(g, Whg, s_src, s_dst, "gat_bwd")
+    _check_transposed(g, "gat_bwd transposed")
     dout = dout.contiguous().float()
     rstat = torch.empty(n, K, 4, dtype=torch.float32, device=dev)
     ds_dst = torch.empty(n, K, dtype=torch.float32, device=dev)

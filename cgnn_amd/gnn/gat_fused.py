@@ -159,6 +159,8 @@ def pack_grad(dWh, ds_src, ds_dst, dy):
 
 # ------------------------------------------------------------------ aggregation
 def _agg_fwd(Wh, s_src, s_dst, g, K, Fh):
+    from .gat import _check_graph
+    _check_graph(g, Wh, s_src, s_dst, "fused gat_fwd")
     n = g.n
     if Wh.is_cuda:
         out = torch.empty(n, K * Fh, dtype=torch.float32, device=Wh.device)
@@ -174,6 +176,9 @@ def _agg_fwd(Wh, s_src, s_dst, g, K, Fh):
 def _agg_bwd_rows(Wh, s_src, s_dst, out, lse, dout, g, K, Fh):
     """Row half of the aggregation backward: ds_dst [n, K] and the per-(row, head)
     statistics (s_dst, lse, <dout, out>) the column half recomputes alpha from (GPU)."""
+    from .gat import _check_graph, _check_transposed
+    _check_graph(g, Wh, s_src, s_dst, "fused gat_bwd_row")
+    _check_transposed(g, "fused gat_bwd_col")
     dev = Wh.device
     rstat = torch.empty(g.n, K, 4, dtype=torch.float32, device=dev)
     ds_dst = torch.empty(g.n, K, dtype=torch.float32, device=dev)

@@ -23,6 +23,7 @@ from typing import Optional
 import torch
 
 from .. import native
+from ..utils import checks
 from .ops import _st, _step_args, _step_value, dropout_keep_mask
 
 _GPART = {}
@@ -85,6 +86,13 @@ def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = No
     if out is None:
         ldy = ldy or ((N if tail is None else nsplit) + 7) // 8 * 8
         out = torch.empty(n, ldy, dtype=torch.bfloat16, device=x1.device)
+    if checks.enabled():
+        checks.index(idx1, x1.shape[0], "lin_fwd idx1")
+        if idx1 is None:
+            checks.rows(x1, n, "lin_fwd x1")
+        checks.rows(x2, n if x2 is not None else 0, "lin_fwd x2")
+        checks.rows(out, n, "lin_fwd out")
+        checks.rows(rscale, n if rscale is not None else 0, "lin_fwd rscale")
     if x1.is_cuda:
         sv, sp = _step_args(step)
         hip = native.hip()
@@ -169,6 +177,9 @@ def lin_bwd_weight(x1: torch.Tensor, dY: torch.Tensor, N: int, x2: Optional[torc
         dW = torch.empty(K1 + K2, N, dtype=torch.float32, device=dev)
     if db is None:
         db = torch.empty(N, dtype=torch.float32, device=dev)
+    if checks.enabled():
+        checks.index(idx1, x1.shape[0], "lin_bwd_weight idx1")
+        checks.rows(dY, n, "lin_bwd_weight dY")
     if x1.is_cuda:
         hip = native.hip()
         chunks = hip.gnn_lin_wgrad_chunks(max(n, 1), N)

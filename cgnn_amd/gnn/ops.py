@@ -9,7 +9,7 @@ from __future__ import annotations
 import torch
 
 from .. import native
-from ..utils import philox
+from ..utils import checks, philox
 
 
 def _st(t):
@@ -44,6 +44,11 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
     ldo = ld_out or X.shape[1]
     if out is None:
         out = torch.empty(n, ldo, dtype=out_dtype, device=X.device)
+    if checks.enabled():
+        checks.csr(rowptr, col, X.shape[0], "spmm")
+        checks.rows(out, n, "spmm out")
+        checks.rows(rscale, n, "spmm rscale")
+        checks.rows(cscale, X.shape[0], "spmm cscale")
     if X.is_cuda:
         hip = native.hip()
         hip.gnn_spmm(rowptr.data_ptr(), col.data_ptr(), X.data_ptr(), out.data_ptr(),
@@ -82,6 +87,10 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
     ``init`` (optional fp32 [n, >=C]): partial sums of other edges.
     ``gslot`` (optional int32 [n]): G is compact -- row i (a train row, gslot[i] >= 0)
     goes to G[gslot[i]], other rows (whose dlogits are zero) are not written."""
+    if checks.enabled():
+        checks.csr(rowptr, col, Z.shape[0], "spmm_ce")
+        checks.rows(labels, rowptr.numel() - 1, "spmm_ce labels")
+        checks.rows(mask, rowptr.numel() - 1, "spmm_ce mask")
     n = rowptr.numel() - 1
     ld = Z.shape[1]
     if Z.is_cuda:

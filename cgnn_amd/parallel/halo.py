@@ -53,6 +53,14 @@ def _rows(src: torch.Tensor, dst: torch.Tensor, src_idx=None, dst_idx=None, mode
             dst_idx.numel() if dst_idx is not None else src.shape[0])
     if rows == 0:
         return
+    from ..utils import checks
+    if checks.enabled():
+        checks.index(src_idx, src.shape[0], "halo rows src_idx")
+        checks.index(dst_idx, dst.shape[0], "halo rows dst_idx")
+        if src_idx is None:
+            checks.rows(src, rows, "halo rows src")
+        if dst_idx is None:
+            checks.rows(dst, rows, "halo rows dst")
     if dst.is_cuda:
         from .. import native
         words = dst.shape[1] if mode else dst.shape[1] * dst.element_size() // 4
