@@ -250,6 +250,10 @@ class PipelinedSampler:
         """Start sampling ``seeds`` (int32 device tensor, <= batch) on the side stream."""
         if seeds.numel() > self.batch:
             raise ValueError("more seeds than the sampler's batch bound")
+        from ..utils import checks
+        if checks.enabled():
+            checks.index(seeds, self.n, "sample_blocks seeds")
+            checks.csr(self.rowptr, self.col, self.n, "sample_blocks graph", n_rows=self.n)
         sl = self.slots[self._next]
         self._next = (self._next + 1) % len(self.slots)
         main = torch.cuda.current_stream(self.dev)
