@@ -264,6 +264,21 @@ def _use_fused(fused, dev, F, heads, head_dim, n_classes):
     return bool(fused)
 
 
+def _gat_state_tensors(tr):
+    if tr.fused is not None:
+        return tr.fused.state_tensors()
+    from .checkpoint import module_optimizer_tensors
+    return module_optimizer_tensors(tr.model, tr.opt)
+
+
+def _gat_load_state_tensors(tr, t):
+    if tr.fused is not None:
+        tr.fused.load_state_tensors(t)
+    else:
+        from .checkpoint import load_module_optimizer_tensors
+        load_module_optimizer_tensors(tr.model, tr.opt, t)
+
+
 class GATTrainer:
     """Full-graph GAT node classification (Adam, cross-entropy on the train split).
     ``fused`` (default: on a GPU): the whole epoch on HIP kernels (``gat_fused``);
@@ -294,6 +309,12 @@ class GATTrainer:
             return
         self.model = GAT(x.shape[1], gd.n_classes, heads, head_dim, dropout, seed).to(self.dev)
         self.opt = torch.optim.Adam(self.model.parameters(), lr=lr, fused=self.dev.type == "cuda")
+
+    def state_tensors(self):
+        return _gat_state_tensors(self)
+
+    def load_state_tensors(self, t):
+        _gat_load_state_tensors(self, t)
 
     def train_step(self):
         if self.fused is not None:
@@ -412,6 +433,12 @@ class ShardedGATTrainer:
             self.ddp = GradBucketer(list(self.model.parameters()), bucket_mb)
             self.ddp.broadcast_parameters(0)
         self.epoch = 0
+
+    def state_tensors(self):
+        return _gat_state_tensors(self)
+
+    def load_state_tensors(self, t):
+        _gat_load_state_tensors(self, t)
 
     def halo_stats(self):
         """Rows / bytes this rank receives and sends per layer-1 exchange (Wh bf16 + fp32 scores)."""

@@ -305,6 +305,14 @@ class _FusedSAGE:
     def state_tensors(self):
         return {"params": self.params, "adam_m": self.m, "adam_v": self.v, "adam_step": self.step_t}
 
+    def load_state_tensors(self, t):
+        for name, dst in (("params", self.params), ("adam_m", self.m), ("adam_v", self.v),
+                          ("adam_step", self.step_t)):
+            if t[name].shape != dst.shape:
+                raise ValueError("checkpoint %s has shape %s, trainer %s" % (name, tuple(t[name].shape),
+                                                                              tuple(dst.shape)))
+            dst.copy_(t[name].to(dst.device))
+
 
 def _pad8(x: torch.Tensor) -> torch.Tensor:
     F = x.shape[1]
@@ -388,6 +396,20 @@ class SAGETrainer:
         self._full = None
         self.prefetch = bool(prefetch)
         self.epoch = 0
+
+    # ----------------------------------------------------------- checkpoint
+    def state_tensors(self):
+        if self.fused:
+            return self._fused.state_tensors()
+        from .checkpoint import module_optimizer_tensors
+        return module_optimizer_tensors(self.model, self.opt)
+
+    def load_state_tensors(self, t):
+        if self.fused:
+            self._fused.load_state_tensors(t)
+        else:
+            from .checkpoint import load_module_optimizer_tensors
+            load_module_optimizer_tensors(self.model, self.opt, t)
 
     # ----------------------------------------------------------- blocks
     def full_blocks(self):

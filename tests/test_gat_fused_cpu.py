@@ -96,3 +96,26 @@ def test_wcat_backward_is_the_adjoint():
     np.testing.assert_allclose(gW.numpy(), W.grad.numpy(), rtol=1e-12)
     np.testing.assert_allclose(gs.numpy(), a_s.grad.numpy(), rtol=1e-12)
     np.testing.assert_allclose(gd.numpy(), a_d.grad.numpy(), rtol=1e-12)
+
+
+def test_fused_gat_and_sage_checkpoint_resume(tmp_path):
+    """safetensors checkpoints of the fused trainers: resuming equals training on."""
+    from cgnn_amd.gnn.checkpoint import load_trainer, save_trainer
+    from cgnn_amd.gnn.sage import SAGETrainer
+    g = synthetic("ogbn-products", seed=6, scale=0.0005)
+    for make, step in ((lambda: GATTrainer(g, heads=4, head_dim=8, dropout=0.3, lr=0.01, fused=True),
+                        lambda t: t.train_step()),
+                       (lambda: SAGETrainer(g, hidden=32, layers=2, fanouts=[5, 5], batch_size=64, fused=True),
+                        lambda t: t.train_epoch())):
+        a = make()
+        step(a)
+        path = str(tmp_path / "ck.safetensors")
+        save_trainer(a, path)
+        step(a)
+        b = make()
+        load_trainer(b, path)
+        step(b)
+        pa = a.state_tensors()["params"]
+        pb = b.state_tensors()["params"]
+        # (CPU reference ops sum with index_add_, whose thread order may vary: ~1e-8)
+        assert torch.allclose(pa, pb, rtol=0, atol=1e-6), (make, (pa - pb).abs().max())
