@@ -53,6 +53,34 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
                     (uint32_t)bf16_bits(c) | ((uint32_t)bf16_bits(d) << 16));
 }
 
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+// Byte offset of 16-B chunk `ch` of row `row` in a [32][256 B] staging image.  The
+// XOR swizzle keeps the b128 staging writes at the 8-way minimum and makes the b128
+// row reads and the ds_read_b64_tr_b16 column reads of the 32x32x16 operands
+// conflict-free (cdna_hip_programming.md T10, image (b)).
+__device__ __forceinline__ int stg_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+// Byte offset of 8-B unit `u` (0..7) of row `row` in a wave's [32 rows][32 hidden]
+// H1 / dP1 image (64-B rows): the packed accumulator writes are at the 4-way minimum,
+// the transposed reads conflict-free.
+__device__ __forceinline__ int img_off(int row, int u) {
+  return 64 * row + 8 * (u ^ ((row >> 1) & 7));
+}
+
+// ds_read_b64_tr_b16 (gfx950): lane 4q+p of a 16-lane group gives the address of
+// row q, columns 4p..4p+3 of a 4x16 block; lane i receives column i of the 4 rows.
+// Two reads (rows +0..3, +4..7) form one 32x32x16 operand fragment.
+__device__ __forceinline__ bf16x8 tr_frag(const uint16_t* base, int off0, int off1) {
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  const char* b = reinterpret_cast<const char*>(base);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(b + off0));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(b + off1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 }  // namespace
 
 // KS = k-steps of 16 over the input features (F <= 16*KS <= ldx rounded), HD hidden width.
@@ -227,12 +255,16 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_bwd_kernel(
 // Block = HD/32 waves, wave w owns hidden block w (32 units) for all three
 // products, so its weight-gradient tiles (KF/32 + 2 of 32x32) stay in its
 // accumulators for the whole persistent loop; the block walks 32-row tiles.
-// Per tile: stage AX / dY2 rows in LDS (row-major for the row-operand reads and
-// transposed [col][row] for the contraction over rows), recompute, write the
-// wave's H1^T / dP1^T block transposed ([hidden][row]) so the row contraction
-// reads 16 contiguous bytes per fragment; next tile's rows are prefetched into
-// registers meanwhile.  Output: one fp32 slab per block,
-// gpart[block][HD][KF + 64] = [gW1^T | gW2], summed in fixed order afterwards.
+// Per tile: stage the AX / dY2 rows ONCE, row-major in swizzled 256-B rows: the
+// recompute reads them by rows (b128), the contractions over the rows by columns
+// with ds_read_b64_tr_b16 (no second, transposed copy).  The recomputed H1^T /
+// dP1^T accumulators (lane = row) are stored packed, 4 hidden units per 8-B write,
+// into the wave's own [row][hidden] images and read back transposed as the
+// contractions' A operands.  The next tile's rows are prefetched into registers
+// meanwhile.  Output: one fp32 slab per block, gpart[block][HD][KF + 64] =
+// [gW1^T | gW2], summed in fixed order afterwards.
+// (The round-1 form staged separate transposed images with 2-byte scattered writes
+// and wrote H1^T / dP1^T one element at a time: 0.74 ms on the ogbn-products shape.)
 // ============================================================================
 template <int KS, int KC, int HD>
 __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
@@ -247,18 +279,15 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
   constexpr int KF = (KP + 31) / 32 * 32;     // gW1^T columns (f), padded to whole tiles
   constexpr int CP = KC * 16;                 // classes, padded
   constexpr int W1S = KP + 8, W2S = CP + 8;
-  constexpr int AXS = KP + 8, DYS = CP + 8;
-  constexpr int TR = TILE + 8;                // transposed images: 32 rows + pad (80-B rows)
+  static_assert(KF <= 128 && CP <= 64, "staging rows are 256 B");
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* sW1T = lds;                       // [HD][W1S]
   uint16_t* sW2 = sW1T + HD * W1S;            // [HD][W2S]   W2 rows (hidden-major)
-  uint16_t* sAX = sW2 + HD * W2S;             // [32][AXS]   row-major tile
-  uint16_t* sDY = sAX + TILE * AXS;           // [32][DYS]
-  uint16_t* sAXt = sDY + TILE * DYS;          // [KF][TR]    transposed tile
-  uint16_t* sDYt = sAXt + KF * TR;            // [64][TR]
-  uint16_t* sH1t = sDYt + 64 * TR;            // [HD][TR]
-  uint16_t* sDPt = sH1t + HD * TR;            // [HD][TR]
-  float* sB1 = reinterpret_cast<float*>(sDPt + HD * TR);   // [HD]
+  uint16_t* sAX = sW2 + HD * W2S;             // [32][128]   swizzled (stg_off)
+  uint16_t* sDY = sAX + TILE * 128;           // [32][128]   swizzled, columns < 64 used
+  uint16_t* sH1 = sDY + TILE * 128;           // [NW][32][32] per-wave images (img_off)
+  uint16_t* sDP = sH1 + NW * TILE * 32;       // [NW][32][32]
+  float* sB1 = reinterpret_cast<float*>(sDP + NW * TILE * 32);   // [HD]
 
   const int tid = threadIdx.x;
   for (int i = tid; i < HD * KP; i += NT) {
@@ -270,14 +299,17 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
     sW2[nn * W2S + c] = bf16_bits(c < C ? W2[(size_t)nn * C + c] : 0.f);
   }
   for (int i = tid; i < HD; i += NT) sB1[i] = b1[i];
-  // zero the padding the per-tile staging never writes
-  for (int i = tid; i < TILE * AXS; i += NT) sAX[i] = 0;
-  for (int i = tid; i < TILE * DYS; i += NT) sDY[i] = 0;
-  for (int i = tid; i < KF * TR; i += NT) sAXt[i] = 0;
-  for (int i = tid; i < 64 * TR; i += NT) sDYt[i] = 0;
+  // zero the staging images: chunks the per-tile staging never writes (columns past
+  // the staged K, read by the padded contraction tiles) stay zero
+  for (int i = tid; i < 2 * TILE * 128 / 8; i += NT)
+    reinterpret_cast<uint4*>(sAX)[i] = make_uint4(0u, 0u, 0u, 0u);
 
   const int lane = tid & 63, h = lane >> 5, lr = lane & 31;
   const int t = tid >> 6;                     // this wave's hidden block
+  // transposed-read lane roles: 16-lane group, block row qq, column quad pq
+  const int gb = (lane >> 4) & 1, qq = (lane >> 2) & 3, pq = lane & 3;
+  uint16_t* wH1 = sH1 + t * TILE * 32;
+  uint16_t* wDP = sDP + t * TILE * 32;
   const int n_tiles = (n + TILE - 1) / TILE;
   const float scale = 1.f / (1.f - p);
   // 16-byte chunks staged per row: the K columns the products read (a row pitch wider
@@ -290,11 +322,8 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
   g2[0] = f32x16{};
   g2[1] = f32x16{};
 
-  // prefetch registers: chunks tid, tid + NT, ... of the AX tile and of the dY2 tile.
-  // Chunk i is row i % 32, 16-byte column chunk i / 32: consecutive lanes take
-  // consecutive rows, so the transposed image writes ([column][row], 2 bytes) of a
-  // wave land in consecutive bytes -- with row-major chunk order every lane of a wave
-  // hit the same LDS bank (32-way conflicts, 18 % of the kernel's wave cycles)
+  // prefetch registers: chunks tid, tid + NT, ... (chunk i = row i % 32, column chunk
+  // i / 32) of the AX tile and of the dY2 tile
   constexpr int PFX = (TILE * (KP / 8) + NT - 1) / NT, PFY = (TILE * (CP / 8) + NT - 1) / NT;
   uint4 pax[PFX], pdy[PFY];
   auto prefetch = [&](int tile) {
@@ -319,29 +348,19 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
   if ((int)blockIdx.x < n_tiles) prefetch(blockIdx.x);
   __syncthreads();
 
+  char* const bAX = reinterpret_cast<char*>(sAX);
+  char* const bDY = reinterpret_cast<char*>(sDY);
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    // ---- stage this tile (row-major + transposed), prefetch the next ----
+    // ---- stage this tile, prefetch the next ----
 #pragma unroll
     for (int k = 0; k < PFX; ++k) {
       const int i = tid + k * NT;
-      if (i < TILE * xch) {
-        const int rr = i % TILE, ch = i / TILE;
-        *reinterpret_cast<uint4*>(sAX + rr * AXS + 8 * ch) = pax[k];
-        const uint32_t w[4] = {pax[k].x, pax[k].y, pax[k].z, pax[k].w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sAXt[(8 * ch + e) * TR + rr] = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
-      }
+      if (i < TILE * xch) *reinterpret_cast<uint4*>(bAX + stg_off(i % TILE, i / TILE)) = pax[k];
     }
 #pragma unroll
     for (int k = 0; k < PFY; ++k) {
       const int i = tid + k * NT;
-      if (i < TILE * ych) {
-        const int rr = i % TILE, ch = i / TILE;
-        *reinterpret_cast<uint4*>(sDY + rr * DYS + 8 * ch) = pdy[k];
-        const uint32_t w[4] = {pdy[k].x, pdy[k].y, pdy[k].z, pdy[k].w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sDYt[(8 * ch + e) * TR + rr] = (uint16_t)(w[e >> 1] >> (16 * (e & 1)));
-      }
+      if (i < TILE * ych) *reinterpret_cast<uint4*>(bDY + stg_off(i % TILE, i / TILE)) = pdy[k];
     }
     if (tile + (int)gridDim.x < n_tiles) prefetch(tile + gridDim.x);
     __syncthreads();
@@ -351,37 +370,47 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
     f32x16 acc = {};
     {
       const uint16_t* arow = sW1T + (32 * t + lr) * W1S + 8 * h;
-      const uint16_t* xrow = sAX + lr * AXS + 8 * h;
 #pragma unroll
       for (int s2 = 0; s2 < KS; ++s2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(load_bf16x8(arow + 16 * s2), load_bf16x8(xrow + 16 * s2),
-                                                      acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            load_bf16x8(arow + 16 * s2),
+            load_bf16x8(reinterpret_cast<const uint16_t*>(bAX + stg_off(lr, 2 * s2 + h))), acc, 0, 0, 0);
     }
     f32x16 dh = {};
     {
       const uint16_t* arow = sW2 + (32 * t + lr) * W2S + 8 * h;
-      const uint16_t* yrow = sDY + lr * DYS + 8 * h;
 #pragma unroll
       for (int s2 = 0; s2 < KC; ++s2)
-        dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(load_bf16x8(arow + 16 * s2), load_bf16x8(yrow + 16 * s2),
-                                                     dh, 0, 0, 0);
+        dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            load_bf16x8(arow + 16 * s2),
+            load_bf16x8(reinterpret_cast<const uint16_t*>(bDY + stg_off(lr, 2 * s2 + h))), dh, 0, 0, 0);
     }
     uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
     if (thr8 > 0) {
       const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
       w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
     }
+    // registers 4g..4g+3 = hidden 32t + 8g + 4h + 0..3 of this lane's row: one packed
+    // 8-B write per image and g
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int nn = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
-      float x = fmaxf(acc[q] + sB1[nn], 0.f);
-      if (thr8 > 0) x = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
-      const float d = x > 0.f ? dh[q] * scale : 0.f;
-      sH1t[nn * TR + lr] = bf16_bits(x);
-      sDPt[nn * TR + lr] = bf16_bits(d);
+    for (int g = 0; g < 4; ++g) {
+      const float4 bb = *reinterpret_cast<const float4*>(sB1 + 32 * t + 8 * g + 4 * h);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+      float xv[4], dv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = 4 * g + i;
+        float x = fmaxf(acc[q] + bv[i], 0.f);
+        if (thr8 > 0) x = (((w[g] >> (8 * i)) & 0xffu) >= thr8) ? x * scale : 0.f;
+        xv[i] = x;
+        dv[i] = x > 0.f ? dh[q] * scale : 0.f;
+      }
+      const int off = img_off(lr, 2 * g + h);
+      *reinterpret_cast<uint2*>(reinterpret_cast<char*>(wH1) + off) = pack4(xv[0], xv[1], xv[2], xv[3]);
+      *reinterpret_cast<uint2*>(reinterpret_cast<char*>(wDP) + off) = pack4(dv[0], dv[1], dv[2], dv[3]);
     }
-    // the contraction below reads only this wave's own hidden rows of the H1^T / dP1^T
-    // images: a wave-local ordering of the LDS writes and reads suffices (no block barrier)
+    // the contraction below reads only this wave's own images: a wave-local ordering
+    // of the LDS writes and reads suffices (no block barrier)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -389,18 +418,20 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
     // ---- contractions over the tile's 32 rows (two k-steps of 16) ----
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 adp = load_bf16x8(sDPt + (32 * t + lr) * TR + 16 * s2 + 8 * h);
-      const bf16x8 ah1 = load_bf16x8(sH1t + (32 * t + lr) * TR + 16 * s2 + 8 * h);
+      const int ra = 16 * s2 + 8 * h + qq;      // block rows ra (+4 for the second read)
+      const bf16x8 adp = tr_frag(wDP, img_off(ra, 4 * gb + pq), img_off(ra + 4, 4 * gb + pq));
+      const bf16x8 ah1 = tr_frag(wH1, img_off(ra, 4 * gb + pq), img_off(ra + 4, 4 * gb + pq));
+      const int cb = 2 * gb + (pq >> 1), cx = 8 * (pq & 1);
 #pragma unroll
       for (int q = 0; q < KF / 32; ++q)
         g1[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            adp, load_bf16x8(sAXt + (32 * q + lr) * TR + 16 * s2 + 8 * h), g1[q], 0, 0, 0);
+            adp, tr_frag(sAX, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 4, 4 * q + cb) + cx), g1[q], 0, 0, 0);
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         g2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            ah1, load_bf16x8(sDYt + (32 * q + lr) * TR + 16 * s2 + 8 * h), g2[q], 0, 0, 0);
+            ah1, tr_frag(sDY, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 4, 4 * q + cb) + cx), g2[q], 0, 0, 0);
     }
-    __syncthreads();      // images are rewritten by the next tile
+    __syncthreads();      // the staging images are rewritten by the next tile
   }
 
   // ---- this block's partial slab: rows = hidden 32t + m, columns [f | KF + c] ----
@@ -511,9 +542,10 @@ static int fused_bwd_launch(const uint16_t* AX, const uint16_t* dY2, const float
                             const float* W2, float* gpart, int n, int F, int ldx, int C, int ldc, float p,
                             uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0,
                             const int* stepp, hipStream_t st) {
-  constexpr int KP = KS * 16, KF = (KP + 31) / 32 * 32, CP = KC * 16, TR = TILE + 8;
-  const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KP + 8) + (size_t)HD * (CP + 8) + TILE * (KP + 8) +
-                                         TILE * (CP + 8) + (size_t)KF * TR + 64 * TR + 2 * (size_t)HD * TR) +
+  constexpr int KP = KS * 16, CP = KC * 16;
+  // weights, two [32][128] staging images, two [HD/32][32][32] H1 / dP1 images, b1
+  const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KP + 8) + (size_t)HD * (CP + 8) + 2 * TILE * 128 +
+                                         2 * (size_t)HD * TILE) +
                      sizeof(float) * HD;
   if (lds > 160 * 1024) return -2;
   (void)hipFuncSetAttribute((const void*)gcn_fused_bwd_kernel<KS, KC, HD>,

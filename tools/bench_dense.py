@@ -23,11 +23,14 @@ def main():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--p", type=float, nargs="+", default=[0.5, 0.25, 0.1, 0.0])
+    ap.add_argument("--aligned", action="store_true", help="row pitches of the headline: whole 128-B lines")
     a = ap.parse_args()
     from cgnn_amd.gnn import ops
     dev = torch.device("cuda", 0)
     n, F, C, HD = a.rows, a.F, a.C, a.hidden
     ldx, ldc = (F + 1 + 7) // 8 * 8, (C + 7) // 8 * 8
+    if a.aligned:
+        ldx, ldc = (F + 1 + 63) // 64 * 64, (C + 63) // 64 * 64
     g = torch.Generator(device=dev).manual_seed(0)
     AX = torch.randn(n, ldx, device=dev, generator=g).to(torch.bfloat16)
     dY2 = (torch.randn(n, ldc, device=dev, generator=g) * 1e-3).to(torch.bfloat16)
