@@ -170,13 +170,15 @@ class GCNTrainer:
         # multi-GPU: the layer-1 aggregation of the NEXT epoch is computed into a second
         # buffer while the forward all-gather of Z2 is in flight (it does not depend on the
         # parameters), then the buffers swap; every epoch still performs its own SpMM
-        # One GPU: the same double buffer, filled on a side stream -- the next epoch's
-        # layer-1 aggregation runs concurrently with this epoch's dense, layer-2 and backward
-        # kernels (the gather-bound SpMM beside the latency-bound MFMA kernels).  Env
-        # CGNN_AX_PIPELINE=0 keeps it in line; a captured epoch (hipGraph) keeps it in line.
+        # One GPU, opt-in (env CGNN_AX_PIPELINE=1): the same double buffer filled on a side
+        # stream, so the next epoch's layer-1 aggregation runs concurrently with this
+        # epoch's dense, layer-2 and backward kernels.  Exact, but measured neutral on the
+        # products shape (208.2 vs 208.8 epochs/s): the SpMM's blocks occupy every CU and
+        # the dense forward (one 1024-thread, LDS-heavy block per CU) only starts as they
+        # drain -- the kernel trace shows it stretched from 0.33 to 2.4 ms, no overlap won.
         self._side = None
         pipe = (self.world == 1 and dev.type == "cuda" and not capture
-                and os.environ.get("CGNN_AX_PIPELINE", "1") != "0")
+                and os.environ.get("CGNN_AX_PIPELINE", "0") != "0")
         self.AX_next = torch.zeros_like(self.AX) if (self.world > 1 or pipe) else None
         if pipe:
             self._side = torch.cuda.Stream(dev)

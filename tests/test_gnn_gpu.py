@@ -501,8 +501,8 @@ def test_spmm_win_matches_reference(F, ld, R, WR, row_off, n_src):
 
 
 def test_gcn_side_stream_layer1_pipeline_is_exact(monkeypatch):
-    """One GPU: the next epoch's layer-1 aggregation on a side stream (default) gives
-    bitwise the same losses as the in-line schedule (CGNN_AX_PIPELINE=0), including an
+    """One GPU: the next epoch's layer-1 aggregation on a side stream (CGNN_AX_PIPELINE=1)
+    gives bitwise the same losses as the in-line schedule (default), including an
     evaluation between epochs."""
     g = synthetic("ogbn-products", seed=2, device="cuda:0", scale=0.002)
     runs = []
