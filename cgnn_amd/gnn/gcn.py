@@ -341,7 +341,8 @@ class GCNTrainer:
                 self._ax_event.record(self._side)
         H1 = self.H1[:n]
         p = self.p if train else 0.0
-        self.W2b[:, :C] = self.W2.to(torch.bfloat16)
+        if not self.fused_bwd:           # bf16 W2 of the unfused fallbacks (the fused kernels read fp32)
+            self.W2b[:, :C] = self.W2.to(torch.bfloat16)
         if not (self.fused and ops.dense_fwd(self.AX, self.W1, self.b1, self.W2, self.dinv,
                                              None if self.fused_bwd else H1,
                                              self.Z2loc[:n], F, p, self.key, self._dropout_step(), self.r0)):
