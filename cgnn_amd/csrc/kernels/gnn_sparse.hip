@@ -27,6 +27,19 @@ using namespace cgnn;
 #ifndef CGNN_SPMM_MINW
 #define CGNN_SPMM_MINW 1
 #endif
+// streamed operands (column indices, read once; the aggregate, written once) with the
+// non-temporal hint, so they do not displace gathered rows from the caches (A/B knob)
+#ifndef CGNN_SPMM_NT
+#define CGNN_SPMM_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+#if CGNN_SPMM_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 
 namespace {
 
@@ -121,7 +134,7 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
                                            int e0, int e1, int ldx, int f0, bool fv, int sub_base,
                                            int sl, float* acc, const float* __restrict__ cscale = nullptr) {
   for (int e = e0; e < e1; e += L) {
-    const int myj = (e + sl < e1) ? col[e + sl] : 0;
+    const int myj = (e + sl < e1) ? ld_stream(col + e + sl) : 0;
     const float mycs = CS ? cscale[myj] : 1.f;
     const int cnt = min(L, e1 - e);
     int k = 0;
@@ -407,7 +420,11 @@ __global__ __launch_bounds__(256, CGNN_SPMM_MINW) void spmm_kernel(
     y[q] = f < F ? v : (f == unit_col ? 1.f : 0.f);
   }
   if (YBF == 1) {
+#if CGNN_SPMM_NT
+    __builtin_nontemporal_store(f32x8_to_bf16(y), reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0));
+#else
     *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
+#endif
   } else if (YBF == 2) {
     f16x8 o;
 #pragma unroll

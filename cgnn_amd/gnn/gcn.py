@@ -194,6 +194,13 @@ class GCNTrainer:
         self.gslot, self.rp_T, self.col_T, self.maxT = self._train_columns(g, per)
         self.Gc_loc = torch.zeros(self.maxT, self.ldc, **bf)
         self.Gc = torch.zeros(self.maxT * self.world, self.ldc, **bf) if self.world > 1 else self.Gc_loc
+        if self.world > 1:
+            # backward aggregation split like the forward's: the edges to this rank's own
+            # train rows (slots [rank * maxT, + maxT), read straight from Gc_loc) run while
+            # the all-gather of the other ranks' compact gradients is in flight
+            lo = self.rank * self.maxT
+            self.rpT_loc, self.colT_loc, self.rpT_rem, self.colT_rem = self._split_local(
+                lo, lo + self.maxT, self.rp_T, self.col_T)
         self.H1 = torch.zeros(self.npad, hidden, **bf)
         self.dH1 = torch.zeros(self.npad, hidden, **bf)
         self.W2b = torch.zeros(hidden, self.ldc, **bf)
@@ -232,8 +239,11 @@ class GCNTrainer:
         cap_ok = dev.type == "cuda" and self.world == 1 and self.fused_bwd
         self._graph = StepGraph(self._train_body, enabled=bool(capture) and cap_ok, device=dev)
 
-    def _split_local(self, r0, r1):
-        rp, col = self.rowptr.long(), self.col.long()
+    def _split_local(self, r0, r1, rowptr=None, col=None):
+        """(rp, col) split into the edges whose column lies in [r0, r1) (columns shifted
+        by -r0) and the rest."""
+        rp = (self.rowptr if rowptr is None else rowptr).long()
+        col = (self.col if col is None else col).long()
         n = rp.numel() - 1
         rows = torch.repeat_interleave(torch.arange(n, device=col.device), rp[1:] - rp[:-1])
         loc = (col >= r0) & (col < r1)
@@ -376,8 +386,12 @@ class GCNTrainer:
     def backward(self, stats):
         n, F, C = self.nloc, self.F, self.C
         if self.world > 1:
-            torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc)
-        ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
+            work = torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc, async_op=True)
+            ops.spmm(self.rpT_loc, self.colT_loc, self.Gc_loc, C, out=self.part, out_dtype=torch.float32)
+            work.wait()
+            ops.spmm(self.rpT_rem, self.colT_rem, self.Gc, C, rscale=self.dinv, out=self.dY2, init=self.part)
+        else:
+            ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
         self.gb2.copy_(stats[4:4 + C])
         if self.fused_bwd:
             gW1, gb1, gW2, self._gpart = ops.fused_bwd(self.AX, self.dY2, self.W1, self.b1, self.W2, n, F,
