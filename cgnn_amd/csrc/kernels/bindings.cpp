@@ -58,6 +58,7 @@ int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, flo
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
 int gnn_spmm_ce_blocks(int);
 int gnn_spmm_win_rows(int);
+int gnn_slab_sum(const float*, long, int, float*, int, float*, const int*, hipStream_t);
 int gnn_spmm_win_plan(const int*, const int*, void*, int, int, int, int, int, hipStream_t);
 int gnn_launch_spmm_win(const int*, const int*, const void*, const void*, void*, const float*, int, int, int, int,
                         int, int, int, int, int, int, hipStream_t);
@@ -251,6 +252,11 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("gnn_spmm_ce_blocks", &gnn_spmm_ce_blocks);
   m.def("gnn_spmm_win_rows", &gnn_spmm_win_rows);
+  m.def("gnn_slab_sum", [](uint64_t P, long rows, int W, uint64_t stage, int G, uint64_t out, uint64_t map,
+                           uint64_t st) {
+    chk(gnn_slab_sum(Pt<const float>(P), rows, W, Pt<float>(stage), G, Pt<float>(out), Pt<const int>(map), S(st)),
+        "gnn_slab_sum");
+  });
   m.def("gnn_spmm_win_plan", [](uint64_t rowptr, uint64_t col, uint64_t split, int n_rows, int row_off, int n_src,
                                 int R, int WR, uint64_t st) {
     chk(gnn_spmm_win_plan(Pt<const int>(rowptr), Pt<const int>(col), Pt<void>(split), n_rows, row_off, n_src, R, WR,

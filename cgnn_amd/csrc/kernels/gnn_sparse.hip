@@ -382,6 +382,38 @@ __global__ void spmm_win_plan_kernel(const int* __restrict__ rowptr, const int* 
   split[i] = make_int2(a, b);
 }
 
+// Fixed-order column sums of per-block partials P [S][W] (fp32, row-major): block
+// (x, y) sums rows [y * per, (y + 1) * per) of columns [64 x, 64 x + 64), blockDim / 64
+// row lanes striding the rows, their sums combined in lane order -- deterministic, no
+// atomics.  With gridDim.y > 1 the result is a stage [gridDim.y][W] for a second pass;
+// with gridDim.y == 1 it is written to out[map[c]] (map[c] < 0: dropped; no map:
+// out[c]), so the final pass also scatters the sums into their places (e.g. the weight
+// gradients into the flat parameter-gradient buffer).
+__global__ __launch_bounds__(1024) void slab_sum_kernel(const float* __restrict__ P, long S, int W, long per,
+                                                       float* __restrict__ out, const int* __restrict__ map) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6, nrl = blockDim.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const long r0 = (long)blockIdx.y * per, r1 = min(S, r0 + per);
+  float acc = 0.f;
+  if (c < W) {
+#pragma unroll 8
+    for (long r = r0 + rl; r < r1; r += nrl) acc += P[r * W + c];
+  }
+  red[rl][cl] = acc;
+  __syncthreads();
+  if (rl == 0 && c < W) {
+    float v = red[0][cl];
+    for (int q = 1; q < nrl; ++q) v += red[q][cl];
+    if (gridDim.y > 1) {
+      out[(long)blockIdx.y * W + c] = v;
+    } else {
+      const int d = map ? map[c] : c;
+      if (d >= 0) out[d] = v;
+    }
+  }
+}
+
 template <int L, int XBF, int YBF, int U, bool CS>
 __global__ __launch_bounds__(256, CGNN_SPMM_MINW) void spmm_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
@@ -765,6 +797,24 @@ extern "C" int gnn_launch_spmm_win(const int* rowptr, const int* col, const void
     default: return -5;
   }
 #undef CGNN_WIN
+  return (int)hipGetLastError();
+}
+
+// out[map[c]] = sum_r P[r][c] (fixed order).  stage: fp32 [>= G * W] scratch for the
+// first of two passes when S is large (G groups of rows), or null for one pass.
+extern "C" int gnn_slab_sum(const float* P, long S, int W, float* stage, int G, float* out, const int* map,
+                            hipStream_t st) {
+  if (S <= 0 || W <= 0) return -3;
+  const unsigned gx = (unsigned)((W + 63) / 64);
+  if (stage && G > 1) {
+    const long per = (S + G - 1) / G;
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(gx, (unsigned)G), dim3(256), 0, st, P, S, W, per, stage,
+                       (const int*)nullptr);
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(gx, 1), dim3(1024), 0, st, (const float*)stage, (long)G, W,
+                       (long)G, out, map);
+  } else {
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(gx, 1), dim3(S >= 64 ? 1024 : 256), 0, st, P, S, W, S, out, map);
+  }
   return (int)hipGetLastError();
 }
 

@@ -229,6 +229,7 @@ class GCNTrainer:
         self.fused_bwd = (self.fused and dev.type == "cuda" and
                           ops.fused_bwd_supported(self.F, hidden, self.C))
         self._gpart = None
+        self._grad_index = None
         # capture=True (one GPU, fully fused path): the whole epoch (9 kernels + Adam) is
         # captured into a hipGraph and replayed; the dropout step is read from the device
         # step counter (Adam's), so replays draw the current epoch's mask.  Off by default:
@@ -394,12 +395,12 @@ class GCNTrainer:
             ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
         self.gb2.copy_(stats[4:4 + C])
         if self.fused_bwd:
-            gW1, gb1, gW2, self._gpart = ops.fused_bwd(self.AX, self.dY2, self.W1, self.b1, self.W2, n, F,
-                                                       self.p, self.key, self._dropout_step(), self.r0,
-                                                       self._gpart)
-            self.gW1.copy_(gW1)
-            self.gb1.copy_(gb1)
-            self.gW2.copy_(gW2)
+            if self._grad_index is None:
+                self._grad_index = ops.fused_bwd_grad_index(
+                    F, self.hidden, C, ops.fused_bwd_width(F), device=self.dev)
+            _, _, _, self._gpart = ops.fused_bwd(self.AX, self.dY2, self.W1, self.b1, self.W2, n, F,
+                                                 self.p, self.key, self._dropout_step(), self.r0,
+                                                 self._gpart, grads=self.grads, grad_index=self._grad_index)
             if self.world > 1:
                 torch.distributed.all_reduce(self.grads)
             return

@@ -108,7 +108,9 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
                         init.data_ptr() if init is not None else 0, init.shape[1] if init is not None else 0,
                         n, C, ld, mode, float(inv_count), _st(Z),
                         gslot.data_ptr() if gslot is not None else 0)
-        return stats.sum(0), G
+        out = torch.empty(68, dtype=torch.float32, device=Z.device)
+        slab_sum(stats, out)
+        return out, G
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, C, dtype=torch.float32)
     acc.index_add_(0, rows, Z[col.long(), :C].float())
@@ -139,6 +141,39 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
             G.zero_()
             G[:, :C] = gval.to(G.dtype)
     return stats, G
+
+
+_STAGE = {}
+
+
+def slab_sum(P, out, index=None, groups=None):
+    """out[index[c]] = sum_r P[r, c] (``index`` None: out[c]; index < 0: dropped) -- the
+    fixed-order column sum of per-block partials (deterministic, no atomics), in one pass
+    or, for many rows, two (``groups`` row groups, default 512 when P has > 4096 rows).
+    On the CPU: the same sums with torch."""
+    S, W = P.shape
+    if not P.is_cuda:
+        v = P.sum(0)
+        if index is None:
+            out[:W] = v
+        else:
+            keep = index >= 0
+            out[index[keep].long()] = v[keep]
+        return out
+    if not (P.dtype == torch.float32 and out.dtype == torch.float32 and P.is_contiguous()):
+        raise TypeError("slab_sum: contiguous fp32 partials and fp32 output expected")
+    if index is not None and (index.dtype != torch.int32 or index.numel() != W):
+        raise TypeError("slab_sum: index must be int32 of the partials' width")
+    G = groups if groups is not None else (512 if S > 4096 else 1)
+    stage = None
+    if G > 1:
+        key = (P.device, G * W)
+        stage = _STAGE.get(key)
+        if stage is None:
+            stage = _STAGE[key] = torch.empty(G * W, dtype=torch.float32, device=P.device)
+    native.hip().gnn_slab_sum(P.data_ptr(), S, W, stage.data_ptr() if stage is not None else 0, G,
+                              out.data_ptr(), index.data_ptr() if index is not None else 0, _st(P))
+    return out
 
 
 def win_start(rb0: int, R: int, WR: int, row_off: int, n_src: int) -> int:
@@ -334,10 +369,12 @@ def fused_bwd_supported(F, hidden, C):
     return bool(native.hip().gnn_fused_bwd_supported(int(F) + 1, int(hidden), int(C)))
 
 
-def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None):
+def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None, grads=None, grad_index=None):
     """Fused GCN dense backward (GPU): recomputes H1 from AX, then
     dP1 = (dY2 W2^T) * [H1 > 0] / (1-p) and the weight gradients in one pass.
-    Returns (gW1 [F, HD], gb1 [HD], gW2 [HD, C], gpart)."""
+    Returns (gW1 [F, HD], gb1 [HD], gW2 [HD, C], gpart); with ``grads`` (the flat fp32
+    gradient buffer, gW1 | gb1 | gW2 at its start) the sums are written there instead
+    and (None, None, None, gpart) is returned."""
     hip = native.hip()
     HD, C = W1.shape[1], W2.shape[1]
     ldx = AX.shape[1]
@@ -350,9 +387,35 @@ def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None):
                            sv, int(row0), _st(AX), step_ptr=sp)
     if rc != 0:
         raise RuntimeError("gnn_fused_bwd failed (%d)" % rc)
+    if grads is not None:
+        # fixed-order reduction over the block slabs, scattered straight into the flat
+        # gradient buffer [gW1 (F x HD) | gb1 | gW2 (HD x C) | ...]
+        if grad_index is None:
+            grad_index = fused_bwd_grad_index(F, HD, C, width, device=AX.device)
+        slab_sum(gpart.view(nb, HD * width), grads, grad_index)
+        return None, None, None, gpart
     g = gpart.sum(0)                     # fixed-order reduction over the block slabs
     kf = width - 64
     return g[:, :F].t(), g[:, F], g[:, kf:kf + C], gpart
+
+
+def fused_bwd_width(F):
+    """Row width of a fused-backward slab for F features (+ the ones column)."""
+    return native.hip().gnn_fused_bwd_width(int(F) + 1)
+
+
+def fused_bwd_grad_index(F, HD, C, width, device=None):
+    """Destination in the flat gradient buffer [gW1 (F x HD) | gb1 (HD) | gW2 (HD x C)] of
+    every element (h, j) of a fused-backward slab [HD][width] (-1: padding)."""
+    kf = width - 64
+    h = torch.arange(HD).view(HD, 1)
+    j = torch.arange(width).view(1, width)
+    n1 = F * HD
+    idx = torch.full((HD, width), -1, dtype=torch.int64)
+    idx = torch.where(j < F, j * HD + h, idx)
+    idx = torch.where(j == F, n1 + h, idx)
+    idx = torch.where((j >= kf) & (j < kf + C), n1 + HD + h * C + (j - kf), idx)
+    return idx.view(-1).to(torch.int32).to(device)
 
 
 def relu_dropout_bwd_(dH, H, p):

@@ -516,3 +516,29 @@ def test_gcn_side_stream_layer1_pipeline_is_exact(monkeypatch):
         runs.append((losses, ev))
     assert runs[0][0] == runs[1][0]
     assert runs[0][1] == runs[1][1]
+
+
+@pytest.mark.parametrize("S,W,G,mapped", [(76531, 68, None, False), (256, 49152, None, True), (7, 5, 1, False),
+                                          (5000, 130, 64, True)])
+def test_slab_sum_matches_torch(S, W, G, mapped):
+    """Fixed-order column sums of block partials (one or two passes, optional scatter)."""
+    torch.manual_seed(0)
+    P = torch.randn(S, W, device="cuda:0")
+    ref = P.double().sum(0).float()
+    if mapped:
+        perm = torch.randperm(W + 9, device="cuda:0")[:W].to(torch.int32)
+        perm[::7] = -1
+        out = torch.zeros(W + 9, device="cuda:0")
+        ops.slab_sum(P, out, perm, groups=G)
+        keep = perm >= 0
+        got, want = out[perm[keep].long()], ref[keep]
+        assert torch.all(out[torch.tensor(sorted(set(range(W + 9)) - set(perm[keep].tolist())),
+                                          dtype=torch.long, device="cuda:0")] == 0)
+    else:
+        out = torch.empty(W, device="cuda:0")
+        ops.slab_sum(P, out, groups=G)
+        got, want = out, ref
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-3)
+    out2 = out.clone()
+    ops.slab_sum(P, out2, perm if mapped else None, groups=G)
+    assert torch.equal(out, out2)          # deterministic

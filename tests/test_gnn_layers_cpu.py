@@ -191,3 +191,20 @@ def test_window_plan_split_marks_exactly_the_in_window_edges():
             assert torch.all((c[a:b] >= w0) & (c[a:b] < w0 + plan.WR))
             assert torch.all((c[:a] < w0)) and torch.all(c[b:] >= w0 + plan.WR)
         assert 0 < plan.in_window_fraction() <= 1
+
+
+def test_fused_bwd_grad_index_scatters_the_slab_layout():
+    """The index map that scatters a fused-backward slab sum [HD][width] into the flat
+    gradient buffer reproduces (gW1 = g[:, :F]^T, gb1 = g[:, F], gW2 = g[:, kf:kf+C])."""
+    from cgnn_amd.gnn import ops
+    F, HD, C, width = 100, 64, 47, 192
+    kf = width - 64
+    g = torch.randn(3, HD, width)
+    flat = torch.zeros(F * HD + HD + HD * C + C)
+    idx = ops.fused_bwd_grad_index(F, HD, C, width)
+    ops.slab_sum(g.view(3, -1), flat, idx)
+    s = g.sum(0)
+    assert torch.allclose(flat[:F * HD].view(F, HD), s[:, :F].t())
+    assert torch.allclose(flat[F * HD:F * HD + HD], s[:, F])
+    assert torch.allclose(flat[F * HD + HD:F * HD + HD + HD * C].view(HD, C), s[:, kf:kf + C])
+    assert torch.all(flat[F * HD + HD + HD * C:] == 0)
