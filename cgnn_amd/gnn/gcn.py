@@ -194,7 +194,8 @@ class GCNTrainer:
         self.gslot, self.rp_T, self.col_T, self.maxT = self._train_columns(g, per)
         self.Gc_loc = torch.zeros(self.maxT, self.ldc, **bf)
         self.Gc = torch.zeros(self.maxT * self.world, self.ldc, **bf) if self.world > 1 else self.Gc_loc
-        if self.world > 1:
+        self._bwd_overlap = self.world > 1 and os.environ.get("CGNN_BWD_OVERLAP", "0") != "0"
+        if self._bwd_overlap:
             # backward aggregation split like the forward's: the edges to this rank's own
             # train rows (slots [rank * maxT, + maxT), read straight from Gc_loc) run while
             # the all-gather of the other ranks' compact gradients is in flight
@@ -386,12 +387,14 @@ class GCNTrainer:
 
     def backward(self, stats):
         n, F, C = self.nloc, self.F, self.C
-        if self.world > 1:
+        if self.world > 1 and self._bwd_overlap:
             work = torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc, async_op=True)
             ops.spmm(self.rpT_loc, self.colT_loc, self.Gc_loc, C, out=self.part, out_dtype=torch.float32)
             work.wait()
             ops.spmm(self.rpT_rem, self.colT_rem, self.Gc, C, rscale=self.dinv, out=self.dY2, init=self.part)
         else:
+            if self.world > 1:
+                torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc)
             ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
         self.gb2.copy_(stats[4:4 + C])
         if self.fused_bwd:

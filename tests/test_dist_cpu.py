@@ -79,10 +79,14 @@ def _gcn_worker(rank, world, port, out, halo=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,halo", [(2, False), (2, True), (4, None)])
-def test_gcn_row_partition_matches_single_process(world, halo):
+@pytest.mark.parametrize("world,halo,overlap", [(2, False, "0"), (2, True, "0"), (4, None, "0"), (2, False, "1"),
+                                                (4, None, "1")])
+def test_gcn_row_partition_matches_single_process(world, halo, overlap, monkeypatch):
     """Row-partitioned GCN over gloo ranks == one process; layer-2 rows of other
-    ranks by all-gather or by the halo all-to-all (the default from 4 ranks)."""
+    ranks by all-gather or by the halo all-to-all (the default from 4 ranks); the
+    backward's compact-gradient all-gather blocking or overlapped with the local edges
+    (CGNN_BWD_OVERLAP)."""
+    monkeypatch.setenv("CGNN_BWD_OVERLAP", overlap)
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
     g = synthetic("ogbn-products", seed=0, scale=0.002)
