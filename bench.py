@@ -72,6 +72,11 @@ def main():
         # no launcher around us: start the N ranks here (children re-run this script)
         sys.exit(_launcher().spawn_ranks(a.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
 
+    if os.environ.get("CGNN_TRACEBACK_AFTER"):
+        # diagnostics: dump every thread's Python stack to stderr periodically (a hung rank
+        # shows where it waits)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["CGNN_TRACEBACK_AFTER"]), repeat=True)
     import torch
     import torch.distributed as dist
     from cgnn_amd.parallel import dist as pdist
