@@ -6,7 +6,9 @@ an ogbn-products-shaped graph, 1/2/4/8 MI355X.
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One step = one full-graph training epoch (forward + backward + Adam) over all
-2,449,029 nodes.  Data: synthetic graph of the ogbn-products shape (no network
+2,449,029 nodes (layer 1 and both dense layers at every row; the layer-2
+aggregation at the train rows, the only rows whose logits reach the loss --
+exact, see gnn/gcn.py; CGNN_L2_ALL_ROWS=1 aggregates every row).  Data: synthetic graph of the ogbn-products shape (no network
 for the real dataset), random-init weights.  Multi-GPU: 1-D row partition of
 the graph over ranks (strong scaling: the whole job trains the same graph),
 RCCL all-gathers of the layer-2 activations / gradients and an all-reduce of
@@ -168,7 +170,9 @@ def main():
                        "seq_len": None, "parallelism": "graph-rowpart%d" % world,
                        "dataset": a.dataset, "nnz_with_self_loops": nnz, "dropout": a.dropout,
                        "optimizer": "adam", "lr": a.lr, "id_order": a.id_order,
-                       "reordered": a.reorder != "none"},
+                       "reordered": a.reorder != "none",
+                       # training epochs aggregate layer 2 at the rows the loss reads
+                       "train_layer2_rows": "all" if tr._l2 is None else "train"},
             "val_acc": round(res["val_acc"], 4),
             "test_acc": round(res["test_acc"], 4),
             "train_loss": round(train_loss, 5),

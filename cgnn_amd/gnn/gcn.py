@@ -10,9 +10,12 @@ One epoch = one full-graph forward + backward + optimizer step:
   2. H1   = dropout(relu(AX W1 + b1))      } one fused MFMA kernel (gnn_dense.hip): both GEMMs,
   3. Z2   = D^-1/2 (H1 W2)                 } bias, ReLU, Philox dropout, row scale; Z2 all-gathered
   4. loss, G = spmm_ce(Z2)                 aggregate + bias + log-softmax + NLL + dlogits, fused;
+                                           in training only at the train rows (8 % of
+                                           ogbn-products): no other row's logits reach the
+                                           loss; evaluation aggregates every row.
                                            G is stored COMPACT: dL/dlogits is zero outside
-                                           the train rows (8 % of ogbn-products), so only
-                                           train rows are written, to slots 0..T-1
+                                           the train rows, so only train rows are written,
+                                           to slots 0..T-1
   5. dY2  = D^-1/2 spmm_T(G)               Â symmetric; spmm_T runs over the train COLUMNS
                                            of the adjacency only (a CSR built once: 9.5 M
                                            of the 118 M entries) -- the same sums, without
@@ -38,6 +41,7 @@ from __future__ import annotations
 
 import math
 import os
+import types
 from typing import Optional
 
 import numpy as np
@@ -194,11 +198,13 @@ class GCNTrainer:
         self.gslot, self.rp_T, self.col_T, self.maxT = self._train_columns(g, per)
         self.Gc_loc = torch.zeros(self.maxT, self.ldc, **bf)
         self.Gc = torch.zeros(self.maxT * self.world, self.ldc, **bf) if self.world > 1 else self.Gc_loc
-        self._bwd_overlap = self.world > 1 and os.environ.get("CGNN_BWD_OVERLAP", "0") != "0"
+        self._bwd_overlap = self.world > 1 and os.environ.get("CGNN_BWD_OVERLAP", "1") != "0"
         if self._bwd_overlap:
             # backward aggregation split like the forward's: the edges to this rank's own
             # train rows (slots [rank * maxT, + maxT), read straight from Gc_loc) run while
-            # the all-gather of the other ranks' compact gradients is in flight
+            # the all-gather of the other ranks' compact gradients is in flight.  Default
+            # on: the 4-rank one-GPU rehearsal reproduces the serial schedule's loss bit
+            # for bit (profiles/r02_final/r4_ov{0,1}.log); CGNN_BWD_OVERLAP=0 serialises
             lo = self.rank * self.maxT
             self.rpT_loc, self.colT_loc, self.rpT_rem, self.colT_rem = self._split_local(
                 lo, lo + self.maxT, self.rp_T, self.col_T)
@@ -220,6 +226,15 @@ class GCNTrainer:
             self.Z2 = None
         else:
             self.Z2 = torch.zeros(per * self.world, self.ldc, **bf) if self.world > 1 else self.Z2loc
+        # Training epochs aggregate layer 2 only at the rows the loss reads (this rank's
+        # train rows): the other rows' logits enter neither the loss nor any gradient, so
+        # the update is the same (the output-node pruning of DGL's last message-flow
+        # block); every layer-1 row and every Z2 row is still computed, and evaluate()
+        # aggregates all rows.  Env CGNN_L2_ALL_ROWS=1: all rows in training too.
+        self._l2 = None
+        trows = torch.nonzero(self.mask == 1).flatten()
+        if trows.numel() and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
+            self._l2 = self._train_row_csr(trows)
         self.epoch = 0
         self.last_stats = None
         # fused MFMA dense kernels (gnn_dense.hip); shapes they do not cover fall back to
@@ -260,40 +275,82 @@ class GCNTrainer:
         c, d = csr(~loc, 0)
         return a, b, c, d
 
-    def _setup_halo(self, r0, r1, per):
-        """Exchange plan of the layer-2 halo: the distinct remote source rows this rank
-        reads (sorted global ids, hence grouped by owner in rank order) are requested
-        from their owners once; each epoch every rank sends the requested rows of its Z2
-        with one all-to-all, and the remote edges index the received buffer."""
+    def _halo_plan(self, col_rem):
+        """Exchange plan of a layer-2 halo: the distinct remote source rows that the
+        edges ``col_rem`` (global ids) read -- sorted, hence grouped by owner in rank
+        order -- are requested from their owners once; each exchange every rank sends
+        the requested rows of its Z2 with one all-to-all.  Returns the plan with
+        ``col``: the edges re-indexed into the received buffer."""
         dist = torch.distributed
         dev = self.dev
-        col_rem = self.col_rem.long()
+        col_rem = col_rem.long()
         need = torch.unique(col_rem)                                  # sorted global ids
-        recv_counts = torch.bincount(need // per, minlength=self.world).to(torch.int64)
+        recv_counts = torch.bincount(need // self.per, minlength=self.world).to(torch.int64)
         send_counts = torch.empty_like(recv_counts)
         dist.all_to_all_single(send_counts, recv_counts)
         rc, sc = [int(v) for v in recv_counts.tolist()], [int(v) for v in send_counts.tolist()]
         req = torch.empty(sum(sc), dtype=torch.int64, device=dev)
         dist.all_to_all_single(req, need, output_split_sizes=sc, input_split_sizes=rc)
-        if req.numel() and (int(req.min()) < r0 or int(req.max()) >= r1):
+        if req.numel() and (int(req.min()) < self.r0 or int(req.max()) >= self.r1):
             raise RuntimeError("halo plan: a peer requested a row this rank does not own")
-        self.send_idx = (req - r0).contiguous()
-        self.recv_splits, self.send_splits = rc, sc
-        self.col_rem = torch.searchsorted(need, col_rem).to(torch.int32).contiguous()
         bf = dict(dtype=torch.bfloat16, device=dev)
-        self.Zrecv = torch.zeros(max(sum(rc), 1), self.ldc, **bf)
-        self.Zsend = torch.zeros(max(sum(sc), 1), self.ldc, **bf)
+        return types.SimpleNamespace(
+            need=need, send_idx=(req - self.r0).contiguous(), recv_splits=rc, send_splits=sc,
+            col=torch.searchsorted(need, col_rem).to(torch.int32).contiguous(),
+            Zrecv=torch.zeros(max(sum(rc), 1), self.ldc, **bf),
+            Zsend=torch.zeros(max(sum(sc), 1), self.ldc, **bf))
 
-    def _exchange_z2(self):
-        """Start the transfer of the other ranks' layer-2 rows; returns (work, buffer the
-        remote edges index)."""
-        if not self.halo:
+    def _setup_halo(self, r0, r1, per):
+        """The full halo (every remote row this rank's edges read): evaluation, and
+        training with CGNN_L2_ALL_ROWS=1."""
+        self._hplan = self._halo_plan(self.col_rem)
+        self.col_rem = self._hplan.col
+
+    def _train_row_csr(self, trows):
+        """Layer-2 operands of the train rows ``trows`` (local ids, ascending): their
+        CSR rows, output-row scale / labels / split, the compact-gradient slot (the k-th
+        train row of this rank is slot k, as in ``_train_columns``), and on several ranks
+        the same local / remote edge split (remote columns re-indexed like ``col_rem``)."""
+        dev = self.dev
+        rp = self.rowptr.long()
+        lo, deg = rp[trows], rp[trows + 1] - rp[trows]
+        trp = torch.zeros(trows.numel() + 1, dtype=torch.int64, device=dev)
+        trp[1:] = torch.cumsum(deg, 0)
+        eid = torch.arange(int(trp[-1]), device=dev) + torch.repeat_interleave(lo - trp[:-1], deg)
+        l2 = types.SimpleNamespace(
+            rp=trp.to(torch.int32).contiguous(), col=self.col[eid].contiguous(),
+            dinv=self.dinv[trows].contiguous(), y=self.y[trows].contiguous(),
+            mask=self.mask[trows].contiguous(),
+            gslot=torch.arange(trows.numel(), dtype=torch.int32, device=dev))
+        l2.plan = None
+        if self.world > 1:
+            l2.rp_loc, l2.col_loc, l2.rp_rem, col_rem = self._split_local(self.r0, self.r1, l2.rp, l2.col)
+            if torch.distributed.is_initialized() and os.environ.get("CGNN_TRAIN_HALO", "1") != "0":
+                # a halo of its own: only the remote rows the train rows read travel in
+                # training epochs (planted-community graph after the reorder: ~10 % of
+                # the other ranks' rows at 8 ranks, ~40 % at 2, against 66-97 % for the
+                # full halo); env CGNN_TRAIN_HALO=0: the evaluation's exchange
+                l2.plan = self._halo_plan(col_rem)
+                col_rem = l2.plan.col
+            elif self.halo:
+                col_rem = torch.searchsorted(self._hplan.need, col_rem.long()).to(torch.int32)
+            l2.col_rem = col_rem.contiguous()
+            l2.part = torch.zeros(trows.numel(), self.ldc, dtype=torch.float32, device=dev)
+        return l2
+
+    def _exchange_z2(self, plan=None):
+        """Start the transfer of the other ranks' layer-2 rows: the halo of ``plan``
+        or, without one, the full halo (``self.halo``) or an all-gather of every row.
+        Returns (work, buffer the remote edges index)."""
+        if plan is None and self.halo:
+            plan = self._hplan
+        if plan is None:
             return torch.distributed.all_gather_into_tensor(self.Z2, self.Z2loc, async_op=True), self.Z2
-        S, R = sum(self.send_splits), sum(self.recv_splits)
-        torch.index_select(self.Z2loc, 0, self.send_idx, out=self.Zsend[:S])
-        work = torch.distributed.all_to_all_single(self.Zrecv[:R], self.Zsend[:S], self.recv_splits,
-                                                   self.send_splits, async_op=True)
-        return work, self.Zrecv
+        S, R = sum(plan.send_splits), sum(plan.recv_splits)
+        torch.index_select(self.Z2loc, 0, plan.send_idx, out=plan.Zsend[:S])
+        work = torch.distributed.all_to_all_single(plan.Zrecv[:R], plan.Zsend[:S], plan.recv_splits,
+                                                   plan.send_splits, async_op=True)
+        return work, plan.Zrecv
 
     def _train_columns(self, g: GraphData, per: int):
         """Slots of the compact gradient and the local CSR restricted to train columns.
@@ -367,22 +424,34 @@ class GCNTrainer:
             y2 = _mm_f32(H1, self.W2b)
             torch.mul(y2, self.dinv[:, None], out=y2)
             self.Z2loc[:n] = y2.to(torch.bfloat16)
+        l2 = self._l2 if train else None          # train rows only (see __init__)
         if self.world > 1:
             # the Z2 exchange is the epoch's one large transfer (up to [n, 48] bf16, 7/8
             # of it inbound at 8 ranks): the rank-local layer-2 edges and, in training, the
             # next epoch's layer-1 aggregation (parameter-independent) run while it is in flight
-            work, zsrc = self._exchange_z2()
-            ops.spmm(self.rp_loc, self.col_loc, self.Z2loc, C, out=self.part, out_dtype=torch.float32)
+            work, zsrc = self._exchange_z2(l2.plan if l2 is not None else None)
+            if l2 is not None:
+                ops.spmm(l2.rp_loc, l2.col_loc, self.Z2loc, C, out=l2.part, out_dtype=torch.float32)
+            else:
+                ops.spmm(self.rp_loc, self.col_loc, self.Z2loc, C, out=self.part, out_dtype=torch.float32)
             if train:
                 self._aggregate_features(self.AX_next)
             work.wait()
-            rp, col, init = self.rp_rem, self.col_rem, self.part
+            if l2 is not None:
+                rp, col, init = l2.rp_rem, l2.col_rem, l2.part
+            else:
+                rp, col, init = self.rp_rem, self.col_rem, self.part
+        elif l2 is not None:
+            rp, col, init, zsrc = l2.rp, l2.col, None, self.Z2
         else:
             rp, col, init, zsrc = self.rowptr, self.col, None, self.Z2
-        stats, _ = ops.spmm_ce(rp, col, zsrc, C, self.dinv, self.b2, self.y, self.mask,
+        if l2 is not None:
+            dinv, y, mask, gslot = l2.dinv, l2.y, l2.mask, l2.gslot
+        else:
+            dinv, y, mask, gslot = self.dinv, self.y, self.mask, (self.gslot if train else None)
+        stats, _ = ops.spmm_ce(rp, col, zsrc, C, dinv, self.b2, y, mask,
                                1.0 / max(self.n_train, 1), mode=0 if train else 1,
-                               G=self.Gc_loc if train else None, init=init,
-                               gslot=self.gslot if train else None)
+                               G=self.Gc_loc if train else None, init=init, gslot=gslot)
         return stats
 
     def backward(self, stats):

@@ -70,6 +70,8 @@ def _gcn_worker(rank, world, port, out, halo=None):
     g = synthetic("ogbn-products", seed=0, scale=0.002)
     tr = GCNTrainer(g, hidden=64, halo=halo)
     assert tr.halo == (halo if halo is not None else world >= 4)
+    if tr._l2 is not None:
+        assert (tr._l2.plan is not None) == (os.environ["CGNN_TRAIN_HALO"] != "0")
     tr.train_step()
     p1 = tr.params.clone().numpy().tolist()
     for _ in range(3):
@@ -79,18 +81,25 @@ def _gcn_worker(rank, world, port, out, halo=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,halo,overlap", [(2, False, "0"), (2, True, "0"), (4, None, "0"), (2, False, "1"),
-                                                (4, None, "1")])
-def test_gcn_row_partition_matches_single_process(world, halo, overlap, monkeypatch):
+@pytest.mark.parametrize("world,halo,overlap,all_rows,train_halo", [
+    (2, False, "0", "0", "0"), (2, True, "0", "0", "0"), (4, None, "0", "0", "0"), (2, False, "1", "0", "1"),
+    (4, None, "1", "0", "1"), (2, True, "1", "1", "1"), (4, None, "1", "1", "1"), (3, True, "1", "0", "1")])
+def test_gcn_row_partition_matches_single_process(world, halo, overlap, all_rows, train_halo, monkeypatch):
     """Row-partitioned GCN over gloo ranks == one process; layer-2 rows of other
     ranks by all-gather or by the halo all-to-all (the default from 4 ranks); the
     backward's compact-gradient all-gather blocking or overlapped with the local edges
-    (CGNN_BWD_OVERLAP)."""
+    (CGNN_BWD_OVERLAP); training layer 2 over the train rows only (default) or over
+    every row (CGNN_L2_ALL_ROWS=1, against the one-process train-row run); the
+    training epochs' own halo of the train rows' sources (CGNN_TRAIN_HALO)."""
     monkeypatch.setenv("CGNN_BWD_OVERLAP", overlap)
+    monkeypatch.setenv("CGNN_L2_ALL_ROWS", "0")
+    monkeypatch.setenv("CGNN_TRAIN_HALO", train_halo)
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
     g = synthetic("ogbn-products", seed=0, scale=0.002)
     tr = GCNTrainer(g, hidden=64, rank=0, world=1)
+    assert tr._l2 is not None
+    monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
     tr.train_step()
     p1 = tr.params.clone().numpy()
     for _ in range(3):
@@ -109,6 +118,27 @@ def test_gcn_row_partition_matches_single_process(world, halo, overlap, monkeypa
     # the ranks hold bitwise-identical replicated parameters
     for r in range(1, world):
         np.testing.assert_array_equal(out[0][1], out[r][1])
+
+
+def test_gcn_train_row_layer2_matches_all_rows(monkeypatch):
+    """Training epochs that aggregate layer 2 only at the train rows give the same
+    losses and parameters as aggregating every row (one process)."""
+    from cgnn_amd.gnn.data import synthetic
+    from cgnn_amd.gnn.gcn import GCNTrainer
+    g = synthetic("ogbn-products", seed=1, scale=0.002)
+    runs = []
+    for all_rows in ("1", "0"):
+        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
+        tr = GCNTrainer(g, hidden=64, rank=0, world=1)
+        assert (tr._l2 is None) == (all_rows == "1")
+        losses = []
+        for _ in range(4):
+            tr.train_step()
+            losses.append(tr.train_loss())
+        runs.append((losses, tr.params.clone(), tr.evaluate()))
+    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=1e-5)
+    torch.testing.assert_close(runs[1][1], runs[0][1], rtol=1e-4, atol=1e-5)
+    assert runs[1][2] == pytest.approx(runs[0][2], rel=1e-4, abs=1e-4)
 
 
 def _mmd_data():
