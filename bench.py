@@ -54,7 +54,7 @@ def main():
     ap.add_argument("--rows", choices=["auto", "aligned", "packed", "mixed"], default="auto",
                     help="row pitch of gathered matrices: whole 128-B lines, packed to 8 elements, "
                          "mixed (features aligned, layer-2 rows packed), "
-                         "or auto (features aligned; layer-2 rows aligned on one GPU only)")
+                         "or auto (features aligned, layer-2 rows packed: the same as mixed)")
     ap.add_argument("--no-fused", action="store_true", help="hipBLASLt GEMMs + separate epilogues")
     ap.add_argument("--capture", action="store_true", help="replay the epoch from a hipGraph (one GPU)")
     ap.add_argument("--id-order", choices=["shuffled", "banded"], default="shuffled",

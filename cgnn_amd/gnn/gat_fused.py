@@ -11,6 +11,8 @@ input, so they fold into the projection ``Wc = [W | W a_src | W a_dst]``):
                                               first exchange [Wh | s_src] halo rows)
             layer 1: h1 = bf16(dropout(elu(out + b1)))        gat_act_fwd
             layer 2: loss, dlogits = CE(out + b2) (train rows) gat_row_ce
+                      (training epochs aggregate layer 2 at the train rows only:
+                      no other row's logits reach the loss -- exact)
   backward  dWh, ds_src, ds_dst               gat_bwd_row / gat_bwd_col (+ halo
                                               reduce-back of the received rows)
             dy = bf16([dWh | ds_src | ds_dst])                 gat_pack_grad
@@ -30,6 +32,8 @@ bf16-stored arithmetic), so the sharded path is tested with gloo ranks on CPU.
 from __future__ import annotations
 
 import math
+import os
+import types
 from typing import Optional
 
 import torch
@@ -227,7 +231,7 @@ def wcat_bwd(dWc, W, a_src, a_dst, gW, ga_src, ga_dst):
 
 
 class _Layer:
-    pass
+    tr = None                 # the train-row CSR of the last training forward, if any
 
 
 class FusedGAT:
@@ -299,6 +303,26 @@ class FusedGAT:
         self.dout1b = torch.zeros(self.nloc, L1.KF, **bf)
         self.dout2 = torch.zeros(self.nloc, L2.KF, dtype=torch.float32, device=dev)
         self.dout2b = torch.zeros(self.nloc, L2.KF, **bf)
+        # Training epochs aggregate layer 2 only at this rank's train rows (the only
+        # logits the loss reads; the epoch's update is unchanged -- the output-node
+        # pruning of DGL's last block): a CSR of those rows over the same sources.
+        # Evaluation aggregates every row.  Env CGNN_L2_ALL_ROWS=1: every row always.
+        self._tr = None
+        trows = torch.nonzero(self.mask == 1).flatten()
+        if trows.numel() and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
+            from .gat import GraphCSR
+            rp = g.rowptr.long()
+            lo, deg = rp[trows], rp[trows + 1] - rp[trows]
+            trp = torch.zeros(trows.numel() + 1, dtype=torch.int64, device=dev)
+            trp[1:] = torch.cumsum(deg, 0)
+            eid = torch.arange(int(trp[-1]), device=dev) + torch.repeat_interleave(lo - trp[:-1], deg)
+            nT = trows.numel()
+            self._tr = types.SimpleNamespace(
+                rows=trows, g=GraphCSR(trp.to(g.rowptr.dtype), g.col[eid], nT, g.n_cols),
+                y=self.y[trows].contiguous(), mask=self.mask[trows].contiguous(),
+                dout=torch.zeros(nT, L2.KF, dtype=torch.float32, device=dev),
+                doutb=torch.zeros(nT, L2.KF, **bf))
+            self.dout2 = self.dout2b = None          # all-row layer-2 gradients: not needed
         self.epoch = 0
         self.last_stats = None
 
@@ -313,7 +337,8 @@ class FusedGAT:
         return self.step_t if self.dev.type == "cuda" else int(self.step_t.item())
 
     # ------------------------------------------------------------------ passes
-    def _project_aggregate(self, L, x, K1):
+    def _project_aggregate(self, L, x, K1, tr=None):
+        """Projection + attention aggregation; ``tr`` (train-row CSR): only at those rows."""
         wcat(L.W, L.a_src, L.a_dst, L.Wc)
         lin_fwd(x, L.Wc, None, K1=K1, out=L.Wh, tail=L.s, nsplit=L.KF, tk=L.K)
         s_src, s_dst = L.s[0], L.s[1]
@@ -321,8 +346,12 @@ class FusedGAT:
             Wh_ext, s_ext = self.halo.exchange_parts([L.Wh, s_src])
         else:
             Wh_ext, s_ext = L.Wh, s_src
-        out, lse = _agg_fwd(Wh_ext, s_ext, s_dst, self.g, L.K, L.Fh)
+        g = self.g
+        if tr is not None:
+            g, s_dst = tr.g, s_dst.index_select(0, tr.rows)
+        out, lse = _agg_fwd(Wh_ext, s_ext, s_dst, g, L.K, L.Fh)
         L.saved = (Wh_ext, s_ext, s_dst, out, lse)
+        L.tr = tr
         return out
 
     def forward(self, train: bool):
@@ -331,8 +360,12 @@ class FusedGAT:
         step = self._dropout_step()
         out1 = self._project_aggregate(L1, self.xb, self.F)
         act_fwd(out1, L1.b, self.h1, p, self.key, step, self.row0)
-        out2 = self._project_aggregate(L2, self.h1, L1.KF)
-        if train:
+        tr = self._tr if train else None
+        out2 = self._project_aggregate(L2, self.h1, L1.KF, tr)
+        if tr is not None:
+            stats = row_ce(out2, L2.b, self.C, tr.y, tr.mask, 1.0 / self.n_train, dZ=tr.dout,
+                           dZb=tr.doutb, db=L2.gb)
+        elif train:
             stats = row_ce(out2, L2.b, self.C, self.y, self.mask, 1.0 / self.n_train, dZ=self.dout2,
                            dZb=self.dout2b, db=L2.gb)
         else:
@@ -345,7 +378,8 @@ class FusedGAT:
     def _layer_backward(self, L, dout, doutb, x, K1):
         Wh_ext, s_ext, s_dst, out, lse = L.saved
         L.saved = None
-        g, K, Fh = self.g, L.K, L.Fh
+        tr, L.tr = L.tr, None
+        g, K, Fh = (self.g if tr is None else tr.g), L.K, L.Fh
         if not self.dev.type == "cuda":
             dWh, ds_src, ds_dst = _agg_bwd_torch(Wh_ext, s_ext, s_dst, dout, g, K, Fh)
             del Wh_ext, s_ext
@@ -366,6 +400,10 @@ class FusedGAT:
                     return [a, b]
                 self.halo.reduce_back_stream(produce, [dWh, ds_src], getattr(self.halo, "grad_wire", torch.float32))
             del rstat, Wh_ext, s_ext
+        if tr is not None:               # the other rows' destination-score gradients are 0
+            full = torch.zeros(self.nloc, K, dtype=ds_dst.dtype, device=ds_dst.device)
+            full.index_copy_(0, tr.rows, ds_dst)
+            ds_dst = full
         pack_grad(dWh, ds_src, ds_dst, L.dy)
         del dWh, ds_src, ds_dst
         lin_bwd_weight(x, L.dy, L.N, K1=K1, dW=L.dWc, db=L.db_scratch)
@@ -374,7 +412,10 @@ class FusedGAT:
     def backward(self):
         L1, L2 = self.layers
         out1 = L1.saved[3]
-        self._layer_backward(L2, self.dout2, self.dout2b, self.h1, L1.KF)
+        if L2.tr is not None:
+            self._layer_backward(L2, L2.tr.dout, L2.tr.doutb, self.h1, L1.KF)
+        else:
+            self._layer_backward(L2, self.dout2, self.dout2b, self.h1, L1.KF)
         lin_bwd_data(L2.dy, L2.Wc, L1.KF, out1=self.dh1)
         act_bwd(self.dh1, out1, L1.b, self.p, self.key, self._dropout_step(), self.row0, self.dout1, self.dout1b,
                 L1.gb)

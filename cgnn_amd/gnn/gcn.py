@@ -108,9 +108,10 @@ class GCNTrainer:
         # Gathered rows padded to whole 128-byte lines (a 208-B row straddles 2-3 lines, a
         # 256-B aligned one exactly 2; measured on the ogbn-products shape: layer-1 SpMM
         # 2.42 -> 2.20 ms, 3 % per epoch).  Default (None): the features always; the
-        # layer-2 rows only on one GPU, since multi-GPU all-gathers them every epoch and
-        # 64 columns instead of 48 would move a third more bytes.
-        pad_c = (self.world == 1) if align_rows is None else bool(align_rows)
+        # layer-2 rows never: since training gathers them only for the train rows, the
+        # packed 96-B rows (less to write, read and exchange) measured faster on one GPU
+        # too (3.564 vs 3.590 ms, profiles/r02_l2gat/ab2_*.log).
+        pad_c = False if align_rows is None else bool(align_rows)
         if align_c is not None:                  # layer-2 pitch chosen separately
             pad_c = bool(align_c)
         pad_x = True if align_rows is None else bool(align_rows)

@@ -28,6 +28,7 @@ epilogue, and the whole forward captured into one hipGraph.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -203,6 +204,20 @@ class _FusedDeepGCN:
         self.rp_T = rp.to(torch.int32).contiguous()
         self.col_T = self.gslot[col[keep]].contiguous()
         self.Gc = torch.zeros(max(self.n_train, 1), ld[-1], **bf)
+        # training epochs: the last aggregation (+ cross-entropy) only at the train rows,
+        # the only logits the loss reads (exact; see gcn.GCNTrainer).  Env
+        # CGNN_L2_ALL_ROWS=1: every row
+        self._tr = None
+        trows = torch.nonzero(train).flatten()
+        if trows.numel() and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
+            rpl = self.rowptr.long()
+            lo, dg = rpl[trows], rpl[trows + 1] - rpl[trows]
+            trp = torch.zeros(trows.numel() + 1, dtype=torch.int64, device=dev)
+            trp[1:] = torch.cumsum(dg, 0)
+            eid = torch.arange(int(trp[-1]), device=dev) + torch.repeat_interleave(lo - trp[:-1], dg)
+            self._tr = (trp.to(torch.int32).contiguous(), self.col[eid].contiguous(),
+                        self.dinv[trows].contiguous(), self.y[trows].contiguous(), self.mask[trows].contiguous(),
+                        torch.arange(trows.numel(), dtype=torch.int32, device=dev))
         self.last_stats = None
 
     def _dropout_step(self):
@@ -218,6 +233,11 @@ class _FusedDeepGCN:
                     rscale=self.dinv, out=self.Hs[l])
             src = self.Hs[l]
         lin_fwd(src, self.W[L - 1], None, K1=self.dims[L - 1], out=self.Zs)
+        if train and self._tr is not None:
+            rp, col, dinv, y, mask, gslot = self._tr
+            stats, _ = ops.spmm_ce(rp, col, self.Zs, self.C, dinv, self.b[L - 1], y, mask,
+                                   1.0 / max(self.n_train, 1), mode=0, G=self.Gc, gslot=gslot)
+            return stats
         stats, _ = ops.spmm_ce(self.rowptr, self.col, self.Zs, self.C, self.dinv, self.b[L - 1], self.y, self.mask,
                                1.0 / max(self.n_train, 1), mode=0 if train else 1, G=self.Gc if train else None,
                                gslot=self.gslot if train else None)

@@ -46,6 +46,26 @@ def test_fused_gat_gradients_match_autograd():
             off += k
 
 
+def test_fused_gat_train_row_layer2_matches_all_rows(monkeypatch):
+    """Training epochs aggregating layer 2 only at the train rows: the same first-step
+    gradients as aggregating every row (dropout on: the same masks), up to the bf16
+    rounding of the stored operands, and the same losses over a few Adam steps."""
+    runs = []
+    for all_rows in ("1", "0"):
+        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
+        g, tr = _setup(dropout=0.3)
+        f = tr.fused
+        assert (f._tr is None) == (all_rows == "1")
+        f.forward(train=True)
+        f.backward()
+        grads = f.grads.clone()
+        g, tr = _setup(dropout=0.3)
+        runs.append((grads, [float(tr.train_step()) for _ in range(3)]))
+    scale = runs[0][0].abs().max().item()
+    assert (runs[1][0] - runs[0][0]).abs().max().item() < 2e-4 * scale
+    np.testing.assert_allclose(runs[1][1], runs[0][1], rtol=1e-4)
+
+
 def test_fused_gat_learns_and_evaluates():
     g, tr = _setup(dropout=0.3)
     first = float(tr.train_step())

@@ -208,3 +208,19 @@ def test_fused_bwd_grad_index_scatters_the_slab_layout():
     assert torch.allclose(flat[F * HD:F * HD + HD], s[:, F])
     assert torch.allclose(flat[F * HD + HD:F * HD + HD + HD * C].view(HD, C), s[:, kf:kf + C])
     assert torch.all(flat[F * HD + HD + HD * C:] == 0)
+
+
+def test_fused_deep_gcn_train_row_last_layer_matches_all_rows(monkeypatch):
+    """The fused L-layer GCN aggregating its last layer only at the train rows in
+    training: same losses and parameters as aggregating every row (CPU branches)."""
+    g = synthetic("cora", seed=3, device="cpu")
+    runs = []
+    for all_rows in ("1", "0"):
+        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
+        tr = DeepGCNTrainer(g, hidden=32, layers=3, dropout=0.5, fused=True)
+        assert (tr._fused._tr is None) == (all_rows == "1")
+        losses = [float(tr.train_step()) for _ in range(4)]
+        runs.append((losses, tr._fused.params.clone(), tr.evaluate()))
+    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=1e-4)
+    torch.testing.assert_close(runs[1][1], runs[0][1], rtol=1e-3, atol=1e-4)
+    assert runs[1][2]["val_acc"] == pytest.approx(runs[0][2]["val_acc"], abs=0.01)
