@@ -233,8 +233,10 @@ class GCNTrainer:
         # block); every layer-1 row and every Z2 row is still computed, and evaluate()
         # aggregates all rows.  Env CGNN_L2_ALL_ROWS=1: all rows in training too.
         self._l2 = None
+        # The switch is global (env), never per rank: the training halo is negotiated
+        # collectively, so a rank without train rows takes part with a placeholder row.
         trows = torch.nonzero(self.mask == 1).flatten()
-        if trows.numel() and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
+        if self.nloc > 0 and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
             self._l2 = self._train_row_csr(trows)
         self.epoch = 0
         self.last_stats = None
@@ -314,15 +316,21 @@ class GCNTrainer:
         the same local / remote edge split (remote columns re-indexed like ``col_rem``)."""
         dev = self.dev
         rp = self.rowptr.long()
+        placeholder = trows.numel() == 0
+        if placeholder:            # no train rows here: one edgeless, non-train row (writes nothing)
+            trows = torch.zeros(1, dtype=torch.int64, device=dev)
         lo, deg = rp[trows], rp[trows + 1] - rp[trows]
+        if placeholder:
+            deg = torch.zeros_like(deg)
         trp = torch.zeros(trows.numel() + 1, dtype=torch.int64, device=dev)
         trp[1:] = torch.cumsum(deg, 0)
         eid = torch.arange(int(trp[-1]), device=dev) + torch.repeat_interleave(lo - trp[:-1], deg)
         l2 = types.SimpleNamespace(
             rp=trp.to(torch.int32).contiguous(), col=self.col[eid].contiguous(),
             dinv=self.dinv[trows].contiguous(), y=self.y[trows].contiguous(),
-            mask=self.mask[trows].contiguous(),
-            gslot=torch.arange(trows.numel(), dtype=torch.int32, device=dev))
+            mask=torch.zeros_like(self.mask[trows]) if placeholder else self.mask[trows].contiguous(),
+            gslot=torch.full((1,), -1, dtype=torch.int32, device=dev) if placeholder
+            else torch.arange(trows.numel(), dtype=torch.int32, device=dev))
         l2.plan = None
         if self.world > 1:
             l2.rp_loc, l2.col_loc, l2.rp_rem, col_rem = self._split_local(self.r0, self.r1, l2.rp, l2.col)

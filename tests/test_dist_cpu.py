@@ -63,11 +63,21 @@ def test_score_jobs_sharded_equals_single_process():
         np.testing.assert_allclose(out[r], single, rtol=1e-12)   # same noise: exact
 
 
-def _gcn_worker(rank, world, port, out, halo=None):
+def _strip_train(g, world):
+    """No train rows in the last rank's block (they become validation rows)."""
+    lo = (g.n + world - 1) // world * (world - 1)
+    m = g.mask[lo:]
+    m[m == 1] = 2
+    return g
+
+
+def _gcn_worker(rank, world, port, out, halo=None, strip=False):
     _init(rank, world, port)
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
     g = synthetic("ogbn-products", seed=0, scale=0.002)
+    if strip:
+        _strip_train(g, world)
     tr = GCNTrainer(g, hidden=64, halo=halo)
     assert tr.halo == (halo if halo is not None else world >= 4)
     if tr._l2 is not None:
@@ -83,20 +93,27 @@ def _gcn_worker(rank, world, port, out, halo=None):
 
 @pytest.mark.parametrize("world,halo,overlap,all_rows,train_halo", [
     (2, False, "0", "0", "0"), (2, True, "0", "0", "0"), (4, None, "0", "0", "0"), (2, False, "1", "0", "1"),
-    (4, None, "1", "0", "1"), (2, True, "1", "1", "1"), (4, None, "1", "1", "1"), (3, True, "1", "0", "1")])
+    (4, None, "1", "0", "1"), (2, True, "1", "1", "1"), (4, None, "1", "1", "1"), (3, True, "1", "0", "1"),
+    (3, None, "1", "0", "strip")])
 def test_gcn_row_partition_matches_single_process(world, halo, overlap, all_rows, train_halo, monkeypatch):
     """Row-partitioned GCN over gloo ranks == one process; layer-2 rows of other
     ranks by all-gather or by the halo all-to-all (the default from 4 ranks); the
     backward's compact-gradient all-gather blocking or overlapped with the local edges
     (CGNN_BWD_OVERLAP); training layer 2 over the train rows only (default) or over
     every row (CGNN_L2_ALL_ROWS=1, against the one-process train-row run); the
-    training epochs' own halo of the train rows' sources (CGNN_TRAIN_HALO)."""
+    training epochs' own halo of the train rows' sources (CGNN_TRAIN_HALO); "strip":
+    the last rank owns no train row (it joins the training halo with a placeholder)."""
+    strip = train_halo == "strip"
+    if strip:
+        train_halo = "1"
     monkeypatch.setenv("CGNN_BWD_OVERLAP", overlap)
     monkeypatch.setenv("CGNN_L2_ALL_ROWS", "0")
     monkeypatch.setenv("CGNN_TRAIN_HALO", train_halo)
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
     g = synthetic("ogbn-products", seed=0, scale=0.002)
+    if strip:
+        _strip_train(g, world)
     tr = GCNTrainer(g, hidden=64, rank=0, world=1)
     assert tr._l2 is not None
     monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
@@ -107,7 +124,7 @@ def test_gcn_row_partition_matches_single_process(world, halo, overlap, all_rows
     ref = tr.evaluate()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_gcn_worker, args=(world, _free_port(), out, halo), nprocs=world, join=True)
+    mp.spawn(_gcn_worker, args=(world, _free_port(), out, halo, strip), nprocs=world, join=True)
     for r in range(world):
         res, params, q1 = out[r]
         # after one step the partitioned run equals the single-process one up to the
