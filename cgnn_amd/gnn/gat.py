@@ -18,6 +18,7 @@ GPU kernels are tested against).
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -422,8 +423,13 @@ class ShardedGATTrainer:
         if _use_fused(fused, self.dev, x.shape[1], heads, head_dim, shard.n_classes):
             # the whole epoch on HIP kernels; one all-reduce of the flat gradient buffer
             from .gat_fused import FusedGAT
+            train_l2 = None
+            if (self.world > 1 and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0"
+                    and os.environ.get("CGNN_TRAIN_HALO", "1") != "0"):
+                train_l2 = self._train_halo(shard, r0, r1, per, emulate, wide, halo_chunk_bytes)
             self.fused = FusedGAT(self.x, self.y, self.mask, shard.n_classes, self.g, heads, head_dim, dropout, lr,
-                                  seed, halo=self.halo, row0=r0, n_train=int(self.n_train), distributed=distributed)
+                                  seed, halo=self.halo, row0=r0, n_train=int(self.n_train), distributed=distributed,
+                                  train_l2=train_l2)
             self.model = self.opt = None
             self.epoch = 0
             return
@@ -434,6 +440,31 @@ class ShardedGATTrainer:
             self.ddp.broadcast_parameters(0)
         self.epoch = 0
 
+    def _train_halo(self, shard, r0, r1, per, emulate, wide, chunk):
+        """Training epochs aggregate layer 2 at the train rows only (gat_fused), so they
+        get a halo of their own: the remote rows those rows' edges read (papers100M
+        shape: ~1 % train rows, so a small fraction of the full halo).  Collective: every
+        rank builds it; a rank without train rows brings one placeholder row (non-train,
+        its self edge only).  Returns (rows, CSR over the halo's row space, halo,
+        placeholder) for ``FusedGAT(train_l2=...)``."""
+        from ..parallel.halo import HaloExchange
+        dev = self.dev
+        trows = torch.nonzero(shard.mask == 1).flatten()
+        placeholder = trows.numel() == 0
+        rp = shard.rowptr.long()
+        if placeholder:
+            trows = torch.zeros(1, dtype=torch.int64, device=dev)
+            trp = torch.tensor([0, 1], dtype=torch.int64, device=dev)
+            tcol = torch.full((1,), r0, dtype=shard.col.dtype, device=dev)
+        else:
+            lo, deg = rp[trows], rp[trows + 1] - rp[trows]
+            trp = torch.zeros(trows.numel() + 1, dtype=torch.int64, device=dev)
+            trp[1:] = torch.cumsum(deg, 0)
+            eid = torch.arange(int(trp[-1]), device=dev) + torch.repeat_interleave(lo - trp[:-1], deg)
+            tcol = shard.col[eid]
+        th = HaloExchange(tcol, r0, r1, per, shard.n, emulate=emulate, max_row_bytes=wide, chunk_bytes=chunk)
+        gT = GraphCSR(trp.to(torch.int32), th.col_ext, trows.numel(), n_cols=th.n_ext)
+        return trows, gT, th, placeholder
     def state_tensors(self):
         return _gat_state_tensors(self)
 

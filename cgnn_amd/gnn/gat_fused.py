@@ -242,7 +242,7 @@ class FusedGAT:
     Parameters are initialised exactly like ``gat.GAT(F, C, heads, head_dim, seed)``."""
 
     def __init__(self, x, y, mask, n_classes, g, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0,
-                 halo=None, row0=0, n_train=None, distributed=False):
+                 halo=None, row0=0, n_train=None, distributed=False, train_l2=None):
         from .gat import GAT
         dev = x.device
         self.dev, self.g, self.halo = dev, g, halo
@@ -309,7 +309,19 @@ class FusedGAT:
         # Evaluation aggregates every row.  Env CGNN_L2_ALL_ROWS=1: every row always.
         self._tr = None
         trows = torch.nonzero(self.mask == 1).flatten()
-        if trows.numel() and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
+        if train_l2 is not None:
+            # built by the sharded trainer: the train rows' CSR over a training halo of
+            # its own (only the remote rows those rows read travel in training epochs);
+            # a rank without train rows brings a non-train placeholder row
+            trows, gT, thalo, placeholder = train_l2
+            nT = trows.numel()
+            self._tr = types.SimpleNamespace(
+                rows=trows, g=gT, halo=thalo, y=self.y[trows].contiguous(),
+                mask=torch.zeros_like(self.mask[trows]) if placeholder else self.mask[trows].contiguous(),
+                dout=torch.zeros(nT, L2.KF, dtype=torch.float32, device=dev),
+                doutb=torch.zeros(nT, L2.KF, **bf))
+            self.dout2 = self.dout2b = None
+        elif trows.numel() and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
             from .gat import GraphCSR
             rp = g.rowptr.long()
             lo, deg = rp[trows], rp[trows + 1] - rp[trows]
@@ -318,7 +330,7 @@ class FusedGAT:
             eid = torch.arange(int(trp[-1]), device=dev) + torch.repeat_interleave(lo - trp[:-1], deg)
             nT = trows.numel()
             self._tr = types.SimpleNamespace(
-                rows=trows, g=GraphCSR(trp.to(g.rowptr.dtype), g.col[eid], nT, g.n_cols),
+                rows=trows, g=GraphCSR(trp.to(g.rowptr.dtype), g.col[eid], nT, g.n_cols), halo=halo,
                 y=self.y[trows].contiguous(), mask=self.mask[trows].contiguous(),
                 dout=torch.zeros(nT, L2.KF, dtype=torch.float32, device=dev),
                 doutb=torch.zeros(nT, L2.KF, **bf))
@@ -342,8 +354,9 @@ class FusedGAT:
         wcat(L.W, L.a_src, L.a_dst, L.Wc)
         lin_fwd(x, L.Wc, None, K1=K1, out=L.Wh, tail=L.s, nsplit=L.KF, tk=L.K)
         s_src, s_dst = L.s[0], L.s[1]
-        if self.halo is not None:
-            Wh_ext, s_ext = self.halo.exchange_parts([L.Wh, s_src])
+        halo = self.halo if tr is None else tr.halo
+        if halo is not None:
+            Wh_ext, s_ext = halo.exchange_parts([L.Wh, s_src])
         else:
             Wh_ext, s_ext = L.Wh, s_src
         g = self.g
@@ -380,25 +393,26 @@ class FusedGAT:
         L.saved = None
         tr, L.tr = L.tr, None
         g, K, Fh = (self.g if tr is None else tr.g), L.K, L.Fh
+        halo = self.halo if tr is None else tr.halo
         if not self.dev.type == "cuda":
             dWh, ds_src, ds_dst = _agg_bwd_torch(Wh_ext, s_ext, s_dst, dout, g, K, Fh)
             del Wh_ext, s_ext
-            if self.halo is not None:
-                dWh, ds_src = self.halo.reduce_back([dWh, ds_src])
+            if halo is not None:
+                dWh, ds_src = halo.reduce_back([dWh, ds_src])
         else:
             rstat, ds_dst = _agg_bwd_rows(Wh_ext, s_ext, s_dst, out, lse, dout, g, K, Fh)
             n = self.nloc
             dWh = torch.empty(n, L.KF, dtype=torch.float32, device=self.dev)
             ds_src = torch.empty(n, K, dtype=torch.float32, device=self.dev)
             _agg_bwd_cols(Wh_ext, s_ext, rstat, doutb, g, K, Fh, 0, n, dWh, ds_src)
-            if self.halo is not None:
+            if halo is not None:
                 # the received rows' gradients are made one exchange round at a time
                 def produce(lo, hi):
                     a = torch.empty(hi - lo, L.KF, dtype=torch.float32, device=self.dev)
                     b = torch.empty(hi - lo, K, dtype=torch.float32, device=self.dev)
                     _agg_bwd_cols(Wh_ext, s_ext, rstat, doutb, g, K, Fh, lo, hi, a, b)
                     return [a, b]
-                self.halo.reduce_back_stream(produce, [dWh, ds_src], getattr(self.halo, "grad_wire", torch.float32))
+                halo.reduce_back_stream(produce, [dWh, ds_src], getattr(self.halo, "grad_wire", torch.float32))
             del rstat, Wh_ext, s_ext
         if tr is not None:               # the other rows' destination-score gradients are 0
             full = torch.zeros(self.nloc, K, dtype=ds_dst.dtype, device=ds_dst.device)

@@ -254,16 +254,22 @@ def _gat_params(tr):
     return torch.cat([p.detach().flatten() for p in tr.model.parameters()]).numpy()
 
 
-def _gat_shard_worker(rank, world, port, out, fused=False, heads=2, dropout=0.0, chunk=4 << 30):
+def _gat_shard_worker(rank, world, port, out, fused=False, heads=2, dropout=0.0, chunk=4 << 30, strip=False):
     _init(rank, world, port)
     from cgnn_amd.gnn.data import synthetic_shard
     from cgnn_amd.gnn.gat import ShardedGATTrainer
     # rank-local generation: this rank never builds the rest of the graph
     shard = synthetic_shard("ogbn-products", rank, world, seed=1, scale=0.0005)
+    if strip and rank == world - 1:          # this rank owns no train row
+        shard.mask[shard.mask == 1] = 2
     tr = ShardedGATTrainer(shard, heads=heads, head_dim=8, dropout=dropout, lr=0.01, seed=rank, fused=fused,
                            halo_chunk_bytes=chunk)
     if chunk < (1 << 20):
         assert tr.halo.rounds > 1
+    if tr.fused is not None:
+        # training epochs exchange only the train rows' sources (their own halo)
+        th = tr.fused._tr.halo
+        assert th is not tr.halo and th.n_recv <= tr.halo.n_recv
     losses = []
     grads1 = None
     for _ in range(3):
@@ -304,14 +310,19 @@ def test_sharded_gat_matches_single_process(world, chunk):
     np.testing.assert_array_equal(out[0][2], out[1][2])
 
 
-@pytest.mark.parametrize("world,chunk", [(2, 4 << 30), (4, 4 << 30), (2, 16 << 10), (4, 16 << 10)])
-def test_sharded_fused_gat_matches_single_process(world, chunk):
+@pytest.mark.parametrize("world,chunk,strip", [(2, 4 << 30, False), (4, 4 << 30, False), (2, 16 << 10, False),
+                                               (4, 16 << 10, False), (3, 4 << 30, True)])
+def test_sharded_fused_gat_matches_single_process(world, chunk, strip):
     """The fused GAT epoch (gat_fused: every dense op a HIP kernel on a GPU; its fp32
     reference branches here) sharded over gloo ranks equals the one-process fused
-    model -- with dropout on, since the masks are keyed by the global row."""
+    model -- with dropout on, since the masks are keyed by the global row.  Training
+    layer 2 runs at the train rows over a training halo; ``strip``: the last rank
+    owns no train row (placeholder row in the collective plan)."""
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gat import ShardedGATTrainer
     g = synthetic("ogbn-products", seed=1, scale=0.0005)
+    if strip:
+        _strip_train(g, world)
     ref = ShardedGATTrainer(g, heads=4, head_dim=8, dropout=0.3, lr=0.01, seed=0, fused=True)
     assert ref.fused is not None
     ref_losses = [float(ref.train_step())]
@@ -322,7 +333,7 @@ def test_sharded_fused_gat_matches_single_process(world, chunk):
     mgr = mp.Manager()
     out = mgr.dict()
     # chunk 16 KB: the halo exchanges run in several rounds (bounded staging memory)
-    mp.spawn(_gat_shard_worker, args=(world, _free_port(), out, True, 4, 0.3, chunk), nprocs=world, join=True)
+    mp.spawn(_gat_shard_worker, args=(world, _free_port(), out, True, 4, 0.3, chunk, strip), nprocs=world, join=True)
     for r in range(world):
         losses, res, params, hs, grads1 = out[r]
         # first-step gradients (rank-summed): equal up to the summation order of the
