@@ -478,8 +478,13 @@ class ShardedGATTrainer:
         l1 = self.fused.layers[0] if self.fused is not None else self.model.l1
         w = 2 * l1.K * l1.Fh + 4 * l1.K
         rb, sb = self.halo.bytes_per_exchange(w)
-        return {"recv_rows": self.halo.n_recv, "send_rows": self.halo.n_send, "local_rows": self.halo.nloc,
-                "layer1_recv_bytes": rb, "layer1_send_bytes": sb}
+        out = {"recv_rows": self.halo.n_recv, "send_rows": self.halo.n_send, "local_rows": self.halo.nloc,
+               "layer1_recv_bytes": rb, "layer1_send_bytes": sb}
+        tr = self.fused._tr if self.fused is not None else None
+        if tr is not None and tr.halo is not None and tr.halo is not self.halo:
+            out["layer2_train_recv_rows"] = tr.halo.n_recv    # the training epochs' layer-2 halo
+            out["layer2_train_send_rows"] = tr.halo.n_send
+        return out
 
     def train_step(self):
         if self.fused is not None:
