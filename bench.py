@@ -11,8 +11,9 @@ aggregation at the train rows, the only rows whose logits reach the loss --
 exact, see gnn/gcn.py; CGNN_L2_ALL_ROWS=1 aggregates every row).  Data: synthetic graph of the ogbn-products shape (no network
 for the real dataset), random-init weights.  Multi-GPU: 1-D row partition of
 the graph over ranks (strong scaling: the whole job trains the same graph),
-RCCL all-gathers of the layer-2 activations / gradients and an all-reduce of
-the weight gradients.  W untimed warm-up epochs, then exactly K timed epochs
+an RCCL all-to-all of the layer-2 rows the rank's train rows read (a training
+halo, negotiated once), an all-gather of the compact train-row gradient and an
+all-reduce of the weight gradients.  W untimed warm-up epochs, then exactly K timed epochs
 bracketed by barrier + device synchronize; the MAX time over ranks is reported.
 """
 import argparse

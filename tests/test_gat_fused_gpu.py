@@ -193,3 +193,22 @@ def test_sharded_fused_gat_gpu_matches_one_rank(world, chunk):
         np.testing.assert_allclose(losses, ref_losses, rtol=2e-3)
         assert abs(res["val_acc"] - ref_res["val_acc"]) < 5e-3
     np.testing.assert_array_equal(out[0][2], out[1][2])              # replicas identical
+
+
+def test_fused_gat_train_row_layer2_gpu_matches_all_rows(monkeypatch):
+    """HIP path: layer 2 aggregated at the train rows only in training (default) gives
+    the first-step gradients and the losses of the all-row aggregation."""
+    g = synthetic("ogbn-products", seed=5, device="cuda:0", scale=0.003)
+    runs = []
+    for all_rows in ("1", "0"):
+        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
+        tr = GATTrainer(g, heads=4, head_dim=32, dropout=0.5, lr=0.01, seed=0)
+        assert tr.fused is not None and (tr.fused._tr is None) == (all_rows == "1")
+        losses = [float(tr.train_step())]
+        grads = tr.fused.grads.clone().cpu()
+        losses += [float(tr.train_step()) for _ in range(2)]
+        runs.append((losses, grads, tr.evaluate()))
+    ga, gb = runs[0][1], runs[1][1]
+    assert (gb - ga).abs().max() < 2e-3 * ga.abs().max(), ((gb - ga).abs().max(), ga.abs().max())
+    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=1e-3)
+    assert abs(runs[1][2]["val_acc"] - runs[0][2]["val_acc"]) < 5e-3

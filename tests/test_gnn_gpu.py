@@ -542,3 +542,24 @@ def test_slab_sum_matches_torch(S, W, G, mapped):
     out2 = out.clone()
     ops.slab_sum(P, out2, perm if mapped else None, groups=G)
     assert torch.equal(out, out2)          # deterministic
+
+
+def test_gcn_train_row_layer2_gpu_matches_all_rows(monkeypatch):
+    """One GPU, HIP path: training epochs that aggregate layer 2 only at the train rows
+    (default) give the losses, parameters and evaluation of the all-row aggregation
+    (CGNN_L2_ALL_ROWS=1) up to summation order."""
+    g = synthetic("ogbn-products", seed=4, device="cuda:0", scale=0.004)
+    runs = []
+    for all_rows in ("1", "0"):
+        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
+        tr = GCNTrainer(g, hidden=64, rank=0, world=1)
+        assert (tr._l2 is None) == (all_rows == "1")
+        losses = []
+        for _ in range(4):
+            tr.train_step()
+            losses.append(tr.train_loss())
+        runs.append((losses, tr.params.clone().cpu(), tr.evaluate()))
+    np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=1e-4)
+    d = (runs[1][1] - runs[0][1]).abs()
+    assert d.max().item() < 1e-3 and (d > 1e-4).float().mean().item() < 0.01, (d.max(), (d > 1e-4).float().mean())
+    assert runs[1][2]["val_acc"] == pytest.approx(runs[0][2]["val_acc"], abs=2e-3)
