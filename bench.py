@@ -6,8 +6,9 @@ an ogbn-products-shaped graph, 1/2/4/8 MI355X.
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One step = one full-graph training epoch (forward + backward + Adam) over all
-2,449,029 nodes (layer 1 and both dense layers at every row; the layer-2
-aggregation at the train rows, the only rows whose logits reach the loss --
+2,449,029 nodes (both dense layers at every row; the layer-2 aggregation at the
+train rows, the only rows whose logits reach the loss, and the layer-1
+aggregation at the rows with a train neighbour, the only ones those read --
 exact, see gnn/gcn.py; CGNN_L2_ALL_ROWS=1 aggregates every row).  Data: synthetic graph of the ogbn-products shape (no network
 for the real dataset), random-init weights.  Multi-GPU: 1-D row partition of
 the graph over ranks (strong scaling: the whole job trains the same graph),
@@ -173,7 +174,8 @@ def main():
                        "optimizer": "adam", "lr": a.lr, "id_order": a.id_order,
                        "reordered": a.reorder != "none",
                        # training epochs aggregate layer 2 at the rows the loss reads
-                       "train_layer2_rows": "all" if tr._l2 is None else "train"},
+                       "train_layer2_rows": "all" if tr._l2 is None else "train",
+                       "train_layer1_rows": "all" if tr._l1 is None else "train-neighbours"},
             "val_acc": round(res["val_acc"], 4),
             "test_acc": round(res["test_acc"], 4),
             "train_loss": round(train_loss, 5),
