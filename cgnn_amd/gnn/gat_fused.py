@@ -335,8 +335,36 @@ class FusedGAT:
                 dout=torch.zeros(nT, L2.KF, dtype=torch.float32, device=dev),
                 doutb=torch.zeros(nT, L2.KF, **bf))
             self.dout2 = self.dout2b = None          # all-row layer-2 gradients: not needed
+        # ... and then layer 1 is needed only at the rows those aggregations read: the
+        # rows with a train neighbour (any rank's; A is symmetric; the neighbours' train
+        # flags come over the halo once).  Training epochs aggregate layer 1 over a CSR
+        # whose other rows are empty (they produce out = 0, finite, read by no train row,
+        # with zero gradient); evaluation aggregates every row.  The papers100M shape has
+        # ~1 % train rows, so most layer-1 edges drop out.  Not in a dry run (emulated
+        # halo: the received rows' flags are not real).  Env CGNN_L1_TRAIN_NBRS=0: off.
+        self._g1 = None
+        if (self._tr is not None and os.environ.get("CGNN_L1_TRAIN_NBRS", "1") != "0"
+                and not (halo is not None and getattr(halo, "emulate", False))):
+            self._g1 = self._train_neighbour_graph(g, halo)
         self.epoch = 0
         self.last_stats = None
+
+    def _train_neighbour_graph(self, g, halo):
+        from .gat import GraphCSR
+        flag = (self.mask == 1).to(torch.float32)[:, None].contiguous()
+        if halo is not None:
+            flag = halo.exchange_parts([flag])[0]          # [own | received] train flags
+        tflag = flag[:, 0] > 0.5
+        rp, col = g.rowptr.long(), g.col.long()
+        deg = rp[1:] - rp[:-1]
+        rows = torch.repeat_interleave(torch.arange(g.n, device=col.device), deg)
+        hit = torch.zeros(g.n, dtype=torch.bool, device=col.device)
+        hit[rows[tflag[col]]] = True
+        keep = hit[rows]
+        del rows
+        nrp = torch.zeros(g.n + 1, dtype=torch.int64, device=col.device)
+        nrp[1:] = torch.cumsum(torch.where(hit, deg, torch.zeros_like(deg)), 0)
+        return GraphCSR(nrp.to(g.rowptr.dtype), g.col[keep], g.n, g.n_cols)
 
     @staticmethod
     def supported(F, heads, head_dim, n_classes):
@@ -349,8 +377,9 @@ class FusedGAT:
         return self.step_t if self.dev.type == "cuda" else int(self.step_t.item())
 
     # ------------------------------------------------------------------ passes
-    def _project_aggregate(self, L, x, K1, tr=None):
-        """Projection + attention aggregation; ``tr`` (train-row CSR): only at those rows."""
+    def _project_aggregate(self, L, x, K1, tr=None, g1=None):
+        """Projection + attention aggregation; ``tr`` (train-row CSR): only at those rows;
+        ``g1``: the aggregation graph instead of the full one (same rows)."""
         wcat(L.W, L.a_src, L.a_dst, L.Wc)
         lin_fwd(x, L.Wc, None, K1=K1, out=L.Wh, tail=L.s, nsplit=L.KF, tk=L.K)
         s_src, s_dst = L.s[0], L.s[1]
@@ -359,19 +388,19 @@ class FusedGAT:
             Wh_ext, s_ext = halo.exchange_parts([L.Wh, s_src])
         else:
             Wh_ext, s_ext = L.Wh, s_src
-        g = self.g
+        g = self.g if g1 is None else g1
         if tr is not None:
             g, s_dst = tr.g, s_dst.index_select(0, tr.rows)
         out, lse = _agg_fwd(Wh_ext, s_ext, s_dst, g, L.K, L.Fh)
         L.saved = (Wh_ext, s_ext, s_dst, out, lse)
-        L.tr = tr
+        L.tr, L.g_used = tr, g
         return out
 
     def forward(self, train: bool):
         L1, L2 = self.layers
         p = self.p if train else 0.0
         step = self._dropout_step()
-        out1 = self._project_aggregate(L1, self.xb, self.F)
+        out1 = self._project_aggregate(L1, self.xb, self.F, g1=self._g1 if train else None)
         act_fwd(out1, L1.b, self.h1, p, self.key, step, self.row0)
         tr = self._tr if train else None
         out2 = self._project_aggregate(L2, self.h1, L1.KF, tr)
@@ -392,7 +421,7 @@ class FusedGAT:
         Wh_ext, s_ext, s_dst, out, lse = L.saved
         L.saved = None
         tr, L.tr = L.tr, None
-        g, K, Fh = (self.g if tr is None else tr.g), L.K, L.Fh
+        g, K, Fh = L.g_used, L.K, L.Fh
         halo = self.halo if tr is None else tr.halo
         if not self.dev.type == "cuda":
             dWh, ds_src, ds_dst = _agg_bwd_torch(Wh_ext, s_ext, s_dst, dout, g, K, Fh)
