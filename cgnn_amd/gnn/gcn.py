@@ -85,6 +85,17 @@ def _tsgemm(A, B, chunk=CHUNK):
     return part.sum(0)
 
 
+class _Done:
+    """Work handle of a collective that already completed."""
+
+    @staticmethod
+    def wait():
+        return True
+
+
+_DONE = _Done()
+
+
 class GCNTrainer:
     def __init__(self, g: GraphData, hidden: int = 256, dropout: float = 0.5, lr: float = 0.01,
                  weight_decay: float = 0.0, seed: int = 0, rank: Optional[int] = None,
@@ -248,6 +259,7 @@ class GCNTrainer:
         if (self._l2 is not None and self._win is None
                 and os.environ.get("CGNN_L1_TRAIN_NBRS", "1") != "0"):
             self._l1 = self._train_neighbour_csr(g)
+        self._async = None                 # collectives overlapped? (decided at first use)
         self.epoch = 0
         self.last_stats = None
         # fused MFMA dense kernels (gnn_dense.hip); shapes they do not cover fall back to
@@ -371,6 +383,17 @@ class GCNTrainer:
             l2.part = torch.zeros(trows.numel(), self.ldc, dtype=torch.float32, device=dev)
         return l2
 
+    def _collective(self, fn, *args):
+        """``fn(*args)`` asynchronously (returns its work handle) on RCCL and on CPU
+        tensors; blocking for device tensors over gloo (the one-GPU rehearsal), whose
+        async CUDA path showed intermittent hangs with several ranks on one device."""
+        if self._async is None:
+            self._async = (self.dev.type == "cpu" or torch.distributed.get_backend() != "gloo")
+        if self._async:
+            return fn(*args, async_op=True)
+        fn(*args)
+        return _DONE
+
     def _exchange_z2(self, plan=None):
         """Start the transfer of the other ranks' layer-2 rows: the halo of ``plan``
         or, without one, the full halo (``self.halo``) or an all-gather of every row.
@@ -378,11 +401,11 @@ class GCNTrainer:
         if plan is None and self.halo:
             plan = self._hplan
         if plan is None:
-            return torch.distributed.all_gather_into_tensor(self.Z2, self.Z2loc, async_op=True), self.Z2
+            return self._collective(torch.distributed.all_gather_into_tensor, self.Z2, self.Z2loc), self.Z2
         S, R = sum(plan.send_splits), sum(plan.recv_splits)
         torch.index_select(self.Z2loc, 0, plan.send_idx, out=plan.Zsend[:S])
-        work = torch.distributed.all_to_all_single(plan.Zrecv[:R], plan.Zsend[:S], plan.recv_splits,
-                                                   plan.send_splits, async_op=True)
+        work = self._collective(torch.distributed.all_to_all_single, plan.Zrecv[:R], plan.Zsend[:S],
+                                plan.recv_splits, plan.send_splits)
         return work, plan.Zrecv
 
     def _train_columns(self, g: GraphData, per: int):
@@ -492,7 +515,7 @@ class GCNTrainer:
     def backward(self, stats):
         n, F, C = self.nloc, self.F, self.C
         if self.world > 1 and self._bwd_overlap:
-            work = torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc, async_op=True)
+            work = self._collective(torch.distributed.all_gather_into_tensor, self.Gc, self.Gc_loc)
             ops.spmm(self.rpT_loc, self.colT_loc, self.Gc_loc, C, out=self.part, out_dtype=torch.float32)
             work.wait()
             ops.spmm(self.rpT_rem, self.colT_rem, self.Gc, C, rscale=self.dinv, out=self.dY2, init=self.part)
