@@ -117,8 +117,12 @@ def main():
             torch.cuda.synchronize()
 
     t_setup = time.perf_counter()
-    g = synthetic(a.dataset, seed=a.seed, device=dev, scale=a.scale, feat_noise=a.feat_noise,
-                  label_noise=a.label_noise, id_order=a.id_order)
+    # a rehearsal's ranks share one device: build the CSR with the host C++ path there
+    # (N concurrent device radix sorts of the edge keys stalled the setup)
+    g = synthetic(a.dataset, seed=a.seed, device="cpu" if shared else dev, scale=a.scale,
+                  feat_noise=a.feat_noise, label_noise=a.label_noise, id_order=a.id_order)
+    if shared:
+        g = g.to(dev)
     sync()
     gen_s = time.perf_counter() - t_setup
     tr = GCNTrainer(g, hidden=a.hidden, dropout=a.dropout, lr=a.lr, seed=a.seed,
