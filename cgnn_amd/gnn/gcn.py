@@ -385,8 +385,8 @@ class GCNTrainer:
 
     def _collective(self, fn, *args):
         """``fn(*args)`` asynchronously (returns its work handle) on RCCL and on CPU
-        tensors; blocking for device tensors over gloo (the one-GPU rehearsal), whose
-        async CUDA path showed intermittent hangs with several ranks on one device."""
+        tensors; blocking for device tensors over gloo (only the one-GPU rehearsal,
+        where gloo stages them through the host anyway and nothing can overlap)."""
         if self._async is None:
             self._async = (self.dev.type == "cpu" or torch.distributed.get_backend() != "gloo")
         if self._async:
