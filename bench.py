@@ -111,6 +111,18 @@ def main():
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
+    backend = {"backend": "none (one process)", "world_size": 1}
+    if world > 1:
+        # content-checked collectives before anything is timed: a mis-launched job (wrong
+        # world size, transport that drops or reorders) exits non-zero instead of timing
+        from cgnn_amd.parallel.collectives import selftest
+        try:
+            backend = selftest(dev)
+        except RuntimeError as exc:
+            sys.stderr.write("bench.py: %s\n" % exc)
+            sys.exit(3)
+        if backend["world_size"] != world:
+            sys.exit("bench.py: process group has %d ranks, expected %d" % (backend["world_size"], world))
 
     def sync():
         if cuda:
@@ -172,6 +184,9 @@ def main():
                     "%d classes; planted communities; %s node ids), random-init weights"
                     % (a.dataset, n, m, F, C, a.id_order),
             "shared_gpu_rehearsal": bool(shared),
+            "backend": backend["backend"],
+            "world_size": backend["world_size"],
+            "collective_selftest_ms": backend.get("ms"),
             "config": {"model": "GCN-2layer-hidden%d" % a.hidden, "global_batch": n_nodes,
                        "seq_len": None, "parallelism": "graph-rowpart%d" % world,
                        "dataset": a.dataset, "nnz_with_self_loops": nnz, "dropout": a.dropout,

@@ -29,8 +29,10 @@ int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, 
                               const int*, int, int, hipStream_t);
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t, int);
+int cgnn_gen_bwd_variant(int, int, int, int);
+size_t cgnn_gen_bwd_generic_lds(int, int);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
-                        const float*, int, int, int, int, int, int, int, float*, hipStream_t);
+                        const float*, int, int, int, int, int, int, int, float*, hipStream_t, float*);
 int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
                      int, float, float, float, float, int, hipStream_t);
 int cgnn_launch_init(float*, float*, float*, const int*, int, int, const uint32_t*, float, int,
@@ -70,17 +72,15 @@ int gnn_launch_relu_dropout_bwd(void*, const void*, long, float, hipStream_t);
 int gnn_launch_dense_fwd(const void*, const float*, const float*, const float*, const float*, void*, void*,
                          int, int, int, int, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t,
                          const int*, hipStream_t);
-int gnn_launch_gat_fwd(const int*, const int*, const void*, const float*, const float*, float*, float*, int,
-                       int, int, int, hipStream_t);
-int gnn_launch_gat_bwd_row(const int*, const int*, const void*, const float*, const float*, const float*,
-                           const float*, const float*, float*, float*, int, int, int, int, hipStream_t);
-int gnn_launch_gat_bwd_col(const int*, const int*, const void*, const float*, const float*, const void*, float*,
-                           float*, int, int, int, int, hipStream_t);
-int gnn_launch_gat_act_fwd(const float*, const float*, void*, int, long, int, float, uint32_t, uint32_t, uint32_t,
-                           const int*, uint32_t, hipStream_t);
-int gnn_gat_act_bwd_blocks();
-int gnn_launch_gat_act_bwd(const void*, int, const float*, const float*, float*, void*, float*, float*, long, int,
-                           float, uint32_t, uint32_t, uint32_t, const int*, uint32_t, hipStream_t);
+int gnn_launch_gat_fwd(const int*, const int*, const void*, const float*, const float*, const int*, float*, float*,
+                       void*, int, int, int, int, const float*, void*, int, float, uint32_t, uint32_t, uint32_t,
+                       const int*, uint32_t, hipStream_t);
+int gnn_gat_row_blocks();
+int gnn_launch_gat_rows(int, const void*, int, const float*, const void*, const float*, const float*, const int*,
+                        float*, float*, void*, int, void*, const float*, float*, float*, float, uint32_t, uint32_t,
+                        uint32_t, const int*, uint32_t, int, int, int, int, hipStream_t);
+int gnn_launch_gat_col(const int*, const int*, const void*, const float*, const float*, const void*, float*, float*,
+                       void*, int, int, int, int, int, hipStream_t);
 int gnn_gat_row_ce_waves();
 int gnn_launch_gat_row_ce(const float*, int, const float*, int, const int*, const uint8_t*, float, float*, void*,
                           float*, float*, float*, float*, long, hipStream_t);
@@ -100,7 +100,7 @@ int gnn_launch_dense_bwd(const void*, const float*, const void*, void*, int, int
                          hipStream_t);
 int gnn_launch_lin_fwd(const void*, int, int, const void*, int, int, const float*, int, const float*, void*, int,
                        int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, const int*, const float*,
-                       const int*, void*, float*, int, int, hipStream_t);
+                       const int*, void*, float*, int, int, hipStream_t, int);
 int gnn_launch_lin_bwd_data(const void*, int, const void*, int, float, int, const float*, int, int, void*, int,
                             void*, int, const float*, int, int, void*, hipStream_t);
 long gnn_lin_fwd_image_bytes(int, int, int);
@@ -120,7 +120,7 @@ static void chk(int rc, const char* what) {
 class PyEngine {
  public:
   PyEngine(std::vector<int> icfg, std::vector<float> fcfg, std::vector<uint64_t> ptrs, uint64_t stream) {
-    if (icfg.size() < 17 || fcfg.size() < 5 || ptrs.size() < 20) throw std::invalid_argument("engine config size");
+    if (icfg.size() < 17 || fcfg.size() < 5 || ptrs.size() < 21) throw std::invalid_argument("engine config size");
     std::vector<const void*> p(ptrs.size());
     for (size_t k = 0; k < ptrs.size(); ++k) p[k] = reinterpret_cast<const void*>(ptrs[k]);
     h_ = cgnn_engine_create(icfg.data(), fcfg.data(), p.data(), S(stream));
@@ -154,6 +154,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gen_supported_h", &cgnn_gen_supported_h);
   m.def("gen_bwd_blocks", &cgnn_gen_bwd_blocks);
   m.def("gen_bwd_lds", &cgnn_gen_bwd_lds);
+  m.def("gen_bwd_variant", &cgnn_gen_bwd_variant);
+  m.def("gen_bwd_generic_lds", &cgnn_gen_bwd_generic_lds);
   m.def("read_stamps", []() {
     unsigned long long v[16] = {0};
     const int rc = cgnn_read_stamps(v);
@@ -190,11 +192,13 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("N"), py::arg("D"), py::arg("H"), py::arg("R"), py::arg("st"), py::arg("row0") = 0);
   m.def("gen_bwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t xhat, uint64_t noise, int NS,
                       uint64_t gradp, int nch, int R, int N, int D, int Dt, int H, int max_in, uint64_t gpart,
-                      uint64_t st) {
+                      uint64_t st, uint64_t dxs) {
     chk(cgnn_launch_gen_bwd(Pt<const int>(prog), ps, Pt<const float>(params), P, Pt<const float>(xhat),
                             Pt<const float>(noise), NS, Pt<const float>(gradp), nch, R, N, D, Dt, H, max_in,
-                            Pt<float>(gpart), S(st)), "gen_bwd");
-  });
+                            Pt<float>(gpart), S(st), Pt<float>(dxs)), "gen_bwd");
+  }, py::arg("prog"), py::arg("ps"), py::arg("params"), py::arg("P"), py::arg("xhat"), py::arg("noise"),
+     py::arg("NS"), py::arg("gradp"), py::arg("nch"), py::arg("R"), py::arg("N"), py::arg("D"), py::arg("Dt"),
+     py::arg("H"), py::arg("max_in"), py::arg("gpart"), py::arg("st"), py::arg("dxs") = 0);
   m.def("adam", [](uint64_t params, uint64_t mm, uint64_t vv, uint64_t gpart, int G, uint64_t prog, int ps, int P,
                    uint64_t step, int off, float lr, float b1, float b2, float eps, int R, uint64_t st) {
     chk(cgnn_launch_adam(Pt<float>(params), Pt<float>(mm), Pt<float>(vv), Pt<const float>(gpart), G,
@@ -298,43 +302,42 @@ PYBIND11_MODULE(_hip, m) {
                                 HD, C, ldc, p, S(st));
   });
   m.def("gnn_gat_fwd", [](uint64_t rp, uint64_t col, uint64_t wh, uint64_t ss, uint64_t sd, uint64_t out,
-                          uint64_t lse, int n, int K, int Fh, uint64_t st, int wbf) {
+                          uint64_t lse, int n, int K, int Fh, uint64_t st, int wbf, uint64_t dst_rows, uint64_t q,
+                          uint64_t bias, uint64_t H, int ldh, float p, uint32_t k0, uint32_t k1, uint32_t step,
+                          uint64_t stepp, uint32_t row0) {
     chk(gnn_launch_gat_fwd(Pt<const int>(rp), Pt<const int>(col), Pt<const void>(wh), Pt<const float>(ss),
-                           Pt<const float>(sd), Pt<float>(out), Pt<float>(lse), n, K, Fh, wbf, S(st)),
+                           Pt<const float>(sd), Pt<const int>(dst_rows), Pt<float>(out), Pt<float>(lse), Pt<void>(q),
+                           n, K, Fh, wbf, Pt<const float>(bias), Pt<void>(H), ldh, p, k0, k1, step,
+                           Pt<const int>(stepp), row0, S(st)),
         "gnn_gat_fwd");
   }, py::arg("rp"), py::arg("col"), py::arg("wh"), py::arg("ss"), py::arg("sd"), py::arg("out"), py::arg("lse"),
-     py::arg("n"), py::arg("K"), py::arg("Fh"), py::arg("st"), py::arg("wbf") = 0);
-  m.def("gnn_gat_bwd_row", [](uint64_t rp, uint64_t col, uint64_t wh, uint64_t ss, uint64_t sd, uint64_t out,
-                              uint64_t lse, uint64_t dout, uint64_t rstat, uint64_t dsd, int n, int K, int Fh,
-                              uint64_t st, int wbf) {
-    chk(gnn_launch_gat_bwd_row(Pt<const int>(rp), Pt<const int>(col), Pt<const void>(wh), Pt<const float>(ss),
-                               Pt<const float>(sd), Pt<const float>(out), Pt<const float>(lse),
-                               Pt<const float>(dout), Pt<float>(rstat), Pt<float>(dsd), n, K, Fh, wbf, S(st)),
-        "gnn_gat_bwd_row");
-  }, py::arg("rp"), py::arg("col"), py::arg("wh"), py::arg("ss"), py::arg("sd"), py::arg("out"), py::arg("lse"),
-     py::arg("dout"), py::arg("rstat"), py::arg("dsd"), py::arg("n"), py::arg("K"), py::arg("Fh"), py::arg("st"),
-     py::arg("wbf") = 0);
-  m.def("gnn_gat_bwd_col", [](uint64_t rpt, uint64_t colt, uint64_t wh, uint64_t ss, uint64_t rstat, uint64_t dout,
-                              uint64_t dwh, uint64_t dss, int n, int K, int Fh, uint64_t st, int wbf) {
-    chk(gnn_launch_gat_bwd_col(Pt<const int>(rpt), Pt<const int>(colt), Pt<const void>(wh), Pt<const float>(ss),
-                               Pt<const float>(rstat), Pt<const void>(dout), Pt<float>(dwh), Pt<float>(dss), n, K,
-                               Fh, wbf, S(st)), "gnn_gat_bwd_col");
+     py::arg("n"), py::arg("K"), py::arg("Fh"), py::arg("st"), py::arg("wbf") = 0, py::arg("dst_rows") = 0,
+     py::arg("q") = 0, py::arg("bias") = 0, py::arg("H") = 0, py::arg("ldh") = 0, py::arg("p") = 0.f,
+     py::arg("k0") = 0, py::arg("k1") = 0, py::arg("step") = 0, py::arg("stepp") = 0, py::arg("row0") = 0);
+  m.def("gnn_gat_row_blocks", &gnn_gat_row_blocks);
+  m.def("gnn_gat_rows", [](int act, uint64_t dout, int ldh, uint64_t out, uint64_t q, uint64_t lse, uint64_t sd,
+                           uint64_t dst_rows, uint64_t rstat, uint64_t dsd, uint64_t dy, int ldy, uint64_t dout_w,
+                           uint64_t bias, uint64_t bpart, uint64_t db, float p, uint32_t k0, uint32_t k1,
+                           uint32_t step, uint64_t stepp, uint32_t row0, int n, int K, int Fh, int wbf, uint64_t st) {
+    chk(gnn_launch_gat_rows(act, Pt<const void>(dout), ldh, Pt<const float>(out), Pt<const void>(q),
+                            Pt<const float>(lse), Pt<const float>(sd), Pt<const int>(dst_rows), Pt<float>(rstat),
+                            Pt<float>(dsd), Pt<void>(dy), ldy, Pt<void>(dout_w), Pt<const float>(bias),
+                            Pt<float>(bpart), Pt<float>(db), p, k0, k1, step, Pt<const int>(stepp), row0, n, K, Fh,
+                            wbf, S(st)), "gnn_gat_rows");
+  }, py::arg("act"), py::arg("dout"), py::arg("ldh"), py::arg("out"), py::arg("q"), py::arg("lse"), py::arg("sd"),
+     py::arg("dst_rows"), py::arg("rstat"), py::arg("dsd"), py::arg("dy"), py::arg("ldy"), py::arg("dout_w"),
+     py::arg("bias"), py::arg("bpart"), py::arg("db"), py::arg("p"), py::arg("k0"), py::arg("k1"), py::arg("step"),
+     py::arg("stepp"), py::arg("row0"), py::arg("n"), py::arg("K"), py::arg("Fh"), py::arg("wbf"), py::arg("st"));
+  m.def("gnn_gat_col", [](uint64_t rpt, uint64_t colt, uint64_t wh, uint64_t ss, uint64_t rstat, uint64_t dout,
+                          uint64_t dwh, uint64_t dss, uint64_t dy, int ldy, int n, int K, int Fh, uint64_t st,
+                          int wbf) {
+    chk(gnn_launch_gat_col(Pt<const int>(rpt), Pt<const int>(colt), Pt<const void>(wh), Pt<const float>(ss),
+                           Pt<const float>(rstat), Pt<const void>(dout), Pt<float>(dwh), Pt<float>(dss), Pt<void>(dy),
+                           ldy, n, K, Fh, wbf, S(st)), "gnn_gat_col");
   }, py::arg("rpt"), py::arg("colt"), py::arg("wh"), py::arg("ss"), py::arg("rstat"), py::arg("dout"),
-     py::arg("dwh"), py::arg("dss"), py::arg("n"), py::arg("K"), py::arg("Fh"), py::arg("st"), py::arg("wbf") = 0);
+     py::arg("dwh"), py::arg("dss"), py::arg("dy"), py::arg("ldy"), py::arg("n"), py::arg("K"), py::arg("Fh"),
+     py::arg("st"), py::arg("wbf") = 1);
   // dense-side kernels of the fused GAT epoch (gnn_gat.hip)
-  m.def("gnn_gat_act_fwd", [](uint64_t out, uint64_t b, uint64_t h, int ldh, long n, int F, float p, uint32_t k0,
-                              uint32_t k1, uint32_t step, uint64_t stepp, uint32_t row0, uint64_t st) {
-    chk(gnn_launch_gat_act_fwd(Pt<const float>(out), Pt<const float>(b), Pt<void>(h), ldh, n, F, p, k0, k1, step,
-                               Pt<const int>(stepp), row0, S(st)), "gnn_gat_act_fwd");
-  });
-  m.def("gnn_gat_act_bwd_blocks", &gnn_gat_act_bwd_blocks);
-  m.def("gnn_gat_act_bwd", [](uint64_t dh, int ldh, uint64_t out, uint64_t b, uint64_t dout, uint64_t doutb,
-                              uint64_t bpart, uint64_t db, long n, int F, float p, uint32_t k0, uint32_t k1,
-                              uint32_t step, uint64_t stepp, uint32_t row0, uint64_t st) {
-    chk(gnn_launch_gat_act_bwd(Pt<const void>(dh), ldh, Pt<const float>(out), Pt<const float>(b), Pt<float>(dout),
-                               Pt<void>(doutb), Pt<float>(bpart), Pt<float>(db), n, F, p, k0, k1, step,
-                               Pt<const int>(stepp), row0, S(st)), "gnn_gat_act_bwd");
-  });
   m.def("gnn_gat_row_ce_waves", &gnn_gat_row_ce_waves);
   m.def("gnn_gat_row_ce", [](uint64_t z, int ldz, uint64_t b, int C, uint64_t y, uint64_t mask, float inv_count,
                              uint64_t dz, uint64_t dzb, uint64_t spart, uint64_t bpart, uint64_t stats, uint64_t db,
@@ -397,16 +400,16 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gnn_lin_fwd", [](uint64_t x1, int ld1, int K1, uint64_t x2, int ld2, int K2, uint64_t w, int N, uint64_t b,
                           uint64_t y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step,
                           uint32_t row0, uint64_t stepp, uint64_t rscale, uint64_t st, uint64_t idx1, uint64_t wimg,
-                          uint64_t yf, int nsplit, int tk) {
+                          uint64_t yf, int nsplit, int tk, int et) {
     return gnn_launch_lin_fwd(Pt<const void>(x1), ld1, K1, Pt<const void>(x2), ld2, K2, Pt<const float>(w), N,
                               Pt<const float>(b), Pt<void>(y), ldy, n, relu, p, k0, k1, step, row0,
                               Pt<const int>(stepp), Pt<const float>(rscale), Pt<const int>(idx1), Pt<void>(wimg),
-                              Pt<float>(yf), nsplit, tk, S(st));
+                              Pt<float>(yf), nsplit, tk, S(st), et);
   }, py::arg("x1"), py::arg("ld1"), py::arg("K1"), py::arg("x2"), py::arg("ld2"), py::arg("K2"), py::arg("w"),
      py::arg("N"), py::arg("b"), py::arg("y"), py::arg("ldy"), py::arg("n"), py::arg("relu"), py::arg("p"),
      py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("stepp"), py::arg("rscale"),
      py::arg("st"), py::arg("idx1") = 0, py::arg("wimg") = 0, py::arg("yf") = 0, py::arg("nsplit") = 0,
-     py::arg("tk") = 1);
+     py::arg("tk") = 1, py::arg("et") = 0);
   m.def("gnn_lin_fwd_image_bytes", &gnn_lin_fwd_image_bytes);
   m.def("gnn_lin_bwd_image_bytes", &gnn_lin_bwd_image_bytes);
   m.def("gnn_lin_bwd_data", [](uint64_t dy, int lddy, uint64_t ym, int ldym, float mscale, int N, uint64_t w, int K1,

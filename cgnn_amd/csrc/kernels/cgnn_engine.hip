@@ -28,7 +28,8 @@ int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, 
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t, int);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
-                        const float*, int, int, int, int, int, int, int, float*, hipStream_t);
+                        const float*, int, int, int, int, int, int, int, float*, hipStream_t, float*);
+int cgnn_mmd_supported_d(int);
 int cgnn_gen_bwd_blocks(int);
 int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
                      int, float, float, float, float, int, hipStream_t);
@@ -75,6 +76,7 @@ struct EngineBuffers {
   float* rff_diff = nullptr;    // [R][7k]
   float* xnorm = nullptr;       // [R][N] squared norms of xhat rows (written by gen_fwd)
   const float* ynorm = nullptr; // [R][N] squared norms of the data rows
+  float* dxs = nullptr;         // [R][d_true][N] sample-gradient scratch of the generic-width backward
 };
 
 class Engine {
@@ -100,7 +102,12 @@ class Engine {
     if (c_.mfma) return c_.mf_chunks * cgnn_mmd_mfma_row_blocks(c_.N);
     return c_.n_chunks * c_.row_tiles;
   }
-  int n_parts_tt() const { return c_.n_chunks * c_.row_tiles; }
+  // the vector kernel's true-true pass where it has a variant; the matrix-core one
+  // (mode 2) for the wide joints only it covers
+  bool tt_mfma() const { return c_.mfma && !cgnn_mmd_supported_d(c_.D); }
+  int n_parts_tt() const {
+    return tt_mfma() ? c_.mf_chunks * cgnn_mmd_mfma_row_blocks(c_.N) : c_.n_chunks * c_.row_tiles;
+  }
   int grad_chunks() const { return c_.rff_k > 0 ? 1 : (c_.mfma ? c_.mf_chunks : c_.n_chunks); }
 
   // loss (+ gradient when train) of the current xhat; `need_loss` false lets the
@@ -138,8 +145,12 @@ class Engine {
   void compute_tt() {
     if (c_.rff_k > 0) return;   // the Fourier loss has no constant block
     const float inv = 1.f / ((float)c_.N * (float)c_.N);
-    check(cgnn_launch_mmd(2, c_.D, b_.xhat, b_.data, b_.gradp, b_.lpart, c_.N, c_.R, c_.row_tiles,
-                          c_.n_chunks, c_.tpc, 0.f, st_), "mmd(tt)");
+    if (tt_mfma())
+      check(cgnn_launch_mmd_mfma(2, c_.D, b_.xhat, b_.data, b_.xnorm, b_.ynorm, b_.gradp, b_.lpart, c_.N, c_.R,
+                                 c_.mf_chunks, c_.mf_tpc, 0.f, st_), "mmd_mfma(tt)");
+    else
+      check(cgnn_launch_mmd(2, c_.D, b_.xhat, b_.data, b_.gradp, b_.lpart, c_.N, c_.R, c_.row_tiles,
+                            c_.n_chunks, c_.tpc, 0.f, st_), "mmd(tt)");
     check(cgnn_launch_loss_finalize(b_.lpart, n_parts_tt(), b_.tt, b_.loss_last, b_.loss_acc, inv, 2,
                                     nullptr, 0, b_.step, 0, c_.R, st_), "finalize(tt)");
   }
@@ -154,7 +165,7 @@ class Engine {
       check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 0,
                                       b_.loss_hist, c_.hist_stride, b_.step, off, c_.R, st_), "finalize");
     check(cgnn_launch_gen_bwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.xhat, b_.noise, c_.NS, b_.gradp,
-                              grad_chunks(), c_.R, c_.N, c_.D, c_.d_true, c_.H, c_.max_in, b_.gpart, st_),
+                              grad_chunks(), c_.R, c_.N, c_.D, c_.d_true, c_.H, c_.max_in, b_.gpart, st_, b_.dxs),
           "gen_bwd");
     check(cgnn_launch_adam(b_.params, b_.m, b_.v, b_.gpart, G_, b_.prog, c_.prog_stride, c_.P, b_.step,
                            off, c_.lr, c_.beta1, c_.beta2, c_.eps, c_.R, st_), "adam");
@@ -239,7 +250,7 @@ extern "C" void* cgnn_engine_create(const int* icfg, const float* fcfg, const vo
   b.gpart = (float*)ptrs[9]; b.tt = (float*)ptrs[10]; b.loss_last = (float*)ptrs[11];
   b.loss_acc = (float*)ptrs[12]; b.loss_hist = (float*)ptrs[13]; b.step = (int*)ptrs[14];
   b.keys = (const uint32_t*)ptrs[15]; b.rff_w = (float*)ptrs[16]; b.rff_diff = (float*)ptrs[17];
-  b.xnorm = (float*)ptrs[18]; b.ynorm = (const float*)ptrs[19];
+  b.xnorm = (float*)ptrs[18]; b.ynorm = (const float*)ptrs[19]; b.dxs = (float*)ptrs[20];
   return new cgnn::Engine(c, b, st);
 }
 

@@ -4,20 +4,21 @@
 // Per edge (i <- j) and head k:  e_ijk = LeakyReLU(s_dst[i,k] + s_src[j,k], 0.2)
 //   alpha_ijk = softmax over j in N(i) of e_ijk,  out[i,k,:] = sum_j alpha_ijk Wh[j,k,:]
 //
-//   gat_fwd_kernel      one CSR row per L-lane sub-group, each lane 8 features of one
-//                       head; single pass with an ONLINE softmax (running max and
-//                       rescaled sum), so the edge scores are never materialised;
-//                       writes out and the per-(row, head) log-sum-exp.
-//   gat_bwd_row_kernel  per row i: alpha recomputed from the lse, the SDDMM
-//                       dalpha_ij = <dout_i, Wh_j> (head-group shuffle reduction),
-//                       de = alpha (dalpha - <dout_i, out_i>), LeakyReLU'; the row
-//                       term d s_dst[i] in registers; per (row, head) statistics
-//                       (s_dst, lse, D) for the column half -- nothing per edge.
-//   gat_bwd_col_kernel  per source row j over the TRANSPOSED CSR: alpha and the
-//                       score gradient recomputed from the gathered dout_i and row
-//                       statistics against the own row Wh_j: dWh[j] = sum alpha_ij
-//                       dout_i, d s_src[j] = sum dscore_ij -- gathers only, no atomics.
-// Everything fp32, fixed summation orders (deterministic).
+//   gat_fwd_kernel   one CSR row per L-lane sub-group, each lane 8 features of one
+//                    head; single pass with an ONLINE softmax (running max and rescaled
+//                    sums), so the edge scores are never materialised; writes out, the
+//                    per-(row, head) log-sum-exp and (training) the LeakyReLU split q
+//                    that turns the row half of the backward into a per-row product;
+//                    optionally the hidden layer's activation (ELU + Philox dropout).
+//   gat_row_kernel   per row: D = <dout, out>, d s_dst = -0.8 <dout, q>, the statistics
+//                    (s_dst, lse, D) for the column half; optionally fused with the
+//                    activation backward (dropout mask, ELU', bias gradient) -- no gather.
+//   gat_col_kernel   per source row j over the TRANSPOSED CSR: alpha and the score
+//                    gradient recomputed from the gathered dout_i and row statistics
+//                    against the own row Wh_j: dWh[j] = sum alpha_ij dout_i, d s_src[j] =
+//                    sum dscore_ij -- gathers only, no atomics; fp32 out, or bf16 straight
+//                    into the projection-gradient operand dy.
+// Arithmetic fp32, fixed summation orders (deterministic).
 #include "cgnn_common.h"
 #include <algorithm>
 #include <cmath>
@@ -29,21 +30,6 @@ namespace {
 __device__ __forceinline__ void ld8(const float* p, float* f) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
   f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
-}
-// 8 gathered values of a row stored fp32 (WT = 0) or bf16 (WT = 1), returned as fp32
-template <int WT>
-__device__ __forceinline__ void ldg8(const void* base, size_t off, float* f) {
-  if (WT == 1) {
-    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(base) + off);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f[2 * q] = __uint_as_float(w[q] << 16);
-      f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
-    }
-  } else {
-    ld8(reinterpret_cast<const float*>(base) + off, f);
-  }
 }
 __device__ __forceinline__ void st8(float* p, const float* f) {
   *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
@@ -58,311 +44,465 @@ __device__ __forceinline__ float group_sum(float v) {
 }
 __device__ __forceinline__ float leaky(float x) { return x > 0.f ? x : 0.2f * x; }
 
+// ---------------------------------------------------------------- aggregation
+// Row layout of every aggregation kernel: L lanes per CSR row (L * 8 >= K * Fh), each
+// lane 8 consecutive features of one head, G = Fh / 8 lanes per head (a power of two,
+// groups aligned; one head: the row's whole sub-group).  Gathers run in batches of EC
+// edges whose rows are all requested before any is consumed (EC loads of 16 B per lane
+// in flight), and the next chunk's column indices are fetched one chunk ahead.
+//
+// LeakyReLU split.  With n_ij = [raw_ij <= 0] (the 0.2-slope side), the row half of
+// the backward is
+//   d s_dst[i] = sum_j alpha_ij (dalpha_ij - D_i) (1 - 0.8 n_ij)
+//              = (<dout_i, out_i> - D_i) - 0.8 (<dout_i, out-_i> - D_i c-_i)
+// with out-_i = sum_j n_ij alpha_ij Wh_j, c-_i = sum_j n_ij alpha_ij and D_i =
+// <dout_i, out_i> (sum alpha = 1): the first bracket vanishes, so
+//   d s_dst[i] = -0.8 <dout_i, q_i>,   q_i = out-_i - c-_i out_i,
+// a per-row product.  The forward accumulates out- beside out (same gathered rows, one
+// more FMA per feature) and stores q, so the row half needs no gather at all.
+template <int WT>
+__device__ __forceinline__ void ld_raw(const void* base, size_t off, uint4* r) {
+  if (WT == 1) {
+    r[0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(base) + off);
+  } else {
+    const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(base) + off);
+    r[0] = p[0];
+    r[1] = p[1];
+  }
+}
+// the same from a lane's byte base and a row's byte offset (one 64-bit multiply-add per
+// gathered row: j * row_bytes + lane base)
+template <int WT>
+__device__ __forceinline__ void ld_raw_b(const char* lane_base, uint32_t j, uint32_t row_bytes, uint4* r) {
+  const uint4* p = reinterpret_cast<const uint4*>(lane_base + (uint64_t)j * row_bytes);
+  r[0] = p[0];
+  if (WT == 0) r[1] = p[1];
+}
+template <int WT>
+__device__ __forceinline__ void raw_f32(const uint4* r, float* f) {
+  if (WT == 1) {
+    const uint32_t w[4] = {r[0].x, r[0].y, r[0].z, r[0].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f[2 * q] = __uint_as_float(w[q] << 16);
+      f[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+    }
+  } else {
+    const uint32_t w[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) f[q] = __uint_as_float(w[q]);
+  }
+}
+__device__ __forceinline__ uint32_t bf16u(float x) { return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)x); }
+__device__ __forceinline__ uint4 f8_bf16(const float* v) {
+  return make_uint4(bf16u(v[0]) | (bf16u(v[1]) << 16), bf16u(v[2]) | (bf16u(v[3]) << 16),
+                    bf16u(v[4]) | (bf16u(v[5]) << 16), bf16u(v[6]) | (bf16u(v[7]) << 16));
+}
+// 8 values stored as WT (bf16 / fp32)
+template <int WT>
+__device__ __forceinline__ void st_w8(void* base, size_t off, const float* v) {
+  if (WT == 1) *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(base) + off) = f8_bf16(v);
+  else st8(reinterpret_cast<float*>(base) + off, v);
+}
+template <int WT>
+__device__ __forceinline__ void ld_w8(const void* base, size_t off, float* v) {
+  uint4 r[2];
+  ld_raw<WT>(base, off, r);
+  raw_f32<WT>(r, v);
+}
+
+// Dropout convention of ops.dropout_keep_mask / the fused GCN kernels: column c is kept
+// iff byte (c % 4) + 4 ((c % 32) / 8) of the Philox draw keyed (row, 2 (c / 32) + (c % 8) / 4,
+// step) is >= thr8.  A lane's 8 columns f0..f0+7 (f0 % 8 == 0) read word (f0 % 32) / 8 of
+// the draws for h = 0 (first 4) and h = 1 (last 4).
+__device__ __forceinline__ void keep8(bool* kp, uint32_t thr8, uint32_t grow, int f0, uint32_t step, uint32_t k0,
+                                      uint32_t k1) {
+  if (thr8 == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kp[i] = true;
+    return;
+  }
+  const int t = f0 >> 5, g = (f0 & 31) >> 3;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const u32x4 r = philox4x32_10(u32x4{grow, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
+    const uint32_t w = g == 0 ? r.x : g == 1 ? r.y : g == 2 ? r.z : r.w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) kp[4 * h + i] = ((w >> (8 * i)) & 0xffu) >= thr8;
+  }
+}
+
 }  // namespace
 
-// L lanes per row (L * 8 >= K * Fh), G = Fh / 8 lanes per head.
-constexpr int EB = 4;   // edges per online-softmax step (gat_fwd_kernel)
+struct GatFwdArgs {
+  const int* rowptr;
+  const int* col;
+  const void* Wh;          // [n_cols][HF] WT
+  const float* s_src;      // [n_cols][K]
+  const float* s_dst;      // [*][K], row dst_rows[i] (or i)
+  const int* dst_rows;     // optional
+  float* out;              // [n][HF] fp32
+  float* lse;              // [n][K]
+  void* q;                 // optional [n][HF] WT: out- - c- out (training)
+  // optional fused hidden activation H = bf16(dropout(elu(out + bias))) (HF % 32 == 0)
+  const float* bias;
+  uint16_t* H;
+  int ldh;
+  float p;
+  uint32_t k0, k1, step, thr8, row0;
+  const int* stepp;
+  int n, K, HF;
+};
 
-template <int L, int G, int WT>
-__global__ __launch_bounds__(256) void gat_fwd_kernel(
-    const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Wh,
-    const float* __restrict__ s_src, const float* __restrict__ s_dst, float* __restrict__ out,
-    float* __restrict__ lse, int n, int K, int HF) {
+// Occupancy of the two gather kernels: they are latency-bound (rows in flight per CU),
+// so a register cap that buys waves can pay (A/B: -DCGNN_GAT_WAVES=N, N waves per SIMD)
+#ifdef CGNN_GAT_WAVES
+#define GAT_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(CGNN_GAT_WAVES)))
+#else
+#define GAT_WAVES_ATTR
+#endif
+
+// Scores run in the log2 domain (LeakyReLU is positively homogeneous: leaky(c x) =
+// c leaky(x) for c > 0), so every exponential is one v_exp_f32.
+constexpr float L2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+__device__ __forceinline__ float leaky2(float x) { return fmaxf(x, 0.2f * x); }
+
+template <int L, int G, int WT, int EC>
+__global__ __launch_bounds__(256) GAT_WAVES_ATTR void gat_fwd_kernel(GatFwdArgs a) {
   constexpr int RPW = 64 / L;
   const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
   const int row = (xcd_remap(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
-  const bool rv = row < n;
-  const int f0 = 8 * sl;
+  const bool rv = row < a.n;
+  const int f0 = 8 * sl, K = a.K, HF = a.HF;
   const bool fv = rv && f0 < HF;
   const int k = fv ? f0 / (8 * G) : 0;
-  const float sd = fv ? s_dst[(size_t)row * K + k] : 0.f;
-  float m = -INFINITY, l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
+  const int srow = rv ? (a.dst_rows ? a.dst_rows[row] : row) : 0;
+  const float sd = fv ? a.s_dst[(size_t)srow * K + k] * L2E : 0.f;
+  const char* wh_lane = reinterpret_cast<const char*>(a.Wh) + (size_t)f0 * (WT == 1 ? 2 : 4);
+  const uint32_t wh_row = (uint32_t)HF * (WT == 1 ? 2 : 4);
+  const char* ss_lane = reinterpret_cast<const char*>(a.s_src) + (size_t)k * 4;
+  const uint32_t ss_row = (uint32_t)K * 4;
+  float m = -INFINITY, l = 0.f, ln = 0.f;
+  float acc[8], accn[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) acc[f] = accn[f] = 0.f;
+  const int e0 = rv ? a.rowptr[row] : 0, e1 = rv ? a.rowptr[row + 1] : 0;
+  int nj = (e0 + sl < e1) ? a.col[e0 + sl] : 0;
   for (int e = e0; e < e1; e += L) {
-    const int myj = (e + sl < e1) ? col[e + sl] : 0;
+    const int myj = nj;
+    nj = (e + L + sl < e1) ? a.col[e + L + sl] : 0;       // next chunk's indices, one chunk ahead
     const int cnt = min(L, e1 - e);
-    // EB edges per step: their rows are requested together, and the online softmax
-    // rescales once per step (EB + 1 exponentials instead of 2 EB)
-    for (int q = 0; q < cnt; q += EB) {
-      int j[EB];
+    for (int q0 = 0; q0 < cnt; q0 += EC) {
+      // the batch's rows: edges past the row's end re-read the batch's first row (a cache
+      // hit) and get weight 0, so the loads issue back to back without branches
+      int js[EC];
+      const int jf = __shfl(myj, sub * L + q0, 64);
 #pragma unroll
-      for (int u = 0; u < EB; ++u) j[u] = __shfl(myj, sub * L + min(q + u, L - 1), 64);
+      for (int u = 0; u < EC; ++u) {
+        const int j = __shfl(myj, sub * L + q0 + u, 64);
+        js[u] = q0 + u < cnt ? j : jf;
+      }
       if (fv) {
-        float w[EB][8], sc[EB];
+        uint4 raw[EC][WT == 1 ? 1 : 2];
+        float sc[EC];
 #pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          ldg8<WT>(Wh, (size_t)j[u] * HF + f0, w[u]);
-          sc[u] = s_src[(size_t)j[u] * K + k];
+        for (int u = 0; u < EC; ++u) {
+          ld_raw_b<WT>(wh_lane, (uint32_t)js[u], wh_row, raw[u]);
+          sc[u] = *reinterpret_cast<const float*>(ss_lane + (uint64_t)(uint32_t)js[u] * ss_row);
         }
-        float mn = m;
+        float mx = m;
 #pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          sc[u] = (q + u < cnt) ? leaky(sd + sc[u]) : -INFINITY;
-          mn = fmaxf(mn, sc[u]);
+        for (int u = 0; u < EC; ++u) {
+          sc[u] = (q0 + u < cnt) ? leaky2(fmaf(sc[u], L2E, sd)) : -INFINITY;
+          mx = fmaxf(mx, sc[u]);
         }
-        const float a = __expf(m - mn);
-        float b[EB];
-#pragma unroll
-        for (int u = 0; u < EB; ++u) b[u] = __expf(sc[u] - mn);
+        const float sa = __builtin_amdgcn_exp2f(m - mx);
+        l *= sa;
+        ln *= sa;
 #pragma unroll
         for (int f = 0; f < 8; ++f) {
-          float t = acc[f] * a;
-#pragma unroll
-          for (int u = 0; u < EB; ++u) t = fmaf(b[u], w[u][f], t);
-          acc[f] = t;
+          acc[f] *= sa;
+          accn[f] *= sa;
         }
-        float ls = l * a;
 #pragma unroll
-        for (int u = 0; u < EB; ++u) ls += b[u];
-        l = ls;
-        m = mn;
+        for (int u = 0; u < EC; ++u) {
+          const float b = __builtin_amdgcn_exp2f(sc[u] - mx);
+          const float bn = sc[u] <= 0.f ? b : 0.f;
+          float w[8];
+          raw_f32<WT>(raw[u], w);
+#pragma unroll
+          for (int f = 0; f < 8; ++f) {
+            acc[f] = fmaf(b, w[f], acc[f]);
+            accn[f] = fmaf(bn, w[f], accn[f]);
+          }
+          l += b;
+          ln += bn;
+        }
+        m = mx;
       }
     }
   }
   if (!fv) return;
   const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
-  for (int u = 0; u < 8; ++u) acc[u] *= inv;
-  st8(out + (size_t)row * HF + f0, acc);
-  if (f0 % (8 * G) == 0) lse[(size_t)row * K + k] = l > 0.f ? m + __logf(l) : 0.f;
+  for (int f = 0; f < 8; ++f) acc[f] *= inv;
+  st8(a.out + (size_t)row * HF + f0, acc);
+  if (f0 % (8 * G) == 0) a.lse[(size_t)row * K + k] = l > 0.f ? (m + __log2f(l)) * LN2 : 0.f;
+  if (a.q) {
+    const float cn = ln * inv;
+    float qv[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) qv[f] = fmaf(accn[f], inv, -cn * acc[f]);
+    st_w8<WT>(a.q, (size_t)row * HF + f0, qv);
+  }
+  if (a.H) {
+    const uint32_t step = a.stepp ? (uint32_t)*a.stepp : a.step;
+    bool kp[8];
+    keep8(kp, a.thr8, a.row0 + (uint32_t)row, f0, step, a.k0, a.k1);
+    const float scale = a.thr8 > 0 ? 1.f / (1.f - a.p) : 1.f;
+    float hv[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      const float z = acc[f] + a.bias[f0 + f];
+      const float e = z > 0.f ? z : expm1f(z);
+      hv[f] = kp[f] ? e * scale : 0.f;
+    }
+    *reinterpret_cast<uint4*>(a.H + (size_t)row * a.ldh + f0) = f8_bf16(hv);
+  }
 }
 
-// Row half of the backward, per destination row i and head k: D_ik = <dout_ik, out_ik>,
-// and over the row's edges the SDDMM da_ij = <dout_i, Wh_j>, the attention weight
-// recomputed from the lse, ds_ij = alpha_ij (da_ij - D_ik) LeakyReLU'; their row sum is
-// d s_dst[i,k].  Nothing is stored per edge: the column half recomputes alpha and ds
-// from the row statistics rs[i][k] = (s_dst, lse, D, 0) (one 16-B gather per edge and
-// head) -- no [nnz, K] fp32 arrays, no edge permutation.
-template <int L, int G, int WT>
-__global__ __launch_bounds__(256) void gat_bwd_row_kernel(
-    const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ Wh,
-    const float* __restrict__ s_src, const float* __restrict__ s_dst, const float* __restrict__ out,
-    const float* __restrict__ lse, const float* __restrict__ dout, float4* __restrict__ rstat,
-    float* __restrict__ ds_dst, int n, int K, int HF) {
+// Row statistics of the backward (per destination row i, head k): D_ik = <dout_ik, out_ik>
+// and d s_dst[i,k] = -0.8 <dout_ik, q_ik>; rstat[i][k] = (s_dst, lse, D, 0) for the column
+// half (s_dst and lse scaled by log2 e).  dout / q as WT.  ds_dst goes to an fp32 [*][K] array (row dst_rows[i] or i) and /
+// or straight into column HF + K + k of the bf16 GEMM operand dy (same row).
+//
+// act (hidden layer): dout is first made from the layer output's gradient dH, dout =
+// dH * dropout mask * elu'(out + bias), stored as WT, and the bias gradient is summed per
+// block (bpart[block][HF], fixed order) -- the activation backward and the row half in
+// one pass.  Fixed grid, rows grid-strided (the per-lane column sums stay in registers).
+struct GatRowArgs {
+  const void* dout;        // act: the output rows' gradient dH (bf16, ldh); else dout (WT)
+  int ldh;
+  const float* out;
+  const void* q;
+  const float* lse;
+  const float* s_dst;
+  const int* dst_rows;
+  float4* rstat;
+  float* ds_dst;
+  uint16_t* dy;
+  int ldy;
+  // act only
+  void* dout_w;            // dout as WT
+  const float* bias;
+  float* bpart;
+  float p;
+  uint32_t k0, k1, step, thr8, row0;
+  const int* stepp;
+  int n, K, HF;
+};
+
+template <int L, int G, int WT, bool ACT>
+__global__ __launch_bounds__(256) void gat_row_kernel(GatRowArgs a) {
   constexpr int RPW = 64 / L;
-  const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
-  const int row = (xcd_remap(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
-  const bool rv = row < n;
-  const int f0 = 8 * sl;
-  const bool fv = rv && f0 < HF;
-  const int k = fv ? f0 / (8 * G) : 0;
-  const bool lead = fv && (f0 % (8 * G) == 0);
-  float go[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  float sd = 0.f, ls = 0.f;
-  if (fv) {
-    ld8(dout + (size_t)row * HF + f0, go);
-    ld8(out + (size_t)row * HF + f0, o);
-    sd = s_dst[(size_t)row * K + k];
-    ls = lse[(size_t)row * K + k];
+  __shared__ float red[4][64][8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, sub = lane / L, sl = lane - sub * L;
+  const int f0 = 8 * sl, K = a.K, HF = a.HF;
+  const bool fl = f0 < HF;
+  const int k = fl ? f0 / (8 * G) : 0;
+  const bool lead = fl && (f0 % (8 * G) == 0);
+  const long rows_per_pass = (long)gridDim.x * 4 * RPW;
+  const uint32_t step = ACT ? (a.stepp ? (uint32_t)*a.stepp : a.step) : 0u;
+  const float scale = (ACT && a.thr8 > 0) ? 1.f / (1.f - a.p) : 1.f;
+  float bsum[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) bsum[f] = 0.f;
+  float bv[8];
+  if (ACT) {
+#pragma unroll
+    for (int f = 0; f < 8; ++f) bv[f] = fl ? a.bias[f0 + f] : 0.f;
   }
-  float dd = 0.f;
+  for (long base = ((long)blockIdx.x * 4 + wv) * RPW; base < a.n; base += rows_per_pass) {
+    const long row = base + sub;
+    const bool fv = row < a.n && fl;
+    float d[8], o[8], qv[8];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) dd = fmaf(go[u], o[u], dd);
-  dd = group_sum<G>(dd);                       // D_ik = <dout_ik, out_ik>
-  float dsd = 0.f;
-  const int e0 = rv ? rowptr[row] : 0, e1 = rv ? rowptr[row + 1] : 0;
-  for (int e = e0; e < e1; e += L) {
-    const int myj = (e + sl < e1) ? col[e + sl] : 0;
-    const int cnt = min(L, e1 - e);
-    for (int q = 0; q < cnt; q += EB) {          // EB edges' rows requested together
-      int j[EB];
+    for (int f = 0; f < 8; ++f) d[f] = o[f] = qv[f] = 0.f;
+    if (fv) {
+      ld8(a.out + (size_t)row * HF + f0, o);
+      ld_w8<WT>(a.q, (size_t)row * HF + f0, qv);
+      if (ACT) {
+        float dh[8];
+        ld_w8<1>(a.dout, (size_t)row * a.ldh + f0, dh);
+        bool kp[8];
+        keep8(kp, a.thr8, a.row0 + (uint32_t)row, f0, step, a.k0, a.k1);
 #pragma unroll
-      for (int u = 0; u < EB; ++u) j[u] = __shfl(myj, sub * L + min(q + u, L - 1), 64);
-      float w[EB][8], raw[EB];
-#pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        if (fv) {
-          ldg8<WT>(Wh, (size_t)j[u] * HF + f0, w[u]);
-          raw[u] = sd + s_src[(size_t)j[u] * K + k];
-        } else {
-#pragma unroll
-          for (int f = 0; f < 8; ++f) w[u][f] = 0.f;
-          raw[u] = 0.f;
+        for (int f = 0; f < 8; ++f) {
+          const float z = o[f] + bv[f];
+          d[f] = kp[f] ? dh[f] * scale * (z > 0.f ? 1.f : __expf(z)) : 0.f;
+          bsum[f] += d[f];
         }
-      }
-      float da[EB];
-#pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        float d = 0.f;
-#pragma unroll
-        for (int f = 0; f < 8; ++f) d = fmaf(go[f], w[u][f], d);
-        da[u] = d;
-      }
-#pragma unroll
-      for (int off = 1; off < G; off <<= 1) {   // SDDMM: dalpha_ij = <dout_i, Wh_j>
-#pragma unroll
-        for (int u = 0; u < EB; ++u) da[u] += __shfl_xor(da[u], off, 64);
-      }
-      if (fv) {
-#pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          if (q + u < cnt) {
-            const float al = __expf(leaky(raw[u]) - ls);
-            dsd += al * (da[u] - dd) * (raw[u] > 0.f ? 1.f : 0.2f);
-          }
+        st_w8<WT>(a.dout_w, (size_t)row * HF + f0, d);
+        if (WT == 1) {                 // the column half gathers the rounded values: use them here too
+          uint4 r[1];
+          r[0] = f8_bf16(d);
+          raw_f32<1>(r, d);
         }
+      } else {
+        ld_w8<WT>(a.dout, (size_t)row * HF + f0, d);
       }
     }
+    float dd = 0.f, dq = 0.f;
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      dd = fmaf(d[f], o[f], dd);
+      dq = fmaf(d[f], qv[f], dq);
+    }
+    dd = group_sum<G>(dd);
+    dq = group_sum<G>(dq);
+    if (fv && f0 % (8 * G) == 0) {
+      const long srow = a.dst_rows ? a.dst_rows[row] : row;
+      const float dsd = -0.8f * dq;
+      // (s_dst, lse) in log2 units for the column half's exp2
+      a.rstat[(size_t)row * K + k] =
+          make_float4(a.s_dst[(size_t)srow * K + k] * L2E, a.lse[(size_t)row * K + k] * L2E, dd, 0.f);
+      if (a.ds_dst) a.ds_dst[(size_t)srow * K + k] = dsd;
+      if (a.dy) a.dy[(size_t)srow * a.ldy + HF + K + k] = (uint16_t)bf16u(dsd);
+    }
   }
-  if (lead) {
-    ds_dst[(size_t)row * K + k] = dsd;
-    rstat[(size_t)row * K + k] = make_float4(sd, ls, dd, 0.f);
+  (void)lead;
+  if (ACT) {
+    // bias gradient: lanes with equal sl hold the same columns; sum the RPW sub-groups
+    // (fixed xor order), then the 4 waves in order
+#pragma unroll
+    for (int off = L; off < 64; off <<= 1)
+#pragma unroll
+      for (int f = 0; f < 8; ++f) bsum[f] += __shfl_xor(bsum[f], off, 64);
+    if (sub == 0) {
+#pragma unroll
+      for (int f = 0; f < 8; ++f) red[wv][sl][f] = bsum[f];
+    }
+    __syncthreads();
+    if (wv == 0 && sub == 0 && fl) {
+#pragma unroll
+      for (int f = 0; f < 8; ++f)
+        a.bpart[(size_t)blockIdx.x * HF + f0 + f] = (red[0][sl][f] + red[1][sl][f]) + (red[2][sl][f] + red[3][sl][f]);
+    }
   }
 }
 
 // Column half, per SOURCE row j of the transposed CSR (the destinations i that read j,
 // in increasing order) and head k: the own row Wh_j and s_src[j,k] stay in registers;
-// per edge the gathered dout_i and rs[i][k] give alpha_ij = exp(LeakyReLU(s_dst_i +
+// per edge the gathered dout_i and rstat[i][k] give alpha_ij = exp(LeakyReLU(s_dst_i +
 // s_src_j) - lse_i) and ds_ij = alpha_ij (<dout_i, Wh_j> - D_i) LeakyReLU':
 // dWh_j = sum_i alpha_ij dout_i, d s_src[j,k] = sum_i ds_ij -- gathers only, no atomics,
-// fixed order.  Rows are independent, so a row range is a pointer offset (halo rounds).
-template <int L, int G, int WT>
-__global__ __launch_bounds__(256) void gat_bwd_col_kernel(
-    const int* __restrict__ rowptr_t, const int* __restrict__ col_t, const void* __restrict__ Wh,
-    const float* __restrict__ s_src, const float4* __restrict__ rstat, const void* __restrict__ dout,
-    float* __restrict__ dWh, float* __restrict__ ds_src, int n, int K, int HF) {
+// fixed order.  Output: fp32 dWh / ds_src (rows of the launch), or bf16 straight into
+// columns [0, HF + K) of the GEMM operand dy (row j, stride ldy).  Rows are independent,
+// so a row range is a pointer offset (halo rounds).
+struct GatColArgs {
+  const int* rowptr_t;
+  const int* col_t;
+  const void* Wh;
+  const float* s_src;
+  const float4* rstat;
+  const void* dout;        // WT
+  float* dWh;
+  float* ds_src;
+  uint16_t* dy;
+  int ldy;
+  int n, K, HF;
+};
+
+template <int L, int G, int WT, int EC>
+__global__ __launch_bounds__(256) GAT_WAVES_ATTR void gat_col_kernel(GatColArgs a) {
   constexpr int RPW = 64 / L;
   const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
   const int row = (xcd_remap(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
-  const bool rv = row < n;
-  const int f0 = 8 * sl;
+  const bool rv = row < a.n;
+  const int f0 = 8 * sl, K = a.K, HF = a.HF;
   const bool fv = rv && f0 < HF;
   const int k = fv ? f0 / (8 * G) : 0;
   float wj[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float ss = 0.f;
   if (fv) {
-    ldg8<WT>(Wh, (size_t)row * HF + f0, wj);
-    ss = s_src[(size_t)row * K + k];
+    ld_w8<WT>(a.Wh, (size_t)row * HF + f0, wj);
+    ss = a.s_src[(size_t)row * K + k] * L2E;
   }
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float dss = 0.f;
-  const int e0 = rv ? rowptr_t[row] : 0, e1 = rv ? rowptr_t[row + 1] : 0;
+  const char* do_lane = reinterpret_cast<const char*>(a.dout) + (size_t)f0 * (WT == 1 ? 2 : 4);
+  const uint32_t do_row = (uint32_t)HF * (WT == 1 ? 2 : 4);
+  const char* rs_lane = reinterpret_cast<const char*>(a.rstat) + (size_t)k * 16;
+  const uint32_t rs_row = (uint32_t)K * 16;
+  const int e0 = rv ? a.rowptr_t[row] : 0, e1 = rv ? a.rowptr_t[row + 1] : 0;
+  int ni = (e0 + sl < e1) ? a.col_t[e0 + sl] : 0;
   for (int e = e0; e < e1; e += L) {
-    const int myi = (e + sl < e1) ? col_t[e + sl] : 0;
+    const int myi = ni;
+    ni = (e + L + sl < e1) ? a.col_t[e + L + sl] : 0;
     const int cnt = min(L, e1 - e);
-    for (int q = 0; q < cnt; q += EB) {          // EB edges' rows requested together
-      int i[EB];
+    for (int q0 = 0; q0 < cnt; q0 += EC) {
+      int is[EC];
+      const int i_f = __shfl(myi, sub * L + q0, 64);
 #pragma unroll
-      for (int u = 0; u < EB; ++u) i[u] = __shfl(myi, sub * L + min(q + u, L - 1), 64);
-      float g[EB][8];
-      float4 rs[EB];
+      for (int u = 0; u < EC; ++u) {
+        const int i = __shfl(myi, sub * L + q0 + u, 64);
+        is[u] = q0 + u < cnt ? i : i_f;
+      }
+      uint4 raw[EC][WT == 1 ? 1 : 2];
+      float4 rs[EC];
+      if (fv) {
 #pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        if (fv) {
-          ldg8<WT>(dout, (size_t)i[u] * HF + f0, g[u]);
-          rs[u] = rstat[(size_t)i[u] * K + k];
-        } else {
+        for (int u = 0; u < EC; ++u) {
+          ld_raw_b<WT>(do_lane, (uint32_t)is[u], do_row, raw[u]);
+          rs[u] = *reinterpret_cast<const float4*>(rs_lane + (uint64_t)(uint32_t)is[u] * rs_row);
+        }
+      } else {
 #pragma unroll
-          for (int f = 0; f < 8; ++f) g[u][f] = 0.f;
+        for (int u = 0; u < EC; ++u) {
+          raw[u][0] = make_uint4(0u, 0u, 0u, 0u);
+          if (WT == 0) raw[u][WT == 1 ? 0 : 1] = make_uint4(0u, 0u, 0u, 0u);
           rs[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      float da[EB];
+      float da[EC];
 #pragma unroll
-      for (int u = 0; u < EB; ++u) {
+      for (int u = 0; u < EC; ++u) {
+        float g[8];
+        raw_f32<WT>(raw[u], g);
         float d = 0.f;
 #pragma unroll
-        for (int f = 0; f < 8; ++f) d = fmaf(g[u][f], wj[f], d);
+        for (int f = 0; f < 8; ++f) d = fmaf(g[f], wj[f], d);
         da[u] = d;
       }
 #pragma unroll
       for (int off = 1; off < G; off <<= 1) {
 #pragma unroll
-        for (int u = 0; u < EB; ++u) da[u] += __shfl_xor(da[u], off, 64);
+        for (int u = 0; u < EC; ++u) da[u] += __shfl_xor(da[u], off, 64);
       }
       if (fv) {
 #pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          if (q + u < cnt) {
-            const float raw = rs[u].x + ss;
-            const float al = __expf(leaky(raw) - rs[u].y);
-            dss += al * (da[u] - rs[u].z) * (raw > 0.f ? 1.f : 0.2f);
+        for (int u = 0; u < EC; ++u) {
+          const float raw2 = rs[u].x + ss;                       // log2 units
+          const float al = q0 + u < cnt ? __builtin_amdgcn_exp2f(leaky2(raw2) - rs[u].y) : 0.f;
+          dss = fmaf(al * (da[u] - rs[u].z), raw2 > 0.f ? 1.f : 0.2f, dss);
+          float g[8];
+          raw_f32<WT>(raw[u], g);
 #pragma unroll
-            for (int f = 0; f < 8; ++f) acc[f] = fmaf(al, g[u][f], acc[f]);
-          }
+          for (int f = 0; f < 8; ++f) acc[f] = fmaf(al, g[f], acc[f]);
         }
       }
     }
   }
   if (!fv) return;
-  st8(dWh + (size_t)row * HF + f0, acc);
-  if (f0 % (8 * G) == 0) ds_src[(size_t)row * K + k] = dss;
-}
-
-// ---------------------------------------------------------------- launchers
-namespace {
-template <template <int, int> class, int, int> struct Unused {};
-
-int lanes_for(int HF) {
-  const int c = (HF + 7) / 8;
-  return c <= 8 ? 8 : c <= 16 ? 16 : c <= 32 ? 32 : c <= 64 ? 64 : -1;
-}
-}  // namespace
-
-#define GAT_DISPATCH(KERNEL, WT, ...)                                                                  \
-  do {                                                                                             \
-    /* one head: its group is the row's whole sub-group (lanes past HF add 0) */                  \
-    const int L = lanes_for(HF), G = K == 1 ? L : Fh / 8;                                          \
-    if (L < 0 || Fh % 8 || HF != K * Fh) return -3;                                                \
-    const int rpb = 4 * (64 / L);                                                                  \
-    dim3 grid((n + rpb - 1) / rpb), block(256);                                                    \
-    switch (L * 100 + G) {                                                                         \
-      case 801: hipLaunchKernelGGL((KERNEL<8, 1, WT>), grid, block, 0, st, __VA_ARGS__); break;        \
-      case 802: hipLaunchKernelGGL((KERNEL<8, 2, WT>), grid, block, 0, st, __VA_ARGS__); break;        \
-      case 804: hipLaunchKernelGGL((KERNEL<8, 4, WT>), grid, block, 0, st, __VA_ARGS__); break;        \
-      case 808: hipLaunchKernelGGL((KERNEL<8, 8, WT>), grid, block, 0, st, __VA_ARGS__); break;        \
-      case 1601: hipLaunchKernelGGL((KERNEL<16, 1, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 1602: hipLaunchKernelGGL((KERNEL<16, 2, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 1604: hipLaunchKernelGGL((KERNEL<16, 4, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 1608: hipLaunchKernelGGL((KERNEL<16, 8, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 1616: hipLaunchKernelGGL((KERNEL<16, 16, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
-      case 3202: hipLaunchKernelGGL((KERNEL<32, 2, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 3204: hipLaunchKernelGGL((KERNEL<32, 4, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 3208: hipLaunchKernelGGL((KERNEL<32, 8, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 3216: hipLaunchKernelGGL((KERNEL<32, 16, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
-      case 3232: hipLaunchKernelGGL((KERNEL<32, 32, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
-      case 6404: hipLaunchKernelGGL((KERNEL<64, 4, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 6408: hipLaunchKernelGGL((KERNEL<64, 8, WT>), grid, block, 0, st, __VA_ARGS__); break;      \
-      case 6416: hipLaunchKernelGGL((KERNEL<64, 16, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
-      case 6464: hipLaunchKernelGGL((KERNEL<64, 64, WT>), grid, block, 0, st, __VA_ARGS__); break;    \
-      default: return -1;                                                                          \
-    }                                                                                              \
-    return (int)hipGetLastError();                                                                 \
-  } while (0)
-
-// Wh [n][HF], s_src / s_dst / lse [n][K], HF = K * Fh, Fh % 8 == 0; HF <= 512.
-// wbf: the gathered matrix (Wh in the forward and the row backward, dout in the
-// column backward) is stored bf16 -- half the bytes of the edge gathers, values
-// widened to fp32 in registers (all arithmetic and every other operand fp32).
-extern "C" int gnn_launch_gat_fwd(const int* rowptr, const int* col, const void* Wh, const float* s_src,
-                                  const float* s_dst, float* out, float* lse, int n, int K, int Fh, int wbf,
-                                  hipStream_t st) {
-  const int HF = K * Fh;
-  if (wbf) GAT_DISPATCH(gat_fwd_kernel, 1, rowptr, col, Wh, s_src, s_dst, out, lse, n, K, HF);
-  GAT_DISPATCH(gat_fwd_kernel, 0, rowptr, col, Wh, s_src, s_dst, out, lse, n, K, HF);
-}
-
-// rstat: [n][K] float4 (s_dst, lse, D, 0), written for the column half
-extern "C" int gnn_launch_gat_bwd_row(const int* rowptr, const int* col, const void* Wh, const float* s_src,
-                                      const float* s_dst, const float* out, const float* lse,
-                                      const float* dout, float* rstat, float* ds_dst, int n, int K, int Fh, int wbf,
-                                      hipStream_t st) {
-  const int HF = K * Fh;
-  float4* rs = reinterpret_cast<float4*>(rstat);
-  if (wbf)
-    GAT_DISPATCH(gat_bwd_row_kernel, 1, rowptr, col, Wh, s_src, s_dst, out, lse, dout, rs, ds_dst, n, K, HF);
-  GAT_DISPATCH(gat_bwd_row_kernel, 0, rowptr, col, Wh, s_src, s_dst, out, lse, dout, rs, ds_dst, n, K, HF);
-}
-
-// Wh / s_src / dWh / ds_src: rows of the launch's source range; rstat / dout: all
-// destination rows.  wbf: Wh and the gathered dout are bf16.
-extern "C" int gnn_launch_gat_bwd_col(const int* rowptr_t, const int* col_t, const void* Wh, const float* s_src,
-                                      const float* rstat, const void* dout, float* dWh, float* ds_src, int n, int K,
-                                      int Fh, int wbf, hipStream_t st) {
-  const int HF = K * Fh;
-  const float4* rs = reinterpret_cast<const float4*>(rstat);
-  if (wbf) GAT_DISPATCH(gat_bwd_col_kernel, 1, rowptr_t, col_t, Wh, s_src, rs, dout, dWh, ds_src, n, K, HF);
-  GAT_DISPATCH(gat_bwd_col_kernel, 0, rowptr_t, col_t, Wh, s_src, rs, dout, dWh, ds_src, n, K, HF);
+  const bool lead = f0 % (8 * G) == 0;
+  if (a.dy) {
+    *reinterpret_cast<uint4*>(a.dy + (size_t)row * a.ldy + f0) = f8_bf16(acc);
+    if (lead) a.dy[(size_t)row * a.ldy + HF + k] = (uint16_t)bf16u(dss);
+  } else {
+    st8(a.dWh + (size_t)row * HF + f0, acc);
+    if (lead) a.ds_src[(size_t)row * K + k] = dss;
+  }
 }
 
 // ============================================================================
@@ -370,9 +510,8 @@ extern "C" int gnn_launch_gat_bwd_col(const int* rowptr_t, const int* col_t, con
 // [Wh | s_src | s_dst] = h [W | W a_src | W a_dst] run on the MFMA lin_* kernels
 // (gnn_linear.hip); these cover everything between them and the aggregation:
 //
-//   gat_act_fwd     h = bf16(dropout(elu(out + b)))        (hidden layer output)
-//   gat_act_bwd     dout = dh * mask * elu'(out + b), fp32 + bf16 copy, and the
-//                   bias gradient as per-block column partials
+//   (the hidden activation and its backward are fused into gat_fwd_kernel and
+//   gat_row_kernel above)
 //   gat_row_ce      logits = out + b: log-softmax, NLL, accuracy counts, and
 //                   dlogits (train rows; zero elsewhere), per-wave partials of the
 //                   loss statistics and of the bias gradient
@@ -385,106 +524,10 @@ extern "C" int gnn_launch_gat_bwd_col(const int* rowptr_t, const int* col_t, con
 // keyed (row0 + row, 2t + h, step), byte (i + 4g) of it, kept if >= thr8.
 // ============================================================================
 namespace {
-__device__ __forceinline__ uint32_t bf16u(float x) { return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)x); }
 __device__ __forceinline__ uint2 pack4bf(const float* v) {
   return make_uint2(bf16u(v[0]) | (bf16u(v[1]) << 16), bf16u(v[2]) | (bf16u(v[3]) << 16));
 }
-__device__ __forceinline__ void dropout_words(uint32_t* w, uint32_t thr8, uint32_t grow, int t, int h,
-                                              uint32_t step, uint32_t k0, uint32_t k1) {
-  w[0] = w[1] = w[2] = w[3] = 0xffffffffu;
-  if (thr8 > 0) {
-    const u32x4 r = philox4x32_10(u32x4{grow, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
-    w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
-  }
-}
-__device__ __forceinline__ bool kept(const uint32_t* w, int q, uint32_t thr8) {
-  return thr8 == 0 || ((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8;
-}
 }  // namespace
-
-__global__ __launch_bounds__(256) void gat_act_fwd_kernel(const float* __restrict__ out, const float* __restrict__ bias,
-                                                          uint16_t* __restrict__ H, int ldh, long n, int F, float p,
-                                                          uint32_t k0, uint32_t k1, uint32_t step,
-                                                          const int* __restrict__ stepp, uint32_t thr8, uint32_t row0) {
-  if (stepp) step = (uint32_t)*stepp;
-  const int tpr = F / 16;
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long row = gid / tpr;
-  if (row >= n) return;
-  const int k = (int)(gid - row * tpr), t = k >> 1, h = k & 1;
-  const float scale = thr8 > 0 ? 1.f / (1.f - p) : 1.f;
-  uint32_t w[4];
-  dropout_words(w, thr8, row0 + (uint32_t)row, t, h, step, k0, k1);
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int c0 = 32 * t + 8 * g + 4 * h;
-    const float4 o = *reinterpret_cast<const float4*>(out + (size_t)row * F + c0);
-    const float ov[4] = {o.x, o.y, o.z, o.w};
-    float v[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float z = ov[i] + bias[c0 + i];
-      const float e = z > 0.f ? z : expm1f(z);
-      v[i] = kept(w, i + 4 * g, thr8) ? e * scale : 0.f;
-    }
-    *reinterpret_cast<uint2*>(H + (size_t)row * ldh + c0) = pack4bf(v);
-  }
-}
-
-// grid-stride over rows with a fixed grid: thread slot k = tid % (F/16) is constant,
-// so every thread keeps the bias-gradient sums of its 16 columns in registers;
-// blocks write [gridDim.x][F] partials (rows of a block summed in a fixed order)
-__global__ __launch_bounds__(256) void gat_act_bwd_kernel(const uint16_t* __restrict__ dH, int ldh,
-                                                          const float* __restrict__ out, const float* __restrict__ bias,
-                                                          float* __restrict__ dout, uint16_t* __restrict__ doutb,
-                                                          float* __restrict__ bpart, long n, int F, float p, uint32_t k0,
-                                                          uint32_t k1, uint32_t step, const int* __restrict__ stepp,
-                                                          uint32_t thr8, uint32_t row0) {
-  __shared__ float red[256][17];
-  if (stepp) step = (uint32_t)*stepp;
-  const int tpr = F / 16, rpb = 256 / tpr;
-  const int rl = threadIdx.x / tpr, k = threadIdx.x - rl * tpr, t = k >> 1, h = k & 1;
-  const float scale = thr8 > 0 ? 1.f / (1.f - p) : 1.f;
-  float bs[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) bs[q] = 0.f;
-  if (rl < rpb) {
-    for (long row = (long)blockIdx.x * rpb + rl; row < n; row += (long)gridDim.x * rpb) {
-      uint32_t w[4];
-      dropout_words(w, thr8, row0 + (uint32_t)row, t, h, step, k0, k1);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c0 = 32 * t + 8 * g + 4 * h;
-        const float4 o = *reinterpret_cast<const float4*>(out + (size_t)row * F + c0);
-        const uint2 hv = *reinterpret_cast<const uint2*>(dH + (size_t)row * ldh + c0);
-        const float ov[4] = {o.x, o.y, o.z, o.w};
-        const float gv[4] = {__uint_as_float(hv.x << 16), __uint_as_float(hv.x & 0xffff0000u),
-                             __uint_as_float(hv.y << 16), __uint_as_float(hv.y & 0xffff0000u)};
-        float d[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float z = ov[i] + bias[c0 + i];
-          d[i] = kept(w, i + 4 * g, thr8) ? gv[i] * scale * (z > 0.f ? 1.f : __expf(z)) : 0.f;
-          bs[4 * g + i] += d[i];
-        }
-        *reinterpret_cast<float4*>(dout + (size_t)row * F + c0) = make_float4(d[0], d[1], d[2], d[3]);
-        if (doutb) *reinterpret_cast<uint2*>(doutb + (size_t)row * F + c0) = pack4bf(d);
-      }
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) red[threadIdx.x][q] = bs[q];
-  __syncthreads();
-  if (threadIdx.x < tpr) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      float s = 0.f;
-      for (int r = 0; r < rpb; ++r) s += red[r * tpr + threadIdx.x][q];
-      const int c = 32 * t + 8 * (q >> 2) + 4 * h + (q & 3);
-      bpart[(size_t)blockIdx.x * F + c] = s;
-    }
-  }
-}
 
 // one wave per row (grid-stride, fixed grid); lane owns columns lane + 64 q, q < CP.
 // stats[wave][4] = (sum of train NLL, correct train, correct valid, correct test);
@@ -605,42 +648,15 @@ __global__ __launch_bounds__(256) void gat_colsum_kernel(const float* __restrict
 }
 
 namespace {
-int act_grid() {
+int row_ce_grid() {
   int dev = 0, cus = 256;
   hipDeviceProp_t prop;
   if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
   return 4 * cus;
 }
-uint32_t thr8_of(float p) { return (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5)); }
 }  // namespace
 
-extern "C" int gnn_launch_gat_act_fwd(const float* out, const float* bias, void* H, int ldh, long n, int F, float p,
-                                      uint32_t k0, uint32_t k1, uint32_t step, const int* stepp, uint32_t row0,
-                                      hipStream_t st) {
-  if (F % 32 || ldh < F || ldh % 4) return -3;
-  if (n <= 0) return 0;
-  const long threads = n * (F / 16);
-  hipLaunchKernelGGL(gat_act_fwd_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, out, bias,
-                     (uint16_t*)H, ldh, n, F, p, k0, k1, step, stepp, thr8_of(p), row0);
-  return (int)hipGetLastError();
-}
-
-extern "C" int gnn_gat_act_bwd_blocks() { return act_grid(); }
-
-// bpart: [gnn_gat_act_bwd_blocks()][F] fp32 scratch; db (optional): [F]
-extern "C" int gnn_launch_gat_act_bwd(const void* dH, int ldh, const float* out, const float* bias, float* dout,
-                                      void* doutb, float* bpart, float* db, long n, int F, float p, uint32_t k0,
-                                      uint32_t k1, uint32_t step, const int* stepp, uint32_t row0, hipStream_t st) {
-  if (F % 32 || F > 4096 || ldh < F || ldh % 4) return -3;
-  const int nb = act_grid();
-  hipLaunchKernelGGL(gat_act_bwd_kernel, dim3(nb), dim3(256), 0, st, (const uint16_t*)dH, ldh, out, bias, dout,
-                     (uint16_t*)doutb, bpart, n, F, p, k0, k1, step, stepp, thr8_of(p), row0);
-  if (db)
-    hipLaunchKernelGGL(gat_colsum_kernel, dim3((F + 31) / 32), dim3(256), 0, st, bpart, (long)nb, F, 1.f, db);
-  return (int)hipGetLastError();
-}
-
-extern "C" int gnn_gat_row_ce_waves() { return 4 * act_grid(); }
+extern "C" int gnn_gat_row_ce_waves() { return 4 * row_ce_grid(); }
 
 // stats_part: [waves][4], bpart: [waves][C] scratch; stats (optional): [4] (sums);
 // db (optional): [C]; dZ / dZb (optional, training): [n][ldz] fp32 / bf16
@@ -648,7 +664,7 @@ extern "C" int gnn_launch_gat_row_ce(const float* Z, int ldz, const float* bias,
                                      const uint8_t* mask, float inv_count, float* dZ, void* dZb, float* stats_part,
                                      float* bpart, float* stats, float* db, long n, hipStream_t st) {
   if (C <= 0 || C > 256 || ldz < C) return -3;
-  const int nb = act_grid(), nw = 4 * nb;
+  const int nb = row_ce_grid(), nw = 4 * nb;
   const int cp = (C + 63) / 64;
   float* bp = (dZ || dZb) ? bpart : nullptr;
   auto zb = (uint16_t*)dZb;
@@ -670,5 +686,131 @@ extern "C" int gnn_launch_gat_pack_grad(const float* dWh, const float* ds_src, c
   const long threads = n * (ldy / 4);
   hipLaunchKernelGGL(gat_pack_grad_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, dWh, ds_src,
                      ds_dst, HF, K, (uint16_t*)dy, ldy, n);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------- launchers
+namespace {
+int lanes_for(int HF) {
+  const int c = (HF + 7) / 8;
+  return c <= 8 ? 8 : c <= 16 ? 16 : c <= 32 ? 32 : c <= 64 ? 64 : -1;
+}
+}  // namespace
+
+// edges per gather batch: 4 (measured on the products epoch: 12.73 ms at 4, 13.0 at 8,
+// 14.4 at 16 -- a wider batch costs more occupancy than its rows in flight buy;
+// A/B with -DCGNN_GAT_EC=N)
+#ifndef CGNN_GAT_EC
+#define CGNN_GAT_EC 4
+#endif
+#define GAT_EC_OF(L) ((L) < CGNN_GAT_EC ? (L) : CGNN_GAT_EC)
+
+#define GAT_SWITCH(LAUNCH)                                                                  \
+  switch (L * 100 + G) {                                                                   \
+    case 801: LAUNCH(8, 1); break;                                                         \
+    case 802: LAUNCH(8, 2); break;                                                         \
+    case 804: LAUNCH(8, 4); break;                                                         \
+    case 808: LAUNCH(8, 8); break;                                                         \
+    case 1601: LAUNCH(16, 1); break;                                                       \
+    case 1602: LAUNCH(16, 2); break;                                                       \
+    case 1604: LAUNCH(16, 4); break;                                                       \
+    case 1608: LAUNCH(16, 8); break;                                                       \
+    case 1616: LAUNCH(16, 16); break;                                                      \
+    case 3202: LAUNCH(32, 2); break;                                                       \
+    case 3204: LAUNCH(32, 4); break;                                                       \
+    case 3208: LAUNCH(32, 8); break;                                                       \
+    case 3216: LAUNCH(32, 16); break;                                                      \
+    case 3232: LAUNCH(32, 32); break;                                                      \
+    case 6404: LAUNCH(64, 4); break;                                                       \
+    case 6408: LAUNCH(64, 8); break;                                                       \
+    case 6416: LAUNCH(64, 16); break;                                                      \
+    case 6464: LAUNCH(64, 64); break;                                                      \
+    default: return -1;                                                                    \
+  }
+
+// geometry shared by the launchers: one head -> its group is the row's whole sub-group
+#define GAT_GEOM                                                                            \
+  const int HF = K * Fh;                                                                   \
+  const int L = lanes_for(HF), G = K == 1 ? L : Fh / 8;                                    \
+  if (L < 0 || Fh % 8 || (K > 1 && (G & (G - 1)))) return -3;                              \
+  const int rpb = 4 * (64 / L);
+
+namespace {
+uint32_t thr8_of(float p) { return (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5)); }
+int act_grid() {
+  int dev = 0, cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+  return 4 * cus;
+}
+}  // namespace
+
+// Wh [n_cols][HF] (wbf: bf16, else fp32), s_src [n_cols][K], s_dst [*][K] (row dst_rows[i]
+// or i); out [n][HF] fp32, lse [n][K]; q (optional, training) [n][HF] like Wh; H
+// (optional) the fused hidden activation bf16(dropout(elu(out + bias))) with stride ldh.
+extern "C" int gnn_launch_gat_fwd(const int* rowptr, const int* col, const void* Wh, const float* s_src,
+                                  const float* s_dst, const int* dst_rows, float* out, float* lse, void* q, int n,
+                                  int K, int Fh, int wbf, const float* bias, void* H, int ldh, float p, uint32_t k0,
+                                  uint32_t k1, uint32_t step, const int* stepp, uint32_t row0, hipStream_t st) {
+  GAT_GEOM
+  if (H && (HF % 32 || ldh < HF || !bias)) return -3;
+  if (n <= 0) return 0;
+  GatFwdArgs a{rowptr, col, Wh, s_src, s_dst, dst_rows, out, lse, q, bias, (uint16_t*)H, ldh, p, k0, k1, step,
+               H ? thr8_of(p) : 0u, row0, stepp, n, K, HF};
+  dim3 grid((n + rpb - 1) / rpb), block(256);
+#define FWD(l, g)                                                                                     \
+  if (wbf) hipLaunchKernelGGL((gat_fwd_kernel<l, g, 1, GAT_EC_OF(l)>), grid, block, 0, st, a);        \
+  else hipLaunchKernelGGL((gat_fwd_kernel<l, g, 0, GAT_EC_OF(l)>), grid, block, 0, st, a)
+  GAT_SWITCH(FWD)
+#undef FWD
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_gat_row_blocks() { return act_grid(); }
+
+// act == 0: dout (wbf ? bf16 : fp32) given.  act == 1: dH (bf16, stride ldh) given,
+// dout = dH * mask * elu'(out + bias) written to dout_w (wbf ? bf16 : fp32), bias partials
+// to bpart [gnn_gat_row_blocks()][HF], db (optional) their fixed-order column sum.
+extern "C" int gnn_launch_gat_rows(int act, const void* dout, int ldh, const float* out, const void* q,
+                                   const float* lse, const float* s_dst, const int* dst_rows, float* rstat,
+                                   float* ds_dst, void* dy, int ldy, void* dout_w, const float* bias, float* bpart,
+                                   float* db, float p, uint32_t k0, uint32_t k1, uint32_t step, const int* stepp,
+                                   uint32_t row0, int n, int K, int Fh, int wbf, hipStream_t st) {
+  GAT_GEOM
+  (void)rpb;
+  if (act && (HF % 32 || !bias || !bpart || !dout_w)) return -3;
+  const int nb = act_grid();
+  GatRowArgs a{dout, ldh, out, q, lse, s_dst, dst_rows, reinterpret_cast<float4*>(rstat), ds_dst, (uint16_t*)dy,
+               ldy, dout_w, bias, bpart, p, k0, k1, step, act ? thr8_of(p) : 0u, row0, stepp, n, K, HF};
+#define ROWS(l, g)                                                                                              \
+  if (act) {                                                                                                    \
+    if (wbf) hipLaunchKernelGGL((gat_row_kernel<l, g, 1, true>), dim3(nb), dim3(256), 0, st, a);                \
+    else hipLaunchKernelGGL((gat_row_kernel<l, g, 0, true>), dim3(nb), dim3(256), 0, st, a);                    \
+  } else {                                                                                                      \
+    if (wbf) hipLaunchKernelGGL((gat_row_kernel<l, g, 1, false>), dim3(nb), dim3(256), 0, st, a);               \
+    else hipLaunchKernelGGL((gat_row_kernel<l, g, 0, false>), dim3(nb), dim3(256), 0, st, a);                   \
+  }
+  GAT_SWITCH(ROWS)
+#undef ROWS
+  if (act && db) hipLaunchKernelGGL(gat_colsum_kernel, dim3((HF + 31) / 32), dim3(256), 0, st, bpart, (long)nb, HF, 1.f, db);
+  return (int)hipGetLastError();
+}
+
+// Wh / s_src / dWh / ds_src / dy: rows of the launch's source range; rstat / dout: all
+// destination rows.  dy given: bf16 [dWh | ds_src] into its columns [0, HF + K).
+extern "C" int gnn_launch_gat_col(const int* rowptr_t, const int* col_t, const void* Wh, const float* s_src,
+                                  const float* rstat, const void* dout, float* dWh, float* ds_src, void* dy, int ldy,
+                                  int n, int K, int Fh, int wbf, hipStream_t st) {
+  GAT_GEOM
+  if (dy && ldy < HF + 2 * K) return -3;
+  if (n <= 0) return 0;
+  GatColArgs a{rowptr_t, col_t, Wh, s_src, reinterpret_cast<const float4*>(rstat), dout, dWh, ds_src,
+               (uint16_t*)dy, ldy, n, K, HF};
+  dim3 grid((n + rpb - 1) / rpb), block(256);
+#define COL(l, g)                                                                                     \
+  if (wbf) hipLaunchKernelGGL((gat_col_kernel<l, g, 1, GAT_EC_OF(l)>), grid, block, 0, st, a);        \
+  else hipLaunchKernelGGL((gat_col_kernel<l, g, 0, GAT_EC_OF(l)>), grid, block, 0, st, a)
+  GAT_SWITCH(COL)
+#undef COL
   return (int)hipGetLastError();
 }

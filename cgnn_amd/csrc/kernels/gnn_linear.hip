@@ -42,6 +42,7 @@ using namespace cgnn;
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int TILE = 32;
@@ -61,6 +62,26 @@ __device__ __forceinline__ float bf16_val(uint32_t bits16) { return __uint_as_fl
 __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
   return make_uint2((uint32_t)bf16_bits(a) | ((uint32_t)bf16_bits(b) << 16),
                     (uint32_t)bf16_bits(c) | ((uint32_t)bf16_bits(d) << 16));
+}
+
+// element type ET of the 16-bit operands: 0 = bf16 (training storage), 1 = fp16 (the
+// fp16 inference path)
+__device__ __forceinline__ uint16_t f16_bits(float x) { return __builtin_bit_cast(uint16_t, (_Float16)x); }
+template <int ET>
+__device__ __forceinline__ uint16_t e16_bits(float x) { return ET == 1 ? f16_bits(x) : bf16_bits(x); }
+template <int ET>
+__device__ __forceinline__ uint2 pack4e(float a, float b, float c, float d) {
+  return make_uint2((uint32_t)e16_bits<ET>(a) | ((uint32_t)e16_bits<ET>(b) << 16),
+                    (uint32_t)e16_bits<ET>(c) | ((uint32_t)e16_bits<ET>(d) << 16));
+}
+template <int ET>
+__device__ __forceinline__ f32x16 mma16(uint4 a, uint4 b, f32x16 c) {
+  if constexpr (ET == 1)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, a), __builtin_bit_cast(f16x8v, b), c,
+                                                   0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                    0, 0, 0);
 }
 
 // zero the elements [valid, 8) of a bf16x8 chunk (padding columns may hold anything,
@@ -152,7 +173,7 @@ int device_cus() {
 // lin_fwd: Y[row][c] = epi(sum_k [X1 | X2][row][k] W[k][c] + b[c]) for the column
 // slab c in [blockIdx.y * ncols, +ncols); KS k-steps of 16 cover K1 + K2.
 // ============================================================================
-template <int KS, int FWD_WAVES = FwdWaves<KS>::value>
+template <int KS, int ET = 0, int FWD_WAVES = FwdWaves<KS>::value>
 __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     const uint16_t* __restrict__ x1, int ld1, int K1, const uint16_t* __restrict__ x2, int ld2, int K2,
     const float* __restrict__ W, int N, const float* __restrict__ bias, uint16_t* __restrict__ Y, int ldy,
@@ -189,10 +210,10 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
   for (int tile = wave; tile < n_tiles; tile += n_waves) {
     const int row = tile * TILE + lr;
     const bool rv = row < n;
-    bf16x8 bx[KS];
+    uint4 bx[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      bx[s] = as_bf16x8(rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h, idx1) : make_uint4(0u, 0u, 0u, 0u));
+      bx[s] = rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h, idx1) : make_uint4(0u, 0u, 0u, 0u);
     const float rs = (rv && rscale) ? rscale[row] : 1.f;
 #pragma unroll 1
     for (int t = 0; t < nt; ++t) {
@@ -200,8 +221,7 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
       const uint16_t* arow = sWT + (32 * t + lr) * WS + 8 * h;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(*reinterpret_cast<const uint4*>(arow + 16 * s)),
-                                                      bx[s], acc, 0, 0, 0);
+        acc = mma16<ET>(*reinterpret_cast<const uint4*>(arow + 16 * s), bx[s], acc);
       if (!rv) continue;
       const int cg = c0 + 32 * t;                // global column of this tile
       uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
@@ -229,7 +249,8 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
             if (c + e < N) Yf[(size_t)(t / tk) * n * tk + (size_t)row * tk + t % tk] = v[4 * g + e];
           }
         } else if (c < ldy) {
-          *reinterpret_cast<uint2*>(Y + (size_t)row * ldy + c) = pack4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+          *reinterpret_cast<uint2*>(Y + (size_t)row * ldy + c) =
+              pack4e<ET>(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
         }
       }
     }
@@ -462,6 +483,7 @@ __global__ __launch_bounds__(256) void lin_reduce_kernel(const float* __restrict
 //   fwd: img[slab][c][k]  = W[k][slab * ncols + c]   (W^T, row stride WS = KP + 8)
 //   bwd: img[slab][kk][c] = W[slab * kcols + kk][c]  (W rows, row stride WS = NP + 8)
 // zero outside the matrix and in the pad columns
+template <int ET>
 __global__ __launch_bounds__(256) void lin_prep_fwd_kernel(const float* __restrict__ W, int K, int N, int ncols,
                                                            int KP, int WS, long total, uint16_t* __restrict__ img) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -469,7 +491,7 @@ __global__ __launch_bounds__(256) void lin_prep_fwd_kernel(const float* __restri
   const int k = (int)(i % WS);
   const long rc = i / WS;                       // slab * ncols + c = global column
   const int c = (int)rc;
-  img[i] = bf16_bits(k < K && k < KP && c < N ? W[(size_t)k * N + c] : 0.f);
+  img[i] = e16_bits<ET>(k < K && k < KP && c < N ? W[(size_t)k * N + c] : 0.f);
 }
 
 __global__ __launch_bounds__(256) void lin_prep_bwd_kernel(const float* __restrict__ W, int K, int N, int NP, int WS,
@@ -489,7 +511,7 @@ static int grid_rows(int n, int waves) {
 
 static int pick_ks(int K) {
   const int ks = (K + 15) / 16;
-  for (int c : {4, 8, 16, 24, 32}) if (ks <= c) return c;
+  for (int c : {4, 8, 16, 24, 32, 40, 48}) if (ks <= c) return c;
   return -1;
 }
 
@@ -503,7 +525,7 @@ static int slab_cols(int N, int KP) {
 
 
 
-template <int KS>
+template <int KS, int ET>
 static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const float* W, int N,
                       const float* bias, uint16_t* Y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1,
                       uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
@@ -515,21 +537,23 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
   {
     const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
     const long total = (long)slabs * ncols * (KP + 8);
-    hipLaunchKernelGGL(lin_prep_fwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2, N,
-                       ncols, KP, KP + 8, total, wimg);
+    hipLaunchKernelGGL(lin_prep_fwd_kernel<ET>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2,
+                       N, ncols, KP, KP + 8, total, wimg);
   }
-  (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS, ET>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
-  hipLaunchKernelGGL((lin_fwd_kernel<KS>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
+  hipLaunchKernelGGL((lin_fwd_kernel<KS, ET>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
                      x1, ld1, K1, x2, ld2, K2, W, N, bias, Y, ldy, n, ncols, relu, p, k0, k1, step, thr8, row0,
                      stepp, rscale, idx1, wimg, Yf, nsplit, tk);
   return (int)hipGetLastError();
 }
 
+// et: element type of X / Y (0 bf16, 1 fp16: the inference path; fp16 takes K <= 768,
+// no dropout or fp32 tail)
 extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2, const float* W,
                                   int N, const float* bias, void* Y, int ldy, int n, int relu, float p, uint32_t k0,
                                   uint32_t k1, uint32_t step, uint32_t row0, const int* stepp, const float* rscale,
-                                  const int* idx1, void* wimg, float* Yf, int nsplit, int tk, hipStream_t st) {
+                                  const int* idx1, void* wimg, float* Yf, int nsplit, int tk, hipStream_t st, int et) {
   if (n <= 0) return 0;
   if ((x2 && K1 % 8) || ld1 % 8 || (x2 && (ld2 % 8)) || ldy % 8 || K1 > ld1 || (x2 && K2 > ld2))
     return -3;
@@ -540,7 +564,14 @@ extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x
   auto a = (const uint16_t*)x1;
   auto b = (const uint16_t*)x2;
   auto y = (uint16_t*)Y;
-#define LF(c) if (ks == c) return fwd_launch<c>(a, ld1, K1, b, ld2, K2, W, N, bias, y, ldy, n, relu, p, k0, k1, step, thr8, row0, stepp, rscale, idx1, (uint16_t*)wimg, Yf, nsplit, tk, st);
+  if (et == 1) {
+    if (thr8 || Yf) return -3;
+#define LH(c) if (ks == c) return fwd_launch<c, 1>(a, ld1, K1, b, ld2, K2, W, N, bias, y, ldy, n, relu, p, k0, k1, step, thr8, row0, stepp, rscale, idx1, (uint16_t*)wimg, Yf, nsplit, tk, st);
+    LH(4) LH(8) LH(16) LH(24) LH(32) LH(40) LH(48)
+#undef LH
+    return -1;
+  }
+#define LF(c) if (ks == c) return fwd_launch<c, 0>(a, ld1, K1, b, ld2, K2, W, N, bias, y, ldy, n, relu, p, k0, k1, step, thr8, row0, stepp, rscale, idx1, (uint16_t*)wimg, Yf, nsplit, tk, st);
   LF(4) LF(8) LF(16) LF(24) LF(32)
 #undef LF
   return -1;

@@ -75,7 +75,9 @@ __global__ __launch_bounds__(256) void mmd_mfma_kernel(
   // rows: generated samples [row_begin, row_begin + n_rows) (a sample-sharded
   // MMD owns a row range, columns are all N); gradient rows use stride n_rows.
   // MODE 0 train (loss + gradient), 1 eval (loss), 3 train without the loss
-  // (nobody reads the training loss unless a history is recorded)
+  // (nobody reads the training loss unless a history is recorded), 2 the constant
+  // true-true block (launched with xhat = data, xnorm = ynorm: the first column part
+  // only; used for the widths the vector kernel does not cover)
   constexpr bool GRAD = MODE == 0 || MODE == 3;
   constexpr bool LOSS = MODE != 3;
   constexpr int KP = (KD + 15) / 16 * 16;   // distance K padded to the MFMA k-step
@@ -120,12 +122,12 @@ __global__ __launch_bounds__(256) void mmd_mfma_kernel(
   }
 
   const int TX = (N + MT - 1) / MT;         // column tiles per part
-  const int ct = 2 * TX;
+  const int ct = MODE == 2 ? TX : 2 * TX;
   // evaluation over all rows: the pred-pred block is symmetric -- column tiles left of
   // this block's rows are skipped, the wave's own diagonal tile counts once, tiles
   // right of it twice (and tiles left of the wave inside the block's band not at all):
   // ~25 % fewer distances per evaluation step, geometry still fixed by N
-  const bool sym = MODE == 1 && row_begin == 0 && n_rows == N;
+  const bool sym = (MODE == 1 || MODE == 2) && row_begin == 0 && n_rows == N;
   const int wr = rb * WAVES + wave;         // this wave's row tile (in MT columns)
   int t_begin = chunk * tiles_per_chunk;
   const int t_end = min(ct, t_begin + tiles_per_chunk);
@@ -314,6 +316,8 @@ int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const floa
     hipLaunchKernelGGL((mmd_mfma_kernel<KD, 3>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
   else if (mode == 1)
     hipLaunchKernelGGL((mmd_mfma_kernel<KD, 1>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
+  else if (mode == 2)
+    hipLaunchKernelGGL((mmd_mfma_kernel<KD, 2>), grid, block, 0, st, data, data, yn, yn, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
   else
     return -3;
   return (int)hipGetLastError();
@@ -321,10 +325,12 @@ int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const floa
 
 }  // namespace
 
-// Supported widths (the padded D of engine/batch.py SUPPORTED_D, >= 8)
+// Supported widths (the padded D of engine/batch.py SUPPORTED_D, >= 8; above 64 the
+// matrix-core kernel is the only MMD)
 extern "C" int cgnn_mmd_mfma_supported(int D) {
   switch (D) {
-    case 8: case 12: case 16: case 20: case 24: case 32: case 48: case 64: return 1;
+    case 8: case 12: case 16: case 20: case 24: case 32: case 48: case 64:
+    case 80: case 96: case 128: case 160: case 192: case 224: case 256: return 1;
     default: return 0;
   }
 }
@@ -341,6 +347,7 @@ extern "C" int cgnn_launch_mmd_mfma_rows(int mode, int D, const float* xhat, con
   switch (D) {
 #define CASE_D(d) case d: return launch_mmd_mfma_d<d>(mode, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale, row_begin, n_rows, st);
     CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20) CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64)
+    CASE_D(80) CASE_D(96) CASE_D(128) CASE_D(160) CASE_D(192) CASE_D(224) CASE_D(256)
 #undef CASE_D
     default: return -1;
   }

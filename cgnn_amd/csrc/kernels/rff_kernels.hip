@@ -196,27 +196,26 @@ __global__ __launch_bounds__(512) void rff_mfma_feat_kernel(const float* __restr
 //   G[k][n] += sum_f W^T[k][f] S'[f][n]            (k-step q takes register q of every
 //                                                    lane as B: f = (q&3) + 8(q>>2) + 4(l/32)
 //                                                    -- the accumulator IS the operand)
-// W of the model is staged in LDS once per block.
+// W of the model is staged in LDS, FC features at a time (the whole [F][D + 1] matrix for
+// narrow joints; chunks of it for wide ones -- the f order of the accumulation is the
+// same either way).
 template <int D>
 __global__ __launch_bounds__(256) void rff_mfma_grad_kernel(const float* __restrict__ xhat,
                                                             const float* __restrict__ W,
                                                             const float* __restrict__ diff,
                                                             float* __restrict__ grad, int N, int F,
-                                                            float coef) {
+                                                            float coef, int FC) {
   constexpr int KS = (D + 2) / 2;
   constexpr int DT = (D + 31) / 32;        // 32-row tiles of the gradient's k (feature dim)
   constexpr int WS = D + 1;
   typedef float f32x16 __attribute__((ext_vector_type(16)));
-  extern __shared__ float sW[];            // [F][WS] then diff [F]
-  float* sD = sW + (size_t)F * WS;
+  extern __shared__ float sW[];            // [FC][WS] then diff [FC]
+  float* sD = sW + (size_t)FC * WS;
   const int r = blockIdx.y;
   const float* Wr = W + (size_t)r * F * WS;
-  for (int i = threadIdx.x; i < F * WS; i += blockDim.x) sW[i] = Wr[i];
-  for (int i = threadIdx.x; i < F; i += blockDim.x) sD[i] = -coef * diff[(size_t)r * F + i];
-  __syncthreads();
   const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31, wv = threadIdx.x >> 6;
   const int n0 = (blockIdx.x * 4 + wv) * 32;
-  if (n0 >= N) return;                      // after the only barrier
+  const bool active = n0 < N;               // waves past N still join every barrier
   const int n = n0 + lr;
   const float* X = xhat + (size_t)r * D * N;
   float xb[KS];                             // B of the first product: [x | 1][k = 2s + h][n]
@@ -228,32 +227,40 @@ __global__ __launch_bounds__(256) void rff_mfma_grad_kernel(const float* __restr
   f32x16 g[DT];
 #pragma unroll
   for (int t = 0; t < DT; ++t) g[t] = f32x16{};
-  for (int f0 = 0; f0 < F; f0 += 32) {
-    const int fa = f0 + lr;                 // this lane's A row of the first product
-    f32x16 c = {};
+  for (int fc0 = 0; fc0 < F; fc0 += FC) {
+    const int fcn = min(FC, F - fc0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < fcn * WS; i += blockDim.x) sW[i] = Wr[(size_t)fc0 * WS + i];
+    for (int i = threadIdx.x; i < fcn; i += blockDim.x) sD[i] = -coef * diff[(size_t)r * F + fc0 + i];
+    __syncthreads();
+    if (!active) continue;
+    for (int f0 = 0; f0 < fcn; f0 += 32) {
+      const int fa = f0 + lr;               // this lane's A row of the first product (chunk-local)
+      f32x16 c = {};
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int k = 2 * s + h;
-      const float a = (fa < F && k <= D) ? sW[fa * WS + k] : 0.f;
-      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xb[s], c, 0, 0, 0);
-    }
+      for (int s = 0; s < KS; ++s) {
+        const int k = 2 * s + h;
+        const float a = (fa < fcn && k <= D) ? sW[fa * WS + k] : 0.f;
+        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xb[s], c, 0, 0, 0);
+      }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int ff = f0 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      c[q] = ff < F ? sD[ff] * sin_rev(c[q]) : 0.f;
-    }
+      for (int q = 0; q < 16; ++q) {
+        const int ff = f0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        c[q] = ff < fcn ? sD[ff] * sin_rev(c[q]) : 0.f;
+      }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int ff = f0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      for (int q = 0; q < 16; ++q) {
+        const int ff = f0 + (q & 3) + 8 * (q >> 2) + 4 * h;
 #pragma unroll
-      for (int t = 0; t < DT; ++t) {
-        const int k = 32 * t + lr;
-        const float a = (ff < F && k < D) ? sW[ff * WS + k] : 0.f;
-        g[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, c[q], g[t], 0, 0, 0);
+        for (int t = 0; t < DT; ++t) {
+          const int k = 32 * t + lr;
+          const float a = (ff < fcn && k < D) ? sW[ff * WS + k] : 0.f;
+          g[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, c[q], g[t], 0, 0, 0);
+        }
       }
     }
   }
-  if (n >= N) return;
+  if (!active || n >= N) return;
   float* gr = grad + (size_t)r * D * N;
 #pragma unroll
   for (int t = 0; t < DT; ++t)
@@ -285,26 +292,35 @@ template <int D>
 static int rff_fb_d(int mode, const float* xhat, const float* data, const float* W, float* diff,
                     float* loss_part, float* grad, int N, int F, int R, int k, float norm,
                     hipStream_t st) {
-  const size_t glds = sizeof(float) * ((size_t)F * (D + 1) + F);
-  if (D >= rff_mfma_min_d() && glds <= 160 * 1024) {
+  // features staged per chunk of the gradient kernel: all of them when [F][D + 1] fits
+  // in 160 KiB, else the largest multiple of 32 that does
+  const size_t cap = 160 * 1024 / sizeof(float);
+  const bool whole = (size_t)F * (D + 2) <= cap;
+  const int FC = whole ? F : (int)(cap / (D + 2)) / 32 * 32;
+  if (D > 64 || (D >= rff_mfma_min_d() && whole)) {    // the vector kernels stop at D = 64
+    if (FC < 32) return -2;
+    const size_t glds = sizeof(float) * (size_t)FC * (D + 2);
     hipLaunchKernelGGL((rff_mfma_feat_kernel<D>), dim3((F + 255) / 256, R), dim3(512), 0, st, xhat, data, W, diff,
                        loss_part, N, F, norm);
     if (mode == 0) {
       (void)hipFuncSetAttribute((const void*)rff_mfma_grad_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)glds);
       hipLaunchKernelGGL((rff_mfma_grad_kernel<D>), dim3((N + 127) / 128, R), dim3(256), glds, st, xhat, W, diff,
-                         grad, N, F, 2.f * norm / (float)N);
+                         grad, N, F, 2.f * norm / (float)N, FC);
     }
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL((rff_feat_kernel<D>), dim3((F + 255) / 256, R), dim3(256), 0, st, xhat, data,
-                     W, diff, loss_part, N, F, norm);
-  if (mode == 0) {
-    const float coef = 2.f * norm / (float)N;
-    hipLaunchKernelGGL((rff_grad_kernel<D>), dim3((N + 255) / 256, R), dim3(256), 0, st, xhat, W,
-                       diff, grad, N, F, coef);
+  if constexpr (D <= 64) {
+    hipLaunchKernelGGL((rff_feat_kernel<D>), dim3((F + 255) / 256, R), dim3(256), 0, st, xhat, data,
+                       W, diff, loss_part, N, F, norm);
+    if (mode == 0) {
+      const float coef = 2.f * norm / (float)N;
+      hipLaunchKernelGGL((rff_grad_kernel<D>), dim3((N + 255) / 256, R), dim3(256), 0, st, xhat, W,
+                         diff, grad, N, F, coef);
+    }
+    return (int)hipGetLastError();
   }
-  return (int)hipGetLastError();
+  return -1;
 }
 
 // mode 0: loss partials + gradient; mode 1: loss partials only.
@@ -314,7 +330,8 @@ extern "C" int rff_launch_fwd_bwd(int mode, const float* xhat, const float* data
   switch (D) {
 #define CASE_D(d) case d: return rff_fb_d<d>(mode, xhat, data, W, diff, loss_part, grad, N, F, R, k, norm, st);
     CASE_D(1) CASE_D(2) CASE_D(3) CASE_D(4) CASE_D(6) CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20)
-    CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64)
+    CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64) CASE_D(80) CASE_D(96) CASE_D(128) CASE_D(160) CASE_D(192)
+    CASE_D(224) CASE_D(256)
 #undef CASE_D
     default: return -1;
   }

@@ -17,7 +17,9 @@ import torch
 from .. import native
 from .program import Program, pack_programs
 
-SUPPORTED_D = (1, 2, 3, 4, 6, 8, 12, 16, 20, 24, 32, 48, 64)
+# padded variable counts with compiled kernels; above 64 only the matrix-core MMD
+SUPPORTED_D = (1, 2, 3, 4, 6, 8, 12, 16, 20, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
+MAX_VALU_D = 64
 MMD_TILE = 256
 TARGET_WGS = 2048
 
@@ -66,10 +68,22 @@ def mmd_kernel_choice(D: int, mmd_kernel: str = "auto") -> str:
     if choice == "auto":
         choice = "mfma" if hip.mmd_mfma_supported(D) else "valu"
     if choice == "mfma" and not hip.mmd_mfma_supported(D):
-        raise ValueError("matrix-core MMD needs D in (8, 12, 16, 20, 24, 32, 48, 64), got %d" % D)
+        raise ValueError("matrix-core MMD needs a padded D >= 8 from engine.batch.SUPPORTED_D, got %d" % D)
+    if choice == "valu" and D > MAX_VALU_D:
+        raise ValueError("the vector MMD kernel covers D <= %d (got %d): use the matrix-core one" % (MAX_VALU_D, D))
     if choice not in ("mfma", "valu"):
         raise ValueError("mmd_kernel must be auto|mfma|valu")
     return choice
+
+
+def device_supported(d: int, H: int, max_in: int) -> bool:
+    """True when the device kernels cover a batch of ``d``-variable programs with hidden
+    width ``H`` and at most ``max_in`` generator inputs per node (the variable count up
+    to SUPPORTED_D[-1]; any H whose generator backward fits in LDS).  Otherwise
+    ``score_jobs`` trains the batch on the CPU reference path (with a warning)."""
+    if d > SUPPORTED_D[-1]:
+        return False
+    return native.hip().gen_bwd_variant(int(H), int(max_in), int(d), 0) != 0
 
 
 def _keys_tensor(keys, device):
@@ -86,8 +100,6 @@ class DeviceTrainer:
                  mmd_kernel="auto"):
         hip = native.hip()
         self.hip = hip
-        if not hip.gen_supported_h(int(H)):
-            raise native.NativeExtensionError("h_layer_dim=%d has no compiled generator kernel" % H)
         self.device = torch.device(device)
         R = len(programs)
         d = programs[0].n_vars
@@ -100,6 +112,10 @@ class DeviceTrainer:
         self.R, self.N, self.d, self.D, self.H = R, N, d, D, int(H)
         prog, stride, P, max_in = pack_programs(programs)
         self.P = P
+        self.bwd_variant = hip.gen_bwd_variant(int(H), int(max_in), int(d), int(stride))
+        if self.bwd_variant == 0:
+            raise native.NativeExtensionError(
+                "generator backward: H=%d with %d inputs per node does not fit in LDS" % (H, max_in))
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         with torch.cuda.device(dev):
@@ -138,6 +154,8 @@ class DeviceTrainer:
             # squared row norms for the Gram-form (matrix-core) MMD
             self.xnorm = torch.zeros(R, N, **f32)
             self.ynorm = (self.data * self.data).sum(1).contiguous()
+            # sample-gradient scratch of the generic-width generator backward
+            self.dxs = torch.zeros(R, d, N, **f32) if self.bwd_variant == 2 else None
             # a dedicated (non-default) stream: hipGraph capture is not allowed on
             # the legacy null stream, and batches on different devices overlap
             self.stream = torch.cuda.Stream(dev)
@@ -150,7 +168,8 @@ class DeviceTrainer:
                                            self.tt, self.loss_last, self.loss_acc)]
             ptrs.append(self.hist.data_ptr() if self.hist_len else 0)
             ptrs += [self.step.data_ptr(), self.keys.data_ptr(), self.rff_w.data_ptr(),
-                     self.rff_diff.data_ptr(), self.xnorm.data_ptr(), self.ynorm.data_ptr()]
+                     self.rff_diff.data_ptr(), self.xnorm.data_ptr(), self.ynorm.data_ptr(),
+                     self.dxs.data_ptr() if self.dxs is not None else 0]
             self.engine = hip.CgnnEngine(icfg, fcfg, ptrs, stream.cuda_stream)
         self.graph_chunk = int(graph_chunk)
 

@@ -38,9 +38,10 @@ class Job:
     key: tuple                    # Philox key of this model
 
 
-def subsample(mat: np.ndarray, max_points: int, seed: int, *salt) -> np.ndarray:
-    """Per-run random subsample of the rows of [N, d] data (CGNN.py:183-185)."""
-    if mat.shape[0] <= max_points:
+def subsample(mat: np.ndarray, max_points: Optional[int], seed: int, *salt) -> np.ndarray:
+    """Per-run random subsample of the rows of [N, d] data (CGNN.py:183-185);
+    ``max_points`` None keeps every row."""
+    if max_points is None or mat.shape[0] <= max_points:
         return mat
     perm = philox.numpy_rng(seed, "subsample", *salt).permutation(mat.shape[0])
     return mat[perm[:int(max_points)]]
@@ -71,6 +72,15 @@ def _group_batches(jobs: Sequence[Job], batch: int):
     return out
 
 
+def _run_reference(jobs: Sequence[Job], idx, cfg) -> np.ndarray:
+    from .reference import ReferenceTrainer
+    tr = ReferenceTrainer([jobs[i].program for i in idx], [jobs[i].data for i in idx],
+                          [jobs[i].key for i in idx], cfg.h_layer_dim,
+                          learning_rate=cfg.learning_rate, init_std=cfg.init_std,
+                          use_fast_mmd=cfg.use_Fast_MMD, nb_vectors=cfg.nb_vectors_approx_MMD)
+    return tr.run(cfg.train_epochs, cfg.test_epochs, verbose=cfg.verbose)
+
+
 def _run_local(jobs: Sequence[Job], cfg) -> np.ndarray:
     import torch
     n = len(jobs)
@@ -80,8 +90,21 @@ def _run_local(jobs: Sequence[Job], cfg) -> np.ndarray:
     devices = pdist.devices_for(cfg)
     t0 = time.perf_counter()
     if devices:
-        from .batch import DeviceTrainer
-        batches = _group_batches(jobs, max(1, cfg.batch_models))
+        from .batch import DeviceTrainer, device_supported
+        batches = []
+        for idx in _group_batches(jobs, max(1, cfg.batch_models)):
+            d = jobs[idx[0]].program.n_vars
+            max_in = max(jobs[i].program.max_in for i in idx)
+            if device_supported(d, cfg.h_layer_dim, max_in):
+                batches.append(idx)
+                continue
+            # a shape no device kernel covers (more variables than the widest compiled
+            # joint, or a generator whose backward does not fit in LDS): the CPU path
+            log.warning("CGNN batch of %d models (%d variables, h_layer_dim=%d, %d inputs per node) "
+                        "is outside the device kernels; training it on the CPU reference path",
+                        len(idx), d, cfg.h_layer_dim, max_in)
+            METRICS.record("cpu_fallback", models=len(idx), variables=d, h_layer_dim=cfg.h_layer_dim)
+            scores[idx] = _run_reference(jobs, idx, cfg)
         pending = []
         for b, idx in enumerate(batches):
             dev = devices[b % len(devices)]
@@ -104,17 +127,49 @@ def _run_local(jobs: Sequence[Job], cfg) -> np.ndarray:
                     for it in range(0, tr.hist_len, 100):
                         log.info('Run:%d, Iter:%d, score:%s', idx[r], it, h[r, it])
     else:
-        from .reference import ReferenceTrainer
         for idx in _group_batches(jobs, max(1, cfg.batch_models)):
-            tr = ReferenceTrainer([jobs[i].program for i in idx], [jobs[i].data for i in idx],
-                                  [jobs[i].key for i in idx], cfg.h_layer_dim,
-                                  learning_rate=cfg.learning_rate, init_std=cfg.init_std,
-                                  use_fast_mmd=cfg.use_Fast_MMD, nb_vectors=cfg.nb_vectors_approx_MMD)
-            scores[idx] = tr.run(cfg.train_epochs, cfg.test_epochs, verbose=cfg.verbose)
+            scores[idx] = _run_reference(jobs, idx, cfg)
     dt = time.perf_counter() - t0
     steps = n * (cfg.train_epochs + cfg.test_epochs)
     METRICS.record("score_jobs", models=n, seconds=dt, model_steps=steps,
                    steps_per_s=steps / dt if dt > 0 else 0.0, devices=len(devices) or 0)
+    return scores
+
+
+def is_long(job: Job, cfg) -> bool:
+    """Runs with more samples than ``cfg.long_n_min`` go to the sample-sharded trainer
+    (the Fourier MMD is O(N) per sample already and stays on the batched engine)."""
+    return (not cfg.use_Fast_MMD) and job.data.shape[1] > int(cfg.long_n_min)
+
+
+def _run_long(jobs: Sequence[Job], cfg) -> np.ndarray:
+    """Long-N jobs on ``engine.sharded.SampleShardedTrainer``: EVERY rank takes part in
+    every job, owning an equal block of its samples (the reference would subsample to
+    1500, CGNN.py:183-185); scores come back identical on all ranks.  N is trimmed to a
+    multiple of the rank count (at most world - 1 trailing samples, a warning)."""
+    import torch
+    from .sharded import SampleShardedTrainer, shard_range
+    n = len(jobs)
+    scores = np.full(n, np.nan)
+    world, rank = pdist.world_size(), pdist.rank()
+    devices = pdist.devices_for(cfg)
+    dev = devices[0] if devices else torch.device("cpu")
+    t0 = time.perf_counter()
+    for idx in _group_batches(jobs, max(1, cfg.batch_models)):
+        N = jobs[idx[0]].data.shape[1]
+        Nw = N - N % world
+        if Nw != N:
+            log.warning("long-N jobs: %d samples over %d ranks, the last %d are not used", N, world, N - Nw)
+        r0, nl = shard_range(Nw, rank, world)
+        tr = SampleShardedTrainer([jobs[i].program for i in idx],
+                                  [np.ascontiguousarray(jobs[i].data[:, r0:r0 + nl]) for i in idx],
+                                  [jobs[i].key for i in idx], cfg.h_layer_dim, dev, Nw,
+                                  learning_rate=cfg.learning_rate, init_std=cfg.init_std)
+        scores[idx] = tr.run(cfg.train_epochs, cfg.test_epochs)
+    dt = time.perf_counter() - t0
+    steps = n * (cfg.train_epochs + cfg.test_epochs)
+    METRICS.record("score_jobs_long_n", models=n, seconds=dt, model_steps=steps, ranks=world,
+                   steps_per_s=steps / dt if dt > 0 else 0.0)
     return scores
 
 
@@ -125,6 +180,33 @@ def score_jobs(jobs: Sequence[Job], cfg, max_retries: Optional[int] = None) -> n
 
 
 def _score_jobs(jobs: Sequence[Job], cfg, max_retries: int) -> np.ndarray:
+    long_idx = [i for i, j in enumerate(jobs) if is_long(j, cfg)]
+    if long_idx:
+        # long-N jobs: every rank trains every job on its block of samples
+        out = np.full(len(jobs), np.nan)
+        short_idx = [i for i in range(len(jobs)) if i not in set(long_idx)]
+        if short_idx:
+            out[short_idx] = _score_jobs([jobs[i] for i in short_idx], cfg, max_retries)
+        ls = _run_long([jobs[i] for i in long_idx], cfg)
+        faults = _fault_indices()
+        for k, i in enumerate(long_idx):
+            if i in faults:
+                ls[k] = np.nan
+        for attempt in range(max_retries):
+            bad = [k for k in range(len(long_idx)) if not np.isfinite(ls[k])]
+            if not bad:
+                break
+            retry = [Job(jobs[long_idx[k]].program, jobs[long_idx[k]].data,
+                         philox.model_key(jobs[long_idx[k]].key[0], jobs[long_idx[k]].key[1], "retry", attempt))
+                     for k in bad]
+            ls[bad] = _run_long(retry, cfg)
+            METRICS.record("retried_runs", attempt=attempt + 1, count=len(bad),
+                           recovered=int(np.isfinite(ls[bad]).sum()))
+        out[long_idx] = ls
+        dropped = int((~np.isfinite(ls)).sum())
+        if dropped:
+            METRICS.record("dropped_runs", count=dropped, total=len(long_idx))
+        return out
     n = len(jobs)
     idx = pdist.shard_indices(n)
     local = _run_local([jobs[i] for i in idx], cfg) if len(idx) else np.zeros(0)

@@ -103,13 +103,15 @@ class SampleShardedTrainer:
     def _init_device(self, datas_local, mmd_kernel):
         hip = native.hip()
         self.hip = hip
-        if not hip.gen_supported_h(self.H):
-            raise native.NativeExtensionError("h_layer_dim=%d has no compiled generator kernel" % self.H)
         R, d, n, N = self.R, self.d, self.n_loc, self.N
         D = padded_dim(d)
         self.D = D
         prog, stride, P, max_in = pack_programs(self.programs)
         self.P, self.stride, self.max_in = P, stride, max_in
+        variant = hip.gen_bwd_variant(int(self.H), int(max_in), int(d), int(stride))
+        if variant == 0:
+            raise native.NativeExtensionError(
+                "generator backward: H=%d with %d inputs per node does not fit in LDS" % (self.H, max_in))
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         self.prog = torch.from_numpy(prog).to(dev)
@@ -132,16 +134,24 @@ class SampleShardedTrainer:
         self.mgeo = _mfma_geometry(n, N, R)
         G = hip.gen_bwd_blocks(n)
         self.gpart = torch.zeros(R, G, P, **f32)
+        self.dxs = torch.zeros(R, d, n, **f32) if variant == 2 else None
         self.dnorm = (self.data_all * self.data_all).sum(1).contiguous()
         self.st = torch.cuda.current_stream(dev).cuda_stream
         hip.init_params(self.params.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.prog.data_ptr(), stride, P,
                         self.keys_t.data_ptr(), self.init_std, R, self.st)
         # constant true-true block of this rank's rows
-        rt, nc, tpc = self.vgeo
-        lp = torch.empty(R, rt * nc, **f32)
         dummy = torch.empty(1, **f32)
-        hip.mmd(2, D, self.data_all.data_ptr(), self.data_all.data_ptr(), dummy.data_ptr(), lp.data_ptr(), N, R, rt,
-                nc, tpc, 0.0, self.st, row_begin=self.row0, n_rows=n)
+        if hip.mmd_supported_d(D):
+            rt, nc, tpc = self.vgeo
+            lp = torch.empty(R, rt * nc, **f32)
+            hip.mmd(2, D, self.data_all.data_ptr(), self.data_all.data_ptr(), dummy.data_ptr(), lp.data_ptr(), N, R,
+                    rt, nc, tpc, 0.0, self.st, row_begin=self.row0, n_rows=n)
+        else:                         # wide joints: the matrix-core kernel's true-true mode
+            rb, nc, tpc = self.mgeo
+            lp = torch.empty(R, rb * nc, **f32)
+            hip.mmd_mfma(2, D, self.data_all.data_ptr(), self.data_all.data_ptr(), self.dnorm.data_ptr(),
+                         self.dnorm.data_ptr(), dummy.data_ptr(), lp.data_ptr(), N, R, nc, tpc, 0.0, self.st,
+                         row_begin=self.row0, n_rows=n)
         self.tt_part = lp.sum(1)
 
     def _device_step(self, train: bool) -> torch.Tensor:
@@ -169,7 +179,7 @@ class SampleShardedTrainer:
         if train:
             hip.gen_bwd(self.prog.data_ptr(), self.stride, self.params.data_ptr(), self.P, self.xhat.data_ptr(),
                         self.noise.data_ptr(), self.NS, gp.data_ptr(), nc, R, n, D, self.d, self.H, self.max_in,
-                        self.gpart.data_ptr(), self.st)
+                        self.gpart.data_ptr(), self.st, dxs=self.dxs.data_ptr() if self.dxs is not None else 0)
             g = self.gpart.sum(1, keepdim=True).contiguous()     # [R, 1, P], fixed order
             self._all_reduce(g)
             hip.adam(self.params.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), g.data_ptr(), 1, self.prog.data_ptr(),

@@ -118,7 +118,11 @@ def synthetic(name: str = "ogbn-products", seed: int = 0, device=None, scale: fl
     deg = (rowptr[1:] - rowptr[:-1]).to(torch.float32)
     dinv = deg.clamp_min(1).rsqrt()
     # split: train / valid / test by a per-node hash with OGB's split proportions (a pure
-    # function of the node id, so a graph shard labels its rows without the full graph)
+    # function of the node id, so a graph shard labels its rows without the full graph).
+    # The split SIZES are therefore random counts near OGB's (binomial around them), not
+    # the exact numbers; trainers normalise the loss by the real global train count
+    # (an emulated dry-run rank, which cannot count other ranks' rows, uses the nominal
+    # ``n_train_global`` of its shard -- its loss scale differs by that ratio).
     mask = np.asarray(native.rt().split_mask(n, n_train, n_val, seed + 1, np.arange(n, dtype=np.int64)))
     return GraphData(n=n, rowptr=rowptr, col=col, dinv=dinv.to(device),
                      x=torch.from_numpy(np.asarray(x)).to(device),
@@ -130,7 +134,7 @@ def partition_rows(g: GraphData, rank: int, world: int):
     """Contiguous row block of ``rank`` (equal sizes, last one padded): local CSR
     with global column ids, plus the row range."""
     per = (g.n + world - 1) // world
-    r0, r1 = rank * per, min(g.n, (rank + 1) * per)
+    r0, r1 = min(g.n, rank * per), min(g.n, (rank + 1) * per)
     rp = g.rowptr[r0:r1 + 1].to(torch.int64)
     col = g.col[int(rp[0]): int(rp[-1])]
     rp = (rp - rp[0]).to(torch.int32)

@@ -7,10 +7,11 @@ Attention aggregation over the CSR of A + I (multi-head):
 
 On a GPU the aggregation runs on three HIP kernels (``gnn_gat.hip``): a fused
 forward with an online softmax (edge scores never stored; per-(row, head)
-log-sum-exp kept), a row-wise backward doing the SDDMM ``<dout_i, Wh_j>`` and the
-softmax / LeakyReLU derivative (per-row statistics only, nothing per edge), and a
-column-wise backward over the transposed CSR that recomputes the attention
-weights and gathers ``dWh`` and the source score gradient -- no atomics anywhere.  The projections ``Wh = h W`` and the
+log-sum-exp kept, plus the LeakyReLU split q), a row-wise backward that is a
+per-row product (the destination-score gradient is -0.8 <dout_i, q_i>, so it
+gathers nothing), and a column-wise backward over the transposed CSR that
+recomputes the attention weights and gathers ``dWh`` and the source score
+gradient -- no atomics anywhere.  The projections ``Wh = h W`` and the
 scores ``s = <Wh, a>`` are PyTorch ops (hipBLASLt), so autograd chains through.
 On the CPU the same math is written with PyTorch index ops (the reference the
 GPU kernels are tested against).
@@ -75,35 +76,39 @@ def _check_transposed(g: "GraphCSR", what):
 
 
 def _gat_forward_kernels(Whg, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool):
+    """(out, lse, q): the forward plus the LeakyReLU split ``q`` the row half of the
+    backward reads (gnn_gat.hip), stored like Whg."""
     _check_graph(g, Whg, s_src, s_dst, "gat_fwd")
     n = g.n
     out = torch.empty(n, K * Fh, dtype=torch.float32, device=Whg.device)
     lse = torch.empty(n, K, dtype=torch.float32, device=Whg.device)
+    q = torch.empty(n, K * Fh, dtype=Whg.dtype, device=Whg.device)
     native.hip().gnn_gat_fwd(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(),
-                             s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Whg), int(lowp))
-    return out, lse
+                             s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Whg), int(lowp),
+                             q=q.data_ptr())
+    return out, lse, q
 
 
-def _gat_backward_kernels(Whg, s_src, s_dst, out, lse, dout, g: GraphCSR, K: int, Fh: int, lowp: bool):
-    """(dWh [n_cols, K*Fh] fp32, ds_src [n_cols, K], ds_dst [n, K]): the row half (SDDMM,
-    d s_dst, per-(row, head) statistics) then the column half over the transposed CSR,
-    which recomputes the attention weights -- nothing is stored per edge."""
+def _gat_backward_kernels(Whg, s_src, s_dst, out, lse, q, dout, g: GraphCSR, K: int, Fh: int, lowp: bool):
+    """(dWh [n_cols, K*Fh] fp32, ds_src [n_cols, K], ds_dst [n, K]): the row half (per-row
+    products: d s_dst and the statistics (s_dst, lse, D) -- no gather) then the column
+    half over the transposed CSR, which recomputes the attention weights -- nothing is
+    stored per edge."""
     hip = native.hip()
     n, dev = g.n, Whg.device
     _check_graph(g, Whg, s_src, s_dst, "gat_bwd")
     _check_transposed(g, "gat_bwd transposed")
-    dout = dout.contiguous().float()
+    doutg = dout.contiguous().to(torch.bfloat16 if lowp else torch.float32)
     rstat = torch.empty(n, K, 4, dtype=torch.float32, device=dev)
     ds_dst = torch.empty(n, K, dtype=torch.float32, device=dev)
-    hip.gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(),
-                        s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), rstat.data_ptr(),
-                        ds_dst.data_ptr(), n, K, Fh, _st(Whg), int(lowp))
+    st = _st(Whg)
+    hip.gnn_gat_rows(0, doutg.data_ptr(), 0, out.data_ptr(), q.data_ptr(), lse.data_ptr(), s_dst.data_ptr(), 0,
+                     rstat.data_ptr(), ds_dst.data_ptr(), 0, 0, 0, 0, 0, 0, 0.0, 0, 0, 0, 0, 0, n, K, Fh, int(lowp), st)
     rp_t, col_t = g.transposed()
-    doutg = dout.to(torch.bfloat16) if lowp else dout
     dWh = torch.empty(g.n_cols, K * Fh, dtype=torch.float32, device=dev)   # one row per source
     ds_src = torch.empty(g.n_cols, K, dtype=torch.float32, device=dev)
-    hip.gnn_gat_bwd_col(rp_t.data_ptr(), col_t.data_ptr(), Whg.data_ptr(), s_src.data_ptr(), rstat.data_ptr(),
-                        doutg.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), g.n_cols, K, Fh, _st(Whg), int(lowp))
+    hip.gnn_gat_col(rp_t.data_ptr(), col_t.data_ptr(), Whg.data_ptr(), s_src.data_ptr(), rstat.data_ptr(),
+                    doutg.data_ptr(), dWh.data_ptr(), ds_src.data_ptr(), 0, 0, g.n_cols, K, Fh, st, int(lowp))
     return dWh, ds_src, ds_dst
 
 
@@ -117,15 +122,15 @@ class _GATAggregate(torch.autograd.Function):
     def forward(ctx, Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool):
         Whg = Wh.to(torch.bfloat16).contiguous() if lowp else Wh.contiguous()
         s_src, s_dst = s_src.contiguous(), s_dst.contiguous()
-        out, lse = _gat_forward_kernels(Whg, s_src, s_dst, g, K, Fh, lowp)
-        ctx.save_for_backward(Whg, s_src, s_dst, out, lse)
+        out, lse, q = _gat_forward_kernels(Whg, s_src, s_dst, g, K, Fh, lowp)
+        ctx.save_for_backward(Whg, s_src, s_dst, out, lse, q)
         ctx.g, ctx.K, ctx.Fh, ctx.lowp = g, K, Fh, lowp
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        Whg, s_src, s_dst, out, lse = ctx.saved_tensors
-        dWh, ds_src, ds_dst = _gat_backward_kernels(Whg, s_src, s_dst, out, lse, dout, ctx.g, ctx.K, ctx.Fh,
+        Whg, s_src, s_dst, out, lse, q = ctx.saved_tensors
+        dWh, ds_src, ds_dst = _gat_backward_kernels(Whg, s_src, s_dst, out, lse, q, dout, ctx.g, ctx.K, ctx.Fh,
                                                     ctx.lowp)
         return dWh, ds_src, ds_dst, None, None, None, None
 
@@ -147,8 +152,8 @@ class _HaloGAT(torch.autograd.Function):
         ctx.g, ctx.K, ctx.Fh, ctx.lowp, ctx.halo = g, K, Fh, lowp, halo
         s_dst = s_dst.contiguous()
         if Wh.is_cuda:
-            out, lse = _gat_forward_kernels(Wh_ext, s_ext, s_dst, g, K, Fh, wdt == torch.bfloat16)
-            ctx.save_for_backward(Wh_ext, s_ext, s_dst, out, lse)
+            out, lse, q = _gat_forward_kernels(Wh_ext, s_ext, s_dst, g, K, Fh, wdt == torch.bfloat16)
+            ctx.save_for_backward(Wh_ext, s_ext, s_dst, out, lse, q)
             return out
         ctx.save_for_backward(Wh_ext, s_ext, s_dst)
         return _gat_aggregate_torch(Wh_ext, s_ext, s_dst, g, K, Fh)
@@ -157,8 +162,8 @@ class _HaloGAT(torch.autograd.Function):
     def backward(ctx, dout):
         g, K, Fh, halo = ctx.g, ctx.K, ctx.Fh, ctx.halo
         if dout.is_cuda:
-            Wh_ext, s_ext, s_dst, out, lse = ctx.saved_tensors
-            dWh, ds_src, ds_dst = _gat_backward_kernels(Wh_ext, s_ext, s_dst, out, lse, dout, g, K, Fh,
+            Wh_ext, s_ext, s_dst, out, lse, q = ctx.saved_tensors
+            dWh, ds_src, ds_dst = _gat_backward_kernels(Wh_ext, s_ext, s_dst, out, lse, q, dout, g, K, Fh,
                                                         Wh_ext.dtype == torch.bfloat16)
         else:
             Wh_ext, s_ext, s_dst = ctx.saved_tensors
@@ -427,9 +432,23 @@ class ShardedGATTrainer:
             if (self.world > 1 and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0"
                     and os.environ.get("CGNN_TRAIN_HALO", "1") != "0"):
                 train_l2 = self._train_halo(shard, r0, r1, per, emulate, wide, halo_chunk_bytes)
+            # layer 1 without communication: its input rows are static, so the rows of the
+            # layer-1 halo cross the links ONCE here (bf16), and every epoch each rank
+            # projects [Wh | s_src] of the received rows itself (lin_fwd) and takes their
+            # weight-gradient share as x_ext^T dy_ext -- per epoch only the layer-2 halo and
+            # the weight all-reduce remain.  Env CGNN_GAT_L1_EXCHANGE=1: exchange per epoch.
+            x_ext = None
+            self.l1_setup_bytes = 0
+            if self.halo is not None and os.environ.get("CGNN_GAT_L1_EXCHANGE", "0") != "1":
+                F = self.x.shape[1]
+                xb = torch.zeros(nloc, (F + 7) // 8 * 8, dtype=torch.bfloat16, device=self.dev)
+                xb[:, :F] = self.x.to(torch.bfloat16)
+                x_ext = self.halo.exchange_parts([xb])[0]
+                self.l1_setup_bytes = self.halo.n_recv * xb.shape[1] * 2
+                del xb
             self.fused = FusedGAT(self.x, self.y, self.mask, shard.n_classes, self.g, heads, head_dim, dropout, lr,
                                   seed, halo=self.halo, row0=r0, n_train=int(self.n_train), distributed=distributed,
-                                  train_l2=train_l2)
+                                  train_l2=train_l2, x_ext=x_ext)
             self.model = self.opt = None
             self.epoch = 0
             return
@@ -478,8 +497,12 @@ class ShardedGATTrainer:
         l1 = self.fused.layers[0] if self.fused is not None else self.model.l1
         w = 2 * l1.K * l1.Fh + 4 * l1.K
         rb, sb = self.halo.bytes_per_exchange(w)
+        local = self.fused is not None and self.fused.l1_local
         out = {"recv_rows": self.halo.n_recv, "send_rows": self.halo.n_send, "local_rows": self.halo.nloc,
-               "layer1_recv_bytes": rb, "layer1_send_bytes": sb}
+               # per epoch (forward; the backward returns as many fp32 bytes): 0 when layer 1 is
+               # projected locally from the setup-time input rows
+               "layer1_recv_bytes": 0 if local else rb, "layer1_send_bytes": 0 if local else sb,
+               "layer1_local": bool(local), "layer1_setup_recv_bytes": getattr(self, "l1_setup_bytes", 0)}
         tr = self.fused._tr if self.fused is not None else None
         if tr is not None and tr.halo is not None and tr.halo is not self.halo:
             out["layer2_train_recv_rows"] = tr.halo.n_recv    # the training epochs' layer-2 halo

@@ -7,21 +7,32 @@ input, so they fold into the projection ``Wc = [W | W a_src | W a_dst]``):
   forward   [Wh | s_src | s_dst] = h Wc       lin_fwd (MFMA), Wh stored bf16 (the
                                               edge-gathered operand), the scores as
                                               exact fp32 planes (its ``tail`` output)
-            out, lse = GAT aggregation        gat_fwd (online softmax; sharded runs
-                                              first exchange [Wh | s_src] halo rows)
-            layer 1: h1 = bf16(dropout(elu(out + b1)))        gat_act_fwd
+            out, lse, q = GAT aggregation     gat_fwd (online softmax); q is the
+                                              LeakyReLU split that makes the row half
+                                              of the backward a per-row product;
+                                              layer 1 also writes h1 = bf16(dropout(
+                                              elu(out + b1))) in the same kernel
             layer 2: loss, dlogits = CE(out + b2) (train rows) gat_row_ce
                       (training epochs aggregate layer 2 at the train rows only:
                       no other row's logits reach the loss -- exact)
-  backward  dWh, ds_src, ds_dst               gat_bwd_row / gat_bwd_col (+ halo
-                                              reduce-back of the received rows)
-            dy = bf16([dWh | ds_src | ds_dst])                 gat_pack_grad
+  backward  row half (per row, no gather)     gat_rows: D = <dout, out>,
+                                              d s_dst = -0.8 <dout, q>; for layer 1
+                                              fused with the activation backward
+                                              (dout1 = dh1 * mask * elu', db1)
+            column half                       gat_col over the transposed CSR:
+                                              dy = bf16([dWh | ds_src | ds_dst]) written
+                                              in place (the GEMM operand)
             dWc = h^T dy                      lin_bwd_weight (split-K MFMA, fixed order)
             dh = dy Wc^T                      lin_bwd_data (MFMA; layer 2 only)
-            dout1 = dh * mask * elu'(out1 + b1), db1           gat_act_bwd
             dW, da_src, da_dst from dWc       (weight-sized tensors only)
   update    gradients summed over ranks (one all-reduce of the flat buffer), Adam
             on the flat fp32 parameter buffer (ops.adam_).
+
+Graph-sharded runs (``halo``): layer 1 is communication-free when the trainer passes
+``x_ext`` -- the static input rows of this rank's layer-1 halo, fetched once at setup --
+so each rank projects ``[Wh | s_src]`` of the received rows itself and takes their
+weight-gradient share as ``x_ext^T dy_ext``; only the layer-2 (training) halo moves per
+epoch, plus the weight all-reduce.
 
 Dropout is keyed by (seed, GLOBAL row, column, device step counter), so a
 sharded run draws exactly the masks of a one-GPU run; together with the
@@ -58,13 +69,11 @@ def _ptr(t):
 
 # ------------------------------------------------------------------ elementwise ops
 def act_fwd(out, bias, H, p, key, step, row0=0):
-    """H[:, :F] = bf16(dropout(elu(out + bias))), F = out.shape[1] (a multiple of 32)."""
-    n, F = out.shape
+    """H[:, :F] = bf16(dropout(elu(out + bias))), F = out.shape[1] (a multiple of 32).
+    CPU reference: on a GPU this runs inside the layer's aggregation kernel (gat_fwd)."""
     if out.is_cuda:
-        sv, sp = ops._step_args(step)
-        native.hip().gnn_gat_act_fwd(out.data_ptr(), bias.data_ptr(), H.data_ptr(), H.stride(0), n, F, float(p),
-                                     int(key[0]), int(key[1]), sv, sp, int(row0), _st(out))
-        return H
+        raise RuntimeError("act_fwd is the CPU reference; the GPU fuses it into gat_fwd (_agg_fwd act=...)")
+    n, F = out.shape
     z = out.float() + bias.float()
     e = torch.where(z > 0, z, torch.expm1(z))
     if p > 0:
@@ -86,16 +95,11 @@ def _scratch(dev, shape):
 
 
 def act_bwd(dH, out, bias, p, key, step, row0, dout, doutb, db):
-    """dout = dH * mask * elu'(out + bias) (fp32, plus a bf16 copy ``doutb``), db = colsum(dout)."""
-    n, F = out.shape
+    """dout = dH * mask * elu'(out + bias) (fp32, plus a bf16 copy ``doutb``), db = colsum(dout).
+    CPU reference: on a GPU this runs inside the row half of the backward (gat_rows)."""
     if out.is_cuda:
-        hip = native.hip()
-        bpart = _scratch(out.device, (hip.gnn_gat_act_bwd_blocks(), F))
-        sv, sp = ops._step_args(step)
-        hip.gnn_gat_act_bwd(dH.data_ptr(), dH.stride(0), out.data_ptr(), bias.data_ptr(), dout.data_ptr(),
-                            _ptr(doutb), bpart.data_ptr(), db.data_ptr(), n, F, float(p), int(key[0]), int(key[1]),
-                            sv, sp, int(row0), _st(out))
-        return dout
+        raise RuntimeError("act_bwd is the CPU reference; the GPU fuses it into gat_rows (_agg_rows act=...)")
+    n, F = out.shape
     z = out.float() + bias.float()
     d = dH[:n, :F].float() * torch.where(z > 0, torch.ones_like(z), torch.exp(z))
     if p > 0:
@@ -162,44 +166,75 @@ def pack_grad(dWh, ds_src, ds_dst, dy):
 
 
 # ------------------------------------------------------------------ aggregation
-def _agg_fwd(Wh, s_src, s_dst, g, K, Fh):
+def _check_rows(g, Wh, s_src, s_dst, dst_rows, what):
     from .gat import _check_graph
-    _check_graph(g, Wh, s_src, s_dst, "fused gat_fwd")
+    from ..utils import checks
+    _check_graph(g, Wh, s_src, s_dst, what)
+    if dst_rows is not None and checks.enabled():
+        checks.rows(dst_rows, g.n, what + " dst_rows")
+        checks.index(dst_rows, s_dst.shape[0], what + " dst_rows")
+
+
+def _agg_fwd(Wh, s_src, s_dst, g, K, Fh, dst_rows=None, q=None, act=None):
+    """out [g.n, K Fh] fp32, lse [g.n, K]: attention aggregation over ``g``; the
+    destination scores of row i are ``s_dst[dst_rows[i]]`` (or ``s_dst[i]``).  GPU
+    extras: ``q`` (training) receives the LeakyReLU split for the row backward;
+    ``act = (bias, H, p, key, step, row0)`` writes the hidden activation
+    ``H = bf16(dropout(elu(out + bias)))`` in the same kernel."""
+    _check_rows(g, Wh, s_src, s_dst, dst_rows, "fused gat_fwd")
     n = g.n
     if Wh.is_cuda:
         out = torch.empty(n, K * Fh, dtype=torch.float32, device=Wh.device)
         lse = torch.empty(n, K, dtype=torch.float32, device=Wh.device)
+        kw = {}
+        if act is not None:
+            bias, H, p, key, step, row0 = act
+            sv, sp = ops._step_args(step)
+            kw = dict(bias=bias.data_ptr(), H=H.data_ptr(), ldh=H.stride(0), p=float(p), k0=int(key[0]),
+                      k1=int(key[1]), step=sv, stepp=sp, row0=int(row0))
         native.hip().gnn_gat_fwd(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(),
                                  s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Wh),
-                                 int(Wh.dtype == torch.bfloat16))
+                                 int(Wh.dtype == torch.bfloat16), dst_rows=_ptr(dst_rows), q=_ptr(q), **kw)
         return out, lse
     from .gat import _gat_aggregate_torch
-    return _gat_aggregate_torch(Wh.float(), s_src, s_dst, g, K, Fh).float(), None
+    sd = s_dst if dst_rows is None else s_dst.index_select(0, dst_rows.long())
+    return _gat_aggregate_torch(Wh.float(), s_src, sd, g, K, Fh).float(), None
 
 
-def _agg_bwd_rows(Wh, s_src, s_dst, out, lse, dout, g, K, Fh):
-    """Row half of the aggregation backward: ds_dst [n, K] and the per-(row, head)
-    statistics (s_dst, lse, <dout, out>) the column half recomputes alpha from (GPU)."""
-    from .gat import _check_graph, _check_transposed
-    _check_graph(g, Wh, s_src, s_dst, "fused gat_bwd_row")
-    _check_transposed(g, "fused gat_bwd_col")
-    dev = Wh.device
-    rstat = torch.empty(g.n, K, 4, dtype=torch.float32, device=dev)
-    ds_dst = torch.empty(g.n, K, dtype=torch.float32, device=dev)
-    native.hip().gnn_gat_bwd_row(g.rowptr.data_ptr(), g.col.data_ptr(), Wh.data_ptr(), s_src.data_ptr(),
-                                 s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(), rstat.data_ptr(),
-                                 ds_dst.data_ptr(), g.n, K, Fh, _st(Wh), int(Wh.dtype == torch.bfloat16))
-    return rstat, ds_dst
+def _agg_rows(out, q, lse, s_dst, dst_rows, K, Fh, rstat, dout=None, dH=None, act=None, ds_dst=None, dy=None):
+    """Row half of the aggregation backward (GPU, no gather): rstat [n, K, 4] =
+    (s_dst, lse, D, 0) per (row, head), d s_dst = -0.8 <dout, q> into ``ds_dst`` (fp32
+    [*, K]) and / or column HF + K + k of ``dy`` (bf16, row dst_rows[i] or i).  Either
+    ``dout`` (bf16) is given, or ``dH`` with ``act = (dout_w, bias, db, p, key, step,
+    row0)``: dout = dH * mask * elu'(out + bias) is made here, written to ``dout_w``
+    (bf16), and db = colsum(dout)."""
+    n = out.shape[0]
+    hip = native.hip()
+    kw = dict(dout_w=0, bias=0, bpart=0, db=0, p=0.0, k0=0, k1=0, step=0, stepp=0, row0=0)
+    if act is not None:
+        dout_w, bias, db, p, key, step, row0 = act
+        sv, sp = ops._step_args(step)
+        bpart = _scratch(out.device, (hip.gnn_gat_row_blocks(), K * Fh))
+        kw = dict(dout_w=dout_w.data_ptr(), bias=bias.data_ptr(), bpart=bpart.data_ptr(), db=db.data_ptr(),
+                  p=float(p), k0=int(key[0]), k1=int(key[1]), step=sv, stepp=sp, row0=int(row0))
+        src, ldh = dH, dH.stride(0)
+    else:
+        src, ldh = dout, 0
+    hip.gnn_gat_rows(int(act is not None), src.data_ptr(), ldh, out.data_ptr(), q.data_ptr(), lse.data_ptr(),
+                     s_dst.data_ptr(), _ptr(dst_rows), rstat.data_ptr(), _ptr(ds_dst), _ptr(dy),
+                     dy.stride(0) if dy is not None else 0, n=n, K=K, Fh=Fh, wbf=1, st=_st(out), **kw)
 
 
-def _agg_bwd_cols(Wh, s_src, rstat, doutb, g, K, Fh, lo, hi, dWh, ds_src):
+def _agg_cols(Wh, s_src, rstat, doutb, g, K, Fh, lo, hi, dWh=None, ds_src=None, dy=None):
     """Column half for source rows [lo, hi) of the transposed CSR (rows are independent,
-    so a row range is a pointer offset): dWh [hi - lo, K Fh], ds_src [hi - lo, K] (GPU)."""
+    so a row range is a pointer offset): fp32 ``dWh`` [hi - lo, K Fh] / ``ds_src`` [hi - lo,
+    K], or bf16 [dWh | ds_src] straight into ``dy`` rows [lo, hi) (GPU)."""
     rp_t, col_t = g.transposed()
     KF = K * Fh
-    native.hip().gnn_gat_bwd_col(rp_t.data_ptr() + 4 * lo, col_t.data_ptr(), Wh.data_ptr() + Wh.element_size() * KF * lo,
-                                 s_src.data_ptr() + 4 * K * lo, rstat.data_ptr(), doutb.data_ptr(), dWh.data_ptr(),
-                                 ds_src.data_ptr(), hi - lo, K, Fh, _st(doutb), 1)
+    dyp = dy.data_ptr() + dy.element_size() * dy.stride(0) * lo if dy is not None else 0
+    native.hip().gnn_gat_col(rp_t.data_ptr() + 4 * lo, col_t.data_ptr(), Wh.data_ptr() + Wh.element_size() * KF * lo,
+                             s_src.data_ptr() + 4 * K * lo, rstat.data_ptr(), doutb.data_ptr(), _ptr(dWh),
+                             _ptr(ds_src), dyp, dy.stride(0) if dy is not None else 0, hi - lo, K, Fh, _st(doutb), 1)
 
 
 def _agg_bwd_torch(Wh, s_src, s_dst, dout, g, K, Fh):
@@ -239,10 +274,13 @@ class FusedGAT:
     ``halo`` is None).  ``g``: GraphCSR over [own | received] source rows;
     ``x``: fp32 [nloc, F] input features (already standardised); ``row0``: the
     global id of the first own row (dropout keys); ``n_train``: GLOBAL train count.
+    ``x_ext`` (sharded, optional): bf16 [n_ext, >= F] input rows of [own | received]
+    (the layer-1 halo's static features): layer 1 then projects every row it reads
+    itself and needs no exchange.
     Parameters are initialised exactly like ``gat.GAT(F, C, heads, head_dim, seed)``."""
 
     def __init__(self, x, y, mask, n_classes, g, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0,
-                 halo=None, row0=0, n_train=None, distributed=False, train_l2=None):
+                 halo=None, row0=0, n_train=None, distributed=False, train_l2=None, x_ext=None):
         from .gat import GAT
         dev = x.device
         self.dev, self.g, self.halo = dev, g, halo
@@ -256,8 +294,14 @@ class FusedGAT:
             n_train = int((self.mask == 1).sum())
         self.n_train = max(int(n_train), 1)
         bf = dict(dtype=torch.bfloat16, device=dev)
-        self.xb = torch.zeros(self.nloc, _ru8(self.F), **bf)
-        self.xb[:, :self.F] = x.to(torch.bfloat16)
+        if x_ext is not None:
+            if halo is None or x_ext.shape[0] != halo.n_ext or x_ext.dtype != torch.bfloat16:
+                raise ValueError("x_ext must be bf16 [halo.n_ext, >= F] rows of [own | received]")
+            self.xb = x_ext
+        else:
+            self.xb = torch.zeros(self.nloc, _ru8(self.F), **bf)
+            self.xb[:, :self.F] = x.to(torch.bfloat16)
+        self.l1_local = x_ext is not None
         ref = GAT(self.F, self.C, heads, head_dim, dropout, seed)          # the init of the autograd model
         mods = [ref.l1, ref.l2]
         flat = torch.cat([t.detach().reshape(-1) for m in mods for t in (m.W, m.a_src, m.a_dst, m.bias)])
@@ -276,7 +320,7 @@ class FusedGAT:
         off = 0
         self.layers = []
         kin = self.F
-        for m in mods:
+        for li, m in enumerate(mods):
             L = _Layer()
             L.K, L.Fh = m.K, m.Fh
             L.KF = L.K * L.Fh
@@ -291,16 +335,19 @@ class FusedGAT:
             L.Wc = torch.zeros(kin, L.N, dtype=torch.float32, device=dev)
             L.dWc = torch.zeros_like(L.Wc)
             L.db_scratch = torch.zeros(L.N, dtype=torch.float32, device=dev)
-            L.Wh = torch.zeros(self.nloc, L.KF, **bf)
-            L.s = torch.zeros(2, self.nloc, L.K, dtype=torch.float32, device=dev)
-            L.dy = torch.zeros(self.nloc, _ru8(L.N), **bf)
+            # layer 1 with local projection: every [own | received] row is projected here
+            rows = self.xb.shape[0] if (li == 0 and self.l1_local) else self.nloc
+            L.local = li == 0 and self.l1_local
+            L.Wh = torch.zeros(rows, L.KF, **bf)
+            L.s = torch.zeros(2, rows, L.K, dtype=torch.float32, device=dev)
+            L.dy = torch.zeros(rows, _ru8(L.N), **bf)
             self.layers.append(L)
             kin = L.KF
         L1, L2 = self.layers
         self.h1 = torch.zeros(self.nloc, L1.KF, **bf)
         self.dh1 = torch.zeros(self.nloc, L1.KF, **bf)
-        self.dout1 = torch.zeros(self.nloc, L1.KF, dtype=torch.float32, device=dev)
         self.dout1b = torch.zeros(self.nloc, L1.KF, **bf)
+        self.dout1 = torch.zeros(self.nloc, L1.KF, dtype=torch.float32, device=dev) if dev.type != "cuda" else None
         self.dout2 = torch.zeros(self.nloc, L2.KF, dtype=torch.float32, device=dev)
         self.dout2b = torch.zeros(self.nloc, L2.KF, **bf)
         # Training epochs aggregate layer 2 only at this rank's train rows (the only
@@ -316,7 +363,7 @@ class FusedGAT:
             trows, gT, thalo, placeholder = train_l2
             nT = trows.numel()
             self._tr = types.SimpleNamespace(
-                rows=trows, g=gT, halo=thalo, y=self.y[trows].contiguous(),
+                rows=trows, rows32=trows.to(torch.int32).contiguous(), g=gT, halo=thalo, y=self.y[trows].contiguous(),
                 mask=torch.zeros_like(self.mask[trows]) if placeholder else self.mask[trows].contiguous(),
                 dout=torch.zeros(nT, L2.KF, dtype=torch.float32, device=dev),
                 doutb=torch.zeros(nT, L2.KF, **bf))
@@ -330,7 +377,8 @@ class FusedGAT:
             eid = torch.arange(int(trp[-1]), device=dev) + torch.repeat_interleave(lo - trp[:-1], deg)
             nT = trows.numel()
             self._tr = types.SimpleNamespace(
-                rows=trows, g=GraphCSR(trp.to(g.rowptr.dtype), g.col[eid], nT, g.n_cols), halo=halo,
+                rows=trows, rows32=trows.to(torch.int32).contiguous(),
+                g=GraphCSR(trp.to(g.rowptr.dtype), g.col[eid], nT, g.n_cols), halo=halo,
                 y=self.y[trows].contiguous(), mask=self.mask[trows].contiguous(),
                 dout=torch.zeros(nT, L2.KF, dtype=torch.float32, device=dev),
                 doutb=torch.zeros(nT, L2.KF, **bf))
@@ -342,8 +390,11 @@ class FusedGAT:
         # with zero gradient); evaluation aggregates every row.  The papers100M shape has
         # ~1 % train rows, so most layer-1 edges drop out.  Not in a dry run (emulated
         # halo: the received rows' flags are not real).  Env CGNN_L1_TRAIN_NBRS=0: off.
+        # The decision is the same on every rank whenever there is a halo (the flag
+        # exchange is collective): a rank without train rows still takes part.
         self._g1 = None
-        if (self._tr is not None and os.environ.get("CGNN_L1_TRAIN_NBRS", "1") != "0"
+        want = (halo is not None) or (self._tr is not None)
+        if (want and os.environ.get("CGNN_L1_TRAIN_NBRS", "1") != "0"
                 and not (halo is not None and getattr(halo, "emulate", False))):
             self._g1 = self._train_neighbour_graph(g, halo)
         self.epoch = 0
@@ -377,22 +428,28 @@ class FusedGAT:
         return self.step_t if self.dev.type == "cuda" else int(self.step_t.item())
 
     # ------------------------------------------------------------------ passes
-    def _project_aggregate(self, L, x, K1, tr=None, g1=None):
+    def _project_aggregate(self, L, x, K1, train, tr=None, g1=None, act=None):
         """Projection + attention aggregation; ``tr`` (train-row CSR): only at those rows;
-        ``g1``: the aggregation graph instead of the full one (same rows)."""
+        ``g1``: the aggregation graph instead of the full one (same rows); ``act``: the
+        fused hidden activation (GPU)."""
         wcat(L.W, L.a_src, L.a_dst, L.Wc)
         lin_fwd(x, L.Wc, None, K1=K1, out=L.Wh, tail=L.s, nsplit=L.KF, tk=L.K)
         s_src, s_dst = L.s[0], L.s[1]
-        halo = self.halo if tr is None else tr.halo
+        halo = None if L.local else (self.halo if tr is None else tr.halo)
         if halo is not None:
             Wh_ext, s_ext = halo.exchange_parts([L.Wh, s_src])
         else:
             Wh_ext, s_ext = L.Wh, s_src
         g = self.g if g1 is None else g1
+        dst_rows = None
         if tr is not None:
-            g, s_dst = tr.g, s_dst.index_select(0, tr.rows)
-        out, lse = _agg_fwd(Wh_ext, s_ext, s_dst, g, L.K, L.Fh)
-        L.saved = (Wh_ext, s_ext, s_dst, out, lse)
+            g, dst_rows = tr.g, (tr.rows32 if self.dev.type == "cuda" else tr.rows)
+        q = None
+        if train and self.dev.type == "cuda":
+            q = torch.empty(g.n, L.KF, dtype=torch.bfloat16, device=self.dev)
+        out, lse = _agg_fwd(Wh_ext, s_ext, s_dst, g, L.K, L.Fh, dst_rows=dst_rows, q=q,
+                            act=act if self.dev.type == "cuda" else None)
+        L.saved = (Wh_ext, s_ext, s_dst, dst_rows, out, lse, q)
         L.tr, L.g_used = tr, g
         return out
 
@@ -400,10 +457,12 @@ class FusedGAT:
         L1, L2 = self.layers
         p = self.p if train else 0.0
         step = self._dropout_step()
-        out1 = self._project_aggregate(L1, self.xb, self.F, g1=self._g1 if train else None)
-        act_fwd(out1, L1.b, self.h1, p, self.key, step, self.row0)
+        act = (L1.b, self.h1, p, self.key, step, self.row0)
+        out1 = self._project_aggregate(L1, self.xb, self.F, train, g1=self._g1 if train else None, act=act)
+        if self.dev.type != "cuda":
+            act_fwd(out1, L1.b, self.h1, p, self.key, step, self.row0)
         tr = self._tr if train else None
-        out2 = self._project_aggregate(L2, self.h1, L1.KF, tr)
+        out2 = self._project_aggregate(L2, self.h1, L1.KF, train, tr)
         if tr is not None:
             stats = row_ce(out2, L2.b, self.C, tr.y, tr.mask, 1.0 / self.n_train, dZ=tr.dout,
                            dZb=tr.doutb, db=L2.gb)
@@ -417,52 +476,81 @@ class FusedGAT:
                 L.saved = None
         return stats
 
-    def _layer_backward(self, L, dout, doutb, x, K1):
-        Wh_ext, s_ext, s_dst, out, lse = L.saved
+    def _layer_backward(self, L, dout, doutb, x, K1, act=None):
+        """``dout`` fp32 (CPU) / ``doutb`` bf16 (GPU) gradient of the aggregation output;
+        GPU layer 1: ``doutb`` is None and ``act = (dH, bias, db)`` -- the activation
+        backward runs inside the row half."""
+        Wh_ext, s_ext, s_dst, dst_rows, out, lse, q = L.saved
         L.saved = None
         tr, L.tr = L.tr, None
         g, K, Fh = L.g_used, L.K, L.Fh
-        halo = self.halo if tr is None else tr.halo
+        halo = None if L.local else (self.halo if tr is None else tr.halo)
         if not self.dev.type == "cuda":
-            dWh, ds_src, ds_dst = _agg_bwd_torch(Wh_ext, s_ext, s_dst, dout, g, K, Fh)
+            sd = s_dst if dst_rows is None else s_dst.index_select(0, dst_rows)
+            dWh, ds_src, ds_dst = _agg_bwd_torch(Wh_ext, s_ext, sd, dout, g, K, Fh)
             del Wh_ext, s_ext
             if halo is not None:
                 dWh, ds_src = halo.reduce_back([dWh, ds_src])
+            if tr is not None or ds_dst.shape[0] != dWh.shape[0]:
+                # the other rows' destination-score gradients are 0 (rows outside the train
+                # CSR; the received rows of a locally projected layer 1)
+                full = torch.zeros(dWh.shape[0], K, dtype=ds_dst.dtype, device=ds_dst.device)
+                if tr is not None:
+                    full.index_copy_(0, tr.rows, ds_dst)
+                else:
+                    full[:ds_dst.shape[0]] = ds_dst
+                ds_dst = full
+            pack_grad(dWh, ds_src, ds_dst, L.dy)
+            del dWh, ds_src, ds_dst
         else:
-            rstat, ds_dst = _agg_bwd_rows(Wh_ext, s_ext, s_dst, out, lse, dout, g, K, Fh)
-            n = self.nloc
-            dWh = torch.empty(n, L.KF, dtype=torch.float32, device=self.dev)
-            ds_src = torch.empty(n, K, dtype=torch.float32, device=self.dev)
-            _agg_bwd_cols(Wh_ext, s_ext, rstat, doutb, g, K, Fh, 0, n, dWh, ds_src)
-            if halo is not None:
+            rstat = torch.empty(g.n, K, 4, dtype=torch.float32, device=self.dev)
+            rargs = {}
+            if act is not None:
+                dH, bias, db = act
+                doutb = self.dout1b
+                rargs = dict(dH=dH, act=(doutb, bias, db, self.p, self.key, self._dropout_step(), self.row0))
+            else:
+                rargs = dict(dout=doutb)
+            if halo is None:
+                # dy written in place: [dWh | ds_src] by the column half, ds_dst by the row half
+                _agg_rows(out, q, lse, s_dst, dst_rows, K, Fh, rstat, dy=L.dy, **rargs)
+                _agg_cols(Wh_ext, s_ext, rstat, doutb, g, K, Fh, 0, g.n_cols, dy=L.dy)
+            else:
+                n = self.nloc
+                ds_dst = torch.zeros(n, K, dtype=torch.float32, device=self.dev)
+                _agg_rows(out, q, lse, s_dst, dst_rows, K, Fh, rstat, ds_dst=ds_dst, **rargs)
+                dWh = torch.empty(n, L.KF, dtype=torch.float32, device=self.dev)
+                ds_src = torch.empty(n, K, dtype=torch.float32, device=self.dev)
+                _agg_cols(Wh_ext, s_ext, rstat, doutb, g, K, Fh, 0, n, dWh=dWh, ds_src=ds_src)
+
                 # the received rows' gradients are made one exchange round at a time
                 def produce(lo, hi):
                     a = torch.empty(hi - lo, L.KF, dtype=torch.float32, device=self.dev)
                     b = torch.empty(hi - lo, K, dtype=torch.float32, device=self.dev)
-                    _agg_bwd_cols(Wh_ext, s_ext, rstat, doutb, g, K, Fh, lo, hi, a, b)
+                    _agg_cols(Wh_ext, s_ext, rstat, doutb, g, K, Fh, lo, hi, dWh=a, ds_src=b)
                     return [a, b]
                 halo.reduce_back_stream(produce, [dWh, ds_src], getattr(self.halo, "grad_wire", torch.float32))
-            del rstat, Wh_ext, s_ext
-        if tr is not None:               # the other rows' destination-score gradients are 0
-            full = torch.zeros(self.nloc, K, dtype=ds_dst.dtype, device=ds_dst.device)
-            full.index_copy_(0, tr.rows, ds_dst)
-            ds_dst = full
-        pack_grad(dWh, ds_src, ds_dst, L.dy)
-        del dWh, ds_src, ds_dst
+                pack_grad(dWh, ds_src, ds_dst, L.dy)
+                del dWh, ds_src, ds_dst
+            del rstat, Wh_ext, s_ext, q
         lin_bwd_weight(x, L.dy, L.N, K1=K1, dW=L.dWc, db=L.db_scratch)
         wcat_bwd(L.dWc, L.W, L.a_src, L.a_dst, L.gW, L.ga_src, L.ga_dst)
 
     def backward(self):
         L1, L2 = self.layers
-        out1 = L1.saved[3]
-        if L2.tr is not None:
-            self._layer_backward(L2, L2.tr.dout, L2.tr.doutb, self.h1, L1.KF)
+        out1 = L1.saved[4]
+        tr = L2.tr
+        if tr is not None:
+            self._layer_backward(L2, tr.dout, tr.doutb, self.h1, L1.KF)
         else:
             self._layer_backward(L2, self.dout2, self.dout2b, self.h1, L1.KF)
         lin_bwd_data(L2.dy, L2.Wc, L1.KF, out1=self.dh1)
-        act_bwd(self.dh1, out1, L1.b, self.p, self.key, self._dropout_step(), self.row0, self.dout1, self.dout1b,
-                L1.gb)
-        self._layer_backward(L1, self.dout1, self.dout1b, self.xb, self.F)
+        if self.dev.type == "cuda":
+            self._layer_backward(L1, None, None, self.xb, self.F, act=(self.dh1, L1.b, L1.gb))
+        else:
+            act_bwd(self.dh1, out1, L1.b, self.p, self.key, self._dropout_step(), self.row0, self.dout1,
+                    self.dout1b, L1.gb)
+            self._layer_backward(L1, self.dout1, self.dout1b, self.xb, self.F)
 
     def train_step(self):
         stats = self.forward(train=True)

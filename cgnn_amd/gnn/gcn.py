@@ -29,13 +29,17 @@ One epoch = one full-graph forward + backward + optimizer step:
 
 Multi-GPU: each rank owns a contiguous block of rows (1-D partition); the
 static features are replicated (0.5 GB for ogbn-products, trivial against
-288 GB of HBM), so layer 1 needs no communication; layer 2 needs one
-all-gather of Z2 in the forward ([n, 48] bf16) and one of the compact G in the
-backward (train rows only, padded to the largest rank's count: 1/12 of Z2's
-bytes), plus one all-reduce of the ~40k gradient floats.  The Z2 all-gather
-runs asynchronously on RCCL's stream while the rank aggregates the edges whose
-source rows it owns, the remaining edges are added afterwards through an fp32
-partial, and so does the next epoch's layer-1 SpMM (parameter-independent).
+288 GB of HBM), so layer 1 needs no communication.  Layer 2 in training: the
+rank aggregates only its train rows, and only the remote Z2 rows THOSE read
+travel -- a training halo negotiated once at setup, one all-to-all per epoch
+(``_train_row_csr``; env CGNN_TRAIN_HALO=0 uses the evaluation's exchange).
+Evaluation aggregates every row, with the full halo from 4 ranks on (``halo``)
+and an all-gather of Z2 below that.  The backward all-gathers the compact G (train
+rows only, padded to the largest rank's count: 1/12 of Z2's bytes), plus one
+all-reduce of the ~40k gradient floats.  Each exchange runs asynchronously on
+RCCL's stream while the rank aggregates the edges whose source rows it owns;
+the remaining edges are added afterwards through an fp32 partial, and the next
+epoch's layer-1 SpMM (parameter-independent) overlaps the forward exchange.
 """
 from __future__ import annotations
 
@@ -105,8 +109,10 @@ class GCNTrainer:
         # reorder=True: relabel the nodes for gather locality first (data.reorder: LP
         # clusters + Cuthill-McKee, ~4-8 s of host C++ on the ogbn-products shape, part
         # of setup); the row partition of a multi-GPU run then cuts mostly between
-        # clusters, which also shrinks the layer-2 halo.  Losses and accuracies are
-        # invariant; ``self.new_id`` maps the caller's node ids to the trainer's rows.
+        # clusters, which also shrinks the layer-2 halo.  Evaluation, and training with
+        # dropout 0, are invariant; with dropout > 0 the masks are keyed by the RELABELLED
+        # row, so a reordered run draws other masks (equal in distribution, not bitwise).
+        # ``self.new_id`` maps the caller's node ids to the trainer's rows.
         self.new_id = None
         if reorder:
             from .data import reorder as _reorder
@@ -131,6 +137,11 @@ class GCNTrainer:
         self.p, self.lr, self.wd = float(dropout), float(lr), float(weight_decay)
         self.key = model_key(seed, "gcn-dropout")
         r0, r1, per, rp, col = partition_rows(g, self.rank, self.world)
+        if (self.world - 1) * per >= g.n:
+            # every collective plan below assumes each rank owns rows (an empty rank would
+            # skip the collectives its peers block in)
+            raise ValueError("GCNTrainer: %d nodes over %d ranks leaves the last rank without rows"
+                             % (g.n, self.world))
         self.r0, self.r1, self.per, self.nloc = r0, r1, per, r1 - r0
         self.rowptr, self.col = rp.contiguous(), col.contiguous()
         self.dinv = g.dinv[r0:r1].contiguous()
@@ -247,7 +258,7 @@ class GCNTrainer:
         # The switch is global (env), never per rank: the training halo is negotiated
         # collectively, so a rank without train rows takes part with a placeholder row.
         trows = torch.nonzero(self.mask == 1).flatten()
-        if self.nloc > 0 and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
+        if os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
             self._l2 = self._train_row_csr(trows)
         # ... and then layer 1 is needed only at the rows with a train neighbour (the
         # sources those aggregations read; 94 % of the rows, 96.7 % of the entries on the

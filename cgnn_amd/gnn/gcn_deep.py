@@ -303,7 +303,7 @@ class GCNInference:
         F = g.n_features
         # features pre-scaled by the column normalisation once (static input)
         self.xs = pad_cols(g.x.float() * g.dinv[:, None]).to(dtype).contiguous()
-        self.W, self.b = [], []
+        self.W, self.b, self.Wf = [], [], []
         for k, (W, b) in enumerate(weights):
             W = W.detach().float()
             if k == 0 and W.shape[0] < self.xs.shape[1]:
@@ -315,9 +315,16 @@ class GCNInference:
             bp = torch.zeros(padded)
             bp[:out] = b.detach().float().cpu()
             self.W.append(Wp.to(self.dev, dtype).contiguous())
+            self.Wf.append(Wp.to(self.dev).contiguous())        # fp32 master: lin_fwd stages it itself
             self.b.append(bp.to(self.dev).contiguous())
         self.out_dim = weights[-1][0].shape[1]
         cuda = self.dev.type == "cuda"
+        # GPU: every transform on the hand-written MFMA layer (lin_fwd, fp16 / bf16 matrix
+        # cores, the D^-1/2 row scale of the next gather in its epilogue) into fixed buffers
+        self._lin = cuda and dtype in (torch.float16, torch.bfloat16)
+        if self._lin:
+            self.z = [torch.zeros(g.n, W.shape[1], dtype=dtype, device=self.dev) for W in self.Wf]
+            self.dinv32 = self.ng.dinv.float().contiguous()
         self._graph = StepGraph(self._forward, warmup=2, enabled=cuda if capture is None else capture and cuda,
                                 device=self.dev)
 
@@ -330,11 +337,15 @@ class GCNInference:
         h = self.xs
         L = len(self.W)
         for k in range(L):
-            z = h @ self.W[k]
-            if k > 0:
-                # one elementwise pass over the narrow Z is cheaper than a per-edge
-                # column-scale load in the gather (measured: 4.97 vs 5.47 ms on reddit)
-                z = z * self.ng.dinv[:, None].to(z.dtype)
+            if self._lin:
+                # Z = rs * (H W) on the MFMA layer; rs = D^-1/2 folded into the epilogue
+                # (the input features are pre-scaled once, so layer 1 has no row scale)
+                z = lin_fwd(h, self.Wf[k], None, K1=self.Wf[k].shape[0],
+                            rscale=self.dinv32 if k > 0 else None, out=self.z[k])
+            else:
+                z = h @ self.W[k]
+                if k > 0:
+                    z = z * self.ng.dinv[:, None].to(z.dtype)
             h = aggregate(z, self.ng, prescaled=True, bias=self.b[k], relu=k < L - 1)
         return h
 

@@ -65,7 +65,9 @@ def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = No
             step=0, row0: int = 0, rscale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
             ldy: Optional[int] = None, idx1: Optional[torch.Tensor] = None, n: Optional[int] = None,
             tail: Optional[torch.Tensor] = None, nsplit: Optional[int] = None, tk: int = 1) -> torch.Tensor:
-    """``out[:, :N] = epi([x1[:, :K1] | x2[:, :K2]] @ W + bias)`` in bf16 (columns N..ldy zero).
+    """``out[:, :N] = epi([x1[:, :K1] | x2[:, :K2]] @ W + bias)`` in bf16 (columns N..ldy zero);
+    fp16 operands (``x1`` fp16, GPU) run the same kernel on the fp16 matrix cores (the
+    inference path: no dropout, no fp32 tail).
 
     ``W``: fp32 [K1 + K2, N]; ``step``: int or device int32[1] (read at launch time);
     ``idx1`` (int32): row r reads ``x1[idx1[r]]`` (gather-on-load); ``n``: output rows
@@ -83,9 +85,10 @@ def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = No
     if tail is not None:
         if nsplit is None or nsplit % 4 or (N - nsplit) % tk or tail.numel() < (N - nsplit) * n:
             raise ValueError("lin_fwd tail: nsplit %% 4 == 0 and [%d, n, %d] fp32 planes needed" % ((N - nsplit) // tk, tk))
+    et = 1 if x1.dtype == torch.float16 else 0        # fp16 storage: the inference path
     if out is None:
         ldy = ldy or ((N if tail is None else nsplit) + 7) // 8 * 8
-        out = torch.empty(n, ldy, dtype=torch.bfloat16, device=x1.device)
+        out = torch.empty(n, ldy, dtype=torch.float16 if et else torch.bfloat16, device=x1.device)
     if checks.enabled():
         checks.index(idx1, x1.shape[0], "lin_fwd idx1")
         if idx1 is None:
@@ -101,7 +104,7 @@ def lin_fwd(x1: torch.Tensor, W: torch.Tensor, bias: Optional[torch.Tensor] = No
                                       K2, W.data_ptr(), N, _ptr(bias), out.data_ptr(), out.stride(0), n, int(relu),
                                       float(p), int(key[0]), int(key[1]), sv, int(row0), sp, _ptr(rscale), _st(x1),
                                       idx1=_ptr(idx1), wimg=img.data_ptr(), yf=_ptr(tail),
-                                      nsplit=int(nsplit or 0), tk=int(tk))
+                                      nsplit=int(nsplit or 0), tk=int(tk), et=et)
         _check(rc, "lin_fwd")
         return out
     a = x1[idx1.long()] if idx1 is not None else x1[:n]

@@ -43,13 +43,19 @@ class _MMDHip(torch.autograd.Function):
         step = torch.zeros(2, dtype=torch.int32, device=dev)
         st = torch.cuda.current_stream(dev).cuda_stream
         inv = 1.0 / (N * N)
-        hip.mmd(2, D, P.data_ptr(), T.data_ptr(), gradp.data_ptr(), lpart.data_ptr(), N, R,
-                row_tiles, n_chunks, tpc, 0.0, st)
-        hip.loss_finalize(lpart.data_ptr(), row_tiles * n_chunks, tt.data_ptr(), last.data_ptr(),
+        pn = (P * P).sum(1).contiguous()
+        tn = (T * T).sum(1).contiguous()
+        if hip.mmd_supported_d(D):          # constant true-true block
+            hip.mmd(2, D, P.data_ptr(), T.data_ptr(), gradp.data_ptr(), lpart.data_ptr(), N, R,
+                    row_tiles, n_chunks, tpc, 0.0, st)
+            tt_parts = row_tiles * n_chunks
+        else:                               # wide joints: the matrix-core kernel's mode 2
+            hip.mmd_mfma(2, D, T.data_ptr(), T.data_ptr(), tn.data_ptr(), tn.data_ptr(), gradp.data_ptr(),
+                         lpart.data_ptr(), N, R, mf_chunks, mf_tpc, 0.0, st)
+            tt_parts = mf_rb * mf_chunks
+        hip.loss_finalize(lpart.data_ptr(), tt_parts, tt.data_ptr(), last.data_ptr(),
                           acc.data_ptr(), inv, 2, 0, 0, step.data_ptr(), 0, R, st)
         if kernel == "mfma":
-            pn = (P * P).sum(1).contiguous()
-            tn = (T * T).sum(1).contiguous()
             hip.mmd_mfma(0, D, P.data_ptr(), T.data_ptr(), pn.data_ptr(), tn.data_ptr(), gradp.data_ptr(),
                          lpart.data_ptr(), N, R, mf_chunks, mf_tpc, 4.0 * inv, st)
             parts, chunks = mf_rb * mf_chunks, mf_chunks

@@ -61,6 +61,11 @@ def _rows(src: torch.Tensor, dst: torch.Tensor, src_idx=None, dst_idx=None, mode
             checks.rows(src, rows, "halo rows src")
         if dst_idx is None:
             checks.rows(dst, rows, "halo rows dst")
+    if mode == 0 and (dst.shape[1] * dst.element_size()) % 4:
+        # the row kernel copies whole 4-byte words: a row of odd bf16 width would lose its
+        # last element on the GPU (pad the column group to 4 bytes)
+        raise ValueError("halo row copy: %d-byte rows are not a multiple of 4 bytes"
+                         % (dst.shape[1] * dst.element_size()))
     if dst.is_cuda:
         from .. import native
         words = dst.shape[1] if mode else dst.shape[1] * dst.element_size() // 4

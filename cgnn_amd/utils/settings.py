@@ -17,6 +17,12 @@ New (not in the reference):
                                 dropped (0 = the reference's drop-only behaviour;
                                 the reference re-runs only its polynomial generator,
                                 generators.py:165-178)
+  * ``long_n_min``           -- runs with MORE samples than this (possible once
+                                ``max_nb_points`` is raised, or ``None`` = no
+                                subsampling) train on the sample-sharded long-N
+                                trainer: the samples split over the ranks of the
+                                process group (engine/sharded.py; default 1500, the
+                                reference's cap, CGNN.py:183-185)
 
 Every field can also be overridden from the environment as ``CGNN_<NAME>``
 (e.g. ``CGNN_NB_RUNS=8``) when the singleton is created.
@@ -53,7 +59,8 @@ class DefaultSettings(object):
                  "compat_remove_cycles",
                  "batch_models",
                  "verbose",
-                 "max_retries")
+                 "max_retries",
+                 "long_n_min")
 
     def __init__(self):
         self.NB_RUNS = 32
@@ -80,6 +87,7 @@ class DefaultSettings(object):
         self.batch_models = 256
         self.verbose = False
         self.max_retries = 0
+        self.long_n_min = 1500
         self._apply_env()
 
     def _apply_env(self):
@@ -97,6 +105,8 @@ class DefaultSettings(object):
                 val = float(raw)
             elif name == "device_ids":
                 val = tuple(int(x) for x in raw.split(",") if x.strip())
+            elif name == "max_nb_points" and raw.lower() in ("none", "0", ""):
+                val = None
             else:
                 val = raw
             setattr(self, name, val)
@@ -117,7 +127,7 @@ class DefaultSettings(object):
             gpu_offset=int(g("gpu_offset", self.GPU_OFFSET)),
             learning_rate=float(g("learning_rate", self.learning_rate)),
             init_std=float(g("init_std", self.init_weights)),
-            max_nb_points=int(g("max_nb_points", self.max_nb_points)),
+            max_nb_points=_opt_int(g("max_nb_points", self.max_nb_points)),
             h_layer_dim=int(g("h_layer_dim", self.h_layer_dim)),
             train_epochs=int(g("train_epochs", self.train_epochs)),
             test_epochs=int(g("test_epochs", self.test_epochs)),
@@ -130,11 +140,16 @@ class DefaultSettings(object):
             batch_models=int(g("batch_models", self.batch_models)),
             verbose=bool(g("verbose", self.verbose)),
             max_retries=int(g("max_retries", self.max_retries)),
+            long_n_min=int(g("long_n_min", self.long_n_min)),
         )
 
     def __repr__(self):
         return "DefaultSettings(%s)" % ", ".join(
             "%s=%r" % (k, getattr(self, k)) for k in self.__slots__)
+
+
+def _opt_int(v) -> Optional[int]:
+    return None if v is None else int(v)
 
 
 def _as_tuple(v) -> Optional[Tuple[int, ...]]:
@@ -155,7 +170,7 @@ class RunConfig:
     gpu_offset: int = 0
     learning_rate: float = 0.01
     init_std: float = 0.05
-    max_nb_points: int = 1500
+    max_nb_points: Optional[int] = 1500      # None: no subsampling
     h_layer_dim: int = 20
     train_epochs: int = 1000
     test_epochs: int = 500
@@ -168,6 +183,7 @@ class RunConfig:
     batch_models: int = 256
     verbose: bool = False
     max_retries: int = 0
+    long_n_min: int = 1500
 
     def replace(self, **kw) -> "RunConfig":
         return dataclasses.replace(self, **kw)

@@ -42,6 +42,8 @@ def test_bench_gloo_ranks_print_one_json_line(nproc, launcher):
     assert out["n_gpus"] == nproc and out["steps"] == 2 and out["warmup"] == 1
     assert out["value"] > 0 and abs(out["value"] * out["ms_per_step"] / 1000.0 - 1.0) < 1e-3
     assert out["config"]["parallelism"] == "graph-rowpart%d" % nproc
+    # the process group that ran it (checked by the pre-timing collective self-test)
+    assert out["backend"] == "gloo" and out["world_size"] == nproc
 
 
 def test_bench_rejects_rank_count_mismatch():

@@ -1,0 +1,135 @@
+"""CGNN beyond the narrow shapes: causal graphs with more than 64 variables and any
+``h_layer_dim`` (the reference builds one MLP per node for any d and h,
+/root/reference/Code/cgnn/CGNN.py:63-90; its generator defaults to 200 variables,
+generators/random_graph_generator.py:26).  Device trainers vs the fp64 oracle."""
+import numpy as np
+import pytest
+import torch
+
+from cgnn_amd import native
+from cgnn_amd.engine.batch import DeviceTrainer, device_supported, padded_dim
+from cgnn_amd.engine.program import program_for_dag
+from cgnn_amd.engine.reference import ReferenceTrainer, mmd_loss_dense
+from cgnn_amd.utils.graph import DirectedGraph
+from cgnn_amd.utils.philox import model_key
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_dag(d, seed, max_par=3):
+    rng = np.random.default_rng(seed)
+    g = DirectedGraph()
+    names = ["V%d" % k for k in range(d)]
+    for k in range(1, d):
+        for p in rng.choice(k, size=min(k, int(rng.integers(1, max_par + 1))), replace=False):
+            g.add(names[int(p)], names[k])
+    return g
+
+
+def _data(d, N, seed):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((d, N)).astype(np.float32)
+    x[1:] += 0.5 * x[:-1]
+    return x
+
+
+@pytest.mark.parametrize("N,d", [(300, 100), (130, 200), (97, 256)])
+def test_wide_mmd_matches_oracle(N, d):
+    from cgnn_amd.ops.mmd import mmd_loss
+    torch.manual_seed(d)
+    R = 2
+    pred = torch.randn(R, N, d, dtype=torch.float64) * 0.3
+    true = torch.randn(R, N, d, dtype=torch.float64) * 0.3 + 0.05
+    ref_l, ref_g = [], []
+    for r in range(R):
+        p = pred[r].clone().requires_grad_(True)
+        L = mmd_loss_dense(p, true[r])
+        (g,) = torch.autograd.grad(L, p)
+        ref_l.append(float(L))
+        ref_g.append(g)
+    pg = pred.float().cuda().requires_grad_(True)
+    out = mmd_loss(pg, true.float().cuda(), kernel="auto")
+    out.sum().backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref_l, rtol=5e-4, atol=5e-5)
+    gref = torch.stack(ref_g).numpy()
+    np.testing.assert_allclose(pg.grad.cpu().numpy(), gref, rtol=3e-3, atol=3e-3 * np.abs(gref).max())
+
+
+@pytest.mark.parametrize("d,H", [(100, 25), (100, 100), (200, 25), (200, 100)])
+def test_wide_dag_trainer_matches_oracle(d, H):
+    g = _random_dag(d, seed=d + H)
+    prog = program_for_dag(g, H)
+    assert padded_dim(d) > 64 and device_supported(d, H, prog.max_in)
+    N = 160
+    datas = [_data(d, N, s) for s in range(2)]
+    keys = [model_key(13, "wide", r) for r in range(2)]
+    ref = ReferenceTrainer([prog] * 2, datas, keys, H)
+    ref_scores = ref.run(4, 2)
+    dev = DeviceTrainer([prog] * 2, datas, keys, H, "cuda:0", record_history=4, graph_chunk=2)
+    assert dev.mmd_kernel == "mfma"
+    scores = dev.run(4, 2)
+    np.testing.assert_allclose(dev.history(), np.array(ref.loss_history), rtol=3e-3, atol=1e-5)
+    np.testing.assert_allclose(scores, ref_scores, rtol=3e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("H", [7, 25, 100])
+def test_generic_width_backward_small_graph_matches_oracle(H):
+    """A hidden width with no compiled generator kernel on a narrow graph."""
+    g = DirectedGraph()
+    for a, b in [("A", "B"), ("A", "C"), ("B", "D"), ("C", "D")]:
+        g.add(a, b)
+    prog = program_for_dag(g, H)
+    datas = [_data(4, 200, s) for s in range(3)]
+    keys = [model_key(2, "h", r) for r in range(3)]
+    ref = ReferenceTrainer([prog] * 3, datas, keys, H).run(5, 3)
+    got = DeviceTrainer([prog] * 3, datas, keys, H, "cuda:0").run(5, 3)
+    np.testing.assert_allclose(got, ref, rtol=3e-3, atol=1e-5)
+
+
+def test_generic_backward_bitwise_equals_specialised(monkeypatch):
+    """For a compiled H the generic-width backward is the same arithmetic in the same
+    order: scores are bitwise equal."""
+    g = _random_dag(12, seed=3)
+    prog = program_for_dag(g, 20)
+    datas = [_data(12, 300, s) for s in range(2)]
+    keys = [model_key(4, "gb", r) for r in range(2)]
+    a = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0")
+    assert a.bwd_variant == 1
+    sa = a.run(10, 4)
+    monkeypatch.setenv("CGNN_GEN_BWD_GENERIC", "1")
+    b = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0")
+    assert b.bwd_variant == 2
+    np.testing.assert_array_equal(b.run(10, 4), sa)
+
+
+def test_wide_fourier_mmd_matches_oracle():
+    g = _random_dag(90, seed=5)
+    prog = program_for_dag(g, 20)
+    datas = [_data(90, 150, s) for s in range(2)]
+    keys = [model_key(6, "wf", r) for r in range(2)]
+    kw = dict(use_fast_mmd=True, nb_vectors=40)
+    ref = ReferenceTrainer([prog] * 2, datas, keys, 20, **kw).run(4, 2)
+    got = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0", **kw).run(4, 2)
+    np.testing.assert_allclose(got, ref, rtol=3e-3, atol=1e-5)
+
+
+def test_200_variable_generated_graph_orients_on_gpu(monkeypatch):
+    """RandomGraphGenerator's default 200-variable graph through the public API on the
+    GPU (short schedule: the point is the shape, not the statistics); no batch may take
+    the CPU fallback."""
+    import cgnn
+    from cgnn_amd.engine import scorer
+    from cgnn_amd.generators import RandomGraphGenerator
+
+    def no_fallback(*a, **k):
+        raise AssertionError("a 200-variable batch fell back to the CPU path")
+    monkeypatch.setattr(scorer, "_run_reference", no_fallback)
+    gen = RandomGraphGenerator(num_nodes=200, number_points=300, seed=0)
+    graph, data = gen.generate(gen_cat=False)[:2]
+    assert len(graph.get_list_nodes()) >= 200       # the last layer may overshoot (reference behaviour)
+    out = cgnn.CGNN(backend="TensorFlow").orient_directed_graph(
+        data, graph, nb_runs=2, train_epochs=3, test_epochs=2, h_layer_dim=20, gpu=True)
+    assert isinstance(out, DirectedGraph)
+    assert len(out.get_list_edges()) == len(graph.get_list_edges())
+    assert not out.is_cyclic()
+    assert native.hip() is not None

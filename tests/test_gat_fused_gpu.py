@@ -18,27 +18,90 @@ def _cuda(*ts):
     return [t.cuda() if t is not None else None for t in ts]
 
 
+def _ring_graph(n, deg, seed):
+    from cgnn_amd.gnn.gat import GraphCSR
+    g = torch.Generator().manual_seed(seed)
+    d = torch.randint(1, deg + 1, (n,), generator=g)
+    d[::17] = 0                                            # some rows without edges
+    rp = torch.zeros(n + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(d, 0)
+    col = torch.randint(0, n, (int(rp[-1]),), generator=g, dtype=torch.int64)
+    return GraphCSR(rp.to(torch.int32), col.to(torch.int32), n)
+
+
 @pytest.mark.parametrize("F,p,row0", [(128, 0.5, 0), (256, 0.3, 1000), (32, 0.0, 7)])
-def test_act_fwd_bwd_match_reference(F, p, row0):
+def test_fused_activation_fwd_bwd_match_reference(F, p, row0):
+    """The hidden layer's activation runs inside the aggregation kernels on a GPU: the
+    forward writes bf16(dropout(elu(out + b))) (act_fwd's CPU reference), the row half of
+    the backward makes dout = dH * mask * elu'(out + b) and db (act_bwd's)."""
+    from cgnn_amd.gnn.gat_fused import _agg_fwd, _agg_rows
     torch.manual_seed(0)
-    n = 777
-    out = torch.randn(n, F) * 2
+    n, K = 777, F // 32
+    Fh = F // K
+    g = _ring_graph(n, 9, 1)
+    Wh = (torch.randn(n, F) * 2).to(torch.bfloat16)
+    s_src, s_dst = torch.randn(n, K), torch.randn(n, K)
     b = torch.randn(F) * 0.1
     key, step = (11, 22), 5
+    out, _ = _agg_fwd(Wh, s_src, s_dst, g, K, Fh)
     H = torch.zeros(n, F, dtype=torch.bfloat16)
     act_fwd(out, b, H, p, key, step, row0)
     Hg = torch.zeros(n, F, dtype=torch.bfloat16, device="cuda")
-    act_fwd(out.cuda(), b.cuda(), Hg, p, key, torch.tensor([step], dtype=torch.int32, device="cuda"), row0)
-    np.testing.assert_allclose(Hg.cpu().float().numpy(), H.float().numpy(), rtol=8e-3, atol=1e-6)
+    stp = torch.tensor([step], dtype=torch.int32, device="cuda")
+    gg = _ring_graph(n, 9, 1)
+    gg.rowptr, gg.col = gg.rowptr.cuda(), gg.col.cuda()
+    outg, lse = _agg_fwd(*_cuda(Wh, s_src, s_dst), gg, K, Fh, q=torch.empty(n, F, dtype=torch.bfloat16, device="cuda"),
+                         act=(b.cuda(), Hg, p, key, stp, row0))
+    np.testing.assert_allclose(outg.cpu().numpy(), out.numpy(), rtol=1e-4, atol=1e-4)
+    # the GPU activation reads its own fp32 out: compare against the reference on it
+    Hr = torch.zeros(n, F, dtype=torch.bfloat16)
+    act_fwd(outg.cpu(), b, Hr, p, key, step, row0)
+    np.testing.assert_allclose(Hg.cpu().float().numpy(), Hr.float().numpy(), rtol=8e-3, atol=1e-6)
+    np.testing.assert_allclose(Hg.cpu().float().numpy(), H.float().numpy(), rtol=2e-2, atol=1e-3)
     dH = torch.randn(n, F).to(torch.bfloat16)
     dout, doutb, db = torch.zeros(n, F), torch.zeros(n, F, dtype=torch.bfloat16), torch.zeros(F)
-    act_bwd(dH, out, b, p, key, step, row0, dout, doutb, db)
-    dg, dgb, dbg = torch.zeros(n, F, device="cuda"), torch.zeros(n, F, dtype=torch.bfloat16, device="cuda"), \
-        torch.zeros(F, device="cuda")
-    act_bwd(dH.cuda(), out.cuda(), b.cuda(), p, key, step, row0, dg, dgb, dbg)
-    np.testing.assert_allclose(dg.cpu().numpy(), dout.numpy(), rtol=1e-5, atol=1e-6)
+    act_bwd(dH, outg.cpu(), b, p, key, step, row0, dout, doutb, db)
+    dgb, dbg = torch.zeros(n, F, dtype=torch.bfloat16, device="cuda"), torch.zeros(F, device="cuda")
+    rstat = torch.empty(n, K, 4, device="cuda")
+    q = torch.zeros(n, F, dtype=torch.bfloat16, device="cuda")
+    _agg_rows(outg, q, lse, s_dst.cuda(), None, K, Fh, rstat, dH=dH.cuda(),
+              act=(dgb, b.cuda(), dbg, p, key, stp, row0), ds_dst=torch.empty(n, K, device="cuda"))
     np.testing.assert_allclose(dgb.cpu().float().numpy(), doutb.float().numpy(), rtol=8e-3, atol=1e-6)
     np.testing.assert_allclose(dbg.cpu().numpy(), db.numpy(), rtol=1e-4, atol=1e-4)
+    D = (dgb.float() * outg).view(n, K, Fh).sum(-1)
+    np.testing.assert_allclose(rstat[:, :, 2].cpu().numpy(), D.cpu().numpy(), rtol=1e-4, atol=1e-4)
+    # (s_dst, lse) are handed to the column half in log2 units
+    L2E = 1.4426950408889634
+    np.testing.assert_allclose(rstat[:, :, 0].cpu().numpy(), s_dst.numpy() * L2E, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(rstat[:, :, 1].cpu().numpy(), lse.cpu().numpy() * L2E, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("K,Fh", [(4, 32), (1, 48), (8, 16)])
+def test_row_half_split_equals_edge_sum(K, Fh):
+    """d s_dst from the forward's LeakyReLU split (-0.8 <dout, q>) equals the per-edge sum
+    sum_j alpha_ij (dalpha_ij - D_i) LeakyReLU'_ij of the autograd reference."""
+    from cgnn_amd.gnn.gat import _gat_aggregate_torch
+    from cgnn_amd.gnn.gat_fused import _agg_fwd, _agg_rows
+    torch.manual_seed(3)
+    n = 1500
+    HF = K * Fh
+    g = _ring_graph(n, 20, 2)
+    Wh = torch.randn(n, HF).to(torch.bfloat16)
+    s_src, s_dst = torch.randn(n, K), torch.randn(n, K)
+    dout = torch.randn(n, HF).to(torch.bfloat16)
+    with torch.enable_grad():
+        c = s_dst.clone().requires_grad_()
+        o = _gat_aggregate_torch(Wh.float(), s_src, c, g, K, Fh)
+        (ref,) = torch.autograd.grad(o, (c,), dout.float())
+    gg = _ring_graph(n, 20, 2)
+    gg.rowptr, gg.col = gg.rowptr.cuda(), gg.col.cuda()
+    q = torch.empty(n, HF, dtype=torch.bfloat16, device="cuda")
+    out, lse = _agg_fwd(*_cuda(Wh, s_src, s_dst), gg, K, Fh, q=q)
+    rstat = torch.empty(n, K, 4, device="cuda")
+    dsd = torch.empty(n, K, device="cuda")
+    _agg_rows(out, q, lse, s_dst.cuda(), None, K, Fh, rstat, dout=dout.cuda(), ds_dst=dsd)
+    scale = ref.abs().max().item()
+    np.testing.assert_allclose(dsd.cpu().numpy(), ref.numpy(), rtol=2e-2, atol=1e-2 * scale)
 
 
 @pytest.mark.parametrize("C,ld", [(47, 48), (172, 176), (7, 8), (256, 256)])

@@ -133,6 +133,36 @@ def test_gcn_steps_match_cpu(name, fused):
     assert dp < 2e-3, dp
 
 
+@pytest.mark.parametrize("reorder", [False, True])
+def test_gcn_benched_config_matches_cpu(reorder):
+    """The composed path bench.py times -- hidden 256 (the fused MFMA dense forward and
+    backward: gcn_dense_fwd / gcn_fused_bwd, slab_sum straight into the flat gradient),
+    layer 2 aggregated at the train rows, layer 1 at the rows with a train neighbour,
+    dropout 0.5 -- against the fp32 CPU reference of the same bf16-stored arithmetic
+    over 4 epochs (the benched graph shape, scaled down; reorder pass on and off)."""
+    g = synthetic("ogbn-products", seed=3, device="cpu", scale=0.004)
+    cpu = GCNTrainer(g, hidden=256, rank=0, world=1, reorder=reorder)
+    gpu = GCNTrainer(g.to("cuda:0"), hidden=256, rank=0, world=1, reorder=reorder)
+    assert gpu.fused and gpu.fused_bwd
+    assert gpu._l2 is not None and gpu._l1 is not None       # train-row layer 2, train-neighbour layer 1
+    lc, lg = [], []
+    for _ in range(4):
+        cpu.train_step()
+        gpu.train_step()
+        lc.append(cpu.train_loss())
+        lg.append(gpu.train_loss())
+    np.testing.assert_allclose(lg, lc, rtol=3e-3)
+    a, b = cpu.evaluate(), gpu.evaluate()
+    dp = (gpu.params.cpu() - cpu.params).abs()
+    print("gcn-256 reorder=%s: losses cpu %s gpu %s, val %.4f / %.4f, max |dparam| %.2e, >1e-4: %.4f"
+          % (reorder, lc, lg, a["val_acc"], b["val_acc"], dp.max().item(), (dp > 1e-4).float().mean().item()))
+    assert abs(a["train_loss"] - b["train_loss"]) < 5e-3 * max(a["train_loss"], 1e-3)
+    assert abs(a["val_acc"] - b["val_acc"]) < 0.01
+    # Adam moves a weight by <= lr per step; a wrong gradient term shows as O(lr) on many
+    assert (dp > 2e-3).float().mean().item() < 1e-3, (dp > 2e-3).float().mean().item()
+    assert dp.max().item() < 4 * 0.01
+
+
 def test_gcn_learns_products_shape_small():
     g = synthetic("ogbn-products", seed=0, device="cuda:0", scale=0.01, feat_noise=4.0)
     tr = GCNTrainer(g, hidden=128)
@@ -218,9 +248,9 @@ def test_sage_minibatch_learns_gpu():
 @pytest.mark.parametrize("K,Fh", [(4, 16), (1, 64), (8, 32), (3, 8), (1, 176), (1, 40)])
 def test_gat_kernels_match_torch_autograd(K, Fh, lowp):
     """HIP GAT forward / backward vs PyTorch autograd in fp64.  lowp: the gathered
-    rows (Wh, and dout in the column backward) are stored bf16 -- the reference then
-    takes bf16-rounded Wh and dout, and the tolerance allows the rounding of dout
-    that the row kernel (fp32 dout) does not do."""
+    rows (Wh, dout) are stored bf16 -- the reference then takes bf16-rounded Wh and
+    dout; the row half also reads the forward's LeakyReLU split q stored bf16, one more
+    rounding inside d s_dst = -0.8 <dout, q> (its tolerance is 4e-3)."""
     from cgnn_amd.gnn.gat import GraphCSR, gat_aggregate
     n = 700
     rng = np.random.default_rng(K * 100 + Fh)
@@ -240,8 +270,8 @@ def test_gat_kernels_match_torch_autograd(K, Fh, lowp):
         out = gat_aggregate(a, b, c, g, K, Fh, lowp=lowp)
         out.backward(gout.to(dev, out.dtype))
         res.append([t.detach().double().cpu() for t in (out, a.grad, b.grad, c.grad)])
-    tol = 2e-3 if lowp else 1e-4
     for x, y, name in zip(res[1], res[0], ("out", "dWh", "ds_src", "ds_dst")):
+        tol = (4e-3 if name == "ds_dst" else 2e-3) if lowp else 1e-4
         scale = y.abs().max().item()
         np.testing.assert_allclose(x.numpy(), y.numpy(), rtol=0, atol=tol * scale + 1e-6, err_msg=name)
 
@@ -339,6 +369,7 @@ def test_gcn_inference_fp16_graph_matches_cpu():
     model.eval()
     ref = GCNInference.from_model(g, model)()                       # fp32 CPU reference
     inf = GCNInference.from_model(g.to("cuda:0"), model.to("cuda:0"), dtype=torch.float16)
+    assert inf._lin                       # transforms on the hand-written fp16 MFMA layer
     for _ in range(4):                                              # warm-up, capture, replays
         got = inf()
     assert inf._graph.graph is not None

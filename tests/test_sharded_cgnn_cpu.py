@@ -65,3 +65,51 @@ def test_sample_sharded_cgnn_matches_single_process(N, world, kind):
     if N <= 1000:      # and the unsharded oracle trainer (exact dense MMD) agrees
         ref = ReferenceTrainer([prog], [data], [model_key(3, kind)], 8).run(2, 1)
         np.testing.assert_allclose(single, ref, rtol=1e-9)
+
+
+def _pair_data(N):
+    rng = np.random.default_rng(1)
+    a = rng.standard_normal(N)
+    b = np.tanh(a) + 0.3 * rng.standard_normal(N)
+    return a, b
+
+
+_KW = dict(nb_runs=1, train_epochs=1, test_epochs=1, max_nb_points=None, gpu=False, h_layer_dim=8)
+
+
+def _api_worker(rank, world, port, N, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import cgnn
+    a, b = _pair_data(N)
+    out[rank] = cgnn.GNN().predict_proba(a, b, **_KW)
+    dist.destroy_process_group()
+
+
+def test_public_api_long_n_pairwise_sample_sharded(monkeypatch):
+    """``GNN().predict_proba`` with subsampling off (max_nb_points=None) and N (6000) above
+    ``long_n_min``: the jobs go to the sample-sharded trainer; 2 gloo ranks (each owning
+    half the samples of every job) give the one-process score."""
+    import cgnn
+    from cgnn_amd.engine import scorer
+    N = 6000
+    calls = []
+    real = scorer._run_long
+
+    def spy(jobs, cfg):
+        calls.append((len(jobs), jobs[0].data.shape))
+        return real(jobs, cfg)
+    monkeypatch.setattr(scorer, "_run_long", spy)
+    a, b = _pair_data(N)
+    single = cgnn.GNN().predict_proba(a, b, **_KW)
+    assert calls == [(2, (2, N))], calls             # the run's A->B and B->A models, all samples
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_api_worker, args=(2, _free_port(), N, out), nprocs=2, join=True)
+    for r in range(2):
+        np.testing.assert_allclose(out[r], single, rtol=1e-9)
+    # the reference's cap (1500) keeps the batched engine
+    calls.clear()
+    cgnn.GNN().predict_proba(a[:3000], b[:3000], **dict(_KW, max_nb_points=1500))
+    assert calls == []
