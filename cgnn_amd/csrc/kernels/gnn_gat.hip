@@ -697,11 +697,11 @@ int lanes_for(int HF) {
 }
 }  // namespace
 
-// edges per gather batch: 4 (measured on the products epoch: 12.73 ms at 4, 13.0 at 8,
-// 14.4 at 16 -- a wider batch costs more occupancy than its rows in flight buy;
-// A/B with -DCGNN_GAT_EC=N)
+// edges per gather batch: 2 (measured on the products epoch: 11.80 ms at 2, 12.66 at 4,
+// 13.0 at 8, 14.4 at 16 -- the gathers are latency-bound and a wider batch costs more
+// occupancy than its rows in flight buy; A/B with -DCGNN_GAT_EC=N)
 #ifndef CGNN_GAT_EC
-#define CGNN_GAT_EC 4
+#define CGNN_GAT_EC 2
 #endif
 #define GAT_EC_OF(L) ((L) < CGNN_GAT_EC ? (L) : CGNN_GAT_EC)
 

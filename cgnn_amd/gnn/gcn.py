@@ -105,7 +105,7 @@ class GCNTrainer:
                  weight_decay: float = 0.0, seed: int = 0, rank: Optional[int] = None,
                  world: Optional[int] = None, fused: bool = True, align_rows: Optional[bool] = None,
                  halo: Optional[bool] = None, capture: Optional[bool] = None, reorder: bool = False,
-                 align_c: Optional[bool] = None):
+                 align_c: Optional[bool] = None, collectives: Optional[bool] = None):
         # reorder=True: relabel the nodes for gather locality first (data.reorder: LP
         # clusters + Cuthill-McKee, ~4-8 s of host C++ on the ogbn-products shape, part
         # of setup); the row partition of a multi-GPU run then cuts mostly between
@@ -119,6 +119,11 @@ class GCNTrainer:
             g, self.new_id = _reorder(g, seed=seed)
         self.rank = pdist.rank() if rank is None else rank
         self.world = pdist.world_size() if world is None else world
+        # the multi-rank code paths (exchanges, split aggregations, all-reduces): on with
+        # more than one rank; ``collectives=True`` forces them on a 1-rank process group
+        # (tests: the async RCCL exchange / stream-wait code without a second GPU)
+        self.multi = self.world > 1 if collectives is None else (
+            bool(collectives) and torch.distributed.is_available() and torch.distributed.is_initialized())
         self.dev = g.rowptr.device
         dev = self.dev
         self.F, self.C, self.hidden = g.n_features, g.n_classes, hidden
@@ -204,14 +209,14 @@ class GCNTrainer:
         # the dense forward (one 1024-thread, LDS-heavy block per CU) only starts as they
         # drain -- the kernel trace shows it stretched from 0.33 to 2.4 ms, no overlap won.
         self._side = None
-        pipe = (self.world == 1 and dev.type == "cuda" and not capture
+        pipe = (not self.multi and dev.type == "cuda" and not capture
                 and os.environ.get("CGNN_AX_PIPELINE", "0") != "0")
-        self.AX_next = torch.zeros_like(self.AX) if (self.world > 1 or pipe) else None
+        self.AX_next = torch.zeros_like(self.AX) if (self.multi or pipe) else None
         if pipe:
             self._side = torch.cuda.Stream(dev)
             self._ax_event = torch.cuda.Event()
         self._ax_ready = False
-        if self.world > 1:
+        if self.multi:
             # layer-2 aggregations split into edges whose source row this rank owns
             # (computed while the all-gather of the other ranks' rows is in flight) and
             # the remaining edges (after it), summed through an fp32 partial
@@ -220,8 +225,8 @@ class GCNTrainer:
         # compact dL/dlogits (train rows only) and the adjacency restricted to train columns
         self.gslot, self.rp_T, self.col_T, self.maxT = self._train_columns(g, per)
         self.Gc_loc = torch.zeros(self.maxT, self.ldc, **bf)
-        self.Gc = torch.zeros(self.maxT * self.world, self.ldc, **bf) if self.world > 1 else self.Gc_loc
-        self._bwd_overlap = self.world > 1 and os.environ.get("CGNN_BWD_OVERLAP", "1") != "0"
+        self.Gc = torch.zeros(self.maxT * self.world, self.ldc, **bf) if self.multi else self.Gc_loc
+        self._bwd_overlap = self.multi and os.environ.get("CGNN_BWD_OVERLAP", "1") != "0"
         if self._bwd_overlap:
             # backward aggregation split like the forward's: the edges to this rank's own
             # train rows (slots [rank * maxT, + maxT), read straight from Gc_loc) run while
@@ -243,12 +248,12 @@ class GCNTrainer:
         # initialised process group (the exchange plan is negotiated at setup).
         if halo is None:
             halo = self.world >= 4
-        self.halo = bool(halo) and self.world > 1 and torch.distributed.is_initialized()
+        self.halo = bool(halo) and self.multi and torch.distributed.is_initialized()
         if self.halo:
             self._setup_halo(r0, r1, per)
             self.Z2 = None
         else:
-            self.Z2 = torch.zeros(per * self.world, self.ldc, **bf) if self.world > 1 else self.Z2loc
+            self.Z2 = torch.zeros(per * self.world, self.ldc, **bf) if self.multi else self.Z2loc
         # Training epochs aggregate layer 2 only at the rows the loss reads (this rank's
         # train rows): the other rows' logits enter neither the loss nor any gradient, so
         # the update is the same (the output-node pruning of DGL's last message-flow
@@ -289,7 +294,7 @@ class GCNTrainer:
         # the replay measured 0.4 % SLOWER than eager launches (5.16 vs 5.14 ms, 2 x 40
         # epochs each).  Multi-GPU epochs are never captured (collectives, buffer swaps).
         from ..utils.hipgraph import StepGraph
-        cap_ok = dev.type == "cuda" and self.world == 1 and self.fused_bwd
+        cap_ok = dev.type == "cuda" and not self.multi and self.fused_bwd
         self._graph = StepGraph(self._train_body, enabled=bool(capture) and cap_ok, device=dev)
 
     def _split_local(self, r0, r1, rowptr=None, col=None):
@@ -379,7 +384,7 @@ class GCNTrainer:
             gslot=torch.full((1,), -1, dtype=torch.int32, device=dev) if placeholder
             else torch.arange(trows.numel(), dtype=torch.int32, device=dev))
         l2.plan = None
-        if self.world > 1:
+        if self.multi:
             l2.rp_loc, l2.col_loc, l2.rp_rem, col_rem = self._split_local(self.r0, self.r1, l2.rp, l2.col)
             if torch.distributed.is_initialized() and os.environ.get("CGNN_TRAIN_HALO", "1") != "0":
                 # a halo of its own: only the remote rows the train rows read travel in
@@ -451,7 +456,7 @@ class GCNTrainer:
 
     # ------------------------------------------------------------------ passes
     def _all_gather(self, out, inp):
-        if self.world > 1:
+        if self.multi:
             torch.distributed.all_gather_into_tensor(out, inp)
 
     def _aggregate_features(self, out, train: bool = False):
@@ -494,7 +499,7 @@ class GCNTrainer:
             torch.mul(y2, self.dinv[:, None], out=y2)
             self.Z2loc[:n] = y2.to(torch.bfloat16)
         l2 = self._l2 if train else None          # train rows only (see __init__)
-        if self.world > 1:
+        if self.multi:
             # the Z2 exchange is the epoch's one large transfer (up to [n, 48] bf16, 7/8
             # of it inbound at 8 ranks): the rank-local layer-2 edges and, in training, the
             # next epoch's layer-1 aggregation (parameter-independent) run while it is in flight
@@ -525,13 +530,13 @@ class GCNTrainer:
 
     def backward(self, stats):
         n, F, C = self.nloc, self.F, self.C
-        if self.world > 1 and self._bwd_overlap:
+        if self.multi and self._bwd_overlap:
             work = self._collective(torch.distributed.all_gather_into_tensor, self.Gc, self.Gc_loc)
             ops.spmm(self.rpT_loc, self.colT_loc, self.Gc_loc, C, out=self.part, out_dtype=torch.float32)
             work.wait()
             ops.spmm(self.rpT_rem, self.colT_rem, self.Gc, C, rscale=self.dinv, out=self.dY2, init=self.part)
         else:
-            if self.world > 1:
+            if self.multi:
                 torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc)
             ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
         self.gb2.copy_(stats[4:4 + C])
@@ -542,7 +547,7 @@ class GCNTrainer:
             _, _, _, self._gpart = ops.fused_bwd(self.AX, self.dY2, self.W1, self.b1, self.W2, n, F,
                                                  self.p, self.key, self._dropout_step(), self.r0,
                                                  self._gpart, grads=self.grads, grad_index=self._grad_index)
-            if self.world > 1:
+            if self.multi:
                 torch.distributed.all_reduce(self.grads)
             return
         self.gW2.copy_(_tsgemm(self.H1, self.dY2)[:, :C])
@@ -556,7 +561,7 @@ class GCNTrainer:
         g1 = _tsgemm(self.AX, self.dH1)               # rows 0..F-1: dW1, row F: db1 (ones column)
         self.gW1.copy_(g1[:F])
         self.gb1.copy_(g1[F])
-        if self.world > 1:
+        if self.multi:
             torch.distributed.all_reduce(self.grads)
 
     def _dropout_step(self):
@@ -583,7 +588,7 @@ class GCNTrainer:
     def evaluate(self):
         """Accuracies on train / valid / test (no dropout), reduced over ranks."""
         stats = self.forward(train=False).clone()
-        if self.world > 1:
+        if self.multi:
             torch.distributed.all_reduce(stats)
         s = stats.cpu().numpy()
         return {"train_loss": float(s[0]) / max(self.n_train, 1),
@@ -613,7 +618,7 @@ class GCNTrainer:
 
     def train_loss(self):
         s = self.last_stats.clone()
-        if self.world > 1:
+        if self.multi:
             torch.distributed.all_reduce(s)
         return float(s[0]) / max(self.n_train, 1)
 

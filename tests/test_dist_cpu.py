@@ -388,3 +388,27 @@ def test_sharded_fused_gat_without_train_halo_rank_without_train_rows():
              nprocs=world, join=True)
     for r in range(world):
         np.testing.assert_allclose(out[r][0], ref_losses, rtol=5e-4)
+
+
+@pytest.mark.parametrize("halo", [False, True])
+def test_gcn_forced_collectives_one_rank_equals_plain(halo):
+    """GCNTrainer(collectives=True) on a 1-rank group takes every multi-rank branch
+    (exchanges, split aggregation, gradient all-reduce) and reproduces the plain trainer
+    (the GPU variant of this test runs the same over RCCL, tests/test_rccl_gpu.py)."""
+    from cgnn_amd.gnn.data import synthetic
+    from cgnn_amd.gnn.gcn import GCNTrainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        g = synthetic("ogbn-products", seed=2, scale=0.001)
+        ref = GCNTrainer(g, hidden=64, rank=0, world=1)
+        forced = GCNTrainer(g, hidden=64, rank=0, world=1, collectives=True, halo=halo)
+        assert forced.multi and not ref.multi and forced.halo == halo
+        for _ in range(3):
+            ref.train_step()
+            forced.train_step()
+        assert abs(ref.train_loss() - forced.train_loss()) < 1e-4 * ref.train_loss()
+        np.testing.assert_allclose(forced.params.numpy(), ref.params.numpy(), atol=1e-4, rtol=0)
+        assert ref.evaluate() == pytest.approx(forced.evaluate(), abs=2e-3)
+    finally:
+        dist.destroy_process_group()

@@ -23,7 +23,13 @@ def main():
     ap.add_argument("--h", type=int, default=20)
     ap.add_argument("--train", type=int, default=20)
     ap.add_argument("--test", type=int, default=10)
+    ap.add_argument("--api", action="store_true",
+                    help="through the public API: cgnn.GNN().predict_proba(a, b) with max_nb_points=None "
+                         "(the scorer routes the long runs to the sample-sharded trainer)")
+    ap.add_argument("--runs", type=int, default=1, help="--api: nb_runs (2 models each)")
     a = ap.parse_args()
+    if a.api:
+        return api(a)
     from cgnn_amd.engine.program import program_for_dag, program_for_pair
     from cgnn_amd.engine.sharded import SampleShardedTrainer, shard_range
     from cgnn_amd.parallel import dist as pdist
@@ -66,6 +72,30 @@ def main():
                           "mmd_pairs_per_s_train": round(pairs * a.train / (t2 - t1), 1),
                           "exp_evals_per_s_train": round(7 * pairs * a.train / (t2 - t1), 1),
                           "score": float(score[0]), "setup_s": round(setup, 2)}), flush=True)
+
+
+def api(a):
+    import cgnn
+    from cgnn_amd.parallel import dist as pdist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        pdist.init_process_group("nccl")
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal(a.N)
+    y = np.tanh(x) + 0.3 * rng.standard_normal(a.N)
+    kw = dict(nb_runs=a.runs, train_epochs=a.train, test_epochs=a.test, max_nb_points=None, h_layer_dim=a.h)
+    cgnn.GNN().predict_proba(x[:4096], y[:4096], **dict(kw, train_epochs=2, test_epochs=1))   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s = cgnn.GNN().predict_proba(x, y, **kw)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if pdist.rank() == 0:
+        steps = a.train + a.test
+        print(json.dumps({"bench": "cgnn_long_n_api", "call": "cgnn.GNN().predict_proba", "N": a.N, "nb_runs": a.runs,
+                          "models": 2 * a.runs, "train_epochs": a.train, "test_epochs": a.test, "ranks": world,
+                          "seconds": round(dt, 3), "ms_per_step": round(1e3 * dt / steps, 3), "score": float(s),
+                          "direction_correct": bool(s > 0)}), flush=True)
 
 
 if __name__ == "__main__":
