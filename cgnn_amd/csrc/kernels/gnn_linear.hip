@@ -85,14 +85,18 @@ __device__ __forceinline__ f32x16 mma16(uint4 a, uint4 b, f32x16 c) {
 }
 
 // zero the elements [valid, 8) of a bf16x8 chunk (padding columns may hold anything,
-// and 0 * NaN would poison a product)
+// and 0 * NaN would poison a product); branch-free (selects), valid may be <= 0
 __device__ __forceinline__ uint4 keep_first(uint4 v, int valid) {
-  if (valid >= 8) return v;
+  // `valid` is loop-invariant in the callers' tile loops: without this empty asm, which
+  // ties it to the loaded data, LICM hoists the 4 masks of every unrolled k-step out of
+  // the loop (4 * KS live VGPRs -> scratch spills); with it they are computed as each
+  // load lands and die at once
+  asm volatile("" : "+v"(valid) : "v"(v.x));
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const int lo = 2 * e, hi = 2 * e + 1;
-    w[e] = (lo < valid ? (w[e] & 0xffffu) : 0u) | (hi < valid ? (w[e] & 0xffff0000u) : 0u);
+    const uint32_t lo = 2 * e < valid ? 0x0000ffffu : 0u, hi = 2 * e + 1 < valid ? 0xffff0000u : 0u;
+    w[e] &= lo | hi;
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
@@ -100,27 +104,31 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, int valid) {
 // 8 features [f0, f0 + 8) of row `row` of the virtual concatenation [X1 | X2]
 // (K1 % 8 == 0 when X2 is given, so a chunk never straddles the two); zeros past K1 + K2
 // idx1 (optional): X1 row of output row r is idx1[r] (gather-on-load: GraphSAGE's
-// first layer reads the seed / frontier rows straight out of the resident features)
+// first layer reads the seed / frontier rows straight out of the resident features).
+// Branch-free: every lane loads from a valid address (a chunk outside both operands
+// re-reads its row's first chunk) and the value is masked afterwards -- per-lane
+// branches in the unrolled k loop cost exec-mask saves that spilled the SGPR file.
 __device__ __forceinline__ uint4 load_cat8(const uint16_t* __restrict__ x1, int ld1, int K1,
                                            const uint16_t* __restrict__ x2, int ld2, int K2, int row, int f0,
                                            const int* __restrict__ idx1) {
-  if (f0 < K1) {
-    const size_t r1 = idx1 ? (size_t)idx1[row] : (size_t)row;
-    return keep_first(*reinterpret_cast<const uint4*>(x1 + r1 * ld1 + f0), K1 - f0);
-  }
+  const size_t r1 = idx1 ? (size_t)idx1[row] : (size_t)row;
   const int g = f0 - K1;
-  if (x2 && g < K2) return keep_first(*reinterpret_cast<const uint4*>(x2 + (size_t)row * ld2 + g), K2 - g);
-  return make_uint4(0u, 0u, 0u, 0u);
+  const bool in1 = f0 < K1;
+  const bool in2 = x2 != nullptr && !in1 && g < K2;
+  const uint16_t* p = in2 ? x2 + (size_t)row * ld2 + g : x1 + r1 * ld1 + (in1 ? f0 : 0);
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  return keep_first(v, in1 ? K1 - f0 : in2 ? K2 - g : 0);
 }
 
 // 8 gradient values [c0, c0 + 8) of row `row`, times the mask [Ym > 0] * mscale
 __device__ __forceinline__ uint4 load_masked8(const uint16_t* __restrict__ dY, int lddy,
                                               const uint16_t* __restrict__ Ym, int ldym, float mscale,
                                               int N, int row, int c0) {
-  if (c0 >= N) return make_uint4(0u, 0u, 0u, 0u);
-  uint4 g = keep_first(*reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + c0), N - c0);
+  // branch-free like load_cat8: chunks past N re-read the row's first chunk, then masked
+  const int cc = c0 < N ? c0 : 0;
+  const uint4 g = keep_first(*reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + cc), N - c0);
   if (!Ym && mscale == 1.f) return g;
-  const uint4 y = Ym ? *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + c0) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  const uint4 y = Ym ? *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + cc) : make_uint4(~0u, ~0u, ~0u, ~0u);
   uint32_t gw[4] = {g.x, g.y, g.z, g.w};
   const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
@@ -210,10 +218,15 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
   for (int tile = wave; tile < n_tiles; tile += n_waves) {
     const int row = tile * TILE + lr;
     const bool rv = row < n;
+    // fh is opaque per tile (empty asm) so the per-k-step offsets and validity selects
+    // derived from it are recomputed next to their loads instead of being hoisted out of
+    // the tile loop as 2 * KS live registers
+    int fh = 8 * h;
+    asm volatile("" : "+v"(fh));
     uint4 bx[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      bx[s] = rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h, idx1) : make_uint4(0u, 0u, 0u, 0u);
+      bx[s] = load_cat8(x1, ld1, K1, x2, ld2, K2, rv ? row : n - 1, 16 * s + fh, idx1);
     const float rs = (rv && rscale) ? rscale[row] : 1.f;
 #pragma unroll 1
     for (int t = 0; t < nt; ++t) {
@@ -289,10 +302,12 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
   for (int tile = wave; tile < n_tiles; tile += n_waves) {
     const int row = tile * TILE + lr;
     const bool rv = row < n;
+    int fh = 8 * h;                              // opaque per tile, as in lin_fwd
+    asm volatile("" : "+v"(fh));
     bf16x8 by[KN];
 #pragma unroll
     for (int s = 0; s < KN; ++s)
-      by[s] = as_bf16x8(rv ? load_masked8(dY, lddy, Ym, ldym, mscale, N, row, 16 * s + 8 * h) : make_uint4(0u, 0u, 0u, 0u));
+      by[s] = as_bf16x8(load_masked8(dY, lddy, Ym, ldym, mscale, N, rv ? row : n - 1, 16 * s + fh));
     const float rs = (rv && rscale) ? rscale[row] : 1.f;
 #pragma unroll 1
     for (int t = 0; t < nt; ++t) {

@@ -82,11 +82,18 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
     return out
 
 
-def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=None, init=None, gslot=None):
+_DB_INDEX = {}
+
+
+def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=None, init=None, gslot=None,
+            db_out=None):
     """Layer-2 aggregate + log-softmax + NLL.  Returns (stats[68] summed, G).
     ``init`` (optional fp32 [n, >=C]): partial sums of other edges.
     ``gslot`` (optional int32 [n]): G is compact -- row i (a train row, gslot[i] >= 0)
-    goes to G[gslot[i]], other rows (whose dlogits are zero) are not written."""
+    goes to G[gslot[i]], other rows (whose dlogits are zero) are not written.
+    ``db_out`` (optional fp32 [C], GPU): the per-class dlogits sums (the bias gradient,
+    stats[4:4 + C]) are also summed straight into it -- a second fixed-order pass over
+    the partials instead of a device-to-device copy."""
     if checks.enabled():
         checks.csr(rowptr, col, Z.shape[0], "spmm_ce")
         checks.rows(labels, rowptr.numel() - 1, "spmm_ce labels")
@@ -110,6 +117,13 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
                         gslot.data_ptr() if gslot is not None else 0)
         out = torch.empty(68, dtype=torch.float32, device=Z.device)
         slab_sum(stats, out)
+        if db_out is not None:
+            key = (Z.device, C)
+            idx = _DB_INDEX.get(key)
+            if idx is None:
+                c = torch.arange(68, dtype=torch.int32)
+                idx = _DB_INDEX[key] = torch.where((c >= 4) & (c < 4 + C), c - 4, -1).to(torch.int32).to(Z.device)
+            slab_sum(stats, db_out, index=idx)
         return out, G
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, C, dtype=torch.float32)

@@ -262,12 +262,13 @@ class _FusedSAGE:
 
     def loss_and_grad(self, logits, labels, inv_count, mask=None):
         """Fused softmax cross-entropy (+ the last bias) over the rows with mask == 1 (all
-        rows by default): stats, dlogits."""
+        rows by default): stats, dlogits; the last bias gradient goes straight into the
+        flat gradient buffer (GPU)."""
         n = logits.shape[0]
         rp, col, ones, tr = self._identity(n)
         G = torch.empty_like(logits)
         stats, G = ops.spmm_ce(rp, col, logits, self.C, ones, self.b[-1], labels, tr if mask is None else mask,
-                               inv_count, mode=0, G=G)
+                               inv_count, mode=0, G=G, db_out=self.gb[-1] if logits.is_cuda else None)
         return stats, G
 
     def backward(self, saved, G, stats):
@@ -280,7 +281,7 @@ class _FusedSAGE:
             Ym, m = (None, 1.0) if last else (out, ms)
             lin_bwd_weight(x1, dY, N, x2=agg, K1=F, K2=F, Ym=Ym, mscale=m, dW=self.gW[k],
                            db=self.db_scratch if last else self.gb[k], idx1=idx1, n=nd)
-            if last:
+            if last and not dY.is_cuda:          # (GPU: written by loss_and_grad's spmm_ce)
                 self.gb[k].copy_(stats[4:4 + self.C])
             if k == 0:
                 break

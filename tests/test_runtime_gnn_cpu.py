@@ -135,9 +135,9 @@ def test_gcn_trainer_gradients_match_autograd(world):
         grads = torch.zeros_like(tr0.grads)
         for r, tr in enumerate(trs):
             tr.Gc = gc
-            tr.world = 1                     # backward without collectives
+            tr.multi = False                 # backward without collectives
             tr.backward(stats[r])
-            tr.world = world
+            tr.multi = True
             grads += tr.grads
         grads[tr0.n_params - tr0.C:] = sum(s[4:4 + tr0.C] for s in stats)
     ref = torch.cat([W1.grad.flatten(), b1.grad, W2.grad.flatten(), b2.grad])
