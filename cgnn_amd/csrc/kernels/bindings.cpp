@@ -24,7 +24,8 @@ int cgnn_gen_bwd_blocks(int);
 size_t cgnn_gen_bwd_lds(int, int, int, int);
 int cgnn_read_stamps(unsigned long long*);
 int cgnn_launch_mmd_rows(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
-                         float, int, int, hipStream_t);
+                         float, int, int, hipStream_t, int);
+int cgnn_mmd_mirror_slots(int, int);
 int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, int, float*, int,
                               const int*, int, int, hipStream_t);
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
@@ -120,7 +121,7 @@ static void chk(int rc, const char* what) {
 class PyEngine {
  public:
   PyEngine(std::vector<int> icfg, std::vector<float> fcfg, std::vector<uint64_t> ptrs, uint64_t stream) {
-    if (icfg.size() < 17 || fcfg.size() < 5 || ptrs.size() < 21) throw std::invalid_argument("engine config size");
+    if (icfg.size() < 18 || fcfg.size() < 5 || ptrs.size() < 21) throw std::invalid_argument("engine config size");
     std::vector<const void*> p(ptrs.size());
     for (size_t k = 0; k < ptrs.size(); ++k) p[k] = reinterpret_cast<const void*>(ptrs[k]);
     h_ = cgnn_engine_create(icfg.data(), fcfg.data(), p.data(), S(stream));
@@ -166,13 +167,16 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("mmd", [](int mode, int D, uint64_t xhat, uint64_t data, uint64_t gp, uint64_t lp, int N, int R,
-                  int row_tiles, int n_chunks, int tpc, float gscale, uint64_t st, int row_begin, int n_rows) {
+                  int row_tiles, int n_chunks, int tpc, float gscale, uint64_t st, int row_begin, int n_rows,
+                  int mirror) {
     chk(cgnn_launch_mmd_rows(mode, D, Pt<const float>(xhat), Pt<const float>(data), Pt<float>(gp),
                              Pt<float>(lp), N, R, row_tiles, n_chunks, tpc, gscale, row_begin,
-                             n_rows < 0 ? N : n_rows, S(st)), "mmd");
+                             n_rows < 0 ? N : n_rows, S(st), mirror), "mmd");
   }, py::arg("mode"), py::arg("D"), py::arg("xhat"), py::arg("data"), py::arg("gp"), py::arg("lp"), py::arg("N"),
      py::arg("R"), py::arg("row_tiles"), py::arg("n_chunks"), py::arg("tpc"), py::arg("gscale"), py::arg("st"),
-     py::arg("row_begin") = 0, py::arg("n_rows") = -1);
+     py::arg("row_begin") = 0, py::arg("n_rows") = -1, py::arg("mirror") = 0);
+  // gradient slots a symmetric (mirror=1) training launch adds after its n_chunks
+  m.def("mmd_mirror_slots", &cgnn_mmd_mirror_slots, py::arg("D"), py::arg("N"));
   m.def("loss_finalize", [](uint64_t lp, int n_parts, uint64_t tt, uint64_t last, uint64_t acc, float inv_n2,
                             int flags, uint64_t hist, int hist_stride, uint64_t step, int step_off, int R,
                             uint64_t st) {

@@ -19,7 +19,7 @@
 
 extern "C" {
 int cgnn_launch_mmd(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
-                    float, hipStream_t);
+                    float, hipStream_t, int);
 int cgnn_launch_mmd_mfma(int, int, const float*, const float*, const float*, const float*, float*, float*,
                          int, int, int, int, float, hipStream_t);
 int cgnn_mmd_mfma_row_blocks(int);
@@ -53,6 +53,7 @@ struct EngineConfig {
   int NS = 0;        // noise streams per model = D + max #confounder streams
   int mfma = 0;      // 1: train/eval MMD on the matrix cores (mmd_mfma.hip), D >= 8
   int mf_chunks = 1, mf_tpc = 0;   // its column chunking (32-wide tiles per chunk)
+  int mirror = 0;    // > 0: symmetric vector-kernel training, `mirror` extra gradient slots
 };
 
 struct EngineBuffers {
@@ -108,7 +109,7 @@ class Engine {
   int n_parts_tt() const {
     return tt_mfma() ? c_.mf_chunks * cgnn_mmd_mfma_row_blocks(c_.N) : c_.n_chunks * c_.row_tiles;
   }
-  int grad_chunks() const { return c_.rff_k > 0 ? 1 : (c_.mfma ? c_.mf_chunks : c_.n_chunks); }
+  int grad_chunks() const { return c_.rff_k > 0 ? 1 : (c_.mfma ? c_.mf_chunks : c_.n_chunks + (c_.mirror > 0 ? c_.mirror : 0)); }
 
   // loss (+ gradient when train) of the current xhat; `need_loss` false lets the
   // matrix-core kernel skip the (unread) training loss
@@ -127,7 +128,8 @@ class Engine {
     } else {
       const float inv = 1.f / ((float)c_.N * (float)c_.N);
       check(cgnn_launch_mmd(train ? (need_loss ? 0 : 3) : 1, c_.D, b_.xhat, b_.data, b_.gradp, b_.lpart, c_.N, c_.R,
-                            c_.row_tiles, c_.n_chunks, c_.tpc, train ? 4.f * inv : 0.f, st_), "mmd");
+                            c_.row_tiles, c_.n_chunks, c_.tpc, train ? 4.f * inv : 0.f, st_,
+                            train && c_.mirror > 0 ? 1 : 0), "mmd");
     }
   }
   float loss_scale() const { return c_.rff_k > 0 ? 1.f : 1.f / ((float)c_.N * (float)c_.N); }
@@ -150,7 +152,7 @@ class Engine {
                                  c_.mf_chunks, c_.mf_tpc, 0.f, st_), "mmd_mfma(tt)");
     else
       check(cgnn_launch_mmd(2, c_.D, b_.xhat, b_.data, b_.gradp, b_.lpart, c_.N, c_.R, c_.row_tiles,
-                            c_.n_chunks, c_.tpc, 0.f, st_), "mmd(tt)");
+                            c_.n_chunks, c_.tpc, 0.f, st_, 0), "mmd(tt)");
     check(cgnn_launch_loss_finalize(b_.lpart, n_parts_tt(), b_.tt, b_.loss_last, b_.loss_acc, inv, 2,
                                     nullptr, 0, b_.step, 0, c_.R, st_), "finalize(tt)");
   }
@@ -241,7 +243,7 @@ extern "C" void* cgnn_engine_create(const int* icfg, const float* fcfg, const vo
   c.R = icfg[0]; c.N = icfg[1]; c.D = icfg[2]; c.H = icfg[3]; c.P = icfg[4];
   c.prog_stride = icfg[5]; c.max_in = icfg[6]; c.row_tiles = icfg[7]; c.n_chunks = icfg[8];
   c.tpc = icfg[9]; c.hist_stride = icfg[10]; c.rff_k = icfg[11]; c.d_true = icfg[12]; c.NS = icfg[13];
-  c.mfma = icfg[14]; c.mf_chunks = icfg[15]; c.mf_tpc = icfg[16];
+  c.mfma = icfg[14]; c.mf_chunks = icfg[15]; c.mf_tpc = icfg[16]; c.mirror = icfg[17];
   c.lr = fcfg[0]; c.beta1 = fcfg[1]; c.beta2 = fcfg[2]; c.eps = fcfg[3]; c.init_std = fcfg[4];
   cgnn::EngineBuffers b;
   b.prog = (const int*)ptrs[0]; b.params = (float*)ptrs[1]; b.m = (float*)ptrs[2];

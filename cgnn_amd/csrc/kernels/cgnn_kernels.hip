@@ -57,16 +57,38 @@ constexpr float MMD_SENTINEL = 1.0e17f;   // padded columns: exp(-g*d2) == 0 exa
 // Rows: generated samples [row_begin, row_begin + n_rows) of the N columns (a
 // sample-sharded MMD evaluates only its own rows against all columns); gradient
 // partials are written with the local row stride n_rows.
+//
+// mirror (training, D <= MMD_SYM_MAX_D, all rows): the pred-pred block is evaluated only
+// at and right of the diagonal tile.  An off-diagonal tile (a, b > a) feeds both sides:
+// row i of a takes w_ij (x_j - p_i) as usual, and column j of b -- itself a generated
+// row -- takes the mirrored w_ij (p_i - x_j), summed over the 256 rows of the tile.
+// That column sum is done without atomics or shuffles-per-column: lane l of a wave
+// visits the column pairs of a 64-pair group in the staggered order (l + s) mod 64, and
+// the per-pair accumulators ride along with a full-wave DPP rotate fused into the add
+// (v_add_f32_dpp wave_rol:1), so after 64 steps each lane holds the complete wave sum
+// of one pair; the 4 waves' sums are added in LDS in a fixed order and written to
+// grad_part slot n_chunks + a (rows of b).  Blocks (a, b <= a) zero their rows of that
+// slot, so the consumer just sums n_chunks + row_tiles - 1 slots (cgnn_mmd_mirror_slots).
+// Every order is a function of N only: bitwise reproducible and batch-independent.
+constexpr int MMD_SYM_MAX_D = 8;
+
+__device__ __forceinline__ float rot_next(float x) {      // lane l <- lane (l + 1) mod 64
+  // a full rotate has no out-of-range source lane, so no `old` value to initialise
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x134, 0xf, 0xf, true));
+}
+
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void mmd_rbf_kernel(
     const float* __restrict__ xhat, const float* __restrict__ data,
     float* __restrict__ grad_part, float* __restrict__ loss_part,
-    int N, int R, int tiles_per_chunk, float grad_scale, int row_begin, int n_rows) {
+    int N, int R, int tiles_per_chunk, float grad_scale, int row_begin, int n_rows, int mirror) {
   // MODE 3: training step whose loss nobody reads (no history): gradient only
   constexpr bool GRAD = MODE == 0 || MODE == 3;
   constexpr bool LOSS = MODE != 3;
+  constexpr bool SYMG = GRAD && D <= MMD_SYM_MAX_D;
   constexpr int T = 256;
   __shared__ __attribute__((aligned(16))) float s_x[T * D];   // [T/2][D][2]
+  __shared__ __attribute__((aligned(16))) float s_col[SYMG ? 4 * D * T : 1];   // [wave][D][T]
   __shared__ float s_red[4];
 
   const int rt = blockIdx.x, chunk = blockIdx.y, r = blockIdx.z;
@@ -79,10 +101,13 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
   const float* P = (MODE == 2 ? data : xhat) + mbase;
   const float* Tm = data + mbase;
 
+  // padding rows sit at the sentinel: their weights against every real column are
+  // exactly 0, so they add nothing to the mirrored column sums (their own row sums
+  // and loss are discarded)
   f2 p[D], g[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) {
-    const float pk = valid ? P[(size_t)k * N + i] : 0.f;
+    const float pk = valid ? P[(size_t)k * N + i] : MMD_SENTINEL;
     p[k] = f2{pk, pk};
     g[k] = f2{0.f, 0.f};
   }
@@ -94,13 +119,22 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
   const int tile_hi = min(n_tiles, tile_lo + tiles_per_chunk);
   float* my = s_x + ((t >> 1) * D) * 2 + (t & 1);
 
-  // evaluation over all rows: the pred-pred block is symmetric, so only column tiles at
-  // or right of the row tile are evaluated, those strictly right counting twice
-  // (25 % fewer distances per evaluation step; geometry fixed by N, so still bitwise
-  // reproducible and independent of the batch)
-  const bool sym = MODE == 1 && row_begin == 0 && n_rows == N;
+  // the pred-pred block is symmetric, so only column tiles at or right of the row tile
+  // are evaluated, those strictly right counting twice in the loss (25 % fewer
+  // distances; geometry fixed by N, so still bitwise reproducible and independent of
+  // the batch).  Evaluation: always over all rows; training: with mirror slots.
+  const bool all_rows = row_begin == 0 && n_rows == N;
+  const bool msym = SYMG && mirror && all_rows;
+  const bool sym = (MODE == 1 && all_rows) || msym;
+  float* gmir = msym && rt < row_tiles - 1 ? grad_part + ((size_t)(n_chunks + rt) * R + r) * D * N : nullptr;
   for (int tile = tile_lo; tile < tile_hi; ++tile) {
     const bool is_pred = (MODE != 2) && tile < ct;
+    if (sym && is_pred && tile <= rt && gmir) {          // this block's mirror rows of the tile: none
+      const int c = tile * T + t;
+      if (c < N)
+#pragma unroll
+        for (int k = 0; k < D; ++k) gmir[(size_t)k * N + c] = 0.f;
+    }
     if (sym && is_pred && tile < rt) continue;           // block-uniform: no barrier divergence
     const float* src = is_pred ? P : Tm;
     const int col0 = (is_pred || MODE == 2 ? tile : tile - ct) * T;
@@ -113,6 +147,53 @@ __global__ __launch_bounds__(256) void mmd_rbf_kernel(
     const float gsign = is_pred ? 1.f : -1.f;
     f2 tl = {0.f, 0.f};
     const f2* xp = reinterpret_cast<const f2*>(s_x);
+    if constexpr (SYMG) {
+      if (msym && is_pred && tile > rt) {                // block-uniform
+        const int lane = t & 63, wv = t >> 6;
+#pragma unroll 1
+        for (int grp = 0; grp < 2; ++grp) {
+          f2 ca[D];
+#pragma unroll
+          for (int k = 0; k < D; ++k) ca[k] = f2{0.f, 0.f};
+#pragma unroll 2
+          for (int s = 0; s < 64; ++s) {
+            const f2* xj = xp + (grp * 64 + ((lane + s) & 63)) * D;
+            f2 diff[D];
+            f2 d2 = {0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+              diff[k] = xj[k] - p[k];
+              d2 = diff[k] * diff[k] + d2;
+            }
+            f2 ks, w;
+            rbf7x2(d2, ks, w);
+            if (LOSS) tl += ks;
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+              const f2 wd = w * diff[k];
+              g[k] += wd;
+              ca[k] = f2{rot_next(ca[k].x), rot_next(ca[k].y)} + wd;
+            }
+          }
+          // lane l now holds the wave's sums for pair (l - 1) mod 64 of the group
+          const int q = grp * 64 + ((lane + 63) & 63);
+#pragma unroll
+          for (int k = 0; k < D; ++k)
+            *reinterpret_cast<f2*>(s_col + (wv * D + k) * T + 2 * q) = ca[k];
+        }
+        __syncthreads();
+        if (c < N && gmir) {
+#pragma unroll
+          for (int k = 0; k < D; ++k) {
+            const float v = (s_col[(0 * D + k) * T + t] + s_col[(1 * D + k) * T + t]) +
+                            (s_col[(2 * D + k) * T + t] + s_col[(3 * D + k) * T + t]);
+            gmir[(size_t)k * N + c] = -v * grad_scale;     // w_ij (p_i - x_j) = -w_ij diff_ij
+          }
+        }
+        if (LOSS) lacc = fmaf(lsign, tl.x + tl.y, lacc);
+        continue;
+      }
+    }
 #pragma unroll 2
     for (int jj = 0; jj < T / 2; ++jj) {
       const f2* xj = xp + jj * D;
@@ -723,12 +804,14 @@ __global__ void advance_step_kernel(int* step_base, int d_rng, int d_opt) {
 template <int D>
 static int launch_mmd_d(int mode, const float* xhat, const float* data, float* gpart, float* lpart,
                         int row_begin, int n_rows, int N, int R, int row_tiles, int n_chunks, int tpc, float gscale,
-                        hipStream_t st) {
+                        int mirror, hipStream_t st) {
   dim3 grid(row_tiles, n_chunks, R), block(256);
-  if (mode == 0) hipLaunchKernelGGL((mmd_rbf_kernel<D, 0>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
-  else if (mode == 3) hipLaunchKernelGGL((mmd_rbf_kernel<D, 3>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
-  else if (mode == 1) hipLaunchKernelGGL((mmd_rbf_kernel<D, 1>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
-  else hipLaunchKernelGGL((mmd_rbf_kernel<D, 2>), grid, block, 0, st, xhat, data, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
+#define MMD_ARGS xhat, data, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows, mirror
+  if (mode == 0) hipLaunchKernelGGL((mmd_rbf_kernel<D, 0>), grid, block, 0, st, MMD_ARGS);
+  else if (mode == 3) hipLaunchKernelGGL((mmd_rbf_kernel<D, 3>), grid, block, 0, st, MMD_ARGS);
+  else if (mode == 1) hipLaunchKernelGGL((mmd_rbf_kernel<D, 1>), grid, block, 0, st, MMD_ARGS);
+  else hipLaunchKernelGGL((mmd_rbf_kernel<D, 2>), grid, block, 0, st, MMD_ARGS);
+#undef MMD_ARGS
   return (int)hipGetLastError();
 }
 
@@ -737,14 +820,25 @@ extern "C" int cgnn_mmd_supported_d(int D) {
     case 32: case 48: case 64: return 1; default: return 0; }
 }
 
+// extra gradient slots (after the n_chunks column chunks) a symmetric training launch
+// of the vector kernel writes over all N rows: row_tiles - 1 for D <= MMD_SYM_MAX_D, else 0
+extern "C" int cgnn_mmd_mirror_slots(int D, int N) {
+  if (!cgnn_mmd_supported_d(D) || D > MMD_SYM_MAX_D || N < 1) return 0;
+  return (N + 255) / 256 - 1;
+}
+
 // row_begin / n_rows: the rows (generated samples) this launch evaluates; (0, N)
-// for the whole set.  row_tiles must cover n_rows.
+// for the whole set.  row_tiles must cover n_rows.  mirror: symmetric training over all
+// rows -- grad_part then holds n_chunks + cgnn_mmd_mirror_slots(D, N) slots.
 extern "C" int cgnn_launch_mmd_rows(int mode, int D, const float* xhat, const float* data, float* gpart,
                                     float* lpart, int N, int R, int row_tiles, int n_chunks, int tpc,
-                                    float gscale, int row_begin, int n_rows, hipStream_t st) {
+                                    float gscale, int row_begin, int n_rows, hipStream_t st, int mirror) {
   if (row_begin < 0 || n_rows < 1 || row_begin + n_rows > N || (long)row_tiles * 256 < n_rows) return -2;
+  if (mirror && ((mode != 0 && mode != 3) || row_begin != 0 || n_rows != N || cgnn_mmd_mirror_slots(D, N) == 0 ||
+                 row_tiles != (N + 255) / 256))
+    return -2;
   switch (D) {
-#define CASE_D(d) case d: return launch_mmd_d<d>(mode, xhat, data, gpart, lpart, row_begin, n_rows, N, R, row_tiles, n_chunks, tpc, gscale, st);
+#define CASE_D(d) case d: return launch_mmd_d<d>(mode, xhat, data, gpart, lpart, row_begin, n_rows, N, R, row_tiles, n_chunks, tpc, gscale, mirror, st);
     CASE_D(1) CASE_D(2) CASE_D(3) CASE_D(4) CASE_D(6) CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20)
     CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64)
 #undef CASE_D
@@ -754,8 +848,9 @@ extern "C" int cgnn_launch_mmd_rows(int mode, int D, const float* xhat, const fl
 
 extern "C" int cgnn_launch_mmd(int mode, int D, const float* xhat, const float* data, float* gpart,
                                float* lpart, int N, int R, int row_tiles, int n_chunks, int tpc,
-                               float gscale, hipStream_t st) {
-  return cgnn_launch_mmd_rows(mode, D, xhat, data, gpart, lpart, N, R, row_tiles, n_chunks, tpc, gscale, 0, N, st);
+                               float gscale, hipStream_t st, int mirror) {
+  return cgnn_launch_mmd_rows(mode, D, xhat, data, gpart, lpart, N, R, row_tiles, n_chunks, tpc, gscale, 0, N, st,
+                              mirror);
 }
 
 extern "C" int cgnn_launch_loss_finalize(const float* lpart, int n_parts, float* tt, float* last,

@@ -57,6 +57,15 @@ def mmd_mfma_geometry(N: int, R: int = 0):
     return rb, n_chunks, tpc
 
 
+def mmd_mirror_slots(D: int, N: int) -> int:
+    """Extra gradient slots of a symmetric vector-kernel training launch (0: the launch
+    evaluates the full pred-pred block).  ``CGNN_MMD_SYM=0`` disables symmetry."""
+    import os
+    if os.environ.get("CGNN_MMD_SYM", "1") == "0":
+        return 0
+    return int(native.hip().mmd_mirror_slots(D, N))
+
+
 def mmd_kernel_choice(D: int, mmd_kernel: str = "auto") -> str:
     """'mfma' (matrix cores, D >= 8) or 'valu' (packed-fp32 vector kernel).
     ``CGNN_MMD_KERNEL=valu|mfma`` overrides 'auto'."""
@@ -139,7 +148,10 @@ class DeviceTrainer:
             mf_rb, mf_chunks, mf_tpc = mmd_mfma_geometry(N, R)
             F = 7 * self.rff_k
             n_parts = max(row_tiles * n_chunks, mf_rb * mf_chunks, (F + 255) // 256 if F else 0)
-            self.gradp = torch.zeros(max(n_chunks, mf_chunks, 1), R, D, N, **f32)
+            # symmetric pred-pred training on the vector kernel: extra gradient slots for
+            # the mirrored column sums (CGNN_MMD_SYM=0 turns it off for A/B)
+            self.mirror = mmd_mirror_slots(D, N) if self.mmd_kernel == "valu" else 0
+            self.gradp = torch.zeros(max(n_chunks + self.mirror, mf_chunks, 1), R, D, N, **f32)
             self.lpart = torch.zeros(R, n_parts, **f32)
             G = hip.gen_bwd_blocks(N)
             self.gpart = torch.zeros(R, G, P, **f32)
@@ -161,7 +173,7 @@ class DeviceTrainer:
             self.stream = torch.cuda.Stream(dev)
             stream = self.stream
             icfg = [R, N, D, self.H, P, stride, max_in, row_tiles, n_chunks, tpc, self.hist_len,
-                    self.rff_k, d, self.NS, int(self.mmd_kernel == "mfma"), mf_chunks, mf_tpc]
+                    self.rff_k, d, self.NS, int(self.mmd_kernel == "mfma"), mf_chunks, mf_tpc, self.mirror]
             fcfg = [float(learning_rate), 0.9, 0.999, 1e-8, float(init_std)]
             ptrs = [t.data_ptr() for t in (self.prog, self.params, self.m, self.v, self.data,
                                            self.xhat, self.noise, self.gradp, self.lpart, self.gpart,

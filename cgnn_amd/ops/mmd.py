@@ -12,7 +12,7 @@ import math
 import torch
 
 from .. import native
-from ..engine.batch import mmd_geometry, mmd_kernel_choice, mmd_mfma_geometry, padded_dim
+from ..engine.batch import mmd_geometry, mmd_kernel_choice, mmd_mfma_geometry, mmd_mirror_slots, padded_dim
 from ..engine.reference import GAMMAS, mmd_loss_dense
 
 
@@ -35,7 +35,8 @@ class _MMDHip(torch.autograd.Function):
         row_tiles, n_chunks, tpc = mmd_geometry(N, R)
         dev = pred.device
         mf_rb, mf_chunks, mf_tpc = mmd_mfma_geometry(N, R)
-        gradp = torch.empty(max(n_chunks, mf_chunks), R, D, N, dtype=torch.float32, device=dev)
+        mirror = mmd_mirror_slots(D, N) if kernel == "valu" else 0
+        gradp = torch.empty(max(n_chunks + mirror, mf_chunks), R, D, N, dtype=torch.float32, device=dev)
         lpart = torch.empty(R, max(row_tiles * n_chunks, mf_rb * mf_chunks), dtype=torch.float32, device=dev)
         tt = torch.zeros(R, dtype=torch.float32, device=dev)
         last = torch.zeros(R, dtype=torch.float32, device=dev)
@@ -61,8 +62,8 @@ class _MMDHip(torch.autograd.Function):
             parts, chunks = mf_rb * mf_chunks, mf_chunks
         else:
             hip.mmd(0, D, P.data_ptr(), T.data_ptr(), gradp.data_ptr(), lpart.data_ptr(), N, R,
-                    row_tiles, n_chunks, tpc, 4.0 * inv, st)
-            parts, chunks = row_tiles * n_chunks, n_chunks
+                    row_tiles, n_chunks, tpc, 4.0 * inv, st, mirror=int(mirror > 0))
+            parts, chunks = row_tiles * n_chunks, n_chunks + mirror
         hip.loss_finalize(lpart.data_ptr(), parts, tt.data_ptr(), last.data_ptr(),
                           acc.data_ptr(), inv, 0, 0, 0, step.data_ptr(), 0, R, st)
         g = gradp[:chunks].sum(0)[:, :d].transpose(1, 2).contiguous()    # [R, N, d]

@@ -20,7 +20,8 @@ def test_native_extension_is_loaded():
 
 
 @pytest.mark.parametrize("N,d,kernel", [(2, 1, "valu"), (63, 2, "valu"), (64, 5, "valu"), (257, 22, "valu"),
-                                        (1000, 22, "valu"), (1500, 2, "valu"), (33, 8, "mfma"),
+                                        (1000, 22, "valu"), (1500, 2, "valu"), (700, 1, "valu"), (600, 4, "valu"),
+                                        (513, 6, "valu"), (800, 8, "valu"), (33, 8, "mfma"),
                                         (257, 22, "mfma"), (1000, 22, "mfma"), (500, 40, "mfma"),
                                         (130, 64, "mfma")])
 def test_mmd_loss_and_grad_match_oracle(N, d, kernel):
@@ -44,6 +45,29 @@ def test_mmd_loss_and_grad_match_oracle(N, d, kernel):
     gref = torch.stack(ref_g).numpy()
     scale = np.abs(gref).max()
     np.testing.assert_allclose(pg.grad.cpu().numpy(), gref, rtol=2e-3, atol=2e-3 * scale)
+
+
+@pytest.mark.parametrize("N,d", [(1500, 2), (513, 6), (800, 8)])
+def test_mmd_symmetric_training_matches_full_block(N, d, monkeypatch):
+    """The mirrored pred-pred evaluation (off-diagonal tiles once, column sums by the
+    staggered DPP rotation) equals the full-block kernel to fp32 rounding, and the
+    symmetric launch really adds its mirror slots."""
+    from cgnn_amd.engine.batch import mmd_mirror_slots
+    from cgnn_amd.ops.mmd import mmd_loss
+    assert mmd_mirror_slots(padded_dim(d), N) == (N + 255) // 256 - 1
+    torch.manual_seed(N + d)
+    pred = torch.randn(4, N, d, device="cuda")
+    true = torch.randn(4, N, d, device="cuda") * 0.8 - 0.3
+    outs = []
+    for sym in ("1", "0"):
+        monkeypatch.setenv("CGNN_MMD_SYM", sym)
+        p = pred.clone().requires_grad_(True)
+        L = mmd_loss(p, true, kernel="valu")
+        L.sum().backward()
+        outs.append((L.detach(), p.grad))
+    (l1, g1), (l0, g0) = outs
+    torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-4 * float(g0.abs().max()))
 
 
 def _toy_dag():
@@ -136,7 +160,7 @@ def test_batch_composition_does_not_change_scores():
     H = 20
     g = _toy_dag()
     prog = program_for_dag(g, H)
-    datas = [_data(5, 256, s) for s in range(4)]
+    datas = [_data(5, 600, s) for s in range(4)]      # 3 row tiles: the symmetric MMD's mirror slots
     keys = [model_key(11, "y", r) for r in range(4)]
     full = DeviceTrainer([prog] * 4, datas, keys, H, "cuda:0").run(10, 5)
     for r in range(4):

@@ -10,6 +10,7 @@ and commit the new file with the change that caused it."""
 import json
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
@@ -25,9 +26,16 @@ def main():
     from test_examples_gpu import REFERENCE_SETTINGS, run_confounders, run_graph, run_pairwise
     for k, v in REFERENCE_SETTINGS.items():
         setattr(cgnn.SETTINGS, k, v)
+    wall = {}
+    t0 = time.perf_counter()
     pred, targets = run_pairwise()
+    wall["pairwise"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
     dag, target = run_graph()
+    wall["graph"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
     cdag, ctarget = run_confounders()
+    wall["confounders"] = time.perf_counter() - t0
     rec = {
         "pairwise": {"signs": [int(x > 0) - int(x < 0) for x in pred], "predictions": [float(x) for x in pred],
                      "sign_accuracy": float(sign_accuracy(pred, targets))},
@@ -38,7 +46,8 @@ def main():
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps({"pairwise_sign_accuracy": rec["pairwise"]["sign_accuracy"], "graph_shd": rec["graph"]["shd"],
-                      "confounders": rec["confounders"]["scores"]}))
+                      "confounders": rec["confounders"]["scores"],
+                      "wall_s": {k: round(v, 2) for k, v in wall.items()}}))
 
 
 if __name__ == "__main__":
