@@ -105,6 +105,7 @@ int gnn_launch_lin_fwd(const void*, int, int, const void*, int, int, const float
 int gnn_launch_lin_bwd_data(const void*, int, const void*, int, float, int, const float*, int, int, void*, int,
                             void*, int, const float*, int, int, void*, hipStream_t);
 long gnn_lin_fwd_image_bytes(int, int, int);
+int gnn_lin_fwd_kc_wanted(int, int, int);
 long gnn_lin_bwd_image_bytes(int, int);
 int gnn_lin_wgrad_chunks(int, int);
 int gnn_launch_lin_bwd_weight(const void*, int, int, const void*, int, int, const void*, int, const void*, int,
@@ -415,6 +416,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("st"), py::arg("idx1") = 0, py::arg("wimg") = 0, py::arg("yf") = 0, py::arg("nsplit") = 0,
      py::arg("tk") = 1, py::arg("et") = 0);
   m.def("gnn_lin_fwd_image_bytes", &gnn_lin_fwd_image_bytes);
+  m.def("gnn_lin_fwd_kc_wanted", &gnn_lin_fwd_kc_wanted);
   m.def("gnn_lin_bwd_image_bytes", &gnn_lin_bwd_image_bytes);
   m.def("gnn_lin_bwd_data", [](uint64_t dy, int lddy, uint64_t ym, int ldym, float mscale, int N, uint64_t w, int K1,
                                int K2, uint64_t dx1, int ldx1, uint64_t dx2, int ldx2, uint64_t rscale, int n,

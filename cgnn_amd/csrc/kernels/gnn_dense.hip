@@ -83,8 +83,16 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint16_t* base, int off0, int of
 
 }  // namespace
 
-// KS = k-steps of 16 over the input features (F <= 16*KS <= ldx rounded), HD hidden width.
-template <int KS, int HD>
+// KS = k-steps of 16 over the input features (F <= 16*KS <= ldx rounded), HD hidden width;
+// DROP: dropout active (p > 0), a compile-time switch so the epilogue has no per-element
+// branches.
+//
+// Latency structure (the kernel runs 4 waves / SIMD -- one 16-wave block per CU -- and
+// was measured MFMA-busy ~23 %): per hidden tile t the accumulator starts as the bias
+// (4 b128 LDS reads issued ahead, fp32 exact) instead of a bias add per element after
+// the chain, and the KS weight fragments of the chain are read from LDS as one batch
+// before the first MFMA rather than one LDS round trip per MFMA.
+template <int KS, int HD, bool DROP>
 __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
     const uint16_t* __restrict__ AX, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ dinv, uint16_t* __restrict__ H1,
@@ -130,24 +138,32 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
     f32x16 z0 = {}, z1 = {};
 #pragma unroll 1
     for (int t = 0; t < HD / 32; ++t) {
-      f32x16 acc = {};
-      const uint16_t* arow = sW1T + (32 * t + lr) * W1S + 8 * h;
+      // accumulator = bias: registers 4g..4g+3 are hidden 32t + 8g + 4h + 0..3
+      f32x16 acc;
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(load_bf16x8(arow + 16 * s), bx[s], acc, 0, 0, 0);
-      // epilogue: bias, relu, dropout (one Philox draw = this lane's 16 bytes)
-      uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-      if (thr8 > 0) {
-        const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
-        w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
+      for (int g = 0; g < 4; ++g) {
+        const float4 bb = *reinterpret_cast<const float4*>(sB1 + 32 * t + 8 * g + 4 * h);
+        acc[4 * g] = bb.x; acc[4 * g + 1] = bb.y; acc[4 * g + 2] = bb.z; acc[4 * g + 3] = bb.w;
       }
-      float v[16];
+      const uint16_t* arow = sW1T + (32 * t + lr) * W1S + 8 * h;
+      bf16x8 af[KS];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int nn = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
-        float x = fmaxf(acc[q] + sB1[nn], 0.f);
-        if (thr8 > 0) x = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
-        v[q] = x;
+      for (int s = 0; s < KS; ++s) af[s] = load_bf16x8(arow + 16 * s);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bx[s], acc, 0, 0, 0);
+      // epilogue: relu, dropout (one Philox draw = this lane's 16 bytes)
+      float v[16];
+      if constexpr (DROP) {
+        const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
+        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const float x = fmaxf(acc[q], 0.f);
+          v[q] = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = fmaxf(acc[q], 0.f);
       }
       if (rv && H1) {          // H1 == nullptr: the fused backward recomputes it
 #pragma unroll
@@ -165,14 +181,14 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
         {
           const uint16_t* a = sW2T + lr * W2S + nbase;
           const uint2 lo = *reinterpret_cast<const uint2*>(a), hi = *reinterpret_cast<const uint2*>(a + 8);
-          const bf16x8 af = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-          z0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, xb, z0, 0, 0, 0);
+          const bf16x8 af2 = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+          z0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af2, xb, z0, 0, 0, 0);
         }
         {
           const uint16_t* a = sW2T + (32 + lr) * W2S + nbase;
           const uint2 lo = *reinterpret_cast<const uint2*>(a), hi = *reinterpret_cast<const uint2*>(a + 8);
-          const bf16x8 af = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-          z1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, xb, z1, 0, 0, 0);
+          const bf16x8 af2 = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+          z1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af2, xb, z1, 0, 0, 0);
         }
       }
     }
@@ -266,7 +282,15 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_bwd_kernel(
 // (The round-1 form staged separate transposed images with 2-byte scattered writes
 // and wrote H1^T / dP1^T one element at a time: 0.74 ms on the ogbn-products shape.)
 // ============================================================================
-template <int KS, int KC, int HD>
+// LDS bytes of the fused backward: weights, nbuf x two [32][128] staging images, two
+// [HD/32][32][32] H1 / dP1 images, b1
+constexpr size_t fused_bwd_lds(int KP, int CP, int HD, int nbuf) {
+  return sizeof(uint16_t) * ((size_t)HD * (KP + 8) + (size_t)HD * (CP + 8) + (size_t)nbuf * 2 * 32 * 128 +
+                             2 * (size_t)HD * 32) +
+         sizeof(float) * HD;
+}
+
+template <int KS, int KC, int HD, bool DROP>
 __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
     const uint16_t* __restrict__ AX, const uint16_t* __restrict__ dY2, const float* __restrict__ W1,
     const float* __restrict__ b1, const float* __restrict__ W2, float* __restrict__ gpart, int n, int F,
@@ -280,12 +304,17 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
   constexpr int CP = KC * 16;                 // classes, padded
   constexpr int W1S = KP + 8, W2S = CP + 8;
   static_assert(KF <= 128 && CP <= 64, "staging rows are 256 B");
+  static_assert(KC <= KS, "the dh chain is interleaved into the layer-1 chain");
+  // double-buffered staging where the LDS budget allows it (HD = 256: K <= 112, C <= 48)
+  constexpr int NBUF = fused_bwd_lds(KP, CP, HD, 2) <= 160 * 1024 ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* sW1T = lds;                       // [HD][W1S]
   uint16_t* sW2 = sW1T + HD * W1S;            // [HD][W2S]   W2 rows (hidden-major)
-  uint16_t* sAX = sW2 + HD * W2S;             // [32][128]   swizzled (stg_off)
-  uint16_t* sDY = sAX + TILE * 128;           // [32][128]   swizzled, columns < 64 used
-  uint16_t* sH1 = sDY + TILE * 128;           // [NW][32][32] per-wave images (img_off)
+  // staging: NBUF buffers (two: tile i computes from one while tile i + 1 is written to
+  // the other, one block barrier per tile), each = AX [32][128] | dY2 [32][128],
+  // swizzled (stg_off), dY2 columns < 64 used
+  uint16_t* sStg = sW2 + HD * W2S;
+  uint16_t* sH1 = sStg + NBUF * 2 * TILE * 128;   // [NW][32][32] per-wave images (img_off)
   uint16_t* sDP = sH1 + NW * TILE * 32;       // [NW][32][32]
   float* sB1 = reinterpret_cast<float*>(sDP + NW * TILE * 32);   // [HD]
 
@@ -301,8 +330,8 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
   for (int i = tid; i < HD; i += NT) sB1[i] = b1[i];
   // zero the staging images: chunks the per-tile staging never writes (columns past
   // the staged K, read by the padded contraction tiles) stay zero
-  for (int i = tid; i < 2 * TILE * 128 / 8; i += NT)
-    reinterpret_cast<uint4*>(sAX)[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < NBUF * 2 * TILE * 128 / 8; i += NT)
+    reinterpret_cast<uint4*>(sStg)[i] = make_uint4(0u, 0u, 0u, 0u);
 
   const int lane = tid & 63, h = lane >> 5, lr = lane & 31;
   const int t = tid >> 6;                     // this wave's hidden block
@@ -345,48 +374,84 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
                    : make_uint4(0u, 0u, 0u, 0u);
     }
   };
-  if ((int)blockIdx.x < n_tiles) prefetch(blockIdx.x);
-  __syncthreads();
-
-  char* const bAX = reinterpret_cast<char*>(sAX);
-  char* const bDY = reinterpret_cast<char*>(sDY);
-  for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    // ---- stage this tile, prefetch the next ----
+  auto stage = [&](int buf) {
+    char* const bA = reinterpret_cast<char*>(sStg + buf * 2 * TILE * 128);
+    char* const bD = bA + 2 * TILE * 128;
 #pragma unroll
     for (int k = 0; k < PFX; ++k) {
       const int i = tid + k * NT;
-      if (i < TILE * xch) *reinterpret_cast<uint4*>(bAX + stg_off(i % TILE, i / TILE)) = pax[k];
+      if (i < TILE * xch) *reinterpret_cast<uint4*>(bA + stg_off(i % TILE, i / TILE)) = pax[k];
     }
 #pragma unroll
     for (int k = 0; k < PFY; ++k) {
       const int i = tid + k * NT;
-      if (i < TILE * ych) *reinterpret_cast<uint4*>(bDY + stg_off(i % TILE, i / TILE)) = pdy[k];
+      if (i < TILE * ych) *reinterpret_cast<uint4*>(bD + stg_off(i % TILE, i / TILE)) = pdy[k];
     }
-    if (tile + (int)gridDim.x < n_tiles) prefetch(tile + gridDim.x);
-    __syncthreads();
+  };
+  const int G = gridDim.x;
+  __syncthreads();                            // the zeroed staging images
+  if ((int)blockIdx.x < n_tiles) {
+    prefetch(blockIdx.x);
+    if constexpr (NBUF == 2) {
+      stage(0);
+      if ((int)blockIdx.x + G < n_tiles) prefetch(blockIdx.x + G);
+    }
+  }
+  __syncthreads();
+
+  int it = 0;
+  for (int tile = blockIdx.x; tile < n_tiles; tile += G, ++it) {
+    int cur = 0;
+    if constexpr (NBUF == 2) {
+      // stage the next tile into the other buffer (read by the previous tile, which
+      // every wave finished at the last barrier), prefetch the one after
+      cur = it & 1;
+      if (tile + G < n_tiles) {
+        stage(cur ^ 1);
+        if (tile + 2 * G < n_tiles) prefetch(tile + 2 * G);
+      }
+    } else {
+      stage(0);
+      if (tile + G < n_tiles) prefetch(tile + G);
+      __syncthreads();
+    }
+    uint16_t* const sAX = sStg + cur * 2 * TILE * 128;
+    uint16_t* const sDY = sAX + TILE * 128;
+    char* const bAX = reinterpret_cast<char*>(sAX);
+    char* const bDY = reinterpret_cast<char*>(sDY);
 
     // ---- recompute H1^T block t, dP1^T block t (lane = row, registers = hidden) ----
     const int row = tile * TILE + lr;
-    f32x16 acc = {};
+    // both chains' operands read from LDS as one batch (not one round trip per MFMA);
+    // the layer-1 accumulator starts as the bias (fp32)
+    f32x16 acc, dh = {};
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 bb = *reinterpret_cast<const float4*>(sB1 + 32 * t + 8 * g + 4 * h);
+      acc[4 * g] = bb.x; acc[4 * g + 1] = bb.y; acc[4 * g + 2] = bb.z; acc[4 * g + 3] = bb.w;
+    }
     {
       const uint16_t* arow = sW1T + (32 * t + lr) * W1S + 8 * h;
+      const uint16_t* drow = sW2 + (32 * t + lr) * W2S + 8 * h;
+      bf16x8 a1[KS], x1[KS], a2[KC], y2[KC];
 #pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            load_bf16x8(arow + 16 * s2),
-            load_bf16x8(reinterpret_cast<const uint16_t*>(bAX + stg_off(lr, 2 * s2 + h))), acc, 0, 0, 0);
-    }
-    f32x16 dh = {};
-    {
-      const uint16_t* arow = sW2 + (32 * t + lr) * W2S + 8 * h;
+      for (int s2 = 0; s2 < KS; ++s2) {
+        a1[s2] = load_bf16x8(arow + 16 * s2);
+        x1[s2] = load_bf16x8(reinterpret_cast<const uint16_t*>(bAX + stg_off(lr, 2 * s2 + h)));
+      }
 #pragma unroll
-      for (int s2 = 0; s2 < KC; ++s2)
-        dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            load_bf16x8(arow + 16 * s2),
-            load_bf16x8(reinterpret_cast<const uint16_t*>(bDY + stg_off(lr, 2 * s2 + h))), dh, 0, 0, 0);
+      for (int s2 = 0; s2 < KC; ++s2) {
+        a2[s2] = load_bf16x8(drow + 16 * s2);
+        y2[s2] = load_bf16x8(reinterpret_cast<const uint16_t*>(bDY + stg_off(lr, 2 * s2 + h)));
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[s2], x1[s2], acc, 0, 0, 0);
+        if (s2 < KC) dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[s2], y2[s2], dh, 0, 0, 0);
+      }
     }
     uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-    if (thr8 > 0) {
+    if constexpr (DROP) {
       const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
       w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
     }
@@ -394,14 +459,12 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
     // 8-B write per image and g
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const float4 bb = *reinterpret_cast<const float4*>(sB1 + 32 * t + 8 * g + 4 * h);
-      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
       float xv[4], dv[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int q = 4 * g + i;
-        float x = fmaxf(acc[q] + bv[i], 0.f);
-        if (thr8 > 0) x = (((w[g] >> (8 * i)) & 0xffu) >= thr8) ? x * scale : 0.f;
+        float x = fmaxf(acc[q], 0.f);
+        if constexpr (DROP) x = (((w[g] >> (8 * i)) & 0xffu) >= thr8) ? x * scale : 0.f;
         xv[i] = x;
         dv[i] = x > 0.f ? dh[q] * scale : 0.f;
       }
@@ -431,7 +494,7 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
         g2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
             ah1, tr_frag(sDY, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 4, 4 * q + cb) + cx), g2[q], 0, 0, 0);
     }
-    __syncthreads();      // the staging images are rewritten by the next tile
+    __syncthreads();      // this buffer is rewritten two tiles on; the next one is staged
   }
 
   // ---- this block's partial slab: rows = hidden 32t + m, columns [f | KF + c] ----
@@ -462,17 +525,29 @@ static int dense_grid(int n) {
   return std::max(1, std::min(cus, (tiles + WAVES - 1) / WAVES));
 }
 
+template <int KS, int HD, bool DROP>
+static int fwd_launch_d(const uint16_t* AX, const float* W1, const float* b1, const float* W2,
+                        const float* dinv, uint16_t* H1, uint16_t* Z2, int n, int F, int ldx, int C,
+                        int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
+                        uint32_t row0, const int* stepp, hipStream_t st) {
+  const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KS * 16 + 8) + 64 * (size_t)(HD + 8)) + sizeof(float) * HD;
+  (void)hipFuncSetAttribute((const void*)gcn_dense_fwd_kernel<KS, HD, DROP>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((gcn_dense_fwd_kernel<KS, HD, DROP>), dim3(dense_grid(n)), dim3(WAVES * 64), lds, st, AX, W1,
+                     b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp);
+  return (int)hipGetLastError();
+}
+
 template <int KS, int HD>
 static int fwd_launch(const uint16_t* AX, const float* W1, const float* b1, const float* W2,
                       const float* dinv, uint16_t* H1, uint16_t* Z2, int n, int F, int ldx, int C,
                       int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
                       uint32_t row0, const int* stepp, hipStream_t st) {
-  const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KS * 16 + 8) + 64 * (size_t)(HD + 8)) + sizeof(float) * HD;
-  (void)hipFuncSetAttribute((const void*)gcn_dense_fwd_kernel<KS, HD>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((gcn_dense_fwd_kernel<KS, HD>), dim3(dense_grid(n)), dim3(WAVES * 64), lds, st, AX, W1,
-                     b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp);
-  return (int)hipGetLastError();
+  if (thr8 > 0)
+    return fwd_launch_d<KS, HD, true>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
+                                      stepp, st);
+  return fwd_launch_d<KS, HD, false>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
+                                     stepp, st);
 }
 
 extern "C" int gnn_launch_dense_fwd(const void* AX, const float* W1, const float* b1, const float* W2,
@@ -543,14 +618,12 @@ static int fused_bwd_launch(const uint16_t* AX, const uint16_t* dY2, const float
                             uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0,
                             const int* stepp, hipStream_t st) {
   constexpr int KP = KS * 16, CP = KC * 16;
-  // weights, two [32][128] staging images, two [HD/32][32][32] H1 / dP1 images, b1
-  const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KP + 8) + (size_t)HD * (CP + 8) + 2 * TILE * 128 +
-                                         2 * (size_t)HD * TILE) +
-                     sizeof(float) * HD;
+  const size_t lds2 = fused_bwd_lds(KP, CP, HD, 2);
+  const size_t lds = lds2 <= 160 * 1024 ? lds2 : fused_bwd_lds(KP, CP, HD, 1);
   if (lds > 160 * 1024) return -2;
-  (void)hipFuncSetAttribute((const void*)gcn_fused_bwd_kernel<KS, KC, HD>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((gcn_fused_bwd_kernel<KS, KC, HD>), dim3(gnn_fused_bwd_blocks(n)), dim3(HD * 2), lds, st,
+  auto kern = thr8 > 0 ? gcn_fused_bwd_kernel<KS, KC, HD, true> : gcn_fused_bwd_kernel<KS, KC, HD, false>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(gnn_fused_bwd_blocks(n)), dim3(HD * 2), lds, st,
                      AX, dY2, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp);
   return (int)hipGetLastError();
 }

@@ -85,13 +85,20 @@ __device__ __forceinline__ f32x16 mma16(uint4 a, uint4 b, f32x16 c) {
 }
 
 // zero the elements [valid, 8) of a bf16x8 chunk (padding columns may hold anything,
-// and 0 * NaN would poison a product); branch-free (selects), valid may be <= 0
+// and 0 * NaN would poison a product)
 __device__ __forceinline__ uint4 keep_first(uint4 v, int valid) {
-  // `valid` is loop-invariant in the callers' tile loops: without this empty asm, which
-  // ties it to the loaded data, LICM hoists the 4 masks of every unrolled k-step out of
-  // the loop (4 * KS live VGPRs -> scratch spills); with it they are computed as each
-  // load lands and die at once
-  asm volatile("" : "+v"(valid) : "v"(v.x));
+  if (valid >= 8) return v;
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int lo = 2 * e, hi = 2 * e + 1;
+    w[e] = (lo < valid ? (w[e] & 0xffffu) : 0u) | (hi < valid ? (w[e] & 0xffff0000u) : 0u);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// branch-free form (selects only), valid may be <= 0
+__device__ __forceinline__ uint4 keep_first_sel(uint4 v, int valid) {
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -104,31 +111,45 @@ __device__ __forceinline__ uint4 keep_first(uint4 v, int valid) {
 // 8 features [f0, f0 + 8) of row `row` of the virtual concatenation [X1 | X2]
 // (K1 % 8 == 0 when X2 is given, so a chunk never straddles the two); zeros past K1 + K2
 // idx1 (optional): X1 row of output row r is idx1[r] (gather-on-load: GraphSAGE's
-// first layer reads the seed / frontier rows straight out of the resident features).
-// Branch-free: every lane loads from a valid address (a chunk outside both operands
-// re-reads its row's first chunk) and the value is masked afterwards -- per-lane
-// branches in the unrolled k loop cost exec-mask saves that spilled the SGPR file.
+// first layer reads the seed / frontier rows straight out of the resident features)
 __device__ __forceinline__ uint4 load_cat8(const uint16_t* __restrict__ x1, int ld1, int K1,
                                            const uint16_t* __restrict__ x2, int ld2, int K2, int row, int f0,
                                            const int* __restrict__ idx1) {
+  if (f0 < K1) {
+    const size_t r1 = idx1 ? (size_t)idx1[row] : (size_t)row;
+    return keep_first(*reinterpret_cast<const uint4*>(x1 + r1 * ld1 + f0), K1 - f0);
+  }
+  const int g = f0 - K1;
+  if (x2 && g < K2) return keep_first(*reinterpret_cast<const uint4*>(x2 + (size_t)row * ld2 + g), K2 - g);
+  return make_uint4(0u, 0u, 0u, 0u);
+}
+
+// Branch-free load_cat8 for lin_fwd's unrolled k loop: every lane loads from a valid
+// address (a chunk outside both operands re-reads its row's first chunk) and the value
+// is masked afterwards.  The per-lane branches of load_cat8, unrolled KS times, cost
+// exec-mask saves that spilled the SGPR file (KS = 40: 1259 SGPR spills); this form has
+// none up to KS = 40 and measured 365 vs 410 us on Reddit's K = 602 layer; at KS = 8
+// (2 % slower) and in the weight-gradient prefetch (43 % slower) load_cat8 stays.
+__device__ __forceinline__ uint4 load_cat8_sel(const uint16_t* __restrict__ x1, int ld1, int K1,
+                                               const uint16_t* __restrict__ x2, int ld2, int K2, int row, int f0,
+                                               const int* __restrict__ idx1) {
   const size_t r1 = idx1 ? (size_t)idx1[row] : (size_t)row;
   const int g = f0 - K1;
   const bool in1 = f0 < K1;
   const bool in2 = x2 != nullptr && !in1 && g < K2;
   const uint16_t* p = in2 ? x2 + (size_t)row * ld2 + g : x1 + r1 * ld1 + (in1 ? f0 : 0);
   const uint4 v = *reinterpret_cast<const uint4*>(p);
-  return keep_first(v, in1 ? K1 - f0 : in2 ? K2 - g : 0);
+  return keep_first_sel(v, in1 ? K1 - f0 : in2 ? K2 - g : 0);
 }
 
 // 8 gradient values [c0, c0 + 8) of row `row`, times the mask [Ym > 0] * mscale
 __device__ __forceinline__ uint4 load_masked8(const uint16_t* __restrict__ dY, int lddy,
                                               const uint16_t* __restrict__ Ym, int ldym, float mscale,
                                               int N, int row, int c0) {
-  // branch-free like load_cat8: chunks past N re-read the row's first chunk, then masked
-  const int cc = c0 < N ? c0 : 0;
-  const uint4 g = keep_first(*reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + cc), N - c0);
+  if (c0 >= N) return make_uint4(0u, 0u, 0u, 0u);
+  uint4 g = keep_first(*reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + c0), N - c0);
   if (!Ym && mscale == 1.f) return g;
-  const uint4 y = Ym ? *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + cc) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  const uint4 y = Ym ? *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + c0) : make_uint4(~0u, ~0u, ~0u, ~0u);
   uint32_t gw[4] = {g.x, g.y, g.z, g.w};
   const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
@@ -225,8 +246,12 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     asm volatile("" : "+v"(fh));
     uint4 bx[KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-      bx[s] = load_cat8(x1, ld1, K1, x2, ld2, K2, rv ? row : n - 1, 16 * s + fh, idx1);
+    for (int s = 0; s < KS; ++s) {
+      if constexpr (KS > 16)     // wide K: the branch-free form (no exec-mask spills)
+        bx[s] = load_cat8_sel(x1, ld1, K1, x2, ld2, K2, rv ? row : n - 1, 16 * s + fh, idx1);
+      else
+        bx[s] = rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h, idx1) : make_uint4(0u, 0u, 0u, 0u);
+    }
     const float rs = (rv && rscale) ? rscale[row] : 1.f;
 #pragma unroll 1
     for (int t = 0; t < nt; ++t) {
@@ -271,6 +296,136 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
 }
 
 // ============================================================================
+// lin_fwd_kc: the same product for weights too wide to sit in LDS whole (K * N * 2 B
+// beyond the budget: Reddit's first layer, K = 602 x N = 256 fp16), where the slab form
+// would re-read X once per column slab.  A plain tiled GEMM instead: the weight streams
+// through LDS in K chunks of 32 (double-buffered, one block barrier per chunk) while
+// each wave keeps a 64-row x 128-column output block in registers (2 x 4 accumulator
+// tiles: every LDS weight fragment feeds two MFMAs) and reads its X rows straight from
+// HBM as MFMA B fragments, one chunk ahead.  Block = 4 waves = FG feature groups of
+// 128 columns x (4 / FG) row groups of 64 rows.  Epilogue: bias, ReLU, row scale.
+// No dropout / concatenation / gather (the inference path; lin_fwd keeps those).
+// ============================================================================
+template <int FG, int ET>
+__global__ __launch_bounds__(256, 2) void lin_fwd_kc_kernel(
+    const uint16_t* __restrict__ x, int ldx, int K, const uint16_t* __restrict__ img, int KPc,
+    const float* __restrict__ bias, uint16_t* __restrict__ Y, int ldy, int N, int n, int relu,
+    const float* __restrict__ rscale) {
+  // img: W^T as [FG * 128][KPc] 16-bit (zero past K and N), KPc % 32 == 0
+  constexpr int BK = 32, LS = BK + 8, NP = FG * 128;
+  constexpr int RG = 4 / FG;                     // row groups of 64 rows per block
+  constexpr int WCH = NP * BK / 8 / 256;         // 16-B weight chunks per thread per K chunk
+  __shared__ __attribute__((aligned(16))) uint16_t sW[2][NP * LS];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, lr = lane & 31, wv = tid >> 6;
+  const int fg = wv % FG, rg = wv / FG;
+  const int rbase = (blockIdx.x * RG + rg) * 64;   // this wave's 64 rows: two 32-row tiles
+  int rows[2];
+  bool rv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = rbase + 32 * u + lr;
+    rv[u] = r < n;
+    rows[u] = rv[u] ? r : n - 1;
+  }
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = f32x16{};
+  const int nch = KPc / BK;
+  uint4 wr[WCH];
+  auto wload = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < WCH; ++j) {
+      const int i = tid + 256 * j, rr = i / (BK / 8), cc = i % (BK / 8);
+      wr[j] = *reinterpret_cast<const uint4*>(img + (size_t)rr * KPc + c * BK + 8 * cc);
+    }
+  };
+  auto wstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < WCH; ++j) {
+      const int i = tid + 256 * j, rr = i / (BK / 8), cc = i % (BK / 8);
+      *reinterpret_cast<uint4*>(&sW[buf][rr * LS + 8 * cc]) = wr[j];
+    }
+  };
+  // X fragments of chunk c: k-steps s = 0, 1 at k = 32c + 16s + 8h for both row tiles;
+  // chunks past K re-read column 0 and are masked (padding columns may hold anything)
+  uint4 xb[2][2], xn[2][2];
+  auto xload = [&](int c, uint4 (&dst)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int k = BK * c + 16 * s + 8 * h;
+      const int kk = k < K ? k : 0;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        dst[u][s] = keep_first_sel(*reinterpret_cast<const uint4*>(x + (size_t)rows[u] * ldx + kk), K - k);
+    }
+  };
+  wload(0);
+  xload(0, xb);
+  wstore(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nch;
+    if (more) {
+      wload(c + 1);
+      xload(c + 1, xn);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint4 a = *reinterpret_cast<const uint4*>(&sW[buf][(128 * fg + 32 * t + lr) * LS + 16 * s + 8 * h]);
+        acc[0][t] = mma16<ET>(a, xb[0][s], acc[0][t]);
+        acc[1][t] = mma16<ET>(a, xb[1][s], acc[1][t]);
+      }
+    }
+    if (more) {
+      wstore(buf ^ 1);       // the other buffer: every wave finished reading it at the last barrier
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) xb[u][s] = xn[u][s];
+    }
+    __syncthreads();
+  }
+  // epilogue: lane = row, registers 4g..4g+3 = columns 32t + 8g + 4h + 0..3
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (!rv[u]) continue;
+    const int row = rows[u];
+    const float rs = rscale ? rscale[row] : 1.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 128 * fg + 32 * t + 8 * g + 4 * h;
+        if (c >= ldy) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float y = acc[u][t][4 * g + e] + ((bias && c + e < N) ? bias[c + e] : 0.f);
+          if (relu) y = fmaxf(y, 0.f);
+          v[e] = y * rs;
+        }
+        *reinterpret_cast<uint2*>(Y + (size_t)row * ldy + c) = pack4e<ET>(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
+// W^T image of the K-chunked kernel: img[c][k] = W[k][c], row stride KPc, zero outside
+template <int ET>
+__global__ __launch_bounds__(256) void lin_prep_kc_kernel(const float* __restrict__ W, int K, int N, int KPc,
+                                                          long total, uint16_t* __restrict__ img) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int k = (int)(i % KPc), c = (int)(i / KPc);
+  img[i] = e16_bits<ET>(k < K && c < N ? W[(size_t)k * N + c] : 0.f);
+}
+
+// ============================================================================
 // lin_bwd_data: dX^T[k][row] = sum_c W[k][c] (dY * m)[row][c] for the k slab
 // [blockIdx.y * kcols, +kcols); KN k-steps of 16 cover the N gradient columns.
 // Output k < K1 -> dX1, K1 <= k < K1 + K2 -> dX2; times rscale[row] (optional).
@@ -302,12 +457,10 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
   for (int tile = wave; tile < n_tiles; tile += n_waves) {
     const int row = tile * TILE + lr;
     const bool rv = row < n;
-    int fh = 8 * h;                              // opaque per tile, as in lin_fwd
-    asm volatile("" : "+v"(fh));
     bf16x8 by[KN];
 #pragma unroll
     for (int s = 0; s < KN; ++s)
-      by[s] = as_bf16x8(load_masked8(dY, lddy, Ym, ldym, mscale, N, rv ? row : n - 1, 16 * s + fh));
+      by[s] = as_bf16x8(rv ? load_masked8(dY, lddy, Ym, ldym, mscale, N, row, 16 * s + 8 * h) : make_uint4(0u, 0u, 0u, 0u));
     const float rs = (rv && rscale) ? rscale[row] : 1.f;
 #pragma unroll 1
     for (int t = 0; t < nt; ++t) {
@@ -563,6 +716,33 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
   return (int)hipGetLastError();
 }
 
+// K-chunked form: taken when the weight does not fit LDS whole and no lin_fwd-only
+// feature (dropout, concatenation, gather, fp32 tail) is asked for; N <= 256
+static bool kc_wanted(int K, int N, int ldy) {
+  const int Nc = std::max(N, ldy);
+  if (Nc > 256) return false;
+  const int ks = pick_ks(K);
+  if (ks < 0) return true;
+  return slab_cols(Nc, ks * 16) < (Nc + 31) / 32 * 32;
+}
+
+static int kc_pad(int K) { return (K + 31) / 32 * 32; }
+
+extern "C" int gnn_lin_fwd_kc_wanted(int K, int N, int ldy) { return kc_wanted(K, N, ldy) ? 1 : 0; }
+
+template <int FG, int ET>
+static int kc_launch(const uint16_t* x, int ldx, int K, const float* W, int N, const float* bias, uint16_t* Y,
+                     int ldy, int n, int relu, const float* rscale, uint16_t* wimg, hipStream_t st) {
+  const int KPc = kc_pad(K);
+  const long total = (long)FG * 128 * KPc;
+  hipLaunchKernelGGL(lin_prep_kc_kernel<ET>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K, N, KPc,
+                     total, wimg);
+  const int rows_per_block = 4 / FG * 64;
+  hipLaunchKernelGGL((lin_fwd_kc_kernel<FG, ET>), dim3((n + rows_per_block - 1) / rows_per_block), dim3(256), 0, st,
+                     x, ldx, K, wimg, KPc, bias, Y, ldy, N, n, relu, rscale);
+  return (int)hipGetLastError();
+}
+
 // et: element type of X / Y (0 bf16, 1 fp16: the inference path; fp16 takes K <= 768,
 // no dropout or fp32 tail)
 extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2, const float* W,
@@ -579,6 +759,15 @@ extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x
   auto a = (const uint16_t*)x1;
   auto b = (const uint16_t*)x2;
   auto y = (uint16_t*)Y;
+  if (!x2 && !idx1 && !thr8 && !Yf && kc_wanted(K1, N, ldy)) {
+    const int fg = std::max(N, ldy) > 128 ? 2 : 1;
+    auto w = (uint16_t*)wimg;
+    if (et == 1)
+      return fg == 2 ? kc_launch<2, 1>(a, ld1, K1, W, N, bias, y, ldy, n, relu, rscale, w, st)
+                     : kc_launch<1, 1>(a, ld1, K1, W, N, bias, y, ldy, n, relu, rscale, w, st);
+    return fg == 2 ? kc_launch<2, 0>(a, ld1, K1, W, N, bias, y, ldy, n, relu, rscale, w, st)
+                   : kc_launch<1, 0>(a, ld1, K1, W, N, bias, y, ldy, n, relu, rscale, w, st);
+  }
   if (et == 1) {
     if (thr8 || Yf) return -3;
 #define LH(c) if (ks == c) return fwd_launch<c, 1>(a, ld1, K1, b, ld2, K2, W, N, bias, y, ldy, n, relu, p, k0, k1, step, thr8, row0, stepp, rscale, idx1, (uint16_t*)wimg, Yf, nsplit, tk, st);
@@ -635,10 +824,11 @@ extern "C" int gnn_launch_lin_bwd_data(const void* dY, int lddy, const void* Ym,
 // (upper bounds over every slab width the launchers may pick for any row count:
 // slabs * width < columns + 256)
 extern "C" long gnn_lin_fwd_image_bytes(int K, int N, int ldy) {
+  const long kc = kc_wanted(K, N, ldy) ? 2L * 256 * kc_pad(K) : 0;
   const int ks = pick_ks(K);
-  if (ks < 0) return -1;
+  if (ks < 0) return kc > 0 ? kc : -1;
   const int KP = ks * 16;
-  return 2L * ((std::max(N, ldy) + 31) / 32 * 32 + 256) * (KP + 8);
+  return std::max(kc, 2L * ((std::max(N, ldy) + 31) / 32 * 32 + 256) * (KP + 8));
 }
 
 extern "C" long gnn_lin_bwd_image_bytes(int K, int N) {

@@ -294,7 +294,9 @@ class GATTrainer:
                  fused: Optional[bool] = None, reorder: bool = False):
         # reorder=True: the framework's locality pass first (data.reorder; the attention
         # kernels gather rows like the SpMM, so their L2 hit rate follows the order);
-        # accuracies are invariant, ``new_id`` maps caller ids to trainer rows
+        # evaluation and dropout-0 training are invariant, with dropout > 0 the masks are
+        # keyed by the relabelled rows (equal in distribution only); ``new_id`` maps
+        # caller ids to trainer rows
         self.new_id = None
         if reorder:
             from .data import reorder as _reorder

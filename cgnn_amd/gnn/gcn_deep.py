@@ -322,12 +322,11 @@ class GCNInference:
         # GPU: every transform on the hand-written MFMA layer (lin_fwd, fp16 / bf16 matrix
         # cores, the D^-1/2 row scale of the next gather in its epilogue) into fixed buffers
         self._lin = cuda and dtype in (torch.float16, torch.bfloat16)
-        # layers whose input is wider than this take the library GEMM: Reddit's 602-wide
-        # first layer is a plain GEMM (the features are pre-scaled, no epilogue), where
-        # the generic lin_fwd (3 weight slabs of K = 640 in LDS) measured 0.41 ms and the
-        # whole forward 4.72 ms against 4.47 ms with hipBLASLt (profiles/r03_configs);
-        # the second layer keeps lin_fwd with D^-1/2 in its epilogue.  Env knob for A/B.
-        self._lin_kmax = int(os.environ.get("CGNN_INFER_LIN_KMAX", "256"))
+        # every layer on the hand-written MFMA layer: Reddit's 602-wide first layer (a
+        # weight too wide for LDS whole) takes lin_fwd's K-chunked GEMM form; layers wider
+        # than CGNN_INFER_LIN_KMAX (env knob for A/B against the library GEMM) use
+        # torch.matmul instead
+        self._lin_kmax = int(os.environ.get("CGNN_INFER_LIN_KMAX") or "100000")
         if self._lin:
             self.z = [torch.zeros(g.n, W.shape[1], dtype=dtype, device=self.dev) for W in self.Wf]
             self.dinv32 = self.ng.dinv.float().contiguous()

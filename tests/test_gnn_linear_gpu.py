@@ -44,6 +44,32 @@ def test_lin_fwd_matches_reference(n, K, ld, N, ldy, relu, p, rs):
     assert torch.all(out.cpu()[:, N:] == 0)
 
 
+@pytest.mark.parametrize("n,K,ld,N,ldy,dt", [
+    (3001, 602, 608, 256, 256, torch.float16),    # Reddit's first layer (fp16 inference)
+    (3001, 602, 608, 256, 256, torch.bfloat16),
+    (1000, 700, 704, 100, 104, torch.bfloat16),   # one 128-column feature group, odd K
+    (70, 1000, 1000, 200, 200, torch.float16),    # fewer rows than one block
+])
+def test_lin_fwd_k_chunked_matches_reference(n, K, ld, N, ldy, dt):
+    """Weights too wide for LDS whole take the K-chunked GEMM (lin_fwd_kc_kernel): bias,
+    ReLU and row scale against the fp32 reference; padding columns of X hold NaN, which
+    must not leak into the product."""
+    from cgnn_amd import native
+    assert native.hip().gnn_lin_fwd_kc_wanted(K, N, ldy)
+    g = torch.Generator().manual_seed(K + N)
+    x = torch.full((n, ld), float("nan"), dtype=dt)
+    x[:, :K] = torch.randn(n, K, generator=g).to(dt)
+    W = torch.randn(K, N, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g) * 0.1
+    r = torch.rand(n, generator=g) + 0.5
+    ref = (x[:, :K].float() @ W.to(dt).float() + b).relu() * r[:, None]
+    out = lin_fwd(x.to(DEV), W.to(DEV), b.to(DEV), K1=K, relu=True, rscale=r.to(DEV), ldy=ldy)
+    torch.cuda.synchronize()
+    assert out.dtype == dt
+    _close(out[:, :N], ref, 2e-2, 2e-2)
+    assert torch.all(out.cpu()[:, N:] == 0)
+
+
 def test_lin_fwd_two_inputs_is_the_concatenation():
     g = torch.Generator().manual_seed(1)
     n, K1, K2, N = 3000, 256, 256, 256
