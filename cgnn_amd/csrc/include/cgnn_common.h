@@ -77,6 +77,38 @@ enum RngPurpose : uint32_t {
   RNG_SAMPLE     = 6u,   // GNN neighbour sampling             (node, salt, draw/4)
 };
 
+// ---- dropout keep masks (every GNN kernel, and ops.dropout_keep_mask on the host) ----
+// Unit n of row `row` of a dropout layer: n = 32 t + 8 g + 4 h + i, q = 4 g + i; the 16
+// units of one (row, t, h) share one call.  thr8 = round(256 p).
+//   byte mode (any p): byte q of the draw keyed (row, 2 t + h, step) kept iff >= thr8;
+//   bit mode (p = 1/2, thr8 = 128): bit 16 (t % 8) + q of the draw keyed
+//   (row, DROP_BIT_CTR + 2 (t / 8) + h, step) kept iff set -- one random bit per decision,
+//   so one draw covers eight 32-unit blocks (a 256-wide hidden layer draws once per
+//   (row, half) instead of eight times).
+constexpr uint32_t DROP_BIT_CTR = 0x80000000u;
+
+__device__ __forceinline__ bool drop_bit_mode(uint32_t thr8) { return thr8 == 128u; }
+
+__device__ __forceinline__ u32x4 drop_draw(uint32_t row, int t, int h, uint32_t step, uint32_t k0, uint32_t k1,
+                                           bool bit_mode) {
+  const uint32_t c = bit_mode ? DROP_BIT_CTR + 2u * (uint32_t)(t >> 3) + (uint32_t)h : 2u * (uint32_t)t + (uint32_t)h;
+  return philox4x32_10(u32x4{row, c, step, RNG_DROPOUT}, k0, k1);
+}
+
+// the 16 keep bits (bit q) of block t from its draw
+__device__ __forceinline__ uint32_t drop_keep16(const u32x4& r, int t, uint32_t thr8, bool bit_mode) {
+  if (bit_mode) {
+    const int wi = (t & 7) >> 1;
+    const uint32_t w = wi == 0 ? r.x : wi == 1 ? r.y : wi == 2 ? r.z : r.w;
+    return (w >> (16 * (t & 1))) & 0xffffu;
+  }
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  uint32_t m = 0u;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) m |= (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8 ? 1u : 0u) << q;
+  return m;
+}
+
 __device__ __forceinline__ float rng_normal(uint32_t k0, uint32_t k1, uint32_t a, uint32_t b,
                                             uint32_t step, uint32_t purpose) {
   u32x4 c = {a, b, step, purpose};

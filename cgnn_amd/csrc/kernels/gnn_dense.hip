@@ -23,6 +23,7 @@
 // processed in 32-row tiles, one tile per wave at a time, grid-strided.
 #include "cgnn_common.h"
 #include <algorithm>
+#include <cstdlib>
 
 using namespace cgnn;
 
@@ -55,6 +56,16 @@ __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 
+// x with the dropout decision of keep bit q of m applied: x AND the bit sign-extended
+// (v_bfe_i32 + v_and_b32; the AND is opaque so it is not turned back into a
+// test / compare / select sequence of three instructions)
+__device__ __forceinline__ float keep_and(float x, uint32_t m, uint32_t q) {
+  const uint32_t k = (uint32_t)__builtin_amdgcn_sbfe((int)m, q, 1);
+  uint32_t r;
+  asm("v_and_b32 %0, %1, %2" : "=v"(r) : "v"(__float_as_uint(x)), "v"(k));
+  return __uint_as_float(r);
+}
+
 // Byte offset of 16-B chunk `ch` of row `row` in a [32][256 B] staging image.  The
 // XOR swizzle keeps the b128 staging writes at the 8-way minimum and makes the b128
 // row reads and the ds_read_b64_tr_b16 column reads of the 32x32x16 operands
@@ -84,15 +95,16 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint16_t* base, int off0, int of
 }  // namespace
 
 // KS = k-steps of 16 over the input features (F <= 16*KS <= ldx rounded), HD hidden width;
-// DROP: dropout active (p > 0), a compile-time switch so the epilogue has no per-element
-// branches.
+// DROP: dropout mode, a compile-time switch so the epilogue has no per-element branches:
+// 0 none, 1 byte mode (any p), 2 bit mode (p = 1/2: one Philox draw per row and half for
+// all eight hidden blocks, cgnn_common.h drop_draw).
 //
 // Latency structure (the kernel runs 4 waves / SIMD -- one 16-wave block per CU -- and
 // was measured MFMA-busy ~23 %): per hidden tile t the accumulator starts as the bias
 // (4 b128 LDS reads issued ahead, fp32 exact) instead of a bias add per element after
 // the chain, and the KS weight fragments of the chain are read from LDS as one batch
 // before the first MFMA rather than one LDS round trip per MFMA.
-template <int KS, int HD, bool DROP>
+template <int KS, int HD, int DROP>
 __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
     const uint16_t* __restrict__ AX, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ dinv, uint16_t* __restrict__ H1,
@@ -113,9 +125,13 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
     const int k = i / HD, nn = i - k * HD;
     sW1T[nn * W1S + k] = bf16_bits(k < F ? W1[(size_t)k * HD + nn] : 0.f);
   }
+  // the dropout scale 1/(1-p) of the kept units is folded into W2^T (exact for p = 1/2):
+  // Z2 = (x * keep * s) W2 = (x * keep) (s W2), so the epilogue never multiplies
+  const float scale = 1.f / (1.f - p);
+  const float w2s = DROP != 0 ? scale : 1.f;
   for (int i = threadIdx.x; i < 64 * HD; i += blockDim.x) {
     const int nn = i / 64, c = i - nn * 64;
-    sW2T[c * W2S + nn] = bf16_bits(c < C ? W2[(size_t)nn * C + c] : 0.f);
+    sW2T[c * W2S + nn] = bf16_bits(c < C ? W2[(size_t)nn * C + c] * w2s : 0.f);
   }
   for (int i = threadIdx.x; i < HD; i += blockDim.x) sB1[i] = b1[i];
   __syncthreads();
@@ -124,7 +140,6 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
   const int wave = blockIdx.x * WAVES + (threadIdx.x >> 6);
   const int n_waves = gridDim.x * WAVES;
   const int n_tiles = (n + TILE - 1) / TILE;
-  const float scale = 1.f / (1.f - p);
 
   for (int tile = wave; tile < n_tiles; tile += n_waves) {
     const int row = tile * TILE + lr;
@@ -136,40 +151,40 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
       bx[s] = (rv && f0 < ldx) ? load_bf16x8(AX + (size_t)row * ldx + f0) : zero_bf16x8();
     }
     f32x16 z0 = {}, z1 = {};
+    static_assert(HD <= 256, "bit-mode dropout: one draw covers 8 hidden blocks");
+    u32x4 rb{};
+    if constexpr (DROP == 2) rb = drop_draw(row0 + (uint32_t)row, 0, h, step, k0, k1, true);
 #pragma unroll 1
     for (int t = 0; t < HD / 32; ++t) {
-      // accumulator = bias: registers 4g..4g+3 are hidden 32t + 8g + 4h + 0..3
-      f32x16 acc;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 bb = *reinterpret_cast<const float4*>(sB1 + 32 * t + 8 * g + 4 * h);
-        acc[4 * g] = bb.x; acc[4 * g + 1] = bb.y; acc[4 * g + 2] = bb.z; acc[4 * g + 3] = bb.w;
-      }
       const uint16_t* arow = sW1T + (32 * t + lr) * W1S + 8 * h;
       bf16x8 af[KS];
 #pragma unroll
       for (int s = 0; s < KS; ++s) af[s] = load_bf16x8(arow + 16 * s);
+      f32x16 acc = {};
 #pragma unroll
       for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bx[s], acc, 0, 0, 0);
-      // epilogue: relu, dropout (one Philox draw = this lane's 16 bytes)
+      // epilogue (registers 4g..4g+3 are hidden 32t + 8g + 4h + 0..3): bias (packed adds),
+      // relu, dropout as an AND with the sign-extended keep bit (the scale is in W2^T)
       float v[16];
-      if constexpr (DROP) {
-        const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
-        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const float x = fmaxf(acc[q], 0.f);
-          v[q] = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
-        }
-      } else {
+      for (int g = 0; g < 4; ++g) {
+        const float4 bb = *reinterpret_cast<const float4*>(sB1 + 32 * t + 8 * g + 4 * h);
+        const f2 lo = f2{acc[4 * g], acc[4 * g + 1]} + f2{bb.x, bb.y};
+        const f2 hi = f2{acc[4 * g + 2], acc[4 * g + 3]} + f2{bb.z, bb.w};
+        v[4 * g] = fmaxf(lo.x, 0.f); v[4 * g + 1] = fmaxf(lo.y, 0.f);
+        v[4 * g + 2] = fmaxf(hi.x, 0.f); v[4 * g + 3] = fmaxf(hi.y, 0.f);
+      }
+      if constexpr (DROP != 0) {
+        const uint32_t m = drop_keep16(DROP == 2 ? rb : drop_draw(row0 + (uint32_t)row, t, h, step, k0, k1, false), t,
+                                       thr8, DROP == 2);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = fmaxf(acc[q], 0.f);
+        for (int q = 0; q < 16; ++q) v[q] = keep_and(v[q], m, q);
       }
       if (rv && H1) {          // H1 == nullptr: the fused backward recomputes it
 #pragma unroll
         for (int g = 0; g < 4; ++g)
           *reinterpret_cast<uint2*>(H1 + (size_t)row * HD + 32 * t + 8 * g + 4 * h) =
-              pack4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+              pack4(v[4 * g] * w2s, v[4 * g + 1] * w2s, v[4 * g + 2] * w2s, v[4 * g + 3] * w2s);
       }
       // second product: Z2^T += W2^T[:, 32t..32t+31] * H1^T tile (accumulator as B operand)
 #pragma unroll
@@ -450,11 +465,10 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
         if (s2 < KC) dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[s2], y2[s2], dh, 0, 0, 0);
       }
     }
-    uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-    if constexpr (DROP) {
-      const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
-      w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
-    }
+    uint32_t m = 0xffffu;
+    if constexpr (DROP)
+      m = drop_keep16(drop_draw(row0 + (uint32_t)row, t, h, step, k0, k1, drop_bit_mode(thr8)), t, thr8,
+                      drop_bit_mode(thr8));
     // registers 4g..4g+3 = hidden 32t + 8g + 4h + 0..3 of this lane's row: one packed
     // 8-B write per image and g
 #pragma unroll
@@ -464,7 +478,7 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
       for (int i = 0; i < 4; ++i) {
         const int q = 4 * g + i;
         float x = fmaxf(acc[q], 0.f);
-        if constexpr (DROP) x = (((w[g] >> (8 * i)) & 0xffu) >= thr8) ? x * scale : 0.f;
+        if constexpr (DROP) x = ((m >> q) & 1u) ? x * scale : 0.f;
         xv[i] = x;
         dv[i] = x > 0.f ? dh[q] * scale : 0.f;
       }
@@ -510,6 +524,258 @@ __global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
   }
 }
 
+// ============================================================================
+// Fused backward, round-3 form: the same four products with the recompute chains
+// swapped to ROWS x HIDDEN output tiles,
+//   P1[row][h]  = AX[row][:] W1[:][h] (+ b1),   dP1[row][h] = dY2[row][:] W2^T[:][h],
+// so that the accumulators (lane = hidden unit, registers = 16 rows of the tile) are
+// ALREADY the A operands of the contractions over the rows (dP1^T, H1^T: hidden x
+// rows; the k order inside a 16-row step is permuted -- rows 4h..4h+3, 8+4h..8+4h+3
+// -- and the transposed B reads of AX / dY2 use the same permutation).  Against the
+// round-2 form above this removes, per wave and 32-row tile:
+//   * the 10 b128 LDS reads of the weight fragments: each wave owns one 32-unit hidden
+//     block for the whole launch, so its W1 / W2^T B fragments (KS + KC bf16x8) are
+//     loaded once into registers and the weights need no LDS at all;
+//   * the H1 / dP1 images (8 packed LDS writes, 8 transposed reads, a wave barrier).
+// LDS is the double-buffered AX / dY2 staging (32 KiB) and a 128-B keep-bit image per
+// wave and hidden block.  The dropout mask is the forward's (cgnn_common.h drop_draw):
+// each lane draws for its (row, half) as the forward does and writes its 16 keep bits
+// as one halfword of the image's word `row`; every lane then reads the 16 words of its
+// rows (four b128 reads) and takes its unit's bit with a sign-extending bit-field
+// extract -- the keep mask as an AND mask, no ballots, no per-element branches.  As
+// in the forward the 1/(1-p) of the kept units is applied once, to the weight-gradient
+// slab, not per element.  The bias is added in the epilogue (packed), not as the
+// accumulator's initial value.
+// ============================================================================
+constexpr size_t fused_bwd2_lds(int HD) { return sizeof(uint16_t) * 2 * 2 * 32 * 128 + sizeof(uint32_t) * HD; }
+
+// TB hidden blocks per wave (1: HD/32 waves of <= 256 registers, 2 waves / SIMD; 2: HD/64
+// waves of up to 512 registers -- accumulators in AGPRs -- one wave / SIMD, and every
+// LDS fragment a wave reads (the AX / dY2 rows, the transposed contraction operands)
+// feeds two hidden blocks' MFMAs, half the LDS traffic per tile)
+template <int KS, int KC, int HD, int DROP, int TB>
+__global__ __launch_bounds__(HD * 2 / TB, 1) void gcn_fused_bwd2_kernel(
+    const uint16_t* __restrict__ AX, const uint16_t* __restrict__ dY2, const float* __restrict__ W1,
+    const float* __restrict__ b1, const float* __restrict__ W2, float* __restrict__ gpart, int n, int F,
+    int ldx, int C, int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
+    uint32_t row0, const int* __restrict__ stepp) {
+  if (stepp) step = (uint32_t)*stepp;         // device-resident dropout step (graph replays)
+  constexpr int NW = HD / 32 / TB;            // waves per block; wave w owns hidden blocks w + NW b
+  constexpr int NT = NW * 64;
+  constexpr int KP = KS * 16;                 // layer-1 K (features + ones column), padded
+  constexpr int KF = (KP + 31) / 32 * 32;     // gW1^T columns (f), padded to whole tiles
+  constexpr int CP = KC * 16;                 // classes, padded
+  static_assert(KF <= 128 && CP <= 64, "staging rows are 256 B");
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* sStg = lds;                       // 2 x (AX [32][128] | dY2 [32][128]), stg_off swizzle
+  uint32_t* sKeep = reinterpret_cast<uint32_t*>(lds + 2 * 2 * TILE * 128);   // [NW * TB][32] words
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, h = lane >> 5, lr = lane & 31;
+  const int wv = tid >> 6;
+  const int gb = (lane >> 4) & 1, qq = (lane >> 2) & 3, pq = lane & 3;
+
+  // B fragments of the two recompute chains (lane = hidden unit, k = 16 s + 8 h + j)
+  bf16x8 w1f[TB][KS], w2f[TB][KC];
+  float bias[TB];
+#pragma unroll
+  for (int b = 0; b < TB; ++b) {
+    const int hid = 32 * (wv + NW * b) + lr;  // this lane's hidden unit in block b
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * s + 8 * h + j;
+        const float v = W1[(size_t)min(k, F - 1) * HD + hid];
+        w1f[b][s][j] = (__bf16)(k < F ? v : 0.f);
+      }
+#pragma unroll
+    for (int s = 0; s < KC; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = 16 * s + 8 * h + j;
+        const float v = W2[(size_t)hid * C + min(c, C - 1)];
+        w2f[b][s][j] = (__bf16)(c < C ? v : 0.f);
+      }
+    bias[b] = b1[hid];
+  }
+  for (int i = tid; i < 2 * 2 * TILE * 128 / 8; i += NT)
+    reinterpret_cast<uint4*>(sStg)[i] = make_uint4(0u, 0u, 0u, 0u);
+
+  const int n_tiles = (n + TILE - 1) / TILE;
+  const float scale = 1.f / (1.f - p);
+  const int xch = min(ldx, KP) / 8, ych = min(ldc, CP) / 8;
+  // this lane's hidden unit lr in the keep-bit image words: bit 16 half + q with
+  // half = (lr >> 2) & 1, q = 4 (lr >> 3) + (lr & 3) (the forward's register order)
+  const uint32_t kpos = 16u * ((lr >> 2) & 1) + 4u * (lr >> 3) + (lr & 3);
+
+  f32x16 g1[TB][KF / 32], g2[TB][2];
+#pragma unroll
+  for (int b = 0; b < TB; ++b) {
+#pragma unroll
+    for (int q = 0; q < KF / 32; ++q) g1[b][q] = f32x16{};
+    g2[b][0] = f32x16{};
+    g2[b][1] = f32x16{};
+  }
+
+  constexpr int PFX = (TILE * (KP / 8) + NT - 1) / NT, PFY = (TILE * (CP / 8) + NT - 1) / NT;
+  uint4 pax[PFX], pdy[PFY];
+  auto prefetch = [&](int tile) {
+    const int r0 = tile * TILE;
+#pragma unroll
+    for (int k = 0; k < PFX; ++k) {
+      const int i = tid + k * NT;
+      const int rr = i % TILE, ch = i / TILE;
+      pax[k] = (i < TILE * xch && r0 + rr < n)
+                   ? *reinterpret_cast<const uint4*>(AX + (size_t)(r0 + rr) * ldx + 8 * ch)
+                   : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int k = 0; k < PFY; ++k) {
+      const int i = tid + k * NT;
+      const int rr = i % TILE, ch = i / TILE;
+      pdy[k] = (i < TILE * ych && r0 + rr < n)
+                   ? *reinterpret_cast<const uint4*>(dY2 + (size_t)(r0 + rr) * ldc + 8 * ch)
+                   : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto stage = [&](int buf) {
+    char* const bA = reinterpret_cast<char*>(sStg + buf * 2 * TILE * 128);
+    char* const bD = bA + 2 * TILE * 128;
+#pragma unroll
+    for (int k = 0; k < PFX; ++k) {
+      const int i = tid + k * NT;
+      if (i < TILE * xch) *reinterpret_cast<uint4*>(bA + stg_off(i % TILE, i / TILE)) = pax[k];
+    }
+#pragma unroll
+    for (int k = 0; k < PFY; ++k) {
+      const int i = tid + k * NT;
+      if (i < TILE * ych) *reinterpret_cast<uint4*>(bD + stg_off(i % TILE, i / TILE)) = pdy[k];
+    }
+  };
+  const int G = gridDim.x;
+  __syncthreads();                            // the zeroed staging images
+  if ((int)blockIdx.x < n_tiles) {
+    prefetch(blockIdx.x);
+    stage(0);
+    if ((int)blockIdx.x + G < n_tiles) prefetch(blockIdx.x + G);
+  }
+  __syncthreads();
+
+  int it = 0;
+  for (int tile = blockIdx.x; tile < n_tiles; tile += G, ++it) {
+    const int cur = it & 1;
+    if (tile + G < n_tiles) {                 // stage the next tile, prefetch the one after
+      stage(cur ^ 1);
+      if (tile + 2 * G < n_tiles) prefetch(tile + 2 * G);
+    }
+    const uint16_t* const sAX = sStg + cur * 2 * TILE * 128;
+    const uint16_t* const sDY = sAX + TILE * 128;
+    const char* const bAX = reinterpret_cast<const char*>(sAX);
+    const char* const bDY = reinterpret_cast<const char*>(sDY);
+
+    // ---- recompute P1 and dP1 (rows x hidden blocks; lane = hidden, regs = rows) ----
+    f32x16 acc[TB], dh[TB];
+#pragma unroll
+    for (int b = 0; b < TB; ++b) {
+      acc[b] = f32x16{};
+      dh[b] = f32x16{};
+    }
+    {
+      bf16x8 x1[KS], y2[KC];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) x1[s] = load_bf16x8(reinterpret_cast<const uint16_t*>(bAX + stg_off(lr, 2 * s + h)));
+#pragma unroll
+      for (int s = 0; s < KC; ++s) y2[s] = load_bf16x8(reinterpret_cast<const uint16_t*>(bDY + stg_off(lr, 2 * s + h)));
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int b = 0; b < TB; ++b) {
+          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1[s], w1f[b][s], acc[b], 0, 0, 0);
+          if (s < KC) dh[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(y2[s], w2f[b][s], dh[b], 0, 0, 0);
+        }
+    }
+    // H1 = dropout(relu(P1 + b1)), dP1 = dh * [H1 > 0] (both without the 1/(1-p), applied
+    // to the slab), as the contractions' A operands (register 8 s + j = row
+    // 16 s + 8 (j / 4) + 4 h + j % 4)
+    bf16x8 ah1[TB][2], adp[TB][2];
+    static_assert(HD <= 256, "bit-mode dropout: one draw covers 8 hidden blocks");
+    u32x4 rb{};             // bit mode: the draw of (row lr, half h), shared by every block
+    if constexpr (DROP == 2) rb = drop_draw(row0 + (uint32_t)(tile * TILE + lr), 0, h, step, k0, k1, true);
+#pragma unroll
+    for (int b = 0; b < TB; ++b) {
+      uint4 kw[4];          // keep-bit words of rows 8 g + 4 h + 0..3
+      if constexpr (DROP != 0) {
+        const int t = wv + NW * b;
+        const uint32_t m = drop_keep16(DROP == 2 ? rb : drop_draw(row0 + (uint32_t)(tile * TILE + lr), t, h, step,
+                                                                  k0, k1, false),
+                                       t, thr8, DROP == 2);
+        uint32_t* img = sKeep + (wv * TB + b) * 32;
+        reinterpret_cast<uint16_t*>(img)[2 * lr + h] = (uint16_t)m;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+        for (int g = 0; g < 4; ++g) kw[g] = *reinterpret_cast<const uint4*>(img + 8 * g + 4 * h);
+      }
+      const f2 bb = {bias[b], bias[b]};
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const f2 z = f2{acc[b][r], acc[b][r + 1]} + bb;
+        float x[2] = {fmaxf(z.x, 0.f), fmaxf(z.y, 0.f)};
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int rr = r + e;
+          if constexpr (DROP != 0) {
+            const uint4 q4 = kw[rr >> 2];
+            const uint32_t wd = (rr & 3) == 0 ? q4.x : (rr & 3) == 1 ? q4.y : (rr & 3) == 2 ? q4.z : q4.w;
+            x[e] = keep_and(x[e], wd, kpos);
+          }
+          ah1[b][rr >> 3][rr & 7] = (__bf16)x[e];
+          adp[b][rr >> 3][rr & 7] = (__bf16)(x[e] > 0.f ? dh[b][rr] : 0.f);
+        }
+      }
+    }
+
+    // ---- contractions over the tile's 32 rows (two k-steps of 16, permuted rows) ----
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int ra = 16 * s2 + 4 * h + qq;      // block rows ra (+8 for the second read)
+      const int cb = 2 * gb + (pq >> 1), cx = 8 * (pq & 1);
+#pragma unroll
+      for (int q = 0; q < KF / 32; ++q) {
+        const bf16x8 bx = tr_frag(sAX, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 8, 4 * q + cb) + cx);
+#pragma unroll
+        for (int b = 0; b < TB; ++b) g1[b][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(adp[b][s2], bx, g1[b][q], 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const bf16x8 by = tr_frag(sDY, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 8, 4 * q + cb) + cx);
+#pragma unroll
+        for (int b = 0; b < TB; ++b) g2[b][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1[b][s2], by, g2[b][q], 0, 0, 0);
+      }
+    }
+    __syncthreads();      // this buffer is rewritten two tiles on; the next one is staged
+  }
+
+  // ---- this block's partial slab: rows = hidden 32t + m, columns [f | KF + c] ----
+  const float gs = DROP != 0 ? scale : 1.f;   // the kept units' 1/(1-p)
+  float* gp = gpart + (size_t)blockIdx.x * HD * (KF + 64);
+#pragma unroll
+  for (int b = 0; b < TB; ++b) {
+    const int t = wv + NW * b;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int hrow = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+      float* dst = gp + (size_t)hrow * (KF + 64);
+#pragma unroll
+      for (int fb = 0; fb < KF / 32; ++fb) dst[32 * fb + lr] = g1[b][fb][q] * gs;
+      dst[KF + lr] = g2[b][0][q] * gs;
+      dst[KF + 32 + lr] = g2[b][1][q] * gs;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- launchers
 static int dense_grid(int n) {
   static int cached_cus[64] = {0};
@@ -525,7 +791,7 @@ static int dense_grid(int n) {
   return std::max(1, std::min(cus, (tiles + WAVES - 1) / WAVES));
 }
 
-template <int KS, int HD, bool DROP>
+template <int KS, int HD, int DROP>
 static int fwd_launch_d(const uint16_t* AX, const float* W1, const float* b1, const float* W2,
                         const float* dinv, uint16_t* H1, uint16_t* Z2, int n, int F, int ldx, int C,
                         int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
@@ -543,10 +809,13 @@ static int fwd_launch(const uint16_t* AX, const float* W1, const float* b1, cons
                       const float* dinv, uint16_t* H1, uint16_t* Z2, int n, int F, int ldx, int C,
                       int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
                       uint32_t row0, const int* stepp, hipStream_t st) {
+  if (thr8 == 128)
+    return fwd_launch_d<KS, HD, 2>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
+                                   stepp, st);
   if (thr8 > 0)
-    return fwd_launch_d<KS, HD, true>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
-                                      stepp, st);
-  return fwd_launch_d<KS, HD, false>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
+    return fwd_launch_d<KS, HD, 1>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
+                                   stepp, st);
+  return fwd_launch_d<KS, HD, 0>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
                                      stepp, st);
 }
 
@@ -618,6 +887,29 @@ static int fused_bwd_launch(const uint16_t* AX, const uint16_t* dY2, const float
                             uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0,
                             const int* stepp, hipStream_t st) {
   constexpr int KP = KS * 16, CP = KC * 16;
+  // round-3 form by default; env CGNN_FUSED_BWD_V1=1 launches the round-2 form (A/B)
+  static const bool v1 = [] {
+    const char* e = std::getenv("CGNN_FUSED_BWD_V1");
+    return e && e[0] && e[0] != '0';
+  }();
+  // hidden blocks per wave of the round-3 form: env CGNN_FUSED_BWD_TB (1 or 2, default 1:
+  // 680 vs 772 us on the ogbn-products shape, profiles/r03_bwd)
+  static const int tb = [] {
+    const char* e = std::getenv("CGNN_FUSED_BWD_TB");
+    return e && e[0] == '2' ? 2 : 1;
+  }();
+  if (!v1) {
+    const size_t lds = fused_bwd2_lds(HD);
+    const int dm = thr8 == 128 ? 2 : thr8 > 0 ? 1 : 0;
+    auto kern = tb == 1 ? (dm == 2 ? gcn_fused_bwd2_kernel<KS, KC, HD, 2, 1>
+                           : dm == 1 ? gcn_fused_bwd2_kernel<KS, KC, HD, 1, 1> : gcn_fused_bwd2_kernel<KS, KC, HD, 0, 1>)
+                        : (dm == 2 ? gcn_fused_bwd2_kernel<KS, KC, HD, 2, 2>
+                           : dm == 1 ? gcn_fused_bwd2_kernel<KS, KC, HD, 1, 2> : gcn_fused_bwd2_kernel<KS, KC, HD, 0, 2>);
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(kern, dim3(gnn_fused_bwd_blocks(n)), dim3(HD * 2 / tb), lds, st,
+                       AX, dY2, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp);
+    return (int)hipGetLastError();
+  }
   const size_t lds2 = fused_bwd_lds(KP, CP, HD, 2);
   const size_t lds = lds2 <= 160 * 1024 ? lds2 : fused_bwd_lds(KP, CP, HD, 1);
   if (lds > 160 * 1024) return -2;

@@ -111,10 +111,10 @@ __device__ __forceinline__ void ld_w8(const void* base, size_t off, float* v) {
   raw_f32<WT>(r, v);
 }
 
-// Dropout convention of ops.dropout_keep_mask / the fused GCN kernels: column c is kept
-// iff byte (c % 4) + 4 ((c % 32) / 8) of the Philox draw keyed (row, 2 (c / 32) + (c % 8) / 4,
-// step) is >= thr8.  A lane's 8 columns f0..f0+7 (f0 % 8 == 0) read word (f0 % 32) / 8 of
-// the draws for h = 0 (first 4) and h = 1 (last 4).
+// Dropout convention of ops.dropout_keep_mask / the fused GCN kernels (cgnn_common.h
+// drop_draw / drop_keep16): column c = 32 t + 8 g + 4 h + i is decided by position
+// q = 4 g + i of the draw of (row, t, h).  A lane's 8 columns f0..f0+7 (f0 % 8 == 0) take
+// positions 4 g .. 4 g + 3 of the draws for h = 0 (first 4) and h = 1 (last 4).
 __device__ __forceinline__ void keep8(bool* kp, uint32_t thr8, uint32_t grow, int f0, uint32_t step, uint32_t k0,
                                       uint32_t k1) {
   if (thr8 == 0) {
@@ -123,12 +123,12 @@ __device__ __forceinline__ void keep8(bool* kp, uint32_t thr8, uint32_t grow, in
     return;
   }
   const int t = f0 >> 5, g = (f0 & 31) >> 3;
+  const bool bm = drop_bit_mode(thr8);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const u32x4 r = philox4x32_10(u32x4{grow, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
-    const uint32_t w = g == 0 ? r.x : g == 1 ? r.y : g == 2 ? r.z : r.w;
+    const uint32_t m = drop_keep16(drop_draw(grow, t, h, step, k0, k1, bm), t, thr8, bm);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) kp[4 * h + i] = ((w >> (8 * i)) & 0xffu) >= thr8;
+    for (int i = 0; i < 4; ++i) kp[4 * h + i] = (m >> (4 * g + i)) & 1u;
   }
 }
 

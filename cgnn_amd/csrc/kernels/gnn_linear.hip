@@ -262,19 +262,17 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
         acc = mma16<ET>(*reinterpret_cast<const uint4*>(arow + 16 * s), bx[s], acc);
       if (!rv) continue;
       const int cg = c0 + 32 * t;                // global column of this tile
-      uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-      if (thr8 > 0) {
-        const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * (cg / 32) + h), step, RNG_DROPOUT},
-                                      k0, k1);
-        w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
-      }
+      uint32_t m = 0xffffu;
+      if (thr8 > 0)
+        m = drop_keep16(drop_draw(row0 + (uint32_t)row, cg / 32, h, step, k0, k1, drop_bit_mode(thr8)), cg / 32, thr8,
+                        drop_bit_mode(thr8));
       float v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int cl = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
         float x = acc[q] + sB[cl];
         if (relu) x = fmaxf(x, 0.f);
-        if (thr8 > 0) x = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
+        if (thr8 > 0) x = ((m >> q) & 1u) ? x * scale : 0.f;
         v[q] = x * rs;
       }
 #pragma unroll

@@ -597,9 +597,10 @@ __global__ __launch_bounds__(256, 8) void spmm_ce_kernel(
 
 // H = dropout(relu(P + b)) in place on a bf16 [rows][ld] matrix (F valid columns,
 // F % 32 == 0).  Dropout keeps with probability 1-p (p quantised to 1/256) and scales
-// kept units by 1/(1-p).  Mask of element (row, n): byte (n%4) + 4*((n%32)/8) of the
-// Philox4x32 draw keyed (row, 2*(n/32) + (n/4)%2, step) -- the layout in which the
-// fused MFMA kernel (gnn_dense.hip) holds the values, so both produce the same mask.
+// kept units by 1/(1-p).  Mask of element (row, n), n = 32 t + 8 g + 4 h + i: position
+// q = 4 g + i of the draw of (row, t, h) (cgnn_common.h drop_draw / drop_keep16) -- the
+// layout in which the fused MFMA kernel (gnn_dense.hip) holds the values, so both
+// produce the same mask.
 // One thread per (row, 32-column group, half): 16 values, one draw.
 __global__ __launch_bounds__(256) void bias_relu_dropout_kernel(
     uint16_t* __restrict__ Hm, const float* __restrict__ bias, long rows, int F, int ld, float p,
@@ -613,11 +614,10 @@ __global__ __launch_bounds__(256) void bias_relu_dropout_kernel(
   const int k = (int)(threadIdx.x - rloc * tpr);
   const int t = k >> 1, h = k & 1;
   const float scale = 1.f / (1.f - p);
-  uint32_t w[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
-  if (thr8 > 0) {
-    const u32x4 r = philox4x32_10(u32x4{row0 + (uint32_t)row, (uint32_t)(2 * t + h), step, RNG_DROPOUT}, k0, k1);
-    w[0] = r.x; w[1] = r.y; w[2] = r.z; w[3] = r.w;
-  }
+  uint32_t m = 0xffffu;
+  if (thr8 > 0)
+    m = drop_keep16(drop_draw(row0 + (uint32_t)row, t, h, step, k0, k1, drop_bit_mode(thr8)), t, thr8,
+                    drop_bit_mode(thr8));
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int n0 = 32 * t + 8 * g + 4 * h;
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(256) void bias_relu_dropout_kernel(
     for (int i = 0; i < 4; ++i) {
       const int q = i + 4 * g;
       float x = fmaxf(v[i] + bias[n0 + i], 0.f);
-      if (thr8 > 0) x = (((w[q >> 2] >> (8 * (q & 3))) & 0xffu) >= thr8) ? x * scale : 0.f;
+      if (thr8 > 0) x = ((m >> q) & 1u) ? x * scale : 0.f;
       v[i] = x;
     }
     *ptr = make_uint2(f32_to_bf16_rne(v[0]) | (f32_to_bf16_rne(v[1]) << 16),

@@ -304,12 +304,16 @@ class GCNInference:
         # features pre-scaled by the column normalisation once (static input)
         self.xs = pad_cols(g.x.float() * g.dinv[:, None]).to(dtype).contiguous()
         self.W, self.b, self.Wf = [], [], []
+        # gathered rows: packed to 8 elements, or (env CGNN_INFER_ALIGN=1) padded to whole
+        # 128-B lines -- every gather of an aligned row touches exactly one line per 128 B
+        align = 64 if os.environ.get("CGNN_INFER_ALIGN", "0") != "0" and dtype != torch.float32 else 8
         for k, (W, b) in enumerate(weights):
             W = W.detach().float()
-            if k == 0 and W.shape[0] < self.xs.shape[1]:
-                W = torch.nn.functional.pad(W, (0, 0, 0, self.xs.shape[1] - F))
+            if W.shape[0] < (self.xs.shape[1] if k == 0 else self.W[-1].shape[1]):
+                W = torch.nn.functional.pad(
+                    W, (0, 0, 0, (self.xs.shape[1] if k == 0 else self.W[-1].shape[1]) - W.shape[0]))
             out = W.shape[1]
-            padded = (out + 7) // 8 * 8
+            padded = (out + align - 1) // align * align
             Wp = torch.zeros(W.shape[0], padded)
             Wp[:, :out] = W.cpu()
             bp = torch.zeros(padded)

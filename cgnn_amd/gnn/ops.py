@@ -289,21 +289,36 @@ def tall_gemm_tn(A: torch.Tensor, B: torch.Tensor, chunk: int = 8192) -> torch.T
     return out
 
 
+DROP_BIT_CTR = 0x80000000
+
+
 def dropout_keep_mask(rows: int, F: int, p: float, key, step, row0: int = 0) -> torch.Tensor:
-    """Keep mask of the fused dropout: element (row, n) uses byte (n%4) + 4*((n%32)//8)
-    of the Philox draw keyed (row, 2*(n//32) + (n//4)%2, step), kept if >= round(256 p)."""
+    """Keep mask of the fused dropout (host mirror of cgnn_common.h drop_draw /
+    drop_keep16).  Element (row, n), n = 32 t + 8 g + 4 h + i, q = 4 g + i:
+      byte mode (any p): byte q of the Philox draw keyed (row, 2 t + h, step), kept if
+      >= thr8 = round(256 p);
+      bit mode (p = 1/2, thr8 = 128): bit 16 (t % 8) + q of the draw keyed
+      (row, DROP_BIT_CTR + 2 (t // 8) + h, step), kept if set (one bit per decision)."""
     import numpy as np
     thr8 = min(255, int(np.floor(p * 256.0 + 0.5)))
     if thr8 == 0:
         return torch.ones(rows, F, dtype=torch.bool)
     r = (row0 + np.arange(rows)).astype(np.uint32)[:, None]
     n = np.arange(F)
-    ctr = (2 * (n // 32) + (n // 4) % 2).astype(np.uint32)[None, :]
-    words = np.stack(philox.philox4x32_10(r, ctr, step, philox.RNG_DROPOUT, key[0], key[1]), -1)
+    t, h = n // 32, (n // 4) % 2
     q = (n % 4) + 4 * ((n % 32) // 8)
-    wsel = np.take_along_axis(words, (q // 4)[None, :, None].repeat(rows, 0), -1)[..., 0]
-    byte = (wsel >> (8 * (q % 4)).astype(np.uint32)[None, :]) & 0xFF
-    return torch.from_numpy(byte >= thr8)
+    if thr8 == 128:
+        ctr = (DROP_BIT_CTR + 2 * (t // 8) + h).astype(np.uint32)[None, :]
+        b = 16 * (t % 8) + q
+    else:
+        ctr = (2 * t + h).astype(np.uint32)[None, :]
+        b = 8 * q
+    words = np.stack(philox.philox4x32_10(r, ctr, step, philox.RNG_DROPOUT, key[0], key[1]), -1)
+    wsel = np.take_along_axis(words, (b // 32)[None, :, None].repeat(rows, 0), -1)[..., 0]
+    bits = wsel >> (b % 32).astype(np.uint32)[None, :]
+    if thr8 == 128:
+        return torch.from_numpy((bits & 1) == 1)
+    return torch.from_numpy((bits & 0xFF) >= thr8)
 
 
 def bias_relu_dropout_(H, bias, F, p, key, step, row0=0):
