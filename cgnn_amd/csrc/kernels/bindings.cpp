@@ -55,11 +55,11 @@ int gnn_launch_spmm(const int*, const int*, const void*, void*, const float*, co
                     int, int, int, int, int, int, int, const float*, int, const float*, int, hipStream_t);
 int gnn_launch_spmm_ce(const int*, const int*, const void*, const float*, const float*,
                        const int*, const uint8_t*, float*, void*, const float*, int, int, int, int, int, float,
-                       const int*, hipStream_t);
+                       const int*, int, hipStream_t);
 int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, float, float, float,
                     const int*, hipStream_t);
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
-int gnn_spmm_ce_blocks(int);
+int gnn_spmm_ce_blocks(int, int);
 int gnn_spmm_win_rows(int);
 int gnn_slab_sum(const float*, long, int, float*, int, float*, const int*, hipStream_t);
 int gnn_spmm_win_plan(const int*, const int*, void*, int, int, int, int, int, hipStream_t);
@@ -246,14 +246,16 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("cscale") = 0, py::arg("init_rows") = -1);
   m.def("gnn_spmm_ce", [](uint64_t rowptr, uint64_t col, uint64_t z, uint64_t rscale, uint64_t bias,
                           uint64_t labels, uint64_t mask, uint64_t stats, uint64_t dlogits, uint64_t init, int ldi,
-                          int n_rows, int C, int ld, int mode, float inv_count, uint64_t st, uint64_t gslot) {
+                          int n_rows, int C, int ld, int mode, float inv_count, uint64_t st, uint64_t gslot,
+                          int n_long) {
     chk(gnn_launch_spmm_ce(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(z), Pt<const float>(rscale),
                            Pt<const float>(bias), Pt<const int>(labels), Pt<const uint8_t>(mask),
                            Pt<float>(stats), Pt<void>(dlogits), Pt<const float>(init), ldi, n_rows, C, ld, mode,
-                           inv_count, Pt<const int>(gslot), S(st)), "gnn_spmm_ce");
+                           inv_count, Pt<const int>(gslot), n_long, S(st)), "gnn_spmm_ce");
   }, py::arg("rowptr"), py::arg("col"), py::arg("z"), py::arg("rscale"), py::arg("bias"), py::arg("labels"),
      py::arg("mask"), py::arg("stats"), py::arg("dlogits"), py::arg("init"), py::arg("ldi"), py::arg("n_rows"),
-     py::arg("C"), py::arg("ld"), py::arg("mode"), py::arg("inv_count"), py::arg("st"), py::arg("gslot") = 0);
+     py::arg("C"), py::arg("ld"), py::arg("mode"), py::arg("inv_count"), py::arg("st"), py::arg("gslot") = 0,
+     py::arg("n_long") = 0);
   m.def("gnn_adam", [](uint64_t p, uint64_t mm, uint64_t vv, uint64_t g, int n, float lr, float b1, float b2,
                        float eps, float wd, uint64_t step, uint64_t st) {
     chk(gnn_launch_adam(Pt<float>(p), Pt<float>(mm), Pt<float>(vv), Pt<const float>(g), n, lr, b1, b2, eps, wd,

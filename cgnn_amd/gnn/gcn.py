@@ -374,6 +374,10 @@ class GCNTrainer:
         lo, deg = rp[trows], rp[trows + 1] - rp[trows]
         if placeholder:
             deg = torch.zeros_like(deg)
+        # the long rows first (spmm_ce gives each a whole wave, ops.long_row_order); the
+        # compact-gradient slot stays the row's position among the ascending train rows
+        order, n_long = ops.long_row_order(deg)
+        trows, lo, deg = trows[order], lo[order], deg[order]
         trp = torch.zeros(trows.numel() + 1, dtype=torch.int64, device=dev)
         trp[1:] = torch.cumsum(deg, 0)
         eid = torch.arange(int(trp[-1]), device=dev) + torch.repeat_interleave(lo - trp[:-1], deg)
@@ -382,7 +386,7 @@ class GCNTrainer:
             dinv=self.dinv[trows].contiguous(), y=self.y[trows].contiguous(),
             mask=torch.zeros_like(self.mask[trows]) if placeholder else self.mask[trows].contiguous(),
             gslot=torch.full((1,), -1, dtype=torch.int32, device=dev) if placeholder
-            else torch.arange(trows.numel(), dtype=torch.int32, device=dev))
+            else order.to(torch.int32).contiguous(), n_long=n_long)
         l2.plan = None
         if self.multi:
             l2.rp_loc, l2.col_loc, l2.rp_rem, col_rem = self._split_local(self.r0, self.r1, l2.rp, l2.col)
@@ -525,7 +529,8 @@ class GCNTrainer:
             dinv, y, mask, gslot = self.dinv, self.y, self.mask, (self.gslot if train else None)
         stats, _ = ops.spmm_ce(rp, col, zsrc, C, dinv, self.b2, y, mask,
                                1.0 / max(self.n_train, 1), mode=0 if train else 1,
-                               G=self.Gc_loc if train else None, init=init, gslot=gslot)
+                               G=self.Gc_loc if train else None, init=init, gslot=gslot,
+                               n_long=l2.n_long if l2 is not None else 0)
         return stats
 
     def backward(self, stats):

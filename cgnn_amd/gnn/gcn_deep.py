@@ -212,12 +212,15 @@ class _FusedDeepGCN:
         if trows.numel() and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
             rpl = self.rowptr.long()
             lo, dg = rpl[trows], rpl[trows + 1] - rpl[trows]
+            # long rows first (a whole wave each in spmm_ce); slot = ascending position
+            order, self._tr_long = ops.long_row_order(dg)
+            trows, lo, dg = trows[order], lo[order], dg[order]
             trp = torch.zeros(trows.numel() + 1, dtype=torch.int64, device=dev)
             trp[1:] = torch.cumsum(dg, 0)
             eid = torch.arange(int(trp[-1]), device=dev) + torch.repeat_interleave(lo - trp[:-1], dg)
             self._tr = (trp.to(torch.int32).contiguous(), self.col[eid].contiguous(),
                         self.dinv[trows].contiguous(), self.y[trows].contiguous(), self.mask[trows].contiguous(),
-                        torch.arange(trows.numel(), dtype=torch.int32, device=dev))
+                        order.to(torch.int32).contiguous())
         self.last_stats = None
 
     def _dropout_step(self):
@@ -236,7 +239,8 @@ class _FusedDeepGCN:
         if train and self._tr is not None:
             rp, col, dinv, y, mask, gslot = self._tr
             stats, _ = ops.spmm_ce(rp, col, self.Zs, self.C, dinv, self.b[L - 1], y, mask,
-                                   1.0 / max(self.n_train, 1), mode=0, G=self.Gc, gslot=gslot)
+                                   1.0 / max(self.n_train, 1), mode=0, G=self.Gc, gslot=gslot,
+                                   n_long=self._tr_long)
             return stats
         stats, _ = ops.spmm_ce(self.rowptr, self.col, self.Zs, self.C, self.dinv, self.b[L - 1], self.y, self.mask,
                                1.0 / max(self.n_train, 1), mode=0 if train else 1, G=self.Gc if train else None,
@@ -304,9 +308,9 @@ class GCNInference:
         # features pre-scaled by the column normalisation once (static input)
         self.xs = pad_cols(g.x.float() * g.dinv[:, None]).to(dtype).contiguous()
         self.W, self.b, self.Wf = [], [], []
-        # gathered rows: packed to 8 elements, or (env CGNN_INFER_ALIGN=1) padded to whole
-        # 128-B lines -- every gather of an aligned row touches exactly one line per 128 B
-        align = 64 if os.environ.get("CGNN_INFER_ALIGN", "0") != "0" and dtype != torch.float32 else 8
+        # gathered rows padded to whole 128-B lines (env CGNN_INFER_ALIGN=0: packed to 8 elements;
+        # Reddit layer 2: 1.24 vs 1.40 ms, profiles/r03_cfgs) -- an aligned row touches whole lines only
+        align = 64 if os.environ.get("CGNN_INFER_ALIGN", "1") != "0" and dtype != torch.float32 else 8
         for k, (W, b) in enumerate(weights):
             W = W.detach().float()
             if W.shape[0] < (self.xs.shape[1] if k == 0 else self.W[-1].shape[1]):

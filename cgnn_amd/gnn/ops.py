@@ -6,6 +6,9 @@ mandatory -- a missing extension raises instead of silently falling back.
 """
 from __future__ import annotations
 
+import os
+from typing import Optional
+
 import torch
 
 from .. import native
@@ -85,15 +88,30 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
 _DB_INDEX = {}
 
 
+def long_row_order(deg: torch.Tensor, threshold: Optional[int] = None):
+    """Row order for ``spmm_ce(..., n_long=k)``: the rows of degree > threshold first (in
+    their original order), then the others; returns (order, k).  Default threshold: env
+    CGNN_CE_LONG (0 disables the long-row mode)."""
+    if threshold is None:
+        threshold = int(os.environ.get("CGNN_CE_LONG", "256"))
+    if threshold <= 0:
+        return torch.arange(deg.numel(), device=deg.device), 0
+    longr = deg > threshold
+    order = torch.cat([torch.nonzero(longr).flatten(), torch.nonzero(~longr).flatten()])
+    return order, int(longr.sum())
+
+
 def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=None, init=None, gslot=None,
-            db_out=None):
+            db_out=None, n_long=0):
     """Layer-2 aggregate + log-softmax + NLL.  Returns (stats[68] summed, G).
     ``init`` (optional fp32 [n, >=C]): partial sums of other edges.
     ``gslot`` (optional int32 [n]): G is compact -- row i (a train row, gslot[i] >= 0)
     goes to G[gslot[i]], other rows (whose dlogits are zero) are not written.
     ``db_out`` (optional fp32 [C], GPU): the per-class dlogits sums (the bias gradient,
     stats[4:4 + C]) are also summed straight into it -- a second fixed-order pass over
-    the partials instead of a device-to-device copy."""
+    the partials instead of a device-to-device copy.
+    ``n_long``: rows [0, n_long) are long rows the caller ordered first; the GPU kernel
+    gives each of them a whole wave (see ``long_row_order``).  Results do not depend on it."""
     if checks.enabled():
         checks.csr(rowptr, col, Z.shape[0], "spmm_ce")
         checks.rows(labels, rowptr.numel() - 1, "spmm_ce labels")
@@ -102,7 +120,7 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
     ld = Z.shape[1]
     if Z.is_cuda:
         hip = native.hip()
-        nb = hip.gnn_spmm_ce_blocks(n)
+        nb = hip.gnn_spmm_ce_blocks(n, int(n_long))
         stats = torch.empty(nb, 68, dtype=torch.float32, device=Z.device)
         if G is None and mode == 0:
             if gslot is not None:
@@ -114,7 +132,7 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
                         labels.data_ptr(), mask.data_ptr(), stats.data_ptr(), G.data_ptr() if G is not None else 0,
                         init.data_ptr() if init is not None else 0, init.shape[1] if init is not None else 0,
                         n, C, ld, mode, float(inv_count), _st(Z),
-                        gslot.data_ptr() if gslot is not None else 0)
+                        gslot.data_ptr() if gslot is not None else 0, int(n_long))
         out = torch.empty(68, dtype=torch.float32, device=Z.device)
         slab_sum(stats, out)
         if db_out is not None:
