@@ -36,6 +36,7 @@
 #include "cgnn_common.h"
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 using namespace cgnn;
 
@@ -413,6 +414,107 @@ __global__ __launch_bounds__(256, 2) void lin_fwd_kc_kernel(
   }
 }
 
+// ============================================================================
+// lin_gemm: Y = epi(X W) for a weight too wide for one LDS slab (K up to thousands,
+// N <= 256; Reddit's 602-wide first layer): a 256-row x 256-column output tile per
+// block of 8 waves (4 x 2, each 64 rows x 128 columns: 8 accumulators), X and the W^T
+// image streamed through double-buffered LDS in K chunks of 64 (the next chunk's global
+// loads in flight during the current chunk's 32 MFMAs per wave, one barrier per
+// chunk).  LDS rows are 128 B; 16-B chunk c of row r is stored at c ^ ((r >> 1) & 7),
+// which makes the ds_read_b128 fragment reads of any 16 consecutive rows hit 16
+// distinct 4-bank groups.  Output computed transposed (lane = row) as in
+// lin_fwd_kc_kernel; bias, ReLU and the row scale in the epilogue.
+// ============================================================================
+__device__ __forceinline__ int gemm_off(int r, int ch) { return r * 64 + 8 * (ch ^ ((r >> 1) & 7)); }
+
+template <int ET>
+__global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
+    const uint16_t* __restrict__ x, int ldx, int K, const uint16_t* __restrict__ img, int KPc,
+    const float* __restrict__ bias, uint16_t* __restrict__ Y, int ldy, int N, int n, int relu,
+    const float* __restrict__ rscale) {
+  constexpr int BM = 256, BK = 64;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  uint16_t* sX = lds;                       // [2][BM * BK]
+  uint16_t* sW = lds + 2 * BM * BK;         // [2][256 * BK]
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, lr = lane & 31, wv = tid >> 6;
+  const int rg = wv & 3, ng = wv >> 2;
+  const int row0 = blockIdx.x * BM;
+  const int nch = KPc / BK;
+  uint4 xr[4], wr[4];
+  auto load = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + 512 * j, r = i >> 3, ch = i & 7;
+      const int k = BK * c + 8 * ch;
+      const int row = row0 + r;
+      const uint4 v = *reinterpret_cast<const uint4*>(x + (size_t)(row < n ? row : n - 1) * ldx + (k < K ? k : 0));
+      xr[j] = keep_first_sel(v, row < n ? K - k : 0);
+      wr[j] = *reinterpret_cast<const uint4*>(img + (size_t)r * KPc + k);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + 512 * j, r = i >> 3, ch = i & 7;
+      *reinterpret_cast<uint4*>(sX + buf * BM * BK + gemm_off(r, ch)) = xr[j];
+      *reinterpret_cast<uint4*>(sW + buf * 256 * BK + gemm_off(r, ch)) = wr[j];
+    }
+  };
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = f32x16{};
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) load(c + 1);
+    const uint16_t* bx = sX + buf * BM * BK;
+    const uint16_t* bw = sW + buf * 256 * BK;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      uint4 xb[2], wa[4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        xb[u] = *reinterpret_cast<const uint4*>(bx + gemm_off(64 * rg + 32 * u + lr, 2 * s + h));
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        wa[t] = *reinterpret_cast<const uint4*>(bw + gemm_off(128 * ng + 32 * t + lr, 2 * s + h));
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[u][t] = mma16<ET>(wa[t], xb[u], acc[u][t]);
+    }
+    if (c + 1 < nch) store(buf ^ 1);   // the other buffer: its last reader finished at the last barrier
+    __syncthreads();
+  }
+  // epilogue: lane = row, registers 4g..4g+3 = columns 128 ng + 32 t + 8 g + 4 h + 0..3
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = row0 + 64 * rg + 32 * u + lr;
+    if (row >= n) continue;
+    const float rs = rscale ? rscale[row] : 1.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = 128 * ng + 32 * t + 8 * g + 4 * h;
+        if (col >= ldy) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float y = acc[u][t][4 * g + e] + ((bias && col + e < N) ? bias[col + e] : 0.f);
+          if (relu) y = fmaxf(y, 0.f);
+          v[e] = y * rs;
+        }
+        *reinterpret_cast<uint2*>(Y + (size_t)row * ldy + col) = pack4e<ET>(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
 // W^T image of the K-chunked kernel: img[c][k] = W[k][c], row stride KPc, zero outside
 template <int ET>
 __global__ __launch_bounds__(256) void lin_prep_kc_kernel(const float* __restrict__ W, int K, int N, int KPc,
@@ -724,7 +826,7 @@ static bool kc_wanted(int K, int N, int ldy) {
   return slab_cols(Nc, ks * 16) < (Nc + 31) / 32 * 32;
 }
 
-static int kc_pad(int K) { return (K + 31) / 32 * 32; }
+static int kc_pad(int K) { return (K + 63) / 64 * 64; }   // chunks of 32 (kc) and 64 (lin_gemm)
 
 extern "C" int gnn_lin_fwd_kc_wanted(int K, int N, int ldy) { return kc_wanted(K, N, ldy) ? 1 : 0; }
 
@@ -735,6 +837,18 @@ static int kc_launch(const uint16_t* x, int ldx, int K, const float* W, int N, c
   const long total = (long)FG * 128 * KPc;
   hipLaunchKernelGGL(lin_prep_kc_kernel<ET>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K, N, KPc,
                      total, wimg);
+  // the 256 x 256 tiled GEMM (default; env CGNN_LIN_GEMM=0: the kc kernel, A/B)
+  static const bool gemm = [] {
+    const char* e = std::getenv("CGNN_LIN_GEMM");
+    return !(e && e[0] == '0');
+  }();
+  if (gemm && FG == 2) {
+    const size_t lds = sizeof(uint16_t) * 2 * (256 + 256) * 64;
+    (void)hipFuncSetAttribute((const void*)lin_gemm_kernel<ET>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((lin_gemm_kernel<ET>), dim3((n + 255) / 256), dim3(512), lds, st, x, ldx, K, wimg, KPc, bias, Y,
+                       ldy, N, n, relu, rscale);
+    return (int)hipGetLastError();
+  }
   const int rows_per_block = 4 / FG * 64;
   hipLaunchKernelGGL((lin_fwd_kc_kernel<FG, ET>), dim3((n + rows_per_block - 1) / rows_per_block), dim3(256), 0, st,
                      x, ldx, K, wimg, KPc, bias, Y, ldy, N, n, relu, rscale);
