@@ -100,15 +100,50 @@ def test_fused_dense_matches_reference():
     np.testing.assert_allclose(d.numpy(), d_ref.numpy(), atol=2e-3, rtol=5e-2)
 
 
-def test_dropout_mask_matches_reference():
+@pytest.mark.parametrize("p", [0.5, 0.3])     # bit mode (p = 1/2) and byte mode
+def test_dropout_mask_matches_reference(p):
     torch.manual_seed(2)
     H = torch.randn(300, 256).to(torch.bfloat16)
     b = torch.randn(256)
-    ref = ops.bias_relu_dropout_(H.clone(), b, 256, 0.5, (123, 456), 7)
-    got = ops.bias_relu_dropout_(H.clone().cuda(), b.cuda(), 256, 0.5, (123, 456), 7).cpu()
+    ref = ops.bias_relu_dropout_(H.clone(), b, 256, p, (123, 456), 7)
+    got = ops.bias_relu_dropout_(H.clone().cuda(), b.cuda(), 256, p, (123, 456), 7).cpu()
     np.testing.assert_allclose(got.float().numpy(), ref.float().numpy(), rtol=1e-2, atol=1e-2)
     keep = (got.float() != 0).float().mean().item()
-    assert 0.2 < keep < 0.4   # relu (~1/2) x keep (1/2)
+    assert 0.5 * (1 - p) - 0.05 < keep < 0.5 * (1 - p) + 0.05   # relu (~1/2) x keep (1 - p)
+
+
+def test_spmm_ce_long_rows_on_whole_waves_match_reference():
+    """spmm_ce with n_long > 0 (the rows ordered long-first, each on a whole wave: its
+    8 sub-groups walk every 8th chunk and combine) equals the CPU reference, whose
+    result does not depend on n_long."""
+    torch.manual_seed(3)
+    n, C, ld = 900, 47, 48
+    deg = torch.randint(0, 20, (n,))
+    deg[torch.randperm(n)[:60]] = torch.randint(100, 700, (60,))     # power-law-ish tail
+    order, n_long = ops.long_row_order(deg, threshold=64)
+    assert n_long == 60
+    deg = deg[order]
+    rp = torch.zeros(n + 1, dtype=torch.int32)
+    rp[1:] = torch.cumsum(deg, 0).to(torch.int32)
+    col = torch.randint(0, n, (int(rp[-1]),), dtype=torch.int32)
+    Z = torch.zeros(n, ld, dtype=torch.bfloat16)
+    Z[:, :C] = torch.randn(n, C).to(torch.bfloat16)
+    rs = torch.rand(n) + 0.5
+    b = torch.randn(C)
+    y = torch.randint(0, C, (n,), dtype=torch.int32)
+    mask = torch.randint(1, 4, (n,), dtype=torch.uint8)
+    init = torch.randn(n, ld) * 0.1
+    inv = 1.0 / float((mask == 1).sum())
+    s_ref, g_ref = ops.spmm_ce(rp, col, Z, C, rs, b, y, mask, inv, mode=0, init=init)
+    s_got, g_got = ops.spmm_ce(rp.cuda(), col.cuda(), Z.cuda(), C, rs.cuda(), b.cuda(), y.cuda(), mask.cuda(),
+                               inv, mode=0, init=init.cuda(), n_long=n_long)
+    np.testing.assert_allclose(s_got.cpu().numpy()[:4], s_ref.numpy()[:4], rtol=1e-3, atol=1e-2)
+    np.testing.assert_allclose(s_got.cpu().numpy()[4:4 + C], s_ref.numpy()[4:4 + C], atol=1e-5)
+    np.testing.assert_allclose(g_got.cpu().float().numpy(), g_ref.float().numpy(), atol=2e-5, rtol=2e-2)
+    # and equal to the same launch without the long-row mode
+    s0, g0 = ops.spmm_ce(rp.cuda(), col.cuda(), Z.cuda(), C, rs.cuda(), b.cuda(), y.cuda(), mask.cuda(),
+                         inv, mode=0, init=init.cuda(), n_long=0)
+    np.testing.assert_allclose(g_got.cpu().float().numpy(), g0.cpu().float().numpy(), atol=1e-6, rtol=1e-2)
 
 
 @pytest.mark.parametrize("name,fused", [("cora", True), ("ogbn-arxiv", True), ("ogbn-products", True),

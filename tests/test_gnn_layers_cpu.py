@@ -224,3 +224,24 @@ def test_fused_deep_gcn_train_row_last_layer_matches_all_rows(monkeypatch):
     np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=1e-4)
     torch.testing.assert_close(runs[1][1], runs[0][1], rtol=1e-3, atol=1e-4)
     assert runs[1][2]["val_acc"] == pytest.approx(runs[0][2]["val_acc"], abs=0.01)
+
+
+def test_dropout_keep_mask_bit_and_byte_modes():
+    """ops.dropout_keep_mask: p = 1/2 uses one random bit per decision (bit 16 (t % 8) + q
+    of the draw keyed (row, DROP_BIT_CTR + 2 (t // 8) + h)), other p a byte per decision;
+    both keep ~1 - p, depend only on the global row, and differ between the two modes."""
+    import numpy as np
+    from cgnn_amd.gnn.ops import dropout_keep_mask, DROP_BIT_CTR
+    from cgnn_amd.utils import philox
+    for p in (0.5, 0.25):
+        m = dropout_keep_mask(400, 512, p, (9, 11), 5)
+        assert abs(m.float().mean().item() - (1 - p)) < 0.02
+        part = dropout_keep_mask(100, 512, p, (9, 11), 5, row0=300)
+        assert torch.equal(part, m[300:])
+    # one unit by hand in bit mode: row 17, unit n = 32 t + 8 g + 4 h + i
+    n = 32 * 9 + 8 * 2 + 4 * 1 + 3
+    t, g, h, i = 9, 2, 1, 3
+    w = philox.philox4x32_10(np.uint32(17), np.uint32(DROP_BIT_CTR + 2 * (t // 8) + h), 5, philox.RNG_DROPOUT, 9, 11)
+    b = 16 * (t % 8) + 4 * g + i
+    bit = (int(np.asarray(w[b // 32])) >> (b % 32)) & 1
+    assert bool(dropout_keep_mask(18, 512, 0.5, (9, 11), 5)[17, n]) == bool(bit)
