@@ -60,6 +60,8 @@ int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, flo
                     const int*, hipStream_t);
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
 int gnn_spmm_ce_blocks(int, int);
+int gnn_launch_ell_build(const int*, const int*, int*, int, hipStream_t);
+int gnn_launch_spmm_ell(const int*, const int*, const void*, void*, const float*, int, int, int, int, hipStream_t);
 int gnn_spmm_win_rows(int);
 int gnn_slab_sum(const float*, long, int, float*, int, float*, const int*, hipStream_t);
 int gnn_spmm_win_plan(const int*, const int*, void*, int, int, int, int, int, hipStream_t);
@@ -262,6 +264,14 @@ PYBIND11_MODULE(_hip, m) {
                         Pt<const int>(step), S(st)), "gnn_adam");
   });
   m.def("gnn_spmm_ce_blocks", &gnn_spmm_ce_blocks);
+  m.def("gnn_ell_build", [](uint64_t rowptr, uint64_t col, uint64_t ell, int n_rows, uint64_t st) {
+    chk(gnn_launch_ell_build(Pt<const int>(rowptr), Pt<const int>(col), Pt<int>(ell), n_rows, S(st)), "gnn_ell_build");
+  });
+  m.def("gnn_spmm_ell", [](uint64_t ell, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, int n_rows, int F,
+                           int ldx, int ldy, uint64_t st) {
+    chk(gnn_launch_spmm_ell(Pt<const int>(ell), Pt<const int>(col), Pt<const void>(x), Pt<void>(y),
+                            Pt<const float>(rscale), n_rows, F, ldx, ldy, S(st)), "gnn_spmm_ell");
+  });
   m.def("gnn_spmm_win_rows", &gnn_spmm_win_rows);
   m.def("gnn_slab_sum", [](uint64_t P, long rows, int W, uint64_t stage, int G, uint64_t out, uint64_t map,
                            uint64_t st) {

@@ -469,6 +469,67 @@ __global__ __launch_bounds__(256, CGNN_SPMM_MINW) void spmm_kernel(
   }
 }
 
+// Short-row aggregate from an ELL image (the GCN backward's train-column adjacency: ~4
+// entries per row): ell[row][0..7] holds the row's column ids (-1 past its end) or, for a
+// row of more than 8 entries, {-2, e0, e1}: its range in the CSR `col`.  One 32-B load
+// gives the 8-lane sub-group its whole row, so a row costs two dependent round trips
+// (indices, rows) instead of three (row bounds, indices, rows).  bf16 in / out, F <= 64,
+// Y[row] = rscale[row] * sum, padding columns 0.
+__global__ __launch_bounds__(256) void spmm_ell_kernel(const int* __restrict__ ell, const int* __restrict__ col,
+                                                       const uint16_t* __restrict__ X, uint16_t* __restrict__ Y,
+                                                       const float* __restrict__ rscale, int n_rows, int F,
+                                                       int ldx, int ldy) {
+  constexpr int L = 8, RPW = 8;
+  const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
+  const unsigned blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = (blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
+  const bool rv = row < n_rows;
+  const int f0 = sl * 8;
+  const bool fv = rv && f0 < F;
+  const int myj = rv ? ell[(size_t)row * 8 + sl] : -1;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int j0 = __shfl(myj, sub * L, 64);
+  if (j0 == -2) {                          // a long row: its CSR range
+    const int e0 = __shfl(myj, sub * L + 1, 64), e1 = __shfl(myj, sub * L + 2, 64);
+    gather_sum<L, 1, 8>(col, X, e0, e1, ldx, f0, fv, sub * L, sl, acc);
+  } else {
+    uint4 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = __shfl(myj, sub * L + u, 64);
+      r[u] = (fv && j >= 0) ? load_raw16(X, (size_t)j * ldx + f0) : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) acc_bf16_pair(acc, r[u], r[u + 1]);
+  }
+  if (!rv || f0 >= ldy) return;
+  const float rs = rscale ? rscale[row] : 1.f;
+  float y[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) y[q] = f0 + q < F ? acc[q] * rs : 0.f;
+  *reinterpret_cast<uint4*>(Y + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
+}
+
+// ell image of a CSR for spmm_ell_kernel (one thread per row)
+__global__ void ell_build_kernel(const int* __restrict__ rowptr, const int* __restrict__ col, int* __restrict__ ell,
+                                 int n_rows) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rows) return;
+  const int e0 = rowptr[i], e1 = rowptr[i + 1];
+  int v[8];
+  if (e1 - e0 > 8) {
+    v[0] = -2; v[1] = e0; v[2] = e1;
+#pragma unroll
+    for (int u = 3; u < 8; ++u) v[u] = -1;
+  } else {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = e0 + u < e1 ? col[e0 + u] : -1;
+  }
+  int4* o = reinterpret_cast<int4*>(ell + (size_t)i * 8);
+  o[0] = make_int4(v[0], v[1], v[2], v[3]);
+  o[1] = make_int4(v[4], v[5], v[6], v[7]);
+}
+
 // Layer-2 aggregate + bias + log-softmax + NLL.  L = 8 lanes per row, C <= 64.
 //   mask[i]: 0 = unused, 1 = train, 2 = valid, 3 = test
 //   stats[block][4 + 64] = {sum train loss, #correct train, #correct valid, #correct test,
@@ -873,6 +934,21 @@ extern "C" int gnn_launch_spmm_ce(const int* rowptr, const int* col, const void*
   hipLaunchKernelGGL(spmm_ce_kernel, dim3(gnn_spmm_ce_blocks(n_rows, n_long)), dim3(256), 0, st, rowptr, col,
                      Z, rscale, bias, labels, mask, stats, G, n_rows, C, ld, mode, inv_count, init, ldi, gslot,
                      n_long);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_launch_ell_build(const int* rowptr, const int* col, int* ell, int n_rows, hipStream_t st) {
+  if (n_rows <= 0) return 0;
+  hipLaunchKernelGGL(ell_build_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, st, rowptr, col, ell, n_rows);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gnn_launch_spmm_ell(const int* ell, const int* col, const void* X, void* Y, const float* rscale,
+                                   int n_rows, int F, int ldx, int ldy, hipStream_t st) {
+  if (F > 64 || ldx % 8 || ldy % 8 || F > ldx) return -3;
+  if (n_rows <= 0) return 0;
+  hipLaunchKernelGGL(spmm_ell_kernel, dim3((n_rows + 31) / 32), dim3(256), 0, st, ell, col, (const uint16_t*)X,
+                     (uint16_t*)Y, rscale, n_rows, F, ldx, ldy);
   return (int)hipGetLastError();
 }
 

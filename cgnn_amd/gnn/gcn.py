@@ -224,6 +224,12 @@ class GCNTrainer:
             self.part = torch.zeros(self.nloc, self.ldc, dtype=torch.float32, device=dev)
         # compact dL/dlogits (train rows only) and the adjacency restricted to train columns
         self.gslot, self.rp_T, self.col_T, self.maxT = self._train_columns(g, per)
+        # the train-column adjacency's rows are short (~4 entries): on the GPU the backward
+        # aggregation reads them from an ELL image (ops.spmm_ell: two dependent round trips
+        # per row instead of three).  Env CGNN_SPMM_ELL=0: the CSR kernel
+        self._ell_T = None
+        if dev.type == "cuda" and os.environ.get("CGNN_SPMM_ELL", "1") != "0":
+            self._ell_T = ops.ell_image(self.rp_T, self.col_T)
         self.Gc_loc = torch.zeros(self.maxT, self.ldc, **bf)
         self.Gc = torch.zeros(self.maxT * self.world, self.ldc, **bf) if self.multi else self.Gc_loc
         self._bwd_overlap = self.multi and os.environ.get("CGNN_BWD_OVERLAP", "1") != "0"
@@ -543,7 +549,10 @@ class GCNTrainer:
         else:
             if self.multi:
                 torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc)
-            ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
+            if self._ell_T is not None:
+                ops.spmm_ell(self._ell_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
+            else:
+                ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
         self.gb2.copy_(stats[4:4 + C])
         if self.fused_bwd:
             if self._grad_index is None:

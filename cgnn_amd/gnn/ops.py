@@ -88,6 +88,55 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
 _DB_INDEX = {}
 
 
+def ell_image(rowptr, col):
+    """ELL image of a CSR for ``spmm_ell``: int32 [n, 8], the row's column ids (-1 past
+    its end), or {-2, e0, e1, -1...} for a row of more than 8 entries (its CSR range)."""
+    n = rowptr.numel() - 1
+    ell = torch.empty(n, 8, dtype=torch.int32, device=col.device)
+    if col.is_cuda:
+        native.hip().gnn_ell_build(rowptr.data_ptr(), col.data_ptr(), ell.data_ptr(), n, _st(col))
+        return ell
+    rp = rowptr.long()
+    deg = rp[1:] - rp[:-1]
+    ell.fill_(-1)
+    for u in range(8):
+        has = deg > u
+        ell[has, u] = col[(rp[:-1] + u)[has]]
+    longr = deg > 8
+    ell[longr] = -1
+    ell[longr, 0] = -2
+    ell[longr, 1] = rp[:-1][longr].to(torch.int32)
+    ell[longr, 2] = rp[1:][longr].to(torch.int32)
+    return ell
+
+
+def spmm_ell(ell, col, X, F, rscale=None, out=None):
+    """Y[i,:F] = rscale[i] * sum_{j in N(i)} X[j,:F] from an ``ell_image`` (bf16, F <= 64;
+    the same sums as ``spmm`` over the CSR the image was built from)."""
+    n = ell.shape[0]
+    if out is None:
+        out = torch.empty(n, X.shape[1], dtype=torch.bfloat16, device=X.device)
+    if X.is_cuda:
+        native.hip().gnn_spmm_ell(ell.data_ptr(), col.data_ptr(), X.data_ptr(), out.data_ptr(),
+                                  rscale.data_ptr() if rscale is not None else 0, n, F, X.shape[1],
+                                  out.shape[1], _st(X))
+        return out
+    acc = torch.zeros(n, F, dtype=torch.float32)
+    for u in range(8):
+        j = ell[:, u].long()
+        ok = j >= 0
+        acc[ok] += X[j[ok], :F].float()
+    longr = (ell[:, 0] == -2).nonzero().flatten()
+    for i in longr.tolist():
+        e0, e1 = int(ell[i, 1]), int(ell[i, 2])
+        acc[i] = X[col[e0:e1].long(), :F].float().sum(0)
+    if rscale is not None:
+        acc = acc * rscale[:, None]
+    out[:n].zero_()
+    out[:n, :F] = acc.to(out.dtype)
+    return out
+
+
 def long_row_order(deg: torch.Tensor, threshold: Optional[int] = None):
     """Row order for ``spmm_ce(..., n_long=k)``: the rows of degree > threshold first (in
     their original order), then the others; returns (order, k).  Default threshold: env

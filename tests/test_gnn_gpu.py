@@ -629,3 +629,25 @@ def test_gcn_train_row_layer2_gpu_matches_all_rows(monkeypatch):
     d = (runs[1][1] - runs[0][1]).abs()
     assert d.max().item() < 1e-3 and (d > 1e-4).float().mean().item() < 0.01, (d.max(), (d > 1e-4).float().mean())
     assert runs[1][2]["val_acc"] == pytest.approx(runs[0][2]["val_acc"], abs=2e-3)
+
+
+def test_spmm_ell_matches_csr_spmm():
+    """The ELL short-row aggregation (rows up to 8 entries from the image, longer rows
+    through their CSR range) equals the CSR SpMM, bf16 in / out."""
+    torch.manual_seed(4)
+    n_src, n, C, ld = 3000, 2500, 47, 48
+    deg = torch.randint(0, 9, (n,))
+    deg[torch.randperm(n)[:40]] = torch.randint(9, 140, (40,))
+    rp = torch.zeros(n + 1, dtype=torch.int32)
+    rp[1:] = torch.cumsum(deg, 0).to(torch.int32)
+    col = torch.randint(0, n_src, (int(rp[-1]),), dtype=torch.int32)
+    X = torch.zeros(n_src, ld, dtype=torch.bfloat16)
+    X[:, :C] = torch.randn(n_src, C).to(torch.bfloat16)
+    rs = torch.rand(n) + 0.5
+    rpc, colc, Xc, rsc = rp.cuda(), col.cuda(), X.cuda(), rs.cuda()
+    ell = ops.ell_image(rpc, colc)
+    assert torch.equal(ell.cpu(), ops.ell_image(rp, col))
+    got = ops.spmm_ell(ell, colc, Xc, C, rscale=rsc)
+    ref = ops.spmm(rpc, colc, Xc, C, rscale=rsc, out=torch.empty(n, ld, dtype=torch.bfloat16, device="cuda"))
+    np.testing.assert_allclose(got.cpu().float().numpy(), ref.cpu().float().numpy(), rtol=1e-2, atol=1e-2)
+    assert torch.all(got[:, C:] == 0)

@@ -245,3 +245,22 @@ def test_dropout_keep_mask_bit_and_byte_modes():
     b = 16 * (t % 8) + 4 * g + i
     bit = (int(np.asarray(w[b // 32])) >> (b % 32)) & 1
     assert bool(dropout_keep_mask(18, 512, 0.5, (9, 11), 5)[17, n]) == bool(bit)
+
+
+def test_spmm_ell_reference_matches_spmm():
+    from cgnn_amd.gnn import ops
+    torch.manual_seed(4)
+    n, C, ld = 300, 47, 48
+    deg = torch.randint(0, 9, (n,))
+    deg[:5] = torch.tensor([12, 30, 9, 64, 100])
+    rp = torch.zeros(n + 1, dtype=torch.int32)
+    rp[1:] = torch.cumsum(deg, 0).to(torch.int32)
+    col = torch.randint(0, n, (int(rp[-1]),), dtype=torch.int32)
+    X = torch.zeros(n, ld, dtype=torch.bfloat16)
+    X[:, :C] = torch.randn(n, C).to(torch.bfloat16)
+    rs = torch.rand(n) + 0.5
+    ell = ops.ell_image(rp, col)
+    assert int((ell[:, 0] == -2).sum()) == 5
+    got = ops.spmm_ell(ell, col, X, C, rscale=rs)
+    ref = ops.spmm(rp, col, X, C, rscale=rs, out=torch.empty(n, ld, dtype=torch.bfloat16))
+    assert torch.allclose(got.float(), ref.float(), rtol=1e-2, atol=1e-2)
