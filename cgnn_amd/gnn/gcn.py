@@ -224,15 +224,15 @@ class GCNTrainer:
             self.part = torch.zeros(self.nloc, self.ldc, dtype=torch.float32, device=dev)
         # compact dL/dlogits (train rows only) and the adjacency restricted to train columns
         self.gslot, self.rp_T, self.col_T, self.maxT = self._train_columns(g, per)
-        # the train-column adjacency's rows are short (~4 entries): on the GPU the backward
-        # aggregation reads them from an ELL image (ops.spmm_ell: two dependent round trips
-        # per row instead of three).  Env CGNN_SPMM_ELL=0: the CSR kernel
-        self._ell_T = None
-        if dev.type == "cuda" and os.environ.get("CGNN_SPMM_ELL", "1") != "0":
-            self._ell_T = ops.ell_image(self.rp_T, self.col_T)
         self.Gc_loc = torch.zeros(self.maxT, self.ldc, **bf)
         self.Gc = torch.zeros(self.maxT * self.world, self.ldc, **bf) if self.multi else self.Gc_loc
         self._bwd_overlap = self.multi and os.environ.get("CGNN_BWD_OVERLAP", "1") != "0"
+        # the train-column adjacency's rows are short (~4 entries): on the GPU the unsplit
+        # backward aggregation reads them from an ELL image (ops.spmm_ell: two dependent
+        # round trips per row instead of three).  Env CGNN_SPMM_ELL=0: the CSR kernel
+        self._ell_T = None
+        if dev.type == "cuda" and not self._bwd_overlap and os.environ.get("CGNN_SPMM_ELL", "1") != "0":
+            self._ell_T = ops.ell_image(self.rp_T, self.col_T)
         if self._bwd_overlap:
             # backward aggregation split like the forward's: the edges to this rank's own
             # train rows (slots [rank * maxT, + maxT), read straight from Gc_loc) run while
