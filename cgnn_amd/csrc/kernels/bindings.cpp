@@ -109,7 +109,7 @@ int gnn_launch_lin_bwd_data(const void*, int, const void*, int, float, int, cons
 long gnn_lin_fwd_image_bytes(int, int, int);
 int gnn_lin_fwd_kc_wanted(int, int, int);
 long gnn_lin_bwd_image_bytes(int, int);
-int gnn_lin_wgrad_chunks(int, int);
+int gnn_lin_wgrad_chunks(int, int, int);
 int gnn_launch_lin_bwd_weight(const void*, int, int, const void*, int, int, const void*, int, const void*, int,
                               float, int, float*, float*, float*, int, const int*, hipStream_t);
 }
@@ -439,7 +439,7 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("dy"), py::arg("lddy"), py::arg("ym"), py::arg("ldym"), py::arg("mscale"), py::arg("N"), py::arg("w"),
      py::arg("K1"), py::arg("K2"), py::arg("dx1"), py::arg("ldx1"), py::arg("dx2"), py::arg("ldx2"),
      py::arg("rscale"), py::arg("n"), py::arg("st"), py::arg("dx1_f32") = 0, py::arg("wimg") = 0);
-  m.def("gnn_lin_wgrad_chunks", &gnn_lin_wgrad_chunks);
+  m.def("gnn_lin_wgrad_chunks", &gnn_lin_wgrad_chunks, py::arg("n"), py::arg("N"), py::arg("K") = 0);
   m.def("gnn_lin_bwd_weight", [](uint64_t x1, int ld1, int K1, uint64_t x2, int ld2, int K2, uint64_t dy, int lddy,
                                  uint64_t ym, int ldym, float mscale, int N, uint64_t gpart, uint64_t dw, uint64_t db,
                                  int n, uint64_t st, uint64_t idx1) {

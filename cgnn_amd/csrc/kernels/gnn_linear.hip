@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 using namespace cgnn;
 
@@ -55,6 +56,17 @@ constexpr int WGT_WAVES = 8;        // weight-gradient blocks
 constexpr int TR = TILE + 8;        // transposed image row: 32 rows + pad (80 B)
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+// ds_read_b64_tr_b16 pair -> one 32x32x16 operand fragment (lane 4q+p of a 16-lane group
+// addresses row q, columns 4p..4p+3 of a 4x16 block; lane i receives column i).
+__device__ __forceinline__ bf16x8 tr_frag(const uint8_t* base, int off0, int off1) {
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + off0));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + off1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
 
 __device__ __forceinline__ uint16_t bf16_bits(float x) { return __builtin_bit_cast(uint16_t, (__bf16)x); }
 
@@ -143,14 +155,8 @@ __device__ __forceinline__ uint4 load_cat8_sel(const uint16_t* __restrict__ x1, 
   return keep_first_sel(v, in1 ? K1 - f0 : in2 ? K2 - g : 0);
 }
 
-// 8 gradient values [c0, c0 + 8) of row `row`, times the mask [Ym > 0] * mscale
-__device__ __forceinline__ uint4 load_masked8(const uint16_t* __restrict__ dY, int lddy,
-                                              const uint16_t* __restrict__ Ym, int ldym, float mscale,
-                                              int N, int row, int c0) {
-  if (c0 >= N) return make_uint4(0u, 0u, 0u, 0u);
-  uint4 g = keep_first(*reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + c0), N - c0);
-  if (!Ym && mscale == 1.f) return g;
-  const uint4 y = Ym ? *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + c0) : make_uint4(~0u, ~0u, ~0u, ~0u);
+// g * [y > 0] * mscale per bf16 element (has_y false: g * mscale)
+__device__ __forceinline__ uint4 mask8(uint4 g, uint4 y, bool has_y, float mscale) {
   uint32_t gw[4] = {g.x, g.y, g.z, g.w};
   const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
@@ -159,14 +165,41 @@ __device__ __forceinline__ uint4 load_masked8(const uint16_t* __restrict__ dY, i
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const uint32_t yb = (yw[w] >> (16 * half)) & 0xffffu;
-      // kept and active: y > 0 (positive, non-zero); the all-ones pattern = no mask
-      const bool keep = !Ym || ((yb & 0x7fffu) != 0 && !(yb & 0x8000u));
+      // kept and active: y > 0 (positive, non-zero)
+      const bool keep = !has_y || ((yb & 0x7fffu) != 0 && !(yb & 0x8000u));
       const float v = keep ? bf16_val((gw[w] >> (16 * half)) & 0xffffu) * mscale : 0.f;
       o |= (uint32_t)bf16_bits(v) << (16 * half);
     }
     gw[w] = o;
   }
   return make_uint4(gw[0], gw[1], gw[2], gw[3]);
+}
+
+// 8 gradient values [c0, c0 + 8) of row `row`, times the mask [Ym > 0] * mscale
+__device__ __forceinline__ uint4 load_masked8(const uint16_t* __restrict__ dY, int lddy,
+                                              const uint16_t* __restrict__ Ym, int ldym, float mscale,
+                                              int N, int row, int c0) {
+  if (c0 >= N) return make_uint4(0u, 0u, 0u, 0u);
+  uint4 g = keep_first(*reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + c0), N - c0);
+  if (!Ym && mscale == 1.f) return g;
+  const uint4 y = Ym ? *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + c0) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  return mask8(g, y, Ym != nullptr, mscale);
+}
+
+// raw 16-byte chunk f0 of [X1 | X2] row `row`, zero outside both operands.  The padding
+// columns past K1 / K2 are NOT zeroed (for products that discard those rows), so no
+// instruction consumes the loaded value and the load stays in flight until it is staged.
+__device__ __forceinline__ uint4 load_cat8_raw(const uint16_t* __restrict__ x1, int ld1, int K1,
+                                               const uint16_t* __restrict__ x2, int ld2, int K2, int row, int f0,
+                                               const int* __restrict__ idx1) {
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (f0 < K1) {
+    const size_t r1 = idx1 ? (size_t)idx1[row] : (size_t)row;
+    v = *reinterpret_cast<const uint4*>(x1 + r1 * ld1 + f0);
+  } else if (x2 && f0 - K1 < K2) {
+    v = *reinterpret_cast<const uint4*>(x2 + (size_t)row * ld2 + (f0 - K1));
+  }
+  return v;
 }
 
 // block-wide copy of a weight image global -> LDS with 8 loads in flight per thread: a
@@ -722,6 +755,203 @@ __global__ __launch_bounds__(WGT_WAVES * 64) void lin_bwd_weight_kernel(
   }
 }
 
+// ============================================================================
+// lin_bwd_weight2: the same gpart slab as lin_bwd_weight, re-laid for bandwidth.
+//  * one block covers NB column tiles of 32 (all 256 hidden columns when K <= 256), so
+//    X is read from HBM once per chunk instead of once per 64-column slab;
+//  * both tiles are staged ROW-major with b128 writes, lanes running along a row (the
+//    global loads coalesce along rows too), and both MFMA operands of the row
+//    contraction come out of ds_read_b64_tr_b16 -- no 2-byte transposing writes;
+//  * double-buffered images, one barrier per 32-row tile, the loads of tile t + 2 in
+//    flight under tile t's MFMAs.
+// Row pitch of a [32][64 * tiles B] image: a 32-lane half reads 4 consecutive rows x
+// 64 B, conflict-free when the pitch is = 64 or 192 (mod 256) bytes.
+// Wave map: KW = min(KT, 8) waves per column group, WPK = 8 / KW column groups; wave w
+// holds k-tiles (w % KW) + KW a and column tiles (w / KW) + WPK j.
+// ============================================================================
+constexpr int wgt2_pitch(int tiles) { return 64 * tiles + ((tiles & 1) ? 0 : 64); }
+
+template <int KT, int NB>
+struct Wgt2 {
+  static constexpr int KW = KT < 8 ? KT : 8;
+  static constexpr int WPK = 8 / KW;
+  static constexpr int KPW = (KT + KW - 1) / KW;
+  static constexpr int CPW = (NB + WPK - 1) / WPK;
+  static constexpr int PX = wgt2_pitch(KT), PY = wgt2_pitch(NB);
+  static constexpr int XCH = KT * 4, YCH = NB * 4;           // 16-B chunks per staged row
+  static constexpr int BUF = TILE * (PX + PY);
+  static constexpr int LDS = 2 * BUF;
+  static_assert(KPW * CPW <= 8, "accumulators per wave");
+};
+
+template <int KT, int NB>
+__global__ __launch_bounds__(512, 1) void lin_bwd_weight2_kernel(
+    const uint16_t* __restrict__ x1, int ld1, int K1, const uint16_t* __restrict__ x2, int ld2, int K2,
+    const uint16_t* __restrict__ dY, int lddy, const uint16_t* __restrict__ Ym, int ldym, float mscale, int N,
+    float* __restrict__ gpart, int n, int rows_per_chunk, const int* __restrict__ idx1) {
+  using C = Wgt2<KT, NB>;
+  constexpr int NT = 512;
+  constexpr int PFX = (TILE * C::XCH + NT - 1) / NT;
+  constexpr int PFY = (TILE * C::YCH + NT - 1) / NT;
+  extern __shared__ __attribute__((aligned(16))) uint8_t wlds[];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, lr = lane & 31, wv = tid >> 6;
+  const int K = K1 + K2, xch = (K + 7) / 8;
+  const int c0 = blockIdx.y * NB * 32;
+  const int r_begin = blockIdx.x * rows_per_chunk, r_end = min(n, r_begin + rows_per_chunk);
+  const int ntile = r_begin < r_end ? (r_end - r_begin + TILE - 1) / TILE : 0;
+  const bool active = wv < C::KW * C::WPK;
+  const int kw = wv % C::KW, cg = wv / C::KW;
+
+  f32x16 acc[C::KPW][C::CPW];
+#pragma unroll
+  for (int a = 0; a < C::KPW; ++a)
+#pragma unroll
+    for (int j = 0; j < C::CPW; ++j) acc[a][j] = f32x16{};
+  float dsum[PFY][8];
+#pragma unroll
+  for (int q = 0; q < PFY; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dsum[q][e] = 0.f;
+
+  // raw loads only (the mask and scale are applied when staging): nothing waits on a
+  // prefetched value until the next tile's stage.  Padding columns past K or N are
+  // left as loaded -- they only reach output rows / columns that are not written.
+  const bool masked = Ym != nullptr || mscale != 1.f;
+  // two register sets: tile j is loaded into set j & 1 and staged into LDS buffer j & 1,
+  // two tiles ahead of the MFMAs, so two tiles' loads are in flight at every stage
+  uint4 px[2][PFX], py[2][PFY], pm[2][PFY];
+  auto prefetch = [&](auto S, int r0) {
+    constexpr int st = decltype(S)::value;
+#pragma unroll
+    for (int q = 0; q < PFX; ++q) {
+      const int i = tid + q * NT;
+      const int rr = i / C::XCH, ch = i % C::XCH;
+      px[st][q] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < TILE * C::XCH && ch < xch && r0 + rr < r_end)
+        px[st][q] = load_cat8_raw(x1, ld1, K1, x2, ld2, K2, r0 + rr, 8 * ch, idx1);
+    }
+#pragma unroll
+    for (int q = 0; q < PFY; ++q) {
+      const int i = tid + q * NT;
+      const int rr = i / C::YCH, c = c0 + 8 * (i % C::YCH);
+      py[st][q] = make_uint4(0u, 0u, 0u, 0u);
+      pm[st][q] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < TILE * C::YCH && r0 + rr < r_end && c < N) {
+        py[st][q] = *reinterpret_cast<const uint4*>(dY + (size_t)(r0 + rr) * lddy + c);
+        if (Ym) pm[st][q] = *reinterpret_cast<const uint4*>(Ym + (size_t)(r0 + rr) * ldym + c);
+      }
+    }
+  };
+  auto stage = [&](auto S) {
+    constexpr int st = decltype(S)::value;
+    uint8_t* bx = wlds + st * C::BUF;
+    uint8_t* by = bx + TILE * C::PX;
+#pragma unroll
+    for (int q = 0; q < PFX; ++q) {
+      const int i = tid + q * NT;
+      if (i < TILE * C::XCH) *reinterpret_cast<uint4*>(bx + (i / C::XCH) * C::PX + 16 * (i % C::XCH)) = px[st][q];
+    }
+#pragma unroll
+    for (int q = 0; q < PFY; ++q) {
+      const int i = tid + q * NT;
+      if (i < TILE * C::YCH) {
+        const uint4 v = masked ? mask8(py[st][q], pm[st][q], Ym != nullptr, mscale) : py[st][q];
+        *reinterpret_cast<uint4*>(by + (i / C::YCH) * C::PY + 16 * (i % C::YCH)) = v;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dsum[q][e] += bf16_val((w[e >> 1] >> (16 * (e & 1))) & 0xffffu);
+      }
+    }
+  };
+  const int qq = (lane & 15) >> 2, pq = lane & 3, gb = (lane >> 4) & 1;
+  auto compute = [&](int buf) {
+    if (!active) return;
+    const uint8_t* bx = wlds + buf * C::BUF;
+    const uint8_t* by = bx + TILE * C::PX;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int ra = 16 * s2 + 8 * h + qq;                 // k slot j <-> tile row 16 s2 + 8 h + j
+      const int colb = 2 * (16 * gb + 4 * pq);
+      bf16x8 bf[C::CPW];
+#pragma unroll
+      for (int j = 0; j < C::CPW; ++j) {
+        const int ct = cg + C::WPK * j;
+        if (ct < NB) bf[j] = tr_frag(by, ra * C::PY + 64 * ct + colb, (ra + 4) * C::PY + 64 * ct + colb);
+      }
+#pragma unroll
+      for (int a = 0; a < C::KPW; ++a) {
+        const int kt = kw + C::KW * a;
+        if (kt >= KT) continue;
+        const bf16x8 ax = tr_frag(bx, ra * C::PX + 64 * kt + colb, (ra + 4) * C::PX + 64 * kt + colb);
+#pragma unroll
+        for (int j = 0; j < C::CPW; ++j)
+          if (cg + C::WPK * j < NB) acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ax, bf[j], acc[a][j], 0, 0, 0);
+      }
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+
+  if (ntile > 0) prefetch(I0{}, r_begin);
+  if (ntile > 1) prefetch(I1{}, r_begin + TILE);
+  if (ntile > 0) stage(I0{});
+  if (ntile > 2) prefetch(I0{}, r_begin + 2 * TILE);
+  __syncthreads();
+  for (int t = 0; t < ntile; t += 2) {
+    // tile t in buffer 0; tile t + 1 (set 1) staged into buffer 1, tile t + 3 loaded into set 1
+    if (t + 1 < ntile) {
+      stage(I1{});
+      if (t + 3 < ntile) prefetch(I1{}, r_begin + (t + 3) * TILE);
+    }
+    compute(0);
+    __syncthreads();
+    if (t + 1 >= ntile) break;
+    // tile t + 1 in buffer 1; tile t + 2 (set 0) staged into buffer 0, tile t + 4 into set 0
+    if (t + 2 < ntile) {
+      stage(I0{});
+      if (t + 4 < ntile) prefetch(I0{}, r_begin + (t + 4) * TILE);
+    }
+    compute(1);
+    __syncthreads();
+  }
+
+  float* gp = gpart + (size_t)blockIdx.x * (K + 1) * N;
+  if (active) {
+#pragma unroll
+    for (int a = 0; a < C::KPW; ++a) {
+      const int kt = kw + C::KW * a;
+      if (kt >= KT) continue;
+#pragma unroll
+      for (int j = 0; j < C::CPW; ++j) {
+        const int c = c0 + 32 * (cg + C::WPK * j) + lr;
+        if (cg + C::WPK * j >= NB || c >= N) continue;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int k = 32 * kt + (q & 3) + 8 * (q >> 2) + 4 * h;
+          if (k < K) gp[(size_t)k * N + c] = acc[a][j][q];
+        }
+      }
+    }
+  }
+  // bias-gradient row K: per-(row slot, column) partials, summed over the slots in order
+  float* sdb = reinterpret_cast<float*>(wlds);               // [NB * 32][33], images consumed
+#pragma unroll
+  for (int q = 0; q < PFY; ++q) {
+    const int i = tid + q * NT;
+    if (i < TILE * C::YCH) {
+      const int rr = i / C::YCH, ch = i % C::YCH;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sdb[(8 * ch + e) * 33 + rr] = dsum[q][e];
+    }
+  }
+  __syncthreads();
+  if (tid < NB * 32 && c0 + tid < N) {
+    float s = 0.f;
+    for (int r = 0; r < TILE; ++r) s += sdb[tid * 33 + r];
+    gp[(size_t)K * N + c0 + tid] = s;
+  }
+}
+
 // out[i] = sum_{c < chunks} gpart[c][i] (fixed order), i < count; the first k_rows * N
 // go to dW, the last N (the ones row) to db when db != nullptr.  32 consecutive
 // outputs per block, the chunks split over 8 lane groups (8 independent load streams
@@ -774,7 +1004,9 @@ __global__ __launch_bounds__(256) void lin_prep_bwd_kernel(const float* __restri
 // ---------------------------------------------------------------- launchers
 static int grid_rows(int n, int waves) {
   const int tiles = (n + TILE - 1) / TILE;
-  return std::max(1, std::min(device_cus(), (tiles + waves - 1) / waves));
+  static const int per = [] { const char* e = std::getenv("CGNN_LIN_TILES_PER_BLOCK"); return e ? atoi(e) : 0; }();
+  const int w = per > 0 ? per : waves;
+  return std::max(1, std::min(device_cus(), (tiles + w - 1) / w));
 }
 
 static int pick_ks(int K) {
@@ -951,8 +1183,30 @@ extern "C" long gnn_lin_bwd_image_bytes(int K, int N) {
 }
 
 // chunk count of the split-K weight gradient for n rows and N columns (fills the chip)
-extern "C" int gnn_lin_wgrad_chunks(int n, int N) {
+// lin_bwd_weight2's column tiles per block: the widest of {2, 4, 8} the columns need whose
+// accumulators fit a wave (KPW * CPW <= 8, see Wgt2)
+static int wgt2_nb(int kt, int N) {
+  const int kw = std::min(kt, 8), wpk = 8 / kw, kpw = (kt + kw - 1) / kw;
+  int nb = N <= 64 ? 2 : N <= 128 ? 4 : 8;
+  while (nb > 2 && kpw * ((nb + wpk - 1) / wpk) > 8) nb >>= 1;
+  return nb;
+}
+
+static bool wgt_v1() {
+  static const bool v1 = [] { const char* e = std::getenv("CGNN_WGT_V1"); return e && e[0] == '1'; }();
+  return v1;
+}
+
+// Row chunks of the split-K weight gradient (the gpart scratch's leading dimension).
+// lin_bwd_weight2 (K > 0): one 8-wave block per CU over all chunks x column slabs;
+// the v1 kernel: two 8-wave blocks per CU over its 64-column slabs.
+extern "C" int gnn_lin_wgrad_chunks(int n, int N, int K) {
   const int tiles = std::max(1, (n + TILE - 1) / TILE);
+  if (K > 0 && !wgt_v1()) {
+    const int slabs = (N + 32 * wgt2_nb((K + 31) / 32, N) - 1) / (32 * wgt2_nb((K + 31) / 32, N));
+    static const int div = [] { const char* e = std::getenv("CGNN_WGT2_CHUNK_DIV"); return e ? std::max(1, atoi(e)) : 1; }();
+    return std::min(tiles, std::max(1, device_cus() / (std::max(slabs, 1) * div)));
+  }
   const int slabs = std::max(1, (N + 63) / 64);
   const int want = std::max(1, 2 * device_cus() / slabs);
   return std::min(tiles, want);
@@ -969,7 +1223,25 @@ static int wgt_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
   return (int)hipGetLastError();
 }
 
-// gpart: [chunks][K1 + K2 + 1][N] fp32 scratch (chunks = gnn_lin_wgrad_chunks(n, N));
+template <int KT, int NB>
+static int wgt2_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const uint16_t* dY,
+                       int lddy, const uint16_t* Ym, int ldym, float mscale, int N, float* gpart, int n, int chunks,
+                       const int* idx1, hipStream_t st) {
+  const int tiles = (n + TILE - 1) / TILE;
+  const int rpc = (tiles + chunks - 1) / chunks * TILE;
+  constexpr int lds = Wgt2<KT, NB>::LDS;
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)lin_bwd_weight2_kernel<KT, NB>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((lin_bwd_weight2_kernel<KT, NB>), dim3(chunks, (N + 32 * NB - 1) / (32 * NB)), dim3(512), lds,
+                     st, x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, rpc, idx1);
+  return (int)hipGetLastError();
+}
+
+// gpart: [chunks][K1 + K2 + 1][N] fp32 scratch (chunks = gnn_lin_wgrad_chunks(n, N, K1 + K2));
 // dW: [K1 + K2][N] fp32, db: [N] fp32 (optional)
 extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2,
                                          const void* dY, int lddy, const void* Ym, int ldym, float mscale, int N,
@@ -977,7 +1249,7 @@ extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const 
   if ((x2 && K1 % 8) || ld1 % 8 || (x2 && ld2 % 8) || lddy % 8 || (Ym && ldym % 8) || N > lddy) return -3;
   if (!x2) K2 = 0;
   const int K = K1 + K2;
-  const int chunks = gnn_lin_wgrad_chunks(std::max(n, 1), N);
+  const int chunks = gnn_lin_wgrad_chunks(std::max(n, 1), N, K);
   if (n > 0) {
     const int kt = (K + 31) / 32;
     auto a = (const uint16_t*)x1;
@@ -985,9 +1257,17 @@ extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const 
     auto d = (const uint16_t*)dY;
     auto m = (const uint16_t*)Ym;
     int rc = -1;
+    if (!wgt_v1()) {
+      const int nb = wgt2_nb(kt, N);
+#define LW2(c, b_) if (rc == -1 && kt <= c && nb == b_) rc = wgt2_launch<c, b_>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, idx1, st);
+      LW2(2, 2) LW2(2, 4) LW2(2, 8) LW2(4, 2) LW2(4, 4) LW2(4, 8) LW2(5, 2) LW2(5, 4) LW2(5, 8)
+      LW2(8, 2) LW2(8, 4) LW2(8, 8) LW2(9, 2) LW2(9, 4) LW2(12, 2) LW2(12, 4) LW2(16, 2) LW2(16, 4) LW2(17, 2)
+#undef LW2
+    } else {
 #define LW(c) if (rc == -1 && kt <= c) rc = wgt_launch<c>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, idx1, st);
-    LW(2) LW(4) LW(5) LW(8) LW(9) LW(12) LW(16) LW(17)
+      LW(2) LW(4) LW(5) LW(8) LW(9) LW(12) LW(16) LW(17)
 #undef LW
+    }
     if (rc != 0) return rc;
   } else {
     (void)hipMemsetAsync(gpart, 0, sizeof(float) * (size_t)(K + 1) * N * chunks, st);

@@ -1,0 +1,16 @@
+#!/bin/bash
+# lin_bwd_weight2 vs v1: numerics (gpu tests), kernel A/B, SAGE / GAT / arxiv benches, profile
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r03_wgt
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gnn_linear_gpu.py > $O/tests.log 2>&1 &&
+timeout -k 10 200 python -u tools/bench_wgrad.py > $O/wgrad_new.json 2> $O/wgrad_new.err &&
+CGNN_WGT_V1=1 timeout -k 10 200 python -u tools/bench_wgrad.py > $O/wgrad_v1.json 2> $O/wgrad_v1.err &&
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o wg -- python tools/bench_wgrad.py --reps 5 > $O/prof.log 2>&1 &&
+timeout -k 10 300 python -u tools/bench_gnn_configs.py --config products-sage3 > $O/sage_new.log 2>&1 &&
+CGNN_WGT_V1=1 timeout -k 10 300 python -u tools/bench_gnn_configs.py --config products-sage3 > $O/sage_v1.log 2>&1 &&
+timeout -k 10 300 python -u tools/bench_gnn_configs.py --config arxiv-gcn3 > $O/arxiv_new.log 2>&1 &&
+CGNN_WGT_V1=1 timeout -k 10 300 python -u tools/bench_gnn_configs.py --config arxiv-gcn3 > $O/arxiv_v1.log 2>&1 &&
+timeout -k 10 300 python -u tools/bench_gat.py --steps 10 --warmup 2 > $O/gat_new.log 2>&1 &&
+CGNN_WGT_V1=1 timeout -k 10 300 python -u tools/bench_gat.py --steps 10 --warmup 2 > $O/gat_v1.log 2>&1

@@ -109,6 +109,11 @@ def test_lin_bwd_data_matches_reference(n, N, K1, K2, mask, ms, rs):
     (5000, 100, 0, 47, False),        # odd widths
     (4100, 256, 256, 256, True),      # SAGE [h_dst | agg]
     (17, 64, 0, 64, True),            # a single partial tile
+    (3001, 104, 104, 256, True),      # SAGE layer 1 [h_dst | agg], K = 208 (7 k-tiles, one slab)
+    (2000, 544, 0, 47, False),        # 17 k-tiles, 2 column tiles
+    (999, 64, 0, 256, True),          # 2 k-tiles: 4 column groups of waves
+    (1500, 96, 0, 128, False),        # 3 k-tiles in a 4-k-tile block
+    (700, 320, 0, 200, True),         # 10 k-tiles, two 128-column slabs, ragged last slab
 ])
 def test_lin_bwd_weight_matches_reference(n, K1, K2, N, mask):
     g = torch.Generator().manual_seed(n)
