@@ -784,11 +784,11 @@ struct Wgt2 {
   static_assert(KPW * CPW <= 8, "accumulators per wave");
 };
 
-template <int KT, int NB>
+template <int KT, int NB, bool HAS_YM>
 __global__ __launch_bounds__(512, 1) void lin_bwd_weight2_kernel(
     const uint16_t* __restrict__ x1, int ld1, int K1, const uint16_t* __restrict__ x2, int ld2, int K2,
     const uint16_t* __restrict__ dY, int lddy, const uint16_t* __restrict__ Ym, int ldym, float mscale, int N,
-    float* __restrict__ gpart, int n, int rows_per_chunk, const int* __restrict__ idx1) {
+    float* __restrict__ gpart, int n, int rows_per_chunk) {
   using C = Wgt2<KT, NB>;
   constexpr int NT = 512;
   constexpr int PFX = (TILE * C::XCH + NT - 1) / NT;
@@ -813,49 +813,61 @@ __global__ __launch_bounds__(512, 1) void lin_bwd_weight2_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) dsum[q][e] = 0.f;
 
-  // raw loads only (the mask and scale are applied when staging): nothing waits on a
-  // prefetched value until the next tile's stage.  Padding columns past K or N are
-  // left as loaded -- they only reach output rows / columns that are not written.
-  const bool masked = Ym != nullptr || mscale != 1.f;
-  // two register sets: tile j is loaded into set j & 1 and staged into LDS buffer j & 1,
-  // two tiles ahead of the MFMAs, so two tiles' loads are in flight at every stage
-  uint4 px[2][PFX], py[2][PFY], pm[2][PFY];
+  // Loads are UNCONDITIONAL (addresses clamped to the chunk's last row / the slab's first
+  // column / the row's first chunk) and nothing computes on a loaded value until the
+  // tile is staged, where the validity select, the mask and the scale are applied: a
+  // conditional load merged with a zero (or a mask on the loaded value) would make the
+  // compiler wait for the load right there (vmcnt(0)), draining the other set too.
+  // Two register sets: tile j is loaded into set j & 1 and staged into LDS buffer j & 1,
+  // two tiles ahead of the MFMAs.
+  const bool scaled = HAS_YM || mscale != 1.f;
+  uint4 px[2][PFX], py[2][PFY], pm[2][HAS_YM ? PFY : 1];
   auto prefetch = [&](auto S, int r0) {
     constexpr int st = decltype(S)::value;
 #pragma unroll
     for (int q = 0; q < PFX; ++q) {
-      const int i = tid + q * NT;
-      const int rr = i / C::XCH, ch = i % C::XCH;
-      px[st][q] = make_uint4(0u, 0u, 0u, 0u);
-      if (i < TILE * C::XCH && ch < xch && r0 + rr < r_end)
-        px[st][q] = load_cat8_raw(x1, ld1, K1, x2, ld2, K2, r0 + rr, 8 * ch, idx1);
+      const int i = min(tid + q * NT, TILE * C::XCH - 1);
+      const int row = min(r0 + i / C::XCH, r_end - 1), f0 = 8 * (i % C::XCH);
+      const uint16_t* p = f0 < K1 ? x1 + (size_t)row * ld1 + f0
+                        : (x2 && f0 - K1 < K2) ? x2 + (size_t)row * ld2 + (f0 - K1) : x1 + (size_t)row * ld1;
+      px[st][q] = *reinterpret_cast<const uint4*>(p);
     }
 #pragma unroll
     for (int q = 0; q < PFY; ++q) {
-      const int i = tid + q * NT;
-      const int rr = i / C::YCH, c = c0 + 8 * (i % C::YCH);
-      py[st][q] = make_uint4(0u, 0u, 0u, 0u);
-      pm[st][q] = make_uint4(0u, 0u, 0u, 0u);
-      if (i < TILE * C::YCH && r0 + rr < r_end && c < N) {
-        py[st][q] = *reinterpret_cast<const uint4*>(dY + (size_t)(r0 + rr) * lddy + c);
-        if (Ym) pm[st][q] = *reinterpret_cast<const uint4*>(Ym + (size_t)(r0 + rr) * ldym + c);
-      }
+      const int i = min(tid + q * NT, TILE * C::YCH - 1);
+      const int row = min(r0 + i / C::YCH, r_end - 1);
+      const int c = c0 + 8 * (i % C::YCH), cc = c < N ? c : c0;
+      py[st][q] = *reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + cc);
+      if constexpr (HAS_YM) pm[st][q] = *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + cc);
     }
   };
-  auto stage = [&](auto S) {
+  auto stage = [&](auto S, int r0) {
     constexpr int st = decltype(S)::value;
     uint8_t* bx = wlds + st * C::BUF;
     uint8_t* by = bx + TILE * C::PX;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
     for (int q = 0; q < PFX; ++q) {
       const int i = tid + q * NT;
-      if (i < TILE * C::XCH) *reinterpret_cast<uint4*>(bx + (i / C::XCH) * C::PX + 16 * (i % C::XCH)) = px[st][q];
+      if (i < TILE * C::XCH) {
+        const bool ok = r0 + i / C::XCH < r_end && i % C::XCH < xch;
+        uint4 v = px[st][q];
+        if (!ok) v = z;
+        *reinterpret_cast<uint4*>(bx + (i / C::XCH) * C::PX + 16 * (i % C::XCH)) = v;
+      }
     }
 #pragma unroll
     for (int q = 0; q < PFY; ++q) {
       const int i = tid + q * NT;
       if (i < TILE * C::YCH) {
-        const uint4 v = masked ? mask8(py[st][q], pm[st][q], Ym != nullptr, mscale) : py[st][q];
+        const bool ok = r0 + i / C::YCH < r_end && c0 + 8 * (i % C::YCH) < N;
+        uint4 v = py[st][q];
+        if constexpr (HAS_YM) {
+          v = mask8(v, pm[st][q], true, mscale);
+        } else {
+          if (scaled) v = mask8(v, z, false, mscale);
+        }
+        if (!ok) v = z;
         *reinterpret_cast<uint4*>(by + (i / C::YCH) * C::PY + 16 * (i % C::YCH)) = v;
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -894,13 +906,13 @@ __global__ __launch_bounds__(512, 1) void lin_bwd_weight2_kernel(
 
   if (ntile > 0) prefetch(I0{}, r_begin);
   if (ntile > 1) prefetch(I1{}, r_begin + TILE);
-  if (ntile > 0) stage(I0{});
+  if (ntile > 0) stage(I0{}, r_begin);
   if (ntile > 2) prefetch(I0{}, r_begin + 2 * TILE);
   __syncthreads();
   for (int t = 0; t < ntile; t += 2) {
     // tile t in buffer 0; tile t + 1 (set 1) staged into buffer 1, tile t + 3 loaded into set 1
     if (t + 1 < ntile) {
-      stage(I1{});
+      stage(I1{}, r_begin + (t + 1) * TILE);
       if (t + 3 < ntile) prefetch(I1{}, r_begin + (t + 3) * TILE);
     }
     compute(0);
@@ -908,7 +920,7 @@ __global__ __launch_bounds__(512, 1) void lin_bwd_weight2_kernel(
     if (t + 1 >= ntile) break;
     // tile t + 1 in buffer 1; tile t + 2 (set 0) staged into buffer 0, tile t + 4 into set 0
     if (t + 2 < ntile) {
-      stage(I0{});
+      stage(I0{}, r_begin + (t + 2) * TILE);
       if (t + 4 < ntile) prefetch(I0{}, r_begin + (t + 4) * TILE);
     }
     compute(1);
@@ -1205,7 +1217,11 @@ extern "C" int gnn_lin_wgrad_chunks(int n, int N, int K) {
   if (K > 0 && !wgt_v1()) {
     const int slabs = (N + 32 * wgt2_nb((K + 31) / 32, N) - 1) / (32 * wgt2_nb((K + 31) / 32, N));
     static const int div = [] { const char* e = std::getenv("CGNN_WGT2_CHUNK_DIV"); return e ? std::max(1, atoi(e)) : 1; }();
-    return std::min(tiles, std::max(1, device_cus() / (std::max(slabs, 1) * div)));
+    // at least min_tiles row tiles per chunk: each chunk writes a whole K x N fp32 slab,
+    // which at a few tiles per chunk outweighs the rows it reads
+    static const int min_tiles = [] { const char* e = std::getenv("CGNN_WGT2_MIN_TILES"); return e ? std::max(1, atoi(e)) : 1; }();
+    const int cap = (tiles + min_tiles - 1) / min_tiles;
+    return std::min(cap, std::max(1, device_cus() / (std::max(slabs, 1) * div)));
   }
   const int slabs = std::max(1, (N + 63) / 64);
   const int want = std::max(1, 2 * device_cus() / slabs);
@@ -1223,25 +1239,33 @@ static int wgt_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
   return (int)hipGetLastError();
 }
 
-template <int KT, int NB>
-static int wgt2_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const uint16_t* dY,
-                       int lddy, const uint16_t* Ym, int ldym, float mscale, int N, float* gpart, int n, int chunks,
-                       const int* idx1, hipStream_t st) {
+template <int KT, int NB, bool HAS_YM>
+static int wgt2_launch_t(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const uint16_t* dY,
+                         int lddy, const uint16_t* Ym, int ldym, float mscale, int N, float* gpart, int n, int chunks,
+                         hipStream_t st) {
   const int tiles = (n + TILE - 1) / TILE;
   const int rpc = (tiles + chunks - 1) / chunks * TILE;
   constexpr int lds = Wgt2<KT, NB>::LDS;
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)lin_bwd_weight2_kernel<KT, NB>,
+    (void)hipFuncSetAttribute((const void*)lin_bwd_weight2_kernel<KT, NB, HAS_YM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     return true;
   }();
   (void)attr;
-  hipLaunchKernelGGL((lin_bwd_weight2_kernel<KT, NB>), dim3(chunks, (N + 32 * NB - 1) / (32 * NB)), dim3(512), lds,
-                     st, x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, rpc, idx1);
+  hipLaunchKernelGGL((lin_bwd_weight2_kernel<KT, NB, HAS_YM>), dim3(chunks, (N + 32 * NB - 1) / (32 * NB)), dim3(512),
+                     lds, st, x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, rpc);
   return (int)hipGetLastError();
 }
 
-// gpart: [chunks][K1 + K2 + 1][N] fp32 scratch (chunks = gnn_lin_wgrad_chunks(n, N, K1 + K2));
+template <int KT, int NB>
+static int wgt2_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const uint16_t* dY,
+                       int lddy, const uint16_t* Ym, int ldym, float mscale, int N, float* gpart, int n, int chunks,
+                       hipStream_t st) {
+  return Ym ? wgt2_launch_t<KT, NB, true>(x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, chunks, st)
+            : wgt2_launch_t<KT, NB, false>(x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, chunks, st);
+}
+
+// gpart: [chunks][K1 + K2 + 1][N] fp32 scratch (chunks = gnn_lin_wgrad_chunks(n, N, idx1 ? 0 : K1 + K2));
 // dW: [K1 + K2][N] fp32, db: [N] fp32 (optional)
 extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2,
                                          const void* dY, int lddy, const void* Ym, int ldym, float mscale, int N,
@@ -1249,7 +1273,7 @@ extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const 
   if ((x2 && K1 % 8) || ld1 % 8 || (x2 && ld2 % 8) || lddy % 8 || (Ym && ldym % 8) || N > lddy) return -3;
   if (!x2) K2 = 0;
   const int K = K1 + K2;
-  const int chunks = gnn_lin_wgrad_chunks(std::max(n, 1), N, K);
+  const int chunks = gnn_lin_wgrad_chunks(std::max(n, 1), N, idx1 ? 0 : K);   // K = 0: the v1 kernel's chunking
   if (n > 0) {
     const int kt = (K + 31) / 32;
     auto a = (const uint16_t*)x1;
@@ -1257,10 +1281,10 @@ extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const 
     auto d = (const uint16_t*)dY;
     auto m = (const uint16_t*)Ym;
     int rc = -1;
-    if (!wgt_v1()) {
+    if (!wgt_v1() && !idx1) {
       const int nb = wgt2_nb(kt, N);
-#define LW2(c, b_) if (rc == -1 && kt <= c && nb == b_) rc = wgt2_launch<c, b_>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, idx1, st);
-      LW2(2, 2) LW2(2, 4) LW2(2, 8) LW2(4, 2) LW2(4, 4) LW2(4, 8) LW2(5, 2) LW2(5, 4) LW2(5, 8)
+#define LW2(c, b_) if (rc == -1 && kt <= c && nb == b_) rc = wgt2_launch<c, b_>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, st);
+      LW2(2, 2) LW2(2, 4) LW2(2, 8) LW2(4, 2) LW2(4, 4) LW2(4, 8) LW2(5, 2) LW2(5, 4)
       LW2(8, 2) LW2(8, 4) LW2(8, 8) LW2(9, 2) LW2(9, 4) LW2(12, 2) LW2(12, 4) LW2(16, 2) LW2(16, 4) LW2(17, 2)
 #undef LW2
     } else {
