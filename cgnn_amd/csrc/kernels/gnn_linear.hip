@@ -788,7 +788,7 @@ template <int KT, int NB, bool HAS_YM>
 __global__ __launch_bounds__(512, 1) void lin_bwd_weight2_kernel(
     const uint16_t* __restrict__ x1, int ld1, int K1, const uint16_t* __restrict__ x2, int ld2, int K2,
     const uint16_t* __restrict__ dY, int lddy, const uint16_t* __restrict__ Ym, int ldym, float mscale, int N,
-    float* __restrict__ gpart, int n, int rows_per_chunk) {
+    float* __restrict__ gpart, int n, int rows_per_chunk, const int* __restrict__ idx1) {
   using C = Wgt2<KT, NB>;
   constexpr int NT = 512;
   constexpr int PFX = (TILE * C::XCH + NT - 1) / NT;
@@ -801,6 +801,13 @@ __global__ __launch_bounds__(512, 1) void lin_bwd_weight2_kernel(
   const int ntile = r_begin < r_end ? (r_end - r_begin + TILE - 1) / TILE : 0;
   const bool active = wv < C::KW * C::WPK;
   const int kw = wv % C::KW, cg = wv / C::KW;
+  // gathered X1 rows (idx1): the chunk's row ids are staged in LDS once, so a prefetch
+  // reads its row id from LDS instead of a dependent global load inside the ring
+  int* sidx = reinterpret_cast<int*>(wlds + C::LDS);
+  if (idx1) {
+    for (int r = r_begin + tid; r < r_end; r += NT) sidx[r - r_begin] = idx1[r];
+    __syncthreads();
+  }
 
   f32x16 acc[C::KPW][C::CPW];
 #pragma unroll
@@ -828,8 +835,9 @@ __global__ __launch_bounds__(512, 1) void lin_bwd_weight2_kernel(
     for (int q = 0; q < PFX; ++q) {
       const int i = min(tid + q * NT, TILE * C::XCH - 1);
       const int row = min(r0 + i / C::XCH, r_end - 1), f0 = 8 * (i % C::XCH);
-      const uint16_t* p = f0 < K1 ? x1 + (size_t)row * ld1 + f0
-                        : (x2 && f0 - K1 < K2) ? x2 + (size_t)row * ld2 + (f0 - K1) : x1 + (size_t)row * ld1;
+      const size_t r1 = idx1 ? (size_t)sidx[row - r_begin] : (size_t)row;
+      const uint16_t* p = f0 < K1 ? x1 + r1 * ld1 + f0
+                        : (x2 && f0 - K1 < K2) ? x2 + (size_t)row * ld2 + (f0 - K1) : x1 + r1 * ld1;
       px[st][q] = *reinterpret_cast<const uint4*>(p);
     }
 #pragma unroll
@@ -1239,33 +1247,40 @@ static int wgt_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
   return (int)hipGetLastError();
 }
 
+constexpr int WGT2_LDS_MAX = 160 * 1024;
+
+// -1: the staged row ids of a gathered X1 would not fit next to the images (the caller
+// falls back to v1 with the same chunking)
 template <int KT, int NB, bool HAS_YM>
 static int wgt2_launch_t(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const uint16_t* dY,
                          int lddy, const uint16_t* Ym, int ldym, float mscale, int N, float* gpart, int n, int chunks,
-                         hipStream_t st) {
+                         const int* idx1, hipStream_t st) {
   const int tiles = (n + TILE - 1) / TILE;
   const int rpc = (tiles + chunks - 1) / chunks * TILE;
-  constexpr int lds = Wgt2<KT, NB>::LDS;
+  const long lds = Wgt2<KT, NB>::LDS + (idx1 ? 4L * rpc : 0L);
+  if (lds > WGT2_LDS_MAX) return -1;
   static const bool attr = [] {
     (void)hipFuncSetAttribute((const void*)lin_bwd_weight2_kernel<KT, NB, HAS_YM>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, WGT2_LDS_MAX);
     return true;
   }();
   (void)attr;
   hipLaunchKernelGGL((lin_bwd_weight2_kernel<KT, NB, HAS_YM>), dim3(chunks, (N + 32 * NB - 1) / (32 * NB)), dim3(512),
-                     lds, st, x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, rpc);
+                     (size_t)lds, st, x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, rpc, idx1);
   return (int)hipGetLastError();
 }
 
 template <int KT, int NB>
 static int wgt2_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, int ld2, int K2, const uint16_t* dY,
                        int lddy, const uint16_t* Ym, int ldym, float mscale, int N, float* gpart, int n, int chunks,
-                       hipStream_t st) {
-  return Ym ? wgt2_launch_t<KT, NB, true>(x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, chunks, st)
-            : wgt2_launch_t<KT, NB, false>(x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, chunks, st);
+                       const int* idx1, hipStream_t st) {
+  return Ym ? wgt2_launch_t<KT, NB, true>(x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, chunks,
+                                          idx1, st)
+            : wgt2_launch_t<KT, NB, false>(x1, ld1, K1, x2, ld2, K2, dY, lddy, Ym, ldym, mscale, N, gpart, n, chunks,
+                                           idx1, st);
 }
 
-// gpart: [chunks][K1 + K2 + 1][N] fp32 scratch (chunks = gnn_lin_wgrad_chunks(n, N, idx1 ? 0 : K1 + K2));
+// gpart: [chunks][K1 + K2 + 1][N] fp32 scratch (chunks = gnn_lin_wgrad_chunks(n, N, K1 + K2));
 // dW: [K1 + K2][N] fp32, db: [N] fp32 (optional)
 extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const void* x2, int ld2, int K2,
                                          const void* dY, int lddy, const void* Ym, int ldym, float mscale, int N,
@@ -1273,7 +1288,7 @@ extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const 
   if ((x2 && K1 % 8) || ld1 % 8 || (x2 && ld2 % 8) || lddy % 8 || (Ym && ldym % 8) || N > lddy) return -3;
   if (!x2) K2 = 0;
   const int K = K1 + K2;
-  const int chunks = gnn_lin_wgrad_chunks(std::max(n, 1), N, idx1 ? 0 : K);   // K = 0: the v1 kernel's chunking
+  const int chunks = gnn_lin_wgrad_chunks(std::max(n, 1), N, K);
   if (n > 0) {
     const int kt = (K + 31) / 32;
     auto a = (const uint16_t*)x1;
@@ -1281,13 +1296,16 @@ extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const 
     auto d = (const uint16_t*)dY;
     auto m = (const uint16_t*)Ym;
     int rc = -1;
-    if (!wgt_v1() && !idx1) {
+    if (!wgt_v1()) {
       const int nb = wgt2_nb(kt, N);
-#define LW2(c, b_) if (rc == -1 && kt <= c && nb == b_) rc = wgt2_launch<c, b_>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, st);
+#define LW2(c, b_) if (rc == -1 && kt <= c && nb == b_) rc = wgt2_launch<c, b_>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, idx1, st);
       LW2(2, 2) LW2(2, 4) LW2(2, 8) LW2(4, 2) LW2(4, 4) LW2(4, 8) LW2(5, 2) LW2(5, 4)
       LW2(8, 2) LW2(8, 4) LW2(8, 8) LW2(9, 2) LW2(9, 4) LW2(12, 2) LW2(12, 4) LW2(16, 2) LW2(16, 4) LW2(17, 2)
 #undef LW2
-    } else {
+      if (rc == -1) rc = -2;                 // no v2 form: v1 below
+    }
+    if (rc == -2 || wgt_v1()) {
+      rc = -1;
 #define LW(c) if (rc == -1 && kt <= c) rc = wgt_launch<c>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, idx1, st);
       LW(2) LW(4) LW(5) LW(8) LW(9) LW(12) LW(16) LW(17)
 #undef LW

@@ -185,7 +185,7 @@ def lin_bwd_weight(x1: torch.Tensor, dY: torch.Tensor, N: int, x2: Optional[torc
         checks.rows(dY, n, "lin_bwd_weight dY")
     if x1.is_cuda:
         hip = native.hip()
-        chunks = hip.gnn_lin_wgrad_chunks(max(n, 1), N, 0 if idx1 is not None else K1 + K2)
+        chunks = hip.gnn_lin_wgrad_chunks(max(n, 1), N, K1 + K2)
         shape = (chunks, K1 + K2 + 1, N)
         key = (dev.index, shape)
         gp = _GPART.get(key)
