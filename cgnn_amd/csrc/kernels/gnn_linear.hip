@@ -53,6 +53,12 @@ constexpr int TILE = 32;
 // take 4 * KS registers
 template <int KS> struct FwdWaves { static constexpr int value = KS <= 16 ? 16 : 8; };
 constexpr int WGT_WAVES = 8;        // weight-gradient blocks
+#ifndef CGNN_BWD_DATA_SEL
+#define CGNN_BWD_DATA_SEL 1         // lin_bwd_data: branch-free gradient loader (A/B build switch)
+#endif
+#ifndef CGNN_FWD_SEL_KS
+#define CGNN_FWD_SEL_KS 8           // lin_fwd: branch-free X loader from this many k-steps up (A/B build switch)
+#endif
 constexpr int TR = TILE + 8;        // transposed image row: 32 rows + pad (80 B)
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
@@ -141,8 +147,10 @@ __device__ __forceinline__ uint4 load_cat8(const uint16_t* __restrict__ x1, int 
 // address (a chunk outside both operands re-reads its row's first chunk) and the value
 // is masked afterwards.  The per-lane branches of load_cat8, unrolled KS times, cost
 // exec-mask saves that spilled the SGPR file (KS = 40: 1259 SGPR spills); this form has
-// none up to KS = 40 and measured 365 vs 410 us on Reddit's K = 602 layer; at KS = 8
-// (2 % slower) and in the weight-gradient prefetch (43 % slower) load_cat8 stays.
+// none up to KS = 40 and measured 365 vs 410 us on Reddit's K = 602 layer.  Since round 3
+// it serves KS >= 8 too: the branchy form left lin_fwd<16> at 491 SGPR + 11 VGPR spills
+// (64.1 -> 57.8 us at SAGE layer-0 shapes, products-sage3 7.96 -> 8.17 epochs/s,
+// profiles/r03_linsel); KS = 4 keeps load_cat8.
 __device__ __forceinline__ uint4 load_cat8_sel(const uint16_t* __restrict__ x1, int ld1, int K1,
                                                const uint16_t* __restrict__ x2, int ld2, int K2, int row, int f0,
                                                const int* __restrict__ idx1) {
@@ -183,6 +191,19 @@ __device__ __forceinline__ uint4 load_masked8(const uint16_t* __restrict__ dY, i
   uint4 g = keep_first(*reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + c0), N - c0);
   if (!Ym && mscale == 1.f) return g;
   const uint4 y = Ym ? *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + c0) : make_uint4(~0u, ~0u, ~0u, ~0u);
+  return mask8(g, y, Ym != nullptr, mscale);
+}
+
+// Branch-free load_masked8 (selects only, every lane loads from a valid address: the
+// caller clamps `row`; `rv` false zeroes the chunk): unrolled over a k loop, the per-lane
+// branches of load_masked8 cost exec-mask saves that spill the SGPR file.
+__device__ __forceinline__ uint4 load_masked8_sel(const uint16_t* __restrict__ dY, int lddy,
+                                                  const uint16_t* __restrict__ Ym, int ldym, float mscale,
+                                                  int N, int row, int c0, bool rv) {
+  const int cc = c0 < N ? c0 : 0;
+  const uint4 g = keep_first_sel(*reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + cc), rv ? N - c0 : 0);
+  if (!Ym && mscale == 1.f) return g;
+  const uint4 y = Ym ? *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + cc) : make_uint4(~0u, ~0u, ~0u, ~0u);
   return mask8(g, y, Ym != nullptr, mscale);
 }
 
@@ -281,7 +302,7 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     uint4 bx[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      if constexpr (KS > 16)     // wide K: the branch-free form (no exec-mask spills)
+      if constexpr (KS >= CGNN_FWD_SEL_KS)    // wide K: the branch-free form (no exec-mask spills)
         bx[s] = load_cat8_sel(x1, ld1, K1, x2, ld2, K2, rv ? row : n - 1, 16 * s + fh, idx1);
       else
         bx[s] = rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h, idx1) : make_uint4(0u, 0u, 0u, 0u);
@@ -591,9 +612,13 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
     const int row = tile * TILE + lr;
     const bool rv = row < n;
     bf16x8 by[KN];
+    // branch-free unless it would push the 16-wave KN = 16 variant past 128 VGPRs
+    constexpr bool sel = CGNN_BWD_DATA_SEL && !(KN == 16 && FWD_WAVES == 16);
 #pragma unroll
     for (int s = 0; s < KN; ++s)
-      by[s] = as_bf16x8(rv ? load_masked8(dY, lddy, Ym, ldym, mscale, N, row, 16 * s + 8 * h) : make_uint4(0u, 0u, 0u, 0u));
+      by[s] = as_bf16x8(sel ? load_masked8_sel(dY, lddy, Ym, ldym, mscale, N, rv ? row : n - 1, 16 * s + 8 * h, rv)
+                                          : (rv ? load_masked8(dY, lddy, Ym, ldym, mscale, N, row, 16 * s + 8 * h)
+                                                : make_uint4(0u, 0u, 0u, 0u)));
     const float rs = (rv && rscale) ? rscale[row] : 1.f;
 #pragma unroll 1
     for (int t = 0; t < nt; ++t) {
