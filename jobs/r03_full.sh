@@ -3,7 +3,7 @@
 # full-size papers100M rank-0-of-8 dry run with the communication-free layer 1.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r03_full2
+O=gpurun_out/r03_full3
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
     || { echo "gpu tests failed"; grep -E "FAILED|Error" $O/pytest_gpu.log | head; tail -n 30 $O/pytest_gpu.log; exit 1; }
@@ -14,4 +14,10 @@ timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 > $O/bench.log 2>&1 |
 tail -n 1 $O/bench.log
 timeout -k 10 900 python -u tools/bench_gnn_configs.py --config papers-gat2 --scale 1.0 --steps 3 --warmup 1 --emulate-world 8 > $O/gat_emulate_r0of8_full.log 2>&1 || { echo emulate failed; tail $O/gat_emulate_r0of8_full.log; exit 1; }
 tail -n 1 $O/gat_emulate_r0of8_full.log
+timeout -k 10 300 python -u tools/bench_gnn_configs.py --config arxiv-gcn3 > $O/arxiv.log 2>&1 || { echo arxiv failed; tail $O/arxiv.log; exit 1; }
+tail -n 1 $O/arxiv.log
+timeout -k 10 300 python -u tools/bench_gnn_configs.py --config products-sage3 > $O/sage.log 2>&1 || { echo sage failed; tail $O/sage.log; exit 1; }
+tail -n 1 $O/sage.log
+timeout -k 10 300 python -u tools/bench_gat.py --steps 10 --warmup 2 > $O/gat_products.log 2>&1 || { echo gat failed; tail $O/gat_products.log; exit 1; }
+tail -n 1 $O/gat_products.log
 echo done
