@@ -56,6 +56,12 @@ constexpr int WGT_WAVES = 8;        // weight-gradient blocks
 #ifndef CGNN_BWD_DATA_SEL
 #define CGNN_BWD_DATA_SEL 1         // lin_bwd_data: branch-free gradient loader (A/B build switch)
 #endif
+#ifndef CGNN_FWD16_WAVES
+#define CGNN_FWD16_WAVES 8          // lin_fwd KS = 16: waves per block (A/B build switch; profiles/r03_waves)
+#endif
+#ifndef CGNN_BWD16_WAVES
+#define CGNN_BWD16_WAVES 8          // lin_bwd_data KN = 16: waves per block (A/B build switch; profiles/r03_waves)
+#endif
 #ifndef CGNN_FWD_SEL_KS
 #define CGNN_FWD_SEL_KS 8           // lin_fwd: branch-free X loader from this many k-steps up (A/B build switch)
 #endif
@@ -1076,7 +1082,7 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
                       uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
                       const int* idx1, uint16_t* wimg, float* Yf, int nsplit, int tk, hipStream_t st) {
   constexpr int KP = KS * 16;
-  constexpr int WV = FwdWaves<KS>::value;
+  constexpr int WV = KS == 16 ? CGNN_FWD16_WAVES : FwdWaves<KS>::value;
   const int ncols = slab_cols(std::max(N, ldy), KP);
   const size_t lds = (size_t)ncols * (KP + 8) * 2 + (size_t)ncols * 4;
   {
@@ -1085,9 +1091,9 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
     hipLaunchKernelGGL(lin_prep_fwd_kernel<ET>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2,
                        N, ncols, KP, KP + 8, total, wimg);
   }
-  (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS, ET>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS, ET, WV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
-  hipLaunchKernelGGL((lin_fwd_kernel<KS, ET>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
+  hipLaunchKernelGGL((lin_fwd_kernel<KS, ET, WV>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
                      x1, ld1, K1, x2, ld2, K2, W, N, bias, Y, ldy, n, ncols, relu, p, k0, k1, step, thr8, row0,
                      stepp, rscale, idx1, wimg, Yf, nsplit, tk);
   return (int)hipGetLastError();
@@ -1183,11 +1189,11 @@ static int bwd_data_launch(const uint16_t* dY, int lddy, const uint16_t* Ym, int
     hipLaunchKernelGGL(lin_prep_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K, N, NP,
                        NP + 8, total, wimg);
   }
-  constexpr int WV = FwdWaves<KN>::value;
-  (void)hipFuncSetAttribute((const void*)lin_bwd_data_kernel<KN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  constexpr int WV = KN == 16 ? CGNN_BWD16_WAVES : FwdWaves<KN>::value;
+  (void)hipFuncSetAttribute((const void*)lin_bwd_data_kernel<KN, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const int slabs = (K + kcols - 1) / kcols;
-  hipLaunchKernelGGL((lin_bwd_data_kernel<KN>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
+  hipLaunchKernelGGL((lin_bwd_data_kernel<KN, WV>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
                      dY, lddy, Ym, ldym, mscale, N, W, K1, K2, dX1, ldx1, dX2, ldx2, rscale, n, kcols, dx1_f32, wimg);
   return (int)hipGetLastError();
 }
