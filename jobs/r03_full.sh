@@ -3,7 +3,7 @@
 # full-size papers100M rank-0-of-8 dry run with the communication-free layer 1.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r03_full3
+O=gpurun_out/r03_full4
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
     || { echo "gpu tests failed"; grep -E "FAILED|Error" $O/pytest_gpu.log | head; tail -n 30 $O/pytest_gpu.log; exit 1; }
@@ -20,4 +20,6 @@ timeout -k 10 300 python -u tools/bench_gnn_configs.py --config products-sage3 >
 tail -n 1 $O/sage.log
 timeout -k 10 300 python -u tools/bench_gat.py --steps 10 --warmup 2 > $O/gat_products.log 2>&1 || { echo gat failed; tail $O/gat_products.log; exit 1; }
 tail -n 1 $O/gat_products.log
+timeout -k 10 300 python -u tools/bench_gnn_configs.py --config reddit-infer > $O/reddit.log 2>&1 || { echo reddit failed; tail $O/reddit.log; exit 1; }
+tail -n 1 $O/reddit.log
 echo done
