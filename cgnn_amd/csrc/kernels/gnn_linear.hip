@@ -56,6 +56,9 @@ constexpr int WGT_WAVES = 8;        // weight-gradient blocks
 #ifndef CGNN_BWD_DATA_SEL
 #define CGNN_BWD_DATA_SEL 1         // lin_bwd_data: branch-free gradient loader (A/B build switch)
 #endif
+#ifndef CGNN_FWD8_WAVES
+#define CGNN_FWD8_WAVES 16          // lin_fwd KS = 8: waves per block (A/B build switch)
+#endif
 #ifndef CGNN_FWD16_WAVES
 #define CGNN_FWD16_WAVES 8          // lin_fwd KS = 16: waves per block (A/B build switch; profiles/r03_waves)
 #endif
@@ -1082,7 +1085,7 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
                       uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
                       const int* idx1, uint16_t* wimg, float* Yf, int nsplit, int tk, hipStream_t st) {
   constexpr int KP = KS * 16;
-  constexpr int WV = KS == 16 ? CGNN_FWD16_WAVES : FwdWaves<KS>::value;
+  constexpr int WV = KS == 16 ? CGNN_FWD16_WAVES : KS == 8 ? CGNN_FWD8_WAVES : FwdWaves<KS>::value;
   const int ncols = slab_cols(std::max(N, ldy), KP);
   const size_t lds = (size_t)ncols * (KP + 8) * 2 + (size_t)ncols * 4;
   {
