@@ -4,6 +4,10 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/r03_fwd8
 mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gnn_linear_gpu.py > $O/tests_new.log 2>&1 || { echo tests failed; tail -30 $O/tests_new.log; exit 1; }
+tail -n 1 $O/tests_new.log
+timeout -k 10 300 python -u tools/bench_gnn_configs.py --config products-sage3 > $O/sage_new.log 2>&1 || { echo sage failed; exit 1; }
+tail -n 1 $O/sage_new.log | cut -c100-180
 for v in new fwd8w new2 fwd8w2; do
   lib=""
   case $v in fwd8w*) lib=$PWD/abtmp/fwd8w/_hip.cpython-310-x86_64-linux-gnu.so;; esac
