@@ -31,6 +31,7 @@ int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, 
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t, int);
 int cgnn_gen_bwd_variant(int, int, int, int);
+size_t cgnn_gen_fwd_lds(int, int);
 size_t cgnn_gen_bwd_generic_lds(int, int);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
                         const float*, int, int, int, int, int, int, int, float*, hipStream_t, float*);
@@ -74,7 +75,9 @@ int gnn_launch_bias_relu_dropout(void*, const float*, long, int, int, float, uin
 int gnn_launch_relu_dropout_bwd(void*, const void*, long, float, hipStream_t);
 int gnn_launch_dense_fwd(const void*, const float*, const float*, const float*, const float*, void*, void*,
                          int, int, int, int, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t,
-                         const int*, hipStream_t);
+                         const int*, void*, hipStream_t);
+long gnn_keep_image_halfwords(int, int);
+int gnn_launch_keep_image(void*, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, const int*, hipStream_t);
 int gnn_launch_gat_fwd(const int*, const int*, const void*, const float*, const float*, const int*, float*, float*,
                        void*, int, int, int, int, const float*, void*, int, float, uint32_t, uint32_t, uint32_t,
                        const int*, uint32_t, hipStream_t);
@@ -96,9 +99,8 @@ int gnn_launch_sample_blocks(const int*, const int*, int, const int*, int, int, 
 int gnn_fused_bwd_blocks(int);
 int gnn_fused_bwd_width(int);
 int gnn_fused_bwd_supported(int, int, int);
-int gnn_launch_fused_bwd(const void*, const void*, const float*, const float*, const float*, float*, int, int,
-                         int, int, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, const int*,
-                         hipStream_t);
+int gnn_launch_fused_bwd(const void*, const void*, const float*, const float*, const float*, const void*, float*,
+                         int, int, int, int, int, int, float, hipStream_t);
 int gnn_launch_dense_bwd(const void*, const float*, const void*, void*, int, int, int, int, float,
                          hipStream_t);
 int gnn_launch_lin_fwd(const void*, int, int, const void*, int, int, const float*, int, const float*, void*, int,
@@ -159,6 +161,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gen_bwd_blocks", &cgnn_gen_bwd_blocks);
   m.def("gen_bwd_lds", &cgnn_gen_bwd_lds);
   m.def("gen_bwd_variant", &cgnn_gen_bwd_variant);
+  m.def("gen_fwd_lds", &cgnn_gen_fwd_lds);
   m.def("gen_bwd_generic_lds", &cgnn_gen_bwd_generic_lds);
   m.def("read_stamps", []() {
     unsigned long long v[16] = {0};
@@ -306,13 +309,20 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("gnn_dense_fwd", [](uint64_t ax, uint64_t w1, uint64_t b1, uint64_t w2, uint64_t dinv, uint64_t h1,
                             uint64_t z2, int n, int F, int ldx, int HD, int C, int ldc, float p, uint32_t k0,
-                            uint32_t k1, uint32_t step, uint32_t row0, uint64_t st, uint64_t stepp) {
+                            uint32_t k1, uint32_t step, uint32_t row0, uint64_t st, uint64_t stepp, uint64_t kimg) {
     return gnn_launch_dense_fwd(Pt<const void>(ax), Pt<const float>(w1), Pt<const float>(b1), Pt<const float>(w2),
                                 Pt<const float>(dinv), Pt<void>(h1), Pt<void>(z2), n, F, ldx, HD, C, ldc, p, k0,
-                                k1, step, row0, Pt<const int>(stepp), S(st));
+                                k1, step, row0, Pt<const int>(stepp), Pt<void>(kimg), S(st));
   }, py::arg("ax"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("dinv"), py::arg("h1"), py::arg("z2"),
      py::arg("n"), py::arg("F"), py::arg("ldx"), py::arg("HD"), py::arg("C"), py::arg("ldc"), py::arg("p"),
-     py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"), py::arg("step_ptr") = 0);
+     py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"), py::arg("step_ptr") = 0,
+     py::arg("kimg") = 0);
+  m.def("gnn_keep_image_halfwords", &gnn_keep_image_halfwords);
+  m.def("gnn_keep_image", [](uint64_t kimg, int n, int HD, float p, uint32_t k0, uint32_t k1, uint32_t step,
+                             uint32_t row0, uint64_t st, uint64_t stepp) {
+    return gnn_launch_keep_image(Pt<void>(kimg), n, HD, p, k0, k1, step, row0, Pt<const int>(stepp), S(st));
+  }, py::arg("kimg"), py::arg("n"), py::arg("HD"), py::arg("p"), py::arg("k0"), py::arg("k1"), py::arg("step"),
+     py::arg("row0"), py::arg("st"), py::arg("step_ptr") = 0);
   m.def("gnn_dense_bwd", [](uint64_t dy2, uint64_t w2, uint64_t h1, uint64_t dp1, int n, int HD, int C, int ldc,
                             float p, uint64_t st) {
     return gnn_launch_dense_bwd(Pt<const void>(dy2), Pt<const float>(w2), Pt<const void>(h1), Pt<void>(dp1), n,
@@ -404,15 +414,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gnn_fused_bwd_blocks", &gnn_fused_bwd_blocks);
   m.def("gnn_fused_bwd_width", &gnn_fused_bwd_width);
   m.def("gnn_fused_bwd_supported", &gnn_fused_bwd_supported);
-  m.def("gnn_fused_bwd", [](uint64_t ax, uint64_t dy2, uint64_t w1, uint64_t b1, uint64_t w2, uint64_t gpart, int n,
-                            int F, int ldx, int HD, int C, int ldc, float p, uint32_t k0, uint32_t k1,
-                            uint32_t step, uint32_t row0, uint64_t st, uint64_t stepp) {
+  m.def("gnn_fused_bwd", [](uint64_t ax, uint64_t dy2, uint64_t w1, uint64_t b1, uint64_t w2, uint64_t kimg,
+                            uint64_t gpart, int n, int F, int ldx, int HD, int C, int ldc, float p, uint64_t st) {
     return gnn_launch_fused_bwd(Pt<const void>(ax), Pt<const void>(dy2), Pt<const float>(w1), Pt<const float>(b1),
-                                Pt<const float>(w2), Pt<float>(gpart), n, F, ldx, HD, C, ldc, p, k0, k1, step,
-                                row0, Pt<const int>(stepp), S(st));
-  }, py::arg("ax"), py::arg("dy2"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("gpart"), py::arg("n"),
-     py::arg("F"), py::arg("ldx"), py::arg("HD"), py::arg("C"), py::arg("ldc"), py::arg("p"), py::arg("k0"),
-     py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"), py::arg("step_ptr") = 0);
+                                Pt<const float>(w2), Pt<const void>(kimg), Pt<float>(gpart), n, F, ldx, HD, C, ldc,
+                                p, S(st));
+  });
   // generic fused dense layers (gnn_linear.hip); return codes: 0 ok, -1 no variant, -3 bad shape
   m.def("gnn_lin_fwd", [](uint64_t x1, int ld1, int K1, uint64_t x2, int ld2, int K2, uint64_t w, int N, uint64_t b,
                           uint64_t y, int ldy, int n, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step,

@@ -892,13 +892,19 @@ static int gen_fwd_block(int D) {
   return B;
 }
 
+// LDS bytes of the generator forward of D (padded) variables with a program stride of
+// prog_stride ints: the [D][B] sample state plus the block's program copy
+extern "C" size_t cgnn_gen_fwd_lds(int D, int prog_stride) {
+  return sizeof(float) * (size_t)D * gen_fwd_block(D) + sizeof(int) * (size_t)prog_stride;
+}
+
 extern "C" int cgnn_launch_gen_fwd(const int* prog, int prog_stride, const float* params, int P,
                                    const float* data, float* xhat, float* noise, int NS, float* xnorm,
                                    const uint32_t* keys, const int* step_base, int step_off, int N,
                                    int D, int H, int R, hipStream_t st, int row0) {
   const int B = gen_fwd_block(D);
   dim3 grid((N + B - 1) / B, R), block(B);
-  const size_t lds = sizeof(float) * (size_t)D * B + sizeof(int) * (size_t)prog_stride;
+  const size_t lds = cgnn_gen_fwd_lds(D, prog_stride);
   if (lds > 160 * 1024) return -2;
   switch (H) {
 #define CASE_H(h) case h: allow_lds(gen_fwd_kernel<h>, lds); hipLaunchKernelGGL((gen_fwd_kernel<h>), grid, block, lds, st, prog, prog_stride, params, P, data, xhat, noise, NS, xnorm, keys, step_base, step_off, N, D, H, row0); break;

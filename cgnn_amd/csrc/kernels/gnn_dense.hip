@@ -24,6 +24,7 @@
 #include "cgnn_common.h"
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 using namespace cgnn;
 
@@ -74,11 +75,33 @@ __device__ __forceinline__ int stg_off(int row, int ch) {
   return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
-// Byte offset of 8-B unit `u` (0..7) of row `row` in a wave's [32 rows][32 hidden]
-// H1 / dP1 image (64-B rows): the packed accumulator writes are at the 4-way minimum,
-// the transposed reads conflict-free.
-__device__ __forceinline__ int img_off(int row, int u) {
-  return 64 * row + 8 * (u ^ ((row >> 1) & 7));
+// ---- packed bf16 epilogue helpers (two elements per dword, one instruction each) ----
+// two fp32 -> two bf16 in one dword (hipcc emits v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t cvt_pk(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+// relu of two bf16 as signed 16-bit integers: a negative bf16 (sign bit set, -0
+// included) is a negative int16, so max(x, 0) is exactly the bf16 relu
+__device__ __forceinline__ uint32_t pk_relu(uint32_t x) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(x));
+  return r;
+}
+// per 16-bit half: x * k (k in {0, 1}: a keep bit applied without a compare or select)
+__device__ __forceinline__ uint32_t pk_mul16(uint32_t x, uint32_t k) {
+  uint32_t r;
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(x), "v"(k));
+  return r;
+}
+// per 16-bit half: 1 if x != 0 else 0 (x a relu output, so != 0 means > 0).  The 1s
+// come from a register: an inline constant of a packed instruction reaches only the low
+// half (the high half of its 32-bit value, 0, feeds the high half).
+__device__ __forceinline__ uint32_t pk_nz(uint32_t x) {
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(x), "s"(0x00010001u));
+  return r;
 }
 
 // ds_read_b64_tr_b16 (gfx950): lane 4q+p of a 16-lane group gives the address of
@@ -104,18 +127,34 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint16_t* base, int off0, int of
 // (4 b128 LDS reads issued ahead, fp32 exact) instead of a bias add per element after
 // the chain, and the KS weight fragments of the chain are read from LDS as one batch
 // before the first MFMA rather than one LDS round trip per MFMA.
+//
+// Keep image (kimg, optional, training only): the dropout masks the fused backward
+// applies, so that it draws no Philox of its own (bit mode: one draw per row and half
+// here feeds both passes; the byte-mode launch draws the image with
+// gcn_keep_image_kernel, which keeps this kernel within its register budget).  For
+// 32-row tile T and hidden block t, 64 halfwords at kimg[(T * HD/32 + t) * 64]: halfword 32 uh + r = the 16 keep bits of tile row r for
+// the units 32 t + 8 g + 4 uh + i (bit 4 g + i) -- halfword index = the lane that drew
+// them, so each block's image is one contiguous 128-B store per wave.  Read as 32-bit
+// words, word 16 uh + P holds rows 2P (low half) and 2P + 1 (high half).
+//
+// The next tile's AX rows are loaded right after the last hidden block's layer-1 MFMAs
+// (the registers of the current rows are dead from there), so the loads fly during
+// that block's epilogue, its layer-2 products and the Z2 stores.
 template <int KS, int HD, int DROP>
 __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
     const uint16_t* __restrict__ AX, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ dinv, uint16_t* __restrict__ H1,
     uint16_t* __restrict__ Z2, int n, int F, int ldx, int C, int ldc, float p, uint32_t k0,
-    uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0, const int* __restrict__ stepp) {
+    uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0, const int* __restrict__ stepp,
+    uint16_t* __restrict__ kimg) {
   // stepp (optional): the dropout step read from device memory, so a captured hipGraph
   // replays with the current epoch's mask
   if (stepp) step = (uint32_t)*stepp;
   constexpr int KP = KS * 16;
   constexpr int W1S = KP + 8;          // padded row strides (bank-conflict-free b128 / b64 reads)
-  constexpr int W2S = HD + 8;
+  // W2^T rows of HD + 4 elements: a 130-dword pitch puts the 32 rows of a b64 read on
+  // 32 distinct bank pairs (HD + 8 -- 132 dwords -- made rows r and r + 16 collide)
+  constexpr int W2S = HD + 4;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* sW1T = lds;                          // [HD][W1S]   W1^T
   uint16_t* sW2T = sW1T + HD * W1S;              // [64][W2S]   W2^T (rows >= C zero)
@@ -141,28 +180,60 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
   const int n_waves = gridDim.x * WAVES;
   const int n_tiles = (n + TILE - 1) / TILE;
 
+  // A tile's rows.  Hoisted form: unconditional loads (a per-lane "load or zero" makes
+  // hipcc branch around every load); rows past n load row n - 1 (their results are not
+  // stored), and only the last k-step can pass the row pitch (F > 16 (KS - 1), ldx >= F,
+  // ldx % 8 == 0): its upper half then loads the row's last chunk, which meets zero W1^T
+  // rows (k >= F).
+  // The hoisted next-tile loads fit the 128-register budget of 4 waves / SIMD only in
+  // the bit-mode (p = 1/2) form up to 112 features: the other forms load each tile at
+  // its start (and keep the per-lane "load or zero" form, which needs fewer registers)
+  constexpr bool HOIST = DROP == 2 && KS <= 7;
+  bf16x8 bx[KS];
+  auto load_rows = [&](int tl) {
+    if constexpr (HOIST) {
+      const uint16_t* rp = AX + (size_t)min(tl * TILE + lr, n - 1) * ldx;
+#pragma unroll
+      for (int s = 0; s < KS - 1; ++s) bx[s] = load_bf16x8(rp + 16 * s + 8 * h);
+      bx[KS - 1] = load_bf16x8(rp + min(16 * (KS - 1) + 8 * h, ldx - 8));
+    } else {
+      const int rw = tl * TILE + lr;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int f0 = 16 * s + 8 * h;
+        bx[s] = (rw < n && f0 < ldx) ? load_bf16x8(AX + (size_t)rw * ldx + f0) : zero_bf16x8();
+      }
+    }
+  };
+  if (HOIST && wave < n_tiles) load_rows(wave);
   for (int tile = wave; tile < n_tiles; tile += n_waves) {
     const int row = tile * TILE + lr;
     const bool rv = row < n;
-    bf16x8 bx[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int f0 = 16 * s + 8 * h;
-      bx[s] = (rv && f0 < ldx) ? load_bf16x8(AX + (size_t)row * ldx + f0) : zero_bf16x8();
-    }
+    if constexpr (!HOIST) load_rows(tile);
     f32x16 z0 = {}, z1 = {};
     static_assert(HD <= 256, "bit-mode dropout: one draw covers 8 hidden blocks");
     u32x4 rb{};
     if constexpr (DROP == 2) rb = drop_draw(row0 + (uint32_t)row, 0, h, step, k0, k1, true);
-#pragma unroll 1
-    for (int t = 0; t < HD / 32; ++t) {
+    // one hidden block: layer-1 chain, epilogue, layer-2 products; the last block is
+    // peeled (LAST) so the next tile's row loads there do not keep a second set of row
+    // registers live across the whole block loop
+    auto hidden_block = [&](const int t, auto last_tag) {
+      constexpr bool LAST = decltype(last_tag)::value;
       const uint16_t* arow = sW1T + (32 * t + lr) * W1S + 8 * h;
-      bf16x8 af[KS];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) af[s] = load_bf16x8(arow + 16 * s);
+      // the chain's weight fragments in two LDS batches (registers: 4 waves / SIMD)
+      constexpr int KA = (KS + 1) / 2;
+      bf16x8 af[KA];
       f32x16 acc = {};
 #pragma unroll
-      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bx[s], acc, 0, 0, 0);
+      for (int s = 0; s < KA; ++s) af[s] = load_bf16x8(arow + 16 * s);
+#pragma unroll
+      for (int s = 0; s < KA; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bx[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int s = KA; s < KS; ++s) af[s - KA] = load_bf16x8(arow + 16 * s);
+#pragma unroll
+      for (int s = KA; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s - KA], bx[s], acc, 0, 0, 0);
+      if constexpr (LAST && HOIST)
+        if (tile + n_waves < n_tiles) load_rows(tile + n_waves);
       // epilogue (registers 4g..4g+3 are hidden 32t + 8g + 4h + 0..3): bias (packed adds),
       // relu, dropout as an AND with the sign-extended keep bit (the scale is in W2^T)
       float v[16];
@@ -205,6 +276,21 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
           const bf16x8 af2 = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
           z1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af2, xb, z1, 0, 0, 0);
         }
+      }
+    };
+    if constexpr (HOIST) {
+#pragma unroll 1
+      for (int t = 0; t < HD / 32 - 1; ++t) hidden_block(t, std::false_type{});
+      hidden_block(HD / 32 - 1, std::true_type{});
+    } else {
+#pragma unroll 1
+      for (int t = 0; t < HD / 32; ++t) hidden_block(t, std::false_type{});
+    }
+    if constexpr (DROP == 2) {               // the tile's keep image, straight from the draw
+      if (kimg) {
+        uint16_t* kd = kimg + (size_t)tile * (HD / 32) * 64 + lane;
+#pragma unroll
+        for (int t = 0; t < HD / 32; ++t) kd[64 * t] = (uint16_t)drop_keep16(rb, t, thr8, true);
       }
     }
     if (rv) {
@@ -279,296 +365,48 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_bwd_kernel(
 // ============================================================================
 // Fused backward of the dense stages, H1 never stored (recomputed) and the two
 // weight-gradient contractions over the rows done in the same pass:
-//   P1^T = W1^T AX^T, H1 = dropout(relu(P1 + b1))      (as the forward, same Philox)
-//   dP1^T = (W2 dY2^T) * [H1 > 0] / (1-p)
-//   gW1^T[h][f] += sum_rows dP1^T[h][row] AX[row][f]     (f = F is the ones column: gb1)
+//   P1 = AX W1 (+ b1),  H1 = dropout(relu(P1))          (the forward's masks: kimg)
+//   dP1 = (dY2 W2^T) * [H1 > 0]                         (1/(1-p) applied to the slab)
+//   gW1^T[h][f] += sum_rows dP1^T[h][row] AX[row][f]    (f = F, the ones column: gb1)
 //   gW2[h][c]   += sum_rows H1^T[h][row] dY2[row][c]
-// Block = HD/32 waves, wave w owns hidden block w (32 units) for all three
-// products, so its weight-gradient tiles (KF/32 + 2 of 32x32) stay in its
-// accumulators for the whole persistent loop; the block walks 32-row tiles.
-// Per tile: stage the AX / dY2 rows ONCE, row-major in swizzled 256-B rows: the
-// recompute reads them by rows (b128), the contractions over the rows by columns
-// with ds_read_b64_tr_b16 (no second, transposed copy).  The recomputed H1^T /
-// dP1^T accumulators (lane = row) are stored packed, 4 hidden units per 8-B write,
-// into the wave's own [row][hidden] images and read back transposed as the
-// contractions' A operands.  The next tile's rows are prefetched into registers
-// meanwhile.  Output: one fp32 slab per block, gpart[block][HD][KF + 64] =
-// [gW1^T | gW2], summed in fixed order afterwards.
-// (The round-1 form staged separate transposed images with 2-byte scattered writes
-// and wrote H1^T / dP1^T one element at a time: 0.74 ms on the ogbn-products shape.)
+// Block = HD/32 waves; wave w owns hidden block w (32 units) for all four products,
+// so its W1 / W2^T B fragments (KS + KC bf16x8) sit in registers for the whole launch
+// and its weight-gradient tiles (KF/32 + 2 of 32x32) in its accumulators.  The
+// recompute chains produce ROWS x HIDDEN tiles (lane = hidden unit, registers = 16
+// rows of the tile) that are ALREADY the A operands of the contractions over the rows
+// (dP1^T, H1^T: hidden x rows; the k order inside a 16-row step is permuted -- rows
+// 4h..4h+3, 8+4h..8+4h+3 -- and the transposed B reads of AX / dY2 use the same
+// permutation).  Per 32-row tile the block stages the AX / dY2 rows once, row-major
+// in swizzled 256-B rows (the recompute reads them by rows with b128, the contractions
+// by columns with ds_read_b64_tr_b16), and the tile's keep image from the forward;
+// double-buffered behind a register prefetch of the tile after next: one block
+// barrier per tile.
+// Epilogue on packed bf16 pairs (two rows per dword): relu as a signed 16-bit max, the
+// keep bits and the relu derivative as 16-bit multiplies by 0 / 1 -- no compares,
+// selects or per-element bit extracts, and no Philox: the forward drew the masks (a
+// draw costs ~60 VALU instructions, a third of them quarter-rate 32-bit multiplies,
+// and every wave of the round-3 form re-drew its tile's).
+// Output: one fp32 slab per block, gpart[block][HD][KF + 64] = [gW1^T | gW2], summed in
+// fixed order afterwards.
 // ============================================================================
-// LDS bytes of the fused backward: weights, nbuf x two [32][128] staging images, two
-// [HD/32][32][32] H1 / dP1 images, b1
-constexpr size_t fused_bwd_lds(int KP, int CP, int HD, int nbuf) {
-  return sizeof(uint16_t) * ((size_t)HD * (KP + 8) + (size_t)HD * (CP + 8) + (size_t)nbuf * 2 * 32 * 128 +
-                             2 * (size_t)HD * 32) +
-         sizeof(float) * HD;
-}
+// LDS bytes: two staging buffers (AX | dY2, [32][128] bf16 each) + two keep images
+constexpr size_t fused_bwd_lds(int HD) { return sizeof(uint16_t) * 2 * 2 * 32 * 128 + 2 * (size_t)(HD / 32) * 128; }
 
 template <int KS, int KC, int HD, bool DROP>
-__global__ __launch_bounds__(HD * 2) void gcn_fused_bwd_kernel(
+__global__ __launch_bounds__(HD * 2, 1) void gcn_fused_bwd_kernel(
     const uint16_t* __restrict__ AX, const uint16_t* __restrict__ dY2, const float* __restrict__ W1,
-    const float* __restrict__ b1, const float* __restrict__ W2, float* __restrict__ gpart, int n, int F,
-    int ldx, int C, int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
-    uint32_t row0, const int* __restrict__ stepp) {
-  if (stepp) step = (uint32_t)*stepp;         // device-resident dropout step (graph replays)
+    const float* __restrict__ b1, const float* __restrict__ W2, const uint16_t* __restrict__ kimg,
+    float* __restrict__ gpart, int n, int F, int ldx, int C, int ldc, float p) {
   constexpr int NW = HD / 32;                 // waves per block = hidden blocks
   constexpr int NT = NW * 64;
   constexpr int KP = KS * 16;                 // layer-1 K (features + ones column), padded
   constexpr int KF = (KP + 31) / 32 * 32;     // gW1^T columns (f), padded to whole tiles
   constexpr int CP = KC * 16;                 // classes, padded
-  constexpr int W1S = KP + 8, W2S = CP + 8;
-  static_assert(KF <= 128 && CP <= 64, "staging rows are 256 B");
-  static_assert(KC <= KS, "the dh chain is interleaved into the layer-1 chain");
-  // double-buffered staging where the LDS budget allows it (HD = 256: K <= 112, C <= 48)
-  constexpr int NBUF = fused_bwd_lds(KP, CP, HD, 2) <= 160 * 1024 ? 2 : 1;
-  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  uint16_t* sW1T = lds;                       // [HD][W1S]
-  uint16_t* sW2 = sW1T + HD * W1S;            // [HD][W2S]   W2 rows (hidden-major)
-  // staging: NBUF buffers (two: tile i computes from one while tile i + 1 is written to
-  // the other, one block barrier per tile), each = AX [32][128] | dY2 [32][128],
-  // swizzled (stg_off), dY2 columns < 64 used
-  uint16_t* sStg = sW2 + HD * W2S;
-  uint16_t* sH1 = sStg + NBUF * 2 * TILE * 128;   // [NW][32][32] per-wave images (img_off)
-  uint16_t* sDP = sH1 + NW * TILE * 32;       // [NW][32][32]
-  float* sB1 = reinterpret_cast<float*>(sDP + NW * TILE * 32);   // [HD]
-
-  const int tid = threadIdx.x;
-  for (int i = tid; i < HD * KP; i += NT) {
-    const int k = i / HD, nn = i - k * HD;
-    sW1T[nn * W1S + k] = bf16_bits(k < F ? W1[(size_t)k * HD + nn] : 0.f);
-  }
-  for (int i = tid; i < HD * CP; i += NT) {
-    const int nn = i / CP, c = i - nn * CP;
-    sW2[nn * W2S + c] = bf16_bits(c < C ? W2[(size_t)nn * C + c] : 0.f);
-  }
-  for (int i = tid; i < HD; i += NT) sB1[i] = b1[i];
-  // zero the staging images: chunks the per-tile staging never writes (columns past
-  // the staged K, read by the padded contraction tiles) stay zero
-  for (int i = tid; i < NBUF * 2 * TILE * 128 / 8; i += NT)
-    reinterpret_cast<uint4*>(sStg)[i] = make_uint4(0u, 0u, 0u, 0u);
-
-  const int lane = tid & 63, h = lane >> 5, lr = lane & 31;
-  const int t = tid >> 6;                     // this wave's hidden block
-  // transposed-read lane roles: 16-lane group, block row qq, column quad pq
-  const int gb = (lane >> 4) & 1, qq = (lane >> 2) & 3, pq = lane & 3;
-  uint16_t* wH1 = sH1 + t * TILE * 32;
-  uint16_t* wDP = sDP + t * TILE * 32;
-  const int n_tiles = (n + TILE - 1) / TILE;
-  const float scale = 1.f / (1.f - p);
-  // 16-byte chunks staged per row: the K columns the products read (a row pitch wider
-  // than that -- rows padded to whole cache lines -- is not staged)
-  const int xch = min(ldx, KP) / 8, ych = min(ldc, CP) / 8;
-
-  f32x16 g1[KF / 32], g2[2];
-#pragma unroll
-  for (int q = 0; q < KF / 32; ++q) g1[q] = f32x16{};
-  g2[0] = f32x16{};
-  g2[1] = f32x16{};
-
-  // prefetch registers: chunks tid, tid + NT, ... (chunk i = row i % 32, column chunk
-  // i / 32) of the AX tile and of the dY2 tile
-  constexpr int PFX = (TILE * (KP / 8) + NT - 1) / NT, PFY = (TILE * (CP / 8) + NT - 1) / NT;
-  uint4 pax[PFX], pdy[PFY];
-  auto prefetch = [&](int tile) {
-    const int r0 = tile * TILE;
-#pragma unroll
-    for (int k = 0; k < PFX; ++k) {
-      const int i = tid + k * NT;
-      const int rr = i % TILE, ch = i / TILE;
-      pax[k] = (i < TILE * xch && r0 + rr < n)
-                   ? *reinterpret_cast<const uint4*>(AX + (size_t)(r0 + rr) * ldx + 8 * ch)
-                   : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int k = 0; k < PFY; ++k) {
-      const int i = tid + k * NT;
-      const int rr = i % TILE, ch = i / TILE;
-      pdy[k] = (i < TILE * ych && r0 + rr < n)
-                   ? *reinterpret_cast<const uint4*>(dY2 + (size_t)(r0 + rr) * ldc + 8 * ch)
-                   : make_uint4(0u, 0u, 0u, 0u);
-    }
-  };
-  auto stage = [&](int buf) {
-    char* const bA = reinterpret_cast<char*>(sStg + buf * 2 * TILE * 128);
-    char* const bD = bA + 2 * TILE * 128;
-#pragma unroll
-    for (int k = 0; k < PFX; ++k) {
-      const int i = tid + k * NT;
-      if (i < TILE * xch) *reinterpret_cast<uint4*>(bA + stg_off(i % TILE, i / TILE)) = pax[k];
-    }
-#pragma unroll
-    for (int k = 0; k < PFY; ++k) {
-      const int i = tid + k * NT;
-      if (i < TILE * ych) *reinterpret_cast<uint4*>(bD + stg_off(i % TILE, i / TILE)) = pdy[k];
-    }
-  };
-  const int G = gridDim.x;
-  __syncthreads();                            // the zeroed staging images
-  if ((int)blockIdx.x < n_tiles) {
-    prefetch(blockIdx.x);
-    if constexpr (NBUF == 2) {
-      stage(0);
-      if ((int)blockIdx.x + G < n_tiles) prefetch(blockIdx.x + G);
-    }
-  }
-  __syncthreads();
-
-  int it = 0;
-  for (int tile = blockIdx.x; tile < n_tiles; tile += G, ++it) {
-    int cur = 0;
-    if constexpr (NBUF == 2) {
-      // stage the next tile into the other buffer (read by the previous tile, which
-      // every wave finished at the last barrier), prefetch the one after
-      cur = it & 1;
-      if (tile + G < n_tiles) {
-        stage(cur ^ 1);
-        if (tile + 2 * G < n_tiles) prefetch(tile + 2 * G);
-      }
-    } else {
-      stage(0);
-      if (tile + G < n_tiles) prefetch(tile + G);
-      __syncthreads();
-    }
-    uint16_t* const sAX = sStg + cur * 2 * TILE * 128;
-    uint16_t* const sDY = sAX + TILE * 128;
-    char* const bAX = reinterpret_cast<char*>(sAX);
-    char* const bDY = reinterpret_cast<char*>(sDY);
-
-    // ---- recompute H1^T block t, dP1^T block t (lane = row, registers = hidden) ----
-    const int row = tile * TILE + lr;
-    // both chains' operands read from LDS as one batch (not one round trip per MFMA);
-    // the layer-1 accumulator starts as the bias (fp32)
-    f32x16 acc, dh = {};
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 bb = *reinterpret_cast<const float4*>(sB1 + 32 * t + 8 * g + 4 * h);
-      acc[4 * g] = bb.x; acc[4 * g + 1] = bb.y; acc[4 * g + 2] = bb.z; acc[4 * g + 3] = bb.w;
-    }
-    {
-      const uint16_t* arow = sW1T + (32 * t + lr) * W1S + 8 * h;
-      const uint16_t* drow = sW2 + (32 * t + lr) * W2S + 8 * h;
-      bf16x8 a1[KS], x1[KS], a2[KC], y2[KC];
-#pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2) {
-        a1[s2] = load_bf16x8(arow + 16 * s2);
-        x1[s2] = load_bf16x8(reinterpret_cast<const uint16_t*>(bAX + stg_off(lr, 2 * s2 + h)));
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < KC; ++s2) {
-        a2[s2] = load_bf16x8(drow + 16 * s2);
-        y2[s2] = load_bf16x8(reinterpret_cast<const uint16_t*>(bDY + stg_off(lr, 2 * s2 + h)));
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2) {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[s2], x1[s2], acc, 0, 0, 0);
-        if (s2 < KC) dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2[s2], y2[s2], dh, 0, 0, 0);
-      }
-    }
-    uint32_t m = 0xffffu;
-    if constexpr (DROP)
-      m = drop_keep16(drop_draw(row0 + (uint32_t)row, t, h, step, k0, k1, drop_bit_mode(thr8)), t, thr8,
-                      drop_bit_mode(thr8));
-    // registers 4g..4g+3 = hidden 32t + 8g + 4h + 0..3 of this lane's row: one packed
-    // 8-B write per image and g
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float xv[4], dv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int q = 4 * g + i;
-        float x = fmaxf(acc[q], 0.f);
-        if constexpr (DROP) x = ((m >> q) & 1u) ? x * scale : 0.f;
-        xv[i] = x;
-        dv[i] = x > 0.f ? dh[q] * scale : 0.f;
-      }
-      const int off = img_off(lr, 2 * g + h);
-      *reinterpret_cast<uint2*>(reinterpret_cast<char*>(wH1) + off) = pack4(xv[0], xv[1], xv[2], xv[3]);
-      *reinterpret_cast<uint2*>(reinterpret_cast<char*>(wDP) + off) = pack4(dv[0], dv[1], dv[2], dv[3]);
-    }
-    // the contraction below reads only this wave's own images: a wave-local ordering
-    // of the LDS writes and reads suffices (no block barrier)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-
-    // ---- contractions over the tile's 32 rows (two k-steps of 16) ----
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int ra = 16 * s2 + 8 * h + qq;      // block rows ra (+4 for the second read)
-      const bf16x8 adp = tr_frag(wDP, img_off(ra, 4 * gb + pq), img_off(ra + 4, 4 * gb + pq));
-      const bf16x8 ah1 = tr_frag(wH1, img_off(ra, 4 * gb + pq), img_off(ra + 4, 4 * gb + pq));
-      const int cb = 2 * gb + (pq >> 1), cx = 8 * (pq & 1);
-#pragma unroll
-      for (int q = 0; q < KF / 32; ++q)
-        g1[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            adp, tr_frag(sAX, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 4, 4 * q + cb) + cx), g1[q], 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        g2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-            ah1, tr_frag(sDY, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 4, 4 * q + cb) + cx), g2[q], 0, 0, 0);
-    }
-    __syncthreads();      // this buffer is rewritten two tiles on; the next one is staged
-  }
-
-  // ---- this block's partial slab: rows = hidden 32t + m, columns [f | KF + c] ----
-  float* gp = gpart + (size_t)blockIdx.x * HD * (KF + 64);
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int hrow = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
-    float* dst = gp + (size_t)hrow * (KF + 64);
-#pragma unroll
-    for (int fb = 0; fb < KF / 32; ++fb) dst[32 * fb + lr] = g1[fb][q];
-    dst[KF + lr] = g2[0][q];
-    dst[KF + 32 + lr] = g2[1][q];
-  }
-}
-
-// ============================================================================
-// Fused backward, round-3 form: the same four products with the recompute chains
-// swapped to ROWS x HIDDEN output tiles,
-//   P1[row][h]  = AX[row][:] W1[:][h] (+ b1),   dP1[row][h] = dY2[row][:] W2^T[:][h],
-// so that the accumulators (lane = hidden unit, registers = 16 rows of the tile) are
-// ALREADY the A operands of the contractions over the rows (dP1^T, H1^T: hidden x
-// rows; the k order inside a 16-row step is permuted -- rows 4h..4h+3, 8+4h..8+4h+3
-// -- and the transposed B reads of AX / dY2 use the same permutation).  Against the
-// round-2 form above this removes, per wave and 32-row tile:
-//   * the 10 b128 LDS reads of the weight fragments: each wave owns one 32-unit hidden
-//     block for the whole launch, so its W1 / W2^T B fragments (KS + KC bf16x8) are
-//     loaded once into registers and the weights need no LDS at all;
-//   * the H1 / dP1 images (8 packed LDS writes, 8 transposed reads, a wave barrier).
-// LDS is the double-buffered AX / dY2 staging (32 KiB) and a 128-B keep-bit image per
-// wave and hidden block.  The dropout mask is the forward's (cgnn_common.h drop_draw):
-// each lane draws for its (row, half) as the forward does and writes its 16 keep bits
-// as one halfword of the image's word `row`; every lane then reads the 16 words of its
-// rows (four b128 reads) and takes its unit's bit with a sign-extending bit-field
-// extract -- the keep mask as an AND mask, no ballots, no per-element branches.  As
-// in the forward the 1/(1-p) of the kept units is applied once, to the weight-gradient
-// slab, not per element.  The bias is added in the epilogue (packed), not as the
-// accumulator's initial value.
-// ============================================================================
-constexpr size_t fused_bwd2_lds(int HD) { return sizeof(uint16_t) * 2 * 2 * 32 * 128 + sizeof(uint32_t) * HD; }
-
-// TB hidden blocks per wave (1: HD/32 waves of <= 256 registers, 2 waves / SIMD; 2: HD/64
-// waves of up to 512 registers -- accumulators in AGPRs -- one wave / SIMD, and every
-// LDS fragment a wave reads (the AX / dY2 rows, the transposed contraction operands)
-// feeds two hidden blocks' MFMAs, half the LDS traffic per tile)
-template <int KS, int KC, int HD, int DROP, int TB>
-__global__ __launch_bounds__(HD * 2 / TB, 1) void gcn_fused_bwd2_kernel(
-    const uint16_t* __restrict__ AX, const uint16_t* __restrict__ dY2, const float* __restrict__ W1,
-    const float* __restrict__ b1, const float* __restrict__ W2, float* __restrict__ gpart, int n, int F,
-    int ldx, int C, int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
-    uint32_t row0, const int* __restrict__ stepp) {
-  if (stepp) step = (uint32_t)*stepp;         // device-resident dropout step (graph replays)
-  constexpr int NW = HD / 32 / TB;            // waves per block; wave w owns hidden blocks w + NW b
-  constexpr int NT = NW * 64;
-  constexpr int KP = KS * 16;                 // layer-1 K (features + ones column), padded
-  constexpr int KF = (KP + 31) / 32 * 32;     // gW1^T columns (f), padded to whole tiles
-  constexpr int CP = KC * 16;                 // classes, padded
+  constexpr int KCH = DROP ? NW * 8 : 0;      // 16-B chunks of one tile's keep image
   static_assert(KF <= 128 && CP <= 64, "staging rows are 256 B");
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* sStg = lds;                       // 2 x (AX [32][128] | dY2 [32][128]), stg_off swizzle
-  uint32_t* sKeep = reinterpret_cast<uint32_t*>(lds + 2 * 2 * TILE * 128);   // [NW * TB][32] words
+  uint32_t* sKeep = reinterpret_cast<uint32_t*>(lds + 2 * 2 * TILE * 128);   // 2 x [NW][32] words
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, h = lane >> 5, lr = lane & 31;
@@ -576,49 +414,46 @@ __global__ __launch_bounds__(HD * 2 / TB, 1) void gcn_fused_bwd2_kernel(
   const int gb = (lane >> 4) & 1, qq = (lane >> 2) & 3, pq = lane & 3;
 
   // B fragments of the two recompute chains (lane = hidden unit, k = 16 s + 8 h + j)
-  bf16x8 w1f[TB][KS], w2f[TB][KC];
-  float bias[TB];
+  bf16x8 w1f[KS], w2f[KC];
+  const int hid = 32 * wv + lr;               // this lane's hidden unit
 #pragma unroll
-  for (int b = 0; b < TB; ++b) {
-    const int hid = 32 * (wv + NW * b) + lr;  // this lane's hidden unit in block b
+  for (int s = 0; s < KS; ++s)
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * h + j;
+      const float v = W1[(size_t)min(k, F - 1) * HD + hid];
+      w1f[s][j] = (__bf16)(k < F ? v : 0.f);
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 16 * s + 8 * h + j;
-        const float v = W1[(size_t)min(k, F - 1) * HD + hid];
-        w1f[b][s][j] = (__bf16)(k < F ? v : 0.f);
-      }
+  for (int s = 0; s < KC; ++s)
 #pragma unroll
-    for (int s = 0; s < KC; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = 16 * s + 8 * h + j;
-        const float v = W2[(size_t)hid * C + min(c, C - 1)];
-        w2f[b][s][j] = (__bf16)(c < C ? v : 0.f);
-      }
-    bias[b] = b1[hid];
-  }
+    for (int j = 0; j < 8; ++j) {
+      const int c = 16 * s + 8 * h + j;
+      const float v = W2[(size_t)hid * C + min(c, C - 1)];
+      w2f[s][j] = (__bf16)(c < C ? v : 0.f);
+    }
+  const f2 bb = {b1[hid], b1[hid]};
   for (int i = tid; i < 2 * 2 * TILE * 128 / 8; i += NT)
     reinterpret_cast<uint4*>(sStg)[i] = make_uint4(0u, 0u, 0u, 0u);
 
   const int n_tiles = (n + TILE - 1) / TILE;
   const float scale = 1.f / (1.f - p);
   const int xch = min(ldx, KP) / 8, ych = min(ldc, CP) / 8;
-  // this lane's hidden unit lr in the keep-bit image words: bit 16 half + q with
-  // half = (lr >> 2) & 1, q = 4 (lr >> 3) + (lr & 3) (the forward's register order)
-  const uint32_t kpos = 16u * ((lr >> 2) & 1) + 4u * (lr >> 3) + (lr & 3);
+  // this lane's unit in the keep image: the drawing lane's unit half uh, bit kq
+  const int uh = (lr >> 2) & 1;
+  const uint32_t kq = 4u * (lr >> 3) + (lr & 3);
 
-  f32x16 g1[TB][KF / 32], g2[TB][2];
+  f32x16 g1[KF / 32], g2[2];
 #pragma unroll
-  for (int b = 0; b < TB; ++b) {
-#pragma unroll
-    for (int q = 0; q < KF / 32; ++q) g1[b][q] = f32x16{};
-    g2[b][0] = f32x16{};
-    g2[b][1] = f32x16{};
-  }
+  for (int q = 0; q < KF / 32; ++q) g1[q] = f32x16{};
+  g2[0] = f32x16{};
+  g2[1] = f32x16{};
 
-  constexpr int PFX = (TILE * (KP / 8) + NT - 1) / NT, PFY = (TILE * (CP / 8) + NT - 1) / NT;
+  // prefetch registers: AX chunks i = tid + k NT (chunk i = row i % 32, column chunk
+  // i / 32); dY2 chunks in the same form, and the tile's keep image (KCH chunks) in the
+  // slots [TILE * CP / 8, + KCH) of the dY2 index space
+  constexpr int KB = TILE * (CP / 8);
+  constexpr int PFX = (TILE * (KP / 8) + NT - 1) / NT, PFY = (KB + KCH + NT - 1) / NT;
   uint4 pax[PFX], pdy[PFY];
   auto prefetch = [&](int tile) {
     const int r0 = tile * TILE;
@@ -634,9 +469,12 @@ __global__ __launch_bounds__(HD * 2 / TB, 1) void gcn_fused_bwd2_kernel(
     for (int k = 0; k < PFY; ++k) {
       const int i = tid + k * NT;
       const int rr = i % TILE, ch = i / TILE;
-      pdy[k] = (i < TILE * ych && r0 + rr < n)
-                   ? *reinterpret_cast<const uint4*>(dY2 + (size_t)(r0 + rr) * ldc + 8 * ch)
-                   : make_uint4(0u, 0u, 0u, 0u);
+      if (i < TILE * ych && r0 + rr < n)
+        pdy[k] = *reinterpret_cast<const uint4*>(dY2 + (size_t)(r0 + rr) * ldc + 8 * ch);
+      else if (KCH && i >= KB && i < KB + KCH)
+        pdy[k] = reinterpret_cast<const uint4*>(kimg + (size_t)tile * NW * 64)[i - KB];
+      else
+        pdy[k] = make_uint4(0u, 0u, 0u, 0u);
     }
   };
   auto stage = [&](int buf) {
@@ -650,7 +488,10 @@ __global__ __launch_bounds__(HD * 2 / TB, 1) void gcn_fused_bwd2_kernel(
 #pragma unroll
     for (int k = 0; k < PFY; ++k) {
       const int i = tid + k * NT;
-      if (i < TILE * ych) *reinterpret_cast<uint4*>(bD + stg_off(i % TILE, i / TILE)) = pdy[k];
+      if (i < TILE * ych)
+        *reinterpret_cast<uint4*>(bD + stg_off(i % TILE, i / TILE)) = pdy[k];
+      else if (KCH && i >= KB && i < KB + KCH)
+        reinterpret_cast<uint4*>(sKeep + buf * NW * 32)[i - KB] = pdy[k];
     }
   };
   const int G = gridDim.x;
@@ -674,13 +515,8 @@ __global__ __launch_bounds__(HD * 2 / TB, 1) void gcn_fused_bwd2_kernel(
     const char* const bAX = reinterpret_cast<const char*>(sAX);
     const char* const bDY = reinterpret_cast<const char*>(sDY);
 
-    // ---- recompute P1 and dP1 (rows x hidden blocks; lane = hidden, regs = rows) ----
-    f32x16 acc[TB], dh[TB];
-#pragma unroll
-    for (int b = 0; b < TB; ++b) {
-      acc[b] = f32x16{};
-      dh[b] = f32x16{};
-    }
+    // ---- recompute P1 and dP1 (rows x hidden block; lane = hidden, regs = rows) ----
+    f32x16 acc = {}, dh = {};
     {
       bf16x8 x1[KS], y2[KC];
 #pragma unroll
@@ -688,53 +524,41 @@ __global__ __launch_bounds__(HD * 2 / TB, 1) void gcn_fused_bwd2_kernel(
 #pragma unroll
       for (int s = 0; s < KC; ++s) y2[s] = load_bf16x8(reinterpret_cast<const uint16_t*>(bDY + stg_off(lr, 2 * s + h)));
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int b = 0; b < TB; ++b) {
-          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1[s], w1f[b][s], acc[b], 0, 0, 0);
-          if (s < KC) dh[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(y2[s], w2f[b][s], dh[b], 0, 0, 0);
-        }
+      for (int s = 0; s < KS; ++s) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1[s], w1f[s], acc, 0, 0, 0);
+        if (s < KC) dh = __builtin_amdgcn_mfma_f32_32x32x16_bf16(y2[s], w2f[s], dh, 0, 0, 0);
+      }
     }
-    // H1 = dropout(relu(P1 + b1)), dP1 = dh * [H1 > 0] (both without the 1/(1-p), applied
-    // to the slab), as the contractions' A operands (register 8 s + j = row
-    // 16 s + 8 (j / 4) + 4 h + j % 4)
-    bf16x8 ah1[TB][2], adp[TB][2];
-    static_assert(HD <= 256, "bit-mode dropout: one draw covers 8 hidden blocks");
-    u32x4 rb{};             // bit mode: the draw of (row lr, half h), shared by every block
-    if constexpr (DROP == 2) rb = drop_draw(row0 + (uint32_t)(tile * TILE + lr), 0, h, step, k0, k1, true);
+    // register pair i = registers 2i, 2i + 1 = tile rows 2P, 2P + 1 with
+    // P = 4 (i / 2) + 2 h + i % 2: its keep word (rows 2P / 2P + 1 in the low / high
+    // half, this unit's bit at kq) is word 16 uh + P of the block's image
+    uint32_t kw[8];
+    if constexpr (DROP) {
+      const uint32_t* img = sKeep + cur * NW * 32 + wv * 32 + uh * 16 + 2 * h;
 #pragma unroll
-    for (int b = 0; b < TB; ++b) {
-      uint4 kw[4];          // keep-bit words of rows 8 g + 4 h + 0..3
-      if constexpr (DROP != 0) {
-        const int t = wv + NW * b;
-        const uint32_t m = drop_keep16(DROP == 2 ? rb : drop_draw(row0 + (uint32_t)(tile * TILE + lr), t, h, step,
-                                                                  k0, k1, false),
-                                       t, thr8, DROP == 2);
-        uint32_t* img = sKeep + (wv * TB + b) * 32;
-        reinterpret_cast<uint16_t*>(img)[2 * lr + h] = (uint16_t)m;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#pragma unroll
-        for (int g = 0; g < 4; ++g) kw[g] = *reinterpret_cast<const uint4*>(img + 8 * g + 4 * h);
+      for (int g = 0; g < 4; ++g) {
+        const uint2 w = *reinterpret_cast<const uint2*>(img + 4 * g);
+        kw[2 * g] = w.x;
+        kw[2 * g + 1] = w.y;
       }
-      const f2 bb = {bias[b], bias[b]};
+    }
+    // H1 = dropout(relu(P1 + b1)) and dP1 = dh * [H1 > 0], both without the 1/(1-p)
+    // (applied to the slab), as packed bf16 pairs: the contractions' A operands
+    // (fragment s, dword d = register pair 4 s + d)
+    uint32_t ah[8], ad[8];
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const f2 z = f2{acc[b][r], acc[b][r + 1]} + bb;
-        float x[2] = {fmaxf(z.x, 0.f), fmaxf(z.y, 0.f)};
+    for (int i = 0; i < 8; ++i) {
+      const f2 z = f2{acc[2 * i], acc[2 * i + 1]} + bb;
+      uint32_t x = pk_relu(cvt_pk(z.x, z.y));
+      if constexpr (DROP) x = pk_mul16(x, (kw[i] >> kq) & 0x10001u);
+      ah[i] = x;
+      ad[i] = pk_mul16(cvt_pk(dh[2 * i], dh[2 * i + 1]), pk_nz(x));
+    }
+    bf16x8 ah1[2], adp[2];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int rr = r + e;
-          if constexpr (DROP != 0) {
-            const uint4 q4 = kw[rr >> 2];
-            const uint32_t wd = (rr & 3) == 0 ? q4.x : (rr & 3) == 1 ? q4.y : (rr & 3) == 2 ? q4.z : q4.w;
-            x[e] = keep_and(x[e], wd, kpos);
-          }
-          ah1[b][rr >> 3][rr & 7] = (__bf16)x[e];
-          adp[b][rr >> 3][rr & 7] = (__bf16)(x[e] > 0.f ? dh[b][rr] : 0.f);
-        }
-      }
+    for (int s = 0; s < 2; ++s) {
+      ah1[s] = __builtin_bit_cast(bf16x8, make_uint4(ah[4 * s], ah[4 * s + 1], ah[4 * s + 2], ah[4 * s + 3]));
+      adp[s] = __builtin_bit_cast(bf16x8, make_uint4(ad[4 * s], ad[4 * s + 1], ad[4 * s + 2], ad[4 * s + 3]));
     }
 
     // ---- contractions over the tile's 32 rows (two k-steps of 16, permuted rows) ----
@@ -745,35 +569,49 @@ __global__ __launch_bounds__(HD * 2 / TB, 1) void gcn_fused_bwd2_kernel(
 #pragma unroll
       for (int q = 0; q < KF / 32; ++q) {
         const bf16x8 bx = tr_frag(sAX, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 8, 4 * q + cb) + cx);
-#pragma unroll
-        for (int b = 0; b < TB; ++b) g1[b][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(adp[b][s2], bx, g1[b][q], 0, 0, 0);
+        g1[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(adp[s2], bx, g1[q], 0, 0, 0);
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const bf16x8 by = tr_frag(sDY, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 8, 4 * q + cb) + cx);
-#pragma unroll
-        for (int b = 0; b < TB; ++b) g2[b][q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1[b][s2], by, g2[b][q], 0, 0, 0);
+        g2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1[s2], by, g2[q], 0, 0, 0);
       }
     }
     __syncthreads();      // this buffer is rewritten two tiles on; the next one is staged
   }
 
-  // ---- this block's partial slab: rows = hidden 32t + m, columns [f | KF + c] ----
-  const float gs = DROP != 0 ? scale : 1.f;   // the kept units' 1/(1-p)
+  // ---- this block's partial slab: rows = hidden 32 wv + m, columns [f | KF + c] ----
+  const float gs = DROP ? scale : 1.f;        // the kept units' 1/(1-p)
   float* gp = gpart + (size_t)blockIdx.x * HD * (KF + 64);
 #pragma unroll
-  for (int b = 0; b < TB; ++b) {
-    const int t = wv + NW * b;
+  for (int q = 0; q < 16; ++q) {
+    const int hrow = 32 * wv + (q & 3) + 8 * (q >> 2) + 4 * h;
+    float* dst = gp + (size_t)hrow * (KF + 64);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int hrow = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
-      float* dst = gp + (size_t)hrow * (KF + 64);
-#pragma unroll
-      for (int fb = 0; fb < KF / 32; ++fb) dst[32 * fb + lr] = g1[b][fb][q] * gs;
-      dst[KF + lr] = g2[b][0][q] * gs;
-      dst[KF + 32 + lr] = g2[b][1][q] * gs;
-    }
+    for (int fb = 0; fb < KF / 32; ++fb) dst[32 * fb + lr] = g1[fb][q] * gs;
+    dst[KF + lr] = g2[0][q] * gs;
+    dst[KF + 32 + lr] = g2[1][q] * gs;
   }
+}
+
+// The keep image of the forward (gcn_dense_fwd_kernel, kimg) drawn on its own, for a
+// backward that runs without that forward: one lane per (tile row, unit half), the
+// same Philox draws.
+__global__ __launch_bounds__(256) void gcn_keep_image_kernel(uint16_t* __restrict__ kimg, int n, int NB,
+                                                             uint32_t thr8, uint32_t k0, uint32_t k1, uint32_t step,
+                                                             uint32_t row0, const int* __restrict__ stepp) {
+  if (stepp) step = (uint32_t)*stepp;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n_tiles = (n + TILE - 1) / TILE;
+  const int tile = (int)(gid >> 6), lane = (int)(gid & 63);
+  if (tile >= n_tiles) return;
+  const uint32_t row = row0 + (uint32_t)(tile * TILE + (lane & 31));
+  const int h = lane >> 5;
+  const bool bit = drop_bit_mode(thr8);
+  const u32x4 rb = drop_draw(row, 0, h, step, k0, k1, true);
+  for (int t = 0; t < NB; ++t)
+    kimg[(size_t)(tile * NB + t) * 64 + lane] =
+        (uint16_t)drop_keep16(bit ? rb : drop_draw(row, t, h, step, k0, k1, false), t, thr8, bit);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -795,12 +633,17 @@ template <int KS, int HD, int DROP>
 static int fwd_launch_d(const uint16_t* AX, const float* W1, const float* b1, const float* W2,
                         const float* dinv, uint16_t* H1, uint16_t* Z2, int n, int F, int ldx, int C,
                         int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
-                        uint32_t row0, const int* stepp, hipStream_t st) {
-  const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KS * 16 + 8) + 64 * (size_t)(HD + 8)) + sizeof(float) * HD;
+                        uint32_t row0, const int* stepp, uint16_t* kimg, hipStream_t st) {
+  const size_t lds = sizeof(uint16_t) * ((size_t)HD * (KS * 16 + 8) + 64 * (size_t)(HD + 4)) + sizeof(float) * HD;
   (void)hipFuncSetAttribute((const void*)gcn_dense_fwd_kernel<KS, HD, DROP>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((gcn_dense_fwd_kernel<KS, HD, DROP>), dim3(dense_grid(n)), dim3(WAVES * 64), lds, st, AX, W1,
-                     b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp);
+                     b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp, kimg);
+  if (DROP == 1 && kimg) {
+    const long lanes = (long)((n + TILE - 1) / TILE) * 64;
+    hipLaunchKernelGGL(gcn_keep_image_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st, kimg, n,
+                       HD / 32, thr8, k0, k1, step, row0, stepp);
+  }
   return (int)hipGetLastError();
 }
 
@@ -808,31 +651,50 @@ template <int KS, int HD>
 static int fwd_launch(const uint16_t* AX, const float* W1, const float* b1, const float* W2,
                       const float* dinv, uint16_t* H1, uint16_t* Z2, int n, int F, int ldx, int C,
                       int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
-                      uint32_t row0, const int* stepp, hipStream_t st) {
+                      uint32_t row0, const int* stepp, uint16_t* kimg, hipStream_t st) {
   if (thr8 == 128)
     return fwd_launch_d<KS, HD, 2>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
-                                   stepp, st);
+                                   stepp, kimg, st);
   if (thr8 > 0)
     return fwd_launch_d<KS, HD, 1>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
-                                   stepp, st);
+                                   stepp, kimg, st);
   return fwd_launch_d<KS, HD, 0>(AX, W1, b1, W2, dinv, H1, Z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0,
-                                     stepp, st);
+                                 stepp, kimg, st);
 }
 
+static uint32_t drop_thr8(float p) { return (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5)); }
+
+// kimg (optional): the keep image for the fused backward, gnn_keep_image_halfwords(n, HD)
+// halfwords, written when the launch draws dropout masks
 extern "C" int gnn_launch_dense_fwd(const void* AX, const float* W1, const float* b1, const float* W2,
                                     const float* dinv, void* H1, void* Z2, int n, int F, int ldx,
                                     int HD, int C, int ldc, float p, uint32_t k0, uint32_t k1,
-                                    uint32_t step, uint32_t row0, const int* stepp, hipStream_t st) {
+                                    uint32_t step, uint32_t row0, const int* stepp, void* kimg, hipStream_t st) {
   if (C > 64 || ldc % 8 || ldx % 8 || ldc > 64) return -3;
-  const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
+  const uint32_t thr8 = drop_thr8(p);
   const int KS = (F + 15) / 16;
   auto* ax = (const uint16_t*)AX;
   auto* h1 = (uint16_t*)H1;
   auto* z2 = (uint16_t*)Z2;
-#define FWD(ks, hd) if (KS <= ks && HD == hd) return fwd_launch<ks, hd>(ax, W1, b1, W2, dinv, h1, z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp, st);
+  auto* ki = (uint16_t*)kimg;
+#define FWD(ks, hd) if (KS <= ks && HD == hd) return fwd_launch<ks, hd>(ax, W1, b1, W2, dinv, h1, z2, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp, ki, st);
   FWD(4, 256) FWD(7, 256) FWD(8, 256) FWD(4, 128) FWD(8, 128)
 #undef FWD
   return -1;
+}
+
+// halfwords of the keep image of n rows at HD hidden units (1 bit per element, whole tiles)
+extern "C" long gnn_keep_image_halfwords(int n, int HD) { return (long)((n + TILE - 1) / TILE) * (HD / 32) * 64; }
+
+extern "C" int gnn_launch_keep_image(void* kimg, int n, int HD, float p, uint32_t k0, uint32_t k1, uint32_t step,
+                                     uint32_t row0, const int* stepp, hipStream_t st) {
+  if (HD % 32 || HD > 256) return -3;
+  const uint32_t thr8 = drop_thr8(p);
+  if (thr8 == 0) return 0;
+  const long lanes = (long)((n + TILE - 1) / TILE) * 64;
+  hipLaunchKernelGGL(gcn_keep_image_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st,
+                     (uint16_t*)kimg, n, HD / 32, thr8, k0, k1, step, row0, stepp);
+  return (int)hipGetLastError();
 }
 
 template <int KC, int HD>
@@ -883,40 +745,13 @@ extern "C" int gnn_fused_bwd_width(int K) {
 
 template <int KS, int KC, int HD>
 static int fused_bwd_launch(const uint16_t* AX, const uint16_t* dY2, const float* W1, const float* b1,
-                            const float* W2, float* gpart, int n, int F, int ldx, int C, int ldc, float p,
-                            uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0,
-                            const int* stepp, hipStream_t st) {
-  constexpr int KP = KS * 16, CP = KC * 16;
-  // round-3 form by default; env CGNN_FUSED_BWD_V1=1 launches the round-2 form (A/B)
-  static const bool v1 = [] {
-    const char* e = std::getenv("CGNN_FUSED_BWD_V1");
-    return e && e[0] && e[0] != '0';
-  }();
-  // hidden blocks per wave of the round-3 form: env CGNN_FUSED_BWD_TB (1 or 2, default 1:
-  // 680 vs 772 us on the ogbn-products shape, profiles/r03_bwd)
-  static const int tb = [] {
-    const char* e = std::getenv("CGNN_FUSED_BWD_TB");
-    return e && e[0] == '2' ? 2 : 1;
-  }();
-  if (!v1) {
-    const size_t lds = fused_bwd2_lds(HD);
-    const int dm = thr8 == 128 ? 2 : thr8 > 0 ? 1 : 0;
-    auto kern = tb == 1 ? (dm == 2 ? gcn_fused_bwd2_kernel<KS, KC, HD, 2, 1>
-                           : dm == 1 ? gcn_fused_bwd2_kernel<KS, KC, HD, 1, 1> : gcn_fused_bwd2_kernel<KS, KC, HD, 0, 1>)
-                        : (dm == 2 ? gcn_fused_bwd2_kernel<KS, KC, HD, 2, 2>
-                           : dm == 1 ? gcn_fused_bwd2_kernel<KS, KC, HD, 1, 2> : gcn_fused_bwd2_kernel<KS, KC, HD, 0, 2>);
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kern, dim3(gnn_fused_bwd_blocks(n)), dim3(HD * 2 / tb), lds, st,
-                       AX, dY2, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp);
-    return (int)hipGetLastError();
-  }
-  const size_t lds2 = fused_bwd_lds(KP, CP, HD, 2);
-  const size_t lds = lds2 <= 160 * 1024 ? lds2 : fused_bwd_lds(KP, CP, HD, 1);
-  if (lds > 160 * 1024) return -2;
-  auto kern = thr8 > 0 ? gcn_fused_bwd_kernel<KS, KC, HD, true> : gcn_fused_bwd_kernel<KS, KC, HD, false>;
+                            const float* W2, const uint16_t* kimg, float* gpart, int n, int F, int ldx, int C,
+                            int ldc, float p, bool drop, hipStream_t st) {
+  const size_t lds = fused_bwd_lds(HD);
+  auto kern = drop ? gcn_fused_bwd_kernel<KS, KC, HD, true> : gcn_fused_bwd_kernel<KS, KC, HD, false>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(gnn_fused_bwd_blocks(n)), dim3(HD * 2), lds, st,
-                     AX, dY2, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp);
+                     AX, dY2, W1, b1, W2, kimg, gpart, n, F, ldx, C, ldc, p);
   return (int)hipGetLastError();
 }
 
@@ -930,19 +765,21 @@ extern "C" int gnn_fused_bwd_supported(int K, int HD, int C) {
   return 0;
 }
 
-// AX: [n][ldx] bf16 with the ones column at F (ldx covers F + 1); dY2: [n][ldc] bf16.
-// gpart: [gnn_fused_bwd_blocks(n)][HD][gnn_fused_bwd_width(ldx)] fp32.
-// Returns -1 when no compiled variant covers the shape.
+// AX: [n][ldx] bf16 with the ones column at F (ldx covers F + 1); dY2: [n][ldc] bf16;
+// kimg: the forward's keep image of the same n rows (gnn_launch_dense_fwd / _keep_image),
+// required when p draws masks.  gpart: [gnn_fused_bwd_blocks(n)][HD][gnn_fused_bwd_width(ldx)]
+// fp32.  Returns -1 when no compiled variant covers the shape.
 extern "C" int gnn_launch_fused_bwd(const void* AX, const void* dY2, const float* W1, const float* b1,
-                                    const float* W2, float* gpart, int n, int F, int ldx, int HD, int C,
-                                    int ldc, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t row0,
-                                    const int* stepp, hipStream_t st) {
+                                    const float* W2, const void* kimg, float* gpart, int n, int F, int ldx, int HD,
+                                    int C, int ldc, float p, hipStream_t st) {
   if (C > 64 || ldc % 8 || ldx % 8 || C > ldc || F + 1 > ldx) return -3;
-  const uint32_t thr8 = (uint32_t)std::min(255.0, std::floor((double)p * 256.0 + 0.5));
+  const bool drop = drop_thr8(p) > 0;
+  if (drop && !kimg) return -3;
   const int KS = (F + 1 + 15) / 16, KC = (C + 15) / 16;
   auto* ax = (const uint16_t*)AX;
   auto* dy = (const uint16_t*)dY2;
-#define FB(ks, kc, hd) if (KS == ks && KC == kc && HD == hd) return fused_bwd_launch<ks, kc, hd>(ax, dy, W1, b1, W2, gpart, n, F, ldx, C, ldc, p, k0, k1, step, thr8, row0, stepp, st);
+  auto* ki = (const uint16_t*)kimg;
+#define FB(ks, kc, hd) if (KS == ks && KC == kc && HD == hd) return fused_bwd_launch<ks, kc, hd>(ax, dy, W1, b1, W2, ki, gpart, n, F, ldx, C, ldc, p, drop, st);
   FB(7, 3, 256) FB(7, 4, 256) FB(8, 3, 256) FB(8, 4, 256) FB(4, 3, 256) FB(4, 4, 256)
   FB(7, 3, 128) FB(8, 3, 128) FB(4, 3, 128) FB(8, 4, 128)
 #undef FB

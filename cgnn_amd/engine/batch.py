@@ -85,14 +85,19 @@ def mmd_kernel_choice(D: int, mmd_kernel: str = "auto") -> str:
     return choice
 
 
-def device_supported(d: int, H: int, max_in: int) -> bool:
+def device_supported(d: int, H: int, max_in: int, prog_len: int = 0) -> bool:
     """True when the device kernels cover a batch of ``d``-variable programs with hidden
-    width ``H`` and at most ``max_in`` generator inputs per node (the variable count up
-    to SUPPORTED_D[-1]; any H whose generator backward fits in LDS).  Otherwise
-    ``score_jobs`` trains the batch on the CPU reference path (with a warning)."""
+    width ``H``, at most ``max_in`` generator inputs per node and programs of at most
+    ``prog_len`` ints (the variable count up to SUPPORTED_D[-1]; a generator forward
+    whose sample state plus program copy, and a backward whose state, fit in LDS).
+    Otherwise ``score_jobs`` trains the batch on the CPU reference path (with a warning)."""
     if d > SUPPORTED_D[-1]:
         return False
-    return native.hip().gen_bwd_variant(int(H), int(max_in), int(d), 0) != 0
+    hip = native.hip()
+    stride = (int(prog_len) + 3) // 4 * 4              # pack_programs' stride
+    if hip.gen_fwd_lds(padded_dim(d), stride) > 160 * 1024:
+        return False
+    return hip.gen_bwd_variant(int(H), int(max_in), int(d), stride) != 0
 
 
 def _keys_tensor(keys, device):

@@ -81,6 +81,23 @@ def _run_reference(jobs: Sequence[Job], idx, cfg) -> np.ndarray:
     return tr.run(cfg.train_epochs, cfg.test_epochs, verbose=cfg.verbose)
 
 
+def _device_batch_ok(jobs: Sequence[Job], idx, cfg) -> bool:
+    """Whether the device kernels cover the batch ``idx``; if not (more variables than
+    the widest compiled joint, or a generator whose forward or backward state does not
+    fit in LDS) log it -- the caller trains the batch on the CPU reference path."""
+    from .batch import device_supported
+    d = jobs[idx[0]].program.n_vars
+    max_in = max(jobs[i].program.max_in for i in idx)
+    prog_len = max(len(jobs[i].program.prog) for i in idx)
+    if device_supported(d, cfg.h_layer_dim, max_in, prog_len):
+        return True
+    log.warning("CGNN batch of %d models (%d variables, h_layer_dim=%d, %d inputs per node) "
+                "is outside the device kernels; training it on the CPU reference path",
+                len(idx), d, cfg.h_layer_dim, max_in)
+    METRICS.record("cpu_fallback", models=len(idx), variables=d, h_layer_dim=cfg.h_layer_dim)
+    return False
+
+
 def _run_local(jobs: Sequence[Job], cfg) -> np.ndarray:
     import torch
     n = len(jobs)
@@ -90,20 +107,12 @@ def _run_local(jobs: Sequence[Job], cfg) -> np.ndarray:
     devices = pdist.devices_for(cfg)
     t0 = time.perf_counter()
     if devices:
-        from .batch import DeviceTrainer, device_supported
+        from .batch import DeviceTrainer
         batches = []
         for idx in _group_batches(jobs, max(1, cfg.batch_models)):
-            d = jobs[idx[0]].program.n_vars
-            max_in = max(jobs[i].program.max_in for i in idx)
-            if device_supported(d, cfg.h_layer_dim, max_in):
+            if _device_batch_ok(jobs, idx, cfg):
                 batches.append(idx)
                 continue
-            # a shape no device kernel covers (more variables than the widest compiled
-            # joint, or a generator whose backward does not fit in LDS): the CPU path
-            log.warning("CGNN batch of %d models (%d variables, h_layer_dim=%d, %d inputs per node) "
-                        "is outside the device kernels; training it on the CPU reference path",
-                        len(idx), d, cfg.h_layer_dim, max_in)
-            METRICS.record("cpu_fallback", models=len(idx), variables=d, h_layer_dim=cfg.h_layer_dim)
             scores[idx] = _run_reference(jobs, idx, cfg)
         pending = []
         for b, idx in enumerate(batches):
@@ -156,6 +165,11 @@ def _run_long(jobs: Sequence[Job], cfg) -> np.ndarray:
     dev = devices[0] if devices else torch.device("cpu")
     t0 = time.perf_counter()
     for idx in _group_batches(jobs, max(1, cfg.batch_models)):
+        if devices and not _device_batch_ok(jobs, idx, cfg):
+            # every rank trains the whole job on the fp64 CPU reference (same scores on
+            # every rank: no exchange needed)
+            scores[idx] = _run_reference(jobs, idx, cfg)
+            continue
         N = jobs[idx[0]].data.shape[1]
         Nw = N - N % world
         if Nw != N:
@@ -179,18 +193,23 @@ def score_jobs(jobs: Sequence[Job], cfg, max_retries: Optional[int] = None) -> n
         return _score_jobs(jobs, cfg, cfg.max_retries if max_retries is None else int(max_retries))
 
 
-def _score_jobs(jobs: Sequence[Job], cfg, max_retries: int) -> np.ndarray:
+def _score_jobs(jobs: Sequence[Job], cfg, max_retries: int, ids=None) -> np.ndarray:
+    # ids: the callers' job numbers of ``jobs`` (fault injection addresses those, also
+    # when a mixed short / long call recurses on its short subset)
+    ids = list(range(len(jobs))) if ids is None else list(ids)
+    faults = _fault_indices()
     long_idx = [i for i, j in enumerate(jobs) if is_long(j, cfg)]
     if long_idx:
         # long-N jobs: every rank trains every job on its block of samples
         out = np.full(len(jobs), np.nan)
-        short_idx = [i for i in range(len(jobs)) if i not in set(long_idx)]
+        long_set = set(long_idx)
+        short_idx = [i for i in range(len(jobs)) if i not in long_set]
         if short_idx:
-            out[short_idx] = _score_jobs([jobs[i] for i in short_idx], cfg, max_retries)
+            out[short_idx] = _score_jobs([jobs[i] for i in short_idx], cfg, max_retries,
+                                         ids=[ids[i] for i in short_idx])
         ls = _run_long([jobs[i] for i in long_idx], cfg)
-        faults = _fault_indices()
         for k, i in enumerate(long_idx):
-            if i in faults:
+            if ids[i] in faults:
                 ls[k] = np.nan
         for attempt in range(max_retries):
             bad = [k for k in range(len(long_idx)) if not np.isfinite(ls[k])]
@@ -210,9 +229,8 @@ def _score_jobs(jobs: Sequence[Job], cfg, max_retries: int) -> np.ndarray:
     n = len(jobs)
     idx = pdist.shard_indices(n)
     local = _run_local([jobs[i] for i in idx], cfg) if len(idx) else np.zeros(0)
-    faults = _fault_indices()
     for k, i in enumerate(idx):
-        if int(i) in faults:
+        if ids[int(i)] in faults:
             local[k] = np.nan
     for attempt in range(max_retries):
         bad = [k for k in range(len(idx)) if not np.isfinite(local[k])]

@@ -75,17 +75,18 @@ def _check_transposed(g: "GraphCSR", what):
         checks.csr(rp_t, col_t, g.n, what, n_rows=g.n_cols)
 
 
-def _gat_forward_kernels(Whg, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool):
+def _gat_forward_kernels(Whg, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool, need_q: bool = True):
     """(out, lse, q): the forward plus the LeakyReLU split ``q`` the row half of the
-    backward reads (gnn_gat.hip), stored like Whg."""
+    backward reads (gnn_gat.hip), stored like Whg.  ``need_q=False`` (no backward will
+    run: inference, no_grad): q is neither allocated nor written (None)."""
     _check_graph(g, Whg, s_src, s_dst, "gat_fwd")
     n = g.n
     out = torch.empty(n, K * Fh, dtype=torch.float32, device=Whg.device)
     lse = torch.empty(n, K, dtype=torch.float32, device=Whg.device)
-    q = torch.empty(n, K * Fh, dtype=Whg.dtype, device=Whg.device)
+    q = torch.empty(n, K * Fh, dtype=Whg.dtype, device=Whg.device) if need_q else None
     native.hip().gnn_gat_fwd(g.rowptr.data_ptr(), g.col.data_ptr(), Whg.data_ptr(), s_src.data_ptr(),
                              s_dst.data_ptr(), out.data_ptr(), lse.data_ptr(), n, K, Fh, _st(Whg), int(lowp),
-                             q=q.data_ptr())
+                             q=q.data_ptr() if q is not None else 0)
     return out, lse, q
 
 
@@ -122,8 +123,11 @@ class _GATAggregate(torch.autograd.Function):
     def forward(ctx, Wh, s_src, s_dst, g: GraphCSR, K: int, Fh: int, lowp: bool):
         Whg = Wh.to(torch.bfloat16).contiguous() if lowp else Wh.contiguous()
         s_src, s_dst = s_src.contiguous(), s_dst.contiguous()
-        out, lse, q = _gat_forward_kernels(Whg, s_src, s_dst, g, K, Fh, lowp)
-        ctx.save_for_backward(Whg, s_src, s_dst, out, lse, q)
+        # q only when a backward can follow (the tensors' grad flags survive into forward)
+        need_q = any(ctx.needs_input_grad[:3])
+        out, lse, q = _gat_forward_kernels(Whg, s_src, s_dst, g, K, Fh, lowp, need_q=need_q)
+        if need_q:
+            ctx.save_for_backward(Whg, s_src, s_dst, out, lse, q)
         ctx.g, ctx.K, ctx.Fh, ctx.lowp = g, K, Fh, lowp
         return out
 
@@ -152,8 +156,11 @@ class _HaloGAT(torch.autograd.Function):
         ctx.g, ctx.K, ctx.Fh, ctx.lowp, ctx.halo = g, K, Fh, lowp, halo
         s_dst = s_dst.contiguous()
         if Wh.is_cuda:
-            out, lse, q = _gat_forward_kernels(Wh_ext, s_ext, s_dst, g, K, Fh, wdt == torch.bfloat16)
-            ctx.save_for_backward(Wh_ext, s_ext, s_dst, out, lse, q)
+            need_q = any(ctx.needs_input_grad[:3])
+            out, lse, q = _gat_forward_kernels(Wh_ext, s_ext, s_dst, g, K, Fh, wdt == torch.bfloat16,
+                                               need_q=need_q)
+            if need_q:
+                ctx.save_for_backward(Wh_ext, s_ext, s_dst, out, lse, q)
             return out
         ctx.save_for_backward(Wh_ext, s_ext, s_dst)
         return _gat_aggregate_torch(Wh_ext, s_ext, s_dst, g, K, Fh)

@@ -293,6 +293,10 @@ class GCNTrainer:
                           ops.fused_bwd_supported(self.F, hidden, self.C))
         self._gpart = None
         self._grad_index = None
+        # the training forward's dropout masks as the fused backward reads them (1 bit per
+        # element: 78 MB for ogbn-products): the backward draws no Philox of its own
+        self._kimg = (ops.keep_image(self.nloc, hidden, dev)
+                      if self.fused_bwd and self.p > 0 else None)
         # capture=True (one GPU, fully fused path): the whole epoch (9 kernels + Adam) is
         # captured into a hipGraph and replayed; the dropout step is read from the device
         # step counter (Adam's), so replays draw the current epoch's mask.  Off by default:
@@ -498,7 +502,8 @@ class GCNTrainer:
             self.W2b[:, :C] = self.W2.to(torch.bfloat16)
         if not (self.fused and ops.dense_fwd(self.AX, self.W1, self.b1, self.W2, self.dinv,
                                              None if self.fused_bwd else H1,
-                                             self.Z2loc[:n], F, p, self.key, self._dropout_step(), self.r0)):
+                                             self.Z2loc[:n], F, p, self.key, self._dropout_step(), self.r0,
+                                             kimg=self._kimg if train else None)):
             W1b = self.W1.to(torch.bfloat16)
             if self.AX.is_cuda:
                 torch.mm(self.AX[:n, :F], W1b, out=H1)
@@ -560,7 +565,8 @@ class GCNTrainer:
                     F, self.hidden, C, ops.fused_bwd_width(F), device=self.dev)
             _, _, _, self._gpart = ops.fused_bwd(self.AX, self.dY2, self.W1, self.b1, self.W2, n, F,
                                                  self.p, self.key, self._dropout_step(), self.r0,
-                                                 self._gpart, grads=self.grads, grad_index=self._grad_index)
+                                                 self._gpart, grads=self.grads, grad_index=self._grad_index,
+                                                 kimg=self._kimg)
             if self.multi:
                 torch.distributed.all_reduce(self.grads)
             return

@@ -416,10 +416,28 @@ def _step_value(step):
     return int(step.item()) if isinstance(step, torch.Tensor) else int(step)
 
 
-def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step, row0=0):
+def keep_image(n, hidden, device):
+    """Buffer of a keep image (the dropout masks of an n-row, ``hidden``-wide GCN layer as
+    the fused backward reads them: 1 bit per element, whole 32-row tiles)."""
+    hw = native.hip().gnn_keep_image_halfwords(int(n), int(hidden))
+    return torch.empty(hw, dtype=torch.int16, device=device)
+
+
+def draw_keep_image(kimg, n, hidden, p, key, step, row0=0):
+    """Fill ``kimg`` with the masks dense_fwd draws for the same (n, p, key, step, row0)."""
+    sv, sp = _step_args(step)
+    rc = native.hip().gnn_keep_image(kimg.data_ptr(), int(n), int(hidden), float(p), int(key[0]), int(key[1]), sv,
+                                     int(row0), _st(kimg), step_ptr=sp)
+    if rc != 0:
+        raise RuntimeError("gnn_keep_image failed (%d)" % rc)
+    return kimg
+
+
+def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step, row0=0, kimg=None):
     """H1 = dropout(relu(AX[:, :F] W1 + b1)), Z2 = dinv * (H1 W2) (fused MFMA kernel on GPU).
     ``H1=None`` (GPU only): H1 is not stored -- the fused backward recomputes it.
-    ``step``: the dropout step, an int or a device int32[1] tensor."""
+    ``step``: the dropout step, an int or a device int32[1] tensor.  ``kimg`` (GPU, a
+    ``keep_image`` buffer): also write the dropout masks for the fused backward."""
     n = Z2.shape[0]
     HD, C = W1.shape[1], W2.shape[1]
     if AX.is_cuda:
@@ -428,7 +446,8 @@ def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step, row0=0):
                                         dinv.data_ptr(), H1.data_ptr() if H1 is not None else 0,
                                         Z2.data_ptr(), n, F, AX.shape[1],
                                         HD, C, Z2.shape[1], float(p), int(key[0]), int(key[1]), sv,
-                                        int(row0), _st(AX), step_ptr=sp)
+                                        int(row0), _st(AX), step_ptr=sp,
+                                        kimg=kimg.data_ptr() if kimg is not None else 0)
         if rc == 0:
             return True
         if rc != -1:
@@ -465,9 +484,12 @@ def fused_bwd_supported(F, hidden, C):
     return bool(native.hip().gnn_fused_bwd_supported(int(F) + 1, int(hidden), int(C)))
 
 
-def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None, grads=None, grad_index=None):
+def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None, grads=None, grad_index=None,
+              kimg=None):
     """Fused GCN dense backward (GPU): recomputes H1 from AX, then
     dP1 = (dY2 W2^T) * [H1 > 0] / (1-p) and the weight gradients in one pass.
+    The dropout masks come from ``kimg``, the keep image the forward wrote
+    (``dense_fwd(..., kimg=)``); without one they are drawn here from (key, step, row0).
     Returns (gW1 [F, HD], gb1 [HD], gW2 [HD, C], gpart); with ``grads`` (the flat fp32
     gradient buffer, gW1 | gb1 | gW2 at its start) the sums are written there instead
     and (None, None, None, gpart) is returned."""
@@ -477,10 +499,11 @@ def fused_bwd(AX, dY2, W1, b1, W2, n, F, p, key, step, row0=0, gpart=None, grads
     nb, width = hip.gnn_fused_bwd_blocks(n), hip.gnn_fused_bwd_width(F + 1)
     if gpart is None or gpart.shape != (nb, HD, width):
         gpart = torch.empty(nb, HD, width, dtype=torch.float32, device=AX.device)
-    sv, sp = _step_args(step)
+    if p > 0 and kimg is None:
+        kimg = draw_keep_image(keep_image(n, HD, AX.device), n, HD, p, key, step, row0)
     rc = hip.gnn_fused_bwd(AX.data_ptr(), dY2.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
-                           gpart.data_ptr(), n, F, ldx, HD, C, dY2.shape[1], float(p), int(key[0]), int(key[1]),
-                           sv, int(row0), _st(AX), step_ptr=sp)
+                           kimg.data_ptr() if kimg is not None else 0, gpart.data_ptr(), n, F, ldx, HD, C,
+                           dY2.shape[1], float(p), _st(AX))
     if rc != 0:
         raise RuntimeError("gnn_fused_bwd failed (%d)" % rc)
     if grads is not None:

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 4: keep image from the forward (no Philox in the fused backward), packed bf16
+# backward epilogue, hoisted next-tile loads in the forward -- GNN GPU tests, headline
+# bench, kernel trace of the headline epoch
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r04_dense1
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gnn_gpu.py -x -q --timeout 200 --timeout-method thread > $O/pytest_gnn.log 2>&1 \
+    || { echo "tests failed"; grep -E "FAILED|Error|assert" $O/pytest_gnn.log | head -20; tail -n 30 $O/pytest_gnn.log; exit 1; }
+echo "$(tail -n 1 $O/pytest_gnn.log)"
+timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 > $O/bench.log 2>&1 || { echo bench failed; tail $O/bench.log; exit 1; }
+tail -n 1 $O/bench.log | cut -c1-160
+python3 -c "import json;d=json.loads(open('$O/bench.log').read().strip().splitlines()[-1]);print('val_acc',d['val_acc'],'loss',d['train_loss'])"
+B="python3 -u bench.py --steps 6 --warmup 2"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- $B > $O/prof.log 2>&1 || { echo prof failed; tail $O/prof.log; exit 1; }
+python3 - <<'PY'
+import csv, glob
+f = glob.glob("gpurun_out/r04_dense1/prof/**/*kernel_stats.csv", recursive=True)
+for r in list(csv.DictReader(open(f[0])))[:14]:
+    print(r["Name"][:60], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us", round(float(r["Percentage"]), 1))
+PY
+find $O -name "*_trace.csv" -delete
+echo done

@@ -412,3 +412,20 @@ def test_gcn_forced_collectives_one_rank_equals_plain(halo):
         assert ref.evaluate() == pytest.approx(forced.evaluate(), abs=2e-3)
     finally:
         dist.destroy_process_group()
+
+
+def _selftest_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from cgnn_amd.parallel.collectives import selftest
+    out[rank] = selftest("cpu")
+    dist.destroy_process_group()
+
+
+def test_collectives_selftest_gloo_two_ranks():
+    """bench.py gates every multi-rank run on collectives.selftest(): its gloo branch
+    (host tensors, list-form all_gather) passes on 2 ranks and reports the group."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_selftest_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        assert out[r]["backend"] == "gloo" and out[r]["world_size"] == 2, out[r]

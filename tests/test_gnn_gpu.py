@@ -248,6 +248,42 @@ def test_fused_backward_matches_reference(HD, p, row0, ldx, ldc):
         assert (got - ref).abs().mean().item() < 2e-3 * scale
 
 
+@pytest.mark.parametrize("p,HD,n", [(0.5, 256, 1000), (0.3, 256, 777), (0.5, 128, 70)])
+def test_forward_keep_image_matches_drawn_and_reference(p, HD, n):
+    """The keep image the fused forward writes for the backward (bit mode: from the
+    forward's own draw; byte mode: the side launch) equals the standalone draw, and its
+    bits are the reference dropout mask (ops.dropout_keep_mask) in the documented layout:
+    halfword (T * HD/32 + t) * 64 + 32 uh + r, bit 4 g + i <-> row 32 T + r, unit
+    32 t + 8 g + 4 uh + i."""
+    torch.manual_seed(1)
+    F, C = 100, 47
+    dev = "cuda:0"
+    AX = torch.zeros(n, 104, dtype=torch.bfloat16, device=dev)
+    AX[:, :F] = torch.randn(n, F, device=dev).to(torch.bfloat16)
+    AX[:, F] = 1
+    W1, b1, W2 = torch.randn(F, HD, device=dev) * 0.1, torch.zeros(HD, device=dev), torch.randn(HD, C, device=dev)
+    dinv = torch.ones(n, device=dev)
+    Z2 = torch.zeros(n, 48, dtype=torch.bfloat16, device=dev)
+    key, step, row0 = (31, 41), 5, 64
+    kf = ops.keep_image(n, HD, dev).fill_(0x5555)
+    assert ops.dense_fwd(AX, W1, b1, W2, dinv, None, Z2, F, p, key, step, row0, kimg=kf)
+    kd = ops.draw_keep_image(ops.keep_image(n, HD, dev), n, HD, p, key, step, row0)
+    assert torch.equal(kf, kd)
+    # decode against the reference mask
+    nt, NB = (n + 31) // 32, HD // 32
+    words = kd.cpu().view(nt, NB, 2, 32).to(torch.int32) & 0xffff          # [T][t][uh][r]
+    bits = (words[..., None] >> torch.arange(16)) & 1                        # [T][t][uh][r][q]
+    q = torch.arange(16)
+    g, i = q // 4, q % 4
+    keep = torch.zeros(nt * 32, HD, dtype=torch.bool)
+    for uh in range(2):
+        for t in range(NB):
+            units = 32 * t + 8 * g + 4 * uh + i
+            keep[:, units] = bits[:, t, uh].reshape(nt * 32, 16).bool()
+    ref = ops.dropout_keep_mask(n, HD, p, key, step, row0)
+    assert torch.equal(keep[:n], ref)
+
+
 def test_sage_aggregate_gpu_matches_cpu():
     from cgnn_amd.gnn.sage import Block, mean_aggregate
     g = synthetic("ogbn-arxiv", seed=1, scale=0.01)

@@ -167,3 +167,30 @@ def test_confounder_hill_climbing_speculation_keeps_the_sequential_result():
         assert spec.canonical_key() == seq.canonical_key()
         assert spec.search_score == seq.search_score
         assert spec.confounders == seq.confounders
+
+
+def test_fault_injection_keeps_job_ids_across_short_long_split(monkeypatch):
+    """A call mixing long-N jobs (sample-sharded trainer) and short ones (batched
+    engine) recurses on the short subset: CGNN_FAULT job numbers still address the
+    caller's jobs, and max_retries recovers them (the recursion re-indexed)."""
+    from cgnn_amd.engine.program import program_for_pair
+    from cgnn_amd.engine.scorer import Job, score_jobs
+    from cgnn_amd.utils.philox import model_key
+    rng = np.random.default_rng(0)
+
+    def job(N, k):
+        x = rng.standard_normal(N)
+        y = np.tanh(x) + 0.3 * rng.standard_normal(N)
+        return Job(program_for_pair(6), np.stack([x, y]).astype(np.float32), model_key(5, k))
+
+    jobs = [job(300, 0), job(40, 1), job(300, 2), job(40, 3)]     # long, short, long, short
+    cfg = SETTINGS.snapshot(train_epochs=3, test_epochs=2, h_layer_dim=6, gpu=False, long_n_min=100)
+    clean = score_jobs(jobs, cfg, max_retries=0)
+    assert np.all(np.isfinite(clean))
+    for bad in (3, 2):                               # a short job, then a long one
+        monkeypatch.setenv("CGNN_FAULT", "nan@job:%d" % bad)
+        s = score_jobs(jobs, cfg, max_retries=0)
+        assert np.isnan(s[bad]) and np.all(np.isfinite(np.delete(s, bad))), (bad, s)
+        np.testing.assert_array_equal(np.delete(s, bad), np.delete(clean, bad))
+        r = score_jobs(jobs, cfg, max_retries=1)
+        assert np.all(np.isfinite(r)), (bad, r)
