@@ -6,12 +6,23 @@ quantity each ``Parallel(...)(delayed(run_cgnn_function)(...))`` site of the
 reference computes for ONE graph (CGNN.py:214-217, CGNN_confounders.py:234-237).
 Here all candidates x runs are one device batch.
 
-Common random numbers: run r of every candidate uses the same Philox key and
-the same subsample, so score differences between candidates are not polluted
-by independent noise, and a candidate's score does not depend on which other
-candidates share its batch (speculative evaluation stays exact).
+Common random numbers (default): run r of every candidate uses the same Philox
+key and the same subsample, so score differences between candidates are not
+polluted by independent noise, and a candidate's score does not depend on which
+other candidates share its batch (speculative evaluation stays exact).
+``cfg.compat_scores``: every candidate draws runs of its own, as the reference
+does (each ``Parallel(...)`` call re-seeds, CGNN.py:237-238): keys and subsamples
+are keyed by the candidate's canonical edge set -- independent across candidates,
+still independent of the batch.
+
+User ``run_cgnn_function`` plug-ins (the reference's module-level TF functions) run
+one call per (candidate, run) on the host; ``cfg.nb_jobs`` > 1 spreads the calls over
+that many joblib worker processes, like the reference's ``Parallel(n_jobs=NB_JOBS)``
+(plug-ins must be picklable, module-level callables, as there).
 """
 from __future__ import annotations
+
+import hashlib
 
 from typing import Callable, Optional, Sequence
 
@@ -51,21 +62,39 @@ class GraphEvaluator:
             return self.cfg.complexity_graph_param * graph.number_of_edges()
         return 0.0
 
+    def candidate_salt(self, graph) -> int:
+        """Stable 64-bit identity of a candidate's edge set (compat_scores keys)."""
+        h = hashlib.blake2b(repr(graph.canonical_key()).encode(), digest_size=8).digest()
+        return int.from_bytes(h, "little")
+
+    def _runs(self, graph):
+        """(data, key) of every run of ``graph``: shared by all candidates, or the
+        candidate's own under compat_scores."""
+        if not self.cfg.compat_scores:
+            return list(zip(self.subs, self.keys))
+        c = self.candidate_salt(graph)
+        mat = np.asarray(self.data[self.nodes].values, dtype=np.float32)
+        return [(np.ascontiguousarray(subsample(mat, self.cfg.max_nb_points, self.cfg.seed, self.salt, c, run).T),
+                 model_key(self.cfg.seed, self.salt, c, run)) for run in range(self.cfg.nb_runs)]
+
     def run_scores(self, graphs: Sequence) -> np.ndarray:
         """[len(graphs), nb_runs] raw per-run scores."""
         R = self.cfg.nb_runs
         if self.legacy_fn is not None:
-            out = np.zeros((len(graphs), R))
-            for g, graph in enumerate(graphs):
-                for run in range(R):
-                    out[g, run] = self.legacy_fn(self.data, graph, self.n_evaluated + g, run,
-                                                 **self.legacy_kwargs)
-            return out
+            calls = [(self.n_evaluated + g, graph, run) for g, graph in enumerate(graphs) for run in range(R)]
+            if self.cfg.nb_jobs > 1:
+                from joblib import Parallel, delayed
+                vals = Parallel(n_jobs=self.cfg.nb_jobs)(
+                    delayed(self.legacy_fn)(self.data, graph, idx, run, **self.legacy_kwargs)
+                    for idx, graph, run in calls)
+            else:
+                vals = [self.legacy_fn(self.data, graph, idx, run, **self.legacy_kwargs) for idx, graph, run in calls]
+            return np.asarray(vals, dtype=np.float64).reshape(len(graphs), R)
         jobs = []
         for graph in graphs:
             prog = self.program(graph)
-            for run in range(R):
-                jobs.append(Job(prog, self.subs[run], self.keys[run]))
+            for data, key in self._runs(graph):
+                jobs.append(Job(prog, data, key))
         return score_jobs(jobs, self.cfg).reshape(len(graphs), R)
 
     def __call__(self, graphs: Sequence) -> np.ndarray:

@@ -38,9 +38,14 @@ def pair_jobs(a, b, idx, cfg, salt="gnn") -> List[Job]:
     return jobs
 
 
-def pair_score(run_scores: np.ndarray) -> tuple:
-    ab = finite_mean(run_scores[0::2])
-    ba = finite_mean(run_scores[1::2])
+def pair_score(run_scores: np.ndarray, compat: bool = False) -> tuple:
+    """(score A->B, score B->A, (BA - AB) / (BA + AB)).  Default: the mean of the finite
+    runs (the reference's graph scores filter with np.isfinite, CGNN.py:217).
+    ``compat`` (``SETTINGS.compat_scores``): the reference's pairwise mean over every
+    run, a non-finite one propagating (GNN.py:196-197)."""
+    mean = (lambda v: float(np.mean(v))) if compat else finite_mean
+    ab = mean(run_scores[0::2])
+    ba = mean(run_scores[1::2])
     return ab, ba, (ba - ab) / (ba + ab)
 
 
@@ -71,7 +76,7 @@ class GNN(Pairwise_Model):
             scores = score_jobs(jobs, cfg)
         out, self.last_run_scores = [], []
         for s, e in spans:
-            ab, ba, p = pair_score(scores[s:e])
+            ab, ba, p = pair_score(scores[s:e], cfg.compat_scores)
             self.last_run_scores.append((scores[s:e:2].copy(), scores[s + 1:e:2].copy()))
             if cfg.verbose:
                 print("score A->B %.6g  B->A %.6g  -> %.4f" % (ab, ba, p))

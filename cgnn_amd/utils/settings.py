@@ -17,6 +17,14 @@ New (not in the reference):
                                 dropped (0 = the reference's drop-only behaviour;
                                 the reference re-runs only its polynomial generator,
                                 generators.py:165-178)
+  * ``compat_scores``        -- reference scoring statistics (default False):
+                                the pairwise score averages ALL runs, a non-finite
+                                one included (GNN.py:196-197, no np.isfinite
+                                filter), and every HC candidate is scored by runs of
+                                its own (Philox keys and subsamples keyed by the
+                                candidate's edge set -- the reference re-draws per
+                                candidate, CGNN.py:237-238) instead of the common
+                                random numbers shared by all candidates
   * ``long_n_min``           -- runs with MORE samples than this (possible once
                                 ``max_nb_points`` is raised, or ``None`` = no
                                 subsampling) train on the sample-sharded long-N
@@ -60,7 +68,8 @@ class DefaultSettings(object):
                  "batch_models",
                  "verbose",
                  "max_retries",
-                 "long_n_min")
+                 "long_n_min",
+                 "compat_scores")
 
     def __init__(self):
         self.NB_RUNS = 32
@@ -88,6 +97,7 @@ class DefaultSettings(object):
         self.verbose = False
         self.max_retries = 0
         self.long_n_min = 1500
+        self.compat_scores = False
         self._apply_env()
 
     def _apply_env(self):
@@ -141,6 +151,7 @@ class DefaultSettings(object):
             verbose=bool(g("verbose", self.verbose)),
             max_retries=int(g("max_retries", self.max_retries)),
             long_n_min=int(g("long_n_min", self.long_n_min)),
+            compat_scores=bool(g("compat_scores", self.compat_scores)),
         )
 
     def __repr__(self):
@@ -184,6 +195,7 @@ class RunConfig:
     verbose: bool = False
     max_retries: int = 0
     long_n_min: int = 1500
+    compat_scores: bool = False
 
     def replace(self, **kw) -> "RunConfig":
         return dataclasses.replace(self, **kw)

@@ -62,8 +62,8 @@ def run_confounders():
     data = pd.read_csv(example("Example_graph_confounders_numdata.csv"))
     umg = cgnn.UndirectedGraph(pd.read_csv(example("Example_graph_confounders_skeleton.csv")))
     target = cgnn.DirectedGraph(pd.read_csv(example("Example_graph_confounders_target.csv")))
-    pdg = cgnn.GNN().orient_graph_confounders(data, umg, nb_runs=16)
-    dag = cgnn.CGNN_confounders().orient_directed_graph(data, pdg, nb_runs=16)
+    pdg = cgnn.GNN().orient_graph_confounders(data, umg)
+    dag = cgnn.CGNN_confounders().orient_directed_graph(data, pdg)
     return dag, target
 
 
@@ -95,7 +95,7 @@ def test_confounders_example_recovers_edges():
     dag, target = run_confounders()
     assert not dag.is_cyclic()
     sc = orientation_scores(dag, target)
-    assert sc["precision"] >= 0.8 and sc["recall"] >= 0.85, sc   # measured (16 runs): 0.82 / 0.86
+    assert sc["precision"] >= 0.8 and sc["recall"] >= 0.85, sc   # measured (32 runs): 0.818 / 0.857
     pin = _pinned()
     if pin is not None:
         assert sorted([a, b] for a, b, _ in dag.get_list_edges()) == pin["confounders"]["edges"]

@@ -225,3 +225,68 @@ def test_reference_example_files_load():
     assert not target.is_cyclic()
     data = pd.read_csv(example("Example_graph_numdata.csv"))
     assert data.shape == (500, 22)
+
+
+def test_compat_scores_pairwise_mean_and_candidate_keys():
+    """SETTINGS.compat_scores: (1) the pairwise score averages every run, a non-finite
+    one propagating (GNN.py:196-197) -- the default drops it; (2) HC candidates draw
+    runs of their own (keys / subsamples keyed by the edge set), while the default
+    shares run r's key across candidates (common random numbers)."""
+    import numpy as np
+    import pandas as pd
+    from cgnn_amd.engine.evaluator import GraphEvaluator
+    from cgnn_amd.models.gnn import pair_score
+    from cgnn_amd.utils.graph import DirectedGraph
+    from cgnn_amd.utils.settings import SETTINGS
+    s = np.array([1.0, 2.0, np.nan, 2.5, 1.0, 2.0])
+    ab, ba, p = pair_score(s)
+    assert ab == 1.0 and ba == pytest.approx(13 / 6) and np.isfinite(p)
+    ab, ba, p = pair_score(s, compat=True)
+    assert np.isnan(ab) and np.isnan(p)
+    rng = np.random.default_rng(0)
+    df = pd.DataFrame(rng.standard_normal((40, 3)), columns=["A", "B", "C"])
+    g1, g2 = DirectedGraph(), DirectedGraph()
+    g1.add("A", "B")
+    g1.add("B", "C")
+    g2.add("B", "A")
+    g2.add("B", "C")
+    nodes = ["A", "B", "C"]
+    ev = GraphEvaluator(df, SETTINGS.snapshot(nb_runs=3, gpu=False), nodes=nodes)
+    assert [k for _, k in ev._runs(g1)] == [k for _, k in ev._runs(g2)]
+    evc = GraphEvaluator(df, SETTINGS.snapshot(nb_runs=3, gpu=False, compat_scores=True), nodes=nodes)
+    k1, k2 = [k for _, k in evc._runs(g1)], [k for _, k in evc._runs(g2)]
+    assert len(set(k1 + k2)) == 6                     # every (candidate, run) its own stream
+    assert k1 == [k for _, k in evc._runs(g1.copy())]  # a pure function of the edge set
+    tiny = dict(train_epochs=3, test_epochs=2, h_layer_dim=5)
+    evc = GraphEvaluator(df, SETTINGS.snapshot(nb_runs=2, gpu=False, compat_scores=True, **tiny), nodes=nodes)
+    a = evc.run_scores([g1, g2])
+    b = evc.run_scores([g2, g1])                      # batch position does not matter
+    np.testing.assert_array_equal(a, b[::-1])
+    assert not np.array_equal(a[0], a[1])
+
+
+def _plugin(data, graph, idx, run, **kwargs):
+    """A deterministic, picklable run_cgnn_function plug-in."""
+    return float(idx) * 10.0 + run + 0.5 * len(graph.get_list_edges())
+
+
+def test_plugin_nb_jobs_matches_sequential():
+    """User run_cgnn_function plug-ins go through a joblib pool with nb_jobs > 1 (the
+    reference's Parallel(n_jobs=NB_JOBS)); the scores equal the one-process loop."""
+    import numpy as np
+    import pandas as pd
+    from cgnn_amd.engine.evaluator import GraphEvaluator
+    from cgnn_amd.utils.graph import DirectedGraph
+    from cgnn_amd.utils.settings import SETTINGS
+    df = pd.DataFrame(np.zeros((5, 2)), columns=["A", "B"])
+    g = DirectedGraph()
+    g.add("A", "B")
+    h = DirectedGraph()
+    h.add("B", "A")
+    out = []
+    for jobs in (1, 4):
+        ev = GraphEvaluator(df, SETTINGS.snapshot(nb_runs=3, nb_jobs=jobs, gpu=False), nodes=["A", "B"],
+                            legacy_fn=_plugin)
+        out.append(ev.run_scores([g, h, g]))
+    np.testing.assert_array_equal(out[0], out[1])
+    assert out[0][2, 1] == 21.5

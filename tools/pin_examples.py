@@ -2,6 +2,7 @@
 gates of tests/test_examples_gpu.py) at the gates' fixed settings, as JSON.
 
     python tools/pin_examples.py tests/data/expected_examples.json
+    python tools/pin_examples.py --compat compat_examples.json     (SETTINGS.compat_scores)
 
 Scores are deterministic on a given device and kernel build (counter-based RNG,
 fixed-order reductions, bitwise independent of batching), so the gates compare the
@@ -17,7 +18,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else "expected_examples.json"
+    args = [a for a in sys.argv[1:] if a != "--compat"]
+    compat = "--compat" in sys.argv[1:]
+    out = args[0] if args else "expected_examples.json"
     import pandas as pd
     import cgnn
     from conftest import example
@@ -26,6 +29,7 @@ def main():
     from test_examples_gpu import REFERENCE_SETTINGS, run_confounders, run_graph, run_pairwise
     for k, v in REFERENCE_SETTINGS.items():
         setattr(cgnn.SETTINGS, k, v)
+    cgnn.SETTINGS.compat_scores = compat
     wall = {}
     t0 = time.perf_counter()
     pred, targets = run_pairwise()
@@ -37,6 +41,7 @@ def main():
     cdag, ctarget = run_confounders()
     wall["confounders"] = time.perf_counter() - t0
     rec = {
+        "settings": dict(REFERENCE_SETTINGS, compat_scores=compat),
         "pairwise": {"signs": [int(x > 0) - int(x < 0) for x in pred], "predictions": [float(x) for x in pred],
                      "sign_accuracy": float(sign_accuracy(pred, targets))},
         "graph": {"edges": sorted([a, b] for a, b, _ in dag.get_list_edges()), "shd": int(shd(dag, target))},
