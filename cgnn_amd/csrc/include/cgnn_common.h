@@ -16,6 +16,16 @@
 
 namespace cgnn {
 
+// ---------------------------------------------------------------- DAG programs
+// int32 model description (engine/program.py): header, node records, index pool
+constexpr int PROG_HDR = 4;      // n_nodes, n_params, n_conf, max_in
+constexpr int NODE_REC = 8;      // var, kind, n_par, par_off, n_cf, cf_off, param_off, n_in
+constexpr int KIND_GEN = 0;
+constexpr int KIND_OBS = 1;
+
+// wave-uniform load: the value lands in an SGPR (program words, stage tables)
+__device__ __forceinline__ int uni(const int* p) { return __builtin_amdgcn_readfirstlane(*p); }
+
 // ---------------------------------------------------------------- Philox
 struct u32x4 { uint32_t x, y, z, w; };
 

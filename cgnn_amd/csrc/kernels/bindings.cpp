@@ -18,7 +18,7 @@ int cgnn_mmd_supported_d(int);
 int cgnn_mmd_mfma_supported(int);
 int cgnn_mmd_mfma_row_blocks(int);
 int cgnn_launch_mmd_mfma_rows(int, int, const float*, const float*, const float*, const float*, float*, float*,
-                              int, int, int, int, float, int, int, hipStream_t);
+                              int, int, int, int, float, int, int, hipStream_t, int);
 int cgnn_gen_supported_h(int);
 int cgnn_gen_bwd_blocks(int);
 size_t cgnn_gen_bwd_lds(int, int, int, int);
@@ -32,9 +32,17 @@ int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t, int);
 int cgnn_gen_bwd_variant(int, int, int, int);
 size_t cgnn_gen_fwd_lds(int, int);
-size_t cgnn_gen_bwd_generic_lds(int, int);
+int cgnn_staged_plan(int, int, int, int, int*);
+int cgnn_staged_tiles(int);
+int cgnn_launch_gen_noise(const int*, int, const uint32_t*, const int*, int, float*, int, int, int, int, int, int,
+                          hipStream_t);
+int cgnn_launch_gen_fwd_staged(const int*, int, const int*, int, const float*, int, const float*, float*,
+                               const float*, int, float*, int, int, int, int, int, int, hipStream_t, int);
+int cgnn_launch_gen_bwd_staged(const int*, int, const int*, int, const float*, int, const float*, const float*, int,
+                               const float*, int, int, int, int, int, int, int, int, float*, float*, hipStream_t,
+                               int);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
-                        const float*, int, int, int, int, int, int, int, float*, hipStream_t, float*);
+                        const float*, int, int, int, int, int, int, int, float*, hipStream_t);
 int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
                      int, float, float, float, float, int, hipStream_t);
 int cgnn_launch_init(float*, float*, float*, const int*, int, int, const uint32_t*, float, int,
@@ -126,7 +134,7 @@ static void chk(int rc, const char* what) {
 class PyEngine {
  public:
   PyEngine(std::vector<int> icfg, std::vector<float> fcfg, std::vector<uint64_t> ptrs, uint64_t stream) {
-    if (icfg.size() < 18 || fcfg.size() < 5 || ptrs.size() < 21) throw std::invalid_argument("engine config size");
+    if (icfg.size() < 21 || fcfg.size() < 5 || ptrs.size() < 22) throw std::invalid_argument("engine config size");
     std::vector<const void*> p(ptrs.size());
     for (size_t k = 0; k < ptrs.size(); ++k) p[k] = reinterpret_cast<const void*>(ptrs[k]);
     h_ = cgnn_engine_create(icfg.data(), fcfg.data(), p.data(), S(stream));
@@ -150,19 +158,51 @@ PYBIND11_MODULE(_hip, m) {
   m.def("mmd_mfma_row_blocks", &cgnn_mmd_mfma_row_blocks);
   m.def("mmd_mfma", [](int mode, int D, uint64_t xhat, uint64_t data, uint64_t xn, uint64_t yn, uint64_t gp,
                        uint64_t lp, int N, int R, int n_chunks, int tpc, float gscale, uint64_t st,
-                       int row_begin, int n_rows) {
+                       int row_begin, int n_rows, int wide) {
     chk(cgnn_launch_mmd_mfma_rows(mode, D, Pt<const float>(xhat), Pt<const float>(data), Pt<const float>(xn),
                                   Pt<const float>(yn), Pt<float>(gp), Pt<float>(lp), N, R, n_chunks, tpc, gscale,
-                                  row_begin, n_rows < 0 ? N : n_rows, S(st)), "mmd_mfma");
+                                  row_begin, n_rows < 0 ? N : n_rows, S(st), wide), "mmd_mfma");
   }, py::arg("mode"), py::arg("D"), py::arg("xhat"), py::arg("data"), py::arg("xn"), py::arg("yn"), py::arg("gp"),
      py::arg("lp"), py::arg("N"), py::arg("R"), py::arg("n_chunks"), py::arg("tpc"), py::arg("gscale"),
-     py::arg("st"), py::arg("row_begin") = 0, py::arg("n_rows") = -1);
+     py::arg("st"), py::arg("row_begin") = 0, py::arg("n_rows") = -1, py::arg("wide") = -1);
   m.def("gen_supported_h", &cgnn_gen_supported_h);
   m.def("gen_bwd_blocks", &cgnn_gen_bwd_blocks);
   m.def("gen_bwd_lds", &cgnn_gen_bwd_lds);
   m.def("gen_bwd_variant", &cgnn_gen_bwd_variant);
   m.def("gen_fwd_lds", &cgnn_gen_fwd_lds);
-  m.def("gen_bwd_generic_lds", &cgnn_gen_bwd_generic_lds);
+  // level-scheduled (wide-graph) generator kernels, cgnn_staged.hip
+  m.def("staged_plan", [](int Dt, int H, int max_in, int W) -> py::tuple {
+    int out[5];
+    if (cgnn_staged_plan(Dt, H, max_in, W, out) != 0) return py::tuple();
+    return py::make_tuple(out[0], out[1], out[2], out[3], out[4]);
+  }, py::arg("Dt"), py::arg("H"), py::arg("max_in"), py::arg("W"));
+  m.def("staged_tiles", &cgnn_staged_tiles);
+  m.def("gen_noise", [](uint64_t prog, int ps, uint64_t keys, uint64_t step, int off, uint64_t noise, int NS, int N,
+                        int D, int Dt, int R, int row0, uint64_t st) {
+    chk(cgnn_launch_gen_noise(Pt<const int>(prog), ps, Pt<const uint32_t>(keys), Pt<const int>(step), off,
+                              Pt<float>(noise), NS, N, D, Dt, R, row0, S(st)), "gen_noise");
+  }, py::arg("prog"), py::arg("ps"), py::arg("keys"), py::arg("step"), py::arg("off"), py::arg("noise"),
+     py::arg("NS"), py::arg("N"), py::arg("D"), py::arg("Dt"), py::arg("R"), py::arg("row0"), py::arg("st"));
+  m.def("gen_fwd_staged", [](uint64_t prog, int ps, uint64_t sched, int ss, uint64_t params, int P, uint64_t data,
+                             uint64_t xhat, uint64_t noise, int NS, uint64_t xnorm, int N, int D, int Dt, int H,
+                             int R, int W, uint64_t st, int force) {
+    chk(cgnn_launch_gen_fwd_staged(Pt<const int>(prog), ps, Pt<const int>(sched), ss, Pt<const float>(params), P,
+                                   Pt<const float>(data), Pt<float>(xhat), Pt<const float>(noise), NS,
+                                   Pt<float>(xnorm), N, D, Dt, H, R, W, S(st), force), "gen_fwd_staged");
+  }, py::arg("prog"), py::arg("ps"), py::arg("sched"), py::arg("ss"), py::arg("params"), py::arg("P"),
+     py::arg("data"), py::arg("xhat"), py::arg("noise"), py::arg("NS"), py::arg("xnorm"), py::arg("N"), py::arg("D"),
+     py::arg("Dt"), py::arg("H"), py::arg("R"), py::arg("W"), py::arg("st"), py::arg("force") = -1);
+  m.def("gen_bwd_staged", [](uint64_t prog, int ps, uint64_t sched, int ss, uint64_t params, int P, uint64_t xhat,
+                             uint64_t noise, int NS, uint64_t gradp, int nch, int R, int N, int D, int Dt, int H,
+                             int max_in, int W, uint64_t gpart, uint64_t dxs, uint64_t st, int force) {
+    chk(cgnn_launch_gen_bwd_staged(Pt<const int>(prog), ps, Pt<const int>(sched), ss, Pt<const float>(params), P,
+                                   Pt<const float>(xhat), Pt<const float>(noise), NS, Pt<const float>(gradp), nch,
+                                   R, N, D, Dt, H, max_in, W, Pt<float>(gpart), Pt<float>(dxs), S(st), force),
+        "gen_bwd_staged");
+  }, py::arg("prog"), py::arg("ps"), py::arg("sched"), py::arg("ss"), py::arg("params"), py::arg("P"),
+     py::arg("xhat"), py::arg("noise"), py::arg("NS"), py::arg("gradp"), py::arg("nch"), py::arg("R"), py::arg("N"),
+     py::arg("D"), py::arg("Dt"), py::arg("H"), py::arg("max_in"), py::arg("W"), py::arg("gpart"), py::arg("dxs"),
+     py::arg("st"), py::arg("force") = -1);
   m.def("read_stamps", []() {
     unsigned long long v[16] = {0};
     const int rc = cgnn_read_stamps(v);
@@ -202,13 +242,13 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("N"), py::arg("D"), py::arg("H"), py::arg("R"), py::arg("st"), py::arg("row0") = 0);
   m.def("gen_bwd", [](uint64_t prog, int ps, uint64_t params, int P, uint64_t xhat, uint64_t noise, int NS,
                       uint64_t gradp, int nch, int R, int N, int D, int Dt, int H, int max_in, uint64_t gpart,
-                      uint64_t st, uint64_t dxs) {
+                      uint64_t st) {
     chk(cgnn_launch_gen_bwd(Pt<const int>(prog), ps, Pt<const float>(params), P, Pt<const float>(xhat),
                             Pt<const float>(noise), NS, Pt<const float>(gradp), nch, R, N, D, Dt, H, max_in,
-                            Pt<float>(gpart), S(st), Pt<float>(dxs)), "gen_bwd");
+                            Pt<float>(gpart), S(st)), "gen_bwd");
   }, py::arg("prog"), py::arg("ps"), py::arg("params"), py::arg("P"), py::arg("xhat"), py::arg("noise"),
      py::arg("NS"), py::arg("gradp"), py::arg("nch"), py::arg("R"), py::arg("N"), py::arg("D"), py::arg("Dt"),
-     py::arg("H"), py::arg("max_in"), py::arg("gpart"), py::arg("st"), py::arg("dxs") = 0);
+     py::arg("H"), py::arg("max_in"), py::arg("gpart"), py::arg("st"));
   m.def("adam", [](uint64_t params, uint64_t mm, uint64_t vv, uint64_t gpart, int G, uint64_t prog, int ps, int P,
                    uint64_t step, int off, float lr, float b1, float b2, float eps, int R, uint64_t st) {
     chk(cgnn_launch_adam(Pt<float>(params), Pt<float>(mm), Pt<float>(vv), Pt<const float>(gpart), G,

@@ -3,6 +3,7 @@
 //
 //   train step : gen_fwd -> mmd(train) -> loss_finalize -> gen_bwd -> adam
 //   eval step  : gen_fwd -> mmd(eval)  -> loss_finalize(accumulate)
+// (wide graphs: gen_fwd = gen_noise + gen_fwd_staged, gen_bwd = gen_bwd_staged)
 //
 // A chunk of `chunk` steps (step offsets baked in as literals) plus one
 // advance_step node is captured once per (kind, chunk) and replayed; the RNG
@@ -28,7 +29,15 @@ int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, 
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t, int);
 int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const float*, int,
-                        const float*, int, int, int, int, int, int, int, float*, hipStream_t, float*);
+                        const float*, int, int, int, int, int, int, int, float*, hipStream_t);
+int cgnn_staged_tiles(int);
+int cgnn_launch_gen_noise(const int*, int, const uint32_t*, const int*, int, float*, int, int, int, int, int, int,
+                          hipStream_t);
+int cgnn_launch_gen_fwd_staged(const int*, int, const int*, int, const float*, int, const float*, float*,
+                               const float*, int, float*, int, int, int, int, int, int, hipStream_t, int);
+int cgnn_launch_gen_bwd_staged(const int*, int, const int*, int, const float*, int, const float*, const float*, int,
+                               const float*, int, int, int, int, int, int, int, int, float*, float*, hipStream_t,
+                               int);
 int cgnn_mmd_supported_d(int);
 int cgnn_gen_bwd_blocks(int);
 int cgnn_launch_adam(float*, float*, float*, const float*, int, const int*, int, int, const int*,
@@ -54,6 +63,8 @@ struct EngineConfig {
   int mfma = 0;      // 1: train/eval MMD on the matrix cores (mmd_mfma.hip), D >= 8
   int mf_chunks = 1, mf_tpc = 0;   // its column chunking (32-wide tiles per chunk)
   int mirror = 0;    // > 0: symmetric vector-kernel training, `mirror` extra gradient slots
+  int staged = 0;    // 1: level-scheduled generator kernels (wide graphs, cgnn_staged.hip)
+  int sched_stride = 0, stage_w = 8;
 };
 
 struct EngineBuffers {
@@ -77,13 +88,14 @@ struct EngineBuffers {
   float* rff_diff = nullptr;    // [R][7k]
   float* xnorm = nullptr;       // [R][N] squared norms of xhat rows (written by gen_fwd)
   const float* ynorm = nullptr; // [R][N] squared norms of the data rows
-  float* dxs = nullptr;         // [R][d_true][N] sample-gradient scratch of the generic-width backward
+  float* dxs = nullptr;         // [R][d_true][N] dL/dx scratch of a staged backward whose state is global
+  const int* sched = nullptr;   // [R][sched_stride] stage schedules (staged kernels)
 };
 
 class Engine {
  public:
   Engine(const EngineConfig& c, const EngineBuffers& b, hipStream_t s) : c_(c), b_(b), st_(s) {
-    G_ = cgnn_gen_bwd_blocks(c_.N);
+    G_ = c_.staged ? cgnn_staged_tiles(c_.N) : cgnn_gen_bwd_blocks(c_.N);
   }
   ~Engine() { clear_graphs(); }
 
@@ -157,26 +169,42 @@ class Engine {
                                     nullptr, 0, b_.step, 0, c_.R, st_), "finalize(tt)");
   }
 
+  void enqueue_gen_fwd(int off) {
+    if (c_.staged) {
+      check(cgnn_launch_gen_noise(b_.prog, c_.prog_stride, b_.keys, b_.step, off, b_.noise, c_.NS, c_.N, c_.D,
+                                  c_.d_true, c_.R, 0, st_), "gen_noise");
+      check(cgnn_launch_gen_fwd_staged(b_.prog, c_.prog_stride, b_.sched, c_.sched_stride, b_.params, c_.P, b_.data,
+                                       b_.xhat, b_.noise, c_.NS, b_.xnorm, c_.N, c_.D, c_.d_true, c_.H, c_.R,
+                                       c_.stage_w, st_, -1), "gen_fwd_staged");
+    } else {
+      check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
+                                b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_, 0), "gen_fwd");
+    }
+  }
+
   void enqueue_train_step(int off, bool record_hist) {
     const float inv = loss_scale();
-    check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
-                              b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_, 0), "gen_fwd");
+    enqueue_gen_fwd(off);
     enqueue_loss(off, true, record_hist);
     // the training loss is only observable through the recorded history
     if (record_hist)
       check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 0,
                                       b_.loss_hist, c_.hist_stride, b_.step, off, c_.R, st_), "finalize");
-    check(cgnn_launch_gen_bwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.xhat, b_.noise, c_.NS, b_.gradp,
-                              grad_chunks(), c_.R, c_.N, c_.D, c_.d_true, c_.H, c_.max_in, b_.gpart, st_, b_.dxs),
-          "gen_bwd");
+    if (c_.staged)
+      check(cgnn_launch_gen_bwd_staged(b_.prog, c_.prog_stride, b_.sched, c_.sched_stride, b_.params, c_.P, b_.xhat,
+                                       b_.noise, c_.NS, b_.gradp, grad_chunks(), c_.R, c_.N, c_.D, c_.d_true, c_.H,
+                                       c_.max_in, c_.stage_w, b_.gpart, b_.dxs, st_, -1), "gen_bwd_staged");
+    else
+      check(cgnn_launch_gen_bwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.xhat, b_.noise, c_.NS, b_.gradp,
+                                grad_chunks(), c_.R, c_.N, c_.D, c_.d_true, c_.H, c_.max_in, b_.gpart, st_),
+            "gen_bwd");
     check(cgnn_launch_adam(b_.params, b_.m, b_.v, b_.gpart, G_, b_.prog, c_.prog_stride, c_.P, b_.step,
                            off, c_.lr, c_.beta1, c_.beta2, c_.eps, c_.R, st_), "adam");
   }
 
   void enqueue_eval_step(int off) {
     const float inv = loss_scale();
-    check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
-                              b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_, 0), "gen_fwd");
+    enqueue_gen_fwd(off);
     enqueue_loss(off, false);
     check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 1,
                                     nullptr, 0, b_.step, off, c_.R, st_), "finalize(eval)");
@@ -244,6 +272,7 @@ extern "C" void* cgnn_engine_create(const int* icfg, const float* fcfg, const vo
   c.prog_stride = icfg[5]; c.max_in = icfg[6]; c.row_tiles = icfg[7]; c.n_chunks = icfg[8];
   c.tpc = icfg[9]; c.hist_stride = icfg[10]; c.rff_k = icfg[11]; c.d_true = icfg[12]; c.NS = icfg[13];
   c.mfma = icfg[14]; c.mf_chunks = icfg[15]; c.mf_tpc = icfg[16]; c.mirror = icfg[17];
+  c.staged = icfg[18]; c.sched_stride = icfg[19]; c.stage_w = icfg[20];
   c.lr = fcfg[0]; c.beta1 = fcfg[1]; c.beta2 = fcfg[2]; c.eps = fcfg[3]; c.init_std = fcfg[4];
   cgnn::EngineBuffers b;
   b.prog = (const int*)ptrs[0]; b.params = (float*)ptrs[1]; b.m = (float*)ptrs[2];
@@ -253,6 +282,7 @@ extern "C" void* cgnn_engine_create(const int* icfg, const float* fcfg, const vo
   b.loss_acc = (float*)ptrs[12]; b.loss_hist = (float*)ptrs[13]; b.step = (int*)ptrs[14];
   b.keys = (const uint32_t*)ptrs[15]; b.rff_w = (float*)ptrs[16]; b.rff_diff = (float*)ptrs[17];
   b.xnorm = (float*)ptrs[18]; b.ynorm = (const float*)ptrs[19]; b.dxs = (float*)ptrs[20];
+  b.sched = (const int*)ptrs[21];
   return new cgnn::Engine(c, b, st);
 }
 

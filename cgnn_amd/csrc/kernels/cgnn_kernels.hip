@@ -28,10 +28,6 @@ using namespace cgnn;
 
 namespace {
 
-constexpr int PROG_HDR = 4;      // n_nodes, n_params, n_conf, reserved
-constexpr int NODE_REC = 8;      // var, kind, n_par, par_off, n_cf, cf_off, param_off, n_in
-constexpr int KIND_GEN = 0;
-constexpr int KIND_OBS = 1;
 constexpr float MMD_SENTINEL = 1.0e17f;   // padded columns: exp(-g*d2) == 0 exactly
 
 }  // namespace
@@ -292,7 +288,6 @@ extern "C" int cgnn_read_stamps(unsigned long long* out) {
 }
 
 // wave-uniform read of an LDS-resident program word (lands in an SGPR)
-__device__ __forceinline__ int uni(const int* p) { return __builtin_amdgcn_readfirstlane(*p); }
 
 // ============================================================================
 // K1: generator forward.  grid = (ceil(N/256), R), one thread per sample.
@@ -596,157 +591,6 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
 }
 
 // ============================================================================
-// K2, any hidden width and any variable count (the reference builds one MLP per node
-// for any d and h_layer_dim, CGNN.py:63-90; its generator defaults to 200 variables).
-// Same block geometry, phases, summation orders and outputs as gen_bwd_kernel -- for a
-// compiled H the two are bitwise equal -- but:
-//   * H is a runtime value: the hidden pre-activations are produced one unit at a
-//     time from the LDS input row (no register arrays sized by H);
-//   * the sample state x / dL/dx stays in global memory ([R][Dt][N], each thread
-//     touching only its own sample, coalesced along n) instead of LDS, so the LDS
-//     footprint no longer grows with the number of variables.
-// ============================================================================
-template <int BS>
-__global__ __launch_bounds__(BS) void gen_bwd_generic_kernel(
-    const int* __restrict__ prog, int prog_stride, const float* __restrict__ params, int P,
-    const float* __restrict__ xhat, const float* __restrict__ noise, int NS,
-    const float* __restrict__ grad_part, int n_chunks, int R,
-    int N, int D, int Dt, int max_in, int H, float* __restrict__ dxs, float* __restrict__ gpart) {
-  static_assert(BS == 128, "two-wave reduction split assumes 128 samples per block");
-  const int HE = (H + 1) & ~1, HP = HE / 2;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int SI = (max_in + 2) | 1;
-  float* s_z = smem;                                   // [BS][HE]   mg rows
-  f2* s_red = reinterpret_cast<f2*>(s_z + BS * HE);    // [64]       wave-1 partials
-  f2* s_g = s_red + 64;                                // [(max_in+1) * HP]  Gm pairs
-  float* s_in = reinterpret_cast<float*>(s_g + (max_in + 1) * HP);   // [BS][SI]
-  const int* s_prog = prog + (size_t)blockIdx.y * prog_stride;
-
-  const int r = blockIdx.y, blk = blockIdx.x, G = gridDim.x;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int n = blk * BS + t;
-  const bool valid = n < N;
-  const float* th = params + (size_t)r * P;
-  const float* xr = xhat + (size_t)r * D * N;
-  const float* nz = noise + (size_t)r * NS * N;
-  float* dx = dxs + (size_t)r * Dt * N;
-  float* gp = gpart + ((size_t)r * G + blk) * P;
-
-  if (valid) {
-    for (int v = 0; v < Dt; ++v) {
-      float s = 0.f;
-      for (int c = 0; c < n_chunks; ++c) s += grad_part[(((size_t)c * R + r) * D + v) * N + n];
-      dx[(size_t)v * N + n] = s;
-    }
-  }
-  float* my_z = s_z + t * HE;
-  float* my_in = s_in + t * SI;
-  const int nn = uni(s_prog);
-
-  for (int kk = nn - 1; kk >= 0; --kk) {
-    const int* nd = s_prog + PROG_HDR + kk * NODE_REC;
-    if (uni(nd + 1) == KIND_OBS) continue;
-    const int var = uni(nd), npar = uni(nd + 2), paroff = uni(nd + 3), ncf = uni(nd + 4);
-    const int cfoff = uni(nd + 5), poff = uni(nd + 6);
-    const int nin = npar + 1 + ncf;
-    const float* W1 = th + poff;
-    const float* b1 = W1 + (size_t)nin * H;
-    const float* W2 = b1 + H;
-
-    // ---- compute phase (one sample per thread) ----
-    const float gout = valid ? dx[(size_t)var * N + n] : 0.f;
-    for (int j = 0; j < nin; ++j) {
-      float x = 0.f;
-      if (valid) {
-        if (j < npar) x = xr[(size_t)uni(s_prog + paroff + j) * N + n];
-        else if (j == npar) x = nz[(size_t)var * N + n];
-        else x = nz[(size_t)(D + uni(s_prog + cfoff + (j - npar - 1))) * N + n];
-      }
-      my_in[j] = x;
-    }
-    my_in[nin] = 1.f;
-    my_in[nin + 1] = gout;
-    for (int q = 0; q < H; ++q) {
-      float a = b1[q];
-      for (int j = 0; j < nin; ++j) a = fmaf(W1[j * H + q], my_in[j], a);
-      my_z[q] = a > 0.f ? gout : 0.f;
-    }
-    if (HE > H) my_z[H] = 0.f;
-    if (valid) {
-      for (int j = 0; j < npar; ++j) {
-        float s = 0.f;
-        for (int q = 0; q < H; ++q) s = fmaf(W1[j * H + q] * W2[q], my_z[q], s);
-        dx[(size_t)uni(s_prog + paroff + j) * N + n] += s;
-      }
-    }
-    __syncthreads();
-
-    // ---- reduction phase (as gen_bwd_kernel) ----
-    const int n_w1 = (nin + 1) * HP;
-    const int n_items = n_w1 + 1;
-    const bool split = n_items <= 64;
-    auto item = [&](int it, int s_lo, int s_n) -> f2 {
-      f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
-      if (it < n_w1) {
-        const int j = it / HP, qp = it - j * HP;
-        const float* a = s_in + s_lo * SI + j;
-        const float* zb = s_z + s_lo * HE + 2 * qp;
-#pragma unroll 4
-        for (int s2 = 0; s2 < s_n; s2 += 2) {
-          const float a0 = a[s2 * SI], a1 = a[(s2 + 1) * SI];
-          const f2 z0 = *reinterpret_cast<const f2*>(zb + s2 * HE);
-          const f2 z1 = *reinterpret_cast<const f2*>(zb + (s2 + 1) * HE);
-          acc0 = f2{a0, a0} * z0 + acc0;
-          acc1 = f2{a1, a1} * z1 + acc1;
-        }
-      } else {
-        const float* a = s_in + s_lo * SI + (nin + 1);
-        for (int s2 = 0; s2 < s_n; s2 += 2) {
-          acc0.x += a[s2 * SI];
-          acc1.x += a[(s2 + 1) * SI];
-        }
-      }
-      return acc0 + acc1;
-    };
-    auto emit = [&](int it, f2 acc) {
-      if (it < n_w1) {
-        const int j = it / HP, qp = it - j * HP, q = 2 * qp;
-        s_g[it] = acc;
-        gp[poff + j * H + q] = W2[q] * acc.x;
-        if (q + 1 < H) gp[poff + j * H + q + 1] = W2[q + 1] * acc.y;
-      } else {
-        gp[poff + (nin + 1) * H + H] = acc.x;      // db2
-      }
-    };
-    auto emit_w2 = [&](int q) {
-      float s = 0.f;
-      for (int j = 0; j <= nin; ++j) {
-        const f2 gm = s_g[j * HP + (q >> 1)];
-        s = fmaf(j < nin ? W1[j * H + q] : b1[q], (q & 1) ? gm.y : gm.x, s);
-      }
-      gp[poff + (nin + 1) * H + q] = s;
-    };
-    if (split) {
-      f2 acc = {0.f, 0.f};
-      if (lane < n_items) acc = item(lane, wave * 64, 64);
-      if (wave == 1) s_red[lane] = acc;
-      __syncthreads();
-      if (wave == 0) {
-        if (lane < n_items) emit(lane, acc + s_red[lane]);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (lane < H) emit_w2(lane);
-      }
-    } else {
-      for (int it = t; it < n_items; it += BS) emit(it, item(it, 0, BS));
-      __syncthreads();
-      for (int q = t; q < H; q += BS) emit_w2(q);
-    }
-    __syncthreads();
-  }
-}
-
-// ============================================================================
 // K5: TF1 Adam with fused fixed-order reduction of the G gradient slabs.
 //   lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t);  theta -= lr_t * m / (sqrt(v) + eps)
 // grid = (ceil(P/256), R)
@@ -930,40 +774,29 @@ extern "C" size_t cgnn_gen_bwd_lds(int H, int max_in, int D, int prog_stride) {
                           (size_t)(max_in + 1) * HE);
 }
 
-// LDS of the generic-width backward (sample state in global memory)
-extern "C" size_t cgnn_gen_bwd_generic_lds(int H, int max_in) {
-  const size_t HE = (size_t)((H + 1) & ~1);
-  return sizeof(float) * ((size_t)GEN_BWD_BS * (HE + ((max_in + 2) | 1)) + 128 + (size_t)(max_in + 1) * HE);
-}
+extern "C" int cgnn_staged_plan(int, int, int, int, int*);
 
-// 1: the specialised kernel (compiled H, LDS sample state fits), 2: the generic one,
-// 0: neither fits in LDS (the caller trains this batch elsewhere)
-// (env CGNN_GEN_BWD_GENERIC=1 forces the generic kernel: A/B and equivalence tests)
+// 1: the specialised per-sample kernel (compiled H, LDS sample state fits), 2: the
+// level-scheduled kernels of cgnn_staged.hip, 0: neither fits (the caller trains this
+// batch elsewhere).  CGNN_GEN_STAGED=1 forces 2 (A/B and equivalence tests).
 extern "C" int cgnn_gen_bwd_variant(int H, int max_in, int Dt, int prog_stride) {
-  const char* force = getenv("CGNN_GEN_BWD_GENERIC");
-  const bool generic = force && atoi(force) == 1;
-  if (!generic && cgnn_gen_supported_h(H) && cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride) <= 160 * 1024) return 1;
-  return cgnn_gen_bwd_generic_lds(H, max_in) <= 160 * 1024 ? 2 : 0;
+  const char* force = getenv("CGNN_GEN_STAGED");
+  const bool staged = force && atoi(force) == 1;
+  if (!staged && cgnn_gen_supported_h(H) && cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride) <= 160 * 1024) return 1;
+  int plan[5];
+  return cgnn_staged_plan(Dt, H, max_in, 8, plan) == 0 ? 2 : 0;
 }
 
-// dxs: [R][Dt][N] fp32 scratch of the generic kernel (may be null when variant 1)
+// the per-sample backward (variant 1); variant 2 batches launch cgnn_launch_gen_bwd_staged
 extern "C" int cgnn_launch_gen_bwd(const int* prog, int prog_stride, const float* params, int P,
                                    const float* xhat, const float* noise, int NS, const float* gradp,
                                    int n_chunks, int R, int N, int D, int Dt, int H, int max_in,
-                                   float* gpart, hipStream_t st, float* dxs) {
+                                   float* gpart, hipStream_t st) {
   const int G = cgnn_gen_bwd_blocks(N);
   dim3 grid(G, R), block(GEN_BWD_BS);
-  const int variant = cgnn_gen_bwd_variant(H, max_in, Dt, prog_stride);
-  if (variant == 2) {
-    if (!dxs) return -2;
-    const size_t lds = cgnn_gen_bwd_generic_lds(H, max_in);
-    allow_lds(gen_bwd_generic_kernel<GEN_BWD_BS>, lds);
-    hipLaunchKernelGGL((gen_bwd_generic_kernel<GEN_BWD_BS>), grid, block, lds, st, prog, prog_stride, params, P,
-                       xhat, noise, NS, gradp, n_chunks, R, N, D, Dt, max_in, H, dxs, gpart);
-    return (int)hipGetLastError();
-  }
-  if (variant == 0) return -2;
+  if (!cgnn_gen_supported_h(H)) return -1;
   const size_t lds = cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride);
+  if (lds > 160 * 1024) return -2;
   switch (H) {
 #define CASE_H(h) case h: allow_lds(gen_bwd_kernel<h, GEN_BWD_BS>, lds); hipLaunchKernelGGL((gen_bwd_kernel<h, GEN_BWD_BS>), grid, block, lds, st, prog, prog_stride, params, P, xhat, noise, NS, gradp, n_chunks, R, N, D, Dt, max_in, gpart); break;
     CGNN_H_LIST(CASE_H)

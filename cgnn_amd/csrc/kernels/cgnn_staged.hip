@@ -1,0 +1,457 @@
+// Level-scheduled generator kernels for wide causal graphs (the reference's random-graph
+// generator defaults to 200 variables, generators/random_graph_generator.py:26; CGNN
+// builds one MLP per variable for any d, CGNN.py:63-90).
+//
+// The per-sample kernels of cgnn_kernels.hip walk the whole DAG program in one wave per
+// 64..256 samples: at d = 200 that is a 200-node dependent chain per wave, each node
+// waiting on its scalar weight loads, with the block's [D][B] sample state limiting a
+// CU to 2-3 waves.  Here a block owns ONE 64-sample tile of one model, and its W waves
+// share it: the nodes of one topological level are independent, so wave w takes nodes
+// w, w + W, ... of the level and the block synchronises once per level.  The dependent
+// chain shrinks from d nodes to (#levels x level width / W) and every CU runs 8+ waves.
+//
+//   gen_noise_kernel       every Philox normal of the step (node noise and confounder
+//                          streams) in one fully parallel launch, into `noise`
+//                          ([R][NS][N]) -- the same draws, keyed exactly as before.
+//   gen_fwd_staged_kernel  forward over the forward stages (= levels); a node's value is
+//                          bitwise the per-sample kernel's (same fmaf order).
+//   gen_bwd_staged_kernel  backward over the backward sub-stages: levels in reverse,
+//                          split so that no two nodes of a sub-stage share a parent --
+//                          every dL/dparent push is then owned by one wave and the sums
+//                          are in a fixed order (no atomics; bitwise reproducible).  Per
+//                          node the wave recomputes the hidden layer in 16-unit chunks and
+//                          reduces the parameter gradients over its 64 samples through a
+//                          per-wave LDS slab (the item scheme of gen_bwd_kernel).
+//
+// Sample state: x (and dL/dx in the backward) live in LDS ([Dt][64] each) while they fit,
+// otherwise in global memory (xhat itself / the dxs scratch) -- the launcher picks.
+// The schedule (engine/program.py stage_schedule, built by the C++ runtime):
+//   [0] n_fwd_stages [1] n_bwd_stages [2] fwd_base [3] bwd_base
+//   at fwd_base: starts[n_fwd + 1], then program record indices; same at bwd_base.
+// Blocks are dealt XCD-contiguously (xcd_remap), so the tiles of one model share an
+// L2 and its weight stream.
+#include "cgnn_common.h"
+#include <algorithm>
+#include <type_traits>
+
+using namespace cgnn;
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int HZ = 16;            // hidden units per backward chunk
+constexpr int ZS = HZ + 2;        // per-lane mg row stride (floats, even: f2 pairs)
+constexpr int HZP = HZ / 2;
+
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(256) void gen_noise_kernel(const int* __restrict__ prog, int ps,
+                                                        const uint32_t* __restrict__ keys,
+                                                        const int* __restrict__ step_base, int step_off,
+                                                        float* __restrict__ noise, int NS, int N, int D, int Dt,
+                                                        int row0) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int s = blockIdx.y, r = blockIdx.z;
+  if (n >= N) return;
+  const uint32_t step = (uint32_t)(step_base[0] + step_off);
+  const uint32_t k0 = keys[2 * r], k1 = keys[2 * r + 1];
+  float* nz = noise + (size_t)r * NS * N;
+  if (s < Dt) {
+    nz[(size_t)s * N + n] = rng_normal(k0, k1, (uint32_t)(row0 + n), (uint32_t)s, step, RNG_NODE_NOISE);
+  } else {
+    const int cid = s - Dt;
+    if (cid < prog[(size_t)r * ps + 2])
+      nz[(size_t)(D + cid) * N + n] = rng_normal(k0, k1, (uint32_t)(row0 + n), (uint32_t)cid, step, RNG_CONF_NOISE);
+  }
+}
+
+// ---------------------------------------------------------------------------- forward
+template <int HC, bool XG>
+__global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
+    const int* __restrict__ prog, int ps, const int* __restrict__ sched, int ss,
+    const float* __restrict__ params, int P, const float* __restrict__ data, float* __restrict__ xhat,
+    const float* __restrict__ noise, int NS, float* __restrict__ xnorm, int N, int D, int Dt, int H, int T) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int W = blockDim.x >> 6;
+  const int wave = wave_id(), lane = threadIdx.x & 63;
+  const int L = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int r = L / T, tile = L - r * T;
+  const int n = tile * WAVE + lane;
+  const bool valid = n < N;
+  const int nc = valid ? n : N - 1;
+  const int* pg = prog + (size_t)r * ps;
+  const int* sc = sched + (size_t)r * ss;
+  const float* th = params + (size_t)r * P;
+  const float* dr = data + (size_t)r * D * N;
+  const float* nz = noise + (size_t)r * NS * N;
+  float* xr = xhat + (size_t)r * D * N;
+  float* s_x = smem;                                        // [Dt][64] (LDS state)
+  float* s_nrm = smem + (XG ? 0 : (size_t)Dt * WAVE);       // [W][64]
+  auto xget = [&](int v) -> float { return XG ? xr[(size_t)v * N + nc] : s_x[v * WAVE + lane]; };
+  auto xput = [&](int v, float val) {
+    if (XG) {
+      if (valid) xr[(size_t)v * N + n] = val;
+    } else {
+      s_x[v * WAVE + lane] = val;
+    }
+  };
+
+  const int nf = uni(sc), fb = uni(sc + 2);
+  const int* starts = sc + fb;
+  const int* items = starts + nf + 1;
+  for (int st = 0; st < nf; ++st) {
+    const int b = uni(starts + st), e = uni(starts + st + 1);
+    for (int i = b + wave; i < e; i += W) {
+      const int kk = uni(items + i);
+      const int* nd = pg + PROG_HDR + kk * NODE_REC;
+      const int var = uni(nd);
+      if (uni(nd + 1) == KIND_OBS) {
+        xput(var, dr[(size_t)var * N + nc]);
+        continue;
+      }
+      const int npar = uni(nd + 2), paroff = uni(nd + 3), ncf = uni(nd + 4), cfoff = uni(nd + 5);
+      const int poff = uni(nd + 6);
+      const int nin = npar + 1 + ncf;
+      const float* W1 = th + poff;
+      const float* b1 = W1 + (size_t)nin * H;
+      const float* W2 = b1 + H;
+      const float e_own = nz[(size_t)var * N + nc];
+      float out = W2[H];
+      // same per-unit fmaf order as gen_fwd_kernel: own noise + bias, parents, confounders
+      for (int q0 = 0; q0 < H; q0 += HC) {
+        float pre[HC];
+#pragma unroll
+        for (int q = 0; q < HC; ++q) pre[q] = fmaf(W1[npar * H + q0 + q], e_own, b1[q0 + q]);
+        for (int j = 0; j < npar; ++j) {
+          const float x = xget(uni(pg + paroff + j));
+#pragma unroll
+          for (int q = 0; q < HC; ++q) pre[q] = fmaf(W1[j * H + q0 + q], x, pre[q]);
+        }
+        for (int c = 0; c < ncf; ++c) {
+          const float ec = nz[(size_t)(D + uni(pg + cfoff + c)) * N + nc];
+#pragma unroll
+          for (int q = 0; q < HC; ++q) pre[q] = fmaf(W1[(npar + 1 + c) * H + q0 + q], ec, pre[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < HC; ++q) out = fmaf(W2[q0 + q], fmaxf(pre[q], 0.f), out);
+      }
+      xput(var, out);
+    }
+    __syncthreads();
+  }
+
+  if (!XG && valid)
+    for (int v = wave; v < Dt; v += W) xr[(size_t)v * N + n] = s_x[v * WAVE + lane];
+  if (xnorm) {
+    // squared norm for the Gram-form MMD: wave w sums program positions w, w + W, ...
+    // in order, the W partials are added in wave order (fixed)
+    const int nn = uni(pg);
+    float nrm = 0.f;
+    for (int kk = wave; kk < nn; kk += W) {
+      const float v = xget(uni(pg + PROG_HDR + kk * NODE_REC));
+      nrm = fmaf(v, v, nrm);
+    }
+    s_nrm[wave * WAVE + lane] = nrm;
+    __syncthreads();
+    if (wave == 0 && valid) {
+      float s = 0.f;
+      for (int w = 0; w < W; ++w) s += s_nrm[w * WAVE + lane];
+      xnorm[(size_t)r * N + n] = s;
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- backward
+// per-wave LDS slab (floats): input rows [64][SI], mg rows [64][ZS], Gm pairs
+__host__ __device__ __forceinline__ int bwd_si(int max_in) { return (max_in + 2) | 1; }
+__host__ __device__ __forceinline__ int bwd_slab(int max_in) {
+  return WAVE * (bwd_si(max_in) + 1) + WAVE * ZS + (max_in + 1) * HZ;   // [64][SI] padded even
+}
+
+template <bool XG, bool DG>
+__global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
+    const int* __restrict__ prog, int ps, const int* __restrict__ sched, int ss,
+    const float* __restrict__ params, int P, const float* __restrict__ xhat, const float* __restrict__ noise,
+    int NS, const float* __restrict__ grad_part, int n_chunks, int R, int N, int D, int Dt, int H, int max_in,
+    int T, float* __restrict__ gpart, float* __restrict__ dxs) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int W = blockDim.x >> 6;
+  const int wave = wave_id(), lane = threadIdx.x & 63;
+  const int L = (int)xcd_remap(blockIdx.x, gridDim.x);
+  const int r = L / T, tile = L - r * T;
+  const int n = tile * WAVE + lane;
+  const bool valid = n < N;
+  const int nc = valid ? n : N - 1;
+  const int* pg = prog + (size_t)r * ps;
+  const int* sc = sched + (size_t)r * ss;
+  const float* th = params + (size_t)r * P;
+  const float* xr = xhat + (size_t)r * D * N;
+  const float* nz = noise + (size_t)r * NS * N;
+  float* dx = dxs + (size_t)r * Dt * N;
+  float* gp = gpart + ((size_t)r * T + tile) * P;
+  const int SI = bwd_si(max_in);
+  float* s_x = smem;
+  float* s_dx = s_x + (XG ? 0 : (size_t)Dt * WAVE);
+  float* slab = s_dx + (DG ? 0 : (size_t)Dt * WAVE) + (size_t)wave * bwd_slab(max_in);
+  float* s_in = slab;                                        // [64][SI]
+  float* s_z = slab + WAVE * (SI + 1);                       // [64][ZS]
+  f2* s_g = reinterpret_cast<f2*>(s_z + WAVE * ZS);          // [(max_in + 1) * HZP]
+  float* my_in = s_in + lane * SI;
+  float* my_z = s_z + lane * ZS;
+
+  auto xget = [&](int v) -> float { return XG ? xr[(size_t)v * N + nc] : s_x[v * WAVE + lane]; };
+
+  // sample state: x and dL/dx = fixed-order sum of the MMD gradient chunks
+  for (int v = wave; v < Dt; v += W) {
+    float s = 0.f;
+    if (valid)
+      for (int c = 0; c < n_chunks; ++c) s += grad_part[(((size_t)c * R + r) * D + v) * N + n];
+    if (DG) {
+      if (valid) dx[(size_t)v * N + n] = s;
+    } else {
+      s_dx[v * WAVE + lane] = s;
+    }
+    if (!XG) s_x[v * WAVE + lane] = valid ? xr[(size_t)v * N + n] : 0.f;
+  }
+  __syncthreads();
+
+  const int nb = uni(sc + 1), bb = uni(sc + 3);
+  const int* starts = sc + bb;
+  const int* items = starts + nb + 1;
+  for (int st = 0; st < nb; ++st) {
+    const int b = uni(starts + st), e = uni(starts + st + 1);
+    for (int i = b + wave; i < e; i += W) {
+      const int kk = uni(items + i);
+      const int* nd = pg + PROG_HDR + kk * NODE_REC;
+      const int var = uni(nd), npar = uni(nd + 2), paroff = uni(nd + 3), ncf = uni(nd + 4);
+      const int cfoff = uni(nd + 5), poff = uni(nd + 6);
+      const int nin = npar + 1 + ncf;
+      const float* W1 = th + poff;       // W1ext rows 0..nin (row nin = b1)
+      const float* W2 = W1 + (size_t)(nin + 1) * H;
+      float gout = 0.f;
+      if (valid) gout = DG ? dx[(size_t)var * N + n] : s_dx[var * WAVE + lane];
+
+      for (int j = 0; j < nin; ++j) {
+        float x;
+        if (j < npar) x = xget(uni(pg + paroff + j));
+        else if (j == npar) x = nz[(size_t)var * N + nc];
+        else x = nz[(size_t)(D + uni(pg + cfoff + (j - npar - 1))) * N + nc];
+        my_in[j] = x;
+      }
+      my_in[nin] = 1.f;
+
+      for (int q0 = 0; q0 < H; q0 += HZ) {
+        const int hc = min(HZ, H - q0);
+        // ---- recompute this chunk's pre-activations (one sample per lane).  A full
+        // chunk reads 16 contiguous weights per row (wide scalar loads); the tail chunk
+        // clamps its indices to the node's own parameters and zeroes the extra units ----
+        float mg[HZ];
+        auto chunk = [&](auto full) {
+          constexpr bool FULL = decltype(full)::value;
+          auto wi = [&](int row, int q) -> float {
+            return FULL ? W1[row * H + q0 + q] : W1[row * H + q0 + min(q, hc - 1)];
+          };
+          float pre[HZ];
+#pragma unroll
+          for (int q = 0; q < HZ; ++q) pre[q] = wi(nin, q);
+          for (int j = 0; j < nin; ++j) {
+            const float x = my_in[j];
+#pragma unroll
+            for (int q = 0; q < HZ; ++q) pre[q] = fmaf(wi(j, q), x, pre[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < HZ; ++q) mg[q] = ((FULL || q < hc) && pre[q] > 0.f) ? gout : 0.f;
+          // this chunk's share of dL/dparent (the parent is this wave's alone)
+          for (int j = 0; j < npar; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < HZ; ++q) s = fmaf(wi(j, q) * wi(nin + 1, q), mg[q], s);
+            const int pv = uni(pg + paroff + j);
+            if (DG) {
+              if (valid) dx[(size_t)pv * N + n] += s;
+            } else {
+              s_dx[pv * WAVE + lane] += s;
+            }
+          }
+        };
+        if (hc == HZ) chunk(std::true_type{});
+        else chunk(std::false_type{});
+#pragma unroll
+        for (int qp = 0; qp < HZP; ++qp)
+          *reinterpret_cast<f2*>(my_z + 2 * qp) = f2{mg[2 * qp], mg[2 * qp + 1]};
+        wave_sync();
+
+        // ---- Gm[j][q] = sum_s in[s][j] mg[s][q] over the 64 samples: items (row j,
+        // column pair), the samples split over 2 or 4 lane groups when items are few ----
+        const int hp = (hc + 1) >> 1;
+        const int n_items = (nin + 1) * hp;
+        const int grp = n_items <= 16 ? 4 : n_items <= 32 ? 2 : 1;
+        const int span = WAVE / grp;
+        const int part = lane / span, il = lane - part * span;
+        const int s_lo = part * span, s_n = span;
+        for (int it0 = 0; it0 < n_items; it0 += span) {
+          const int it = it0 + il;
+          f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
+          if (it < n_items) {
+            const int j = it / hp, qp = it - j * hp;
+            const float* a = s_in + s_lo * SI + j;
+            const float* zb = s_z + s_lo * ZS + 2 * qp;
+#pragma unroll 4
+            for (int s2 = 0; s2 < s_n; s2 += 2) {
+              const float a0 = a[s2 * SI], a1 = a[(s2 + 1) * SI];
+              const f2 z0 = *reinterpret_cast<const f2*>(zb + s2 * ZS);
+              const f2 z1 = *reinterpret_cast<const f2*>(zb + (s2 + 1) * ZS);
+              acc0 = f2{a0, a0} * z0 + acc0;
+              acc1 = f2{a1, a1} * z1 + acc1;
+            }
+          }
+          f2 acc = acc0 + acc1;
+          if (grp >= 2) acc += f2{__shfl_xor(acc.x, 32), __shfl_xor(acc.y, 32)};
+          if (grp == 4) acc += f2{__shfl_xor(acc.x, 16), __shfl_xor(acc.y, 16)};
+          if (part == 0 && it < n_items) {
+            const int j = it / hp, qp = it - j * hp, q = q0 + 2 * qp;
+            s_g[j * HZP + qp] = acc;
+            gp[poff + j * H + q] = W2[q] * acc.x;                   // dW1 / db1
+            if (2 * qp + 1 < hc) gp[poff + j * H + q + 1] = W2[q + 1] * acc.y;
+          }
+        }
+        wave_sync();
+        // dW2[q] = sum_j W1ext[j][q] Gm[j][q]
+        if (lane < hc) {
+          float s = 0.f;
+          for (int j = 0; j <= nin; ++j) {
+            const f2 gm = s_g[j * HZP + (lane >> 1)];
+            s = fmaf(W1[j * H + q0 + lane], (lane & 1) ? gm.y : gm.x, s);
+          }
+          gp[poff + (nin + 1) * H + q0 + lane] = s;
+        }
+        wave_sync();
+      }
+      const float g2 = wave_sum(gout);                               // db2
+      if (lane == 0) gp[poff + (nin + 2) * H] = g2;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename K>
+void allow_lds(K kernel, size_t lds) {
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+}
+
+constexpr size_t LDS_MAX = 160 * 1024;
+
+size_t fwd_lds(int Dt, int W, bool xg) { return sizeof(float) * ((xg ? 0 : (size_t)Dt * WAVE) + (size_t)W * WAVE); }
+size_t bwd_lds(int Dt, int W, int max_in, bool xg, bool dg) {
+  return sizeof(float) * ((xg ? 0 : (size_t)Dt * WAVE) + (dg ? 0 : (size_t)Dt * WAVE) + (size_t)W * bwd_slab(max_in));
+}
+
+int fwd_hc(int H) {
+  static const int cand[] = {32, 20, 16, 12, 10, 8, 6, 5, 4, 3, 2, 1};
+  for (int c : cand)
+    if (H % c == 0) return c;
+  return 1;
+}
+
+}  // namespace
+
+// Plan of the staged kernels for Dt variables, hidden width H, max_in generator inputs
+// and W waves per block (1..8): out = {fwd_xg, bwd_xg, bwd_dg, W_fwd, W_bwd}.  Returns 0,
+// or -1 when even the all-global variant does not fit (only for absurd max_in).
+extern "C" int cgnn_staged_plan(int Dt, int H, int max_in, int W, int* out) {
+  if (Dt < 1 || H < 1 || W < 1 || W > 8) return -1;
+  const int fxg = fwd_lds(Dt, W, false) <= LDS_MAX ? 0 : 1;
+  int wb = W, bxg = -1, bdg = -1;
+  for (; wb >= 1 && bxg < 0; wb >>= 1) {
+    if (bwd_lds(Dt, wb, max_in, false, false) <= LDS_MAX) { bxg = 0; bdg = 0; }
+    else if (bwd_lds(Dt, wb, max_in, true, false) <= LDS_MAX) { bxg = 1; bdg = 0; }
+    else if (bwd_lds(Dt, wb, max_in, true, true) <= LDS_MAX) { bxg = 1; bdg = 1; }
+    if (bxg >= 0) break;
+  }
+  if (bxg < 0) return -1;
+  out[0] = fxg; out[1] = bxg; out[2] = bdg; out[3] = W; out[4] = wb;
+  return 0;
+}
+
+extern "C" int cgnn_staged_tiles(int N) { return (N + WAVE - 1) / WAVE; }
+
+extern "C" int cgnn_launch_gen_noise(const int* prog, int ps, const uint32_t* keys, const int* step_base,
+                                     int step_off, float* noise, int NS, int N, int D, int Dt, int R, int row0,
+                                     hipStream_t st) {
+  if (NS < D || Dt > D) return -2;
+  dim3 grid((N + 255) / 256, Dt + (NS - D), R), block(256);
+  hipLaunchKernelGGL(gen_noise_kernel, grid, block, 0, st, prog, ps, keys, step_base, step_off, noise, NS, N, D,
+                     Dt, row0);
+  return (int)hipGetLastError();
+}
+
+// forward of R models (noise already drawn).  W waves per block (1..8).  force: -1 the
+// plan's state placement, 0 LDS, 1 global (tests: every placement is bitwise the same)
+extern "C" int cgnn_launch_gen_fwd_staged(const int* prog, int ps, const int* sched, int ss, const float* params,
+                                          int P, const float* data, float* xhat, const float* noise, int NS,
+                                          float* xnorm, int N, int D, int Dt, int H, int R, int W, hipStream_t st,
+                                          int force) {
+  int plan[5];
+  if (cgnn_staged_plan(Dt, H, 1, W, plan) != 0) return -2;
+  const bool xg = force < 0 ? plan[0] != 0 : force == 1;
+  if (!xg && fwd_lds(Dt, W, false) > LDS_MAX) return -2;
+  const int T = cgnn_staged_tiles(N);
+  const size_t lds = fwd_lds(Dt, W, xg);
+  dim3 grid((unsigned)(T * R)), block(WAVE * W);
+#define FWD(HC, XG)                                                                                           \
+  {                                                                                                           \
+    allow_lds(gen_fwd_staged_kernel<HC, XG>, lds);                                                            \
+    hipLaunchKernelGGL((gen_fwd_staged_kernel<HC, XG>), grid, block, lds, st, prog, ps, sched, ss, params, P, \
+                       data, xhat, noise, NS, xnorm, N, D, Dt, H, T);                                         \
+  }
+#define FWD_HC(HC) case HC: if (xg) FWD(HC, true) else FWD(HC, false) break;
+  switch (fwd_hc(H)) {
+    FWD_HC(32) FWD_HC(20) FWD_HC(16) FWD_HC(12) FWD_HC(10) FWD_HC(8) FWD_HC(6) FWD_HC(5) FWD_HC(4) FWD_HC(3)
+    FWD_HC(2) FWD_HC(1)
+    default: return -1;
+  }
+#undef FWD_HC
+#undef FWD
+  return (int)hipGetLastError();
+}
+
+// backward: gpart [R][T][P] (T = cgnn_staged_tiles(N)); dxs [R][Dt][N] is needed when the
+// plan puts dL/dx in global memory (plan[2]).  force: -1 the plan, 0 x and dL/dx in LDS,
+// 1 x global, 2 both global (tests: every placement is bitwise the same)
+extern "C" int cgnn_launch_gen_bwd_staged(const int* prog, int ps, const int* sched, int ss, const float* params,
+                                          int P, const float* xhat, const float* noise, int NS, const float* gradp,
+                                          int n_chunks, int R, int N, int D, int Dt, int H, int max_in, int W,
+                                          float* gpart, float* dxs, hipStream_t st, int force) {
+  int plan[5];
+  if (cgnn_staged_plan(Dt, H, max_in, W, plan) != 0) return -2;
+  bool xg = plan[1] != 0, dg = plan[2] != 0;
+  int wb = plan[4];
+  if (force >= 0) {
+    xg = force >= 1;
+    dg = force == 2;
+    wb = W;
+    if (bwd_lds(Dt, wb, max_in, xg, dg) > LDS_MAX) return -2;
+  }
+  if (dg && !dxs) return -2;
+  const int T = cgnn_staged_tiles(N);
+  const size_t lds = bwd_lds(Dt, wb, max_in, xg, dg);
+  dim3 grid((unsigned)(T * R)), block(WAVE * wb);
+#define BWD(XG, DG)                                                                                            \
+  {                                                                                                            \
+    allow_lds(gen_bwd_staged_kernel<XG, DG>, lds);                                                             \
+    hipLaunchKernelGGL((gen_bwd_staged_kernel<XG, DG>), grid, block, lds, st, prog, ps, sched, ss, params, P,  \
+                       xhat, noise, NS, gradp, n_chunks, R, N, D, Dt, H, max_in, T, gpart, dxs);               \
+  }
+  if (!xg) BWD(false, false)
+  else if (!dg) BWD(true, false)
+  else BWD(true, true)
+#undef BWD
+  return (int)hipGetLastError();
+}

@@ -304,11 +304,285 @@ __global__ __launch_bounds__(256) void mmd_mfma_kernel(
   }
 }
 
+// ============================================================================
+// Wide joints (KD >= 128): 16 generated rows per wave on v_mfma_f32_16x16x32_f16.
+// The 32-row kernel above keeps KD/16 x 16 x-fragment registers and KD/32 x 16
+// gradient accumulators per wave (224 + 112 at KD = 224) and a second, transposed
+// copy of every column tile in LDS (123 KB at KD = 224): one wave per SIMD.  Here
+// a wave holds 16 rows (x fragments KD/32 x 8 regs, accumulators KD/16 x 4), and the
+// column tile is staged ONCE, row-major [j][d] (hi and lo f16 images), row j skewed
+// by 2 (j & 7) 16-B chunks in a row of a whole number of 256-B bank rows, so that both
+// reads are conflict-free and every address is a per-lane base plus an immediate: the
+// Gram's A fragments by ds_read_b128 along d, the gradient's B fragments by
+// ds_read_b64_tr_b16 along j.
+//   C'[j][i] = sum_d Z[j][d] X[i][d]    two 16-column halves, A = Z (LDS), B = X
+//      -> lane l: row i = l&15, columns j = 16 h + 4(l>>4) + v (half h, v = 0..3)
+//   G[i][d] += sum_j W[i][j] Z[j][d]    A = the lane's own 8 W values (k-slot e <->
+//      j = 4g + e for e < 4, 16 + 4g + e - 4 after; g = l>>4), B = Z^T through
+//      the transposed reads of rows 4g..4g+3 and 16+4g..16+4g+3.
+// No symmetric skipping here (every mode evaluates the whole pred-pred block).
+// ============================================================================
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+
+constexpr int W16 = 8;          // waves per block (rows per block = 128, as the 32-row kernel)
+
+__device__ __forceinline__ f4v mma16(h8 a, h8 b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// half offset of (row j, chunk c of 8 halfs) in a [32][ZS] image: skew 2 (j & 7) chunks
+template <int ZS>
+__device__ __forceinline__ int zoff(int j, int c) { return j * ZS + 8 * (c + 2 * (j & 7)); }
+
+template <int KD, int MODE>
+__global__ __launch_bounds__(512) void mmd_mfma16_kernel(
+    const float* __restrict__ xhat, const float* __restrict__ data,
+    const float* __restrict__ xnorm, const float* __restrict__ ynorm,
+    float* __restrict__ grad_part, float* __restrict__ loss_part,
+    int N, int R, int tiles_per_chunk, float grad_scale, int row_begin, int n_rows) {
+  constexpr bool GRAD = MODE == 0 || MODE == 3;
+  constexpr bool LOSS = MODE != 3;
+  constexpr int KP = (KD + 31) / 32 * 32;   // k padded to the MFMA k-step (32)
+  constexpr int KS = KP / 32;
+  constexpr int NT = (KD + 15) / 16;        // 16-wide gradient tiles
+  constexpr int ZS = (KP + 14 * 8 + 127) / 128 * 128;  // row (halfs): skew room, whole 256-B rows
+  static_assert(KP <= 256, "wide MMD covers KD <= 256 per launch");
+  constexpr int NCH = KP / 8;               // 16-B chunks per staged row
+  constexpr int TASKS = MT * NCH;           // (row, chunk) staging tasks per tile
+  constexpr int TPT = (TASKS + 511) / 512;  // per thread
+  __shared__ __attribute__((aligned(16))) _Float16 s_zh[2][MT * ZS];
+  __shared__ __attribute__((aligned(16))) _Float16 s_zl[2][MT * ZS];
+  __shared__ __attribute__((aligned(16))) float s_n[2][MT];
+  __shared__ float s_red[W16];
+
+  const int rb = blockIdx.x, chunk = blockIdx.y, r = blockIdx.z;
+  const int n_chunks = gridDim.y, n_rb = gridDim.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int i = row_begin + rb * (W16 * 16) + wave * 16 + li;
+  const bool row_ok = i - row_begin < n_rows;
+  const size_t mbase = (size_t)r * KD * N;
+  const float* X = xhat + mbase;
+  const float* Y = data + mbase;
+  const float* XN = xnorm + (size_t)r * N;
+  const float* YN = ynorm + (size_t)r * N;
+  const float nx = row_ok ? XN[i] : 0.f;
+
+  // this lane's B fragments of row i: dims 32 s + 8 g + e, split once
+  h8 xbh[KS], xbl[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int d = 32 * s + 8 * g + e;
+      const float v = (row_ok && d < KD) ? X[(size_t)d * N + i] : 0.f;
+      _Float16 hi, lo;
+      split16(v, hi, lo);
+      xbh[s][e] = hi;
+      xbl[s][e] = lo;
+    }
+  }
+
+  const int TX = (N + MT - 1) / MT;
+  const int ct = MODE == 2 ? TX : 2 * TX;
+  const int t_begin = chunk * tiles_per_chunk;
+  const int t_end = min(ct, t_begin + tiles_per_chunk);
+
+  // staging: task k -> (column jj = task & 31, chunk c = task >> 5): 8 consecutive dims
+  float stage[TPT][8];
+  float stage_n = 0.f;
+  auto load_tile = [&](int tile) {
+    const float* src = tile < TX ? X : Y;
+    const int c0 = (tile < TX ? tile : tile - TX) * MT;
+    stage_n = (t < MT && c0 + t < N) ? (tile < TX ? XN : YN)[c0 + t] : 0.f;
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+      const int task = t + 512 * k;
+      const int jj = task & 31, c = task >> 5;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int d = 8 * c + e;
+        stage[k][e] = (task < TASKS && d < KD && c0 + jj < N) ? src[(size_t)d * N + c0 + jj] : 0.f;
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    if (t < MT) s_n[buf][t] = stage_n;
+#pragma unroll
+    for (int k = 0; k < TPT; ++k) {
+      const int task = t + 512 * k;
+      if (task < TASKS) {
+        const int jj = task & 31, c = task >> 5;
+        h8 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          _Float16 a, b;
+          split16(stage[k][e], a, b);
+          hi[e] = a;
+          lo[e] = b;
+        }
+        *reinterpret_cast<h8*>(&s_zh[buf][zoff<ZS>(jj, c)]) = hi;
+        *reinterpret_cast<h8*>(&s_zl[buf][zoff<ZS>(jj, c)]) = lo;
+      }
+    }
+  };
+  if (t_begin < t_end) {
+    load_tile(t_begin);
+    store_tile(0);
+    if (t_begin + 1 < t_end) {
+      load_tile(t_begin + 1);
+      store_tile(1);
+    }
+  }
+  __syncthreads();
+
+  f4v acc_g[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) acc_g[q] = f4v{};
+  float rowsum = 0.f, lacc = 0.f;
+
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const int buf = (tile - t_begin) & 1;
+    const bool pred_part = tile < TX;
+    const int c0 = (pred_part ? tile : tile - TX) * MT;
+    const bool more = tile + 2 < t_end;
+    if (more) load_tile(tile + 2);
+    const _Float16* zh = s_zh[buf];
+    const _Float16* zl = s_zl[buf];
+
+    // ---- Gram, two 16-column halves, three passes per k-step ----
+    f4v c[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      c[h] = f4v{};
+      const int j = 16 * h + li;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const h8 ah = *reinterpret_cast<const h8*>(zh + zoff<ZS>(j, 4 * s + g));
+        const h8 al = *reinterpret_cast<const h8*>(zl + zoff<ZS>(j, 4 * s + g));
+        c[h] = mma16(ah, xbh[s], c[h]);
+        c[h] = mma16(ah, xbl[s], c[h]);
+        c[h] = mma16(al, xbh[s], c[h]);
+      }
+    }
+
+    // ---- epilogue: lane l has row i, columns j = 16 h + 4 g + v ----
+    f2 tl2 = {0.f, 0.f}, rs2 = {0.f, 0.f};
+    const float sg = pred_part ? 1.f : -1.f;
+    const int jlim = N - c0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 nz4 = *reinterpret_cast<const float4*>(&s_n[buf][16 * h + 4 * g]);
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const f2 nzp = qq ? f2{nz4.z, nz4.w} : f2{nz4.x, nz4.y};
+        const f2 cc = {c[h][2 * qq], c[h][2 * qq + 1]};
+        f2 d2 = cc * -2.f + (nzp + nx);
+        const int jr = 16 * h + 4 * g + 2 * qq;
+        d2.x = jr < jlim ? d2.x : 1.0e30f;
+        d2.y = jr + 1 < jlim ? d2.y : 1.0e30f;
+        f2 ks, w;
+        if (GRAD) rbf7x2_chain(d2, ks, w);
+        else rbf7x2(d2, ks, w);
+        if (LOSS) tl2 += ks;
+        if (GRAD) {
+          w *= sg;
+          rs2 += w;
+          c[h][2 * qq] = w.x;
+          c[h][2 * qq + 1] = w.y;
+        }
+      }
+    }
+    if (LOSS) lacc = fmaf(pred_part ? 1.f : -2.f, tl2.x + tl2.y, lacc);
+
+    if (GRAD) {
+      rowsum += rs2.x + rs2.y;
+      h8 wh, wl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 hi, lo;
+        split16(c[e >> 2][e & 3], hi, lo);
+        wh[e] = hi;
+        wl[e] = lo;
+      }
+      // B fragment of tile q: rows 4g..4g+3 (slots 0..3) and 16+4g.. (slots 4..7),
+      // columns 16 q .. 16 q + 15; lane 4 rr + p of each 16-lane group addresses row
+      // rr, columns 4p..4p+3 (chunk 2q + (p >> 1), half (p & 1))
+      const int rr = li >> 2, p = li & 3;
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const int cq = 2 * q + (p >> 1), hq = 4 * (p & 1);
+        const int o0 = zoff<ZS>(4 * g + rr, cq) + hq, o1 = zoff<ZS>(16 + 4 * g + rr, cq) + hq;
+        typedef __attribute__((address_space(3))) s4v lds_s4v;
+        const s4v bh0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(zh + o0));
+        const s4v bh1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(zh + o1));
+        const s4v bl0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(zl + o0));
+        const s4v bl1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(zl + o1));
+        const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(bh0, bh1, 0, 1, 2, 3, 4, 5, 6, 7));
+        const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(bl0, bl1, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc_g[q] = mma16(wh, bh, acc_g[q]);
+        acc_g[q] = mma16(wh, bl, acc_g[q]);
+        acc_g[q] = mma16(wl, bh, acc_g[q]);
+      }
+    }
+    __syncthreads();
+    if (more) store_tile(buf);
+    __syncthreads();
+  }
+
+  // ---- loss partial: fixed-order wave then block reduction ----
+  float v = row_ok ? lacc : 0.f;
+  v = wave_sum(v);
+  if (lane == 0) s_red[wave] = v;
+  __syncthreads();
+  if (t == 0) {
+    const float sum = ((s_red[0] + s_red[1]) + (s_red[2] + s_red[3])) + ((s_red[4] + s_red[5]) + (s_red[6] + s_red[7]));
+    loss_part[((size_t)r * n_chunks + chunk) * n_rb + rb] = sum;
+  }
+
+  if (GRAD) {
+    // sum_j W_ij of row i = l&15: the four lane groups hold disjoint column sets
+    rowsum += __shfl_xor(rowsum, 16);
+    rowsum += __shfl_xor(rowsum, 32);
+    float* gp = grad_part + ((size_t)chunk * R + r) * KD * n_rows;
+    const int i0 = rb * (W16 * 16) + wave * 16;       // local row of li = 0
+#pragma unroll
+    for (int vv = 0; vv < 4; ++vv) {
+      const int il = 4 * g + vv;                      // accumulator row -> local row
+      const float rs = __shfl(rowsum, il);
+      const int ii = i0 + il;
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const int d = 16 * q + li;
+        if (d < KD && ii < n_rows) {
+          const float pv = X[(size_t)d * N + row_begin + ii];
+          gp[(size_t)d * n_rows + ii] = (acc_g[q][vv] - pv * rs) * grad_scale;
+        }
+      }
+    }
+  }
+}
+
 template <int KD>
 int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const float* xn, const float* yn,
                       float* gpart, float* lpart, int N, int R, int n_chunks, int tpc, float gscale,
-                      int row_begin, int n_rows, hipStream_t st) {
+                      int row_begin, int n_rows, hipStream_t st, int wide) {
   const int n_rb = (n_rows + WAVES * MT - 1) / (WAVES * MT);
+  if (wide < 0) wide = KD >= 128;
+  if (KD >= 128 && wide) {
+    if constexpr (KD >= 128) {
+      dim3 grid(n_rb, n_chunks, R), block(512);
+#define WIDE(M, A, B, C, D2) hipLaunchKernelGGL((mmd_mfma16_kernel<KD, M>), grid, block, 0, st, A, B, C, D2, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows)
+      if (mode == 0) WIDE(0, xhat, data, xn, yn);
+      else if (mode == 3) WIDE(3, xhat, data, xn, yn);
+      else if (mode == 1) WIDE(1, xhat, data, xn, yn);
+      else if (mode == 2) WIDE(2, data, data, yn, yn);
+      else return -3;
+#undef WIDE
+      return (int)hipGetLastError();
+    }
+  }
   dim3 grid(n_rb, n_chunks, R), block(256);
   if (mode == 0)
     hipLaunchKernelGGL((mmd_mfma_kernel<KD, 0>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
@@ -340,12 +614,13 @@ extern "C" int cgnn_mmd_mfma_supported(int D) {
 extern "C" int cgnn_mmd_mfma_row_blocks(int N) { return (N + WAVES * MT - 1) / (WAVES * MT); }
 
 // xnorm / ynorm: [R][N] squared norms of the generated / true samples
+// wide: -1 auto (the 16-row kernel from D = 128), 0 / 1 force (A/B and tests)
 extern "C" int cgnn_launch_mmd_mfma_rows(int mode, int D, const float* xhat, const float* data, const float* xnorm,
                                     const float* ynorm, float* gpart, float* lpart, int N, int R, int n_chunks,
-                                    int tpc, float gscale, int row_begin, int n_rows, hipStream_t st) {
+                                    int tpc, float gscale, int row_begin, int n_rows, hipStream_t st, int wide) {
   if (row_begin < 0 || n_rows < 1 || row_begin + n_rows > N) return -2;
   switch (D) {
-#define CASE_D(d) case d: return launch_mmd_mfma_d<d>(mode, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale, row_begin, n_rows, st);
+#define CASE_D(d) case d: return launch_mmd_mfma_d<d>(mode, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale, row_begin, n_rows, st, wide);
     CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20) CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64)
     CASE_D(80) CASE_D(96) CASE_D(128) CASE_D(160) CASE_D(192) CASE_D(224) CASE_D(256)
 #undef CASE_D
@@ -357,5 +632,5 @@ extern "C" int cgnn_launch_mmd_mfma(int mode, int D, const float* xhat, const fl
                                     const float* ynorm, float* gpart, float* lpart, int N, int R, int n_chunks,
                                     int tpc, float gscale, hipStream_t st) {
   return cgnn_launch_mmd_mfma_rows(mode, D, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale,
-                                   0, N, st);
+                                   0, N, st, -1);
 }

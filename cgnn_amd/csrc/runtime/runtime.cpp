@@ -117,6 +117,86 @@ py::tuple dag_program(int n_vars, const std::vector<std::vector<int>>& parents,
   return py::make_tuple(arr, param_off, max_in);
 }
 
+// Stage schedule of one DAG program for the level-scheduled generator kernels
+// (kernels/cgnn_staged.hip).  level(v) = 0 for observed / parentless nodes, else
+// 1 + max level of its parents.  Forward stages = levels in increasing order (record
+// order inside a level).  Backward sub-stages: the generated nodes of each level, levels
+// in decreasing order, split greedily (first fit, records in decreasing order) so that no
+// two nodes of one sub-stage share a parent -- each dL/dparent accumulation is then
+// owned by one wave.  Layout: [nf, nb, fwd_base, bwd_base | fwd starts[nf+1], fwd records |
+// bwd starts[nb+1], bwd records].  Returns (schedule, widest forward stage, widest
+// backward sub-stage).
+py::tuple dag_schedule(py::array_t<i32, py::array::c_style | py::array::forcecast> prog_a) {
+  const i32* prog = prog_a.data();
+  const i64 len = prog_a.size();
+  if (len < PROG_HDR) throw std::invalid_argument("dag_schedule: program too short");
+  const int nn = prog[0];
+  if (len < PROG_HDR + (i64)NODE_REC * nn) throw std::invalid_argument("dag_schedule: truncated program");
+  std::vector<int> level_of_var(nn, -1), level_of_rec(nn, 0);
+  int max_level = 0;
+  for (int k = 0; k < nn; ++k) {
+    const i32* rec = prog + PROG_HDR + (size_t)k * NODE_REC;
+    const int var = rec[0], kind = rec[1], npar = rec[2], paroff = rec[3];
+    if (var < 0 || var >= nn) throw std::invalid_argument("dag_schedule: variable out of range");
+    int lv = 0;
+    if (kind == 0)
+      for (int j = 0; j < npar; ++j) {
+        const int p = prog[paroff + j];
+        if (p < 0 || p >= nn || level_of_var[p] < 0)
+          throw std::invalid_argument("dag_schedule: parent not generated before its child");
+        lv = std::max(lv, level_of_var[p] + 1);
+      }
+    level_of_var[var] = lv;
+    level_of_rec[k] = lv;
+    max_level = std::max(max_level, lv);
+  }
+  std::vector<std::vector<int>> by_level(max_level + 1);
+  for (int k = 0; k < nn; ++k) by_level[level_of_rec[k]].push_back(k);
+  std::vector<std::vector<int>> fwd(by_level.begin(), by_level.end());
+  std::vector<std::vector<int>> bwd;
+  std::vector<char> used(nn, 0);
+  for (int lv = max_level; lv >= 0; --lv) {
+    std::vector<std::vector<int>> subs;
+    std::vector<std::vector<int>> sub_parents;
+    const auto& nodes = by_level[lv];
+    for (auto it = nodes.rbegin(); it != nodes.rend(); ++it) {
+      const int k = *it;
+      const i32* rec = prog + PROG_HDR + (size_t)k * NODE_REC;
+      if (rec[1] != 0) continue;                       // observed: nothing to train
+      const int npar = rec[2], paroff = rec[3];
+      size_t s = 0;
+      for (; s < subs.size(); ++s) {
+        bool clash = false;
+        for (int p : sub_parents[s]) used[p] = 1;
+        for (int j = 0; j < npar && !clash; ++j) clash = used[prog[paroff + j]] != 0;
+        for (int p : sub_parents[s]) used[p] = 0;
+        if (!clash) break;
+      }
+      if (s == subs.size()) { subs.emplace_back(); sub_parents.emplace_back(); }
+      subs[s].push_back(k);
+      for (int j = 0; j < npar; ++j) sub_parents[s].push_back(prog[paroff + j]);
+    }
+    for (auto& sb : subs) bwd.push_back(std::move(sb));
+  }
+  const int nf = (int)fwd.size(), nb = (int)bwd.size();
+  std::vector<i32> out(4);
+  int wf = 0, wb = 0;
+  auto emit = [&](const std::vector<std::vector<int>>& st, int& widest) {
+    int acc = 0;
+    out.push_back(0);
+    for (auto& v : st) { acc += (int)v.size(); out.push_back(acc); widest = std::max(widest, (int)v.size()); }
+    for (auto& v : st) for (int k : v) out.push_back(k);
+  };
+  out[0] = nf; out[1] = nb;
+  out[2] = (i32)out.size();
+  emit(fwd, wf);
+  out[3] = (i32)out.size();
+  emit(bwd, wb);
+  py::array_t<i32> arr(out.size());
+  std::copy(out.begin(), out.end(), arr.mutable_data());
+  return py::make_tuple(arr, wf, wb);
+}
+
 bool is_acyclic(int n, const std::vector<std::pair<int, int>>& edges) {
   std::vector<int> indeg(n, 0);
   std::vector<std::vector<int>> succ(n);
@@ -493,6 +573,7 @@ PYBIND11_MODULE(_rt, m) {
   m.def("dag_program", &dag_program, py::arg("n_vars"), py::arg("parents"), py::arg("kinds"),
         py::arg("confs"), py::arg("H"), py::arg("list_order") = std::vector<int>(),
         py::arg("n_conf") = 0);
+  m.def("dag_schedule", &dag_schedule, py::arg("prog"));
   m.def("is_acyclic", &is_acyclic);
   m.def("canonical_hash", &canonical_hash);
   m.def("csr_from_edges", &csr_from_edges, py::arg("n"), py::arg("src"), py::arg("dst"),

@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from .. import native
-from .program import Program, pack_programs
+from .program import Program, pack_programs, pack_schedules
 
 # padded variable counts with compiled kernels; above 64 only the matrix-core MMD
 SUPPORTED_D = (1, 2, 3, 4, 6, 8, 12, 16, 20, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
@@ -88,16 +88,30 @@ def mmd_kernel_choice(D: int, mmd_kernel: str = "auto") -> str:
 def device_supported(d: int, H: int, max_in: int, prog_len: int = 0) -> bool:
     """True when the device kernels cover a batch of ``d``-variable programs with hidden
     width ``H``, at most ``max_in`` generator inputs per node and programs of at most
-    ``prog_len`` ints (the variable count up to SUPPORTED_D[-1]; a generator forward
-    whose sample state plus program copy, and a backward whose state, fit in LDS).
+    ``prog_len`` ints: the variable count up to SUPPORTED_D[-1], and either the
+    per-sample generator kernels (sample state in LDS) or the level-scheduled ones.
     Otherwise ``score_jobs`` trains the batch on the CPU reference path (with a warning)."""
     if d > SUPPORTED_D[-1]:
         return False
     hip = native.hip()
     stride = (int(prog_len) + 3) // 4 * 4              # pack_programs' stride
-    if hip.gen_fwd_lds(padded_dim(d), stride) > 160 * 1024:
-        return False
-    return hip.gen_bwd_variant(int(H), int(max_in), int(d), stride) != 0
+    variant = hip.gen_bwd_variant(int(H), int(max_in), int(d), stride)
+    if variant == 1:
+        return hip.gen_fwd_lds(padded_dim(d), stride) <= 160 * 1024
+    return variant == 2
+
+
+def staged_setup(programs: Sequence[Program], H: int, max_in: int, d: int):
+    """Schedule + launch plan of the level-scheduled generator kernels for a batch:
+    (schedule [R, stride] int32, stride, waves per block, dL/dx in global memory)."""
+    sched, sstride, width = pack_schedules(programs)
+    W = 8
+    while W > 1 and W // 2 >= width:
+        W //= 2
+    plan = native.hip().staged_plan(int(d), int(H), int(max_in), W)
+    if not plan:
+        raise native.NativeExtensionError("staged generator kernels: no LDS plan for d=%d H=%d" % (d, H))
+    return sched, sstride, W, bool(plan[2])
 
 
 def _keys_tensor(keys, device):
@@ -125,11 +139,17 @@ class DeviceTrainer:
         D = padded_dim(d)
         self.R, self.N, self.d, self.D, self.H = R, N, d, D, int(H)
         prog, stride, P, max_in = pack_programs(programs)
-        self.P = P
+        self.P, self.prog_stride, self.max_in = P, stride, max_in
         self.bwd_variant = hip.gen_bwd_variant(int(H), int(max_in), int(d), int(stride))
         if self.bwd_variant == 0:
             raise native.NativeExtensionError(
                 "generator backward: H=%d with %d inputs per node does not fit in LDS" % (H, max_in))
+        self.staged = self.bwd_variant == 2
+        if self.staged:
+            sched, sstride, self.stage_w, dx_global = staged_setup(programs, H, max_in, d)
+        else:
+            sched, sstride, self.stage_w, dx_global = np.zeros((1, 4), np.int32), 4, 8, False
+        self.sched_stride = sstride
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         with torch.cuda.device(dev):
@@ -158,8 +178,9 @@ class DeviceTrainer:
             self.mirror = mmd_mirror_slots(D, N) if self.mmd_kernel == "valu" else 0
             self.gradp = torch.zeros(max(n_chunks + self.mirror, mf_chunks, 1), R, D, N, **f32)
             self.lpart = torch.zeros(R, n_parts, **f32)
-            G = hip.gen_bwd_blocks(N)
+            G = hip.staged_tiles(N) if self.staged else hip.gen_bwd_blocks(N)
             self.gpart = torch.zeros(R, G, P, **f32)
+            self.sched = torch.from_numpy(sched).to(dev)
             self.tt = torch.zeros(R, **f32)
             self.loss_last = torch.zeros(R, **f32)
             self.loss_acc = torch.zeros(R, **f32)
@@ -171,14 +192,15 @@ class DeviceTrainer:
             # squared row norms for the Gram-form (matrix-core) MMD
             self.xnorm = torch.zeros(R, N, **f32)
             self.ynorm = (self.data * self.data).sum(1).contiguous()
-            # sample-gradient scratch of the generic-width generator backward
-            self.dxs = torch.zeros(R, d, N, **f32) if self.bwd_variant == 2 else None
+            # dL/dx scratch of a staged backward whose sample state does not fit in LDS
+            self.dxs = torch.zeros(R, d, N, **f32) if dx_global else None
             # a dedicated (non-default) stream: hipGraph capture is not allowed on
             # the legacy null stream, and batches on different devices overlap
             self.stream = torch.cuda.Stream(dev)
             stream = self.stream
             icfg = [R, N, D, self.H, P, stride, max_in, row_tiles, n_chunks, tpc, self.hist_len,
-                    self.rff_k, d, self.NS, int(self.mmd_kernel == "mfma"), mf_chunks, mf_tpc, self.mirror]
+                    self.rff_k, d, self.NS, int(self.mmd_kernel == "mfma"), mf_chunks, mf_tpc, self.mirror,
+                    int(self.staged), sstride, self.stage_w]
             fcfg = [float(learning_rate), 0.9, 0.999, 1e-8, float(init_std)]
             ptrs = [t.data_ptr() for t in (self.prog, self.params, self.m, self.v, self.data,
                                            self.xhat, self.noise, self.gradp, self.lpart, self.gpart,
@@ -186,7 +208,7 @@ class DeviceTrainer:
             ptrs.append(self.hist.data_ptr() if self.hist_len else 0)
             ptrs += [self.step.data_ptr(), self.keys.data_ptr(), self.rff_w.data_ptr(),
                      self.rff_diff.data_ptr(), self.xnorm.data_ptr(), self.ynorm.data_ptr(),
-                     self.dxs.data_ptr() if self.dxs is not None else 0]
+                     self.dxs.data_ptr() if self.dxs is not None else 0, self.sched.data_ptr()]
             self.engine = hip.CgnnEngine(icfg, fcfg, ptrs, stream.cuda_stream)
         self.graph_chunk = int(graph_chunk)
 

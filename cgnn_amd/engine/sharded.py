@@ -35,7 +35,7 @@ import torch.distributed as dist
 
 from .. import native
 from ..parallel.sharded_mmd import _mfma_geometry, _valu_geometry, row_partials
-from .batch import _keys_tensor, mmd_kernel_choice, padded_dim
+from .batch import _keys_tensor, mmd_kernel_choice, padded_dim, staged_setup
 from .program import Program, pack_programs
 from .reference import ReferenceTrainer
 
@@ -112,6 +112,11 @@ class SampleShardedTrainer:
         if variant == 0:
             raise native.NativeExtensionError(
                 "generator backward: H=%d with %d inputs per node does not fit in LDS" % (self.H, max_in))
+        self.staged = variant == 2
+        dx_global = False
+        if self.staged:
+            sched, self.sstride, self.stage_w, dx_global = staged_setup(self.programs, self.H, max_in, d)
+            self.sched = torch.from_numpy(sched).to(self.device)
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
         self.prog = torch.from_numpy(prog).to(dev)
@@ -132,9 +137,9 @@ class SampleShardedTrainer:
         self.kernel = mmd_kernel_choice(D, mmd_kernel)
         self.vgeo = _valu_geometry(n, N, R)
         self.mgeo = _mfma_geometry(n, N, R)
-        G = hip.gen_bwd_blocks(n)
+        G = hip.staged_tiles(n) if self.staged else hip.gen_bwd_blocks(n)
         self.gpart = torch.zeros(R, G, P, **f32)
-        self.dxs = torch.zeros(R, d, n, **f32) if variant == 2 else None
+        self.dxs = torch.zeros(R, d, n, **f32) if dx_global else None
         self.dnorm = (self.data_all * self.data_all).sum(1).contiguous()
         self.st = torch.cuda.current_stream(dev).cuda_stream
         hip.init_params(self.params.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), self.prog.data_ptr(), stride, P,
@@ -156,9 +161,17 @@ class SampleShardedTrainer:
 
     def _device_step(self, train: bool) -> torch.Tensor:
         hip, R, D, n, N = self.hip, self.R, self.D, self.n_loc, self.N
-        hip.gen_fwd(self.prog.data_ptr(), self.stride, self.params.data_ptr(), self.P, self.data_loc.data_ptr(),
-                    self.xhat.data_ptr(), self.noise.data_ptr(), self.NS, self.xnorm.data_ptr(), self.keys_t.data_ptr(),
-                    self.step.data_ptr(), 0, n, D, self.H, R, self.st, row0=self.row0)
+        if self.staged:
+            hip.gen_noise(self.prog.data_ptr(), self.stride, self.keys_t.data_ptr(), self.step.data_ptr(), 0,
+                          self.noise.data_ptr(), self.NS, n, D, self.d, R, self.row0, self.st)
+            hip.gen_fwd_staged(self.prog.data_ptr(), self.stride, self.sched.data_ptr(), self.sstride,
+                               self.params.data_ptr(), self.P, self.data_loc.data_ptr(), self.xhat.data_ptr(),
+                               self.noise.data_ptr(), self.NS, self.xnorm.data_ptr(), n, D, self.d, self.H, R,
+                               self.stage_w, self.st)
+        else:
+            hip.gen_fwd(self.prog.data_ptr(), self.stride, self.params.data_ptr(), self.P, self.data_loc.data_ptr(),
+                        self.xhat.data_ptr(), self.noise.data_ptr(), self.NS, self.xnorm.data_ptr(),
+                        self.keys_t.data_ptr(), self.step.data_ptr(), 0, n, D, self.H, R, self.st, row0=self.row0)
         xall = self._gather_cols(self.xhat).contiguous()
         scale = 4.0 / (N * N) if train else 0.0
         mode = 0 if train else 1
@@ -177,9 +190,16 @@ class SampleShardedTrainer:
                     tpc, scale, self.st, row_begin=self.row0, n_rows=n)
         part = lp.sum(1) + self.tt_part                      # this rank's share of the loss (x N^2)
         if train:
-            hip.gen_bwd(self.prog.data_ptr(), self.stride, self.params.data_ptr(), self.P, self.xhat.data_ptr(),
-                        self.noise.data_ptr(), self.NS, gp.data_ptr(), nc, R, n, D, self.d, self.H, self.max_in,
-                        self.gpart.data_ptr(), self.st, dxs=self.dxs.data_ptr() if self.dxs is not None else 0)
+            if self.staged:
+                hip.gen_bwd_staged(self.prog.data_ptr(), self.stride, self.sched.data_ptr(), self.sstride,
+                                   self.params.data_ptr(), self.P, self.xhat.data_ptr(), self.noise.data_ptr(),
+                                   self.NS, gp.data_ptr(), nc, R, n, D, self.d, self.H, self.max_in, self.stage_w,
+                                   self.gpart.data_ptr(), self.dxs.data_ptr() if self.dxs is not None else 0,
+                                   self.st)
+            else:
+                hip.gen_bwd(self.prog.data_ptr(), self.stride, self.params.data_ptr(), self.P, self.xhat.data_ptr(),
+                            self.noise.data_ptr(), self.NS, gp.data_ptr(), nc, R, n, D, self.d, self.H,
+                            self.max_in, self.gpart.data_ptr(), self.st)
             g = self.gpart.sum(1, keepdim=True).contiguous()     # [R, 1, P], fixed order
             self._all_reduce(g)
             hip.adam(self.params.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), g.data_ptr(), 1, self.prog.data_ptr(),

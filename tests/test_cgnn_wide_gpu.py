@@ -86,20 +86,82 @@ def test_generic_width_backward_small_graph_matches_oracle(H):
     np.testing.assert_allclose(got, ref, rtol=3e-3, atol=1e-5)
 
 
-def test_generic_backward_bitwise_equals_specialised(monkeypatch):
-    """For a compiled H the generic-width backward is the same arithmetic in the same
-    order: scores are bitwise equal."""
-    g = _random_dag(12, seed=3)
+def test_staged_forward_bitwise_equals_per_sample(monkeypatch):
+    """The level-scheduled forward evaluates every node with the per-sample kernel's
+    fmaf order, and the noise kernel draws the same Philox normals: the generated
+    samples are bitwise equal."""
+    g = _random_dag(40, seed=3)
     prog = program_for_dag(g, 20)
-    datas = [_data(12, 300, s) for s in range(2)]
-    keys = [model_key(4, "gb", r) for r in range(2)]
-    a = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0")
-    assert a.bwd_variant == 1
-    sa = a.run(10, 4)
-    monkeypatch.setenv("CGNN_GEN_BWD_GENERIC", "1")
-    b = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0")
-    assert b.bwd_variant == 2
-    np.testing.assert_array_equal(b.run(10, 4), sa)
+    datas = [_data(40, 300, s) for s in range(3)]
+    keys = [model_key(4, "gb", r) for r in range(3)]
+    a = DeviceTrainer([prog] * 3, datas, keys, 20, "cuda:0")
+    assert a.bwd_variant == 1 and not a.staged
+    a.run(0, 1)
+    monkeypatch.setenv("CGNN_GEN_STAGED", "1")
+    b = DeviceTrainer([prog] * 3, datas, keys, 20, "cuda:0")
+    assert b.staged
+    b.run(0, 1)
+    np.testing.assert_array_equal(b.generated(), a.generated())
+    np.testing.assert_allclose(b.xnorm.cpu().numpy(), a.xnorm.cpu().numpy(), rtol=1e-6)
+
+
+def test_staged_training_matches_per_sample(monkeypatch):
+    """Same model trained by the per-sample and the level-scheduled kernels: only the
+    backward's summation orders differ."""
+    g = _random_dag(30, seed=4)
+    prog = program_for_dag(g, 20)
+    datas = [_data(30, 257, s) for s in range(2)]
+    keys = [model_key(5, "st", r) for r in range(2)]
+    sa = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0").run(12, 4)
+    monkeypatch.setenv("CGNN_GEN_STAGED", "1")
+    tb = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0")
+    assert tb.staged
+    np.testing.assert_allclose(tb.run(12, 4), sa, rtol=2e-4, atol=1e-7)
+    # bitwise reproducible run to run (no atomics)
+    tc = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0")
+    np.testing.assert_array_equal(tc.run(12, 4), tb.run(12, 4))
+
+
+@pytest.mark.parametrize("H", [20, 36])
+def test_staged_state_placements_bitwise(H):
+    """Sample state in LDS or in global memory: the same arithmetic in the same order."""
+    hip = native.hip()
+    d, N, R = 200, 150, 2
+    g = _random_dag(d, seed=9, max_par=3)
+    prog = program_for_dag(g, H)
+    datas = [_data(d, N, s) for s in range(R)]
+    keys = [model_key(8, "pl", r) for r in range(R)]
+    tr = DeviceTrainer([prog] * R, datas, keys, H, "cuda:0")
+    assert tr.staged
+    tr.run(3, 1)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream().cuda_stream
+    P, D, W = tr.P, tr.D, tr.stage_w
+    outs = []
+    for force in (0, 1):
+        xh = torch.zeros_like(tr.xhat)
+        xn = torch.zeros_like(tr.xnorm)
+        hip.gen_fwd_staged(tr.prog.data_ptr(), tr.prog_stride, tr.sched.data_ptr(), tr.sched_stride,
+                           tr.params.data_ptr(), P, tr.data.data_ptr(), xh.data_ptr(), tr.noise.data_ptr(), tr.NS,
+                           xn.data_ptr(), N, D, d, H, R, W, st, force=force)
+        outs.append((xh, xn))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    torch.manual_seed(0)
+    gradp = (torch.randn(2, R, D, N, device="cuda") * 1e-3).contiguous()
+    T = hip.staged_tiles(N)
+    grads = []
+    for force in (0, 1, 2):
+        gp = torch.zeros(R, T, P, device="cuda")
+        dxs = torch.zeros(R, d, N, device="cuda")
+        hip.gen_bwd_staged(tr.prog.data_ptr(), tr.prog_stride, tr.sched.data_ptr(), tr.sched_stride,
+                           tr.params.data_ptr(), P, outs[0][0].data_ptr(), tr.noise.data_ptr(), tr.NS,
+                           gradp.data_ptr(), 2, R, N, D, d, H, tr.max_in, W, gp.data_ptr(), dxs.data_ptr(), st,
+                           force=force)
+        grads.append(gp)
+    torch.cuda.synchronize()
+    assert torch.isfinite(grads[0]).all() and grads[0].abs().sum() > 0
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[0], grads[2])
 
 
 def test_wide_fourier_mmd_matches_oracle():

@@ -130,6 +130,66 @@ def test_pair_program_clamps_cause():
     assert p.n_params == (2 + 2) * 30 + 1
 
 
+def _check_schedule(prog):
+    from cgnn_amd.engine.program import stage_schedule
+    sched, wf, wb = stage_schedule(prog)
+    nf, nb, fb, bb = (int(x) for x in sched[:4])
+    recs = list(prog.node_records())
+    var_of = [r[0] for r in recs]
+    def stages(base, n):
+        starts = sched[base:base + n + 1]
+        items = sched[base + n + 1:]
+        return [[int(k) for k in items[starts[i]:starts[i + 1]]] for i in range(n)]
+    fwd, bwd = stages(fb, nf), stages(bb, nb)
+    # forward: every record once; parents strictly earlier
+    assert sorted(k for st in fwd for k in st) == list(range(len(recs)))
+    stage_of_var = {var_of[k]: i for i, st in enumerate(fwd) for k in st}
+    for k, (var, kind, pars, confs, poff, nin) in enumerate(recs):
+        for p in pars:
+            assert stage_of_var[p] < stage_of_var[var]
+    # backward: every generated record once; children before parents; no sub-stage
+    # shares a parent
+    gen = sorted(k for k, r in enumerate(recs) if r[1] == 0)
+    assert sorted(k for st in bwd for k in st) == gen
+    pos = {var_of[k]: i for i, st in enumerate(bwd) for k in st}
+    for st in bwd:
+        seen = set()
+        for k in st:
+            pars = recs[k][2]
+            assert not (seen & set(pars))
+            seen |= set(pars)
+            for p in pars:
+                if p in pos:
+                    assert pos[p] > pos[var_of[k]]
+    assert wf == max(len(s) for s in fwd) and wb == max(len(s) for s in bwd)
+    return fwd, bwd
+
+
+def test_stage_schedule_levels_and_conflict_free_backward():
+    """Level schedule of the wide-graph generator kernels (runtime dag_schedule)."""
+    rng = np.random.default_rng(0)
+    g = DirectedGraph()
+    names = ["V%d" % k for k in range(60)]
+    for k in range(1, 60):
+        for p in rng.choice(k, size=min(k, int(rng.integers(1, 5))), replace=False):
+            g.add(names[int(p)], names[k])
+    fwd, bwd = _check_schedule(program_for_dag(g, 20))
+    assert len(fwd) < 60 and len(bwd) >= len(fwd)
+    # diamond: B and C share parent A -> separate backward sub-stages
+    d = DirectedGraph()
+    for a, b in [("A", "B"), ("A", "C"), ("B", "D"), ("C", "D")]:
+        d.add(a, b)
+    fwd, bwd = _check_schedule(program_for_dag(d, 5))
+    assert [len(s) for s in fwd] == [1, 2, 1] and [len(s) for s in bwd] == [1, 1, 1, 1]
+    _check_schedule(program_for_pair(7))
+    skel = UndirectedGraph()
+    skel.add("a", "b")
+    skel.add("b", "c")
+    c = DirectedGraph(skeleton=skel)
+    c.add("a", "b")
+    _check_schedule(program_for_confounders(c, 5))
+
+
 def test_cyclic_graph_program_rejected():
     g = DirectedGraph()
     g.add("a", "b")
