@@ -9,7 +9,7 @@ One step = one full-graph training epoch (forward + backward + Adam) over all
 2,449,029 nodes (both dense layers at every row; the layer-2 aggregation at the
 train rows, the only rows whose logits reach the loss, and the layer-1
 aggregation at the rows with a train neighbour, the only ones those read --
-exact, see gnn/gcn.py; CGNN_L2_ALL_ROWS=1 aggregates every row).  Data: synthetic graph of the ogbn-products shape (no network
+exact, see gnn/gcn.py; GCNTrainer(train_rows_only=False) aggregates every row).  Data: synthetic graph of the ogbn-products shape (no network
 for the real dataset), random-init weights.  Multi-GPU: 1-D row partition of
 the graph over ranks (strong scaling: the whole job trains the same graph),
 an RCCL all-to-all of the layer-2 rows the rank's train rows read (a training

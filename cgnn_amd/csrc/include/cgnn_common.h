@@ -170,33 +170,20 @@ __device__ __forceinline__ f2 exp2_2(f2 x) {
 }
 
 // The seven kernel values exp(-g d2), g in {0.005, 0.05, 0.25, 0.5, 1, 5, 50},
-// for two distances.  CGNN_RBF_POW = 1 (default): two v_exp_f32
+// for two distances: two v_exp_f32
 // and powering -- a = e^{-0.005 d}, a^10 = e^{-0.05 d}; c = e^{-0.25 d}, c^2, c^4,
 // c^20 = e^{-5 d}, c^200 = e^{-50 d} (13 packed multiplies replace 5 exps; the
 // relative error of c^200 is ~200 ulp, i.e. ~1e-5 on a term that matters only
-// for d < 0.1).  CGNN_RBF_POW = 0: five exps + two squarings (compat build).
-#ifndef CGNN_RBF_POW
-#define CGNN_RBF_POW 1
-#endif
+// for d < 0.1).
 
 __device__ __forceinline__ void rbf7_values(f2 d2, f2* e) {
   const float L2E = 1.4426950408889634f;
-#if CGNN_RBF_POW
   const f2 a = exp2_2(d2 * (-0.005f * L2E));
   const f2 a2 = a * a, a4 = a2 * a2, a8 = a4 * a4;
   const f2 c = exp2_2(d2 * (-0.25f * L2E));
   const f2 c2 = c * c, c4 = c2 * c2, c8 = c4 * c4, c16 = c8 * c8, c20 = c16 * c4;
   const f2 c40 = c20 * c20, c80 = c40 * c40, c160 = c80 * c80;
   e[0] = a; e[1] = a8 * a2; e[2] = c; e[3] = c2; e[4] = c4; e[5] = c20; e[6] = c160 * c40;
-#else
-  e[0] = exp2_2(d2 * (-0.005f * L2E));
-  e[1] = exp2_2(d2 * (-0.05f * L2E));
-  e[2] = exp2_2(d2 * (-0.25f * L2E));
-  e[3] = e[2] * e[2];
-  e[4] = e[3] * e[3];
-  e[5] = exp2_2(d2 * (-5.0f * L2E));
-  e[6] = exp2_2(d2 * (-50.0f * L2E));
-#endif
 }
 
 // seven bandwidths for two distances at once; returns ks (kernel sum) and w

@@ -22,7 +22,6 @@ int cgnn_launch_mmd_mfma_rows(int, int, const float*, const float*, const float*
 int cgnn_gen_supported_h(int);
 int cgnn_gen_bwd_blocks(int);
 size_t cgnn_gen_bwd_lds(int, int, int, int);
-int cgnn_read_stamps(unsigned long long*);
 int cgnn_launch_mmd_rows(int, int, const float*, const float*, float*, float*, int, int, int, int, int,
                          float, int, int, hipStream_t, int);
 int cgnn_mmd_mirror_slots(int, int);
@@ -37,7 +36,7 @@ int cgnn_staged_tiles(int);
 int cgnn_launch_gen_noise(const int*, int, const uint32_t*, const int*, int, float*, int, int, int, int, int, int,
                           hipStream_t);
 int cgnn_launch_gen_fwd_staged(const int*, int, const int*, int, const float*, int, const float*, float*,
-                               const float*, int, float*, int, int, int, int, int, int, hipStream_t, int);
+                               const float*, int, float*, int, int, int, int, int, int, int, hipStream_t, int);
 int cgnn_launch_gen_bwd_staged(const int*, int, const int*, int, const float*, int, const float*, const float*, int,
                                const float*, int, int, int, int, int, int, int, int, float*, float*, hipStream_t,
                                int);
@@ -58,7 +57,7 @@ void cgnn_engine_run(void*, int, int, int, int);
 // Fourier (random-feature) MMD
 int rff_launch_freqs(float*, const uint32_t*, const int*, int, int, int, int, int, int, hipStream_t);
 int rff_launch_fwd_bwd(int, const float*, const float*, const float*, float*, float*, float*, int,
-                       int, int, int, int, float, hipStream_t);
+                       int, int, int, int, float, hipStream_t, int);
 // GNN track
 int gnn_launch_spmm(const int*, const int*, const void*, void*, const float*, const float*, int,
                     int, int, int, int, int, int, int, const float*, int, const float*, int, hipStream_t);
@@ -71,11 +70,7 @@ int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
 int gnn_spmm_ce_blocks(int, int);
 int gnn_launch_ell_build(const int*, const int*, int*, int, hipStream_t);
 int gnn_launch_spmm_ell(const int*, const int*, const void*, void*, const float*, int, int, int, int, hipStream_t);
-int gnn_spmm_win_rows(int);
 int gnn_slab_sum(const float*, long, int, float*, int, float*, const int*, hipStream_t);
-int gnn_spmm_win_plan(const int*, const int*, void*, int, int, int, int, int, hipStream_t);
-int gnn_launch_spmm_win(const int*, const int*, const void*, const void*, void*, const float*, int, int, int, int,
-                        int, int, int, int, int, int, hipStream_t);
 int gnn_launch_sample_neighbors(const int*, const int*, const int*, int, int, const int*, int*, uint32_t, uint32_t,
                                 uint32_t, hipStream_t);
 int gnn_launch_bias_relu_dropout(void*, const float*, long, int, int, float, uint32_t, uint32_t,
@@ -185,13 +180,14 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("NS"), py::arg("N"), py::arg("D"), py::arg("Dt"), py::arg("R"), py::arg("row0"), py::arg("st"));
   m.def("gen_fwd_staged", [](uint64_t prog, int ps, uint64_t sched, int ss, uint64_t params, int P, uint64_t data,
                              uint64_t xhat, uint64_t noise, int NS, uint64_t xnorm, int N, int D, int Dt, int H,
-                             int R, int W, uint64_t st, int force) {
+                             int max_in, int R, int W, uint64_t st, int force) {
     chk(cgnn_launch_gen_fwd_staged(Pt<const int>(prog), ps, Pt<const int>(sched), ss, Pt<const float>(params), P,
                                    Pt<const float>(data), Pt<float>(xhat), Pt<const float>(noise), NS,
-                                   Pt<float>(xnorm), N, D, Dt, H, R, W, S(st), force), "gen_fwd_staged");
+                                   Pt<float>(xnorm), N, D, Dt, H, max_in, R, W, S(st), force), "gen_fwd_staged");
   }, py::arg("prog"), py::arg("ps"), py::arg("sched"), py::arg("ss"), py::arg("params"), py::arg("P"),
      py::arg("data"), py::arg("xhat"), py::arg("noise"), py::arg("NS"), py::arg("xnorm"), py::arg("N"), py::arg("D"),
-     py::arg("Dt"), py::arg("H"), py::arg("R"), py::arg("W"), py::arg("st"), py::arg("force") = -1);
+     py::arg("Dt"), py::arg("H"), py::arg("max_in"), py::arg("R"), py::arg("W"), py::arg("st"),
+     py::arg("force") = -1);
   m.def("gen_bwd_staged", [](uint64_t prog, int ps, uint64_t sched, int ss, uint64_t params, int P, uint64_t xhat,
                              uint64_t noise, int NS, uint64_t gradp, int nch, int R, int N, int D, int Dt, int H,
                              int max_in, int W, uint64_t gpart, uint64_t dxs, uint64_t st, int force) {
@@ -203,14 +199,6 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("xhat"), py::arg("noise"), py::arg("NS"), py::arg("gradp"), py::arg("nch"), py::arg("R"), py::arg("N"),
      py::arg("D"), py::arg("Dt"), py::arg("H"), py::arg("max_in"), py::arg("W"), py::arg("gpart"), py::arg("dxs"),
      py::arg("st"), py::arg("force") = -1);
-  m.def("read_stamps", []() {
-    unsigned long long v[16] = {0};
-    const int rc = cgnn_read_stamps(v);
-    py::list out;
-    if (rc == 0)
-      for (int k = 0; k < 16; ++k) out.append(v[k]);
-    return out;
-  });
 
   m.def("mmd", [](int mode, int D, uint64_t xhat, uint64_t data, uint64_t gp, uint64_t lp, int N, int R,
                   int row_tiles, int n_chunks, int tpc, float gscale, uint64_t st, int row_begin, int n_rows,
@@ -271,11 +259,15 @@ PYBIND11_MODULE(_hip, m) {
         "rff_freqs");
   });
   m.def("rff_fwd_bwd", [](int mode, uint64_t xhat, uint64_t data, uint64_t w, uint64_t feat, uint64_t loss,
-                          uint64_t grad, int N, int D, int F, int R, int k, float norm, uint64_t st) {
+                          uint64_t grad, int N, int D, int F, int R, int k, float norm, uint64_t st,
+                          int force_valu) {
     chk(rff_launch_fwd_bwd(mode, Pt<const float>(xhat), Pt<const float>(data), Pt<const float>(w),
-                           Pt<float>(feat), Pt<float>(loss), Pt<float>(grad), N, D, F, R, k, norm, S(st)),
+                           Pt<float>(feat), Pt<float>(loss), Pt<float>(grad), N, D, F, R, k, norm, S(st),
+                           force_valu),
         "rff_fwd_bwd");
-  });
+  }, py::arg("mode"), py::arg("xhat"), py::arg("data"), py::arg("w"), py::arg("feat"), py::arg("loss"),
+     py::arg("grad"), py::arg("N"), py::arg("D"), py::arg("F"), py::arg("R"), py::arg("k"), py::arg("norm"),
+     py::arg("st"), py::arg("force_valu") = 0);
 
   m.def("gnn_spmm", [](uint64_t rowptr, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, uint64_t bias,
                        int n_rows, int F, int ld_x, int ld_y, int x_bf16, int y_bf16, int relu, int unit_col,
@@ -315,23 +307,10 @@ PYBIND11_MODULE(_hip, m) {
     chk(gnn_launch_spmm_ell(Pt<const int>(ell), Pt<const int>(col), Pt<const void>(x), Pt<void>(y),
                             Pt<const float>(rscale), n_rows, F, ldx, ldy, S(st)), "gnn_spmm_ell");
   });
-  m.def("gnn_spmm_win_rows", &gnn_spmm_win_rows);
   m.def("gnn_slab_sum", [](uint64_t P, long rows, int W, uint64_t stage, int G, uint64_t out, uint64_t map,
                            uint64_t st) {
     chk(gnn_slab_sum(Pt<const float>(P), rows, W, Pt<float>(stage), G, Pt<float>(out), Pt<const int>(map), S(st)),
         "gnn_slab_sum");
-  });
-  m.def("gnn_spmm_win_plan", [](uint64_t rowptr, uint64_t col, uint64_t split, int n_rows, int row_off, int n_src,
-                                int R, int WR, uint64_t st) {
-    chk(gnn_spmm_win_plan(Pt<const int>(rowptr), Pt<const int>(col), Pt<void>(split), n_rows, row_off, n_src, R, WR,
-                          S(st)), "gnn_spmm_win_plan");
-  });
-  m.def("gnn_spmm_win", [](uint64_t rowptr, uint64_t col, uint64_t split, uint64_t x, uint64_t y, uint64_t rscale,
-                           int n_rows, int F, int ld_x, int ld_y, int unit_col, int row_off, int n_src, int R, int WR,
-                           int lp, uint64_t st) {
-    chk(gnn_launch_spmm_win(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(split), Pt<const void>(x),
-                            Pt<void>(y), Pt<const float>(rscale), n_rows, F, ld_x, ld_y, unit_col, row_off, n_src,
-                            R, WR, lp, S(st)), "gnn_spmm_win");
   });
   m.def("gnn_sample_neighbors", [](uint64_t rowptr, uint64_t col, uint64_t nodes, int n, int fanout, uint64_t out_ptr,
                                    uint64_t out_col, uint32_t k0, uint32_t k1, uint32_t salt, uint64_t st) {

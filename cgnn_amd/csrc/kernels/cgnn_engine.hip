@@ -34,7 +34,7 @@ int cgnn_staged_tiles(int);
 int cgnn_launch_gen_noise(const int*, int, const uint32_t*, const int*, int, float*, int, int, int, int, int, int,
                           hipStream_t);
 int cgnn_launch_gen_fwd_staged(const int*, int, const int*, int, const float*, int, const float*, float*,
-                               const float*, int, float*, int, int, int, int, int, int, hipStream_t, int);
+                               const float*, int, float*, int, int, int, int, int, int, int, hipStream_t, int);
 int cgnn_launch_gen_bwd_staged(const int*, int, const int*, int, const float*, int, const float*, const float*, int,
                                const float*, int, int, int, int, int, int, int, int, float*, float*, hipStream_t,
                                int);
@@ -47,7 +47,7 @@ int cgnn_launch_init(float*, float*, float*, const int*, int, int, const uint32_
 int cgnn_launch_advance(int*, int, int, hipStream_t);
 int rff_launch_freqs(float*, const uint32_t*, const int*, int, int, int, int, int, int, hipStream_t);
 int rff_launch_fwd_bwd(int, const float*, const float*, const float*, float*, float*, float*, int,
-                       int, int, int, int, float, hipStream_t);
+                       int, int, int, int, float, hipStream_t, int);
 }
 
 namespace cgnn {
@@ -131,7 +131,7 @@ class Engine {
                              c_.R, st_), "rff_freqs");
       check(rff_launch_fwd_bwd(train ? 0 : 1, b_.xhat, b_.data, b_.rff_w, b_.rff_diff, b_.lpart,
                                b_.gradp, c_.N, c_.D, rff_features(), c_.R, c_.rff_k,
-                               sqrtf(2.f / (float)c_.rff_k), st_), "rff");
+                               sqrtf(2.f / (float)c_.rff_k), st_, 0), "rff");
     } else if (c_.mfma) {
       const float inv = 1.f / ((float)c_.N * (float)c_.N);
       check(cgnn_launch_mmd_mfma(train ? (need_loss ? 0 : 3) : 1, c_.D, b_.xhat, b_.data, b_.xnorm, b_.ynorm,
@@ -174,8 +174,8 @@ class Engine {
       check(cgnn_launch_gen_noise(b_.prog, c_.prog_stride, b_.keys, b_.step, off, b_.noise, c_.NS, c_.N, c_.D,
                                   c_.d_true, c_.R, 0, st_), "gen_noise");
       check(cgnn_launch_gen_fwd_staged(b_.prog, c_.prog_stride, b_.sched, c_.sched_stride, b_.params, c_.P, b_.data,
-                                       b_.xhat, b_.noise, c_.NS, b_.xnorm, c_.N, c_.D, c_.d_true, c_.H, c_.R,
-                                       c_.stage_w, st_, -1), "gen_fwd_staged");
+                                       b_.xhat, b_.noise, c_.NS, b_.xnorm, c_.N, c_.D, c_.d_true, c_.H, c_.max_in,
+                                       c_.R, c_.stage_w, st_, -1), "gen_fwd_staged");
     } else {
       check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
                                 b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_, 0), "gen_fwd");

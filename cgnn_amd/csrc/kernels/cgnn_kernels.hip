@@ -259,35 +259,6 @@ __global__ __launch_bounds__(256) void loss_finalize_kernel(
   }
 }
 
-// ---- optional phase timing of the generator backward (s_memtime stamps of one wave;
-// build with CGNN_STAMP=1, read with _hip.read_stamps(); tools/bench_cgnn_batch.py
-// prints them) ----
-#ifndef CGNN_STAMP
-#define CGNN_STAMP 0
-#endif
-#if CGNN_STAMP
-__device__ unsigned long long cgnn_stamps[16];
-__device__ __forceinline__ unsigned long long stamp_now() {
-  unsigned long long v;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return v;
-}
-#define STAMP(slot, since) do { const unsigned long long _n = stamp_now(); st_acc[slot] += _n - since; since = _n; } while (0)
-#else
-#define STAMP(slot, since) do { } while (0)
-#endif
-extern "C" int cgnn_read_stamps(unsigned long long* out) {
-#if CGNN_STAMP
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(cgnn_stamps), sizeof(unsigned long long) * 16);
-#else
-  (void)out;
-  return -1;
-#endif
-}
-
-// wave-uniform read of an LDS-resident program word (lands in an SGPR)
 
 // ============================================================================
 // K1: generator forward.  grid = (ceil(N/256), R), one thread per sample.
@@ -446,11 +417,6 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
   const float* xr = xhat + (size_t)r * D * N;
   const float* nz = noise + (size_t)r * NS * N;
   float* gp = gpart + ((size_t)r * G + blk) * P;
-#if CGNN_STAMP
-  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long st_t = stamp_now();
-  const unsigned long long st_t0 = st_t;
-#endif
 
   // sample state; dL/dxhat = fixed-order sum of the MMD column chunks (0 on padding rows)
   for (int v = 0; v < Dt; ++v) {
@@ -465,7 +431,6 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
   float* my_z = s_z + t * HE;
   float* my_in = s_in + t * SI;
   __syncthreads();
-  STAMP(0, st_t);
   const int nn = uni(s_prog);
   float e_cur = (nn > 0 && valid) ? nz[(size_t)uni(s_prog + PROG_HDR + (nn - 1) * NODE_REC) * N + n] : 0.f;
 
@@ -510,9 +475,7 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
       s_dx[uni(s_prog + paroff + j) * BS + t] += s;
     }
     e_cur = e_next;
-    STAMP(1, st_t);
     __syncthreads();
-    STAMP(2, st_t);
 
     // ---- reduction phase ----
     const int n_w1 = (nin + 1) * HP;           // Gm items: rows 0..nin, column pairs
@@ -564,7 +527,6 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
     if (split) {
       f2 acc = {0.f, 0.f};
       if (lane < n_items) acc = item(lane, wave * 64, 64);
-      STAMP(3, st_t);
       if (wave == 1) s_red[lane] = acc;
       __syncthreads();
       if (wave == 0) {
@@ -578,16 +540,8 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
       __syncthreads();
       if (t < H) emit_w2(t);
     }
-    STAMP(4, st_t);
     __syncthreads();
-    STAMP(5, st_t);
   }
-#if CGNN_STAMP
-  if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0) {
-    for (int k = 0; k < 6; ++k) cgnn_stamps[k] = st_acc[k];
-    cgnn_stamps[6] = stamp_now() - st_t0;
-  }
-#endif
 }
 
 // ============================================================================

@@ -25,6 +25,8 @@
 //
 // Sample state: x (and dL/dx in the backward) live in LDS ([Dt][64] each) while they fit,
 // otherwise in global memory (xhat itself / the dxs scratch) -- the launcher picks.
+// The parameter buffer must extend 64 floats (engine.batch.PARAM_PAD) past its last model (the backward's
+// tail-chunk weight loads run past a node's last row and are zeroed).
 // The schedule (engine/program.py stage_schedule, built by the C++ runtime):
 //   [0] n_fwd_stages [1] n_bwd_stages [2] fwd_base [3] bwd_base
 //   at fwd_base: starts[n_fwd + 1], then program record indices; same at bwd_base.
@@ -32,7 +34,6 @@
 // L2 and its weight stream.
 #include "cgnn_common.h"
 #include <algorithm>
-#include <type_traits>
 
 using namespace cgnn;
 
@@ -75,7 +76,9 @@ template <int HC, bool XG>
 __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
     const int* __restrict__ prog, int ps, const int* __restrict__ sched, int ss,
     const float* __restrict__ params, int P, const float* __restrict__ data, float* __restrict__ xhat,
-    const float* __restrict__ noise, int NS, float* __restrict__ xnorm, int N, int D, int Dt, int H, int T) {
+    const float* __restrict__ noise, int NS, float* __restrict__ xnorm, int N, int D, int Dt, int H, int T,
+    int max_in) {
+  constexpr int HCS = (HC + 3) & ~3;      // weight-slab row stride (16-B aligned rows)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int W = blockDim.x >> 6;
   const int wave = wave_id(), lane = threadIdx.x & 63;
@@ -92,6 +95,7 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
   float* xr = xhat + (size_t)r * D * N;
   float* s_x = smem;                                        // [Dt][64] (LDS state)
   float* s_nrm = smem + (XG ? 0 : (size_t)Dt * WAVE);       // [W][64]
+  float* s_w = s_nrm + W * WAVE + (size_t)wave * (max_in + 2) * HCS;   // this wave's weight rows
   auto xget = [&](int v) -> float { return XG ? xr[(size_t)v * N + nc] : s_x[v * WAVE + lane]; };
   auto xput = [&](int v, float val) {
     if (XG) {
@@ -117,28 +121,59 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
       const int npar = uni(nd + 2), paroff = uni(nd + 3), ncf = uni(nd + 4), cfoff = uni(nd + 5);
       const int poff = uni(nd + 6);
       const int nin = npar + 1 + ncf;
-      const float* W1 = th + poff;
-      const float* b1 = W1 + (size_t)nin * H;
-      const float* W2 = b1 + H;
+      const float* W1 = th + poff;       // rows 0..nin: W1ext (row nin = b1), row nin + 1: W2
       const float e_own = nz[(size_t)var * N + nc];
-      float out = W2[H];
-      // same per-unit fmaf order as gen_fwd_kernel: own noise + bias, parents, confounders
+      float out = W1[(size_t)(nin + 2) * H];                       // b2
       for (int q0 = 0; q0 < H; q0 += HC) {
+        // this chunk's weights (rows 0..nin+1, HC units) into the wave's slab: one load
+        // per lane and 64 weights, all issued together
+        const int nel = (nin + 2) * HC;
+        for (int e0 = 0; e0 < nel; e0 += 4 * WAVE) {
+          float wv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int e = min(e0 + WAVE * k + lane, nel - 1);
+            wv[k] = W1[(e / HC) * H + q0 + e % HC];
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int e = e0 + WAVE * k + lane;
+            if (e < nel) s_w[(e / HC) * HCS + e % HC] = wv[k];
+          }
+        }
+        wave_sync();
+        // same per-unit fmaf order as gen_fwd_kernel: own noise + bias, parents, confounders
         float pre[HC];
 #pragma unroll
-        for (int q = 0; q < HC; ++q) pre[q] = fmaf(W1[npar * H + q0 + q], e_own, b1[q0 + q]);
-        for (int j = 0; j < npar; ++j) {
-          const float x = xget(uni(pg + paroff + j));
+        for (int q = 0; q < HC; ++q) pre[q] = fmaf(s_w[npar * HCS + q], e_own, s_w[nin * HCS + q]);
+        // parents then confounder streams, in order; each batch of 8 inputs is loaded
+        // before the first use (no load -> wait -> use chain per input)
+        for (int j0 = 0; j0 < npar; j0 += 8) {
+          float v[8];
 #pragma unroll
-          for (int q = 0; q < HC; ++q) pre[q] = fmaf(W1[j * H + q0 + q], x, pre[q]);
+          for (int jj = 0; jj < 8; ++jj) v[jj] = xget(uni(pg + paroff + min(j0 + jj, npar - 1)));
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj)
+            if (j0 + jj < npar) {
+#pragma unroll
+              for (int q = 0; q < HC; ++q) pre[q] = fmaf(s_w[(j0 + jj) * HCS + q], v[jj], pre[q]);
+            }
         }
-        for (int c = 0; c < ncf; ++c) {
-          const float ec = nz[(size_t)(D + uni(pg + cfoff + c)) * N + nc];
+        for (int c0 = 0; c0 < ncf; c0 += 8) {
+          float v[8];
 #pragma unroll
-          for (int q = 0; q < HC; ++q) pre[q] = fmaf(W1[(npar + 1 + c) * H + q0 + q], ec, pre[q]);
+          for (int cc = 0; cc < 8; ++cc)
+            v[cc] = nz[(size_t)(D + uni(pg + cfoff + min(c0 + cc, ncf - 1))) * N + nc];
+#pragma unroll
+          for (int cc = 0; cc < 8; ++cc)
+            if (c0 + cc < ncf) {
+#pragma unroll
+              for (int q = 0; q < HC; ++q) pre[q] = fmaf(s_w[(npar + 1 + c0 + cc) * HCS + q], v[cc], pre[q]);
+            }
         }
 #pragma unroll
-        for (int q = 0; q < HC; ++q) out = fmaf(W2[q0 + q], fmaxf(pre[q], 0.f), out);
+        for (int q = 0; q < HC; ++q) out = fmaf(s_w[(nin + 1) * HCS + q], fmaxf(pre[q], 0.f), out);
+        wave_sync();                           // slab reads done before the next chunk's writes
       }
       xput(var, out);
     }
@@ -167,10 +202,11 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
 }
 
 // --------------------------------------------------------------------------- backward
-// per-wave LDS slab (floats): input rows [64][SI], mg rows [64][ZS], Gm pairs
+// per-wave LDS slab (floats)
 __host__ __device__ __forceinline__ int bwd_si(int max_in) { return (max_in + 2) | 1; }
 __host__ __device__ __forceinline__ int bwd_slab(int max_in) {
-  return WAVE * (bwd_si(max_in) + 1) + WAVE * ZS + (max_in + 1) * HZ;   // [64][SI] padded even
+  // [64][SI] (padded even) + [64][ZS] + Gm pairs + weight rows + dL/dparent partials
+  return WAVE * (bwd_si(max_in) + 1) + WAVE * ZS + (max_in + 1) * HZ + (max_in + 2) * HZ + max_in * WAVE;
 }
 
 template <bool XG, bool DG>
@@ -201,6 +237,8 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
   float* s_in = slab;                                        // [64][SI]
   float* s_z = slab + WAVE * (SI + 1);                       // [64][ZS]
   f2* s_g = reinterpret_cast<f2*>(s_z + WAVE * ZS);          // [(max_in + 1) * HZP]
+  float* s_w = s_z + WAVE * ZS + (max_in + 1) * HZ;          // [max_in + 2][16] weight rows
+  float* s_pp = s_w + (max_in + 2) * HZ;                     // [max_in][64] dL/dparent
   float* my_in = s_in + lane * SI;
   float* my_z = s_z + lane * ZS;
 
@@ -231,56 +269,84 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
       const int var = uni(nd), npar = uni(nd + 2), paroff = uni(nd + 3), ncf = uni(nd + 4);
       const int cfoff = uni(nd + 5), poff = uni(nd + 6);
       const int nin = npar + 1 + ncf;
-      const float* W1 = th + poff;       // W1ext rows 0..nin (row nin = b1)
-      const float* W2 = W1 + (size_t)(nin + 1) * H;
-      float gout = 0.f;
-      if (valid) gout = DG ? dx[(size_t)var * N + n] : s_dx[var * WAVE + lane];
-
-      for (int j = 0; j < nin; ++j) {
-        float x;
-        if (j < npar) x = xget(uni(pg + paroff + j));
-        else if (j == npar) x = nz[(size_t)var * N + nc];
-        else x = nz[(size_t)(D + uni(pg + cfoff + (j - npar - 1))) * N + nc];
-        my_in[j] = x;
+      const float* W1 = th + poff;       // rows 0..nin: W1ext (row nin = b1), row nin + 1: W2
+      // dL/dx of this node and its input row [parents, own noise, confounder streams]:
+      // every load issued before the first use (batches of 8).  The pool holds the
+      // parents then the confounder ids (cf_off = par_off + n_par), so input j != n_par
+      // is pool entry par_off + j (- 1 past the own noise); every load is in bounds and
+      // the unused ones are discarded.
+      const float g_ld = DG ? dx[(size_t)var * N + nc] : s_dx[var * WAVE + lane];
+      for (int j0 = 0; j0 < nin; j0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int j = min(j0 + jj, nin - 1);
+          const int pe = uni(pg + paroff + (j < npar ? j : j - 1));
+          const int row = j < npar ? pe : (j == npar ? var : D + pe);
+          if (XG) {
+            const float* base = j < npar ? xr : nz;
+            v[jj] = base[(size_t)row * N + nc];
+          } else {
+            const float a = s_x[(j < npar ? pe : 0) * WAVE + lane];
+            const float b = nz[(size_t)row * N + nc];
+            v[jj] = j < npar ? a : b;
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+          if (j0 + jj < nin) my_in[j0 + jj] = v[jj];
       }
       my_in[nin] = 1.f;
+      const float gout = valid ? g_ld : 0.f;
 
       for (int q0 = 0; q0 < H; q0 += HZ) {
         const int hc = min(HZ, H - q0);
-        // ---- recompute this chunk's pre-activations (one sample per lane).  A full
-        // chunk reads 16 contiguous weights per row (wide scalar loads); the tail chunk
-        // clamps its indices to the node's own parameters and zeroes the extra units ----
-        float mg[HZ];
-        auto chunk = [&](auto full) {
-          constexpr bool FULL = decltype(full)::value;
-          auto wi = [&](int row, int q) -> float {
-            return FULL ? W1[row * H + q0 + q] : W1[row * H + q0 + min(q, hc - 1)];
-          };
-          float pre[HZ];
+        // ---- stage this chunk's weights (rows 0..nin+1, 16 units) in the slab: one
+        // load per lane and 64 weights, all issued together.  Units q >= hc of a tail
+        // chunk read past their row (the parameter buffer is padded) and are zeroed ----
+        const int nel = (nin + 2) * HZ;
+        for (int e0 = 0; e0 < nel; e0 += 4 * WAVE) {
+          float wv[4];
 #pragma unroll
-          for (int q = 0; q < HZ; ++q) pre[q] = wi(nin, q);
-          for (int j = 0; j < nin; ++j) {
-            const float x = my_in[j];
-#pragma unroll
-            for (int q = 0; q < HZ; ++q) pre[q] = fmaf(wi(j, q), x, pre[q]);
+          for (int k = 0; k < 4; ++k) {
+            const int e = min(e0 + WAVE * k + lane, nel - 1);
+            wv[k] = W1[(e >> 4) * H + q0 + (e & 15)];
           }
 #pragma unroll
-          for (int q = 0; q < HZ; ++q) mg[q] = ((FULL || q < hc) && pre[q] > 0.f) ? gout : 0.f;
-          // this chunk's share of dL/dparent (the parent is this wave's alone)
-          for (int j = 0; j < npar; ++j) {
-            float s = 0.f;
+          for (int k = 0; k < 4; ++k) {
+            const int e = e0 + WAVE * k + lane;
+            if (e < nel) s_w[e] = (e & 15) < hc ? wv[k] : 0.f;
+          }
+        }
+        wave_sync();
+        auto wrow = [&](int row, float* w) {        // 16 weights of a row (LDS broadcast)
 #pragma unroll
-            for (int q = 0; q < HZ; ++q) s = fmaf(wi(j, q) * wi(nin + 1, q), mg[q], s);
-            const int pv = uni(pg + paroff + j);
-            if (DG) {
-              if (valid) dx[(size_t)pv * N + n] += s;
-            } else {
-              s_dx[pv * WAVE + lane] += s;
-            }
+          for (int c = 0; c < HZ / 4; ++c) {
+            const float4 v4 = *reinterpret_cast<const float4*>(s_w + row * HZ + 4 * c);
+            w[4 * c] = v4.x; w[4 * c + 1] = v4.y; w[4 * c + 2] = v4.z; w[4 * c + 3] = v4.w;
           }
         };
-        if (hc == HZ) chunk(std::true_type{});
-        else chunk(std::false_type{});
+        // ---- recompute this chunk's pre-activations (one sample per lane) ----
+        float pre[HZ], w[HZ], w2[HZ];
+        wrow(nin, pre);
+        for (int j = 0; j < nin; ++j) {
+          const float x = my_in[j];
+          wrow(j, w);
+#pragma unroll
+          for (int q = 0; q < HZ; ++q) pre[q] = fmaf(w[q], x, pre[q]);
+        }
+        float mg[HZ];
+#pragma unroll
+        for (int q = 0; q < HZ; ++q) mg[q] = (q < hc && pre[q] > 0.f) ? gout : 0.f;
+        // ---- this chunk's share of dL/dparent, kept in the slab until the node ends ----
+        wrow(nin + 1, w2);
+        for (int j = 0; j < npar; ++j) {
+          wrow(j, w);
+          float s = 0.f;
+#pragma unroll
+          for (int q = 0; q < HZ; ++q) s = fmaf(w[q] * w2[q], mg[q], s);
+          s_pp[j * WAVE + lane] = q0 == 0 ? s : s_pp[j * WAVE + lane] + s;
+        }
 #pragma unroll
         for (int qp = 0; qp < HZP; ++qp)
           *reinterpret_cast<f2*>(my_z + 2 * qp) = f2{mg[2 * qp], mg[2 * qp + 1]};
@@ -314,10 +380,11 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
           if (grp >= 2) acc += f2{__shfl_xor(acc.x, 32), __shfl_xor(acc.y, 32)};
           if (grp == 4) acc += f2{__shfl_xor(acc.x, 16), __shfl_xor(acc.y, 16)};
           if (part == 0 && it < n_items) {
-            const int j = it / hp, qp = it - j * hp, q = q0 + 2 * qp;
+            const int j = it / hp, qp = it - j * hp, q = 2 * qp;
+            const f2 w2p = *reinterpret_cast<const f2*>(s_w + (nin + 1) * HZ + q);
             s_g[j * HZP + qp] = acc;
-            gp[poff + j * H + q] = W2[q] * acc.x;                   // dW1 / db1
-            if (2 * qp + 1 < hc) gp[poff + j * H + q + 1] = W2[q + 1] * acc.y;
+            gp[poff + j * H + q0 + q] = w2p.x * acc.x;                 // dW1 / db1
+            if (q + 1 < hc) gp[poff + j * H + q0 + q + 1] = w2p.y * acc.y;
           }
         }
         wave_sync();
@@ -326,11 +393,32 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
           float s = 0.f;
           for (int j = 0; j <= nin; ++j) {
             const f2 gm = s_g[j * HZP + (lane >> 1)];
-            s = fmaf(W1[j * H + q0 + lane], (lane & 1) ? gm.y : gm.x, s);
+            s = fmaf(s_w[j * HZ + lane], (lane & 1) ? gm.y : gm.x, s);
           }
           gp[poff + (nin + 1) * H + q0 + lane] = s;
         }
         wave_sync();
+      }
+      // ---- push dL/dparent (each parent is this wave's alone in the sub-stage):
+      // the read-modify-writes of a batch of 8 parents issued together ----
+      for (int j0 = 0; j0 < npar; j0 += 8) {
+        float cur[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int pv = uni(pg + paroff + min(j0 + jj, npar - 1));
+          cur[jj] = DG ? dx[(size_t)pv * N + nc] : s_dx[pv * WAVE + lane];
+        }
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+          if (j0 + jj < npar) {
+            const int pv = uni(pg + paroff + j0 + jj);
+            const float v = cur[jj] + s_pp[(j0 + jj) * WAVE + lane];
+            if (DG) {
+              if (valid) dx[(size_t)pv * N + n] = v;
+            } else {
+              s_dx[pv * WAVE + lane] = v;
+            }
+          }
       }
       const float g2 = wave_sum(gout);                               // db2
       if (lane == 0) gp[poff + (nin + 2) * H] = g2;
@@ -348,17 +436,21 @@ void allow_lds(K kernel, size_t lds) {
 
 constexpr size_t LDS_MAX = 160 * 1024;
 
-size_t fwd_lds(int Dt, int W, bool xg) { return sizeof(float) * ((xg ? 0 : (size_t)Dt * WAVE) + (size_t)W * WAVE); }
-size_t bwd_lds(int Dt, int W, int max_in, bool xg, bool dg) {
-  return sizeof(float) * ((xg ? 0 : (size_t)Dt * WAVE) + (dg ? 0 : (size_t)Dt * WAVE) + (size_t)W * bwd_slab(max_in));
-}
-
 int fwd_hc(int H) {
   static const int cand[] = {32, 20, 16, 12, 10, 8, 6, 5, 4, 3, 2, 1};
   for (int c : cand)
     if (H % c == 0) return c;
   return 1;
 }
+
+size_t fwd_lds(int Dt, int W, bool xg, int max_in, int hc) {
+  const size_t hcs = (size_t)((hc + 3) & ~3);
+  return sizeof(float) * ((xg ? 0 : (size_t)Dt * WAVE) + (size_t)W * WAVE + (size_t)W * (max_in + 2) * hcs);
+}
+size_t bwd_lds(int Dt, int W, int max_in, bool xg, bool dg) {
+  return sizeof(float) * ((xg ? 0 : (size_t)Dt * WAVE) + (dg ? 0 : (size_t)Dt * WAVE) + (size_t)W * bwd_slab(max_in));
+}
+
 
 }  // namespace
 
@@ -367,7 +459,7 @@ int fwd_hc(int H) {
 // or -1 when even the all-global variant does not fit (only for absurd max_in).
 extern "C" int cgnn_staged_plan(int Dt, int H, int max_in, int W, int* out) {
   if (Dt < 1 || H < 1 || W < 1 || W > 8) return -1;
-  const int fxg = fwd_lds(Dt, W, false) <= LDS_MAX ? 0 : 1;
+  const int fxg = fwd_lds(Dt, W, false, max_in, fwd_hc(H)) <= LDS_MAX ? 0 : 1;
   int wb = W, bxg = -1, bdg = -1;
   for (; wb >= 1 && bxg < 0; wb >>= 1) {
     if (bwd_lds(Dt, wb, max_in, false, false) <= LDS_MAX) { bxg = 0; bdg = 0; }
@@ -396,20 +488,21 @@ extern "C" int cgnn_launch_gen_noise(const int* prog, int ps, const uint32_t* ke
 // plan's state placement, 0 LDS, 1 global (tests: every placement is bitwise the same)
 extern "C" int cgnn_launch_gen_fwd_staged(const int* prog, int ps, const int* sched, int ss, const float* params,
                                           int P, const float* data, float* xhat, const float* noise, int NS,
-                                          float* xnorm, int N, int D, int Dt, int H, int R, int W, hipStream_t st,
-                                          int force) {
+                                          float* xnorm, int N, int D, int Dt, int H, int max_in, int R, int W,
+                                          hipStream_t st, int force) {
   int plan[5];
-  if (cgnn_staged_plan(Dt, H, 1, W, plan) != 0) return -2;
+  if (cgnn_staged_plan(Dt, H, max_in, W, plan) != 0) return -2;
+  const int hc = fwd_hc(H);
   const bool xg = force < 0 ? plan[0] != 0 : force == 1;
-  if (!xg && fwd_lds(Dt, W, false) > LDS_MAX) return -2;
+  if (fwd_lds(Dt, W, xg, max_in, hc) > LDS_MAX) return -2;
   const int T = cgnn_staged_tiles(N);
-  const size_t lds = fwd_lds(Dt, W, xg);
+  const size_t lds = fwd_lds(Dt, W, xg, max_in, hc);
   dim3 grid((unsigned)(T * R)), block(WAVE * W);
 #define FWD(HC, XG)                                                                                           \
   {                                                                                                           \
     allow_lds(gen_fwd_staged_kernel<HC, XG>, lds);                                                            \
     hipLaunchKernelGGL((gen_fwd_staged_kernel<HC, XG>), grid, block, lds, st, prog, ps, sched, ss, params, P, \
-                       data, xhat, noise, NS, xnorm, N, D, Dt, H, T);                                         \
+                       data, xhat, noise, NS, xnorm, N, D, Dt, H, T, max_in);                                         \
   }
 #define FWD_HC(HC) case HC: if (xg) FWD(HC, true) else FWD(HC, false) break;
   switch (fwd_hc(H)) {

@@ -154,13 +154,9 @@ struct GatFwdArgs {
   int n, K, HF;
 };
 
-// Occupancy of the two gather kernels: they are latency-bound (rows in flight per CU),
-// so a register cap that buys waves can pay (A/B: -DCGNN_GAT_WAVES=N, N waves per SIMD)
-#ifdef CGNN_GAT_WAVES
-#define GAT_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(CGNN_GAT_WAVES)))
-#else
+// (Occupancy of the two gather kernels: they are latency-bound, yet a register cap
+// that buys waves per SIMD measured no gain; the compiler's allocation is kept.)
 #define GAT_WAVES_ATTR
-#endif
 
 // Scores run in the log2 domain (LeakyReLU is positively homogeneous: leaky(c x) =
 // c leaky(x) for c > 0), so every exponential is one v_exp_f32.
@@ -699,11 +695,9 @@ int lanes_for(int HF) {
 
 // edges per gather batch: 2 (measured on the products epoch: 11.80 ms at 2, 12.66 at 4,
 // 13.0 at 8, 14.4 at 16 -- the gathers are latency-bound and a wider batch costs more
-// occupancy than its rows in flight buy; A/B with -DCGNN_GAT_EC=N)
-#ifndef CGNN_GAT_EC
-#define CGNN_GAT_EC 2
-#endif
-#define GAT_EC_OF(L) ((L) < CGNN_GAT_EC ? (L) : CGNN_GAT_EC)
+// occupancy than its rows in flight buy)
+constexpr int GAT_EC = 2;
+#define GAT_EC_OF(L) ((L) < GAT_EC ? (L) : GAT_EC)
 
 #define GAT_SWITCH(LAUNCH)                                                                  \
   switch (L * 100 + G) {                                                                   \

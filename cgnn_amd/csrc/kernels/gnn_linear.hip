@@ -53,21 +53,11 @@ constexpr int TILE = 32;
 // take 4 * KS registers
 template <int KS> struct FwdWaves { static constexpr int value = KS <= 16 ? 16 : 8; };
 constexpr int WGT_WAVES = 8;        // weight-gradient blocks
-#ifndef CGNN_BWD_DATA_SEL
-#define CGNN_BWD_DATA_SEL 1         // lin_bwd_data: branch-free gradient loader (A/B build switch)
-#endif
-#ifndef CGNN_FWD8_WAVES
-#define CGNN_FWD8_WAVES 16          // lin_fwd KS = 8: waves per block (A/B build switch)
-#endif
-#ifndef CGNN_FWD16_WAVES
-#define CGNN_FWD16_WAVES 8          // lin_fwd KS = 16: waves per block (A/B build switch; profiles/r03_waves)
-#endif
-#ifndef CGNN_BWD16_WAVES
-#define CGNN_BWD16_WAVES 8          // lin_bwd_data KN = 16: waves per block (A/B build switch; profiles/r03_waves)
-#endif
-#ifndef CGNN_FWD_SEL_KS
-#define CGNN_FWD_SEL_KS 8           // lin_fwd: branch-free X loader from this many k-steps up (A/B build switch)
-#endif
+constexpr bool BWD_DATA_SEL = true;   // lin_bwd_data: branch-free gradient loader
+constexpr int FWD8_WAVES = 16;        // lin_fwd KS = 8: waves per block
+constexpr int FWD16_WAVES = 8;        // lin_fwd KS = 16: waves per block (profiles/r03_waves)
+constexpr int BWD16_WAVES = 8;        // lin_bwd_data KN = 16: waves per block (profiles/r03_waves)
+constexpr int FWD_SEL_KS = 8;         // lin_fwd: branch-free X loader from this many k-steps up
 constexpr int TR = TILE + 8;        // transposed image row: 32 rows + pad (80 B)
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
@@ -311,7 +301,7 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     uint4 bx[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      if constexpr (KS >= CGNN_FWD_SEL_KS)    // wide K: the branch-free form (no exec-mask spills)
+      if constexpr (KS >= FWD_SEL_KS)    // wide K: the branch-free form (no exec-mask spills)
         bx[s] = load_cat8_sel(x1, ld1, K1, x2, ld2, K2, rv ? row : n - 1, 16 * s + fh, idx1);
       else
         bx[s] = rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h, idx1) : make_uint4(0u, 0u, 0u, 0u);
@@ -622,7 +612,7 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
     const bool rv = row < n;
     bf16x8 by[KN];
     // branch-free unless it would push the 16-wave KN = 16 variant past 128 VGPRs
-    constexpr bool sel = CGNN_BWD_DATA_SEL && !(KN == 16 && FWD_WAVES == 16);
+    constexpr bool sel = BWD_DATA_SEL && !(KN == 16 && FWD_WAVES == 16);
 #pragma unroll
     for (int s = 0; s < KN; ++s)
       by[s] = as_bf16x8(sel ? load_masked8_sel(dY, lddy, Ym, ldym, mscale, N, rv ? row : n - 1, 16 * s + 8 * h, rv)
@@ -1058,9 +1048,7 @@ __global__ __launch_bounds__(256) void lin_prep_bwd_kernel(const float* __restri
 // ---------------------------------------------------------------- launchers
 static int grid_rows(int n, int waves) {
   const int tiles = (n + TILE - 1) / TILE;
-  static const int per = [] { const char* e = std::getenv("CGNN_LIN_TILES_PER_BLOCK"); return e ? atoi(e) : 0; }();
-  const int w = per > 0 ? per : waves;
-  return std::max(1, std::min(device_cus(), (tiles + w - 1) / w));
+  return std::max(1, std::min(device_cus(), (tiles + waves - 1) / waves));
 }
 
 static int pick_ks(int K) {
@@ -1085,7 +1073,7 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
                       uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
                       const int* idx1, uint16_t* wimg, float* Yf, int nsplit, int tk, hipStream_t st) {
   constexpr int KP = KS * 16;
-  constexpr int WV = KS == 16 ? CGNN_FWD16_WAVES : KS == 8 ? CGNN_FWD8_WAVES : FwdWaves<KS>::value;
+  constexpr int WV = KS == 16 ? FWD16_WAVES : KS == 8 ? FWD8_WAVES : FwdWaves<KS>::value;
   const int ncols = slab_cols(std::max(N, ldy), KP);
   const size_t lds = (size_t)ncols * (KP + 8) * 2 + (size_t)ncols * 4;
   {
@@ -1123,12 +1111,8 @@ static int kc_launch(const uint16_t* x, int ldx, int K, const float* W, int N, c
   const long total = (long)FG * 128 * KPc;
   hipLaunchKernelGGL(lin_prep_kc_kernel<ET>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K, N, KPc,
                      total, wimg);
-  // the 256 x 256 tiled GEMM (default; env CGNN_LIN_GEMM=0: the kc kernel, A/B)
-  static const bool gemm = [] {
-    const char* e = std::getenv("CGNN_LIN_GEMM");
-    return !(e && e[0] == '0');
-  }();
-  if (gemm && FG == 2) {
+  // the 256 x 256 tiled GEMM where it applies, else the kc kernel
+  if (FG == 2) {
     const size_t lds = sizeof(uint16_t) * 2 * (256 + 256) * 64;
     (void)hipFuncSetAttribute((const void*)lin_gemm_kernel<ET>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((lin_gemm_kernel<ET>), dim3((n + 255) / 256), dim3(512), lds, st, x, ldx, K, wimg, KPc, bias, Y,
@@ -1192,7 +1176,7 @@ static int bwd_data_launch(const uint16_t* dY, int lddy, const uint16_t* Ym, int
     hipLaunchKernelGGL(lin_prep_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K, N, NP,
                        NP + 8, total, wimg);
   }
-  constexpr int WV = KN == 16 ? CGNN_BWD16_WAVES : FwdWaves<KN>::value;
+  constexpr int WV = KN == 16 ? BWD16_WAVES : FwdWaves<KN>::value;
   (void)hipFuncSetAttribute((const void*)lin_bwd_data_kernel<KN, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds);
   const int slabs = (K + kcols - 1) / kcols;
@@ -1246,24 +1230,14 @@ static int wgt2_nb(int kt, int N) {
   return nb;
 }
 
-static bool wgt_v1() {
-  static const bool v1 = [] { const char* e = std::getenv("CGNN_WGT_V1"); return e && e[0] == '1'; }();
-  return v1;
-}
-
 // Row chunks of the split-K weight gradient (the gpart scratch's leading dimension).
 // lin_bwd_weight2 (K > 0): one 8-wave block per CU over all chunks x column slabs;
 // the v1 kernel: two 8-wave blocks per CU over its 64-column slabs.
 extern "C" int gnn_lin_wgrad_chunks(int n, int N, int K) {
   const int tiles = std::max(1, (n + TILE - 1) / TILE);
-  if (K > 0 && !wgt_v1()) {
+  if (K > 0) {
     const int slabs = (N + 32 * wgt2_nb((K + 31) / 32, N) - 1) / (32 * wgt2_nb((K + 31) / 32, N));
-    static const int div = [] { const char* e = std::getenv("CGNN_WGT2_CHUNK_DIV"); return e ? std::max(1, atoi(e)) : 1; }();
-    // at least min_tiles row tiles per chunk: each chunk writes a whole K x N fp32 slab,
-    // which at a few tiles per chunk outweighs the rows it reads
-    static const int min_tiles = [] { const char* e = std::getenv("CGNN_WGT2_MIN_TILES"); return e ? std::max(1, atoi(e)) : 1; }();
-    const int cap = (tiles + min_tiles - 1) / min_tiles;
-    return std::min(cap, std::max(1, device_cus() / (std::max(slabs, 1) * div)));
+    return std::min(tiles, std::max(1, device_cus() / std::max(slabs, 1)));
   }
   const int slabs = std::max(1, (N + 63) / 64);
   const int want = std::max(1, 2 * device_cus() / slabs);
@@ -1330,7 +1304,7 @@ extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const 
     auto d = (const uint16_t*)dY;
     auto m = (const uint16_t*)Ym;
     int rc = -1;
-    if (!wgt_v1()) {
+    {
       const int nb = wgt2_nb(kt, N);
 #define LW2(c, b_) if (rc == -1 && kt <= c && nb == b_) rc = wgt2_launch<c, b_>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, idx1, st);
       LW2(2, 2) LW2(2, 4) LW2(2, 8) LW2(4, 2) LW2(4, 4) LW2(4, 8) LW2(5, 2) LW2(5, 4)
@@ -1338,7 +1312,7 @@ extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const 
 #undef LW2
       if (rc == -1) rc = -2;                 // no v2 form: v1 below
     }
-    if (rc == -2 || wgt_v1()) {
+    if (rc == -2) {
       rc = -1;
 #define LW(c) if (rc == -1 && kt <= c) rc = wgt_launch<c>(a, ld1, K1, b, ld2, K2, d, lddy, m, ldym, mscale, N, gpart, n, chunks, idx1, st);
       LW(2) LW(4) LW(5) LW(8) LW(9) LW(12) LW(16) LW(17)

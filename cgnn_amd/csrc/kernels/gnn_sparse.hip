@@ -24,21 +24,9 @@
 
 using namespace cgnn;
 
-#ifndef CGNN_SPMM_MINW
-#define CGNN_SPMM_MINW 1
-#endif
-// streamed operands (column indices, read once; the aggregate, written once) with the
-// non-temporal hint, so they do not displace gathered rows from the caches (A/B knob)
-#ifndef CGNN_SPMM_NT
-#define CGNN_SPMM_NT 0
-#endif
 template <typename T>
 __device__ __forceinline__ T ld_stream(const T* p) {
-#if CGNN_SPMM_NT
-  return __builtin_nontemporal_load(p);
-#else
   return *p;
-#endif
 }
 
 namespace {
@@ -278,109 +266,8 @@ __device__ __forceinline__ void gather_sum_lds(const int* __restrict__ col, cons
   }
 }
 
-// first source row of the LDS window of the block whose first (local) row is rb0: the
-// window [w0, w0 + WR) is centred on the block's rows [row_off + rb0, + R) and clamped
-// into the source rows [0, n_src) (WR <= n_src)
-__device__ __forceinline__ int win_start(int rb0, int R, int WR, int row_off, int n_src) {
-  const int c = row_off + rb0 + R / 2 - WR / 2;
-  return max(0, min(c, n_src - WR));
-}
-
 }  // namespace
 
-// LDS-windowed CSR aggregate, bf16 rows, F <= 128 (16 lanes x 8 features per row).
-// After the framework's locality reordering most edges of a row join nearby ids
-// (products shape: 74 % within +-256 positions).  A block owns R consecutive rows and
-// first stages the source rows [w0, w0 + WR) around them -- the window -- in LDS
-// (WR x LP x 16 B, up to 160 KiB, one block per CU); every row's sorted column list
-// then splits into [e0, a) below the window, [a, b) inside, [b, e1) above (split[] from
-// spmm_win_plan_kernel).  The in-window rows are read from LDS (ds_read_b128, ~150 TB/s
-// chip-wide against ~17 TB/s for gathers served by L2), the rest are gathered from
-// global memory as in spmm_kernel.  Rows are dealt to the 16 waves four at a time from
-// an LDS counter (power-law degrees: no wave idles on a long row of a neighbour).
-// Epilogue: Y[i] = rscale[i] * sum, padding columns 0, unit_col 1.
-template <int LP>
-__global__ __launch_bounds__(1024, 1) void spmm_win_kernel(
-    const int* __restrict__ rowptr, const int* __restrict__ col, const int2* __restrict__ split,
-    const uint16_t* __restrict__ X, uint16_t* __restrict__ Y, const float* __restrict__ rscale, int n_rows,
-    int F, int ldx, int ldy, int unit_col, int row_off, int n_src, int R, int WR) {
-  constexpr int L = 16, NCH = 10;                   // NCH: staged chunks per thread (WR * LP <= 10240)
-  extern __shared__ uint4 s_win[];
-  __shared__ int s_next;
-  const unsigned blk = xcd_remap(blockIdx.x, gridDim.x);
-  const int rb0 = (int)blk * R, rb1 = min(n_rows, rb0 + R);
-  const int w0 = win_start(rb0, R, WR, row_off, n_src);
-  {
-    const int total = WR * LP;
-    uint4 v[NCH];
-#pragma unroll
-    for (int q = 0; q < NCH; ++q) {
-      const int i = threadIdx.x + q * 1024;
-      const int w = i / LP, c = i - w * LP;
-      v[q] = i < total ? load_raw16(X, (size_t)(w0 + w) * ldx + c * 8) : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < NCH; ++q) {
-      const int i = threadIdx.x + q * 1024;
-      if (i < total) s_win[i] = v[q];
-    }
-  }
-  if (threadIdx.x == 0) s_next = 0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, sub = lane >> 4, sl = lane & 15;
-  const int f0 = sl * 8;
-  const bool fl = f0 < F;
-  for (;;) {
-    int g = 0;
-    if (lane == 0) g = atomicAdd(&s_next, 4);
-    g = __shfl(g, 0, 64);
-    if (rb0 + g >= rb1) break;
-    const int row = rb0 + g + sub;
-    const bool rv = row < rb1;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int e0 = 0, e1 = 0, a = 0, b = 0;
-    if (rv) {
-      e0 = rowptr[row]; e1 = rowptr[row + 1];
-      const int2 s = split[row];
-      a = s.x; b = s.y;
-    }
-    gather_sum_lds<L, LP>(col, s_win, a, b, w0, sl, fl, sub * L, acc);
-    gather_sum_gap<L>(col, X, e0, e1, a, b, ldx, f0, fl, sub * L, sl, acc);
-    if (rv && f0 < ldy) {
-      const float rs = rscale ? rscale[row] : 1.f;
-      float y[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int f = f0 + q;
-        y[q] = f < F ? acc[q] * rs : (f == unit_col ? 1.f : 0.f);
-      }
-      *reinterpret_cast<uint4*>(Y + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
-    }
-  }
-}
-
-// split[i] = (a, b): the edges of row i whose sources lie in its block's window are
-// exactly [a, b) (columns sorted ascending within a row)
-__global__ void spmm_win_plan_kernel(const int* __restrict__ rowptr, const int* __restrict__ col,
-                                     int2* __restrict__ split, int n_rows, int row_off, int n_src, int R,
-                                     int WR) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_rows) return;
-  const int w0 = win_start(i / R * R, R, WR, row_off, n_src), w1 = w0 + WR;
-  int a = rowptr[i], b = rowptr[i + 1];
-  const int e1 = b;
-  {                                   // lower_bound(col, w0)
-    int lo = a, hi = e1;
-    while (lo < hi) { const int m = (lo + hi) >> 1; if (col[m] < w0) lo = m + 1; else hi = m; }
-    a = lo;
-  }
-  {                                   // lower_bound(col, w1) from a
-    int lo = a, hi = e1;
-    while (lo < hi) { const int m = (lo + hi) >> 1; if (col[m] < w1) lo = m + 1; else hi = m; }
-    b = lo;
-  }
-  split[i] = make_int2(a, b);
-}
 
 // Fixed-order column sums of per-block partials P [S][W] (fp32, row-major): block
 // (x, y) sums rows [y * per, (y + 1) * per) of columns [64 x, 64 x + 64), blockDim / 64
@@ -415,7 +302,7 @@ __global__ __launch_bounds__(1024) void slab_sum_kernel(const float* __restrict_
 }
 
 template <int L, int XBF, int YBF, int U, bool CS>
-__global__ __launch_bounds__(256, CGNN_SPMM_MINW) void spmm_kernel(
+__global__ __launch_bounds__(256) void spmm_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
     void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
     int n_rows, int F, int ldx, int ldy, int relu, int unit_col, int wcols,
@@ -452,11 +339,7 @@ __global__ __launch_bounds__(256, CGNN_SPMM_MINW) void spmm_kernel(
     y[q] = f < F ? v : (f == unit_col ? 1.f : 0.f);
   }
   if (YBF == 1) {
-#if CGNN_SPMM_NT
-    __builtin_nontemporal_store(f32x8_to_bf16(y), reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0));
-#else
     *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
-#endif
   } else if (YBF == 2) {
     f16x8 o;
 #pragma unroll
@@ -755,20 +638,11 @@ __global__ void cast_bf16_kernel(const float* __restrict__ src, uint16_t* __rest
 }
 
 // ---------------------------------------------------------------- launchers
-static int spmm_unroll() {
-  static int u = -1;
-  if (u < 0) {
-    // Measured alternative, kept out: a software-pipelined gather (next chunk's column
-    // indices requested early, non-temporal index loads / output stores, 16 raw rows in
-    // flight per lane) ran 30 % SLOWER on the ogbn-products shape (F = 100: 3.43 vs
-    // 2.64 ms; F = 256: 5.49 vs 4.10 ms; F = 47 unchanged) -- the gather is bound by
-    // cache throughput, not by the index round trip.
-    const char* e = getenv("CGNN_SPMM_UNROLL");
-    u = (e && atoi(e) == 4) ? 4 : 8;
-  }
-  return u;
-}
-
+// Gathers unrolled 8 rows deep.  Measured alternatives, kept out: 4 deep (slower on
+// the products shape), and a software-pipelined gather (next chunk's column indices
+// requested early, non-temporal index loads / output stores, 16 raw rows in flight per
+// lane): 30 % SLOWER (F = 100: 3.43 vs 2.64 ms; F = 256: 5.49 vs 4.10 ms; F = 47
+// unchanged) -- the gather is bound by cache throughput, not by the index round trip.
 template <int L, int U>
 static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
@@ -800,10 +674,7 @@ static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void*
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
                          int relu, int uc, int wc, const float* init, int ldi, const float* cs, int ir,
                          hipStream_t st) {
-  if (spmm_unroll() == 8)
-    return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
-                                 ldi, cs, ir, st);
-  return spmm_dispatch_u<L, 4>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
+  return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
                                ldi, cs, ir, st);
 }
 
@@ -841,43 +712,6 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
     if (rc) return rc;
   }
   return 0;
-}
-
-// windowed SpMM: LDS pitch lp >= ceil(F / 8) 16-B chunks; WR * lp <= 10239 (160 KiB)
-extern "C" int gnn_spmm_win_rows(int lp) {
-  return lp >= 1 && lp <= 16 ? (10239 / lp) / 8 * 8 : 0;
-}
-
-extern "C" int gnn_spmm_win_plan(const int* rowptr, const int* col, void* split, int n_rows, int row_off,
-                                 int n_src, int R, int WR, hipStream_t st) {
-  if (R <= 0 || WR <= 0 || WR > n_src) return -3;
-  hipLaunchKernelGGL(spmm_win_plan_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, st, rowptr, col,
-                     (int2*)split, n_rows, row_off, n_src, R, WR);
-  return (int)hipGetLastError();
-}
-
-extern "C" int gnn_launch_spmm_win(const int* rowptr, const int* col, const void* split, const void* X, void* Y,
-                                   const float* rscale, int n_rows, int F, int ldx, int ldy, int unit_col,
-                                   int row_off, int n_src, int R, int WR, int lp, hipStream_t st) {
-  if (lp < (F + 7) / 8) return -3;
-  if (F < 1 || F > 128 || ldy > 128 || (ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
-  if (R <= 0 || R % 4 || WR <= 0 || WR > n_src || WR > gnn_spmm_win_rows(lp)) return -3;
-  const unsigned grid = (unsigned)((n_rows + R - 1) / R);
-  const size_t lds = (size_t)WR * lp * 16;
-#define CGNN_WIN(P)                                                                                             \
-  case P:                                                                                                       \
-    (void)hipFuncSetAttribute((const void*)spmm_win_kernel<P>, hipFuncAttributeMaxDynamicSharedMemorySize,    \
-                              (int)lds);                                                                        \
-    hipLaunchKernelGGL(spmm_win_kernel<P>, dim3(grid), dim3(1024), lds, st, rowptr, col, (const int2*)split,    \
-                       (const uint16_t*)X, (uint16_t*)Y, rscale, n_rows, F, ldx, ldy, unit_col, row_off, n_src, \
-                       R, WR);                                                                                  \
-    break;
-  switch (lp) {
-    CGNN_WIN(4) CGNN_WIN(6) CGNN_WIN(8) CGNN_WIN(12) CGNN_WIN(13) CGNN_WIN(16)
-    default: return -5;
-  }
-#undef CGNN_WIN
-  return (int)hipGetLastError();
 }
 
 // out[map[c]] = sum_r P[r][c] (fixed order).  stage: fp32 [>= G * W] scratch for the

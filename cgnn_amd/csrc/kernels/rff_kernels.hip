@@ -13,7 +13,7 @@
 // data/xhat [R][D][N], grad -> chunk 0 of the MMD gradient buffer [1][R][D][N].
 //
 // Default: matrix-core kernels (below); the vector kernels (one feature / one sample
-// per thread) remain for CGNN_RFF_VALU=1 (A/B) and for W images too large for LDS.
+// per thread) remain for W images too large for LDS (and for A/B, force_valu).
 #include "cgnn_common.h"
 #include <cstdlib>
 
@@ -271,15 +271,6 @@ __global__ __launch_bounds__(256) void rff_mfma_grad_kernel(const float* __restr
     }
 }
 
-// matrix-core path from this padded width on (CGNN_RFF_MFMA_MIN_D, default 1: every width); CGNN_RFF_VALU=1
-// forces the vector kernels.  Read at every enqueue (a captured hipGraph keeps its choice).
-static int rff_mfma_min_d() {
-  const char* v = getenv("CGNN_RFF_VALU");
-  if (v && atoi(v) == 1) return 1 << 30;
-  const char* e = getenv("CGNN_RFF_MFMA_MIN_D");
-  return e ? atoi(e) : 1;
-}
-
 extern "C" int rff_launch_freqs(float* W, const uint32_t* keys, const int* step_base, int step_off,
                                 int k, int D, int n_gamma, int d_true, int R, hipStream_t st) {
   const int tot = k * n_gamma * (D + 1);
@@ -291,13 +282,13 @@ extern "C" int rff_launch_freqs(float* W, const uint32_t* keys, const int* step_
 template <int D>
 static int rff_fb_d(int mode, const float* xhat, const float* data, const float* W, float* diff,
                     float* loss_part, float* grad, int N, int F, int R, int k, float norm,
-                    hipStream_t st) {
+                    hipStream_t st, int force_valu) {
   // features staged per chunk of the gradient kernel: all of them when [F][D + 1] fits
   // in 160 KiB, else the largest multiple of 32 that does
   const size_t cap = 160 * 1024 / sizeof(float);
   const bool whole = (size_t)F * (D + 2) <= cap;
   const int FC = whole ? F : (int)(cap / (D + 2)) / 32 * 32;
-  if (D > 64 || (D >= rff_mfma_min_d() && whole)) {    // the vector kernels stop at D = 64
+  if (D > 64 || (!force_valu && whole)) {    // the vector kernels stop at D = 64
     if (FC < 32) return -2;
     const size_t glds = sizeof(float) * (size_t)FC * (D + 2);
     hipLaunchKernelGGL((rff_mfma_feat_kernel<D>), dim3((F + 255) / 256, R), dim3(512), 0, st, xhat, data, W, diff,
@@ -323,12 +314,13 @@ static int rff_fb_d(int mode, const float* xhat, const float* data, const float*
   return -1;
 }
 
-// mode 0: loss partials + gradient; mode 1: loss partials only.
+// mode 0: loss partials + gradient; mode 1: loss partials only.  force_valu: the vector
+// kernels wherever they exist (D <= 64; A/B and tests)
 extern "C" int rff_launch_fwd_bwd(int mode, const float* xhat, const float* data, const float* W,
                                   float* diff, float* loss_part, float* grad, int N, int D, int F,
-                                  int R, int k, float norm, hipStream_t st) {
+                                  int R, int k, float norm, hipStream_t st, int force_valu) {
   switch (D) {
-#define CASE_D(d) case d: return rff_fb_d<d>(mode, xhat, data, W, diff, loss_part, grad, N, F, R, k, norm, st);
+#define CASE_D(d) case d: return rff_fb_d<d>(mode, xhat, data, W, diff, loss_part, grad, N, F, R, k, norm, st, force_valu);
     CASE_D(1) CASE_D(2) CASE_D(3) CASE_D(4) CASE_D(6) CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20)
     CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64) CASE_D(80) CASE_D(96) CASE_D(128) CASE_D(160) CASE_D(192)
     CASE_D(224) CASE_D(256)

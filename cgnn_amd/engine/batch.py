@@ -57,11 +57,10 @@ def mmd_mfma_geometry(N: int, R: int = 0):
     return rb, n_chunks, tpc
 
 
-def mmd_mirror_slots(D: int, N: int) -> int:
+def mmd_mirror_slots(D: int, N: int, symmetric: bool = True) -> int:
     """Extra gradient slots of a symmetric vector-kernel training launch (0: the launch
-    evaluates the full pred-pred block).  ``CGNN_MMD_SYM=0`` disables symmetry."""
-    import os
-    if os.environ.get("CGNN_MMD_SYM", "1") == "0":
+    evaluates the full pred-pred block; ``symmetric=False`` forces that)."""
+    if not symmetric:
         return 0
     return int(native.hip().mmd_mirror_slots(D, N))
 
@@ -114,6 +113,14 @@ def staged_setup(programs: Sequence[Program], H: int, max_in: int, d: int):
     return sched, sstride, W, bool(plan[2])
 
 
+PARAM_PAD = 64    # floats past the last model (cgnn_staged.hip tail-chunk weight loads)
+
+
+def param_buffer(R: int, P: int, device) -> torch.Tensor:
+    """[R, P] fp32 zeros whose storage runs PARAM_PAD floats past the last model."""
+    return torch.zeros(R * P + PARAM_PAD, dtype=torch.float32, device=device)[:R * P].view(R, P)
+
+
 def _keys_tensor(keys, device):
     arr = np.asarray(keys, dtype=np.uint64).astype(np.uint32).reshape(-1)
     return torch.from_numpy(arr.view(np.int32).copy()).to(device)
@@ -159,7 +166,7 @@ class DeviceTrainer:
                 data[r, :d] = np.asarray(x, dtype=np.float32)
             self.data = torch.from_numpy(data).to(dev)
             self.keys = _keys_tensor(keys, dev)
-            self.params = torch.zeros(R, P, **f32)
+            self.params = param_buffer(R, P, dev)
             self.m = torch.zeros(R, P, **f32)
             self.v = torch.zeros(R, P, **f32)
             self.xhat = torch.zeros(R, D, N, **f32)
@@ -174,7 +181,7 @@ class DeviceTrainer:
             F = 7 * self.rff_k
             n_parts = max(row_tiles * n_chunks, mf_rb * mf_chunks, (F + 255) // 256 if F else 0)
             # symmetric pred-pred training on the vector kernel: extra gradient slots for
-            # the mirrored column sums (CGNN_MMD_SYM=0 turns it off for A/B)
+            # the mirrored column sums
             self.mirror = mmd_mirror_slots(D, N) if self.mmd_kernel == "valu" else 0
             self.gradp = torch.zeros(max(n_chunks + self.mirror, mf_chunks, 1), R, D, N, **f32)
             self.lpart = torch.zeros(R, n_parts, **f32)

@@ -35,7 +35,7 @@ import torch.distributed as dist
 
 from .. import native
 from ..parallel.sharded_mmd import _mfma_geometry, _valu_geometry, row_partials
-from .batch import _keys_tensor, mmd_kernel_choice, padded_dim, staged_setup
+from .batch import _keys_tensor, mmd_kernel_choice, padded_dim, param_buffer, staged_setup
 from .program import Program, pack_programs
 from .reference import ReferenceTrainer
 
@@ -126,7 +126,7 @@ class SampleShardedTrainer:
         self.data_loc = torch.from_numpy(data).to(dev)
         self.data_all = self._gather_cols(self.data_loc).contiguous()
         self.keys_t = _keys_tensor(self.keys, dev)
-        self.params = torch.zeros(R, P, **f32)
+        self.params = param_buffer(R, P, dev)
         self.m = torch.zeros(R, P, **f32)
         self.v = torch.zeros(R, P, **f32)
         self.xhat = torch.zeros(R, D, n, **f32)
@@ -166,8 +166,8 @@ class SampleShardedTrainer:
                           self.noise.data_ptr(), self.NS, n, D, self.d, R, self.row0, self.st)
             hip.gen_fwd_staged(self.prog.data_ptr(), self.stride, self.sched.data_ptr(), self.sstride,
                                self.params.data_ptr(), self.P, self.data_loc.data_ptr(), self.xhat.data_ptr(),
-                               self.noise.data_ptr(), self.NS, self.xnorm.data_ptr(), n, D, self.d, self.H, R,
-                               self.stage_w, self.st)
+                               self.noise.data_ptr(), self.NS, self.xnorm.data_ptr(), n, D, self.d, self.H,
+                               self.max_in, R, self.stage_w, self.st)
         else:
             hip.gen_fwd(self.prog.data_ptr(), self.stride, self.params.data_ptr(), self.P, self.data_loc.data_ptr(),
                         self.xhat.data_ptr(), self.noise.data_ptr(), self.NS, self.xnorm.data_ptr(),

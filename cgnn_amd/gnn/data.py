@@ -211,10 +211,10 @@ def locality(g: GraphData, windows=(64, 256, 1024, 4096, 65536), new_id=None):
 
 
 def reorder(g: GraphData, rounds: int = 8, max_cluster: int = 4096, seed: int = 0,
-            refine: Optional[int] = None):
+            refine: int = 0):
     """Relabel the nodes of ``g`` for gather locality (``csrc/runtime/reorder.cpp``):
     label-propagation clusters + Cuthill-McKee, then ``refine`` rounds of median
-    smoothing (env ``CGNN_REORDER_REFINE``; default 0: on the products shape 4 rounds
+    smoothing (default 0: on the products shape 4 rounds
     narrow the band -- edges within +-256 positions 56 -> 74 % -- yet the GCN epoch
     measured 5 % SLOWER, 197 vs 210 epochs/s: the cluster-walk order's grouping of whole
     communities serves the per-XCD L2 better than a tighter diagonal band).
@@ -228,8 +228,6 @@ def reorder(g: GraphData, rounds: int = 8, max_cluster: int = 4096, seed: int = 
     rp = g.rowptr.cpu().numpy().astype(np.int64)
     col = g.col.cpu().numpy()
     new_id = rt.locality_order(g.n, rp, col, rounds, max_cluster, seed)
-    if refine is None:
-        refine = int(os.environ.get("CGNN_REORDER_REFINE", "0"))
     if refine > 0:
         new_id = rt.locality_refine(g.n, rp, col, new_id, refine)
     rp2, col2 = rt.permute_csr(g.n, rp, col, new_id)

@@ -19,7 +19,6 @@ GPU kernels are tested against).
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional
 
 import torch
@@ -298,7 +297,8 @@ class GATTrainer:
     otherwise the autograd model over the HIP aggregation."""
 
     def __init__(self, gd: GraphData, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True,
-                 fused: Optional[bool] = None, reorder: bool = False):
+                 fused: Optional[bool] = None, reorder: bool = False, train_rows_only: bool = True,
+                 l1_train_neighbours: bool = True):
         # reorder=True: the framework's locality pass first (data.reorder; the attention
         # kernels gather rows like the SpMM, so their L2 hit rate follows the order);
         # evaluation and dropout-0 training are invariant, with dropout > 0 the masks are
@@ -319,7 +319,8 @@ class GATTrainer:
         self.fused = None
         if _use_fused(fused, self.dev, x.shape[1], heads, head_dim, gd.n_classes):
             from .gat_fused import FusedGAT
-            self.fused = FusedGAT(x, gd.y, gd.mask, gd.n_classes, self.g, heads, head_dim, dropout, lr, seed)
+            self.fused = FusedGAT(x, gd.y, gd.mask, gd.n_classes, self.g, heads, head_dim, dropout, lr, seed,
+                                  train_rows_only=train_rows_only, l1_train_neighbours=l1_train_neighbours)
             self.model = self.opt = None
             return
         self.model = GAT(x.shape[1], gd.n_classes, heads, head_dim, dropout, seed).to(self.dev)
@@ -383,7 +384,11 @@ class ShardedGATTrainer:
 
     def __init__(self, shard, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0, standardize=True,
                  bucket_mb: float = 16.0, emulate=None, fused: Optional[bool] = None,
-                 halo_chunk_bytes: int = 4 << 30):
+                 halo_chunk_bytes: int = 4 << 30, train_rows_only: bool = True, train_halo: bool = True,
+                 l1_exchange: bool = False, l1_train_neighbours: bool = True):
+        # train_rows_only / train_halo / l1_train_neighbours: see gcn.GCNTrainer;
+        # l1_exchange=True: exchange the layer-1 projections every epoch instead of the
+        # input rows once at setup.  All must agree across ranks.
         import torch.distributed as dist
         from ..parallel import dist as pdist
         from ..parallel.ddp import GradBucketer
@@ -438,17 +443,16 @@ class ShardedGATTrainer:
             # the whole epoch on HIP kernels; one all-reduce of the flat gradient buffer
             from .gat_fused import FusedGAT
             train_l2 = None
-            if (self.world > 1 and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0"
-                    and os.environ.get("CGNN_TRAIN_HALO", "1") != "0"):
+            if self.world > 1 and train_rows_only and train_halo:
                 train_l2 = self._train_halo(shard, r0, r1, per, emulate, wide, halo_chunk_bytes)
             # layer 1 without communication: its input rows are static, so the rows of the
             # layer-1 halo cross the links ONCE here (bf16), and every epoch each rank
             # projects [Wh | s_src] of the received rows itself (lin_fwd) and takes their
             # weight-gradient share as x_ext^T dy_ext -- per epoch only the layer-2 halo and
-            # the weight all-reduce remain.  Env CGNN_GAT_L1_EXCHANGE=1: exchange per epoch.
+            # the weight all-reduce remain (l1_exchange=True: exchange per epoch).
             x_ext = None
             self.l1_setup_bytes = 0
-            if self.halo is not None and os.environ.get("CGNN_GAT_L1_EXCHANGE", "0") != "1":
+            if self.halo is not None and not l1_exchange:
                 F = self.x.shape[1]
                 xb = torch.zeros(nloc, (F + 7) // 8 * 8, dtype=torch.bfloat16, device=self.dev)
                 xb[:, :F] = self.x.to(torch.bfloat16)
@@ -457,7 +461,8 @@ class ShardedGATTrainer:
                 del xb
             self.fused = FusedGAT(self.x, self.y, self.mask, shard.n_classes, self.g, heads, head_dim, dropout, lr,
                                   seed, halo=self.halo, row0=r0, n_train=int(self.n_train), distributed=distributed,
-                                  train_l2=train_l2, x_ext=x_ext)
+                                  train_l2=train_l2, x_ext=x_ext, train_rows_only=train_rows_only,
+                                  l1_train_neighbours=l1_train_neighbours)
             self.model = self.opt = None
             self.epoch = 0
             return

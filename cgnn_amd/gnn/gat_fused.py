@@ -43,7 +43,6 @@ bf16-stored arithmetic), so the sharded path is tested with gloo ranks on CPU.
 from __future__ import annotations
 
 import math
-import os
 import types
 from typing import Optional
 
@@ -280,7 +279,8 @@ class FusedGAT:
     Parameters are initialised exactly like ``gat.GAT(F, C, heads, head_dim, seed)``."""
 
     def __init__(self, x, y, mask, n_classes, g, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0,
-                 halo=None, row0=0, n_train=None, distributed=False, train_l2=None, x_ext=None):
+                 halo=None, row0=0, n_train=None, distributed=False, train_l2=None, x_ext=None,
+                 train_rows_only: bool = True, l1_train_neighbours: bool = True):
         from .gat import GAT
         dev = x.device
         self.dev, self.g, self.halo = dev, g, halo
@@ -353,7 +353,7 @@ class FusedGAT:
         # Training epochs aggregate layer 2 only at this rank's train rows (the only
         # logits the loss reads; the epoch's update is unchanged -- the output-node
         # pruning of DGL's last block): a CSR of those rows over the same sources.
-        # Evaluation aggregates every row.  Env CGNN_L2_ALL_ROWS=1: every row always.
+        # Evaluation aggregates every row (train_rows_only=False: every row always).
         self._tr = None
         trows = torch.nonzero(self.mask == 1).flatten()
         if train_l2 is not None:
@@ -368,7 +368,7 @@ class FusedGAT:
                 dout=torch.zeros(nT, L2.KF, dtype=torch.float32, device=dev),
                 doutb=torch.zeros(nT, L2.KF, **bf))
             self.dout2 = self.dout2b = None
-        elif trows.numel() and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
+        elif trows.numel() and train_rows_only:
             from .gat import GraphCSR
             rp = g.rowptr.long()
             lo, deg = rp[trows], rp[trows + 1] - rp[trows]
@@ -389,12 +389,12 @@ class FusedGAT:
         # whose other rows are empty (they produce out = 0, finite, read by no train row,
         # with zero gradient); evaluation aggregates every row.  The papers100M shape has
         # ~1 % train rows, so most layer-1 edges drop out.  Not in a dry run (emulated
-        # halo: the received rows' flags are not real).  Env CGNN_L1_TRAIN_NBRS=0: off.
+        # halo: the received rows' flags are not real).  l1_train_neighbours=False: off.
         # The decision is the same on every rank whenever there is a halo (the flag
         # exchange is collective): a rank without train rows still takes part.
         self._g1 = None
         want = (halo is not None) or (self._tr is not None)
-        if (want and os.environ.get("CGNN_L1_TRAIN_NBRS", "1") != "0"
+        if (want and l1_train_neighbours
                 and not (halo is not None and getattr(halo, "emulate", False))):
             self._g1 = self._train_neighbour_graph(g, halo)
         self.epoch = 0

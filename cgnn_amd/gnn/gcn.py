@@ -32,7 +32,7 @@ static features are replicated (0.5 GB for ogbn-products, trivial against
 288 GB of HBM), so layer 1 needs no communication.  Layer 2 in training: the
 rank aggregates only its train rows, and only the remote Z2 rows THOSE read
 travel -- a training halo negotiated once at setup, one all-to-all per epoch
-(``_train_row_csr``; env CGNN_TRAIN_HALO=0 uses the evaluation's exchange).
+(``_train_row_csr``; ``train_halo=False`` uses the evaluation's exchange).
 Evaluation aggregates every row, with the full halo from 4 ranks on (``halo``)
 and an all-gather of Z2 below that.  The backward all-gathers the compact G (train
 rows only, padded to the largest rank's count: 1/12 of Z2's bytes), plus one
@@ -44,7 +44,6 @@ epoch's layer-1 SpMM (parameter-independent) overlaps the forward exchange.
 from __future__ import annotations
 
 import math
-import os
 import types
 from typing import Optional
 
@@ -105,7 +104,15 @@ class GCNTrainer:
                  weight_decay: float = 0.0, seed: int = 0, rank: Optional[int] = None,
                  world: Optional[int] = None, fused: bool = True, align_rows: Optional[bool] = None,
                  halo: Optional[bool] = None, capture: Optional[bool] = None, reorder: bool = False,
-                 align_c: Optional[bool] = None, collectives: Optional[bool] = None):
+                 align_c: Optional[bool] = None, collectives: Optional[bool] = None,
+                 train_rows_only: bool = True, l1_train_neighbours: bool = True, train_halo: bool = True,
+                 bwd_overlap: bool = True):
+        # train_rows_only / l1_train_neighbours: training epochs aggregate layer 2 only at
+        # the train rows and layer 1 only at the rows those read (the update is the same;
+        # False: every row, for equivalence tests).  train_halo: a multi-rank run's
+        # training epochs exchange only the remote rows the train rows read (False: the
+        # evaluation's exchange).  bwd_overlap: the backward's compact-gradient all-gather
+        # overlaps the rank-local edges (False: serial).  All must agree across ranks.
         # reorder=True: relabel the nodes for gather locality first (data.reorder: LP
         # clusters + Cuthill-McKee, ~4-8 s of host C++ on the ogbn-products shape, part
         # of setup); the row partition of a multi-GPU run then cuts mostly between
@@ -159,18 +166,6 @@ class GCNTrainer:
         # replicated normalised features Xs = D^-1/2 X, padded to ldx (zeros)
         self.Xs = torch.zeros(g.n, self.ldx, **bf)
         self.Xs[:, :self.F] = (g.x * g.dinv[:, None]).to(torch.bfloat16)
-        # layer-1 aggregation through the LDS-windowed SpMM (ops.WindowPlan): after the
-        # locality pass most sources of a row block lie in a window of nearby rows that the
-        # block stages in LDS once; kept only when the graph's order puts enough edges in
-        # the windows (a locality-free order would pay the staging for nothing).  Env
-        # CGNN_SPMM_WIN=0: the plain gather kernel
-        self._win = None
-        if dev.type == "cuda" and self.F <= 128 and os.environ.get("CGNN_SPMM_WIN", "0") != "0":
-            self._win = ops.WindowPlan(self.rowptr, self.col, self.F, g.n, row_off=r0,
-                                       R=int(os.environ.get("CGNN_SPMM_WIN_R", "256")),
-                                       pitch=int(os.environ.get("CGNN_SPMM_WIN_PITCH", "0")))
-            if self._win.in_window_fraction() < 0.25:
-                self._win = None
         # parameters: glorot-uniform weights, zero biases (PyG GCNConv init); one flat fp32 buffer
         gen = torch.Generator().manual_seed(seed)
         n1, n2 = self.F * hidden, hidden * self.C
@@ -202,19 +197,11 @@ class GCNTrainer:
         # multi-GPU: the layer-1 aggregation of the NEXT epoch is computed into a second
         # buffer while the forward all-gather of Z2 is in flight (it does not depend on the
         # parameters), then the buffers swap; every epoch still performs its own SpMM
-        # One GPU, opt-in (env CGNN_AX_PIPELINE=1): the same double buffer filled on a side
-        # stream, so the next epoch's layer-1 aggregation runs concurrently with this
-        # epoch's dense, layer-2 and backward kernels.  Exact, but measured neutral on the
-        # products shape (208.2 vs 208.8 epochs/s): the SpMM's blocks occupy every CU and
-        # the dense forward (one 1024-thread, LDS-heavy block per CU) only starts as they
-        # drain -- the kernel trace shows it stretched from 0.33 to 2.4 ms, no overlap won.
-        self._side = None
-        pipe = (not self.multi and dev.type == "cuda" and not capture
-                and os.environ.get("CGNN_AX_PIPELINE", "0") != "0")
-        self.AX_next = torch.zeros_like(self.AX) if (self.multi or pipe) else None
-        if pipe:
-            self._side = torch.cuda.Stream(dev)
-            self._ax_event = torch.cuda.Event()
+        # (Measured, not kept: on one GPU the same double buffer filled on a side stream,
+        # so the next epoch's layer-1 aggregation overlaps this epoch's dense kernels --
+        # neutral, 208.2 vs 208.8 epochs/s: the SpMM's blocks occupy every CU and the dense
+        # forward only starts as they drain.)
+        self.AX_next = torch.zeros_like(self.AX) if self.multi else None
         self._ax_ready = False
         if self.multi:
             # layer-2 aggregations split into edges whose source row this rank owns
@@ -226,19 +213,19 @@ class GCNTrainer:
         self.gslot, self.rp_T, self.col_T, self.maxT = self._train_columns(g, per)
         self.Gc_loc = torch.zeros(self.maxT, self.ldc, **bf)
         self.Gc = torch.zeros(self.maxT * self.world, self.ldc, **bf) if self.multi else self.Gc_loc
-        self._bwd_overlap = self.multi and os.environ.get("CGNN_BWD_OVERLAP", "1") != "0"
+        self._bwd_overlap = self.multi and bool(bwd_overlap)
         # the train-column adjacency's rows are short (~4 entries): on the GPU the unsplit
         # backward aggregation reads them from an ELL image (ops.spmm_ell: two dependent
-        # round trips per row instead of three).  Env CGNN_SPMM_ELL=0: the CSR kernel
+        # round trips per row instead of three)
         self._ell_T = None
-        if dev.type == "cuda" and not self._bwd_overlap and os.environ.get("CGNN_SPMM_ELL", "1") != "0":
+        if dev.type == "cuda" and not self._bwd_overlap:
             self._ell_T = ops.ell_image(self.rp_T, self.col_T)
         if self._bwd_overlap:
             # backward aggregation split like the forward's: the edges to this rank's own
             # train rows (slots [rank * maxT, + maxT), read straight from Gc_loc) run while
             # the all-gather of the other ranks' compact gradients is in flight.  Default
             # on: the 4-rank one-GPU rehearsal reproduces the serial schedule's loss bit
-            # for bit (profiles/r02_final/r4_ov{0,1}.log); CGNN_BWD_OVERLAP=0 serialises
+            # for bit (profiles/r02_final/r4_ov{0,1}.log); bwd_overlap=False serialises
             lo = self.rank * self.maxT
             self.rpT_loc, self.colT_loc, self.rpT_rem, self.colT_rem = self._split_local(
                 lo, lo + self.maxT, self.rp_T, self.col_T)
@@ -264,22 +251,22 @@ class GCNTrainer:
         # train rows): the other rows' logits enter neither the loss nor any gradient, so
         # the update is the same (the output-node pruning of DGL's last message-flow
         # block); every layer-1 row and every Z2 row is still computed, and evaluate()
-        # aggregates all rows.  Env CGNN_L2_ALL_ROWS=1: all rows in training too.
+        # aggregates all rows (train_rows_only=False: all rows in training too).
         self._l2 = None
-        # The switch is global (env), never per rank: the training halo is negotiated
+        # The switch must agree across ranks: the training halo is negotiated
         # collectively, so a rank without train rows takes part with a placeholder row.
         trows = torch.nonzero(self.mask == 1).flatten()
-        if os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
+        self._train_halo = bool(train_halo)
+        if train_rows_only:
             self._l2 = self._train_row_csr(trows)
         # ... and then layer 1 is needed only at the rows with a train neighbour (the
         # sources those aggregations read; 94 % of the rows, 96.7 % of the entries on the
         # ogbn-products shape): training epochs aggregate layer 1 over a CSR whose other
         # rows are empty.  Their AX rows stay finite, their H1 / Z2 rows are read by no
         # train row and their dY2 rows are exactly 0, so the update is unchanged;
-        # evaluation aggregates every row.  Env CGNN_L1_TRAIN_NBRS=0: every row.
+        # evaluation aggregates every row (l1_train_neighbours=False: every row).
         self._l1 = None
-        if (self._l2 is not None and self._win is None
-                and os.environ.get("CGNN_L1_TRAIN_NBRS", "1") != "0"):
+        if self._l2 is not None and l1_train_neighbours:
             self._l1 = self._train_neighbour_csr(g)
         self._async = None                 # collectives overlapped? (decided at first use)
         self.epoch = 0
@@ -353,7 +340,7 @@ class GCNTrainer:
 
     def _setup_halo(self, r0, r1, per):
         """The full halo (every remote row this rank's edges read): evaluation, and
-        training with CGNN_L2_ALL_ROWS=1."""
+        training with train_rows_only=False."""
         self._hplan = self._halo_plan(self.col_rem)
         self.col_rem = self._hplan.col
 
@@ -400,11 +387,11 @@ class GCNTrainer:
         l2.plan = None
         if self.multi:
             l2.rp_loc, l2.col_loc, l2.rp_rem, col_rem = self._split_local(self.r0, self.r1, l2.rp, l2.col)
-            if torch.distributed.is_initialized() and os.environ.get("CGNN_TRAIN_HALO", "1") != "0":
+            if torch.distributed.is_initialized() and self._train_halo:
                 # a halo of its own: only the remote rows the train rows read travel in
                 # training epochs (planted-community graph after the reorder: ~10 % of
                 # the other ranks' rows at 8 ranks, ~40 % at 2, against 66-97 % for the
-                # full halo); env CGNN_TRAIN_HALO=0: the evaluation's exchange
+                # full halo); train_halo=False: the evaluation's exchange
                 l2.plan = self._halo_plan(col_rem)
                 col_rem = l2.plan.col
             elif self.halo:
@@ -474,28 +461,15 @@ class GCNTrainer:
             torch.distributed.all_gather_into_tensor(out, inp)
 
     def _aggregate_features(self, out, train: bool = False):
-        if self._win is not None:
-            ops.spmm_win(self._win, self.rowptr, self.col, self.Xs, self.F, rscale=self.dinv, out=out,
-                         unit_col=self.F)
-            return
         rp, col = self._l1 if (train and self._l1 is not None) else (self.rowptr, self.col)
         ops.spmm(rp, col, self.Xs, self.F, rscale=self.dinv, out=out, unit_col=self.F)
 
     def forward(self, train: bool):
         n, F, C = self.nloc, self.F, self.C
-        if self._ax_ready and self._side is not None:
-            torch.cuda.current_stream(self.dev).wait_event(self._ax_event)
         # a prefetched AX restricted to the train-neighbour rows serves training only
         if not self._ax_ready or not (train or self._l1 is None):
             self._aggregate_features(self.AX, train)
         self._ax_ready = False
-        if train and self._side is not None:
-            # AX_next held the previous epoch's AX: the side stream first waits for
-            # everything queued so far on this stream (that epoch's backward read it)
-            self._side.wait_stream(torch.cuda.current_stream(self.dev))
-            with torch.cuda.stream(self._side):
-                self._aggregate_features(self.AX_next, True)
-                self._ax_event.record(self._side)
         H1 = self.H1[:n]
         p = self.p if train else 0.0
         if not self.fused_bwd:           # bf16 W2 of the unfused fallbacks (the fused kernels read fp32)

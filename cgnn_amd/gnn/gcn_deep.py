@@ -28,7 +28,6 @@ epilogue, and the whole forward captured into one hipGraph.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional, Sequence
 
 import torch
@@ -61,7 +60,7 @@ def _splits(g: GraphData):
 class DeepGCNTrainer:
     def __init__(self, g: GraphData, hidden: int = 256, layers: int = 3, dropout: float = 0.5,
                  lr: float = 0.01, dtype: torch.dtype = torch.bfloat16, seed: int = 0,
-                 capture: Optional[bool] = None, fused: Optional[bool] = None):
+                 capture: Optional[bool] = None, fused: Optional[bool] = None, train_rows_only: bool = True):
         self.dev = g.rowptr.device
         cuda = self.dev.type == "cuda"
         if fused is None:
@@ -74,7 +73,7 @@ class DeepGCNTrainer:
         self.layers = layers
         self.epoch = 0
         if self.fused:
-            self._fused = _FusedDeepGCN(g, hidden, layers, dropout, lr, seed)
+            self._fused = _FusedDeepGCN(g, hidden, layers, dropout, lr, seed, train_rows_only)
             self._step_graph = StepGraph(self._fused.train_body, enabled=cuda if capture is None else capture and cuda,
                                          device=self.dev)
             return
@@ -141,7 +140,8 @@ class _FusedDeepGCN:
     (glorot-uniform W from the same generator sequence, zero b), Adam moments and a
     device step counter beside it."""
 
-    def __init__(self, g: GraphData, hidden: int, layers: int, dropout: float, lr: float, seed: int):
+    def __init__(self, g: GraphData, hidden: int, layers: int, dropout: float, lr: float, seed: int,
+                 train_rows_only: bool = True):
         dev = g.rowptr.device
         self.dev, self.n, self.L = dev, g.n, layers
         self.F, self.C, self.p, self.lr = g.n_features, g.n_classes, float(dropout), float(lr)
@@ -205,11 +205,11 @@ class _FusedDeepGCN:
         self.col_T = self.gslot[col[keep]].contiguous()
         self.Gc = torch.zeros(max(self.n_train, 1), ld[-1], **bf)
         # training epochs: the last aggregation (+ cross-entropy) only at the train rows,
-        # the only logits the loss reads (exact; see gcn.GCNTrainer).  Env
-        # CGNN_L2_ALL_ROWS=1: every row
+        # the only logits the loss reads (exact; see gcn.GCNTrainer; train_rows_only=False:
+        # every row)
         self._tr = None
         trows = torch.nonzero(train).flatten()
-        if trows.numel() and os.environ.get("CGNN_L2_ALL_ROWS", "0") == "0":
+        if trows.numel() and train_rows_only:
             rpl = self.rowptr.long()
             lo, dg = rpl[trows], rpl[trows + 1] - rpl[trows]
             # long rows first (a whole wave each in spmm_ce); slot = ascending position
@@ -308,9 +308,9 @@ class GCNInference:
         # features pre-scaled by the column normalisation once (static input)
         self.xs = pad_cols(g.x.float() * g.dinv[:, None]).to(dtype).contiguous()
         self.W, self.b, self.Wf = [], [], []
-        # gathered rows padded to whole 128-B lines (env CGNN_INFER_ALIGN=0: packed to 8 elements;
-        # Reddit layer 2: 1.24 vs 1.40 ms, profiles/r03_cfgs) -- an aligned row touches whole lines only
-        align = 64 if os.environ.get("CGNN_INFER_ALIGN", "1") != "0" and dtype != torch.float32 else 8
+        # gathered rows padded to whole 128-B lines (against packing to 8 elements: Reddit
+        # layer 2 1.24 vs 1.40 ms, profiles/r03_cfgs) -- an aligned row touches whole lines only
+        align = 64 if dtype != torch.float32 else 8
         for k, (W, b) in enumerate(weights):
             W = W.detach().float()
             if W.shape[0] < (self.xs.shape[1] if k == 0 else self.W[-1].shape[1]):
@@ -331,10 +331,7 @@ class GCNInference:
         # cores, the D^-1/2 row scale of the next gather in its epilogue) into fixed buffers
         self._lin = cuda and dtype in (torch.float16, torch.bfloat16)
         # every layer on the hand-written MFMA layer: Reddit's 602-wide first layer (a
-        # weight too wide for LDS whole) takes lin_fwd's K-chunked GEMM form; layers wider
-        # than CGNN_INFER_LIN_KMAX (env knob for A/B against the library GEMM) use
-        # torch.matmul instead
-        self._lin_kmax = int(os.environ.get("CGNN_INFER_LIN_KMAX") or "100000")
+        # weight too wide for LDS whole) takes lin_fwd's K-chunked GEMM form
         if self._lin:
             self.z = [torch.zeros(g.n, W.shape[1], dtype=dtype, device=self.dev) for W in self.Wf]
             self.dinv32 = self.ng.dinv.float().contiguous()
@@ -350,7 +347,7 @@ class GCNInference:
         h = self.xs
         L = len(self.W)
         for k in range(L):
-            if self._lin and self.Wf[k].shape[0] <= self._lin_kmax:
+            if self._lin:
                 # Z = rs * (H W) on the MFMA layer; rs = D^-1/2 folded into the epilogue
                 # (the input features are pre-scaled once, so layer 1 has no row scale)
                 z = lin_fwd(h, self.Wf[k], None, K1=self.Wf[k].shape[0],

@@ -6,7 +6,6 @@ mandatory -- a missing extension raises instead of silently falling back.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -137,12 +136,15 @@ def spmm_ell(ell, col, X, F, rscale=None, out=None):
     return out
 
 
+CE_LONG_DEGREE = 256     # rows above this degree get a wave of their own in spmm_ce
+
+
 def long_row_order(deg: torch.Tensor, threshold: Optional[int] = None):
     """Row order for ``spmm_ce(..., n_long=k)``: the rows of degree > threshold first (in
-    their original order), then the others; returns (order, k).  Default threshold: env
-    CGNN_CE_LONG (0 disables the long-row mode)."""
+    their original order), then the others; returns (order, k).  Default threshold
+    CE_LONG_DEGREE; 0 disables the long-row mode."""
     if threshold is None:
-        threshold = int(os.environ.get("CGNN_CE_LONG", "256"))
+        threshold = CE_LONG_DEGREE
     if threshold <= 0:
         return torch.arange(deg.numel(), device=deg.device), 0
     longr = deg > threshold
@@ -254,79 +256,6 @@ def slab_sum(P, out, index=None, groups=None):
             stage = _STAGE[key] = torch.empty(G * W, dtype=torch.float32, device=P.device)
     native.hip().gnn_slab_sum(P.data_ptr(), S, W, stage.data_ptr() if stage is not None else 0, G,
                               out.data_ptr(), index.data_ptr() if index is not None else 0, _st(P))
-    return out
-
-
-def win_start(rb0: int, R: int, WR: int, row_off: int, n_src: int) -> int:
-    """First source row of the LDS window of the block starting at local row rb0
-    (mirror of ``win_start`` in gnn_sparse.hip)."""
-    return max(0, min(row_off + rb0 + R // 2 - WR // 2, n_src - WR))
-
-
-class WindowPlan:
-    """Schedule of the LDS-windowed SpMM (``spmm_win_kernel``, gnn_sparse.hip): blocks
-    of ``R`` rows, each staging the ``WR`` source rows around its own rows in LDS;
-    ``split[i] = (a, b)`` marks the edges of row ``i`` that read the window.  Built
-    once per (CSR, feature width) -- by a HIP kernel on a GPU, by searchsorted on the
-    CPU (the reference the GPU plan is tested against).  ``rowptr``/``col``: local rows
-    with column ids into a source matrix of ``n_src`` rows whose row ``row_off + i`` is
-    local row ``i``'s own (the row partition of a multi-GPU run)."""
-
-    def __init__(self, rowptr, col, F: int, n_src: int, row_off: int = 0, R: int = 256, WR=None, pitch=None):
-        self.n = rowptr.numel() - 1
-        self.nnz = int(col.numel())
-        self.F, self.n_src, self.row_off, self.R = int(F), int(n_src), int(row_off), int(R)
-        # LDS row pitch in 16-B chunks: ceil(F / 8), or 16 (256 B: the lane groups of
-        # ds_read_b128 then never conflict, at a smaller window)
-        lp = max(int(pitch or 0), (self.F + 7) // 8)
-        self.lp = lp
-        wmax = (10239 // lp) // 8 * 8 if 1 <= lp <= 16 else 0
-        self.WR = min(int(WR) if WR else wmax, wmax, self.n_src)
-        if self.R <= 0 or self.R % 4 or self.WR <= 0:
-            raise ValueError("WindowPlan: R must be a positive multiple of 4 and the window non-empty")
-        self.split = torch.empty(self.n, 2, dtype=torch.int32, device=rowptr.device)
-        if rowptr.is_cuda:
-            native.hip().gnn_spmm_win_plan(rowptr.data_ptr(), col.data_ptr(), self.split.data_ptr(), self.n,
-                                           self.row_off, self.n_src, self.R, self.WR, _st(rowptr))
-        else:
-            self.split.copy_(self.reference_split(rowptr, col))
-
-    def reference_split(self, rowptr, col):
-        rp = rowptr.cpu().long()
-        c = col.cpu().long()
-        blk = torch.arange(self.n) // self.R * self.R
-        w0 = (self.row_off + blk + self.R // 2 - self.WR // 2).clamp(max=self.n_src - self.WR).clamp(min=0)
-        rows = _row_ids(rp)
-        below = torch.zeros(self.n, dtype=torch.int64).index_add_(0, rows, (c < w0[rows]).long())
-        inside = torch.zeros(self.n, dtype=torch.int64).index_add_(
-            0, rows, ((c >= w0[rows]) & (c < w0[rows] + self.WR)).long())
-        a = rp[:-1] + below
-        return torch.stack([a, a + inside], 1).to(torch.int32)
-
-    def in_window_fraction(self) -> float:
-        s = self.split.long()
-        return float((s[:, 1] - s[:, 0]).sum()) / max(1, self.nnz)
-
-
-def spmm_win(plan: WindowPlan, rowptr, col, X, F, rscale=None, out=None, unit_col=-1):
-    """``spmm`` (no bias / ReLU / init / cscale) through the LDS-windowed kernel; the CPU
-    branch is the plain reference aggregate."""
-    if not X.is_cuda:
-        return spmm(rowptr, col, X, F, rscale=rscale, out=out, unit_col=unit_col)
-    n = rowptr.numel() - 1
-    if out is None:
-        out = torch.empty(n, X.shape[1], dtype=torch.bfloat16, device=X.device)
-    if X.dtype != torch.bfloat16 or out.dtype != torch.bfloat16 or F != plan.F or n != plan.n:
-        raise ValueError("spmm_win: bf16 X / out of the planned shape expected")
-    if X.shape[0] < plan.n_src:
-        raise ValueError("spmm_win: X has fewer rows than the plan's sources")
-    if checks.enabled():
-        checks.csr(rowptr, col, X.shape[0], "spmm_win")
-        checks.rows(out, n, "spmm_win out")
-        checks.rows(rscale, n, "spmm_win rscale")
-    native.hip().gnn_spmm_win(rowptr.data_ptr(), col.data_ptr(), plan.split.data_ptr(), X.data_ptr(),
-                              out.data_ptr(), rscale.data_ptr() if rscale is not None else 0, n, F, X.shape[1],
-                              out.shape[1], int(unit_col), plan.row_off, plan.n_src, plan.R, plan.WR, plan.lp, _st(X))
     return out
 
 

@@ -25,7 +25,7 @@ def _to_feature_major(x: torch.Tensor, D: int) -> torch.Tensor:
 
 class _MMDHip(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pred, true, kernel="auto"):
+    def forward(ctx, pred, true, kernel="auto", symmetric=True):
         hip = native.hip()
         R, N, d = pred.shape
         D = padded_dim(d)
@@ -35,7 +35,7 @@ class _MMDHip(torch.autograd.Function):
         row_tiles, n_chunks, tpc = mmd_geometry(N, R)
         dev = pred.device
         mf_rb, mf_chunks, mf_tpc = mmd_mfma_geometry(N, R)
-        mirror = mmd_mirror_slots(D, N) if kernel == "valu" else 0
+        mirror = mmd_mirror_slots(D, N, symmetric) if kernel == "valu" else 0
         gradp = torch.empty(max(n_chunks + mirror, mf_chunks), R, D, N, dtype=torch.float32, device=dev)
         lpart = torch.empty(R, max(row_tiles * n_chunks, mf_rb * mf_chunks), dtype=torch.float32, device=dev)
         tt = torch.zeros(R, dtype=torch.float32, device=dev)
@@ -73,17 +73,18 @@ class _MMDHip(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         (g,) = ctx.saved_tensors
-        return (gout.view(-1, 1, 1).to(g.dtype) * g).to(gout.dtype), None, None
+        return (gout.view(-1, 1, 1).to(g.dtype) * g).to(gout.dtype), None, None, None
 
 
-def mmd_loss(pred: torch.Tensor, true: torch.Tensor, kernel: str = "auto") -> torch.Tensor:
+def mmd_loss(pred: torch.Tensor, true: torch.Tensor, kernel: str = "auto", symmetric: bool = True) -> torch.Tensor:
     """Biased multi-bandwidth MMD^2; ``[N,d]`` -> scalar or ``[R,N,d]`` -> ``[R]``.
-    ``kernel``: 'auto' | 'mfma' (matrix cores, padded d >= 8) | 'valu'."""
+    ``kernel``: 'auto' | 'mfma' (matrix cores, padded d >= 8) | 'valu'; ``symmetric``
+    (vector kernel): evaluate half of the pred-pred block and mirror it."""
     batched = pred.dim() == 3
     p = pred if batched else pred.unsqueeze(0)
     t = true if batched else true.unsqueeze(0)
     if p.is_cuda:
-        out = _MMDHip.apply(p, t.detach(), kernel)
+        out = _MMDHip.apply(p, t.detach(), kernel, symmetric)
     else:
         out = torch.stack([mmd_loss_dense(p[r], t[r]) for r in range(p.shape[0])])
     return out if batched else out[0]

@@ -48,7 +48,7 @@ def test_mmd_loss_and_grad_match_oracle(N, d, kernel):
 
 
 @pytest.mark.parametrize("N,d", [(1500, 2), (513, 6), (800, 8)])
-def test_mmd_symmetric_training_matches_full_block(N, d, monkeypatch):
+def test_mmd_symmetric_training_matches_full_block(N, d):
     """The mirrored pred-pred evaluation (off-diagonal tiles once, column sums by the
     staggered DPP rotation) equals the full-block kernel to fp32 rounding, and the
     symmetric launch really adds its mirror slots."""
@@ -59,10 +59,9 @@ def test_mmd_symmetric_training_matches_full_block(N, d, monkeypatch):
     pred = torch.randn(4, N, d, device="cuda")
     true = torch.randn(4, N, d, device="cuda") * 0.8 - 0.3
     outs = []
-    for sym in ("1", "0"):
-        monkeypatch.setenv("CGNN_MMD_SYM", sym)
+    for sym in (True, False):
         p = pred.clone().requires_grad_(True)
-        L = mmd_loss(p, true, kernel="valu")
+        L = mmd_loss(p, true, kernel="valu", symmetric=sym)
         L.sum().backward()
         outs.append((L.detach(), p.grad))
     (l1, g1), (l0, g0) = outs
@@ -206,10 +205,9 @@ def test_row_range_mmd_tiles_the_full_mmd(d, kernel):
     np.testing.assert_allclose((total / N**2).numpy(), ref.detach().numpy(), rtol=2e-4, atol=1e-7)
 
 
-@pytest.mark.parametrize("min_d", ["8", "1"])      # 8: the pair on the vector path, the DAG on MFMA
-def test_rff_matrix_core_matches_oracle_and_vector(monkeypatch, min_d):
+def test_rff_matrix_core_matches_oracle():
     """Fast MMD (random Fourier features) on the exact-fp32 matrix cores vs the fp64
-    oracle and vs the vector kernels, on a 10-variable DAG (padded D = 12) and a pair."""
+    oracle, on a 10-variable DAG (padded D = 12) and a pair."""
     H = 16
     g = DirectedGraph()
     for k in range(9):
@@ -221,16 +219,39 @@ def test_rff_matrix_core_matches_oracle_and_vector(monkeypatch, min_d):
         kw = dict(learning_rate=0.01, init_std=0.05, use_fast_mmd=True, nb_vectors=30)
         ref = ReferenceTrainer([prog] * 3, datas, keys, H, **kw)
         ref_scores = ref.run(6, 4)
-        monkeypatch.setenv("CGNN_RFF_MFMA_MIN_D", min_d)
         a = DeviceTrainer([prog] * 3, datas, keys, H, "cuda:0", record_history=6, **kw)
         sa = a.run(6, 4)
-        monkeypatch.setenv("CGNN_RFF_VALU", "1")
-        b = DeviceTrainer([prog] * 3, datas, keys, H, "cuda:0", record_history=6, **kw)
-        sb = b.run(6, 4)
-        monkeypatch.delenv("CGNN_RFF_VALU")
         np.testing.assert_allclose(a.history(), np.array(ref.loss_history), rtol=3e-3, atol=1e-5)
         np.testing.assert_allclose(sa, ref_scores, rtol=3e-3, atol=1e-5)
-        np.testing.assert_allclose(sa, sb, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("D", [2, 12, 64])
+def test_rff_matrix_core_equals_vector_kernels(D):
+    """The matrix-core and the vector Fourier-feature kernels on the same draws: same
+    loss partials and gradient up to summation order."""
+    hip = native.hip()
+    R, N, k = 3, 333, 30
+    F = 7 * k
+    torch.manual_seed(D)
+    xhat = torch.randn(R, D, N, device="cuda") * 0.7
+    data = torch.randn(R, D, N, device="cuda") * 0.7 + 0.1
+    keys = torch.randint(0, 2**31 - 1, (R, 2), dtype=torch.int32, device="cuda")
+    step = torch.zeros(2, dtype=torch.int32, device="cuda")
+    W = torch.zeros(R, F, D + 1, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    hip.rff_freqs(W.data_ptr(), keys.data_ptr(), step.data_ptr(), 0, k, D, 7, D, R, st)
+    outs = []
+    for force in (0, 1):
+        diff = torch.zeros(R, F, device="cuda")
+        lp = torch.zeros(R, (F + 255) // 256, device="cuda")
+        gp = torch.zeros(1, R, D, N, device="cuda")
+        hip.rff_fwd_bwd(0, xhat.data_ptr(), data.data_ptr(), W.data_ptr(), diff.data_ptr(), lp.data_ptr(),
+                        gp.data_ptr(), N, D, F, R, k, (2.0 / k) ** 0.5, st, force_valu=force)
+        outs.append((lp.sum(1), gp))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=1e-6)
+    g = outs[1][1]
+    torch.testing.assert_close(outs[0][1], g, rtol=1e-3, atol=1e-4 * float(g.abs().max()))
 
 
 def test_sample_sharded_trainer_gpu_matches_oracle_and_engine():

@@ -136,14 +136,15 @@ def test_staged_state_placements_bitwise(H):
     tr.run(3, 1)
     torch.cuda.synchronize()
     st = torch.cuda.current_stream().cuda_stream
-    P, D, W = tr.P, tr.D, tr.stage_w
+    P, D = tr.P, tr.D
+    W = 4                     # every placement fits at 4 waves per block
     outs = []
     for force in (0, 1):
         xh = torch.zeros_like(tr.xhat)
         xn = torch.zeros_like(tr.xnorm)
         hip.gen_fwd_staged(tr.prog.data_ptr(), tr.prog_stride, tr.sched.data_ptr(), tr.sched_stride,
                            tr.params.data_ptr(), P, tr.data.data_ptr(), xh.data_ptr(), tr.noise.data_ptr(), tr.NS,
-                           xn.data_ptr(), N, D, d, H, R, W, st, force=force)
+                           xn.data_ptr(), N, D, d, H, tr.max_in, R, W, st, force=force)
         outs.append((xh, xn))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

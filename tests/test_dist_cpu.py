@@ -71,17 +71,18 @@ def _strip_train(g, world):
     return g
 
 
-def _gcn_worker(rank, world, port, out, halo=None, strip=False):
+def _gcn_worker(rank, world, port, out, halo=None, strip=False, kw=None):
     _init(rank, world, port)
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
+    kw = kw or {}
     g = synthetic("ogbn-products", seed=0, scale=0.002)
     if strip:
         _strip_train(g, world)
-    tr = GCNTrainer(g, hidden=64, halo=halo)
+    tr = GCNTrainer(g, hidden=64, halo=halo, **kw)
     assert tr.halo == (halo if halo is not None else world >= 4)
     if tr._l2 is not None:
-        assert (tr._l2.plan is not None) == (os.environ["CGNN_TRAIN_HALO"] != "0")
+        assert (tr._l2.plan is not None) == kw.get("train_halo", True)
     tr.train_step()
     p1 = tr.params.clone().numpy().tolist()
     for _ in range(3):
@@ -95,20 +96,18 @@ def _gcn_worker(rank, world, port, out, halo=None, strip=False):
     (2, False, "0", "0", "0"), (2, True, "0", "0", "0"), (4, None, "0", "0", "0"), (2, False, "1", "0", "1"),
     (4, None, "1", "0", "1"), (2, True, "1", "1", "1"), (4, None, "1", "1", "1"), (3, True, "1", "0", "1"),
     (3, None, "1", "0", "strip")])
-def test_gcn_row_partition_matches_single_process(world, halo, overlap, all_rows, train_halo, monkeypatch):
+def test_gcn_row_partition_matches_single_process(world, halo, overlap, all_rows, train_halo):
     """Row-partitioned GCN over gloo ranks == one process; layer-2 rows of other
     ranks by all-gather or by the halo all-to-all (the default from 4 ranks); the
     backward's compact-gradient all-gather blocking or overlapped with the local edges
-    (CGNN_BWD_OVERLAP); training layer 2 over the train rows only (default) or over
-    every row (CGNN_L2_ALL_ROWS=1, against the one-process train-row run); the
-    training epochs' own halo of the train rows' sources (CGNN_TRAIN_HALO); "strip":
-    the last rank owns no train row (it joins the training halo with a placeholder)."""
+    (bwd_overlap); training layer 2 over the train rows only (default) or over every
+    row (train_rows_only=False, against the one-process train-row run); the training
+    epochs' own halo of the train rows' sources (train_halo); "strip": the last rank
+    owns no train row (it joins the training halo with a placeholder)."""
     strip = train_halo == "strip"
     if strip:
         train_halo = "1"
-    monkeypatch.setenv("CGNN_BWD_OVERLAP", overlap)
-    monkeypatch.setenv("CGNN_L2_ALL_ROWS", "0")
-    monkeypatch.setenv("CGNN_TRAIN_HALO", train_halo)
+    kw = dict(bwd_overlap=overlap == "1", train_rows_only=all_rows == "0", train_halo=train_halo == "1")
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
     g = synthetic("ogbn-products", seed=0, scale=0.002)
@@ -116,7 +115,6 @@ def test_gcn_row_partition_matches_single_process(world, halo, overlap, all_rows
         _strip_train(g, world)
     tr = GCNTrainer(g, hidden=64, rank=0, world=1)
     assert tr._l2 is not None
-    monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
     tr.train_step()
     p1 = tr.params.clone().numpy()
     for _ in range(3):
@@ -124,7 +122,7 @@ def test_gcn_row_partition_matches_single_process(world, halo, overlap, all_rows
     ref = tr.evaluate()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_gcn_worker, args=(world, _free_port(), out, halo, strip), nprocs=world, join=True)
+    mp.spawn(_gcn_worker, args=(world, _free_port(), out, halo, strip, kw), nprocs=world, join=True)
     for r in range(world):
         res, params, q1 = out[r]
         # after one step the partitioned run equals the single-process one up to the
@@ -137,17 +135,16 @@ def test_gcn_row_partition_matches_single_process(world, halo, overlap, all_rows
         np.testing.assert_array_equal(out[0][1], out[r][1])
 
 
-def test_gcn_train_row_layer2_matches_all_rows(monkeypatch):
+def test_gcn_train_row_layer2_matches_all_rows():
     """Training epochs that aggregate layer 2 only at the train rows give the same
     losses and parameters as aggregating every row (one process)."""
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gcn import GCNTrainer
     g = synthetic("ogbn-products", seed=1, scale=0.002)
     runs = []
-    for all_rows in ("1", "0"):
-        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
-        tr = GCNTrainer(g, hidden=64, rank=0, world=1)
-        assert (tr._l2 is None) == (all_rows == "1")
+    for rows_only in (False, True):
+        tr = GCNTrainer(g, hidden=64, rank=0, world=1, train_rows_only=rows_only)
+        assert (tr._l2 is None) == (not rows_only)
         losses = []
         for _ in range(4):
             tr.train_step()
@@ -256,9 +253,6 @@ def _gat_params(tr):
 
 def _gat_shard_worker(rank, world, port, out, fused=False, heads=2, dropout=0.0, chunk=4 << 30, strip=False,
                       l1_exchange=False, train_halo=True):
-    import os
-    os.environ["CGNN_GAT_L1_EXCHANGE"] = "1" if l1_exchange else "0"
-    os.environ["CGNN_TRAIN_HALO"] = "1" if train_halo else "0"
     _init(rank, world, port)
     from cgnn_amd.gnn.data import synthetic_shard
     from cgnn_amd.gnn.gat import ShardedGATTrainer
@@ -267,7 +261,7 @@ def _gat_shard_worker(rank, world, port, out, fused=False, heads=2, dropout=0.0,
     if strip and rank == world - 1:          # this rank owns no train row
         shard.mask[shard.mask == 1] = 2
     tr = ShardedGATTrainer(shard, heads=heads, head_dim=8, dropout=dropout, lr=0.01, seed=rank, fused=fused,
-                           halo_chunk_bytes=chunk)
+                           halo_chunk_bytes=chunk, l1_exchange=l1_exchange, train_halo=train_halo)
     if chunk < (1 << 20):
         assert tr.halo.rounds > 1
     if tr.fused is not None and train_halo:
@@ -325,7 +319,7 @@ def test_sharded_fused_gat_matches_single_process(world, chunk, strip, l1x):
     layer 2 runs at the train rows over a training halo; ``strip``: the last rank
     owns no train row (placeholder row in the collective plan).  Layer 1 is projected
     locally from the setup-time halo input rows (no per-epoch exchange) unless ``l1x``
-    (CGNN_GAT_L1_EXCHANGE=1: the per-epoch [Wh | s_src] exchange)."""
+    (l1_exchange=True: the per-epoch [Wh | s_src] exchange)."""
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.gat import ShardedGATTrainer
     g = synthetic("ogbn-products", seed=1, scale=0.0005)
@@ -372,7 +366,7 @@ def test_sharded_fused_gat_matches_single_process(world, chunk, strip, l1x):
 
 
 def test_sharded_fused_gat_without_train_halo_rank_without_train_rows():
-    """CGNN_TRAIN_HALO=0 with a rank that owns no train row: the train-neighbour flag
+    """train_halo=False with a rank that owns no train row: the train-neighbour flag
     exchange must still run on every rank (a per-rank decision around a collective would
     pair that rank's first training exchange with its peers' flag exchange)."""
     from cgnn_amd.gnn.data import synthetic

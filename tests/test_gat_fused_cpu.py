@@ -11,9 +11,9 @@ from cgnn_amd.gnn.gat import GATTrainer, GraphCSR
 from cgnn_amd.gnn.gat_fused import FusedGAT, row_ce, wcat, wcat_bwd
 
 
-def _setup(heads=4, head_dim=8, dropout=0.0):
+def _setup(heads=4, head_dim=8, dropout=0.0, **kw):
     g = synthetic("ogbn-products", seed=2, scale=0.001)
-    tr = GATTrainer(g, heads=heads, head_dim=head_dim, dropout=dropout, lr=0.01, seed=0, fused=True)
+    tr = GATTrainer(g, heads=heads, head_dim=head_dim, dropout=dropout, lr=0.01, seed=0, fused=True, **kw)
     assert tr.fused is not None
     return g, tr
 
@@ -46,20 +46,19 @@ def test_fused_gat_gradients_match_autograd():
             off += k
 
 
-def test_fused_gat_train_row_layer2_matches_all_rows(monkeypatch):
+def test_fused_gat_train_row_layer2_matches_all_rows():
     """Training epochs aggregating layer 2 only at the train rows: the same first-step
     gradients as aggregating every row (dropout on: the same masks), up to the bf16
     rounding of the stored operands, and the same losses over a few Adam steps."""
     runs = []
-    for all_rows in ("1", "0"):
-        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
-        g, tr = _setup(dropout=0.3)
+    for rows_only in (False, True):
+        g, tr = _setup(dropout=0.3, train_rows_only=rows_only)
         f = tr.fused
-        assert (f._tr is None) == (all_rows == "1")
+        assert (f._tr is None) == (not rows_only)
         f.forward(train=True)
         f.backward()
         grads = f.grads.clone()
-        g, tr = _setup(dropout=0.3)
+        g, tr = _setup(dropout=0.3, train_rows_only=rows_only)
         runs.append((grads, [float(tr.train_step()) for _ in range(3)]))
     scale = runs[0][0].abs().max().item()
     assert (runs[1][0] - runs[0][0]).abs().max().item() < 2e-4 * scale

@@ -258,15 +258,14 @@ def test_sharded_fused_gat_gpu_matches_one_rank(world, chunk):
     np.testing.assert_array_equal(out[0][2], out[1][2])              # replicas identical
 
 
-def test_fused_gat_train_row_layer2_gpu_matches_all_rows(monkeypatch):
+def test_fused_gat_train_row_layer2_gpu_matches_all_rows():
     """HIP path: layer 2 aggregated at the train rows only in training (default) gives
     the first-step gradients and the losses of the all-row aggregation."""
     g = synthetic("ogbn-products", seed=5, device="cuda:0", scale=0.003)
     runs = []
-    for all_rows in ("1", "0"):
-        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
-        tr = GATTrainer(g, heads=4, head_dim=32, dropout=0.5, lr=0.01, seed=0)
-        assert tr.fused is not None and (tr.fused._tr is None) == (all_rows == "1")
+    for rows_only in (False, True):
+        tr = GATTrainer(g, heads=4, head_dim=32, dropout=0.5, lr=0.01, seed=0, train_rows_only=rows_only)
+        assert tr.fused is not None and (tr.fused._tr is None) == (not rows_only)
         losses = [float(tr.train_step())]
         grads = tr.fused.grads.clone().cpu()
         losses += [float(tr.train_step()) for _ in range(2)]

@@ -563,63 +563,6 @@ def test_fused_sage_gpu_matches_cpu_reference():
     assert last < first
 
 
-@pytest.mark.parametrize("F,ld,R,WR,row_off,n_src", [(100, 128, 256, None, 0, None), (100, 104, 64, 200, 0, None),
-                                                  (47, 64, 128, 96, 0, None), (128, 128, 32, 300, 700, 2500),
-                                                  (100, 128, 16, None, 1500, 2500)])
-def test_spmm_win_matches_reference(F, ld, R, WR, row_off, n_src):
-    """LDS-windowed SpMM (window staged per block, in-window edges from LDS, the rest
-    gathered) vs the fp32 reference aggregate; a locality-ordered graph so that both
-    edge classes occur, and a row-partition slice (row_off, n_src) like a rank's rows."""
-    g = synthetic("cora", seed=3, scale=1.0, id_order="banded")
-    n_all = g.n if n_src is None else n_src
-    rng = np.random.default_rng(4)
-    if n_src is not None:      # a rank's slice: local rows [row_off, row_off + nloc) of a bigger source set
-        nloc = 700
-        src = rng.integers(0, nloc, 9000) + row_off
-        dst = np.clip(src + rng.integers(-150, 150, 9000), 0, n_all - 1)
-        dst[::5] = rng.integers(0, n_all, dst[::5].shape[0])
-        full_rp, full_col = build_csr(n_all, src, dst, "cpu")
-        rp = (full_rp[row_off:row_off + nloc + 1] - full_rp[row_off]).to(torch.int32)
-        col = full_col[int(full_rp[row_off]):int(full_rp[row_off + nloc])].contiguous()
-    else:
-        rp, col = g.rowptr.cpu(), g.col.cpu()
-    n = rp.numel() - 1
-    torch.manual_seed(5)
-    X = torch.randn(n_all, ld)
-    X[:, F:] = 0
-    X = X.to(torch.bfloat16)
-    rs = torch.rand(n) + 0.5
-    ref = ops.spmm(rp, col, X, F, rscale=rs, unit_col=F if F < ld else -1)
-    plan_cpu = ops.WindowPlan(rp, col, F, n_all, row_off=row_off, R=R, WR=WR)
-    plan = ops.WindowPlan(rp.cuda(), col.cuda(), F, n_all, row_off=row_off, R=R, WR=WR)
-    assert torch.equal(plan.split.cpu(), plan_cpu.split)
-    frac = plan.in_window_fraction()
-    assert 0.05 < frac < 1.0, frac
-    got = ops.spmm_win(plan, rp.cuda(), col.cuda(), X.cuda(), F, rscale=rs.cuda(),
-                       unit_col=F if F < ld else -1).cpu()
-    np.testing.assert_allclose(got.float().numpy(), ref.float().numpy(), rtol=2e-2, atol=2e-2)
-    if F < ld:
-        assert torch.all(got[:, F] == 1) and torch.all(got[:, F + 1:] == 0)
-
-
-def test_gcn_side_stream_layer1_pipeline_is_exact(monkeypatch):
-    """One GPU: the next epoch's layer-1 aggregation on a side stream (CGNN_AX_PIPELINE=1)
-    gives bitwise the same losses as the in-line schedule (default), including an
-    evaluation between epochs."""
-    g = synthetic("ogbn-products", seed=2, device="cuda:0", scale=0.002)
-    runs = []
-    for pipe in ("1", "0"):
-        monkeypatch.setenv("CGNN_AX_PIPELINE", pipe)
-        tr = GCNTrainer(g, hidden=64, rank=0, world=1, reorder=True)
-        assert (tr._side is not None) == (pipe == "1")
-        losses = [float(tr.train_step()[0]) for _ in range(3)]
-        ev = tr.evaluate()
-        losses += [float(tr.train_step()[0]) for _ in range(2)]
-        runs.append((losses, ev))
-    assert runs[0][0] == runs[1][0]
-    assert runs[0][1] == runs[1][1]
-
-
 @pytest.mark.parametrize("S,W,G,mapped", [(76531, 68, None, False), (256, 49152, None, True), (7, 5, 1, False),
                                           (5000, 130, 64, True)])
 def test_slab_sum_matches_torch(S, W, G, mapped):
@@ -646,16 +589,15 @@ def test_slab_sum_matches_torch(S, W, G, mapped):
     assert torch.equal(out, out2)          # deterministic
 
 
-def test_gcn_train_row_layer2_gpu_matches_all_rows(monkeypatch):
+def test_gcn_train_row_layer2_gpu_matches_all_rows():
     """One GPU, HIP path: training epochs that aggregate layer 2 only at the train rows
     (default) give the losses, parameters and evaluation of the all-row aggregation
-    (CGNN_L2_ALL_ROWS=1) up to summation order."""
+    (train_rows_only=False) up to summation order."""
     g = synthetic("ogbn-products", seed=4, device="cuda:0", scale=0.004)
     runs = []
-    for all_rows in ("1", "0"):
-        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
-        tr = GCNTrainer(g, hidden=64, rank=0, world=1)
-        assert (tr._l2 is None) == (all_rows == "1")
+    for rows_only in (False, True):
+        tr = GCNTrainer(g, hidden=64, rank=0, world=1, train_rows_only=rows_only)
+        assert (tr._l2 is None) == (not rows_only)
         losses = []
         for _ in range(4):
             tr.train_step()

@@ -165,34 +165,6 @@ def test_fused_deep_gcn_dropout_trains_on_cpu():
     assert t.evaluate()["train_loss"] < r0["train_loss"]
 
 
-def test_window_plan_split_marks_exactly_the_in_window_edges():
-    """WindowPlan (the schedule of the LDS-windowed SpMM): for every row, the edges
-    [a, b) are exactly those whose source lies in the row block's window."""
-    import numpy as np
-    from cgnn_amd.gnn import ops
-    from cgnn_amd.gnn.data import build_csr
-    rng = np.random.default_rng(0)
-    n_src, nloc, off = 3000, 800, 1100
-    src = rng.integers(0, nloc, 12000) + off
-    dst = np.clip(src + rng.integers(-200, 200, 12000), 0, n_src - 1)
-    dst[::4] = rng.integers(0, n_src, dst[::4].shape[0])
-    full_rp, full_col = build_csr(n_src, src, dst, "cpu")
-    rp = (full_rp[off:off + nloc + 1] - full_rp[off]).to(torch.int32)
-    col = full_col[int(full_rp[off]):int(full_rp[off + nloc])].contiguous()
-    for R, WR in ((64, 300), (256, None), (4, 5)):
-        plan = ops.WindowPlan(rp, col, 100, n_src, row_off=off, R=R, WR=WR)
-        s = plan.split
-        rpl = rp.long()
-        for i in range(nloc):
-            w0 = ops.win_start(i // R * R, R, plan.WR, off, n_src)
-            c = col[rpl[i]:rpl[i + 1]].long()
-            a, b = int(s[i, 0]) - int(rpl[i]), int(s[i, 1]) - int(rpl[i])
-            assert 0 <= a <= b <= c.numel()
-            assert torch.all((c[a:b] >= w0) & (c[a:b] < w0 + plan.WR))
-            assert torch.all((c[:a] < w0)) and torch.all(c[b:] >= w0 + plan.WR)
-        assert 0 < plan.in_window_fraction() <= 1
-
-
 def test_fused_bwd_grad_index_scatters_the_slab_layout():
     """The index map that scatters a fused-backward slab sum [HD][width] into the flat
     gradient buffer reproduces (gW1 = g[:, :F]^T, gb1 = g[:, F], gW2 = g[:, kf:kf+C])."""
@@ -210,15 +182,14 @@ def test_fused_bwd_grad_index_scatters_the_slab_layout():
     assert torch.all(flat[F * HD + HD + HD * C:] == 0)
 
 
-def test_fused_deep_gcn_train_row_last_layer_matches_all_rows(monkeypatch):
+def test_fused_deep_gcn_train_row_last_layer_matches_all_rows():
     """The fused L-layer GCN aggregating its last layer only at the train rows in
     training: same losses and parameters as aggregating every row (CPU branches)."""
     g = synthetic("cora", seed=3, device="cpu")
     runs = []
-    for all_rows in ("1", "0"):
-        monkeypatch.setenv("CGNN_L2_ALL_ROWS", all_rows)
-        tr = DeepGCNTrainer(g, hidden=32, layers=3, dropout=0.5, fused=True)
-        assert (tr._fused._tr is None) == (all_rows == "1")
+    for rows_only in (False, True):
+        tr = DeepGCNTrainer(g, hidden=32, layers=3, dropout=0.5, fused=True, train_rows_only=rows_only)
+        assert (tr._fused._tr is None) == (not rows_only)
         losses = [float(tr.train_step()) for _ in range(4)]
         runs.append((losses, tr._fused.params.clone(), tr.evaluate()))
     np.testing.assert_allclose(runs[1][0], runs[0][0], rtol=1e-4)

@@ -68,10 +68,6 @@ def main():
     tr._join()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    st = tr.hip.read_stamps() if hasattr(tr.hip, "read_stamps") else []
-    if st:
-        names = ["init", "compute", "barrier1", "reduce", "handoff", "barrier2", "total"]
-        print(json.dumps({"gen_bwd_stamps_cycles": dict(zip(names, st[:7]))}))
     print(json.dumps({"bench": "cgnn_batch", "d": a.d, "edges": a.edges, "conf": a.conf, "N": a.n, "R": a.R,
                       "H": a.h, "us_per_train_step": 1e6 * (t1 - t0) / a.train,
                       "us_per_eval_step": 1e6 * (t2 - t1) / a.test,

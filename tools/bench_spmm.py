@@ -24,8 +24,6 @@ def main():
     ap.add_argument("--homophily", type=float, default=0.8)
     ap.add_argument("--id-order", default="banded", choices=["banded", "shuffled"])
     ap.add_argument("--reorder", action="store_true", help="framework locality pass first")
-    ap.add_argument("--win", default="", help="comma list of block rows R for the LDS-windowed kernel "
-                    "(R or R:pitch, pitch in 16-B chunks)")
     a = ap.parse_args()
     from cgnn_amd.gnn import ops
     from cgnn_amd.gnn.data import synthetic, reorder
@@ -55,27 +53,6 @@ def main():
                           "gather_TBps": round(nnz * row_b / ms / 1e9, 3),
                           "line_TBps": round(nnz * ld * 2 / ms / 1e9, 3),
                           "x_MB": round(n * ld * 2 / 1e6, 1)}), flush=True)
-        for spec in [r for r in a.win.split(",") if r] if (F, ld) == (100, 128) else []:
-            R, pitch = (int(v) for v in (spec.split(":") + ["0"])[:2])
-            plan = ops.WindowPlan(g.rowptr, g.col, F, n, R=R, pitch=pitch)
-            ref = Y.clone()
-            ops.spmm_win(plan, g.rowptr, g.col, X, F, rscale=g.dinv, out=Y)
-            err = float((Y[:, :F].float() - ref[:, :F].float()).abs().max())
-
-            def runw():
-                ops.spmm_win(plan, g.rowptr, g.col, X, F, rscale=g.dinv, out=Y)
-            for _ in range(3):
-                runw()
-            torch.cuda.synchronize()
-            ev0.record()
-            for _ in range(a.reps):
-                runw()
-            ev1.record()
-            torch.cuda.synchronize()
-            ms = ev0.elapsed_time(ev1) / a.reps
-            print(json.dumps({"kernel": "spmm_win", "F": F, "ld": ld, "R": R, "WR": plan.WR, "pitch": plan.lp, "ms": round(ms, 4),
-                              "in_window": round(plan.in_window_fraction(), 4), "max_abs_diff_vs_spmm": err,
-                              "line_TBps": round(nnz * ld * 2 / ms / 1e9, 3)}), flush=True)
         del X, Y
     # the fused layer-2 aggregate + cross-entropy (train mode, compact gradient)
     C, ld = 47, 48

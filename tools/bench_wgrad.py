@@ -1,6 +1,5 @@
 """Time the split-K weight gradient (lin_bwd_weight: dW = [X1 | X2]^T (dY * m), db) on the
-shapes the GNN models hand it; run once as is and once with CGNN_WGT_V1=1 (the v1 kernel:
-64-column slabs, transposing 2-byte LDS writes) for the A/B.
+shapes the GNN models hand it.
 
     python tools/bench_wgrad.py [--reps 20]
 """
@@ -29,7 +28,7 @@ def main():
     from cgnn_amd.gnn.linear import lin_bwd_weight
     dev = torch.device("cuda", 0)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    res = {"v1": os.environ.get("CGNN_WGT_V1", "0") == "1"}
+    res = {}
     for name, n, K1, K2, N, masked in SHAPES:
         x1 = torch.randn(n, K1, device=dev).to(torch.bfloat16)
         x2 = torch.randn(n, K2, device=dev).to(torch.bfloat16) if K2 else None
