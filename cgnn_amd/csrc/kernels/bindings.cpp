@@ -31,7 +31,7 @@ int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t, int);
 int cgnn_gen_bwd_variant(int, int, int, int);
 size_t cgnn_gen_fwd_lds(int, int);
-int cgnn_staged_plan(int, int, int, int, int*);
+int cgnn_staged_plan(int, int, int, int, int, int*);
 int cgnn_staged_tiles(int);
 int cgnn_launch_gen_noise(const int*, int, const uint32_t*, const int*, int, float*, int, int, int, int, int, int,
                           hipStream_t);
@@ -166,11 +166,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gen_bwd_variant", &cgnn_gen_bwd_variant);
   m.def("gen_fwd_lds", &cgnn_gen_fwd_lds);
   // level-scheduled (wide-graph) generator kernels, cgnn_staged.hip
-  m.def("staged_plan", [](int Dt, int H, int max_in, int W) -> py::tuple {
+  m.def("staged_plan", [](int Dt, int H, int max_in, int W, int extra) -> py::tuple {
     int out[5];
-    if (cgnn_staged_plan(Dt, H, max_in, W, out) != 0) return py::tuple();
+    if (cgnn_staged_plan(Dt, H, max_in, W, extra, out) != 0) return py::tuple();
     return py::make_tuple(out[0], out[1], out[2], out[3], out[4]);
-  }, py::arg("Dt"), py::arg("H"), py::arg("max_in"), py::arg("W"));
+  }, py::arg("Dt"), py::arg("H"), py::arg("max_in"), py::arg("W"), py::arg("extra") = 0);
   m.def("staged_tiles", &cgnn_staged_tiles);
   m.def("gen_noise", [](uint64_t prog, int ps, uint64_t keys, uint64_t step, int off, uint64_t noise, int NS, int N,
                         int D, int Dt, int R, int row0, uint64_t st) {

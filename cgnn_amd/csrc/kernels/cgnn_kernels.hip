@@ -728,7 +728,7 @@ extern "C" size_t cgnn_gen_bwd_lds(int H, int max_in, int D, int prog_stride) {
                           (size_t)(max_in + 1) * HE);
 }
 
-extern "C" int cgnn_staged_plan(int, int, int, int, int*);
+extern "C" int cgnn_staged_plan(int, int, int, int, int, int*);
 
 // 1: the specialised per-sample kernel (compiled H, LDS sample state fits), 2: the
 // level-scheduled kernels of cgnn_staged.hip, 0: neither fits (the caller trains this
@@ -738,7 +738,7 @@ extern "C" int cgnn_gen_bwd_variant(int H, int max_in, int Dt, int prog_stride) 
   const bool staged = force && atoi(force) == 1;
   if (!staged && cgnn_gen_supported_h(H) && cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride) <= 160 * 1024) return 1;
   int plan[5];
-  return cgnn_staged_plan(Dt, H, max_in, 8, plan) == 0 ? 2 : 0;
+  return cgnn_staged_plan(Dt, H, max_in, 8, 2 * prog_stride, plan) == 0 ? 2 : 0;
 }
 
 // the per-sample backward (variant 1); variant 2 batches launch cgnn_launch_gen_bwd_staged

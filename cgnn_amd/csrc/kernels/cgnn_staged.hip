@@ -87,6 +87,8 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
   const int n = tile * WAVE + lane;
   const bool valid = n < N;
   const int nc = valid ? n : N - 1;
+  // (program and schedule words are scalar loads: staging them in LDS measured slower,
+  // 1.87 vs 1.47 ms for the d = 200 backward -- the LDS they take costs a block per CU)
   const int* pg = prog + (size_t)r * ps;
   const int* sc = sched + (size_t)r * ss;
   const float* th = params + (size_t)r * P;
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
   const float* nz = noise + (size_t)r * NS * N;
   float* xr = xhat + (size_t)r * D * N;
   float* s_x = smem;                                        // [Dt][64] (LDS state)
-  float* s_nrm = smem + (XG ? 0 : (size_t)Dt * WAVE);       // [W][64]
+  float* s_nrm = s_x + (XG ? 0 : (size_t)Dt * WAVE);        // [W][64]
   float* s_w = s_nrm + W * WAVE + (size_t)wave * (max_in + 2) * HCS;   // this wave's weight rows
   auto xget = [&](int v) -> float { return XG ? xr[(size_t)v * N + nc] : s_x[v * WAVE + lane]; };
   auto xput = [&](int v, float val) {
@@ -108,37 +110,86 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
   const int nf = uni(sc), fb = uni(sc + 2);
   const int* starts = sc + fb;
   const int* items = starts + nf + 1;
+  // software pipeline across a wave's nodes (as the backward): the next chunk's weights,
+  // or the next node's first chunk and own noise, load while this chunk computes
+  constexpr int WK = 8;                  // prefetched weights per lane: (nin + 2) HC <= 512
+  struct Nd { int var, kind, npar, paroff, ncf, cfoff, nin; const float* W1; };
+  auto node_at = [&](int idx) -> Nd {
+    const int* nd = pg + PROG_HDR + uni(items + idx) * NODE_REC;
+    Nd d;
+    d.var = uni(nd); d.kind = uni(nd + 1); d.npar = uni(nd + 2); d.paroff = uni(nd + 3);
+    d.ncf = uni(nd + 4); d.cfoff = uni(nd + 5);
+    d.nin = d.npar + 1 + d.ncf;
+    d.W1 = th + max(uni(nd + 6), 0);     // rows 0..nin: W1ext (row nin = b1), row nin + 1: W2
+    return d;
+  };
+  auto load_w = [&](const Nd& d, int q0, float* w) {
+    const int nel = (d.nin + 2) * HC;
+#pragma unroll
+    for (int k = 0; k < WK; ++k) {
+      const int e = min(WAVE * k + lane, nel - 1);
+      w[k] = d.W1[(e / HC) * H + q0 + e % HC];
+    }
+  };
   for (int st = 0; st < nf; ++st) {
     const int b = uni(starts + st), e = uni(starts + st + 1);
+    float wnx[WK], enx = 0.f;
+    if (b + wave < e) {
+      const Nd d0 = node_at(b + wave);
+      if (d0.kind != KIND_OBS) {
+        load_w(d0, 0, wnx);
+        enx = nz[(size_t)d0.var * N + nc];
+      }
+    }
     for (int i = b + wave; i < e; i += W) {
-      const int kk = uni(items + i);
-      const int* nd = pg + PROG_HDR + kk * NODE_REC;
-      const int var = uni(nd);
-      if (uni(nd + 1) == KIND_OBS) {
+      const Nd cur = node_at(i);
+      const int var = cur.var;
+      if (cur.kind == KIND_OBS) {
         xput(var, dr[(size_t)var * N + nc]);
+        if (i + W < e) {
+          const Nd nx = node_at(i + W);
+          if (nx.kind != KIND_OBS) {
+            load_w(nx, 0, wnx);
+            enx = nz[(size_t)nx.var * N + nc];
+          }
+        }
         continue;
       }
-      const int npar = uni(nd + 2), paroff = uni(nd + 3), ncf = uni(nd + 4), cfoff = uni(nd + 5);
-      const int poff = uni(nd + 6);
-      const int nin = npar + 1 + ncf;
-      const float* W1 = th + poff;       // rows 0..nin: W1ext (row nin = b1), row nin + 1: W2
-      const float e_own = nz[(size_t)var * N + nc];
+      const int npar = cur.npar, paroff = cur.paroff, ncf = cur.ncf, cfoff = cur.cfoff, nin = cur.nin;
+      const float* W1 = cur.W1;
+      const float e_own = enx;
       float out = W1[(size_t)(nin + 2) * H];                       // b2
       for (int q0 = 0; q0 < H; q0 += HC) {
-        // this chunk's weights (rows 0..nin+1, HC units) into the wave's slab: one load
-        // per lane and 64 weights, all issued together
+        // this chunk's weights (rows 0..nin+1, HC units) into the wave's slab
         const int nel = (nin + 2) * HC;
-        for (int e0 = 0; e0 < nel; e0 += 4 * WAVE) {
+        float wcur[WK];
+#pragma unroll
+        for (int k = 0; k < WK; ++k) wcur[k] = wnx[k];
+        if (q0 + HC < H) {
+          load_w(cur, q0 + HC, wnx);
+        } else if (i + W < e) {
+          const Nd nx = node_at(i + W);
+          if (nx.kind != KIND_OBS) {
+            load_w(nx, 0, wnx);
+            enx = nz[(size_t)nx.var * N + nc];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < WK; ++k) {
+          const int el = WAVE * k + lane;
+          if (el < nel) s_w[(el / HC) * HCS + el % HC] = wcur[k];
+        }
+        for (int e0 = WK * WAVE; e0 < nel; e0 += 4 * WAVE) {     // very wide nodes: the rest now
           float wv[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const int e = min(e0 + WAVE * k + lane, nel - 1);
-            wv[k] = W1[(e / HC) * H + q0 + e % HC];
+            const int el = min(e0 + WAVE * k + lane, nel - 1);
+            wv[k] = W1[(el / HC) * H + q0 + el % HC];
           }
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const int e = e0 + WAVE * k + lane;
-            if (e < nel) s_w[(e / HC) * HCS + e % HC] = wv[k];
+            const int el = e0 + WAVE * k + lane;
+            if (el < nel) s_w[(el / HC) * HCS + el % HC] = wv[k];
           }
         }
         wave_sync();
@@ -261,61 +312,110 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
   const int nb = uni(sc + 1), bb = uni(sc + 3);
   const int* starts = sc + bb;
   const int* items = starts + nb + 1;
+
+  // ---- software pipeline across a wave's nodes: while a node's chunk computes, the
+  // loads of the next chunk's weights (or of the next node's first chunk, its first 8
+  // inputs and its dL/dx) are in flight.  Within a sub-stage no node writes another's
+  // dL/dx (only parents, which sit at lower levels), so the next node's is final. ----
+  struct Nd { int var, npar, paroff, ncf, nin; const float* W1; };
+  auto node_at = [&](int idx) -> Nd {
+    const int* nd = pg + PROG_HDR + uni(items + idx) * NODE_REC;
+    Nd d;
+    d.var = uni(nd); d.npar = uni(nd + 2); d.paroff = uni(nd + 3); d.ncf = uni(nd + 4);
+    d.nin = d.npar + 1 + d.ncf;
+    d.W1 = th + uni(nd + 6);               // rows 0..nin: W1ext (row nin = b1), row nin + 1: W2
+    return d;
+  };
+  // weights of one chunk, rows 0..nin+1 x 16 units: elements 64 k + lane (the first 256)
+  auto load_w = [&](const Nd& d, int q0, float* w) {
+    const int nel = (d.nin + 2) * HZ;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = min(WAVE * k + lane, nel - 1);
+      w[k] = d.W1[(e >> 4) * H + q0 + (e & 15)];   // tail units read past the row (padded)
+    }
+  };
+  // inputs j0..j0+7 of a node: the pool holds the parents then the confounder ids
+  // (cf_off = par_off + n_par), so input j != n_par is pool entry par_off + j (- 1 past
+  // the own noise); every load is in bounds and the unused ones are discarded
+  auto load_in = [&](const Nd& d, int j0, float* v) {
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int j = min(j0 + jj, d.nin - 1);
+      const int pe = uni(pg + d.paroff + (j < d.npar ? j : j - 1));
+      const int row = j < d.npar ? pe : (j == d.npar ? d.var : D + pe);
+      if (XG) {
+        const float* base = j < d.npar ? xr : nz;
+        v[jj] = base[(size_t)row * N + nc];
+      } else {
+        const float xa = s_x[(j < d.npar ? pe : 0) * WAVE + lane];
+        const float xb = nz[(size_t)row * N + nc];
+        v[jj] = j < d.npar ? xa : xb;
+      }
+    }
+  };
+  auto load_g = [&](const Nd& d) -> float { return DG ? dx[(size_t)d.var * N + nc] : s_dx[d.var * WAVE + lane]; };
+
   for (int st = 0; st < nb; ++st) {
     const int b = uni(starts + st), e = uni(starts + st + 1);
+    float wnx[4], vnx[8], gnx = 0.f;
+    if (b + wave < e) {
+      const Nd d0 = node_at(b + wave);
+      load_w(d0, 0, wnx);
+      load_in(d0, 0, vnx);
+      gnx = load_g(d0);
+    }
     for (int i = b + wave; i < e; i += W) {
-      const int kk = uni(items + i);
-      const int* nd = pg + PROG_HDR + kk * NODE_REC;
-      const int var = uni(nd), npar = uni(nd + 2), paroff = uni(nd + 3), ncf = uni(nd + 4);
-      const int cfoff = uni(nd + 5), poff = uni(nd + 6);
-      const int nin = npar + 1 + ncf;
-      const float* W1 = th + poff;       // rows 0..nin: W1ext (row nin = b1), row nin + 1: W2
-      // dL/dx of this node and its input row [parents, own noise, confounder streams]:
-      // every load issued before the first use (batches of 8).  The pool holds the
-      // parents then the confounder ids (cf_off = par_off + n_par), so input j != n_par
-      // is pool entry par_off + j (- 1 past the own noise); every load is in bounds and
-      // the unused ones are discarded.
-      const float g_ld = DG ? dx[(size_t)var * N + nc] : s_dx[var * WAVE + lane];
-      for (int j0 = 0; j0 < nin; j0 += 8) {
-        float v[8];
+      const Nd cur = node_at(i);
+      const int var = cur.var, npar = cur.npar, paroff = cur.paroff, nin = cur.nin;
+      const float* W1 = cur.W1;
+      const int poff = (int)(W1 - th);
+      // input row: the first 8 inputs and dL/dx were prefetched; the rest load now
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const int j = min(j0 + jj, nin - 1);
-          const int pe = uni(pg + paroff + (j < npar ? j : j - 1));
-          const int row = j < npar ? pe : (j == npar ? var : D + pe);
-          if (XG) {
-            const float* base = j < npar ? xr : nz;
-            v[jj] = base[(size_t)row * N + nc];
-          } else {
-            const float a = s_x[(j < npar ? pe : 0) * WAVE + lane];
-            const float b = nz[(size_t)row * N + nc];
-            v[jj] = j < npar ? a : b;
-          }
-        }
+      for (int jj = 0; jj < 8; ++jj)
+        if (jj < nin) my_in[jj] = vnx[jj];
+      for (int j0 = 8; j0 < nin; j0 += 8) {
+        float v[8];
+        load_in(cur, j0, v);
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj)
           if (j0 + jj < nin) my_in[j0 + jj] = v[jj];
       }
       my_in[nin] = 1.f;
-      const float gout = valid ? g_ld : 0.f;
+      const float gout = valid ? gnx : 0.f;
 
       for (int q0 = 0; q0 < H; q0 += HZ) {
         const int hc = min(HZ, H - q0);
-        // ---- stage this chunk's weights (rows 0..nin+1, 16 units) in the slab: one
-        // load per lane and 64 weights, all issued together.  Units q >= hc of a tail
-        // chunk read past their row (the parameter buffer is padded) and are zeroed ----
+        // ---- this chunk's weights into the slab (units q >= hc of a tail chunk zeroed),
+        // then the next loads go out ----
         const int nel = (nin + 2) * HZ;
-        for (int e0 = 0; e0 < nel; e0 += 4 * WAVE) {
+        float wcur[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wcur[k] = wnx[k];
+        if (q0 + HZ < H) {
+          load_w(cur, q0 + HZ, wnx);
+        } else if (i + W < e) {
+          const Nd nx = node_at(i + W);
+          load_w(nx, 0, wnx);
+          load_in(nx, 0, vnx);
+          gnx = load_g(nx);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int el = WAVE * k + lane;
+          if (el < nel) s_w[el] = (el & 15) < hc ? wcur[k] : 0.f;
+        }
+        for (int e0 = 4 * WAVE; e0 < nel; e0 += 4 * WAVE) {       // nin > 14: the rest now
           float wv[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const int e = min(e0 + WAVE * k + lane, nel - 1);
-            wv[k] = W1[(e >> 4) * H + q0 + (e & 15)];
+            const int el = min(e0 + WAVE * k + lane, nel - 1);
+            wv[k] = W1[(el >> 4) * H + q0 + (el & 15)];
           }
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const int e = e0 + WAVE * k + lane;
-            if (e < nel) s_w[e] = (e & 15) < hc ? wv[k] : 0.f;
+            const int el = e0 + WAVE * k + lane;
+            if (el < nel) s_w[el] = (el & 15) < hc ? wv[k] : 0.f;
           }
         }
         wave_sync();
@@ -399,8 +499,7 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
         }
         wave_sync();
       }
-      // ---- push dL/dparent (each parent is this wave's alone in the sub-stage):
-      // the read-modify-writes of a batch of 8 parents issued together ----
+      // ---- push dL/dparent (each parent is this wave's alone in the sub-stage) ----
       for (int j0 = 0; j0 < npar; j0 += 8) {
         float cur[8];
 #pragma unroll
@@ -443,12 +542,15 @@ int fwd_hc(int H) {
   return 1;
 }
 
-size_t fwd_lds(int Dt, int W, bool xg, int max_in, int hc) {
+// extra: program + schedule ints staged in LDS
+size_t fwd_lds(int Dt, int W, bool xg, int max_in, int hc, int extra) {
   const size_t hcs = (size_t)((hc + 3) & ~3);
-  return sizeof(float) * ((xg ? 0 : (size_t)Dt * WAVE) + (size_t)W * WAVE + (size_t)W * (max_in + 2) * hcs);
+  return sizeof(float) * ((size_t)extra + (xg ? 0 : (size_t)Dt * WAVE) + (size_t)W * WAVE +
+                          (size_t)W * (max_in + 2) * hcs);
 }
-size_t bwd_lds(int Dt, int W, int max_in, bool xg, bool dg) {
-  return sizeof(float) * ((xg ? 0 : (size_t)Dt * WAVE) + (dg ? 0 : (size_t)Dt * WAVE) + (size_t)W * bwd_slab(max_in));
+size_t bwd_lds(int Dt, int W, int max_in, bool xg, bool dg, int extra) {
+  return sizeof(float) * ((size_t)extra + (xg ? 0 : (size_t)Dt * WAVE) + (dg ? 0 : (size_t)Dt * WAVE) +
+                          (size_t)W * bwd_slab(max_in));
 }
 
 
@@ -457,18 +559,26 @@ size_t bwd_lds(int Dt, int W, int max_in, bool xg, bool dg) {
 // Plan of the staged kernels for Dt variables, hidden width H, max_in generator inputs
 // and W waves per block (1..8): out = {fwd_xg, bwd_xg, bwd_dg, W_fwd, W_bwd}.  Returns 0,
 // or -1 when even the all-global variant does not fit (only for absurd max_in).
-extern "C" int cgnn_staged_plan(int Dt, int H, int max_in, int W, int* out) {
-  if (Dt < 1 || H < 1 || W < 1 || W > 8) return -1;
-  const int fxg = fwd_lds(Dt, W, false, max_in, fwd_hc(H)) <= LDS_MAX ? 0 : 1;
-  int wb = W, bxg = -1, bdg = -1;
-  for (; wb >= 1 && bxg < 0; wb >>= 1) {
-    if (bwd_lds(Dt, wb, max_in, false, false) <= LDS_MAX) { bxg = 0; bdg = 0; }
-    else if (bwd_lds(Dt, wb, max_in, true, false) <= LDS_MAX) { bxg = 1; bdg = 0; }
-    else if (bwd_lds(Dt, wb, max_in, true, true) <= LDS_MAX) { bxg = 1; bdg = 1; }
-    if (bxg >= 0) break;
+// extra: further LDS ints per block (0 in the current kernels)
+extern "C" int cgnn_staged_plan(int Dt, int H, int max_in, int W, int extra, int* out) {
+  if (Dt < 1 || H < 1 || W < 1 || W > 8 || extra < 0) return -1;
+  if (fwd_lds(Dt, W, true, max_in, fwd_hc(H), extra) > LDS_MAX) return -1;
+  const int fxg = fwd_lds(Dt, W, false, max_in, fwd_hc(H), extra) <= LDS_MAX ? 0 : 1;
+  // backward: latency-bound per node, so the placement that keeps the most waves per CU
+  // resident wins (d = 200, H = 20: sample state in LDS at 4 waves / CU 3.76 ms, in
+  // global memory at 16 waves / CU 1.59 ms; profiles/r04_cgnn_wide), at most 4 waves
+  // per block (wider blocks idle on the narrow sub-stages); ties keep the LDS state
+  const int wb = std::min(W, 4);
+  const int cap = 16;                    // ~120 VGPRs: 4 waves per SIMD
+  int best = -1, best_waves = 0;
+  for (int place = 0; place < 3; ++place) {
+    const size_t lds = bwd_lds(Dt, wb, max_in, place >= 1, place == 2, extra);
+    if (lds > LDS_MAX) continue;
+    const int waves = std::min(cap, (int)(LDS_MAX / lds) * wb);
+    if (waves > best_waves) { best = place; best_waves = waves; }
   }
-  if (bxg < 0) return -1;
-  out[0] = fxg; out[1] = bxg; out[2] = bdg; out[3] = W; out[4] = wb;
+  if (best < 0) return -1;
+  out[0] = fxg; out[1] = best >= 1; out[2] = best == 2; out[3] = W; out[4] = wb;
   return 0;
 }
 
@@ -491,12 +601,12 @@ extern "C" int cgnn_launch_gen_fwd_staged(const int* prog, int ps, const int* sc
                                           float* xnorm, int N, int D, int Dt, int H, int max_in, int R, int W,
                                           hipStream_t st, int force) {
   int plan[5];
-  if (cgnn_staged_plan(Dt, H, max_in, W, plan) != 0) return -2;
+  if (cgnn_staged_plan(Dt, H, max_in, W, 0, plan) != 0) return -2;
   const int hc = fwd_hc(H);
   const bool xg = force < 0 ? plan[0] != 0 : force == 1;
-  if (fwd_lds(Dt, W, xg, max_in, hc) > LDS_MAX) return -2;
+  if (fwd_lds(Dt, W, xg, max_in, hc, 0) > LDS_MAX) return -2;
   const int T = cgnn_staged_tiles(N);
-  const size_t lds = fwd_lds(Dt, W, xg, max_in, hc);
+  const size_t lds = fwd_lds(Dt, W, xg, max_in, hc, 0);
   dim3 grid((unsigned)(T * R)), block(WAVE * W);
 #define FWD(HC, XG)                                                                                           \
   {                                                                                                           \
@@ -523,18 +633,18 @@ extern "C" int cgnn_launch_gen_bwd_staged(const int* prog, int ps, const int* sc
                                           int n_chunks, int R, int N, int D, int Dt, int H, int max_in, int W,
                                           float* gpart, float* dxs, hipStream_t st, int force) {
   int plan[5];
-  if (cgnn_staged_plan(Dt, H, max_in, W, plan) != 0) return -2;
+  if (cgnn_staged_plan(Dt, H, max_in, W, 0, plan) != 0) return -2;
   bool xg = plan[1] != 0, dg = plan[2] != 0;
   int wb = plan[4];
   if (force >= 0) {
     xg = force >= 1;
     dg = force == 2;
     wb = W;
-    if (bwd_lds(Dt, wb, max_in, xg, dg) > LDS_MAX) return -2;
+    if (bwd_lds(Dt, wb, max_in, xg, dg, 0) > LDS_MAX) return -2;
   }
   if (dg && !dxs) return -2;
   const int T = cgnn_staged_tiles(N);
-  const size_t lds = bwd_lds(Dt, wb, max_in, xg, dg);
+  const size_t lds = bwd_lds(Dt, wb, max_in, xg, dg, 0);
   dim3 grid((unsigned)(T * R)), block(WAVE * wb);
 #define BWD(XG, DG)                                                                                            \
   {                                                                                                            \

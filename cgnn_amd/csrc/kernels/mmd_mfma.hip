@@ -564,14 +564,223 @@ __global__ __launch_bounds__(512) void mmd_mfma16_kernel(
   }
 }
 
+// ============================================================================
+// Joints wider than 256 (CGNN builds one MLP per variable for any d, CGNN.py:63-90):
+// the Gram and the gradient are sums over groups of 256 dimensions.  A block of 8
+// waves x 16 rows computes, per 32-column tile, the Gram over every group -- group g
+// staged in LDS (hi / lo f16, [32][256] skewed as above) and the wave's x fragments of
+// group g loaded and split on the fly (a 512-wide x would not fit in registers) -- and
+// the gradient for ONE group `dg` only (grid.x = row blocks x groups; the Gram is
+// recomputed per group, the gradient accumulators stay at 16 x 4 registers).  The
+// block's own group is staged last, so the gradient reads it from the same LDS image.
+// Staging is synchronous (no register prefetch): two blocks per CU overlap it.
+// ============================================================================
+template <int KD, int MODE>
+__global__ __launch_bounds__(512) void mmd_mfma16g_kernel(
+    const float* __restrict__ xhat, const float* __restrict__ data,
+    const float* __restrict__ xnorm, const float* __restrict__ ynorm,
+    float* __restrict__ grad_part, float* __restrict__ loss_part,
+    int N, int R, int tiles_per_chunk, float grad_scale, int row_begin, int n_rows) {
+  constexpr bool GRAD = MODE == 0 || MODE == 3;
+  constexpr bool LOSS = MODE != 3;
+  constexpr int KG = 256, NG = (KD + KG - 1) / KG;
+  constexpr int ZS = (KG + 14 * 8 + 127) / 128 * 128;       // 384 halfs per skewed row
+  constexpr int NCH = KG / 8;                                // 32 chunks per row
+  constexpr int TPT = MT * NCH / 512;                        // 2 staging tasks per thread
+  __shared__ __attribute__((aligned(16))) _Float16 s_zh[MT * ZS];
+  __shared__ __attribute__((aligned(16))) _Float16 s_zl[MT * ZS];
+  __shared__ __attribute__((aligned(16))) float s_n[MT];
+  __shared__ float s_red[W16];
+
+  const int n_rb = gridDim.x / NG;
+  const int rb = blockIdx.x % n_rb, dg = blockIdx.x / n_rb;
+  const int chunk = blockIdx.y, r = blockIdx.z, n_chunks = gridDim.y;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int i = row_begin + rb * (W16 * 16) + wave * 16 + li;
+  const bool row_ok = i - row_begin < n_rows;
+  const int ic = row_ok ? i : row_begin;
+  const size_t mbase = (size_t)r * KD * N;
+  const float* X = xhat + mbase;
+  const float* Y = data + mbase;
+  const float* XN = xnorm + (size_t)r * N;
+  const float* YN = ynorm + (size_t)r * N;
+  const float nx = row_ok ? XN[i] : 0.f;
+
+  const int TX = (N + MT - 1) / MT;
+  const int ct = MODE == 2 ? TX : 2 * TX;
+  const int t_begin = chunk * tiles_per_chunk;
+  const int t_end = min(ct, t_begin + tiles_per_chunk);
+
+  f4v acc_g[KG / 16];
+#pragma unroll
+  for (int q = 0; q < KG / 16; ++q) acc_g[q] = f4v{};
+  float rowsum = 0.f, lacc = 0.f;
+
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    const bool pred_part = tile < TX;
+    const int c0 = (pred_part ? tile : tile - TX) * MT;
+    const float* src = pred_part ? X : Y;
+    f4v c[2] = {f4v{}, f4v{}};
+#pragma unroll 1
+    for (int gi = 0; gi < NG; ++gi) {
+      const int grp = (dg + 1 + gi) % NG;                    // the block's own group last
+      __syncthreads();                                       // earlier readers of the image done
+      if (gi == 0 && t < MT) s_n[t] = c0 + t < N ? (pred_part ? XN : YN)[c0 + t] : 0.f;
+#pragma unroll
+      for (int k = 0; k < TPT; ++k) {
+        const int task = t + 512 * k;
+        const int jj = task & 31, ch = task >> 5;
+        h8 hi, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int d = KG * grp + 8 * ch + e;
+          const float v = (d < KD && c0 + jj < N) ? src[(size_t)d * N + c0 + jj] : 0.f;
+          _Float16 a, b;
+          split16(v, a, b);
+          hi[e] = a;
+          lo[e] = b;
+        }
+        *reinterpret_cast<h8*>(&s_zh[zoff<ZS>(jj, ch)]) = hi;
+        *reinterpret_cast<h8*>(&s_zl[zoff<ZS>(jj, ch)]) = lo;
+      }
+      __syncthreads();
+      // Gram over this group: x fragments of row i (dims 32 s + 8 g + e of the group)
+#pragma unroll 1
+      for (int s8 = 0; s8 < KG / 32; ++s8) {
+        h8 xh, xl;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int d = KG * grp + 32 * s8 + 8 * g + e;
+          const float v = (row_ok && d < KD) ? X[(size_t)d * N + ic] : 0.f;
+          _Float16 a, b;
+          split16(v, a, b);
+          xh[e] = a;
+          xl[e] = b;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int j = 16 * h + li;
+          const h8 ah = *reinterpret_cast<const h8*>(s_zh + zoff<ZS>(j, 4 * s8 + g));
+          const h8 al = *reinterpret_cast<const h8*>(s_zl + zoff<ZS>(j, 4 * s8 + g));
+          c[h] = mma16(ah, xh, c[h]);
+          c[h] = mma16(ah, xl, c[h]);
+          c[h] = mma16(al, xh, c[h]);
+        }
+      }
+    }
+
+    // ---- epilogue (as mmd_mfma16_kernel) ----
+    f2 tl2 = {0.f, 0.f}, rs2 = {0.f, 0.f};
+    const float sg = pred_part ? 1.f : -1.f;
+    const int jlim = N - c0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 nz4 = *reinterpret_cast<const float4*>(&s_n[16 * h + 4 * g]);
+#pragma unroll
+      for (int qq = 0; qq < 2; ++qq) {
+        const f2 nzp = qq ? f2{nz4.z, nz4.w} : f2{nz4.x, nz4.y};
+        const f2 cc = {c[h][2 * qq], c[h][2 * qq + 1]};
+        f2 d2 = cc * -2.f + (nzp + nx);
+        const int jr = 16 * h + 4 * g + 2 * qq;
+        d2.x = jr < jlim ? d2.x : 1.0e30f;
+        d2.y = jr + 1 < jlim ? d2.y : 1.0e30f;
+        f2 ks, w;
+        if (GRAD) rbf7x2_chain(d2, ks, w);
+        else rbf7x2(d2, ks, w);
+        if (LOSS) tl2 += ks;
+        if (GRAD) {
+          w *= sg;
+          rs2 += w;
+          c[h][2 * qq] = w.x;
+          c[h][2 * qq + 1] = w.y;
+        }
+      }
+    }
+    if (LOSS) lacc = fmaf(pred_part ? 1.f : -2.f, tl2.x + tl2.y, lacc);
+
+    if (GRAD) {
+      rowsum += rs2.x + rs2.y;
+      h8 wh, wl;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        _Float16 hi, lo;
+        split16(c[e >> 2][e & 3], hi, lo);
+        wh[e] = hi;
+        wl[e] = lo;
+      }
+      // the image holds group dg (staged last)
+      const int rr = li >> 2, p = li & 3;
+#pragma unroll
+      for (int q = 0; q < KG / 16; ++q) {
+        const int cq = 2 * q + (p >> 1), hq = 4 * (p & 1);
+        const int o0 = zoff<ZS>(4 * g + rr, cq) + hq, o1 = zoff<ZS>(16 + 4 * g + rr, cq) + hq;
+        typedef __attribute__((address_space(3))) s4v lds_s4v;
+        const s4v bh0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(s_zh + o0));
+        const s4v bh1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(s_zh + o1));
+        const s4v bl0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(s_zl + o0));
+        const s4v bl1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(s_zl + o1));
+        const h8 bh = __builtin_bit_cast(h8, __builtin_shufflevector(bh0, bh1, 0, 1, 2, 3, 4, 5, 6, 7));
+        const h8 bl = __builtin_bit_cast(h8, __builtin_shufflevector(bl0, bl1, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc_g[q] = mma16(wh, bh, acc_g[q]);
+        acc_g[q] = mma16(wh, bl, acc_g[q]);
+        acc_g[q] = mma16(wl, bh, acc_g[q]);
+      }
+    }
+  }
+
+  // ---- loss partial (group-0 blocks only): fixed-order wave then block reduction ----
+  float v = row_ok ? lacc : 0.f;
+  v = wave_sum(v);
+  if (lane == 0) s_red[wave] = v;
+  __syncthreads();
+  if (t == 0 && dg == 0) {
+    const float sum = ((s_red[0] + s_red[1]) + (s_red[2] + s_red[3])) + ((s_red[4] + s_red[5]) + (s_red[6] + s_red[7]));
+    loss_part[((size_t)r * n_chunks + chunk) * n_rb + rb] = sum;
+  }
+
+  if (GRAD) {
+    rowsum += __shfl_xor(rowsum, 16);
+    rowsum += __shfl_xor(rowsum, 32);
+    float* gp = grad_part + ((size_t)chunk * R + r) * KD * n_rows;
+    const int i0 = rb * (W16 * 16) + wave * 16;
+#pragma unroll
+    for (int vv = 0; vv < 4; ++vv) {
+      const int il = 4 * g + vv;
+      const float rs = __shfl(rowsum, il);
+      const int ii = i0 + il;
+#pragma unroll
+      for (int q = 0; q < KG / 16; ++q) {
+        const int d = KG * dg + 16 * q + li;
+        if (d < KD && ii < n_rows) {
+          const float pv = X[(size_t)d * N + row_begin + ii];
+          gp[(size_t)d * n_rows + ii] = (acc_g[q][vv] - pv * rs) * grad_scale;
+        }
+      }
+    }
+  }
+}
+
 template <int KD>
 int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const float* xn, const float* yn,
                       float* gpart, float* lpart, int N, int R, int n_chunks, int tpc, float gscale,
                       int row_begin, int n_rows, hipStream_t st, int wide) {
   const int n_rb = (n_rows + WAVES * MT - 1) / (WAVES * MT);
+  if constexpr (KD > 256) {
+    constexpr int NG = (KD + 255) / 256;
+    dim3 grid(n_rb * NG, n_chunks, R), block(512);
+#define WIDEG(M, A, B, C, D2) hipLaunchKernelGGL((mmd_mfma16g_kernel<KD, M>), grid, block, 0, st, A, B, C, D2, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows)
+    if (mode == 0) WIDEG(0, xhat, data, xn, yn);
+    else if (mode == 3) WIDEG(3, xhat, data, xn, yn);
+    else if (mode == 1) WIDEG(1, xhat, data, xn, yn);
+    else if (mode == 2) WIDEG(2, data, data, yn, yn);
+    else return -3;
+#undef WIDEG
+    return (int)hipGetLastError();
+  }
   if (wide < 0) wide = KD >= 128;
   if (KD >= 128 && wide) {
-    if constexpr (KD >= 128) {
+    if constexpr (KD >= 128 && KD <= 256) {
       dim3 grid(n_rb, n_chunks, R), block(512);
 #define WIDE(M, A, B, C, D2) hipLaunchKernelGGL((mmd_mfma16_kernel<KD, M>), grid, block, 0, st, A, B, C, D2, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows)
       if (mode == 0) WIDE(0, xhat, data, xn, yn);
@@ -583,6 +792,8 @@ int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const floa
       return (int)hipGetLastError();
     }
   }
+  if constexpr (KD > 256) return -1;
+  else {
   dim3 grid(n_rb, n_chunks, R), block(256);
   if (mode == 0)
     hipLaunchKernelGGL((mmd_mfma_kernel<KD, 0>), grid, block, 0, st, xhat, data, xn, yn, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows);
@@ -595,6 +806,7 @@ int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const floa
   else
     return -3;
   return (int)hipGetLastError();
+  }
 }
 
 }  // namespace
@@ -604,7 +816,8 @@ int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const floa
 extern "C" int cgnn_mmd_mfma_supported(int D) {
   switch (D) {
     case 8: case 12: case 16: case 20: case 24: case 32: case 48: case 64:
-    case 80: case 96: case 128: case 160: case 192: case 224: case 256: return 1;
+    case 80: case 96: case 128: case 160: case 192: case 224: case 256:
+    case 320: case 384: case 448: case 512: case 640: case 768: case 896: case 1024: return 1;
     default: return 0;
   }
 }
@@ -623,6 +836,7 @@ extern "C" int cgnn_launch_mmd_mfma_rows(int mode, int D, const float* xhat, con
 #define CASE_D(d) case d: return launch_mmd_mfma_d<d>(mode, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale, row_begin, n_rows, st, wide);
     CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20) CASE_D(24) CASE_D(32) CASE_D(48) CASE_D(64)
     CASE_D(80) CASE_D(96) CASE_D(128) CASE_D(160) CASE_D(192) CASE_D(224) CASE_D(256)
+    CASE_D(320) CASE_D(384) CASE_D(448) CASE_D(512) CASE_D(640) CASE_D(768) CASE_D(896) CASE_D(1024)
 #undef CASE_D
     default: return -1;
   }

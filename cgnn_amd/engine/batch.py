@@ -17,8 +17,11 @@ import torch
 from .. import native
 from .program import Program, pack_programs, pack_schedules
 
-# padded variable counts with compiled kernels; above 64 only the matrix-core MMD
-SUPPORTED_D = (1, 2, 3, 4, 6, 8, 12, 16, 20, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
+# padded variable counts with compiled kernels; above 64 only the matrix-core MMD, above
+# 256 its dimension-grouped form (and no Fourier-feature MMD)
+SUPPORTED_D = (1, 2, 3, 4, 6, 8, 12, 16, 20, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256,
+               320, 384, 448, 512, 640, 768, 896, 1024)
+MAX_RFF_D = 256
 MAX_VALU_D = 64
 MMD_TILE = 256
 TARGET_WGS = 2048
@@ -84,13 +87,13 @@ def mmd_kernel_choice(D: int, mmd_kernel: str = "auto") -> str:
     return choice
 
 
-def device_supported(d: int, H: int, max_in: int, prog_len: int = 0) -> bool:
+def device_supported(d: int, H: int, max_in: int, prog_len: int = 0, fast_mmd: bool = False) -> bool:
     """True when the device kernels cover a batch of ``d``-variable programs with hidden
     width ``H``, at most ``max_in`` generator inputs per node and programs of at most
     ``prog_len`` ints: the variable count up to SUPPORTED_D[-1], and either the
     per-sample generator kernels (sample state in LDS) or the level-scheduled ones.
     Otherwise ``score_jobs`` trains the batch on the CPU reference path (with a warning)."""
-    if d > SUPPORTED_D[-1]:
+    if d > SUPPORTED_D[-1] or (fast_mmd and padded_dim(d) > MAX_RFF_D):
         return False
     hip = native.hip()
     stride = (int(prog_len) + 3) // 4 * 4              # pack_programs' stride
@@ -100,14 +103,14 @@ def device_supported(d: int, H: int, max_in: int, prog_len: int = 0) -> bool:
     return variant == 2
 
 
-def staged_setup(programs: Sequence[Program], H: int, max_in: int, d: int):
+def staged_setup(programs: Sequence[Program], H: int, max_in: int, d: int, prog_stride: int):
     """Schedule + launch plan of the level-scheduled generator kernels for a batch:
     (schedule [R, stride] int32, stride, waves per block, dL/dx in global memory)."""
     sched, sstride, width = pack_schedules(programs)
     W = 8
     while W > 1 and W // 2 >= width:
         W //= 2
-    plan = native.hip().staged_plan(int(d), int(H), int(max_in), W)
+    plan = native.hip().staged_plan(int(d), int(H), int(max_in), W, int(prog_stride) + int(sstride))
     if not plan:
         raise native.NativeExtensionError("staged generator kernels: no LDS plan for d=%d H=%d" % (d, H))
     return sched, sstride, W, bool(plan[2])
@@ -153,7 +156,7 @@ class DeviceTrainer:
                 "generator backward: H=%d with %d inputs per node does not fit in LDS" % (H, max_in))
         self.staged = self.bwd_variant == 2
         if self.staged:
-            sched, sstride, self.stage_w, dx_global = staged_setup(programs, H, max_in, d)
+            sched, sstride, self.stage_w, dx_global = staged_setup(programs, H, max_in, d, stride)
         else:
             sched, sstride, self.stage_w, dx_global = np.zeros((1, 4), np.int32), 4, 8, False
         self.sched_stride = sstride
@@ -176,6 +179,9 @@ class DeviceTrainer:
             row_tiles, n_chunks, tpc = mmd_geometry(N, R)
             self.geometry = (row_tiles, n_chunks, tpc)
             self.rff_k = int(nb_vectors) if use_fast_mmd else 0
+            if self.rff_k and D > MAX_RFF_D:
+                raise native.NativeExtensionError(
+                    "Fourier-feature MMD covers at most %d (padded) variables, got %d" % (MAX_RFF_D, D))
             self.mmd_kernel = "rff" if self.rff_k else mmd_kernel_choice(D, mmd_kernel)
             mf_rb, mf_chunks, mf_tpc = mmd_mfma_geometry(N, R)
             F = 7 * self.rff_k

@@ -89,7 +89,7 @@ def _device_batch_ok(jobs: Sequence[Job], idx, cfg) -> bool:
     d = jobs[idx[0]].program.n_vars
     max_in = max(jobs[i].program.max_in for i in idx)
     prog_len = max(len(jobs[i].program.prog) for i in idx)
-    if device_supported(d, cfg.h_layer_dim, max_in, prog_len):
+    if device_supported(d, cfg.h_layer_dim, max_in, prog_len, fast_mmd=bool(cfg.use_Fast_MMD)):
         return True
     log.warning("CGNN batch of %d models (%d variables, h_layer_dim=%d, %d inputs per node) "
                 "is outside the device kernels; training it on the CPU reference path",

@@ -115,7 +115,7 @@ class SampleShardedTrainer:
         self.staged = variant == 2
         dx_global = False
         if self.staged:
-            sched, self.sstride, self.stage_w, dx_global = staged_setup(self.programs, self.H, max_in, d)
+            sched, self.sstride, self.stage_w, dx_global = staged_setup(self.programs, self.H, max_in, d, stride)
             self.sched = torch.from_numpy(sched).to(self.device)
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)

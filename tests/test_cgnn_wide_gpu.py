@@ -33,7 +33,7 @@ def _data(d, N, seed):
     return x
 
 
-@pytest.mark.parametrize("N,d", [(300, 100), (130, 200), (97, 256)])
+@pytest.mark.parametrize("N,d", [(300, 100), (130, 200), (97, 256), (150, 300), (100, 512), (70, 1000)])
 def test_wide_mmd_matches_oracle(N, d):
     from cgnn_amd.ops.mmd import mmd_loss
     torch.manual_seed(d)
@@ -55,7 +55,7 @@ def test_wide_mmd_matches_oracle(N, d):
     np.testing.assert_allclose(pg.grad.cpu().numpy(), gref, rtol=3e-3, atol=3e-3 * np.abs(gref).max())
 
 
-@pytest.mark.parametrize("d,H", [(100, 25), (100, 100), (200, 25), (200, 100)])
+@pytest.mark.parametrize("d,H", [(100, 25), (100, 100), (200, 25), (200, 100), (300, 20), (512, 20)])
 def test_wide_dag_trainer_matches_oracle(d, H):
     g = _random_dag(d, seed=d + H)
     prog = program_for_dag(g, H)

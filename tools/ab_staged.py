@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--n", type=int, default=500)
     ap.add_argument("--h", type=int, default=20)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default="", help="kernel:W:placement, e.g. bwd:4:2 (profiling runs)")
     a = ap.parse_args()
     os.environ["CGNN_GEN_STAGED"] = "1"
     import numpy as np
@@ -57,9 +58,14 @@ def main():
         return ts[len(ts) // 2], ts[0]
 
     print(json.dumps({"max_in": int(tr.max_in), "plan_W": tr.stage_w,
-                      "plan": list(hip.staged_plan(d, H, int(tr.max_in), tr.stage_w))}))
+                      "plan": list(hip.staged_plan(d, H, int(tr.max_in), tr.stage_w, tr.prog_stride + tr.sched_stride))}))
+    only = a.only.split(":") if a.only else None
     for W in (1, 2, 4, 8):
+        if only and int(only[1]) != W:
+            continue
         for force in (0, 1):
+            if only and (only[0] != "fwd" or int(only[2]) != force):
+                continue
             try:
                 med, mn = timeit(lambda: hip.gen_fwd_staged(
                     tr.prog.data_ptr(), tr.prog_stride, tr.sched.data_ptr(), tr.sched_stride, tr.params.data_ptr(),
@@ -69,6 +75,8 @@ def main():
             except RuntimeError as e:
                 print(json.dumps({"kernel": "fwd", "W": W, "xg": force, "skip": str(e)[:60]}))
         for force in (0, 1, 2):
+            if only and (only[0] != "bwd" or int(only[2]) != force):
+                continue
             try:
                 med, mn = timeit(lambda: hip.gen_bwd_staged(
                     tr.prog.data_ptr(), tr.prog_stride, tr.sched.data_ptr(), tr.sched_stride, tr.params.data_ptr(),
