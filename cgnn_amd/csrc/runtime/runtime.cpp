@@ -397,26 +397,48 @@ py::tuple synthetic_graph(i64 n, i64 m, int n_feat, int n_class, double homophil
 // (every rank of a graph-sharded job scans the edge hash space and keeps the edges
 // touching its rows: O(m) hashing, O(local nnz) memory).  rowptr is int64 (a shard
 // of a 10^9-edge graph may pass 2^31 entries), columns int32 (n < 2^31).
+//
+// order (optional, [n] int64): a partition order -- node f (final id) becomes row
+// order[f]; the shard is then rows [r0, r1) of the RELABELLED graph (columns relabelled
+// too), and the returned `ids` are the final ids of its rows (for the split mask).
+// with_features = false: structure only (a partitioning pass over the whole graph).
 py::tuple synthetic_shard(i64 n, i64 m, int n_feat, int n_class, double homophily, double feat_noise,
-                          uint64_t seed, double label_noise, int id_order, i64 r0, i64 r1) {
+                          uint64_t seed, double label_noise, int id_order, i64 r0, i64 r1,
+                          py::array_t<i64, py::array::c_style | py::array::forcecast> order_a, bool with_features) {
   if (r0 < 0 || r1 > n || r0 > r1) throw std::invalid_argument("synthetic_shard: bad row range");
   if (n >= (i64)1 << 31) throw std::invalid_argument("synthetic_shard: n >= 2^31 needs int64 columns");
+  const bool relabel = order_a.size() > 0;
+  if (relabel && order_a.size() != n) throw std::invalid_argument("synthetic_shard: order must have n entries");
+  const i64* ord = relabel ? order_a.data() : nullptr;
   const SynthSpec sp(n, m, n_feat, n_class, homophily, feat_noise, seed, label_noise, id_order);
   const i64 nl = r1 - r0;
   py::array_t<i64> rp_a(nl + 1);
   i64* rp = rp_a.mutable_data();
-  py::array_t<float> feat_a({(py::ssize_t)nl, (py::ssize_t)n_feat});
-  py::array_t<i32> label_a(nl);
+  py::array_t<float> feat_a({(py::ssize_t)(with_features ? nl : 0), (py::ssize_t)n_feat});
+  py::array_t<i32> label_a(with_features ? nl : 0);
+  py::array_t<i64> ids_a(nl);
+  i64* ids = ids_a.mutable_data();
   std::vector<i32> col;
   {
     py::gil_scoped_release nogil;
+    // final id of every local row (identity without an order)
+    if (relabel) {
+#pragma omp parallel for schedule(static)
+      for (i64 f = 0; f < n; ++f) {
+        const i64 v = ord[f];
+        if (v >= r0 && v < r1) ids[v - r0] = f;
+      }
+    } else {
+      for (i64 v = 0; v < nl; ++v) ids[v] = r0 + v;
+    }
+    auto fid = [&](i64 x) -> i64 { const i64 p = sp.pid(x); return relabel ? ord[p] : p; };
     std::vector<i64> cnt(nl + 1, 0);
     // pass 1: degree of every local row (both directions of every edge, self loops apart)
 #pragma omp parallel for schedule(static)
     for (i64 e = 0; e < m; ++e) {
       i64 s, t;
       sp.edge(e, s, t);
-      const i64 ps = sp.pid(s), pt = sp.pid(t);
+      const i64 ps = fid(s), pt = fid(t);
       if (ps == pt) continue;
       if (ps >= r0 && ps < r1) __atomic_fetch_add(&cnt[ps - r0 + 1], 1, __ATOMIC_RELAXED);
       if (pt >= r0 && pt < r1) __atomic_fetch_add(&cnt[pt - r0 + 1], 1, __ATOMIC_RELAXED);
@@ -430,7 +452,7 @@ py::tuple synthetic_shard(i64 n, i64 m, int n_feat, int n_class, double homophil
     for (i64 e = 0; e < m; ++e) {
       i64 s, t;
       sp.edge(e, s, t);
-      const i64 ps = sp.pid(s), pt = sp.pid(t);
+      const i64 ps = fid(s), pt = fid(t);
       if (ps == pt) continue;
       if (ps >= r0 && ps < r1) col[__atomic_fetch_add(&cur[ps - r0], 1, __ATOMIC_RELAXED)] = (i32)pt;
       if (pt >= r0 && pt < r1) col[__atomic_fetch_add(&cur[pt - r0], 1, __ATOMIC_RELAXED)] = (i32)ps;
@@ -453,19 +475,21 @@ py::tuple synthetic_shard(i64 n, i64 m, int n_feat, int n_class, double homophil
     }
     col.resize(w);
     col.shrink_to_fit();
-    const std::vector<float> cent = sp.centroids();
-    float* x = feat_a.mutable_data();
-    i32* lab = label_a.mutable_data();
+    if (with_features) {
+      const std::vector<float> cent = sp.centroids();
+      float* x = feat_a.mutable_data();
+      i32* lab = label_a.mutable_data();
 #pragma omp parallel for schedule(static)
-    for (i64 v = 0; v < nl; ++v) {
-      const i64 gv = sp.gen_id(r0 + v);
-      lab[v] = sp.label(gv);
-      sp.features(gv, cent, x + (size_t)v * n_feat);
+      for (i64 v = 0; v < nl; ++v) {
+        const i64 gv = sp.gen_id(ids[v]);
+        lab[v] = sp.label(gv);
+        sp.features(gv, cent, x + (size_t)v * n_feat);
+      }
     }
   }
   py::array_t<i32> col_a((py::ssize_t)col.size());
   std::copy(col.begin(), col.end(), col_a.mutable_data());
-  return py::make_tuple(rp_a, col_a, feat_a, label_a);
+  return py::make_tuple(rp_a, col_a, feat_a, label_a, ids_a);
 }
 
 // Train / valid / test split by a per-node hash: node v is train with probability
@@ -583,7 +607,7 @@ PYBIND11_MODULE(_rt, m) {
         py::arg("seed") = 0, py::arg("label_noise") = 0.0, py::arg("id_order") = 0);
   m.def("synthetic_shard", &synthetic_shard, py::arg("n"), py::arg("m"), py::arg("n_feat"), py::arg("n_class"),
         py::arg("homophily"), py::arg("feat_noise"), py::arg("seed"), py::arg("label_noise"), py::arg("id_order"),
-        py::arg("r0"), py::arg("r1"));
+        py::arg("r0"), py::arg("r1"), py::arg("order") = py::array_t<i64>(0), py::arg("with_features") = true);
   m.def("split_mask", &split_mask, py::arg("n"), py::arg("n_train"), py::arg("n_val"), py::arg("seed"),
         py::arg("ids"));
   m.def("sample_neighbors", &sample_neighbors);

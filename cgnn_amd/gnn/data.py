@@ -157,6 +157,9 @@ class GraphShard:
     n_classes: int
     n_train_global: int = 0
     name: str = "synthetic-shard"
+    # train flags of any global rows (rows of other ranks included): generation is
+    # deterministic, so a one-rank dry run can flag the rows its halo would receive
+    train_flags: Optional[object] = None
 
     @property
     def n_local(self):
@@ -173,32 +176,76 @@ def shard_rows(n: int, rank: int, world: int):
     return rank * per, min(n, (rank + 1) * per), per
 
 
-def synthetic_shard(name: str, rank: int, world: int, seed: int = 0, device=None, scale: float = 1.0,
-                    homophily: float = 0.8, feat_noise: float = 4.0, label_noise: float = 0.25,
-                    id_order: str = "shuffled", feature_dtype=torch.float32) -> GraphShard:
-    """This rank's rows of ``synthetic(name, ...)`` -- the same graph, generated shard-locally
-    (the C++ generator hashes every edge once and keeps those touching the shard; memory
-    is O(shard)).  ``feature_dtype`` bf16 halves the feature bytes of a 10^8-node graph."""
+def _scaled_shape(name: str, scale: float):
     n, m, F, C, n_train, n_val = SHAPES[name]
     n = max(int(n * scale), C * 4)
     m = max(int(m * scale), n)
     n_train = max(int(n_train * scale), C)
     n_val = max(int(n_val * scale), C)
+    return n, m, F, C, n_train, n_val
+
+
+def partition_order(name: str, seed: int = 0, scale: float = 1.0, homophily: float = 0.8,
+                    id_order: str = "shuffled", rounds: int = 8, max_cluster: int = 4096) -> np.ndarray:
+    """Locality partition of ``synthetic(name, ...)`` computed from its structure alone:
+    the framework's reorder pass (label-propagation clusters + Cuthill-McKee over them,
+    ``reorder``) over the whole graph's CSR, generated without features (O(nnz) host
+    memory: 13 GB of column ids for the papers100M shape).  Node ``f`` becomes row
+    ``order[f]``; a rank then owns the contiguous block ``shard_rows(n, rank, world)`` of
+    the new order, i.e. whole communities instead of random ids.  Deterministic for any
+    thread count, so every rank computes the same order without an exchange."""
+    n, m, F, C, _, _ = _scaled_shape(name, scale)
+    rt = native.rt()
+    rp, col = rt.synthetic_shard(n, m, F, C, homophily, 0.0, seed, 0.0, ID_ORDERS[id_order], 0, n,
+                                 with_features=False)[:2]
+    order = np.asarray(rt.locality_order(n, np.asarray(rp), np.asarray(col), rounds, max_cluster, seed))
+    del rp, col
+    return order
+
+
+def synthetic_shard(name: str, rank: int, world: int, seed: int = 0, device=None, scale: float = 1.0,
+                    homophily: float = 0.8, feat_noise: float = 4.0, label_noise: float = 0.25,
+                    id_order: str = "shuffled", feature_dtype=torch.float32, partition: str = "none",
+                    order: Optional[np.ndarray] = None) -> GraphShard:
+    """This rank's rows of ``synthetic(name, ...)`` -- the same graph, generated shard-locally
+    (the C++ generator hashes every edge once and keeps those touching the shard; memory
+    is O(shard)).  ``feature_dtype`` bf16 halves the feature bytes of a 10^8-node graph.
+    ``partition="locality"`` (or an explicit ``order``): the rows of the graph relabelled by
+    :func:`partition_order`, so the rank owns communities and its halo shrinks; the
+    graph equals ``reorder(synthetic(...))`` of the same arguments."""
+    n, m, F, C, n_train, n_val = _scaled_shape(name, scale)
+    if order is None and partition == "locality":
+        order = partition_order(name, seed=seed, scale=scale, homophily=homophily, id_order=id_order)
+    elif partition not in ("none", "locality"):
+        raise ValueError("partition must be 'none' or 'locality'")
     r0, r1, _ = shard_rows(n, rank, world)
     rt = native.rt()
-    rp, col, x, y = rt.synthetic_shard(n, m, F, C, homophily, feat_noise, seed, label_noise, ID_ORDERS[id_order],
-                                       r0, r1)
+    ordv = np.zeros(0, np.int64) if order is None else np.asarray(order, np.int64)
+    rp, col, x, y, ids = rt.synthetic_shard(n, m, F, C, homophily, feat_noise, seed, label_noise,
+                                            ID_ORDERS[id_order], r0, r1, order=ordv)
     rp = np.asarray(rp)
     rp_t = torch.from_numpy(rp.astype(np.int32) if rp[-1] < 2 ** 31 else rp)
-    mask = np.asarray(rt.split_mask(n, n_train, n_val, seed + 1, np.arange(r0, r1, dtype=np.int64)))
+    mask = np.asarray(rt.split_mask(n, n_train, n_val, seed + 1, np.asarray(ids, np.int64)))
     dev = torch.device(device) if device is not None else torch.device("cpu")
     xt = torch.from_numpy(np.asarray(x))
     if feature_dtype != torch.float32:
         xt = xt.to(feature_dtype)
+    inv = None
+    if order is not None:
+        inv = np.empty(n, np.int64)
+        inv[ordv] = np.arange(n, dtype=np.int64)
+
+    def train_flags(rows: torch.Tensor) -> torch.Tensor:
+        """Train flag of global rows (of this shard's numbering)."""
+        r = rows.detach().cpu().numpy().astype(np.int64)
+        f = inv[r] if inv is not None else r
+        return torch.from_numpy(np.asarray(rt.split_mask(n, n_train, n_val, seed + 1, f)) == 1).to(rows.device)
+
+    tag = "-locality" if order is not None else ""
     return GraphShard(n=n, r0=r0, r1=r1, rowptr=rp_t.to(dev), col=torch.from_numpy(np.asarray(col)).to(dev),
                       x=xt.to(dev), y=torch.from_numpy(np.asarray(y).astype(np.int32)).to(dev),
                       mask=torch.from_numpy(mask).to(dev), n_classes=C, n_train_global=n_train,
-                      name="%s-synthetic-shard%d/%d" % (name, rank, world))
+                      name="%s-synthetic%s-shard%d/%d" % (name, tag, rank, world), train_flags=train_flags)
 
 
 def locality(g: GraphData, windows=(64, 256, 1024, 4096, 65536), new_id=None):

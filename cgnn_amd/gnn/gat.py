@@ -462,7 +462,9 @@ class ShardedGATTrainer:
             self.fused = FusedGAT(self.x, self.y, self.mask, shard.n_classes, self.g, heads, head_dim, dropout, lr,
                                   seed, halo=self.halo, row0=r0, n_train=int(self.n_train), distributed=distributed,
                                   train_l2=train_l2, x_ext=x_ext, train_rows_only=train_rows_only,
-                                  l1_train_neighbours=l1_train_neighbours)
+                                  l1_train_neighbours=l1_train_neighbours,
+                                  train_flag_fn=getattr(shard, "train_flags", None) if emulate is not None
+                                  else None)
             self.model = self.opt = None
             self.epoch = 0
             return

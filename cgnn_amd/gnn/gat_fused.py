@@ -280,7 +280,7 @@ class FusedGAT:
 
     def __init__(self, x, y, mask, n_classes, g, heads=8, head_dim=32, dropout=0.5, lr=0.005, seed=0,
                  halo=None, row0=0, n_train=None, distributed=False, train_l2=None, x_ext=None,
-                 train_rows_only: bool = True, l1_train_neighbours: bool = True):
+                 train_rows_only: bool = True, l1_train_neighbours: bool = True, train_flag_fn=None):
         from .gat import GAT
         dev = x.device
         self.dev, self.g, self.halo = dev, g, halo
@@ -388,22 +388,26 @@ class FusedGAT:
         # flags come over the halo once).  Training epochs aggregate layer 1 over a CSR
         # whose other rows are empty (they produce out = 0, finite, read by no train row,
         # with zero gradient); evaluation aggregates every row.  The papers100M shape has
-        # ~1 % train rows, so most layer-1 edges drop out.  Not in a dry run (emulated
-        # halo: the received rows' flags are not real).  l1_train_neighbours=False: off.
+        # ~1 % train rows, so most layer-1 edges drop out.  In a dry run (emulated halo)
+        # the received rows' flags come from ``train_flag_fn`` (the deterministic split of
+        # any global row); without one the pruning is off.  l1_train_neighbours=False: off.
         # The decision is the same on every rank whenever there is a halo (the flag
         # exchange is collective): a rank without train rows still takes part.
         self._g1 = None
         want = (halo is not None) or (self._tr is not None)
-        if (want and l1_train_neighbours
-                and not (halo is not None and getattr(halo, "emulate", False))):
-            self._g1 = self._train_neighbour_graph(g, halo)
+        emulated = halo is not None and getattr(halo, "emulate", False)
+        if want and l1_train_neighbours and (not emulated or train_flag_fn is not None):
+            self._g1 = self._train_neighbour_graph(g, halo, train_flag_fn if emulated else None)
         self.epoch = 0
         self.last_stats = None
 
-    def _train_neighbour_graph(self, g, halo):
+    def _train_neighbour_graph(self, g, halo, flag_fn=None):
         from .gat import GraphCSR
         flag = (self.mask == 1).to(torch.float32)[:, None].contiguous()
-        if halo is not None:
+        if flag_fn is not None:                            # emulated halo: flags generated locally
+            rec = flag_fn(halo.received_ids()).to(torch.float32)[:, None]
+            flag = torch.cat([flag, rec.to(flag.device)], 0).contiguous()
+        elif halo is not None:
             flag = halo.exchange_parts([flag])[0]          # [own | received] train flags
         tflag = flag[:, 0] > 0.5
         rp, col = g.rowptr.long(), g.col.long()

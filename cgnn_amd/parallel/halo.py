@@ -149,6 +149,7 @@ class HaloExchange:
                     pos[soff[p] + a:soff[p] + b] = torch.arange(base, base + b - a, device=self.dev)
                     base += b - a
         self._ext_base.append(base)
+        self._pos = pos
         j = torch.searchsorted(need, c.clamp_min(0))
         ext = torch.where(local, c - self.r0, self.nloc + pos[j.clamp_max(max(self.n_recv - 1, 0))]
                           if self.n_recv else c - self.r0)
@@ -162,6 +163,12 @@ class HaloExchange:
         for t in range(rounds):
             parts = [self.send_idx[off[p] + a:off[p] + b] for p, (a, b) in enumerate(self._send_r[t])]
             self._send_idx_r.append(torch.cat(parts) if parts else self.send_idx[:0])
+
+    def received_ids(self) -> torch.Tensor:
+        """Global id of every received row, in extended-space order (rows nloc...)."""
+        ids = torch.empty(self.n_recv, dtype=torch.int64, device=self.dev)
+        ids[self._pos] = self.need
+        return ids
 
     def _split(self, splits: Sequence[int], t: int):
         R = self.rounds

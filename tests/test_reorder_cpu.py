@@ -93,6 +93,47 @@ def test_shards_reassemble_the_full_graph(world, id_order):
     assert torch.equal(torch.cat([p.mask for p in parts]), full.mask)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_locality_shards_reassemble_the_reordered_graph(world):
+    """partition='locality': the shards are exactly the rows of reorder(synthetic(...)),
+    and every shard can flag any global row as train or not (the dry run's halo flags)."""
+    from cgnn_amd.gnn.data import partition_order, synthetic_shard
+    full, nid = reorder(synthetic("ogbn-products", seed=5, scale=0.002), seed=5)
+    order = partition_order("ogbn-products", seed=5, scale=0.002)
+    assert np.array_equal(order, nid.numpy())
+    parts = [synthetic_shard("ogbn-products", r, world, seed=5, scale=0.002, order=order) for r in range(world)]
+    rp = torch.cat([parts[0].rowptr.long()] + [p.rowptr.long()[1:] + sum(q.nnz for q in parts[:i])
+                                               for i, p in enumerate(parts) if i > 0])
+    assert torch.equal(rp, full.rowptr.long())
+    assert torch.equal(torch.cat([p.col for p in parts]), full.col)
+    assert torch.equal(torch.cat([p.x for p in parts]), full.x)
+    assert torch.equal(torch.cat([p.y for p in parts]), full.y)
+    assert torch.equal(torch.cat([p.mask for p in parts]), full.mask)
+    rows = torch.arange(full.n)
+    assert torch.equal(parts[0].train_flags(rows), full.mask == 1)
+
+
+def test_locality_partition_shrinks_the_halo():
+    """Rank 0 of 8: the rows its edges read from other ranks, shuffled ids vs the
+    locality partition (the papers100M dry run's halo, at a small scale)."""
+    from cgnn_amd.gnn.data import synthetic_shard
+    world = 8
+    kw = dict(seed=1, scale=0.02)
+    plain = synthetic_shard("ogbn-products", 0, world, **kw)
+    loc = synthetic_shard("ogbn-products", 0, world, partition="locality", **kw)
+
+    def halo(sh):
+        c = sh.col.long()
+        return torch.unique(c[(c < sh.r0) | (c >= sh.r1)]).numel()
+    h0, h1 = halo(plain), halo(loc)
+    # the 20 % uniformly random edges (homophily 0.8) bound any partition from below:
+    # ~n_other (1 - exp(-0.2 nnz_local / n_other)) distinct remote rows
+    n_other = plain.n - plain.n_local
+    floor = n_other * (1 - np.exp(-0.2 * loc.nnz / n_other))
+    assert h1 < 0.75 * h0, (h0, h1)
+    assert h1 < 1.15 * floor, (h1, floor)
+
+
 def test_id_permutation_inverse():
     rt = native.rt()
     ids = np.arange(10007)

@@ -68,6 +68,8 @@ def main():
                     help="papers-gat2: one process plays rank --emulate-rank of this many ranks (its "
                          "rank-local shard, halo plan and buffers; received rows zero) -- memory / compute dry run")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--partition", choices=["locality", "none"], default="locality",
+                    help="papers-gat2: locality partition of the sharded graph (data.partition_order, timed in setup)")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal: every rank on cuda:0 with gloo collectives (multi-rank path on one GPU)")
     ap.add_argument("--sampler", choices=["pipelined", "device", "host"], default=None,
@@ -189,8 +191,15 @@ def main():
         emu = (a.emulate_rank, a.emulate_world) if a.emulate_world > 1 else None
         srank, sworld = emu if emu else (rank, world)
         t0 = time.perf_counter()
-        shard = synthetic_shard("ogbn-papers100M", srank, sworld, seed=a.seed, device=dev, scale=a.scale)
-        gen_s = time.perf_counter() - t0
+        order = None
+        if a.partition == "locality":
+            from cgnn_amd.gnn.data import partition_order
+            order = partition_order("ogbn-papers100M", seed=a.seed, scale=a.scale)
+        part_s = time.perf_counter() - t0
+        shard = synthetic_shard("ogbn-papers100M", srank, sworld, seed=a.seed, device=dev, scale=a.scale,
+                                order=order)
+        del order
+        gen_s = time.perf_counter() - t0 - part_s
         n_nodes, nnz_local, n_local = shard.n, shard.nnz, shard.n_local
         tr = ShardedGATTrainer(shard, heads=4, head_dim=32, dropout=0.5, lr=0.005, seed=a.seed, emulate=emu,
                                fused=False if a.unfused else None)
@@ -210,9 +219,12 @@ def main():
                    if dev.type == "cuda" else "fp32",
                    peak_gpu_mem_gib=round(peak, 2) if peak is not None else None,
                    shard={"rank": srank, "world": sworld, "rows": n_local, "nnz": nnz_local, "gen_s": round(gen_s, 2),
-                          "rank_local_generation": True},
-                   halo=tr.halo_stats(), emulated=emu is not None, reordered=False, fused=tr.fused is not None,
-                   note=("DRY RUN: one rank of %d in one process; received halo rows are zero, so timing / memory "
+                          "partition": a.partition, "partition_s": round(part_s, 2), "rank_local_generation": True},
+                   halo=tr.halo_stats(), emulated=emu is not None, reordered=a.partition == "locality",
+                   fused=tr.fused is not None,
+                   layer1_train_pruned=bool(tr.fused is not None and tr.fused._g1 is not None),
+                   note=("DRY RUN: one rank of %d in one process; received halo rows are zero (their train flags "
+                         "are generated locally, so the layer-1 pruning is the real one), so timing / memory "
                          "are those of the rank's kernels and buffers without communication, accuracy is not "
                          "meaningful" % sworld) if emu else None,
                    config={"model": "GAT-2layer-4x32", "parallelism": "graph-rowpart%d" % sworld, "nodes": n_nodes})
