@@ -105,7 +105,8 @@ def main():
         # generation, locality reorder) this rank's share of the node's cores instead
         from cgnn_amd import native
         lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-        native.rt().set_num_threads(max(1, (os.cpu_count() or 8) // max(lw, 1)))
+        cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
+        native.rt().set_num_threads(max(1, cpus // max(lw, 1)))
     if cuda:
         torch.cuda.set_device(0 if shared else local)
         dev = torch.device("cuda", torch.cuda.current_device())
