@@ -195,5 +195,48 @@ __device__ __forceinline__ void rbf7x2(f2 d2, f2& ks, f2& w) {
   w = ((0.005f * e[0] + 0.05f * e[1]) + (0.25f * e[2] + 0.5f * e[3])) + ((e[4] + 5.0f * e[5]) + 50.0f * e[6]);
 }
 
+// ---- packed 16-bit epilogue helpers (two elements per dword, one instruction each) ----
+// two fp32 -> two bf16 in one dword (hipcc emits v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t cvt_pk(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+// two fp32 -> two fp16 in one dword (round to nearest even)
+__device__ __forceinline__ uint32_t cvt_pk_h(float a, float b) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  const h2 v = {(_Float16)a, (_Float16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+// per 16-bit half max(x, lo) as signed integers.  lo = 0 is the relu of two bf16 / fp16
+// values (a negative one, -0 included, is a negative int16); lo = 0x80008000 leaves x as is
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t x, uint32_t lo) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, %2" : "=v"(r) : "v"(x), "s"(lo));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_relu(uint32_t x) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(x));
+  return r;
+}
+// per 16-bit half: x * k (k in {0, 1}: a keep bit applied without a compare or select)
+__device__ __forceinline__ uint32_t pk_mul16(uint32_t x, uint32_t k) {
+  uint32_t r;
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(x), "v"(k));
+  return r;
+}
+// per 16-bit half: 1 if x != 0 else 0 (x a relu output, so != 0 means > 0).  The 1s
+// come from a register: an inline constant of a packed instruction reaches only the low
+// half (the high half of its 32-bit value, 0, feeds the high half).
+__device__ __forceinline__ uint32_t pk_nz(uint32_t x) {
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(x), "s"(0x00010001u));
+  return r;
+}
+// the 16 keep bits m of a dropout block spread for pk_mul16: bit 2i stays, bit 2i + 1
+// moves to bit 2i + 16, so (spread >> 2i) & 0x10001 is the keep pair of values 2i, 2i + 1
+__device__ __forceinline__ uint32_t keep_spread(uint32_t m) { return (m & 0x5555u) | ((m & 0xaaaau) << 15); }
+
 
 }  // namespace cgnn

@@ -75,34 +75,7 @@ __device__ __forceinline__ int stg_off(int row, int ch) {
   return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
-// ---- packed bf16 epilogue helpers (two elements per dword, one instruction each) ----
-// two fp32 -> two bf16 in one dword (hipcc emits v_cvt_pk_bf16_f32)
-__device__ __forceinline__ uint32_t cvt_pk(float a, float b) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  const bf16x2 v = {(__bf16)a, (__bf16)b};
-  return __builtin_bit_cast(uint32_t, v);
-}
-// relu of two bf16 as signed 16-bit integers: a negative bf16 (sign bit set, -0
-// included) is a negative int16, so max(x, 0) is exactly the bf16 relu
-__device__ __forceinline__ uint32_t pk_relu(uint32_t x) {
-  uint32_t r;
-  asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(x));
-  return r;
-}
-// per 16-bit half: x * k (k in {0, 1}: a keep bit applied without a compare or select)
-__device__ __forceinline__ uint32_t pk_mul16(uint32_t x, uint32_t k) {
-  uint32_t r;
-  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(x), "v"(k));
-  return r;
-}
-// per 16-bit half: 1 if x != 0 else 0 (x a relu output, so != 0 means > 0).  The 1s
-// come from a register: an inline constant of a packed instruction reaches only the low
-// half (the high half of its 32-bit value, 0, feeds the high half).
-__device__ __forceinline__ uint32_t pk_nz(uint32_t x) {
-  uint32_t r;
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(x), "s"(0x00010001u));
-  return r;
-}
+// packed bf16 epilogue helpers (cvt_pk, pk_relu, pk_mul16, pk_nz): cgnn_common.h
 
 // ds_read_b64_tr_b16 (gfx950): lane 4q+p of a 16-lane group gives the address of
 // row q, columns 4p..4p+3 of a 4x16 block; lane i receives column i of the 4 rows.

@@ -54,8 +54,14 @@ constexpr int TILE = 32;
 template <int KS> struct FwdWaves { static constexpr int value = KS <= 16 ? 16 : 8; };
 constexpr int WGT_WAVES = 8;        // weight-gradient blocks
 constexpr bool BWD_DATA_SEL = true;   // lin_bwd_data: branch-free gradient loader
-constexpr int FWD8_WAVES = 16;        // lin_fwd KS = 8: waves per block
-constexpr int FWD16_WAVES = 8;        // lin_fwd KS = 16: waves per block (profiles/r03_waves)
+#ifndef LINX_F8W
+#define LINX_F8W 16
+#endif
+#ifndef LINX_F16W
+#define LINX_F16W 8
+#endif
+constexpr int FWD8_WAVES = LINX_F8W;        // lin_fwd KS = 8: waves per block
+constexpr int FWD16_WAVES = LINX_F16W;        // lin_fwd KS = 16: waves per block (profiles/r03_waves)
 constexpr int BWD16_WAVES = 8;        // lin_bwd_data KN = 16: waves per block (profiles/r03_waves)
 constexpr int FWD_SEL_KS = 8;         // lin_fwd: branch-free X loader from this many k-steps up
 constexpr int TR = TILE + 8;        // transposed image row: 32 rows + pad (80 B)
@@ -255,7 +261,24 @@ int device_cus() {
 // ============================================================================
 // lin_fwd: Y[row][c] = epi(sum_k [X1 | X2][row][k] W[k][c] + b[c]) for the column
 // slab c in [blockIdx.y * ncols, +ncols); KS k-steps of 16 cover K1 + K2.
+//
+// Epilogue on packed 16-bit pairs: the accumulators start from the bias (b128 LDS
+// reads), the dropout scale 1/(1-p) is folded into the weight image and the bias
+// (relu(z) / (1-p) = relu(z / (1-p))), so per pair of outputs the epilogue is one
+// v_cvt_pk_bf16_f32, one v_pk_max_i16 (relu; identity with a floor of -32768) and one
+// v_pk_mul_lo_u16 by the two keep bits.  In bit mode (p = 1/2) one Philox draw covers
+// eight 32-column tiles.  The next tile's X rows load while this tile computes (KS <= 16:
+// a second set of B fragments fits the VGPR budget), and the first tile's rows load
+// before the weight image is staged.
 // ============================================================================
+__device__ __forceinline__ void st_y8(uint16_t* p, uint32_t a, uint32_t b) {
+#ifdef LINX_NT
+  __builtin_nontemporal_store(((unsigned long long)b << 32) | a, reinterpret_cast<unsigned long long*>(p));
+#else
+  *reinterpret_cast<uint2*>(p) = make_uint2(a, b);
+#endif
+}
+
 template <int KS, int ET = 0, int FWD_WAVES = FwdWaves<KS>::value>
 __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     const uint16_t* __restrict__ x1, int ld1, int K1, const uint16_t* __restrict__ x2, int ld2, int K2,
@@ -263,86 +286,171 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     int n, int ncols, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
     uint32_t row0, const int* __restrict__ stepp, const float* __restrict__ rscale, const int* __restrict__ idx1,
     const uint16_t* __restrict__ wimg, float* __restrict__ Yf, int nsplit, int tk) {
-  // wimg: the bf16 LDS image of every column slab ([slabs][ncols][WS], lin_prep_fwd_kernel):
-  // one vectorised copy per block instead of converting / transposing the fp32 weights.
+  // wimg: the bf16 LDS image of every column slab ([slabs][ncols][WS], lin_prep_fwd_kernel,
+  // times 1/(1-p) when dropout is on): one vectorised copy per block instead of converting /
+  // transposing the fp32 weights.
   // Yf (optional): columns c >= nsplit (nsplit % 4 == 0) are written EXACTLY, as fp32
   // planes of tk columns -- Yf[(c - nsplit) / tk][row][(c - nsplit) % tk] -- instead of
   // bf16 into Y (GAT: the attention scores s_src / s_dst folded into the projection)
   if (stepp) step = (uint32_t)*stepp;
   constexpr int KP = KS * 16;
   constexpr int WS = KP + 8;                     // padded row stride of the W^T slab
+  constexpr bool PF = KS <= 16 && FWD_WAVES <= 8;   // next-tile prefetch (256 VGPRs)
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* sWT = lds;                           // [ncols][WS]
-  float* sB = reinterpret_cast<float*>(sWT + (size_t)ncols * WS);   // [ncols]
+  float* sB = reinterpret_cast<float*>(sWT + (size_t)ncols * WS);   // [ncols]: bias / (1 - p)
   const int c0 = blockIdx.y * ncols;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(wimg + (size_t)blockIdx.y * ncols * WS);
-    uint4* dst = reinterpret_cast<uint4*>(sWT);
-    copy_image(dst, src, ncols * WS / 8);
-  }
-  for (int c = threadIdx.x; c < ncols; c += blockDim.x) sB[c] = (bias && c0 + c < N) ? bias[c0 + c] : 0.f;
-  __syncthreads();
-
   const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31;
-  const int wave = blockIdx.x * FWD_WAVES + (threadIdx.x >> 6);
   const int n_waves = gridDim.x * FWD_WAVES;
   const int n_tiles = (n + TILE - 1) / TILE;
   const float scale = thr8 > 0 ? 1.f / (1.f - p) : 1.f;
+  const bool bit = drop_bit_mode(thr8);
   const int nt = ncols / 32;
+  const uint32_t floor16 = relu ? 0u : 0x80008000u;
+  const bool full = c0 + ncols <= ldy && !Yf;    // every column of the slab is stored
 
-  for (int tile = wave; tile < n_tiles; tile += n_waves) {
+  // K1 % 8 == 0 and K2 % 8 == 0: every 16-byte chunk is wholly inside or wholly outside
+  // [X1 | X2], and a chunk outside re-reads its row's first chunk against zero weight rows
+  // of the image, so no chunk needs masking (only a chunk straddling K holds padding
+  // columns, which may hold anything)
+  const bool ragged = (K1 & 7) || (K2 & 7);
+  auto load = [&](int tile, uint4 (&bx)[KS]) {
     const int row = tile * TILE + lr;
     const bool rv = row < n;
-    // fh is opaque per tile (empty asm) so the per-k-step offsets and validity selects
-    // derived from it are recomputed next to their loads instead of being hoisted out of
-    // the tile loop as 2 * KS live registers
-    int fh = 8 * h;
-    asm volatile("" : "+v"(fh));
-    uint4 bx[KS];
+    if constexpr (KS >= FWD_SEL_KS) {
+      // wide K: branch-free addresses (per-lane branches unrolled KS times spill the SGPRs)
+      const int rr = rv ? row : n - 1;
+      const uint16_t* p1 = x1 + (idx1 ? (size_t)idx1[rr] : (size_t)rr) * ld1;
+      const uint16_t* p2 = x2 ? x2 + (size_t)rr * ld2 : p1;
+      // fh is opaque per tile (empty asm) so the per-k-step offsets and selects derived
+      // from it are recomputed next to their loads instead of being hoisted out of the
+      // tile loop as 2 * KS live registers
+      int fh = 8 * h;
+      asm volatile("" : "+v"(fh));
+      if (!ragged) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if constexpr (KS >= FWD_SEL_KS)    // wide K: the branch-free form (no exec-mask spills)
-        bx[s] = load_cat8_sel(x1, ld1, K1, x2, ld2, K2, rv ? row : n - 1, 16 * s + fh, idx1);
-      else
+        for (int s = 0; s < KS; ++s) {
+          const int f0 = 16 * s + fh, g = f0 - K1;
+          bx[s] = *reinterpret_cast<const uint4*>(f0 < K1 ? p1 + f0 : g < K2 ? p2 + g : p1);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+          bx[s] = load_cat8_sel(x1, ld1, K1, x2, ld2, K2, rr, 16 * s + fh, idx1);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
         bx[s] = rv ? load_cat8(x1, ld1, K1, x2, ld2, K2, row, 16 * s + 8 * h, idx1) : make_uint4(0u, 0u, 0u, 0u);
     }
+  };
+
+  auto process = [&](int tile, const uint4 (&bx)[KS]) {
+    const int row = tile * TILE + lr;
+    const bool rv = row < n;
     const float rs = (rv && rscale) ? rscale[row] : 1.f;
+    u32x4 r = {0u, 0u, 0u, 0u};
 #pragma unroll 1
     for (int t = 0; t < nt; ++t) {
-      f32x16 acc = {};
+      const int tg = c0 / 32 + t;                // global 32-column tile
+      f32x16 acc;
+      {
+        const float4* bp = reinterpret_cast<const float4*>(sB + 32 * t + 4 * h);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bb = bp[2 * g];
+          acc[4 * g] = bb.x; acc[4 * g + 1] = bb.y; acc[4 * g + 2] = bb.z; acc[4 * g + 3] = bb.w;
+        }
+      }
       const uint16_t* arow = sWT + (32 * t + lr) * WS + 8 * h;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         acc = mma16<ET>(*reinterpret_cast<const uint4*>(arow + 16 * s), bx[s], acc);
       if (!rv) continue;
-      const int cg = c0 + 32 * t;                // global column of this tile
       uint32_t m = 0xffffu;
-      if (thr8 > 0)
-        m = drop_keep16(drop_draw(row0 + (uint32_t)row, cg / 32, h, step, k0, k1, drop_bit_mode(thr8)), cg / 32, thr8,
-                        drop_bit_mode(thr8));
-      float v[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int cl = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
-        float x = acc[q] + sB[cl];
-        if (relu) x = fmaxf(x, 0.f);
-        if (thr8 > 0) x = ((m >> q) & 1u) ? x * scale : 0.f;
-        v[q] = x * rs;
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c = cg + 8 * g + 4 * h;
-        if (Yf && c >= nsplit) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int t = c + e - nsplit;
-            if (c + e < N) Yf[(size_t)(t / tk) * n * tk + (size_t)row * tk + t % tk] = v[4 * g + e];
-          }
-        } else if (c < ldy) {
-          *reinterpret_cast<uint2*>(Y + (size_t)row * ldy + c) =
-              pack4e<ET>(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+      if (thr8 > 0) {
+        if (!bit || t == 0 || (tg & 7) == 0) {
+          // opaque row id: the draw stays behind its condition (hoisted, it ran every tile t)
+          uint32_t gr = row0 + (uint32_t)row;
+          asm volatile("" : "+v"(gr));
+          r = drop_draw(gr, tg, h, step, k0, k1, bit);
         }
+        m = drop_keep16(r, tg, thr8, bit);
       }
+      const int cg = 32 * tg;                    // global column of this tile
+      if (Yf) {
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          float x = acc[q];
+          if (relu) x = fmaxf(x, 0.f);
+          v[q] = ((m >> q) & 1u) ? x * rs : 0.f;
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = cg + 8 * g + 4 * h;
+          if (c >= nsplit) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int u = c + e - nsplit;
+              if (c + e < N) Yf[(size_t)(u / tk) * n * tk + (size_t)row * tk + u % tk] = v[4 * g + e];
+            }
+          } else if (c < ldy) {
+            *reinterpret_cast<uint2*>(Y + (size_t)row * ldy + c) =
+                pack4e<ET>(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+          }
+        }
+        continue;
+      }
+      uint32_t pk[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const f2 z = f2{acc[2 * i], acc[2 * i + 1]} * rs;
+        pk[i] = pk_max_i16(ET == 1 ? cvt_pk_h(z.x, z.y) : cvt_pk(z.x, z.y), floor16);
+      }
+      if (thr8 > 0) {
+        const uint32_t mw = keep_spread(m);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pk[i] = pk_mul16(pk[i], (mw >> (2 * i)) & 0x10001u);
+      }
+      uint16_t* yrow = Y + (size_t)row * ldy + cg + 4 * h;
+      if (full) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) st_y8(yrow + 8 * g, pk[2 * g], pk[2 * g + 1]);
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          if (cg + 8 * g + 4 * h < ldy) st_y8(yrow + 8 * g, pk[2 * g], pk[2 * g + 1]);
+      }
+    }
+  };
+
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int tile = blockIdx.x * FWD_WAVES + wv;
+  uint4 bxa[KS], bxb[KS];
+  if (tile < n_tiles) load(tile, bxa);           // in flight while the weights are staged
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(wimg + (size_t)blockIdx.y * ncols * WS);
+    uint4* dst = reinterpret_cast<uint4*>(sWT);
+    copy_image(dst, src, ncols * WS / 8);
+  }
+  for (int c = threadIdx.x; c < ncols; c += blockDim.x) sB[c] = (bias && c0 + c < N) ? bias[c0 + c] * scale : 0.f;
+  __syncthreads();
+
+  if constexpr (PF) {
+    while (tile < n_tiles) {
+      if (tile + n_waves < n_tiles) load(tile + n_waves, bxb);
+      process(tile, bxa);
+      tile += n_waves;
+      if (tile >= n_tiles) break;
+      if (tile + n_waves < n_tiles) load(tile + n_waves, bxa);
+      process(tile, bxb);
+      tile += n_waves;
+    }
+  } else {
+    for (bool first = true; tile < n_tiles; tile += n_waves, first = false) {
+      if (!first) load(tile, bxa);
+      process(tile, bxa);
     }
   }
 }
@@ -379,11 +487,19 @@ __global__ __launch_bounds__(256, 2) void lin_fwd_kc_kernel(
     rv[u] = r < n;
     rows[u] = rv[u] ? r : n - 1;
   }
+  // accumulators start from the bias (the same rounding as lin_fwd's, which does the same)
   f32x16 acc[2][4];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int t = 0; t < 4; ++t) {
+    f32x16 b0 = {};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[u][t] = f32x16{};
+    for (int q = 0; q < 16; ++q) {
+      const int c = 128 * fg + 32 * t + 8 * (q >> 2) + 4 * h + (q & 3);
+      b0[q] = (bias && c < N) ? bias[c] : 0.f;
+    }
+    acc[0][t] = b0;
+    acc[1][t] = b0;
+  }
   const int nch = KPc / BK;
   uint4 wr[WCH];
   auto wload = [&](int c) {
@@ -457,7 +573,7 @@ __global__ __launch_bounds__(256, 2) void lin_fwd_kc_kernel(
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float y = acc[u][t][4 * g + e] + ((bias && c + e < N) ? bias[c + e] : 0.f);
+          float y = acc[u][t][4 * g + e];
           if (relu) y = fmaxf(y, 0.f);
           v[e] = y * rs;
         }
@@ -513,11 +629,18 @@ __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
       *reinterpret_cast<uint4*>(sW + buf * 256 * BK + gemm_off(r, ch)) = wr[j];
     }
   };
-  f32x16 acc[2][4];
+  f32x16 acc[2][4];                         // from the bias, as lin_fwd
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int t = 0; t < 4; ++t) {
+    f32x16 b0 = {};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[u][t] = f32x16{};
+    for (int q = 0; q < 16; ++q) {
+      const int c = 128 * ng + 32 * t + 8 * (q >> 2) + 4 * h + (q & 3);
+      b0[q] = (bias && c < N) ? bias[c] : 0.f;
+    }
+    acc[0][t] = b0;
+    acc[1][t] = b0;
+  }
   load(0);
   store(0);
   __syncthreads();
@@ -558,7 +681,7 @@ __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float y = acc[u][t][4 * g + e] + ((bias && col + e < N) ? bias[col + e] : 0.f);
+          float y = acc[u][t][4 * g + e];
           if (relu) y = fmaxf(y, 0.f);
           v[e] = y * rs;
         }
@@ -582,6 +705,10 @@ __global__ __launch_bounds__(256) void lin_prep_kc_kernel(const float* __restric
 // lin_bwd_data: dX^T[k][row] = sum_c W[k][c] (dY * m)[row][c] for the k slab
 // [blockIdx.y * kcols, +kcols); KN k-steps of 16 cover the N gradient columns.
 // Output k < K1 -> dX1, K1 <= k < K1 + K2 -> dX2; times rscale[row] (optional).
+// The mask [Ym > 0] is two packed instructions per pair of gradient values
+// (v_pk_max_i16 / v_pk_min_u16 -> 0 / 1, then v_pk_mul_lo_u16); mscale = 1/(1-p) rides on
+// the fp32 row scale of the epilogue.  The next tile's raw dY / Ym rows load while this
+// tile computes and are masked after it (KN <= 16 on 8-wave blocks: the registers fit).
 // ============================================================================
 template <int KN, int FWD_WAVES = FwdWaves<KN>::value>
 __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
@@ -592,33 +719,66 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
   // wimg: bf16 LDS image of every k slab ([slabs][kcols][WS], lin_prep_bwd_kernel)
   constexpr int NP = KN * 16;
   constexpr int WS = NP + 8;
+  constexpr bool PF = KN <= 16 && FWD_WAVES <= 8;
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   uint16_t* sW = lds;                            // [kcols][WS]: rows of W
   const int kb = blockIdx.y * kcols;
-  const int K = K1 + K2;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(wimg + (size_t)blockIdx.y * kcols * WS);
-    uint4* dst = reinterpret_cast<uint4*>(sW);
-    copy_image(dst, src, kcols * WS / 8);
-  }
-  __syncthreads();
   const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31;
-  const int wave = blockIdx.x * FWD_WAVES + (threadIdx.x >> 6);
   const int n_waves = gridDim.x * FWD_WAVES;
   const int n_tiles = (n + TILE - 1) / TILE;
   const int nt = kcols / 32;
-  for (int tile = wave; tile < n_tiles; tile += n_waves) {
+
+  // raw 16-byte chunks of the tile's gradient / stored-output rows (clamped row: every
+  // lane loads from a valid address; a chunk past N re-reads the row's first chunk against
+  // zero weight columns of the image)
+  auto load = [&](int tile, uint4 (&gr)[KN], uint4 (&yr)[KN]) {
+    const int row = min(tile * TILE + lr, n - 1);
+    int fh = 8 * h;
+    asm volatile("" : "+v"(fh));
+#pragma unroll
+    for (int s = 0; s < KN; ++s) {
+      const int c = 16 * s + fh;
+      const int cc = c < N ? c : 0;
+      gr[s] = *reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + cc);
+      if (Ym) yr[s] = *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + cc);
+    }
+  };
+  // N % 8 == 0: no chunk straddles N (rows past n are never stored: no masking either)
+  // chunk s* = (N & ~7) / 16 is the only one that straddles N (in the lanes of half
+  // h* = (N / 8) & 1; in the other half it lies wholly past N and is zeroed as well)
+  const bool ragged = N & 7;
+  const int sstar = (N & ~7) / 16;
+  // dY * [Ym > 0] (and zero past N when a chunk straddles it)
+  auto mask1 = [&](int s, uint4 g, uint4 y, bool rag) {
+    if (rag && s == sstar) g = keep_first_sel(g, N - (16 * s + 8 * h));
+    if (Ym)
+      g = make_uint4(pk_mul16(g.x, pk_nz(pk_relu(y.x))), pk_mul16(g.y, pk_nz(pk_relu(y.y))),
+                     pk_mul16(g.z, pk_nz(pk_relu(y.z))), pk_mul16(g.w, pk_nz(pk_relu(y.w))));
+    return as_bf16x8(g);
+  };
+  auto mask = [&](const uint4 (&gr)[KN], const uint4 (&yr)[KN], bf16x8 (&by)[KN]) {
+#pragma unroll
+    for (int s = 0; s < KN; ++s) by[s] = mask1(s, gr[s], yr[s], false);
+  };
+  // the non-prefetching form: each chunk masked as it arrives (no second register set)
+  auto load_masked = [&](int tile, bf16x8 (&by)[KN]) {
+    const int row = min(tile * TILE + lr, n - 1);
+    int fh = 8 * h;
+    asm volatile("" : "+v"(fh));
+#pragma unroll
+    for (int s = 0; s < KN; ++s) {
+      const int c = 16 * s + fh;
+      const int cc = c < N ? c : 0;
+      const uint4 g = *reinterpret_cast<const uint4*>(dY + (size_t)row * lddy + cc);
+      uint4 y = make_uint4(0u, 0u, 0u, 0u);
+      if (Ym) y = *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + cc);
+      by[s] = mask1(s, g, y, ragged);
+    }
+  };
+  auto process = [&](int tile, const bf16x8 (&by)[KN]) {
     const int row = tile * TILE + lr;
     const bool rv = row < n;
-    bf16x8 by[KN];
-    // branch-free unless it would push the 16-wave KN = 16 variant past 128 VGPRs
-    constexpr bool sel = BWD_DATA_SEL && !(KN == 16 && FWD_WAVES == 16);
-#pragma unroll
-    for (int s = 0; s < KN; ++s)
-      by[s] = as_bf16x8(sel ? load_masked8_sel(dY, lddy, Ym, ldym, mscale, N, rv ? row : n - 1, 16 * s + 8 * h, rv)
-                                          : (rv ? load_masked8(dY, lddy, Ym, ldym, mscale, N, row, 16 * s + 8 * h)
-                                                : make_uint4(0u, 0u, 0u, 0u)));
-    const float rs = (rv && rscale) ? rscale[row] : 1.f;
+    const float rs = ((rv && rscale) ? rscale[row] : 1.f) * mscale;
 #pragma unroll 1
     for (int t = 0; t < nt; ++t) {
       f32x16 acc = {};
@@ -631,19 +791,47 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int k = kb + 32 * t + 8 * g + 4 * h;          // 4 consecutive k, never straddling K1 (K1 % 8 == 0)
-        const uint2 o = pack4(acc[4 * g] * rs, acc[4 * g + 1] * rs, acc[4 * g + 2] * rs, acc[4 * g + 3] * rs);
+        const f2 lo = f2{acc[4 * g], acc[4 * g + 1]} * rs, hi = f2{acc[4 * g + 2], acc[4 * g + 3]} * rs;
         if (k < K1) {
           if (k < ldx1) {
             if (dx1_f32)
               *reinterpret_cast<float4*>(reinterpret_cast<float*>(dX1) + (size_t)row * ldx1 + k) =
-                  make_float4(acc[4 * g] * rs, acc[4 * g + 1] * rs, acc[4 * g + 2] * rs, acc[4 * g + 3] * rs);
+                  make_float4(lo.x, lo.y, hi.x, hi.y);
             else
-              *reinterpret_cast<uint2*>(dX1 + (size_t)row * ldx1 + k) = o;
+              st_y8(dX1 + (size_t)row * ldx1 + k, cvt_pk(lo.x, lo.y), cvt_pk(hi.x, hi.y));
           }
         } else if (dX2 && k - K1 < ldx2 && k < K1 + ldx2) {
-          *reinterpret_cast<uint2*>(dX2 + (size_t)row * ldx2 + (k - K1)) = o;
+          st_y8(dX2 + (size_t)row * ldx2 + (k - K1), cvt_pk(lo.x, lo.y), cvt_pk(hi.x, hi.y));
         }
       }
+    }
+  };
+
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int tile = blockIdx.x * FWD_WAVES + wv;
+  auto stage = [&]() {
+    const uint4* src = reinterpret_cast<const uint4*>(wimg + (size_t)blockIdx.y * kcols * WS);
+    uint4* dst = reinterpret_cast<uint4*>(sW);
+    copy_image(dst, src, kcols * WS / 8);
+    __syncthreads();
+  };
+  bf16x8 by[KN];
+  if (PF && !ragged) {
+    uint4 gr[KN], yr[KN];
+    if (tile < n_tiles) load(tile, gr, yr);      // in flight while the weights are staged
+    stage();
+    if (tile < n_tiles) mask(gr, yr, by);
+    for (; tile < n_tiles; tile += n_waves) {
+      const bool more = tile + n_waves < n_tiles;
+      if (more) load(tile + n_waves, gr, yr);
+      process(tile, by);
+      if (more) mask(gr, yr, by);
+    }
+  } else {
+    stage();
+    for (; tile < n_tiles; tile += n_waves) {
+      load_masked(tile, by);
+      process(tile, by);
     }
   }
 }
@@ -1027,13 +1215,14 @@ __global__ __launch_bounds__(256) void lin_reduce_kernel(const float* __restrict
 // zero outside the matrix and in the pad columns
 template <int ET>
 __global__ __launch_bounds__(256) void lin_prep_fwd_kernel(const float* __restrict__ W, int K, int N, int ncols,
-                                                           int KP, int WS, long total, uint16_t* __restrict__ img) {
+                                                           int KP, int WS, long total, float scale,
+                                                           uint16_t* __restrict__ img) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int k = (int)(i % WS);
   const long rc = i / WS;                       // slab * ncols + c = global column
   const int c = (int)rc;
-  img[i] = e16_bits<ET>(k < K && k < KP && c < N ? W[(size_t)k * N + c] : 0.f);
+  img[i] = e16_bits<ET>(k < K && k < KP && c < N ? W[(size_t)k * N + c] * scale : 0.f);
 }
 
 __global__ __launch_bounds__(256) void lin_prep_bwd_kernel(const float* __restrict__ W, int K, int N, int NP, int WS,
@@ -1079,8 +1268,9 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
   {
     const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
     const long total = (long)slabs * ncols * (KP + 8);
+    const float scale = thr8 > 0 ? 1.f / (1.f - p) : 1.f;     // the dropout scale, folded into the image
     hipLaunchKernelGGL(lin_prep_fwd_kernel<ET>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2,
-                       N, ncols, KP, KP + 8, total, wimg);
+                       N, ncols, KP, KP + 8, total, scale, wimg);
   }
   (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS, ET, WV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
