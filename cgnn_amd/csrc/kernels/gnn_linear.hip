@@ -54,8 +54,17 @@ constexpr int TILE = 32;
 template <int KS> struct FwdWaves { static constexpr int value = KS <= 16 ? 16 : 8; };
 constexpr int WGT_WAVES = 8;        // weight-gradient blocks
 constexpr bool BWD_DATA_SEL = true;   // lin_bwd_data: branch-free gradient loader
+#ifndef LINX_TST
+#define LINX_TST 1
+#endif
+#ifndef LINX_WS
+#define LINX_WS 1
+#endif
+#ifndef LINX_STFIRST
+#define LINX_STFIRST 0
+#endif
 #ifndef LINX_F8W
-#define LINX_F8W 16
+#define LINX_F8W 8
 #endif
 #ifndef LINX_F16W
 #define LINX_F16W 8
@@ -271,6 +280,33 @@ int device_cus() {
 // a second set of B fragments fits the VGPR budget), and the first tile's rows load
 // before the weight image is staged.
 // ============================================================================
+// Output staging of one wave's 32-row x 32-column bf16 tile (lane (lr, h) holds row lr,
+// columns 8 g + 4 h + 0..3 in pk[2 g], pk[2 g + 1]): through a per-wave LDS tile (rows of
+// 80 B) so that each global store instruction writes 16 whole 64-B row segments
+// (16 B per lane, 4 lanes per row) instead of 32 rows x 16 B -- every store leaves L2 as
+// its own fabric requests, so the narrow pieces cost ~4x the bytes' time.  emit(r, c, v):
+// global row r (< n), column offset c in {0, 8, 16, 24}, 8 bf16 values.
+constexpr int OST_PITCH = 80, OST_BYTES = 32 * OST_PITCH;
+template <class Emit>
+__device__ __forceinline__ void out_stage(uint16_t* lds, int ost, const uint32_t (&pk)[8], int tile, int n, Emit emit) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31;
+  uint8_t* so = reinterpret_cast<uint8_t*>(lds) + ost + (threadIdx.x >> 6) * OST_BYTES;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) *reinterpret_cast<uint2*>(so + lr * OST_PITCH + 16 * g + 8 * h) = make_uint2(pk[2 * g], pk[2 * g + 1]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * i + (lane >> 2), c = lane & 3;
+    const uint4 v = *reinterpret_cast<const uint4*>(so + r * OST_PITCH + 16 * c);
+    if (tile * TILE + r < n) emit(tile * TILE + r, 8 * c, v);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ void st_y8(uint16_t* p, uint32_t a, uint32_t b) {
 #ifdef LINX_NT
   __builtin_nontemporal_store(((unsigned long long)b << 32) | a, reinterpret_cast<unsigned long long*>(p));
@@ -285,13 +321,14 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
     const float* __restrict__ W, int N, const float* __restrict__ bias, uint16_t* __restrict__ Y, int ldy,
     int n, int ncols, int relu, float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8,
     uint32_t row0, const int* __restrict__ stepp, const float* __restrict__ rscale, const int* __restrict__ idx1,
-    const uint16_t* __restrict__ wimg, float* __restrict__ Yf, int nsplit, int tk) {
+    const uint16_t* __restrict__ wimg, float* __restrict__ Yf, int nsplit, int tk, int ost) {
   // wimg: the bf16 LDS image of every column slab ([slabs][ncols][WS], lin_prep_fwd_kernel,
   // times 1/(1-p) when dropout is on): one vectorised copy per block instead of converting /
   // transposing the fp32 weights.
   // Yf (optional): columns c >= nsplit (nsplit % 4 == 0) are written EXACTLY, as fp32
   // planes of tk columns -- Yf[(c - nsplit) / tk][row][(c - nsplit) % tk] -- instead of
   // bf16 into Y (GAT: the attention scores s_src / s_dst folded into the projection)
+  // ost >= 0: byte offset of the per-wave output staging tiles in LDS (out_stage)
   if (stepp) step = (uint32_t)*stepp;
   constexpr int KP = KS * 16;
   constexpr int WS = KP + 8;                     // padded row stride of the W^T slab
@@ -366,7 +403,7 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         acc = mma16<ET>(*reinterpret_cast<const uint4*>(arow + 16 * s), bx[s], acc);
-      if (!rv) continue;
+      // (rows past n run the epilogue too: with staged stores their lanes carry other rows)
       uint32_t m = 0xffffu;
       if (thr8 > 0) {
         if (!bit || t == 0 || (tg & 7) == 0) {
@@ -379,6 +416,7 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
       }
       const int cg = 32 * tg;                    // global column of this tile
       if (Yf) {
+        if (!rv) continue;
         float v[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -413,6 +451,13 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_fwd_kernel(
 #pragma unroll
         for (int i = 0; i < 8; ++i) pk[i] = pk_mul16(pk[i], (mw >> (2 * i)) & 0x10001u);
       }
+      if (ost >= 0) {
+        out_stage(lds, ost, pk, tile, n, [&](int r, int c, uint4 v) {
+          if (full || cg + c < ldy) *reinterpret_cast<uint4*>(Y + (size_t)r * ldy + cg + c) = v;
+        });
+        continue;
+      }
+      if (!rv) continue;
       uint16_t* yrow = Y + (size_t)row * ldy + cg + 4 * h;
       if (full) {
 #pragma unroll
@@ -595,6 +640,7 @@ __global__ __launch_bounds__(256, 2) void lin_fwd_kc_kernel(
 // lin_fwd_kc_kernel; bias, ReLU and the row scale in the epilogue.
 // ============================================================================
 __device__ __forceinline__ int gemm_off(int r, int ch) { return r * 64 + 8 * (ch ^ ((r >> 1) & 7)); }
+constexpr int GEMM_OST_PITCH = 272, GEMM_OST_BYTES = 64 * GEMM_OST_PITCH;   // epilogue staging per wave
 
 template <int ET>
 __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
@@ -667,6 +713,42 @@ __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
     __syncthreads();
   }
   // epilogue: lane = row, registers 4g..4g+3 = columns 128 ng + 32 t + 8 g + 4 h + 0..3
+  const uint32_t floor16 = relu ? 0u : 0x80008000u;
+#if LINX_TST
+  // packed 16-bit values staged through the (now free) LDS as the wave's 64-row x
+  // 128-column block, then stored as whole 256-B row pieces (16 lanes per row): a store
+  // instruction of the transposed layout writes 32 rows x 16 B, every piece its own
+  // fabric request
+  uint8_t* so = reinterpret_cast<uint8_t*>(lds) + wv * GEMM_OST_BYTES;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = row0 + 64 * rg + 32 * u + lr;
+    const float rs = (rscale && row < n) ? rscale[row] : 1.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint32_t pk[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const f2 z = f2{acc[u][t][4 * g + 2 * e], acc[u][t][4 * g + 2 * e + 1]} * rs;
+          pk[e] = pk_max_i16(ET == 1 ? cvt_pk_h(z.x, z.y) : cvt_pk(z.x, z.y), floor16);
+        }
+        *reinterpret_cast<uint2*>(so + (32 * u + lr) * GEMM_OST_PITCH + 2 * (32 * t + 8 * g + 4 * h)) =
+            make_uint2(pk[0], pk[1]);
+      }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 4
+  for (int it = 0; it < 16; ++it) {
+    const int r = 4 * it + (lane >> 4), ch = lane & 15;
+    const int row = row0 + 64 * rg + r, col = 128 * ng + 8 * ch;
+    const uint4 v = *reinterpret_cast<const uint4*>(so + r * GEMM_OST_PITCH + 16 * ch);
+    if (row < n && col < ldy) *reinterpret_cast<uint4*>(Y + (size_t)row * ldy + col) = v;
+  }
+#else
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int row = row0 + 64 * rg + 32 * u + lr;
@@ -689,6 +771,7 @@ __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
       }
     }
   }
+#endif
 }
 
 // W^T image of the K-chunked kernel: img[c][k] = W[k][c], row stride KPc, zero outside
@@ -714,8 +797,10 @@ template <int KN, int FWD_WAVES = FwdWaves<KN>::value>
 __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
     const uint16_t* __restrict__ dY, int lddy, const uint16_t* __restrict__ Ym, int ldym, float mscale, int N,
     const float* __restrict__ W, int K1, int K2, uint16_t* __restrict__ dX1, int ldx1, uint16_t* __restrict__ dX2,
-    int ldx2, const float* __restrict__ rscale, int n, int kcols, int dx1_f32, const uint16_t* __restrict__ wimg) {
+    int ldx2, const float* __restrict__ rscale, int n, int kcols, int dx1_f32, const uint16_t* __restrict__ wimg,
+    int ost) {
   // dx1_f32: dX1 is fp32 (e.g. the init partial of a following SpMM) instead of bf16;
+  // ost >= 0 (bf16 outputs only): the per-wave output staging tiles in LDS (out_stage);
   // wimg: bf16 LDS image of every k slab ([slabs][kcols][WS], lin_prep_bwd_kernel)
   constexpr int NP = KN * 16;
   constexpr int WS = NP + 8;
@@ -787,6 +872,24 @@ __global__ __launch_bounds__(FWD_WAVES * 64) void lin_bwd_data_kernel(
       for (int s = 0; s < KN; ++s)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(*reinterpret_cast<const uint4*>(arow + 16 * s)),
                                                       by[s], acc, 0, 0, 0);
+      if (ost >= 0) {
+        uint32_t pk[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const f2 z = f2{acc[2 * i], acc[2 * i + 1]} * rs;
+          pk[i] = cvt_pk(z.x, z.y);
+        }
+        const int kt = kb + 32 * t;
+        out_stage(lds, ost, pk, tile, n, [&](int r, int c, uint4 v) {
+          const int k = kt + c;                              // 8 consecutive k, never straddling K1
+          if (k < K1) {
+            if (k < ldx1) *reinterpret_cast<uint4*>(dX1 + (size_t)r * ldx1 + k) = v;
+          } else if (dX2 && k - K1 < ldx2 && k < K1 + ldx2) {
+            *reinterpret_cast<uint4*>(dX2 + (size_t)r * ldx2 + (k - K1)) = v;
+          }
+        });
+        continue;
+      }
       if (!rv) continue;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1234,6 +1337,185 @@ __global__ __launch_bounds__(256) void lin_prep_bwd_kernel(const float* __restri
   img[i] = bf16_bits(k < K && c < N && c < NP ? W[(size_t)k * N + c] : 0.f);
 }
 
+// ============================================================================
+// lin_ws: the weight-stationary form of lin_fwd (BWD = false) and lin_bwd_data (BWD =
+// true) for a reduction of KP = 16 KS <= 256 and at most 256 output columns.  Block =
+// NW waves; wave w owns output columns [32 w, 32 w + 32) and keeps their weight slab
+// in registers (A operand, KS x 16 B per lane, read once from the image).  The block
+// streams 32-row tiles of the streamed operand (X, or dY masked by [Ym > 0]) in whole
+// rows: each wave loads 1/NW of a tile into a ring of R = 3 register tiles (so two tiles
+// stay in flight while one is consumed), writes it to one of two XOR-swizzled LDS slots
+// (chunk c of row r at c ^ (r & 15): the b128 fragment reads of 16 consecutive rows hit
+// 16 distinct bank groups), and every wave reads its B fragments from the slot.  Output
+// tiles are staged in LDS (double-buffered) and stored as whole rows, 16 B per lane.
+// One block barrier per tile.  The slab kernels above keep the rest: fp32 tails, K
+// straddling chunks, fp32 dX1, wider layers.
+// ============================================================================
+template <int KS, int ET, int NW, bool BWD>
+__global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
+    const uint16_t* __restrict__ a1, int lda1, int K1, const uint16_t* __restrict__ a2, int lda2, int K2,
+    const int* __restrict__ idx1, const uint16_t* __restrict__ Ym, int ldym,
+    const uint16_t* __restrict__ wimg, const float* __restrict__ bias, int N, float scale,
+    uint16_t* __restrict__ Y1, int ldy1, int KO1, uint16_t* __restrict__ Y2, int ldy2,
+    int n, int relu, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0,
+    const int* __restrict__ stepp, const float* __restrict__ rscale, float mscale) {
+  // fwd: A = [a1 | a2] (K1 + K2 = reduction, a1 rows gathered through idx1), Y1[row][c]
+  //      for c < ldy1 (N = output columns with weights, c >= N written 0);
+  // bwd: A = a1 = dY (K1 = its N columns) masked by Ym, outputs c < KO1 -> Y1, else Y2.
+  constexpr int KP = KS * 16, CH = KP / 8;               // 16-B chunks per tile row
+  constexpr int SW = CH < 16 ? CH - 1 : 15;               // chunk swizzle mask
+  constexpr int RB = KP * 2;                              // slot row bytes
+  constexpr int SLOT = 32 * RB;
+  constexpr int LPW = (4 * KP + 64 * NW - 1) / (64 * NW); // 16-B loads per lane per tile (ring entry)
+  static_assert(LPW <= 2, "ring entries of at most two loads per lane");
+  constexpr int OP = NW * 64 + 16;                        // out-staging row pitch (bytes)
+  constexpr int OSZ = 32 * OP;
+  constexpr int OPW = 32 * NW * 4 / (64 * NW);            // 16-B output chunks per lane per tile (2)
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* sX = smem;                                     // [2][SLOT]
+  uint8_t* sO = smem + 2 * SLOT;                          // [2][OSZ]
+  if (stepp) step = (uint32_t)*stepp;
+  const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n_tiles = (n + TILE - 1) / TILE;
+  const int G = gridDim.x;
+  const bool bit = drop_bit_mode(thr8);
+  const uint32_t floor16 = relu ? 0u : 0x80008000u;
+
+  // stationary weights and bias
+  uint4 wa[KS];
+  {
+    const uint16_t* wrow = wimg + (size_t)(32 * wv + lr) * (KP + 8) + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) wa[s] = *reinterpret_cast<const uint4*>(wrow + 16 * s);
+  }
+  f32x16 bacc = {};
+  if (!BWD && bias) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int c = 32 * wv + 8 * (q >> 2) + 4 * h + (q & 3);
+      bacc[q] = c < N ? bias[c] * scale : 0.f;
+    }
+  }
+
+  // this lane's share of a tile: chunk q = (wv * LPW + j) * 64 + lane -> row q / CH, chunk q % CH
+  auto load = [&](int tile, uint4 (&gr)[LPW], uint4 (&yr)[LPW]) {
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+      const int q = (wv * LPW + j) * 64 + lane;
+      if (q >= 4 * KP) break;                             // wave-uniform (4 KP % 64 == 0)
+      const int row = min(tile * TILE + q / CH, n - 1), c = q % CH, k = 8 * c;
+      if constexpr (BWD) {
+        const int kk = k < K1 ? k : 0;                    // past N: chunk 0 against zero weights
+        gr[j] = *reinterpret_cast<const uint4*>(a1 + (size_t)row * lda1 + kk);
+        if (Ym) yr[j] = *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + kk);
+      } else {
+        const uint16_t* p1 = a1 + (idx1 ? (size_t)idx1[row] : (size_t)row) * lda1;
+        const int g = k - K1;
+        gr[j] = *reinterpret_cast<const uint4*>(k < K1 ? p1 + k : g < K2 ? a2 + (size_t)row * lda2 + g : p1);
+      }
+    }
+  };
+  auto put = [&](int slot, const uint4 (&gr)[LPW], const uint4 (&yr)[LPW]) {
+#pragma unroll
+    for (int j = 0; j < LPW; ++j) {
+      const int q = (wv * LPW + j) * 64 + lane;
+      if (q >= 4 * KP) break;
+      const int r = q / CH, c = q % CH;
+      uint4 v = gr[j];
+      if (BWD && Ym) {
+        const uint4 y = yr[j];
+        v = make_uint4(pk_mul16(v.x, pk_nz(pk_relu(y.x))), pk_mul16(v.y, pk_nz(pk_relu(y.y))),
+                       pk_mul16(v.z, pk_nz(pk_relu(y.z))), pk_mul16(v.w, pk_nz(pk_relu(y.w))));
+      }
+      *reinterpret_cast<uint4*>(sX + slot * SLOT + r * RB + 16 * (c ^ (r & SW))) = v;
+    }
+  };
+  // products of tile `tile` (slot) -> packed 16-bit outputs in out-staging buffer ob
+  auto compute = [&](int tile, int slot, int ob) {
+    f32x16 acc = bacc;
+    const uint8_t* xr = sX + slot * SLOT + lr * RB;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const uint4 b = *reinterpret_cast<const uint4*>(xr + 16 * ((2 * s + h) ^ (lr & SW)));
+      acc = mma16<ET>(wa[s], b, acc);
+    }
+    const int row = tile * TILE + lr;
+    const bool rv = row < n;
+    float rs = (rv && rscale) ? rscale[row] : 1.f;
+    if (BWD) rs *= mscale;
+    uint32_t pk[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f2 z = f2{acc[2 * i], acc[2 * i + 1]} * rs;
+      pk[i] = ET == 1 ? cvt_pk_h(z.x, z.y) : cvt_pk(z.x, z.y);
+      if (!BWD) pk[i] = pk_max_i16(pk[i], floor16);
+    }
+    if (!BWD && thr8 > 0) {
+      uint32_t gr32 = row0 + (uint32_t)row;
+      asm volatile("" : "+v"(gr32));
+      const uint32_t mw = keep_spread(drop_keep16(drop_draw(gr32, wv, h, step, k0, k1, bit), wv, thr8, bit));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pk[i] = pk_mul16(pk[i], (mw >> (2 * i)) & 0x10001u);
+    }
+    uint8_t* o = sO + ob * OSZ + lr * OP + 64 * wv + 8 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) *reinterpret_cast<uint2*>(o + 16 * g) = make_uint2(pk[2 * g], pk[2 * g + 1]);
+  };
+  auto store = [&](int tile, int ob) {
+#pragma unroll
+    for (int j = 0; j < OPW; ++j) {
+      const int q = (wv * OPW + j) * 64 + lane;
+      const int r = q / (NW * 4), c = 8 * (q % (NW * 4));
+      const int row = tile * TILE + r;
+      const uint4 v = *reinterpret_cast<const uint4*>(sO + ob * OSZ + r * OP + 16 * (q % (NW * 4)));
+      if (row >= n) continue;
+      if (BWD) {
+        if (c < KO1) {
+          if (c < ldy1) *reinterpret_cast<uint4*>(Y1 + (size_t)row * ldy1 + c) = v;
+        } else if (Y2 && c - KO1 < ldy2) {
+          *reinterpret_cast<uint4*>(Y2 + (size_t)row * ldy2 + (c - KO1)) = v;
+        }
+      } else if (c < ldy1) {
+        *reinterpret_cast<uint4*>(Y1 + (size_t)row * ldy1 + c) = v;
+      }
+    }
+  };
+
+  // tile i of this block: blockIdx.x + i * G; ring slot i % 3, LDS slot / out buffer i & 1
+  const int nt = n_tiles > (int)blockIdx.x ? (n_tiles - 1 - (int)blockIdx.x) / G + 1 : 0;
+  auto T = [&](int i) { return (int)blockIdx.x + i * G; };
+  uint4 g0[LPW], g1[LPW], g2[LPW], y0[LPW], y1[LPW], y2[LPW];
+  if (nt > 0) load(T(0), g0, y0);
+  if (nt > 1) load(T(1), g1, y1);
+  if (nt > 2) load(T(2), g2, y2);
+  if (nt > 0) put(0, g0, y0);
+  if (nt > 3) load(T(3), g0, y0);
+  __syncthreads();
+  // iteration i: put tile i + 1, load tile i + 4 into the freed ring entry, compute tile i,
+  // store the outputs of tile i - 1, barrier
+  auto step_i = [&](int i, uint4 (&gn)[LPW], uint4 (&yn)[LPW]) {
+#if LINX_STFIRST
+    if (i > 0) store(T(i - 1), (i - 1) & 1);
+#endif
+    if (i + 1 < nt) put((i + 1) & 1, gn, yn);
+    if (i + 4 < nt) load(T(i + 4), gn, yn);
+    compute(T(i), i & 1, i & 1);
+#if !LINX_STFIRST
+    if (i > 0) store(T(i - 1), (i - 1) & 1);
+#endif
+    __syncthreads();
+  };
+  for (int i = 0; i < nt; i += 3) {
+    step_i(i, g1, y1);                 // tile i + 1 sits in ring entry (i + 1) % 3 = 1
+    if (i + 1 >= nt) break;
+    step_i(i + 1, g2, y2);
+    if (i + 2 >= nt) break;
+    step_i(i + 2, g0, y0);
+  }
+  if (nt > 0) store(T(nt - 1), (nt - 1) & 1);
+}
+
 // ---------------------------------------------------------------- launchers
 static int grid_rows(int n, int waves) {
   const int tiles = (n + TILE - 1) / TILE;
@@ -1245,6 +1527,8 @@ static int pick_ks(int K) {
   for (int c : {4, 8, 16, 24, 32, 40, 48}) if (ks <= c) return c;
   return -1;
 }
+
+constexpr size_t LDS_MAX = 160 * 1024;
 
 // widest slab (multiple of 32 columns) whose bf16 weight image fits the LDS budget
 static int slab_cols(int N, int KP) {
@@ -1272,11 +1556,16 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
     hipLaunchKernelGGL(lin_prep_fwd_kernel<ET>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2,
                        N, ncols, KP, KP + 8, total, scale, wimg);
   }
-  (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS, ET, WV>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  // output staging tiles after the image when they fit beside it (every shape but the widest slabs)
+  const bool tst = LINX_TST && !Yf && lds + (size_t)WV * OST_BYTES <= LDS_MAX;
+  const int ost = tst ? (int)lds : -1;
+  const size_t lds_all = lds + (tst ? (size_t)WV * OST_BYTES : 0);
+  (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS, ET, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_all);
   const int slabs = (std::max(N, ldy) + ncols - 1) / ncols;
-  hipLaunchKernelGGL((lin_fwd_kernel<KS, ET, WV>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
+  hipLaunchKernelGGL((lin_fwd_kernel<KS, ET, WV>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds_all, st,
                      x1, ld1, K1, x2, ld2, K2, W, N, bias, Y, ldy, n, ncols, relu, p, k0, k1, step, thr8, row0,
-                     stepp, rscale, idx1, wimg, Yf, nsplit, tk);
+                     stepp, rscale, idx1, wimg, Yf, nsplit, tk, ost);
   return (int)hipGetLastError();
 }
 
@@ -1303,7 +1592,7 @@ static int kc_launch(const uint16_t* x, int ldx, int K, const float* W, int N, c
                      total, wimg);
   // the 256 x 256 tiled GEMM where it applies, else the kc kernel
   if (FG == 2) {
-    const size_t lds = sizeof(uint16_t) * 2 * (256 + 256) * 64;
+    const size_t lds = std::max(sizeof(uint16_t) * 2 * (256 + 256) * 64, (size_t)(LINX_TST ? 8 * GEMM_OST_BYTES : 0));
     (void)hipFuncSetAttribute((const void*)lin_gemm_kernel<ET>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((lin_gemm_kernel<ET>), dim3((n + 255) / 256), dim3(512), lds, st, x, ldx, K, wimg, KPc, bias, Y,
                        ldy, N, n, relu, rscale);
@@ -1314,6 +1603,50 @@ static int kc_launch(const uint16_t* x, int ldx, int K, const float* W, int N, c
                      x, ldx, K, wimg, KPc, bias, Y, ldy, N, n, relu, rscale);
   return (int)hipGetLastError();
 }
+
+// ---- weight-stationary launches (lin_ws_kernel) ----
+template <int KS, int ET, int NW, bool BWD>
+static int ws_launch(const uint16_t* a1, int lda1, int K1, const uint16_t* a2, int lda2, int K2, const int* idx1,
+                     const uint16_t* Ym, int ldym, const uint16_t* wimg, const float* bias, int N, float scale,
+                     uint16_t* Y1, int ldy1, int KO1, uint16_t* Y2, int ldy2, int n, int relu, uint32_t k0,
+                     uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
+                     float mscale, hipStream_t st) {
+  constexpr int KP = KS * 16;
+  const size_t lds = 2 * 32 * KP * 2 + 2 * 32 * (NW * 64 + 16);
+  auto kern = lin_ws_kernel<KS, ET, NW, BWD>;
+  static int occ = 0;
+  if (!occ) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, NW * 64, lds) != hipSuccess || occ < 1) occ = 1;
+  }
+  const int tiles = (n + TILE - 1) / TILE;
+  const int grid = std::max(1, std::min(tiles, device_cus() * occ));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, a1, lda1, K1, a2, lda2, K2, idx1, Ym, ldym, wimg, bias,
+                     N, scale, Y1, ldy1, KO1, Y2, ldy2, n, relu, k0, k1, step, thr8, row0, stepp, rscale, mscale);
+  return (int)hipGetLastError();
+}
+
+// waves of the weight-stationary form for `cols` output columns (0: not covered)
+// (the fewest of 2 / 4 / 8 covering the columns whose ring entries stay at <= 2 loads per
+// lane: a narrow layer on a long reduction takes more waves than columns, the extra
+// ones computing zero-weight columns that are never stored)
+static int ws_waves(int KS, int cols) {
+  if (KS > 16 || cols > 256) return 0;
+  for (int nw : {2, 4, 8})
+    if (32 * nw >= cols && (KS + nw - 1) / nw <= 2) return nw;
+  return 0;
+}
+
+#define WS_DISPATCH(KSV, BWDV, ETV, ...)                                                            \
+  switch (KSV * 100 + nw) {                                                                         \
+    case 402: return ws_launch<4, ETV, 2, BWDV>(__VA_ARGS__);                                      \
+    case 404: return ws_launch<4, ETV, 4, BWDV>(__VA_ARGS__);                                      \
+    case 408: return ws_launch<4, ETV, 8, BWDV>(__VA_ARGS__);                                      \
+    case 804: return ws_launch<8, ETV, 4, BWDV>(__VA_ARGS__);                                      \
+    case 808: return ws_launch<8, ETV, 8, BWDV>(__VA_ARGS__);                                      \
+    case 1608: return ws_launch<16, ETV, 8, BWDV>(__VA_ARGS__);                                    \
+    default: break;                                                                                 \
+  }
 
 // et: element type of X / Y (0 bf16, 1 fp16: the inference path; fp16 takes K <= 768,
 // no dropout or fp32 tail)
@@ -1339,6 +1672,27 @@ extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x
                      : kc_launch<1, 1>(a, ld1, K1, W, N, bias, y, ldy, n, relu, rscale, w, st);
     return fg == 2 ? kc_launch<2, 0>(a, ld1, K1, W, N, bias, y, ldy, n, relu, rscale, w, st)
                    : kc_launch<1, 0>(a, ld1, K1, W, N, bias, y, ldy, n, relu, rscale, w, st);
+  }
+  {
+    const int nw = LINX_WS && !Yf && !(K1 & 7) && !(K2 & 7) ? ws_waves(ks, std::max(N, ldy)) : 0;
+    if (nw) {
+      const int KP = ks * 16, cols = nw * 32;
+      const long total = (long)cols * (KP + 8);
+      const float scale = thr8 > 0 ? 1.f / (1.f - p) : 1.f;
+      auto w = (uint16_t*)wimg;
+      if (et == 1) {
+        if (thr8) return -3;
+        hipLaunchKernelGGL(lin_prep_fwd_kernel<1>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2,
+                           N, cols, KP, KP + 8, total, scale, w);
+        WS_DISPATCH(ks, false, 1, a, ld1, K1, b, ld2, K2, idx1, nullptr, 0, w, bias, N, scale, y, ldy, 0, nullptr, 0, n,
+                    relu, k0, k1, step, thr8, row0, stepp, rscale, 1.f, st)
+      } else {
+        hipLaunchKernelGGL(lin_prep_fwd_kernel<0>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2,
+                           N, cols, KP, KP + 8, total, scale, w);
+        WS_DISPATCH(ks, false, 0, a, ld1, K1, b, ld2, K2, idx1, nullptr, 0, w, bias, N, scale, y, ldy, 0, nullptr, 0, n,
+                    relu, k0, k1, step, thr8, row0, stepp, rscale, 1.f, st)
+      }
+    }
   }
   if (et == 1) {
     if (thr8 || Yf) return -3;
@@ -1367,11 +1721,15 @@ static int bwd_data_launch(const uint16_t* dY, int lddy, const uint16_t* Ym, int
                        NP + 8, total, wimg);
   }
   constexpr int WV = KN == 16 ? BWD16_WAVES : FwdWaves<KN>::value;
+  const bool tst = LINX_TST && !dx1_f32 && lds + (size_t)WV * OST_BYTES <= LDS_MAX;
+  const int ost = tst ? (int)lds : -1;
+  const size_t lds_all = lds + (tst ? (size_t)WV * OST_BYTES : 0);
   (void)hipFuncSetAttribute((const void*)lin_bwd_data_kernel<KN, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds);
+                            (int)lds_all);
   const int slabs = (K + kcols - 1) / kcols;
-  hipLaunchKernelGGL((lin_bwd_data_kernel<KN, WV>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds, st,
-                     dY, lddy, Ym, ldym, mscale, N, W, K1, K2, dX1, ldx1, dX2, ldx2, rscale, n, kcols, dx1_f32, wimg);
+  hipLaunchKernelGGL((lin_bwd_data_kernel<KN, WV>), dim3(grid_rows(n, WV), slabs), dim3(WV * 64), lds_all, st,
+                     dY, lddy, Ym, ldym, mscale, N, W, K1, K2, dX1, ldx1, dX2, ldx2, rscale, n, kcols, dx1_f32, wimg,
+                     ost);
   return (int)hipGetLastError();
 }
 
@@ -1386,6 +1744,17 @@ extern "C" int gnn_launch_lin_bwd_data(const void* dY, int lddy, const void* Ym,
   auto m = (const uint16_t*)Ym;
   auto o1 = (uint16_t*)dX1;
   auto o2 = (uint16_t*)dX2;
+  {
+    const int nw = LINX_WS && !dx1_f32 && !(N & 7) ? ws_waves(kn, K1 + K2) : 0;
+    if (nw) {
+      const int NP = kn * 16, rows = nw * 32;
+      const long total = (long)rows * (NP + 8);
+      hipLaunchKernelGGL(lin_prep_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2, N,
+                         NP, NP + 8, total, (uint16_t*)wimg);
+      WS_DISPATCH(kn, true, 0, d, lddy, N, nullptr, 0, 0, nullptr, m, ldym, (const uint16_t*)wimg, nullptr, N, 1.f, o1,
+                  ldx1, K1, o2, ldx2, n, 0, 0u, 0u, 0u, 0u, 0u, nullptr, rscale, mscale, st)
+    }
+  }
 #define LB(c) if (kn == c) return bwd_data_launch<c>(d, lddy, m, ldym, mscale, N, W, K1, K2, o1, ldx1, o2, ldx2, rscale, n, dx1_f32, (uint16_t*)wimg, st);
   LB(4) LB(8) LB(16) LB(24) LB(32)
 #undef LB

@@ -24,6 +24,9 @@ def _close(a, b, rtol, atol):
     (4133, 256, 256, 40, 40, False, 0.0, False),     # last layer to 40 classes (arxiv)
     (777, 47, 48, 256, 264, True, 0.0, True),        # odd K, padded output pitch
     (3, 128, 128, 96, 96, True, 0.3, False),         # fewer rows than one tile
+    (6000, 256, 256, 256, 256, True, 0.5, True),     # arxiv hidden layer: weight-stationary form, bit-mode dropout
+    (2000, 64, 64, 128, 128, True, 0.5, False),      # weight-stationary, 4 waves, a tile chunk per lane
+    (1000, 128, 128, 40, 40, False, 0.0, True),      # narrow output on 8 waves (zero-weight columns unstored)
 ])
 def test_lin_fwd_matches_reference(n, K, ld, N, ldy, relu, p, rs):
     g = torch.Generator().manual_seed(n)
@@ -70,6 +73,23 @@ def test_lin_fwd_k_chunked_matches_reference(n, K, ld, N, ldy, dt):
     assert torch.all(out.cpu()[:, N:] == 0)
 
 
+def test_lin_fwd_gathered_concatenation_matches_reference():
+    """[x1[idx] | x2] on the weight-stationary form (SAGE-style layer, K = 64 + 64)."""
+    g = torch.Generator().manual_seed(5)
+    n, table, K, N = 3001, 9000, 64, 256
+    x1, x2 = _bf(table, K, K, g), _bf(n, K, K, g)
+    idx = torch.randint(0, table, (n,), generator=g, dtype=torch.int32)
+    W = torch.randn(2 * K, N, generator=g) / 11
+    b = torch.randn(N, generator=g) * 0.1
+    step = torch.tensor([3], dtype=torch.int32)
+    ref = lin_fwd(x1, W, b, x2=x2, K1=K, K2=K, relu=True, p=0.5, key=(5, 6), step=3, idx1=idx, n=n)
+    out = lin_fwd(x1.to(DEV), W.to(DEV), b.to(DEV), x2=x2.to(DEV), K1=K, K2=K, relu=True, p=0.5, key=(5, 6),
+                  step=step.to(DEV), idx1=idx.to(DEV), n=n)
+    torch.cuda.synchronize()
+    _close(out, ref, 2e-2, 2e-2)
+    assert (out.cpu() == 0).ne(ref == 0).float().mean() < 1e-3
+
+
 def test_lin_fwd_two_inputs_is_the_concatenation():
     g = torch.Generator().manual_seed(1)
     n, K1, K2, N = 3000, 256, 256, 256
@@ -85,6 +105,8 @@ def test_lin_fwd_two_inputs_is_the_concatenation():
 
 @pytest.mark.parametrize("n,N,K1,K2,mask,ms,rs", [
     (5000, 256, 100, 0, True, 2.0, True),
+    (3000, 128, 64, 64, True, 2.0, False),            # weight-stationary form with both outputs
+    (777, 40, 256, 0, False, 1.0, True),              # the arxiv last layer's backward (N = 40)
     (3001, 256, 256, 256, True, 1.0, False),
     (700, 47, 256, 0, False, 1.0, True),
 ])
