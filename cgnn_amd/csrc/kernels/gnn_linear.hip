@@ -54,23 +54,9 @@ constexpr int TILE = 32;
 template <int KS> struct FwdWaves { static constexpr int value = KS <= 16 ? 16 : 8; };
 constexpr int WGT_WAVES = 8;        // weight-gradient blocks
 constexpr bool BWD_DATA_SEL = true;   // lin_bwd_data: branch-free gradient loader
-#ifndef LINX_TST
-#define LINX_TST 1
-#endif
-#ifndef LINX_WS
-#define LINX_WS 1
-#endif
-#ifndef LINX_STFIRST
-#define LINX_STFIRST 0
-#endif
-#ifndef LINX_F8W
-#define LINX_F8W 8
-#endif
-#ifndef LINX_F16W
-#define LINX_F16W 8
-#endif
-constexpr int FWD8_WAVES = LINX_F8W;        // lin_fwd KS = 8: waves per block
-constexpr int FWD16_WAVES = LINX_F16W;        // lin_fwd KS = 16: waves per block (profiles/r03_waves)
+constexpr int WS_RING = 3;             // lin_ws: register ring depth (tiles in flight; 5 measured no faster)
+constexpr int FWD8_WAVES = 8;         // lin_fwd KS = 8: waves per block (prefetching 8-wave blocks, profiles/r04_lin)
+constexpr int FWD16_WAVES = 8;        // lin_fwd KS = 16: waves per block (profiles/r03_waves)
 constexpr int BWD16_WAVES = 8;        // lin_bwd_data KN = 16: waves per block (profiles/r03_waves)
 constexpr int FWD_SEL_KS = 8;         // lin_fwd: branch-free X loader from this many k-steps up
 constexpr int TR = TILE + 8;        // transposed image row: 32 rows + pad (80 B)
@@ -308,11 +294,7 @@ __device__ __forceinline__ void out_stage(uint16_t* lds, int ost, const uint32_t
 }
 
 __device__ __forceinline__ void st_y8(uint16_t* p, uint32_t a, uint32_t b) {
-#ifdef LINX_NT
-  __builtin_nontemporal_store(((unsigned long long)b << 32) | a, reinterpret_cast<unsigned long long*>(p));
-#else
   *reinterpret_cast<uint2*>(p) = make_uint2(a, b);
-#endif
 }
 
 template <int KS, int ET = 0, int FWD_WAVES = FwdWaves<KS>::value>
@@ -714,7 +696,6 @@ __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
   }
   // epilogue: lane = row, registers 4g..4g+3 = columns 128 ng + 32 t + 8 g + 4 h + 0..3
   const uint32_t floor16 = relu ? 0u : 0x80008000u;
-#if LINX_TST
   // packed 16-bit values staged through the (now free) LDS as the wave's 64-row x
   // 128-column block, then stored as whole 256-B row pieces (16 lanes per row): a store
   // instruction of the transposed layout writes 32 rows x 16 B, every piece its own
@@ -748,30 +729,6 @@ __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
     const uint4 v = *reinterpret_cast<const uint4*>(so + r * GEMM_OST_PITCH + 16 * ch);
     if (row < n && col < ldy) *reinterpret_cast<uint4*>(Y + (size_t)row * ldy + col) = v;
   }
-#else
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int row = row0 + 64 * rg + 32 * u + lr;
-    if (row >= n) continue;
-    const float rs = rscale ? rscale[row] : 1.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int col = 128 * ng + 32 * t + 8 * g + 4 * h;
-        if (col >= ldy) continue;
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float y = acc[u][t][4 * g + e];
-          if (relu) y = fmaxf(y, 0.f);
-          v[e] = y * rs;
-        }
-        *reinterpret_cast<uint2*>(Y + (size_t)row * ldy + col) = pack4e<ET>(v[0], v[1], v[2], v[3]);
-      }
-    }
-  }
-#endif
 }
 
 // W^T image of the K-chunked kernel: img[c][k] = W[k][c], row stride KPc, zero outside
@@ -1351,6 +1308,8 @@ __global__ __launch_bounds__(256) void lin_prep_bwd_kernel(const float* __restri
 // One block barrier per tile.  The slab kernels above keep the rest: fp32 tails, K
 // straddling chunks, fp32 dX1, wider layers.
 // ============================================================================
+constexpr int WS_IDX_TILES = 64;     // tiles per block whose row ids / row scales fit their LDS stage
+
 template <int KS, int ET, int NW, bool BWD>
 __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
     const uint16_t* __restrict__ a1, int lda1, int K1, const uint16_t* __restrict__ a2, int lda2, int K2,
@@ -1374,6 +1333,9 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* sX = smem;                                     // [2][SLOT]
   uint8_t* sO = smem + 2 * SLOT;                          // [2][OSZ]
+  u32x4* sD = reinterpret_cast<u32x4*>(smem + 2 * SLOT + 2 * OSZ);   // [2][64] bit-mode draws
+  int* sIdx = reinterpret_cast<int*>(smem + 2 * SLOT + 2 * OSZ + (BWD ? 0 : 2 * 64 * 16));   // [nt][32] gathered ids
+  float* sRs = reinterpret_cast<float*>(sIdx + (BWD ? 0 : WS_IDX_TILES * TILE));             // [nt][32] row scales
   if (stepp) step = (uint32_t)*stepp;
   const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1388,6 +1350,11 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
     const uint16_t* wrow = wimg + (size_t)(32 * wv + lr) * (KP + 8) + 8 * h;
 #pragma unroll
     for (int s = 0; s < KS; ++s) wa[s] = *reinterpret_cast<const uint4*>(wrow + 16 * s);
+    // consumed here (an empty asm reading them), so they are complete before the loop: the
+    // wait-count pass would otherwise keep counting them behind every ring load, and each
+    // MFMA would wait for nearly every load in flight
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(wa[s].x), "v"(wa[s].y), "v"(wa[s].z), "v"(wa[s].w));
   }
   f32x16 bacc = {};
   if (!BWD && bias) {
@@ -1399,20 +1366,28 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
   }
 
   // this lane's share of a tile: chunk q = (wv * LPW + j) * 64 + lane -> row q / CH, chunk q % CH
+  // (unconditional loads -- a1 in place of a missing mask: a conditional load into a ring
+  // register costs a copy and with it a vmcnt(0), i.e. every older ring load)
   auto load = [&](int tile, uint4 (&gr)[LPW], uint4 (&yr)[LPW]) {
 #pragma unroll
     for (int j = 0; j < LPW; ++j) {
-      const int q = (wv * LPW + j) * 64 + lane;
-      if (q >= 4 * KP) break;                             // wave-uniform (4 KP % 64 == 0)
+      // (waves past the tile's chunks re-load one of them, unused: no branch around a load)
+      const int q = ((wv * LPW + j) * 64 + lane) % (4 * KP);
       const int row = min(tile * TILE + q / CH, n - 1), c = q % CH, k = 8 * c;
       if constexpr (BWD) {
         const int kk = k < K1 ? k : 0;                    // past N: chunk 0 against zero weights
         gr[j] = *reinterpret_cast<const uint4*>(a1 + (size_t)row * lda1 + kk);
-        if (Ym) yr[j] = *reinterpret_cast<const uint4*>(Ym + (size_t)row * ldym + kk);
+        yr[j] = *reinterpret_cast<const uint4*>(Ym ? Ym + (size_t)row * ldym + kk : a1 + (size_t)row * lda1 + kk);
       } else {
-        const uint16_t* p1 = a1 + (idx1 ? (size_t)idx1[row] : (size_t)row) * lda1;
+        // gathered rows: their ids were staged in LDS up front (a global id load here would
+        // need a vmcnt(0) -- every older ring load -- before its address is known)
+        const int r1 = idx1 ? sIdx[(tile - (int)blockIdx.x) / G * TILE + q / CH] : row;
+        const uint16_t* p1 = a1 + (size_t)r1 * lda1;
+        const uint16_t* p2 = a2 + (size_t)row * lda2;
         const int g = k - K1;
-        gr[j] = *reinterpret_cast<const uint4*>(k < K1 ? p1 + k : g < K2 ? a2 + (size_t)row * lda2 + g : p1);
+        const uint16_t* src = k < K1 ? p1 + k : p1;
+        src = (k >= K1 && g < K2) ? p2 + g : src;
+        gr[j] = *reinterpret_cast<const uint4*>(src);
       }
     }
   };
@@ -1420,7 +1395,7 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
 #pragma unroll
     for (int j = 0; j < LPW; ++j) {
       const int q = (wv * LPW + j) * 64 + lane;
-      if (q >= 4 * KP) break;
+      if (4 * KP % (64 * NW) != 0 && q >= 4 * KP) break;
       const int r = q / CH, c = q % CH;
       uint4 v = gr[j];
       if (BWD && Ym) {
@@ -1432,7 +1407,7 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
     }
   };
   // products of tile `tile` (slot) -> packed 16-bit outputs in out-staging buffer ob
-  auto compute = [&](int tile, int slot, int ob) {
+  auto compute = [&](int tile, int slot, int ob, int i) {
     f32x16 acc = bacc;
     const uint8_t* xr = sX + slot * SLOT + lr * RB;
 #pragma unroll
@@ -1442,7 +1417,7 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
     }
     const int row = tile * TILE + lr;
     const bool rv = row < n;
-    float rs = (rv && rscale) ? rscale[row] : 1.f;
+    float rs = rscale ? sRs[i * TILE + lr] : 1.f;
     if (BWD) rs *= mscale;
     uint32_t pk[8];
 #pragma unroll
@@ -1452,9 +1427,15 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
       if (!BWD) pk[i] = pk_max_i16(pk[i], floor16);
     }
     if (!BWD && thr8 > 0) {
-      uint32_t gr32 = row0 + (uint32_t)row;
-      asm volatile("" : "+v"(gr32));
-      const uint32_t mw = keep_spread(drop_keep16(drop_draw(gr32, wv, h, step, k0, k1, bit), wv, thr8, bit));
+      u32x4 r;
+      if (bit) {
+        r = sD[(slot & 1) * 64 + lane];                   // one draw per (row, half) serves all 8 waves
+      } else {
+        uint32_t gr32 = row0 + (uint32_t)row;
+        asm volatile("" : "+v"(gr32));
+        r = drop_draw(gr32, wv, h, step, k0, k1, false);
+      }
+      const uint32_t mw = keep_spread(drop_keep16(r, wv, thr8, bit));
 #pragma unroll
       for (int i = 0; i < 8; ++i) pk[i] = pk_mul16(pk[i], (mw >> (2 * i)) & 0x10001u);
     }
@@ -1482,38 +1463,62 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
     }
   };
 
-  // tile i of this block: blockIdx.x + i * G; ring slot i % 3, LDS slot / out buffer i & 1
+  // tile i of this block: blockIdx.x + i * G; ring entry i % R, LDS slot / out buffer i & 1
+  constexpr int R = WS_RING;
   const int nt = n_tiles > (int)blockIdx.x ? (n_tiles - 1 - (int)blockIdx.x) / G + 1 : 0;
   auto T = [&](int i) { return (int)blockIdx.x + i * G; };
-  uint4 g0[LPW], g1[LPW], g2[LPW], y0[LPW], y1[LPW], y2[LPW];
-  if (nt > 0) load(T(0), g0, y0);
-  if (nt > 1) load(T(1), g1, y1);
-  if (nt > 2) load(T(2), g2, y2);
-  if (nt > 0) put(0, g0, y0);
-  if (nt > 3) load(T(3), g0, y0);
-  __syncthreads();
-  // iteration i: put tile i + 1, load tile i + 4 into the freed ring entry, compute tile i,
-  // store the outputs of tile i - 1, barrier
-  auto step_i = [&](int i, uint4 (&gn)[LPW], uint4 (&yn)[LPW]) {
-#if LINX_STFIRST
-    if (i > 0) store(T(i - 1), (i - 1) & 1);
-#endif
-    if (i + 1 < nt) put((i + 1) & 1, gn, yn);
-    if (i + 4 < nt) load(T(i + 4), gn, yn);
-    compute(T(i), i & 1, i & 1);
-#if !LINX_STFIRST
-    if (i > 0) store(T(i - 1), (i - 1) & 1);
-#endif
+  // gathered row ids and row scales of the block's tiles, staged once (a global load inside
+  // the loop whose value is used at once would wait for every older ring load)
+  if ((!BWD && idx1) || rscale) {
+    for (int e = threadIdx.x; e < nt * TILE; e += NW * 64) {
+      const int row = min(T(e / TILE) * TILE + e % TILE, n - 1);
+      if (!BWD && idx1) sIdx[e] = idx1[row];
+      if (rscale) sRs[e] = rscale[row];
+    }
     __syncthreads();
-  };
-  for (int i = 0; i < nt; i += 3) {
-    step_i(i, g1, y1);                 // tile i + 1 sits in ring entry (i + 1) % 3 = 1
-    if (i + 1 >= nt) break;
-    step_i(i + 1, g2, y2);
-    if (i + 2 >= nt) break;
-    step_i(i + 2, g0, y0);
   }
-  if (nt > 0) store(T(nt - 1), (nt - 1) & 1);
+  // ring loads past the block's last tile re-read that tile (an L2 hit; no branch around the
+  // loads: a conditional load into a ring register costs a copy and with it a vmcnt(0))
+  auto TL = [&](int i) { return T(min(i, nt - 1)); };
+  uint4 gq[R][LPW], yq[R][LPW];
+  if (nt > 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) load(TL(r), gq[r], yq[r]);
+  }
+  // bit-mode dropout: the 64 draws (32 rows x 2 halves) of tile i are made once, by wave
+  // (i - 1) % NW during iteration i - 1, into draw buffer i & 1
+  auto draws = [&](int i) {
+    if (BWD || !bit || i >= nt || wv != (i + NW - 1) % NW) return;
+    uint32_t gr32 = row0 + (uint32_t)(T(i) * TILE + lr);
+    asm volatile("" : "+v"(gr32));
+    sD[(i & 1) * 64 + lane] = drop_draw(gr32, 0, h, step, k0, k1, true);
+  };
+  if (nt > 0) {
+    put(0, gq[0], yq[0]);
+    load(TL(R), gq[0], yq[0]);
+  }
+  if (!BWD && bit && thr8 > 0 && wv == 0 && nt > 0) {
+    uint32_t gr32 = row0 + (uint32_t)(T(0) * TILE + lr);
+    sD[lane] = drop_draw(gr32, 0, h, step, k0, k1, true);
+  }
+  __syncthreads();
+  // iteration i: put tile i + 1 (ring entry (i + 1) % R), load tile i + 1 + R into it,
+  // compute tile i, store the outputs of tile i - 1, barrier
+  // groups of R iterations without exits (the iterations past nt compute nothing): a
+  // loop body the wait-count pass can follow, so the ring loads stay in flight across it
+  for (int i0 = 0; i0 < nt; i0 += R) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = i0 + r;
+      put((i + 1) & 1, gq[(r + 1) % R], yq[(r + 1) % R]);     // past the end: a slot nobody reads
+      load(TL(i + 1 + R), gq[(r + 1) % R], yq[(r + 1) % R]);
+      if (thr8 > 0) draws(i + 1);
+      if (i < nt) compute(T(i), i & 1, i & 1, i);
+      if (i > 0 && i <= nt) store(T(i - 1), (i - 1) & 1);
+      __syncthreads();
+    }
+  }
+  if (nt > 0 && nt % R == 0) store(T(nt - 1), (nt - 1) & 1);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -1557,7 +1562,7 @@ static int fwd_launch(const uint16_t* x1, int ld1, int K1, const uint16_t* x2, i
                        N, ncols, KP, KP + 8, total, scale, wimg);
   }
   // output staging tiles after the image when they fit beside it (every shape but the widest slabs)
-  const bool tst = LINX_TST && !Yf && lds + (size_t)WV * OST_BYTES <= LDS_MAX;
+  const bool tst = !Yf && lds + (size_t)WV * OST_BYTES <= LDS_MAX;
   const int ost = tst ? (int)lds : -1;
   const size_t lds_all = lds + (tst ? (size_t)WV * OST_BYTES : 0);
   (void)hipFuncSetAttribute((const void*)lin_fwd_kernel<KS, ET, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1592,7 +1597,7 @@ static int kc_launch(const uint16_t* x, int ldx, int K, const float* W, int N, c
                      total, wimg);
   // the 256 x 256 tiled GEMM where it applies, else the kc kernel
   if (FG == 2) {
-    const size_t lds = std::max(sizeof(uint16_t) * 2 * (256 + 256) * 64, (size_t)(LINX_TST ? 8 * GEMM_OST_BYTES : 0));
+    const size_t lds = std::max(sizeof(uint16_t) * 2 * (256 + 256) * 64, (size_t)8 * GEMM_OST_BYTES);
     (void)hipFuncSetAttribute((const void*)lin_gemm_kernel<ET>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((lin_gemm_kernel<ET>), dim3((n + 255) / 256), dim3(512), lds, st, x, ldx, K, wimg, KPc, bias, Y,
                        ldy, N, n, relu, rscale);
@@ -1612,7 +1617,8 @@ static int ws_launch(const uint16_t* a1, int lda1, int K1, const uint16_t* a2, i
                      uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
                      float mscale, hipStream_t st) {
   constexpr int KP = KS * 16;
-  const size_t lds = 2 * 32 * KP * 2 + 2 * 32 * (NW * 64 + 16);
+  const size_t lds = 2 * 32 * KP * 2 + 2 * 32 * (NW * 64 + 16) + (BWD ? 0 : 2 * 64 * 16 + WS_IDX_TILES * 32 * 4) +
+                     WS_IDX_TILES * 32 * 4;
   auto kern = lin_ws_kernel<KS, ET, NW, BWD>;
   static int occ = 0;
   if (!occ) {
@@ -1621,6 +1627,7 @@ static int ws_launch(const uint16_t* a1, int lda1, int K1, const uint16_t* a2, i
   }
   const int tiles = (n + TILE - 1) / TILE;
   const int grid = std::max(1, std::min(tiles, device_cus() * occ));
+  if ((idx1 || rscale) && (tiles + grid - 1) / grid > WS_IDX_TILES) return -4;   // row ids / scales do not fit
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, a1, lda1, K1, a2, lda2, K2, idx1, Ym, ldym, wimg, bias,
                      N, scale, Y1, ldy1, KO1, Y2, ldy2, n, relu, k0, k1, step, thr8, row0, stepp, rscale, mscale);
   return (int)hipGetLastError();
@@ -1638,14 +1645,18 @@ static int ws_waves(int KS, int cols) {
 }
 
 #define WS_DISPATCH(KSV, BWDV, ETV, ...)                                                            \
-  switch (KSV * 100 + nw) {                                                                         \
-    case 402: return ws_launch<4, ETV, 2, BWDV>(__VA_ARGS__);                                      \
-    case 404: return ws_launch<4, ETV, 4, BWDV>(__VA_ARGS__);                                      \
-    case 408: return ws_launch<4, ETV, 8, BWDV>(__VA_ARGS__);                                      \
-    case 804: return ws_launch<8, ETV, 4, BWDV>(__VA_ARGS__);                                      \
-    case 808: return ws_launch<8, ETV, 8, BWDV>(__VA_ARGS__);                                      \
-    case 1608: return ws_launch<16, ETV, 8, BWDV>(__VA_ARGS__);                                    \
-    default: break;                                                                                 \
+  {                                                                                                 \
+    int rc_ = -4;                                                                                   \
+    switch (KSV * 100 + nw) {                                                                       \
+      case 402: rc_ = ws_launch<4, ETV, 2, BWDV>(__VA_ARGS__); break;                               \
+      case 404: rc_ = ws_launch<4, ETV, 4, BWDV>(__VA_ARGS__); break;                               \
+      case 408: rc_ = ws_launch<4, ETV, 8, BWDV>(__VA_ARGS__); break;                               \
+      case 804: rc_ = ws_launch<8, ETV, 4, BWDV>(__VA_ARGS__); break;                               \
+      case 808: rc_ = ws_launch<8, ETV, 8, BWDV>(__VA_ARGS__); break;                               \
+      case 1608: rc_ = ws_launch<16, ETV, 8, BWDV>(__VA_ARGS__); break;                             \
+      default: break;                                                                               \
+    }                                                                                               \
+    if (rc_ != -4) return rc_;   /* -4: not this form (the slab kernel follows) */                   \
   }
 
 // et: element type of X / Y (0 bf16, 1 fp16: the inference path; fp16 takes K <= 768,
@@ -1674,7 +1685,7 @@ extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x
                    : kc_launch<1, 0>(a, ld1, K1, W, N, bias, y, ldy, n, relu, rscale, w, st);
   }
   {
-    const int nw = LINX_WS && !Yf && !(K1 & 7) && !(K2 & 7) ? ws_waves(ks, std::max(N, ldy)) : 0;
+    const int nw = !Yf && !(K1 & 7) && !(K2 & 7) ? ws_waves(ks, std::max(N, ldy)) : 0;
     if (nw) {
       const int KP = ks * 16, cols = nw * 32;
       const long total = (long)cols * (KP + 8);
@@ -1721,7 +1732,7 @@ static int bwd_data_launch(const uint16_t* dY, int lddy, const uint16_t* Ym, int
                        NP + 8, total, wimg);
   }
   constexpr int WV = KN == 16 ? BWD16_WAVES : FwdWaves<KN>::value;
-  const bool tst = LINX_TST && !dx1_f32 && lds + (size_t)WV * OST_BYTES <= LDS_MAX;
+  const bool tst = !dx1_f32 && lds + (size_t)WV * OST_BYTES <= LDS_MAX;
   const int ost = tst ? (int)lds : -1;
   const size_t lds_all = lds + (tst ? (size_t)WV * OST_BYTES : 0);
   (void)hipFuncSetAttribute((const void*)lin_bwd_data_kernel<KN, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1745,7 +1756,7 @@ extern "C" int gnn_launch_lin_bwd_data(const void* dY, int lddy, const void* Ym,
   auto o1 = (uint16_t*)dX1;
   auto o2 = (uint16_t*)dX2;
   {
-    const int nw = LINX_WS && !dx1_f32 && !(N & 7) ? ws_waves(kn, K1 + K2) : 0;
+    const int nw = !dx1_f32 && !(N & 7) ? ws_waves(kn, K1 + K2) : 0;
     if (nw) {
       const int NP = kn * 16, rows = nw * 32;
       const long total = (long)rows * (NP + 8);
