@@ -163,7 +163,11 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
   // its start (and keep the per-lane "load or zero" form, which needs fewer registers)
   constexpr bool HOIST = DROP == 2 && KS <= 7;
   bf16x8 bx[KS];
+  // the row's D^-1/2 is loaded with its rows: loaded at the Z2 stores it was the newest
+  // load, and waiting for it meant waiting for the next tile's rows (the prefetch) too
+  float dsv = 0.f;
   auto load_rows = [&](int tl) {
+    dsv = dinv[min(tl * TILE + lr, n - 1)];
     if constexpr (HOIST) {
       const uint16_t* rp = AX + (size_t)min(tl * TILE + lr, n - 1) * ldx;
 #pragma unroll
@@ -178,11 +182,23 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
       }
     }
   };
-  if (HOIST && wave < n_tiles) load_rows(wave);
+  if (HOIST && wave < n_tiles) {
+    load_rows(wave);
+    // the first tile's rows consumed here (empty asm): with loads still pending on the
+    // loop's entry edge the wait-count pass merged it into a vmcnt(0) at every tile start,
+    // which also drained the previous tile's Z2 / keep-image stores
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const uint4 u = __builtin_bit_cast(uint4, bx[s]);
+      asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w));
+    }
+    asm volatile("" ::"v"(dsv));
+  }
   for (int tile = wave; tile < n_tiles; tile += n_waves) {
     const int row = tile * TILE + lr;
     const bool rv = row < n;
     if constexpr (!HOIST) load_rows(tile);
+    const float dsc = dsv;                    // this tile's (the prefetch overwrites dsv)
     f32x16 z0 = {}, z1 = {};
     static_assert(HD <= 256, "bit-mode dropout: one draw covers 8 hidden blocks");
     u32x4 rb{};
@@ -267,7 +283,7 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
       }
     }
     if (rv) {
-      const float ds = dinv[row];
+      const float ds = dsc;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = 8 * g + 4 * h;
@@ -406,6 +422,20 @@ __global__ __launch_bounds__(HD * 2, 1) void gcn_fused_bwd_kernel(
       w2f[s][j] = (__bf16)(c < C ? v : 0.f);
     }
   const f2 bb = {b1[hid], b1[hid]};
+  // the stationary fragments consumed here (empty asm): otherwise the wait-count pass keeps
+  // counting their ~80 loads behind the loop's prefetch loads, and the first use inside the
+  // loop becomes a vmcnt(0) every tile -- draining the prefetch
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const uint4 u = __builtin_bit_cast(uint4, w1f[s]);
+    asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w));
+  }
+#pragma unroll
+  for (int s = 0; s < KC; ++s) {
+    const uint4 u = __builtin_bit_cast(uint4, w2f[s]);
+    asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w));
+  }
+  asm volatile("" ::"v"(bb.x));
   for (int i = tid; i < 2 * 2 * TILE * 128 / 8; i += NT)
     reinterpret_cast<uint4*>(sStg)[i] = make_uint4(0u, 0u, 0u, 0u);
 
