@@ -12,4 +12,4 @@ timeout -k 10 300 python -u tools/bench_gat.py --steps 10 --warmup 2 > $O/gat_pr
 echo "gat $(grep -o '"ms_per_epoch": [0-9.]*' $O/gat_products.log) $(grep -o '"train_loss": [0-9.]*' $O/gat_products.log) $(grep -o '"val_acc": [0-9.]*' $O/gat_products.log)"
 CGNN_L2_ALL_ROWS=1 timeout -k 10 300 python -u tools/bench_gat.py --steps 10 --warmup 2 > $O/gat_products_allrows.log 2>&1 || { echo "gat allrows failed"; exit 1; }
 echo "gat-allrows $(grep -o '"ms_per_epoch": [0-9.]*' $O/gat_products_allrows.log) $(grep -o '"train_loss": [0-9.]*' $O/gat_products_allrows.log) $(grep -o '"val_acc": [0-9.]*' $O/gat_products_allrows.log)"
-bash tools/gpu_r02_ab2.sh
+bash profiles/scripts_r01_r02/gpu_r02_ab2.sh

@@ -12,4 +12,4 @@ for r in 1 2; do
 done
 timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
     python3 bench.py --steps 10 --warmup 3 > $O/trace.log 2>&1 || { echo "rocprof failed"; exit 1; }
-bash tools/gpu_rehearse.sh
+bash profiles/scripts_r01_r02/gpu_rehearse.sh

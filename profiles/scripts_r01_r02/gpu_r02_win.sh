@@ -11,4 +11,4 @@ tail -2 $O/pytest_win.log
 timeout -k 10 300 python -u tools/bench_spmm.py --id-order shuffled --reorder --win 64,128,256 --reps 20 \
     > $O/bench_spmm.log 2>&1 || { echo "bench_spmm failed"; tail -20 $O/bench_spmm.log; exit 1; }
 cat $O/bench_spmm.log
-bash tools/gpu_ab_refine.sh ${REFINE:-0 4}
+bash profiles/scripts_r01_r02/gpu_ab_refine.sh ${REFINE:-0 4}

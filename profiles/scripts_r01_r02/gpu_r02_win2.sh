@@ -10,4 +10,4 @@ timeout -k 10 300 python -u tools/bench_spmm.py --id-order shuffled --reorder --
     > $O/bench_spmm.log 2>&1 || { echo "bench_spmm failed"; tail -20 $O/bench_spmm.log; exit 1; }
 grep -E '"ld": 128' $O/bench_spmm.log
 export CGNN_SPMM_WIN=0
-bash tools/gpu_ab_refine.sh 0 4
+bash profiles/scripts_r01_r02/gpu_ab_refine.sh 0 4
