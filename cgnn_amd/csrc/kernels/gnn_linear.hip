@@ -1314,7 +1314,8 @@ template <int KS, int ET, int NW, bool BWD>
 __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
     const uint16_t* __restrict__ a1, int lda1, int K1, const uint16_t* __restrict__ a2, int lda2, int K2,
     const int* __restrict__ idx1, const uint16_t* __restrict__ Ym, int ldym,
-    const uint16_t* __restrict__ wimg, const float* __restrict__ bias, int N, float scale,
+    const float* __restrict__ W, int WK, int WN, const uint16_t* __restrict__ wimg, const float* __restrict__ bias,
+    int N, float scale,
     uint16_t* __restrict__ Y1, int ldy1, int KO1, uint16_t* __restrict__ Y2, int ldy2,
     int n, int relu, uint32_t k0, uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0,
     const int* __restrict__ stepp, const float* __restrict__ rscale, float mscale) {
@@ -1344,17 +1345,46 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
   const bool bit = drop_bit_mode(thr8);
   const uint32_t floor16 = relu ? 0u : 0x80008000u;
 
-  // stationary weights and bias
+  const int nt = n_tiles > (int)blockIdx.x ? (n_tiles - 1 - (int)blockIdx.x) / G + 1 : 0;
+  auto T = [&](int i) { return (int)blockIdx.x + i * G; };
+  // gathered row ids and row scales of the block's tiles, staged once (a global load inside
+  // the loop whose value is used at once would wait for every older ring load)
+  if ((!BWD && idx1) || rscale) {
+    for (int e = threadIdx.x; e < nt * TILE; e += NW * 64) {
+      const int row = min(T(e / TILE) * TILE + e % TILE, n - 1);
+      if (!BWD && idx1) sIdx[e] = idx1[row];
+      if (rscale) sRs[e] = rscale[row];
+    }
+    __syncthreads();
+  }
+  // ring loads past the block's last tile re-read that tile (an L2 hit; no branch around the
+  // loads: a conditional load into a ring register costs a copy and with it a vmcnt(0))
+  auto TL = [&](int i) { return T(min(i, nt - 1)); };
+  // stationary weights.  fwd: straight from the fp32 master W [WK][WN] (no image kernel):
+  // A[c][k] = W[k][c] * scale (c = 32 wv + lr, k = 16 s + 8 h + j; a column of W, coalesced
+  // across the lanes), zero outside W.  bwd: A[k][c] = W[k][c] from the bf16 image
   uint4 wa[KS];
   {
-    const uint16_t* wrow = wimg + (size_t)(32 * wv + lr) * (KP + 8) + 8 * h;
+    const int wr = 32 * wv + lr;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) wa[s] = *reinterpret_cast<const uint4*>(wrow + 16 * s);
-    // consumed here (an empty asm reading them), so they are complete before the loop: the
-    // wait-count pass would otherwise keep counting them behind every ring load, and each
-    // MFMA would wait for nearly every load in flight
+    for (int s = 0; s < KS; ++s) {
+      float v[8];
+      if constexpr (BWD) {
+        // the bf16 image of W's rows (lin_prep_bwd_kernel, row stride KP + 8): read from the
+        // fp32 master instead (two float4 per k-step and lane) the kernel measured 7 us slower
+        wa[s] = *reinterpret_cast<const uint4*>(wimg + (size_t)wr * (KP + 8) + 16 * s + 8 * h);
+        continue;
+      } else {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(wa[s].x), "v"(wa[s].y), "v"(wa[s].z), "v"(wa[s].w));
+        for (int j = 0; j < 8; ++j) {
+          const int k = 16 * s + 8 * h + j;
+          const float x = W[(size_t)min(k, WK - 1) * WN + min(wr, WN - 1)];
+          v[j] = (k < WK && wr < WN) ? x * scale : 0.f;
+        }
+      }
+      wa[s] = ET == 1 ? make_uint4(cvt_pk_h(v[0], v[1]), cvt_pk_h(v[2], v[3]), cvt_pk_h(v[4], v[5]), cvt_pk_h(v[6], v[7]))
+                      : make_uint4(cvt_pk(v[0], v[1]), cvt_pk(v[2], v[3]), cvt_pk(v[4], v[5]), cvt_pk(v[6], v[7]));
+    }
   }
   f32x16 bacc = {};
   if (!BWD && bias) {
@@ -1465,21 +1495,6 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
 
   // tile i of this block: blockIdx.x + i * G; ring entry i % R, LDS slot / out buffer i & 1
   constexpr int R = WS_RING;
-  const int nt = n_tiles > (int)blockIdx.x ? (n_tiles - 1 - (int)blockIdx.x) / G + 1 : 0;
-  auto T = [&](int i) { return (int)blockIdx.x + i * G; };
-  // gathered row ids and row scales of the block's tiles, staged once (a global load inside
-  // the loop whose value is used at once would wait for every older ring load)
-  if ((!BWD && idx1) || rscale) {
-    for (int e = threadIdx.x; e < nt * TILE; e += NW * 64) {
-      const int row = min(T(e / TILE) * TILE + e % TILE, n - 1);
-      if (!BWD && idx1) sIdx[e] = idx1[row];
-      if (rscale) sRs[e] = rscale[row];
-    }
-    __syncthreads();
-  }
-  // ring loads past the block's last tile re-read that tile (an L2 hit; no branch around the
-  // loads: a conditional load into a ring register costs a copy and with it a vmcnt(0))
-  auto TL = [&](int i) { return T(min(i, nt - 1)); };
   uint4 gq[R][LPW], yq[R][LPW];
   if (nt > 0) {
 #pragma unroll
@@ -1497,6 +1512,11 @@ __global__ __launch_bounds__(NW * 64) void lin_ws_kernel(
     put(0, gq[0], yq[0]);
     load(TL(R), gq[0], yq[0]);
   }
+  // the weights consumed here (an empty asm reading them), behind the first ring loads:
+  // complete before the loop, or the wait-count pass keeps counting them behind every ring
+  // load and each MFMA waits for nearly every load in flight
+#pragma unroll
+  for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(wa[s].x), "v"(wa[s].y), "v"(wa[s].z), "v"(wa[s].w));
   if (!BWD && bit && thr8 > 0 && wv == 0 && nt > 0) {
     uint32_t gr32 = row0 + (uint32_t)(T(0) * TILE + lr);
     sD[lane] = drop_draw(gr32, 0, h, step, k0, k1, true);
@@ -1612,7 +1632,8 @@ static int kc_launch(const uint16_t* x, int ldx, int K, const float* W, int N, c
 // ---- weight-stationary launches (lin_ws_kernel) ----
 template <int KS, int ET, int NW, bool BWD>
 static int ws_launch(const uint16_t* a1, int lda1, int K1, const uint16_t* a2, int lda2, int K2, const int* idx1,
-                     const uint16_t* Ym, int ldym, const uint16_t* wimg, const float* bias, int N, float scale,
+                     const uint16_t* Ym, int ldym, const float* W, int WK, int WN, const uint16_t* wimg, const float* bias,
+                     int N, float scale,
                      uint16_t* Y1, int ldy1, int KO1, uint16_t* Y2, int ldy2, int n, int relu, uint32_t k0,
                      uint32_t k1, uint32_t step, uint32_t thr8, uint32_t row0, const int* stepp, const float* rscale,
                      float mscale, hipStream_t st) {
@@ -1628,7 +1649,7 @@ static int ws_launch(const uint16_t* a1, int lda1, int K1, const uint16_t* a2, i
   const int tiles = (n + TILE - 1) / TILE;
   const int grid = std::max(1, std::min(tiles, device_cus() * occ));
   if ((idx1 || rscale) && (tiles + grid - 1) / grid > WS_IDX_TILES) return -4;   // row ids / scales do not fit
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, a1, lda1, K1, a2, lda2, K2, idx1, Ym, ldym, wimg, bias,
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, st, a1, lda1, K1, a2, lda2, K2, idx1, Ym, ldym, W, WK, WN, wimg, bias,
                      N, scale, Y1, ldy1, KO1, Y2, ldy2, n, relu, k0, k1, step, thr8, row0, stepp, rscale, mscale);
   return (int)hipGetLastError();
 }
@@ -1687,21 +1708,14 @@ extern "C" int gnn_launch_lin_fwd(const void* x1, int ld1, int K1, const void* x
   {
     const int nw = !Yf && !(K1 & 7) && !(K2 & 7) ? ws_waves(ks, std::max(N, ldy)) : 0;
     if (nw) {
-      const int KP = ks * 16, cols = nw * 32;
-      const long total = (long)cols * (KP + 8);
       const float scale = thr8 > 0 ? 1.f / (1.f - p) : 1.f;
-      auto w = (uint16_t*)wimg;
       if (et == 1) {
         if (thr8) return -3;
-        hipLaunchKernelGGL(lin_prep_fwd_kernel<1>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2,
-                           N, cols, KP, KP + 8, total, scale, w);
-        WS_DISPATCH(ks, false, 1, a, ld1, K1, b, ld2, K2, idx1, nullptr, 0, w, bias, N, scale, y, ldy, 0, nullptr, 0, n,
-                    relu, k0, k1, step, thr8, row0, stepp, rscale, 1.f, st)
+        WS_DISPATCH(ks, false, 1, a, ld1, K1, b, ld2, K2, idx1, nullptr, 0, W, K1 + K2, N, nullptr, bias, N, scale, y, ldy, 0,
+                    nullptr, 0, n, relu, k0, k1, step, thr8, row0, stepp, rscale, 1.f, st)
       } else {
-        hipLaunchKernelGGL(lin_prep_fwd_kernel<0>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2,
-                           N, cols, KP, KP + 8, total, scale, w);
-        WS_DISPATCH(ks, false, 0, a, ld1, K1, b, ld2, K2, idx1, nullptr, 0, w, bias, N, scale, y, ldy, 0, nullptr, 0, n,
-                    relu, k0, k1, step, thr8, row0, stepp, rscale, 1.f, st)
+        WS_DISPATCH(ks, false, 0, a, ld1, K1, b, ld2, K2, idx1, nullptr, 0, W, K1 + K2, N, nullptr, bias, N, scale, y, ldy, 0,
+                    nullptr, 0, n, relu, k0, k1, step, thr8, row0, stepp, rscale, 1.f, st)
       }
     }
   }
@@ -1762,7 +1776,8 @@ extern "C" int gnn_launch_lin_bwd_data(const void* dY, int lddy, const void* Ym,
       const long total = (long)rows * (NP + 8);
       hipLaunchKernelGGL(lin_prep_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, W, K1 + K2, N,
                          NP, NP + 8, total, (uint16_t*)wimg);
-      WS_DISPATCH(kn, true, 0, d, lddy, N, nullptr, 0, 0, nullptr, m, ldym, (const uint16_t*)wimg, nullptr, N, 1.f, o1,
+      WS_DISPATCH(kn, true, 0, d, lddy, N, nullptr, 0, 0, nullptr, m, ldym, W, K1 + K2, N, (const uint16_t*)wimg, nullptr,
+                  N, 1.f, o1,
                   ldx1, K1, o2, ldx2, n, 0, 0u, 0u, 0u, 0u, 0u, nullptr, rscale, mscale, st)
     }
   }
