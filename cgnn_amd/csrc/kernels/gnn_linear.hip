@@ -637,25 +637,35 @@ __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
   const int rg = wv & 3, ng = wv >> 2;
   const int row0 = blockIdx.x * BM;
   const int nch = KPc / BK;
-  uint4 xr[4], wr[4];
-  auto load = [&](int c) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = tid + 512 * j, r = i >> 3, ch = i & 7;
-      const int k = BK * c + 8 * ch;
-      const int row = row0 + r;
-      const uint4 v = *reinterpret_cast<const uint4*>(x + (size_t)(row < n ? row : n - 1) * ldx + (k < K ? k : 0));
-      xr[j] = keep_first_sel(v, row < n ? K - k : 0);
-      wr[j] = *reinterpret_cast<const uint4*>(img + (size_t)r * KPc + k);
-    }
+  // the staging registers as named scalars (as arrays captured by the lambdas they were
+  // kept in scratch: 4 x 16 B stored and reloaded per chunk)
+  uint4 xr0, xr1, xr2, xr3, wr0, wr1, wr2, wr3;
+  auto load1 = [&](int c, int j, uint4& xv, uint4& wv) {
+    const int i = tid + 512 * j, r = i >> 3, ch = i & 7;
+    const int k = BK * c + 8 * ch;
+    const int row = row0 + r;
+    // raw: the mask is applied when the chunk is stored, so the loads stay in flight
+    // through the current chunk's MFMAs (masked here, every load was waited for at once)
+    xv = *reinterpret_cast<const uint4*>(x + (size_t)(row < n ? row : n - 1) * ldx + (k < K ? k : 0));
+    wv = *reinterpret_cast<const uint4*>(img + (size_t)r * KPc + k);
   };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = tid + 512 * j, r = i >> 3, ch = i & 7;
-      *reinterpret_cast<uint4*>(sX + buf * BM * BK + gemm_off(r, ch)) = xr[j];
-      *reinterpret_cast<uint4*>(sW + buf * 256 * BK + gemm_off(r, ch)) = wr[j];
-    }
+  auto load = [&](int c) {
+    load1(c, 0, xr0, wr0);
+    load1(c, 1, xr1, wr1);
+    load1(c, 2, xr2, wr2);
+    load1(c, 3, xr3, wr3);
+  };
+  auto store1 = [&](int buf, int c, int j, const uint4& xv, const uint4& wv) {
+    const int i = tid + 512 * j, r = i >> 3, ch = i & 7;
+    const int k = BK * c + 8 * ch;
+    *reinterpret_cast<uint4*>(sX + buf * BM * BK + gemm_off(r, ch)) = keep_first_sel(xv, row0 + r < n ? K - k : 0);
+    *reinterpret_cast<uint4*>(sW + buf * 256 * BK + gemm_off(r, ch)) = wv;
+  };
+  auto store = [&](int buf, int c) {
+    store1(buf, c, 0, xr0, wr0);
+    store1(buf, c, 1, xr1, wr1);
+    store1(buf, c, 2, xr2, wr2);
+    store1(buf, c, 3, xr3, wr3);
   };
   f32x16 acc[2][4];                         // from the bias, as lin_fwd
 #pragma unroll
@@ -670,11 +680,15 @@ __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
     acc[1][t] = b0;
   }
   load(0);
-  store(0);
+  store(0, 0);
   __syncthreads();
   for (int c = 0; c < nch; ++c) {
     const int buf = c & 1;
-    if (c + 1 < nch) load(c + 1);
+    load(min(c + 1, nch - 1));         // unconditional (past the end: a re-load, never stored)
+    // keep the loads here, ahead of the chunk's MFMAs (the compiler sank them to their
+    // LDS stores, which left nothing to overlap their latency)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     const uint16_t* bx = sX + buf * BM * BK;
     const uint16_t* bw = sW + buf * 256 * BK;
 #pragma unroll
@@ -691,7 +705,10 @@ __global__ __launch_bounds__(512, 1) void lin_gemm_kernel(
 #pragma unroll
         for (int u = 0; u < 2; ++u) acc[u][t] = mma16<ET>(wa[t], xb[u], acc[u][t]);
     }
-    if (c + 1 < nch) store(buf ^ 1);   // the other buffer: its last reader finished at the last barrier
+    // the other buffer: its last reader finished at the last barrier.  Unconditional (past
+    // the end: the re-loaded last chunk, never read) -- under an `if` the compiler sank the
+    // loads into it, behind the MFMAs
+    store(buf ^ 1, min(c + 1, nch - 1));
     __syncthreads();
   }
   // epilogue: lane = row, registers 4g..4g+3 = columns 128 ng + 32 t + 8 g + 4 h + 0..3
