@@ -121,8 +121,12 @@ template <int L, int XBF, int U = 4, bool CS = false>
 __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const void* __restrict__ X,
                                            int e0, int e1, int ldx, int f0, bool fv, int sub_base,
                                            int sl, float* acc, const float* __restrict__ cscale = nullptr) {
+  // the next chunk's column ids load while this chunk's rows are gathered (clamped address,
+  // unconditional load: a "load or 0" would branch and wait for it at the join)
+  int nxj = ld_stream(col + max(0, min(e0 + sl, e1 - 1)));
   for (int e = e0; e < e1; e += L) {
-    const int myj = (e + sl < e1) ? ld_stream(col + e + sl) : 0;
+    const int myj = nxj;
+    nxj = ld_stream(col + max(0, min(e + L + sl, e1 - 1)));
     const float mycs = CS ? cscale[myj] : 1.f;
     const int cnt = min(L, e1 - e);
     int k = 0;
