@@ -642,11 +642,12 @@ __global__ void cast_bf16_kernel(const float* __restrict__ src, uint16_t* __rest
 }
 
 // ---------------------------------------------------------------- launchers
-// Gathers unrolled 8 rows deep.  Measured alternatives, kept out: 4 deep (slower on
-// the products shape), and a software-pipelined gather (next chunk's column indices
-// requested early, non-temporal index loads / output stores, 16 raw rows in flight per
-// lane): 30 % SLOWER (F = 100: 3.43 vs 2.64 ms; F = 256: 5.49 vs 4.10 ms; F = 47
-// unchanged) -- the gather is bound by cache throughput, not by the index round trip.
+// Gathers unrolled 8 rows deep, the next chunk's column ids requested during the current
+// chunk's gathers (round 4: headline +1-5 %, arxiv +1.2 %, profiles/r04_spmm).  Measured
+// alternatives, kept out: 4 deep (slower on the products shape), and round 2's
+// software-pipelined gather that combined the early column ids with non-temporal index
+// loads / output stores and 16 raw rows in flight per lane: 30 % SLOWER (F = 100: 3.43 vs
+// 2.64 ms) -- non-temporal stores alone double a store-heavy kernel's time (r04_lin).
 template <int L, int U>
 static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
