@@ -223,35 +223,38 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_fwd_kernel(
       for (int s = KA; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s - KA], bx[s], acc, 0, 0, 0);
       if constexpr (LAST && HOIST)
         if (tile + n_waves < n_tiles) load_rows(tile + n_waves);
-      // epilogue (registers 4g..4g+3 are hidden 32t + 8g + 4h + 0..3): bias (packed adds),
-      // relu, dropout as an AND with the sign-extended keep bit (the scale is in W2^T)
-      float v[16];
+      // epilogue (registers 4g..4g+3 are hidden 32t + 8g + 4h + 0..3) on packed bf16
+      // pairs: bias (packed fp32 adds), one v_cvt_pk_bf16_f32, relu as v_pk_max_i16 and the
+      // two keep bits as one v_pk_mul_lo_u16 per pair (the scale is in W2^T); the same
+      // bits as relu and the keep AND in fp32 followed by the conversion
+      uint32_t pk[8];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const float4 bb = *reinterpret_cast<const float4*>(sB1 + 32 * t + 8 * g + 4 * h);
         const f2 lo = f2{acc[4 * g], acc[4 * g + 1]} + f2{bb.x, bb.y};
         const f2 hi = f2{acc[4 * g + 2], acc[4 * g + 3]} + f2{bb.z, bb.w};
-        v[4 * g] = fmaxf(lo.x, 0.f); v[4 * g + 1] = fmaxf(lo.y, 0.f);
-        v[4 * g + 2] = fmaxf(hi.x, 0.f); v[4 * g + 3] = fmaxf(hi.y, 0.f);
+        pk[2 * g] = pk_relu(cvt_pk(lo.x, lo.y));
+        pk[2 * g + 1] = pk_relu(cvt_pk(hi.x, hi.y));
       }
       if constexpr (DROP != 0) {
-        const uint32_t m = drop_keep16(DROP == 2 ? rb : drop_draw(row0 + (uint32_t)row, t, h, step, k0, k1, false), t,
-                                       thr8, DROP == 2);
+        const uint32_t mw = keep_spread(drop_keep16(
+            DROP == 2 ? rb : drop_draw(row0 + (uint32_t)row, t, h, step, k0, k1, false), t, thr8, DROP == 2));
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = keep_and(v[q], m, q);
+        for (int i = 0; i < 8; ++i) pk[i] = pk_mul16(pk[i], (mw >> (2 * i)) & 0x10001u);
       }
       if (rv && H1) {          // H1 == nullptr: the fused backward recomputes it
+        uint32_t o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          o[i] = cvt_pk(__uint_as_float(pk[i] << 16) * w2s, __uint_as_float(pk[i] & 0xffff0000u) * w2s);
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<uint2*>(H1 + (size_t)row * HD + 32 * t + 8 * g + 4 * h) =
-              pack4(v[4 * g] * w2s, v[4 * g + 1] * w2s, v[4 * g + 2] * w2s, v[4 * g + 3] * w2s);
+          *reinterpret_cast<uint2*>(H1 + (size_t)row * HD + 32 * t + 8 * g + 4 * h) = make_uint2(o[2 * g], o[2 * g + 1]);
       }
       // second product: Z2^T += W2^T[:, 32t..32t+31] * H1^T tile (accumulator as B operand)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 xb;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xb[j] = (__bf16)v[8 * s2 + j];
+        const bf16x8 xb = __builtin_bit_cast(bf16x8, make_uint4(pk[4 * s2], pk[4 * s2 + 1], pk[4 * s2 + 2], pk[4 * s2 + 3]));
         const int nbase = 32 * t + 16 * s2 + 4 * h;
         {
           const uint16_t* a = sW2T + lr * W2S + nbase;
