@@ -66,15 +66,24 @@ def build_hip(force=False, verbose=False, debug=False):
     opt = ["-O0", "-g"] if debug else ["-O3"]
     objdir = os.path.join(HERE, "..", "build", "hip")
     os.makedirs(objdir, exist_ok=True)
-    objs = []
+    objs, cmds = [], []
     for s in srcs:
         o = os.path.join(objdir, os.path.basename(s) + ".o")
         objs.append(o)
         if force or _newer(o, [s] + hdrs + [__file__]):
             lang = ["-x", "hip", "--offload-arch=" + ARCH] if s.endswith(".hip") else []
-            cmd = [hipcc, "-c", "-fPIC", "-std=c++17", *opt, *lang, *inc,
-                   "-Wno-unused-result", "-fvisibility=hidden", s, "-o", o]
-            _run(cmd, verbose)
+            cmds.append([hipcc, "-c", "-fPIC", "-std=c++17", *opt, *lang, *inc,
+                         "-Wno-unused-result", "-fvisibility=hidden", s, "-o", o])
+    # one hipcc per translation unit, a few at a time (each holds 1-3 GB while it
+    # optimises the larger kernel files)
+    jobs = max(1, min(len(cmds), int(os.environ.get("CGNN_BUILD_JOBS", "4"))))
+    if jobs > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(jobs) as pool:
+            list(pool.map(lambda c: _run(c, verbose), cmds))
+    else:
+        for c in cmds:
+            _run(c, verbose)
     cmd = [hipcc, "-shared", "-fPIC", "--offload-arch=" + ARCH, *objs, "-o", target]
     _run(cmd, verbose)
     return target

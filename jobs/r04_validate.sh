@@ -4,7 +4,7 @@
 # full-size papers100M rank-0-of-8 dry run with the locality partition
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r04_validate
+O=gpurun_out/${VAL_OUT:-r04_validate}
 mkdir -p $O
 (while sleep 45; do date >> $O/heartbeat.log; done) &
 HB=$!
