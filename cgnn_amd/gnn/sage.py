@@ -247,7 +247,10 @@ class _FusedSAGE:
             F, nd = self.dims[k], blk.n_dst
             last = k == self.L - 1
             if k == 0 and idx0 is not None:
-                col = idx0[blk.col.long()]
+                # global source ids of the input layer's edges: the sampler's picks when it
+                # kept them (idx0[local] == picks), else one gather through idx0
+                gcol = getattr(blk, "gcol", None)
+                col = gcol if gcol is not None else idx0[blk.col.long()]
                 x1, idx1 = self.x, idx0[:nd]
             else:
                 col, x1, idx1 = blk.col, h, None

@@ -40,8 +40,12 @@ class DeviceBlock:
     ``inv_deg`` / ``transposed`` may be given precomputed (the pipelined sampler
     builds both on the device)."""
 
-    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n_src: int, inv_deg=None, transposed=None):
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, n_src: int, inv_deg=None, transposed=None,
+                 gcol=None):
         self.rowptr, self.col = rowptr, col
+        # global ids of the sources of every edge (= ids[col] for the block's source id
+        # list), when the sampler has them: the pipelined one keeps its picks
+        self.gcol = gcol
         self.n_dst = rowptr.numel() - 1
         self.n_src = int(n_src)
         if inv_deg is None:
@@ -208,7 +212,7 @@ class SampledBatch:
                 if sl.rp_t[l] is not None:
                     t = (sl.rp_t[l][:n_src + 1], sl.col_t[l][:total])
                 blocks.append(DeviceBlock(sl.optr[l][:nd + 1], sl.local[l][:total], n_src,
-                                          inv_deg=sl.inv[l][:nd], transposed=t))
+                                          inv_deg=sl.inv[l][:nd], transposed=t, gcol=sl.picks[l][:total]))
                 nd = n_src
             self._res = (blocks[::-1], sl.src[-1][:nd])
         return self._res

@@ -41,7 +41,9 @@ def _check(ref, seeds, sb, salt):
         assert torch.equal(b.rowptr, r.rowptr)
         assert torch.equal(b.col, r.col)
         assert torch.equal(b.inv_deg, r.inv_deg)
-        if i > 0:                              # every block but the input layer's
+        if i == 0:                             # the input layer's global source ids
+            assert torch.equal(b.gcol.long(), nodes.long()[b.col.long()])
+        if i > 0:                             # every block but the input layer's
             rp_t, col_t = b.transposed()
             erp, ecol = transpose_csr(r.rowptr, r.col, r.n_src)
             assert torch.equal(rp_t, erp) and torch.equal(col_t, ecol)
