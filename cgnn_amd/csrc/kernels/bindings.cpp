@@ -60,7 +60,7 @@ int rff_launch_fwd_bwd(int, const float*, const float*, const float*, float*, fl
                        int, int, int, int, float, hipStream_t, int);
 // GNN track
 int gnn_launch_spmm(const int*, const int*, const void*, void*, const float*, const float*, int,
-                    int, int, int, int, int, int, int, const float*, int, const float*, int, hipStream_t);
+                    int, int, int, int, int, int, int, const float*, int, const float*, int, int, hipStream_t);
 int gnn_launch_spmm_ce(const int*, const int*, const void*, const float*, const float*,
                        const int*, const uint8_t*, float*, void*, const float*, int, int, int, int, int, float,
                        const int*, int, hipStream_t);
@@ -271,16 +271,16 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("gnn_spmm", [](uint64_t rowptr, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, uint64_t bias,
                        int n_rows, int F, int ld_x, int ld_y, int x_bf16, int y_bf16, int relu, int unit_col,
-                       uint64_t st, uint64_t init, int ldi, uint64_t cscale, int init_rows) {
+                       uint64_t st, uint64_t init, int ldi, uint64_t cscale, int init_rows, int slab) {
     chk(gnn_launch_spmm(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(x), Pt<void>(y),
                         Pt<const float>(rscale), Pt<const float>(bias), n_rows, F, ld_x, ld_y, x_bf16,
                         y_bf16, relu, unit_col, Pt<const float>(init), ldi, Pt<const float>(cscale), init_rows,
-                        S(st)),
+                        slab, S(st)),
         "gnn_spmm");
   }, py::arg("rowptr"), py::arg("col"), py::arg("x"), py::arg("y"), py::arg("rscale"), py::arg("bias"),
      py::arg("n_rows"), py::arg("F"), py::arg("ld_x"), py::arg("ld_y"), py::arg("x_bf16"), py::arg("y_bf16"),
      py::arg("relu"), py::arg("unit_col"), py::arg("st"), py::arg("init") = 0, py::arg("ldi") = 0,
-     py::arg("cscale") = 0, py::arg("init_rows") = -1);
+     py::arg("cscale") = 0, py::arg("init_rows") = -1, py::arg("slab") = 0);
   m.def("gnn_spmm_ce", [](uint64_t rowptr, uint64_t col, uint64_t z, uint64_t rscale, uint64_t bias,
                           uint64_t labels, uint64_t mask, uint64_t stats, uint64_t dlogits, uint64_t init, int ldi,
                           int n_rows, int C, int ld, int mode, float inv_count, uint64_t st, uint64_t gslot,

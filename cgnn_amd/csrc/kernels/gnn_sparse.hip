@@ -698,18 +698,21 @@ static int spmm_launch(const int* rowptr, const int* col, const void* X, void* Y
 extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X, void* Y,
                                const float* rscale, const float* bias, int n_rows, int F, int ldx,
                                int ldy, int xbf, int ybf, int relu, int unit_col, const float* init, int ldi,
-                               const float* cscale, int init_rows, hipStream_t st) {
-  if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
+                               const float* cscale, int init_rows, int slab, hipStream_t st) {
+  // slab: output columns per launch (a multiple of 8, at most 512; <= 0: 512)
+  if (slab <= 0) slab = 512;
+  if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy || (slab % 8) || slab > 512) return -3;
   if (init_rows < 0) init_rows = n_rows;
-  if (ldy <= 512 && F <= 512)
+  if (ldy <= slab && F <= slab)
     return spmm_launch(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, ldy, init,
                        ldi, cscale, init_rows, st);
-  // wide rows: column slabs of 512 output columns (16-byte aligned offsets), one
-  // launch each; the last slabs also write the padding / ones columns up to ldy
+  // wide rows (or narrower slabs asked for): column slabs of `slab` output columns
+  // (16-byte aligned offsets), one launch each; the last slabs also write the padding /
+  // ones columns up to ldy
   const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;   // bf16 and fp16 are both 2 bytes
-  for (int c0 = 0; c0 < ldy; c0 += 512) {
-    const int fc = std::max(0, std::min(512, F - c0));
-    const int wc = std::min(512, ldy - c0);
+  for (int c0 = 0; c0 < ldy; c0 += slab) {
+    const int fc = std::max(0, std::min(slab, F - c0));
+    const int wc = std::min(slab, ldy - c0);
     const int rc = spmm_launch(rowptr, col, (const char*)X + (fc ? c0 * xs : 0), (char*)Y + c0 * ys, rscale,
                                bias && fc ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu,
                                unit_col >= 0 ? unit_col - c0 : -1, wc, init && fc ? init + c0 : nullptr, ldi,
