@@ -1285,6 +1285,51 @@ __global__ __launch_bounds__(256) void lin_reduce_kernel(const float* __restrict
   }
 }
 
+// The same sums (same order per output: chunks grp, grp + 8, ... of lane group grp, then
+// the 8 group partials -- bitwise equal to lin_reduce_kernel) with 16-byte loads: lane e
+// of a group owns outputs 4e..4e+3 of the block's 128, and each lane issues its group's
+// chunk loads 4 at a time ahead of the adds.  count % 4 == 0 (16-B aligned chunk rows).
+__global__ __launch_bounds__(256) void lin_reduce4_kernel(const float* __restrict__ gpart, int chunks, long count,
+                                                          int N, float* __restrict__ dW, float* __restrict__ db) {
+  __shared__ float4 s[8][33];
+  const int e = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const long i = ((long)blockIdx.x * 32 + e) * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < count) {
+    const float4* g = reinterpret_cast<const float4*>(gpart + i);
+    const long cs = count >> 2;                          // chunk stride in float4
+    int c = grp;
+    for (; c + 24 < chunks; c += 32) {
+      const float4 v0 = g[(size_t)c * cs], v1 = g[(size_t)(c + 8) * cs];
+      const float4 v2 = g[(size_t)(c + 16) * cs], v3 = g[(size_t)(c + 24) * cs];
+      acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
+      acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
+      acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
+      acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
+    }
+    for (; c < chunks; c += 8) {
+      const float4 v = g[(size_t)c * cs];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  s[grp][e] = acc;
+  __syncthreads();
+  if (grp == 0 && i < count) {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float4 v = s[q][e];
+      t[0] += v.x; t[1] += v.y; t[2] += v.z; t[3] += v.w;
+    }
+    const long kw = count - N;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i + u < kw) dW[i + u] = t[u];
+      else if (db) db[i + u - kw] = t[u];
+    }
+  }
+}
+
 // bf16 LDS images of the weights, written once per step (the blocks of the main
 // kernels then copy them with 16-byte loads):
 //   fwd: img[slab][c][k]  = W[k][slab * ncols + c]   (W^T, row stride WS = KP + 8)
@@ -1925,7 +1970,11 @@ extern "C" int gnn_launch_lin_bwd_weight(const void* x1, int ld1, int K1, const 
     (void)hipMemsetAsync(gpart, 0, sizeof(float) * (size_t)(K + 1) * N * chunks, st);
   }
   const long count = (long)(K + 1) * N;
-  hipLaunchKernelGGL(lin_reduce_kernel, dim3((unsigned)((count + 31) / 32)), dim3(256), 0, st, gpart,
-                     n > 0 ? chunks : 1, count, N, dW, db);
+  if (count % 4 == 0)
+    hipLaunchKernelGGL(lin_reduce4_kernel, dim3((unsigned)((count + 127) / 128)), dim3(256), 0, st, gpart,
+                       n > 0 ? chunks : 1, count, N, dW, db);
+  else
+    hipLaunchKernelGGL(lin_reduce_kernel, dim3((unsigned)((count + 31) / 32)), dim3(256), 0, st, gpart,
+                       n > 0 ? chunks : 1, count, N, dW, db);
   return (int)hipGetLastError();
 }
