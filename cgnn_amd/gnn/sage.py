@@ -435,9 +435,11 @@ class SAGETrainer:
         return blocks[::-1], nodes_in
 
     # ----------------------------------------------------------- training
-    def _step(self, blocks, nodes_in, seeds_t):
+    def _step(self, blocks, nodes_in, seeds_t, labels=None):
         if self.fused:
-            loss = self._fused.step(blocks, nodes_in.to(torch.int32), self.y32[seeds_t.long()], self.world)
+            if labels is None:
+                labels = self.y32[seeds_t.long()]
+            loss = self._fused.step(blocks, nodes_in.to(torch.int32), labels, self.world)
             return loss[0] / max(int(seeds_t.numel()), 1)
         self.model.train()
         out = self.model(self.x[nodes_in.long()], blocks)
@@ -489,9 +491,12 @@ class SAGETrainer:
             ps = self._psampler
             # the epoch's seeds uploaded once; batch k + 1 samples on the side stream while k trains
             flat = torch.as_tensor(np.concatenate(batches).astype(np.int32), device=self.dev)
-            seeds, o = [], 0
+            # the epoch's labels gathered once too (fused path), not per batch
+            yflat = self.y32[flat.long()] if self.fused else None
+            seeds, labels, o = [], [], 0
             for b in batches:
                 seeds.append(flat[o:o + len(b)])
+                labels.append(yflat[o:o + len(b)] if yflat is not None else None)
                 o += len(b)
             salt = lambda k: (self.epoch * 100003 + k) * self.world + self.rank
             pend = ps.enqueue(seeds[0], salt(0))
@@ -499,7 +504,7 @@ class SAGETrainer:
                 nxt = ps.enqueue(seeds[k + 1], salt(k + 1)) if k + 1 < len(batches) else None
                 blocks, nodes_in = pend.resolve()
                 torch.cuda.current_stream(self.dev).wait_event(pend.slot.done)
-                losses.append(self._step(blocks, nodes_in, seeds[k]))
+                losses.append(self._step(blocks, nodes_in, seeds[k], labels[k]))
                 ps.consumed(pend)
                 pend = nxt
         elif self._dsampler is not None:
