@@ -30,7 +30,7 @@ from .sage import transpose_csr
 
 
 def _st(t):
-    return torch.cuda.current_stream(t.device).cuda_stream
+    return torch._C._cuda_getCurrentRawStream(t.get_device())
 
 
 class GraphCSR:

@@ -55,7 +55,7 @@ from .linear import lin_bwd_data, lin_bwd_weight, lin_fwd
 
 
 def _st(t):
-    return torch.cuda.current_stream(t.device).cuda_stream
+    return torch._C._cuda_getCurrentRawStream(t.get_device())
 
 
 def _ru8(x):
