@@ -59,6 +59,8 @@ def main():
                          "or auto (features aligned, layer-2 rows packed: the same as mixed)")
     ap.add_argument("--no-fused", action="store_true", help="hipBLASLt GEMMs + separate epilogues")
     ap.add_argument("--capture", action="store_true", help="replay the epoch from a hipGraph (one GPU)")
+    ap.add_argument("--no-fuse-agg", action="store_true",
+                    help="layer-1 aggregation and dense forward as two kernels (A/B; default on one GPU: one)")
     ap.add_argument("--id-order", choices=["shuffled", "banded"], default="shuffled",
                     help="synthetic node ids: shuffled (no locality in the ids, like a real dataset) or "
                          "the generator's banded ids (locality for free; A/B only)")
@@ -103,10 +105,7 @@ def main():
     if world > 1 and os.environ.get("OMP_NUM_THREADS") == "1":
         # torch.distributed.run pins OMP_NUM_THREADS=1: give the host C++ setup (graph
         # generation, locality reorder) this rank's share of the node's cores instead
-        from cgnn_amd import native
-        lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-        cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
-        native.rt().set_num_threads(max(1, cpus // max(lw, 1)))
+        pdist.set_host_threads()
     if cuda:
         torch.cuda.set_device(0 if shared else local)
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -142,7 +141,8 @@ def main():
                     fused=not a.no_fused,
                     align_rows={'auto': None, 'aligned': True, 'packed': False, 'mixed': None}[a.rows],
                     align_c=False if a.rows == "mixed" else None,
-                    capture=a.capture, reorder=a.reorder != "none")
+                    capture=a.capture, reorder=a.reorder != "none",
+                    fuse_agg=False if a.no_fuse_agg else None)
     n_nodes, nnz = g.n, g.nnz
     del g
     sync()

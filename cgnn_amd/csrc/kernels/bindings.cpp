@@ -30,6 +30,7 @@ int cgnn_launch_loss_finalize(const float*, int, float*, float*, float*, float, 
 int cgnn_launch_gen_fwd(const int*, int, const float*, int, const float*, float*, float*, int, float*,
                         const uint32_t*, const int*, int, int, int, int, int, hipStream_t, int);
 int cgnn_gen_bwd_variant(int, int, int, int);
+int cgnn_gen_staged_supported(int, int, int);
 size_t cgnn_gen_fwd_lds(int, int);
 int cgnn_staged_plan(int, int, int, int, int, int*);
 int cgnn_staged_tiles(int);
@@ -81,6 +82,10 @@ int gnn_launch_dense_fwd(const void*, const float*, const float*, const float*, 
                          const int*, void*, hipStream_t);
 long gnn_keep_image_halfwords(int, int);
 int gnn_launch_keep_image(void*, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, const int*, hipStream_t);
+int gnn_agg_fwd_queue_words();
+int gnn_launch_agg_fwd(const int*, const int*, const void*, void*, const float*, const float*, const float*,
+                       const float*, void*, int, int, int, int, int, int, float, uint32_t, uint32_t, uint32_t,
+                       uint32_t, const int*, void*, int*, hipStream_t);
 int gnn_launch_gat_fwd(const int*, const int*, const void*, const float*, const float*, const int*, float*, float*,
                        void*, int, int, int, int, const float*, void*, int, float, uint32_t, uint32_t, uint32_t,
                        const int*, uint32_t, hipStream_t);
@@ -164,6 +169,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gen_bwd_blocks", &cgnn_gen_bwd_blocks);
   m.def("gen_bwd_lds", &cgnn_gen_bwd_lds);
   m.def("gen_bwd_variant", &cgnn_gen_bwd_variant);
+  m.def("gen_staged_supported", &cgnn_gen_staged_supported);
   m.def("gen_fwd_lds", &cgnn_gen_fwd_lds);
   // level-scheduled (wide-graph) generator kernels, cgnn_staged.hip
   m.def("staged_plan", [](int Dt, int H, int max_in, int W, int extra) -> py::tuple {
@@ -336,6 +342,19 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("n"), py::arg("F"), py::arg("ldx"), py::arg("HD"), py::arg("C"), py::arg("ldc"), py::arg("p"),
      py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"), py::arg("step_ptr") = 0,
      py::arg("kimg") = 0);
+  m.def("gnn_agg_fwd_queue_words", &gnn_agg_fwd_queue_words);
+  m.def("gnn_agg_fwd", [](uint64_t rowptr, uint64_t col, uint64_t xs, uint64_t ax, uint64_t w1, uint64_t b1,
+                          uint64_t w2, uint64_t dinv, uint64_t z2, int n, int F, int ldx, int HD, int C, int ldc,
+                          float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t row0, uint64_t st,
+                          uint64_t stepp, uint64_t kimg, uint64_t ctr) {
+    return gnn_launch_agg_fwd(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(xs), Pt<void>(ax),
+                              Pt<const float>(w1), Pt<const float>(b1), Pt<const float>(w2), Pt<const float>(dinv),
+                              Pt<void>(z2), n, F, ldx, HD, C, ldc, p, k0, k1, step, row0, Pt<const int>(stepp),
+                              Pt<void>(kimg), Pt<int>(ctr), S(st));
+  }, py::arg("rowptr"), py::arg("col"), py::arg("xs"), py::arg("ax"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
+     py::arg("dinv"), py::arg("z2"), py::arg("n"), py::arg("F"), py::arg("ldx"), py::arg("HD"), py::arg("C"),
+     py::arg("ldc"), py::arg("p"), py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"),
+     py::arg("step_ptr") = 0, py::arg("kimg") = 0, py::arg("ctr") = 0);
   m.def("gnn_keep_image_halfwords", &gnn_keep_image_halfwords);
   m.def("gnn_keep_image", [](uint64_t kimg, int n, int HD, float p, uint32_t k0, uint32_t k1, uint32_t step,
                              uint32_t row0, uint64_t st, uint64_t stepp) {

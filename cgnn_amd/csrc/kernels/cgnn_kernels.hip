@@ -732,13 +732,19 @@ extern "C" int cgnn_staged_plan(int, int, int, int, int, int*);
 
 // 1: the specialised per-sample kernel (compiled H, LDS sample state fits), 2: the
 // level-scheduled kernels of cgnn_staged.hip, 0: neither fits (the caller trains this
-// batch elsewhere).  CGNN_GEN_STAGED=1 forces 2 (A/B and equivalence tests).
+// batch elsewhere).  The choice depends only on the arguments: the scorer evaluates it
+// per program and batches programs of one family together (engine/scorer.py), so a
+// model's kernels -- and its score -- do not depend on its batch-mates.
 extern "C" int cgnn_gen_bwd_variant(int H, int max_in, int Dt, int prog_stride) {
-  const char* force = getenv("CGNN_GEN_STAGED");
-  const bool staged = force && atoi(force) == 1;
-  if (!staged && cgnn_gen_supported_h(H) && cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride) <= 160 * 1024) return 1;
+  if (cgnn_gen_supported_h(H) && cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride) <= 160 * 1024) return 1;
   int plan[5];
-  return cgnn_staged_plan(Dt, H, max_in, 8, 2 * prog_stride, plan) == 0 ? 2 : 0;
+  return cgnn_staged_plan(Dt, H, max_in, 8, 0, plan) == 0 ? 2 : 0;
+}
+
+// whether the level-scheduled kernels cover (Dt, H, max_in) at all (a forced staged batch)
+extern "C" int cgnn_gen_staged_supported(int H, int max_in, int Dt) {
+  int plan[5];
+  return cgnn_staged_plan(Dt, H, max_in, 8, 0, plan) == 0;
 }
 
 // the per-sample backward (variant 1); variant 2 batches launch cgnn_launch_gen_bwd_staged

@@ -96,8 +96,7 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
   const float* nz = noise + (size_t)r * NS * N;
   float* xr = xhat + (size_t)r * D * N;
   float* s_x = smem;                                        // [Dt][64] (LDS state)
-  float* s_nrm = s_x + (XG ? 0 : (size_t)Dt * WAVE);        // [W][64]
-  float* s_w = s_nrm + W * WAVE + (size_t)wave * (max_in + 2) * HCS;   // this wave's weight rows
+  float* s_w = s_x + (XG ? 0 : (size_t)Dt * WAVE) + (size_t)wave * (max_in + 2) * HCS;   // this wave's weight rows
   auto xget = [&](int v) -> float { return XG ? xr[(size_t)v * N + nc] : s_x[v * WAVE + lane]; };
   auto xput = [&](int v, float val) {
     if (XG) {
@@ -233,22 +232,22 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
 
   if (!XG && valid)
     for (int v = wave; v < Dt; v += W) xr[(size_t)v * N + n] = s_x[v * WAVE + lane];
-  if (xnorm) {
-    // squared norm for the Gram-form MMD: wave w sums program positions w, w + W, ...
-    // in order, the W partials are added in wave order (fixed)
+  if (xnorm && wave == 0) {
+    // squared norm for the Gram-form MMD: one fmaf chain over the program positions in
+    // order -- the per-sample kernel's order, whatever W (the block width follows the
+    // widest stage of any program in the batch, so a W-dependent order would make a
+    // model's loss depend on its batch-mates)
     const int nn = uni(pg);
     float nrm = 0.f;
-    for (int kk = wave; kk < nn; kk += W) {
-      const float v = xget(uni(pg + PROG_HDR + kk * NODE_REC));
-      nrm = fmaf(v, v, nrm);
+    for (int k0 = 0; k0 < nn; k0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xget(uni(pg + PROG_HDR + min(k0 + u, nn - 1) * NODE_REC));
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 + u < nn) nrm = fmaf(v[u], v[u], nrm);
     }
-    s_nrm[wave * WAVE + lane] = nrm;
-    __syncthreads();
-    if (wave == 0 && valid) {
-      float s = 0.f;
-      for (int w = 0; w < W; ++w) s += s_nrm[w * WAVE + lane];
-      xnorm[(size_t)r * N + n] = s;
-    }
+    if (valid) xnorm[(size_t)r * N + n] = nrm;
   }
 }
 
@@ -545,8 +544,7 @@ int fwd_hc(int H) {
 // extra: program + schedule ints staged in LDS
 size_t fwd_lds(int Dt, int W, bool xg, int max_in, int hc, int extra) {
   const size_t hcs = (size_t)((hc + 3) & ~3);
-  return sizeof(float) * ((size_t)extra + (xg ? 0 : (size_t)Dt * WAVE) + (size_t)W * WAVE +
-                          (size_t)W * (max_in + 2) * hcs);
+  return sizeof(float) * ((size_t)extra + (xg ? 0 : (size_t)Dt * WAVE) + (size_t)W * (max_in + 2) * hcs);
 }
 size_t bwd_lds(int Dt, int W, int max_in, bool xg, bool dg, int extra) {
   return sizeof(float) * ((size_t)extra + (xg ? 0 : (size_t)Dt * WAVE) + (dg ? 0 : (size_t)Dt * WAVE) +

@@ -18,190 +18,17 @@
 // broadcast inside the sub-group with ds_bpermute; four gathered rows are kept
 // in flight per lane.  Accumulation is fp32; storage is bf16.
 #include "cgnn_common.h"
+#include "gnn_gather.h"
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
 using namespace cgnn;
-
-template <typename T>
-__device__ __forceinline__ T ld_stream(const T* p) {
-  return *p;
-}
+using namespace cgnn::gather;
 
 namespace {
 
 struct bf16x8 { uint32_t w[4]; };
-
-__device__ __forceinline__ void bf16x8_to_f32(const uint4 v, float* f) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
-}
-
-__device__ __forceinline__ uint32_t f32_to_bf16_rne(float x) {
-  uint32_t u = __float_as_uint(x);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return u >> 16;
-}
-
-__device__ __forceinline__ uint4 f32x8_to_bf16(const float* f) {
-  uint4 o;
-  o.x = f32_to_bf16_rne(f[0]) | (f32_to_bf16_rne(f[1]) << 16);
-  o.y = f32_to_bf16_rne(f[2]) | (f32_to_bf16_rne(f[3]) << 16);
-  o.z = f32_to_bf16_rne(f[4]) | (f32_to_bf16_rne(f[5]) << 16);
-  o.w = f32_to_bf16_rne(f[6]) | (f32_to_bf16_rne(f[7]) << 16);
-  return o;
-}
-
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-
-// acc[0..7] += a[0..7] + b[0..7] for two raw bf16x8 rows, two instructions per feature
-// pair instead of four: v_perm_b32 pairs feature f of both rows into one dword, then
-// v_dot2c_f32_bf16 against (1, 1) adds both into the fp32 accumulator
-__device__ __forceinline__ void acc_bf16_pair(float* acc, const uint4 a, const uint4 b) {
-  const bf16x2 one = {(__bf16)1.0f, (__bf16)1.0f};
-  const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const uint32_t lo = __builtin_amdgcn_perm(bw[w], aw[w], 0x05040100u);   // (a.f, b.f)
-    const uint32_t hi = __builtin_amdgcn_perm(bw[w], aw[w], 0x07060302u);   // (a.f+1, b.f+1)
-    acc[2 * w] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, lo), one, acc[2 * w], false);
-    acc[2 * w + 1] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, hi), one, acc[2 * w + 1], false);
-  }
-}
-
-// the same for fp16 rows (v_dot2_f32_f16)
-__device__ __forceinline__ void acc_f16_pair(float* acc, const uint4 a, const uint4 b) {
-  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-  const f16x2 one = {(_Float16)1.0f, (_Float16)1.0f};
-  const uint32_t aw[4] = {a.x, a.y, a.z, a.w}, bw[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const uint32_t lo = __builtin_amdgcn_perm(bw[w], aw[w], 0x05040100u);
-    const uint32_t hi = __builtin_amdgcn_perm(bw[w], aw[w], 0x07060302u);
-    acc[2 * w] = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, lo), one, acc[2 * w], false);
-    acc[2 * w + 1] = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, hi), one, acc[2 * w + 1], false);
-  }
-}
-
-template <int XT>
-__device__ __forceinline__ void acc_pair(float* acc, const uint4 a, const uint4 b) {
-  if (XT == 1) acc_bf16_pair(acc, a, b);
-  else acc_f16_pair(acc, a, b);
-}
-
-__device__ __forceinline__ uint4 load_raw16(const void* X, size_t off) {
-  return *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(X) + off);
-}
-
-// element types of the gathered / written matrices: 0 = fp32, 1 = bf16, 2 = fp16
-template <int XT>
-__device__ __forceinline__ void load8(const void* X, size_t off, float* f) {
-  if (XT == 1) {
-    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(X) + off);
-    bf16x8_to_f32(v, f);
-  } else if (XT == 2) {
-    const f16x8 v = *reinterpret_cast<const f16x8*>(reinterpret_cast<const uint16_t*>(X) + off);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) f[q] = (float)v[q];
-  } else {
-    const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + off);
-    const float4 a = p[0], b = p[1];
-    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
-  }
-}
-
-// Sum the rows X[col[e]] for e in [e0, e1) into acc (8 features at f0).
-// CS: gathered row j is scaled by cscale[j] (the column half of a symmetric
-// normalisation, when the producer of X did not fold it in)
-template <int L, int XBF, int U = 4, bool CS = false>
-__device__ __forceinline__ void gather_sum(const int* __restrict__ col, const void* __restrict__ X,
-                                           int e0, int e1, int ldx, int f0, bool fv, int sub_base,
-                                           int sl, float* acc, const float* __restrict__ cscale = nullptr) {
-  // the next chunk's column ids load while this chunk's rows are gathered (clamped address,
-  // unconditional load: a "load or 0" would branch and wait for it at the join)
-  int nxj = ld_stream(col + max(0, min(e0 + sl, e1 - 1)));
-  for (int e = e0; e < e1; e += L) {
-    const int myj = nxj;
-    nxj = ld_stream(col + max(0, min(e + L + sl, e1 - 1)));
-    const float mycs = CS ? cscale[myj] : 1.f;
-    const int cnt = min(L, e1 - e);
-    int k = 0;
-    if (U == 8 && L >= 8) {
-      for (; k + 8 <= cnt; k += 8) {
-        int j[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) j[u] = __shfl(myj, sub_base + k + u, 64);
-        float c[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) c[u] = CS ? __shfl(mycs, sub_base + k + u, 64) : 1.f;
-        if (fv && XBF != 0 && !CS) {
-          uint4 r[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) r[u] = load_raw16(X, (size_t)j[u] * ldx + f0);
-#pragma unroll
-          for (int u = 0; u < 8; u += 2) acc_pair<XBF>(acc, r[u], r[u + 1]);
-        } else if (fv) {
-          float a[8][8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) load8<XBF>(X, (size_t)j[u] * ldx + f0, a[u]);
-          if (CS) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              acc[q] += (fmaf(c[0], a[0][q], c[1] * a[1][q]) + fmaf(c[2], a[2][q], c[3] * a[3][q])) +
-                        (fmaf(c[4], a[4][q], c[5] * a[5][q]) + fmaf(c[6], a[6][q], c[7] * a[7][q]));
-          } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-              acc[q] += ((a[0][q] + a[1][q]) + (a[2][q] + a[3][q])) + ((a[4][q] + a[5][q]) + (a[6][q] + a[7][q]));
-          }
-        }
-      }
-    }
-    for (; k + 4 <= cnt; k += 4) {
-      const int j0 = __shfl(myj, sub_base + k + 0, 64);
-      const int j1 = __shfl(myj, sub_base + k + 1, 64);
-      const int j2 = __shfl(myj, sub_base + k + 2, 64);
-      const int j3 = __shfl(myj, sub_base + k + 3, 64);
-      const float c0 = CS ? __shfl(mycs, sub_base + k + 0, 64) : 1.f;
-      const float c1 = CS ? __shfl(mycs, sub_base + k + 1, 64) : 1.f;
-      const float c2 = CS ? __shfl(mycs, sub_base + k + 2, 64) : 1.f;
-      const float c3 = CS ? __shfl(mycs, sub_base + k + 3, 64) : 1.f;
-      if (fv && XBF != 0 && !CS) {
-        const uint4 r0 = load_raw16(X, (size_t)j0 * ldx + f0), r1 = load_raw16(X, (size_t)j1 * ldx + f0);
-        const uint4 r2 = load_raw16(X, (size_t)j2 * ldx + f0), r3 = load_raw16(X, (size_t)j3 * ldx + f0);
-        acc_pair<XBF>(acc, r0, r1);
-        acc_pair<XBF>(acc, r2, r3);
-      } else if (fv) {
-        float a[8], b[8], c[8], d[8];
-        load8<XBF>(X, (size_t)j0 * ldx + f0, a);
-        load8<XBF>(X, (size_t)j1 * ldx + f0, b);
-        load8<XBF>(X, (size_t)j2 * ldx + f0, c);
-        load8<XBF>(X, (size_t)j3 * ldx + f0, d);
-        if (CS) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc[q] += fmaf(c0, a[q], c1 * b[q]) + fmaf(c2, c[q], c3 * d[q]);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) acc[q] += (a[q] + b[q]) + (c[q] + d[q]);
-        }
-      }
-    }
-    for (; k < cnt; ++k) {
-      const int j = __shfl(myj, sub_base + k, 64);
-      const float cj = CS ? __shfl(mycs, sub_base + k, 64) : 1.f;
-      if (fv) {
-        float a[8];
-        load8<XBF>(X, (size_t)j * ldx + f0, a);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] = CS ? fmaf(cj, a[q], acc[q]) : acc[q] + a[q];
-      }
-    }
-  }
-}
 
 // Sum the bf16 rows X[col[e]] for e in [e0, e1) minus the gap [g0, g1) (the edges served
 // from LDS by the windowed kernel) into acc; 8 raw rows in flight per lane.
@@ -679,6 +506,11 @@ static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void*
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
                          int relu, int uc, int wc, const float* init, int ldi, const float* cs, int ir,
                          hipStream_t st) {
+#ifdef SPMM_U16
+  if (L == 16 && xbf == 1 && ybf == 1 && !cs)
+    return spmm_dispatch_u<L, 16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
+                                  ldi, cs, ir, st);
+#endif
   return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
                                ldi, cs, ir, st);
 }

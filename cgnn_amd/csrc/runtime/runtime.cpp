@@ -410,6 +410,18 @@ py::tuple synthetic_shard(i64 n, i64 m, int n_feat, int n_class, double homophil
   const bool relabel = order_a.size() > 0;
   if (relabel && order_a.size() != n) throw std::invalid_argument("synthetic_shard: order must have n entries");
   const i64* ord = relabel ? order_a.data() : nullptr;
+  if (relabel) {
+    // a permutation of [0, n): every value in range and seen once (otherwise some local
+    // rows would get no id and the split mask / labels would read garbage)
+    std::vector<uint8_t> seen(n, 0);
+    bool ok = true;
+    for (i64 f = 0; f < n && ok; ++f) {
+      const i64 v = ord[f];
+      ok = v >= 0 && v < n && !seen[v];
+      if (ok) seen[v] = 1;
+    }
+    if (!ok) throw std::invalid_argument("synthetic_shard: order must be a permutation of [0, n)");
+  }
   const SynthSpec sp(n, m, n_feat, n_class, homophily, feat_noise, seed, label_noise, id_order);
   const i64 nl = r1 - r0;
   py::array_t<i64> rp_a(nl + 1);

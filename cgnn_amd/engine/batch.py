@@ -87,6 +87,18 @@ def mmd_kernel_choice(D: int, mmd_kernel: str = "auto") -> str:
     return choice
 
 
+def _prog_stride(prog_len: int) -> int:
+    return (int(prog_len) + 3) // 4 * 4              # pack_programs' stride
+
+
+def kernel_family(d: int, H: int, max_in: int, prog_len: int = 0) -> int:
+    """Generator-kernel family of a batch of ``d``-variable programs: 1 the per-sample
+    kernels (sample state in LDS), 2 the level-scheduled ones, 0 neither.  The scorer
+    evaluates it per program and batches programs of one family together, so the kernels
+    that train a model -- and its score -- do not depend on its batch-mates."""
+    return int(native.hip().gen_bwd_variant(int(H), int(max_in), int(d), _prog_stride(prog_len)))
+
+
 def device_supported(d: int, H: int, max_in: int, prog_len: int = 0, fast_mmd: bool = False) -> bool:
     """True when the device kernels cover a batch of ``d``-variable programs with hidden
     width ``H``, at most ``max_in`` generator inputs per node and programs of at most
@@ -95,11 +107,9 @@ def device_supported(d: int, H: int, max_in: int, prog_len: int = 0, fast_mmd: b
     Otherwise ``score_jobs`` trains the batch on the CPU reference path (with a warning)."""
     if d > SUPPORTED_D[-1] or (fast_mmd and padded_dim(d) > MAX_RFF_D):
         return False
-    hip = native.hip()
-    stride = (int(prog_len) + 3) // 4 * 4              # pack_programs' stride
-    variant = hip.gen_bwd_variant(int(H), int(max_in), int(d), stride)
+    variant = kernel_family(d, H, max_in, prog_len)
     if variant == 1:
-        return hip.gen_fwd_lds(padded_dim(d), stride) <= 160 * 1024
+        return native.hip().gen_fwd_lds(padded_dim(d), _prog_stride(prog_len)) <= 160 * 1024
     return variant == 2
 
 
@@ -110,7 +120,9 @@ def staged_setup(programs: Sequence[Program], H: int, max_in: int, d: int, prog_
     W = 8
     while W > 1 and W // 2 >= width:
         W //= 2
-    plan = native.hip().staged_plan(int(d), int(H), int(max_in), W, int(prog_stride) + int(sstride))
+    # the launchers plan with the same arguments (no program words are staged in LDS), so
+    # the dL/dx placement chosen here is the one they launch
+    plan = native.hip().staged_plan(int(d), int(H), int(max_in), W, 0)
     if not plan:
         raise native.NativeExtensionError("staged generator kernels: no LDS plan for d=%d H=%d" % (d, H))
     return sched, sstride, W, bool(plan[2])
@@ -135,7 +147,9 @@ class DeviceTrainer:
     def __init__(self, programs: Sequence[Program], datas: Sequence[np.ndarray],
                  keys: Sequence[tuple], H: int, device, learning_rate=0.01, init_std=0.05,
                  use_fast_mmd=False, nb_vectors=100, record_history=0, graph_chunk=50,
-                 mmd_kernel="auto"):
+                 mmd_kernel="auto", generator="auto"):
+        # generator: "auto" (kernel_family of the batch), "staged" (the level-scheduled
+        # kernels even where the per-sample ones fit: equivalence tests, A/B tools)
         hip = native.hip()
         self.hip = hip
         self.device = torch.device(device)
@@ -150,7 +164,11 @@ class DeviceTrainer:
         self.R, self.N, self.d, self.D, self.H = R, N, d, D, int(H)
         prog, stride, P, max_in = pack_programs(programs)
         self.P, self.prog_stride, self.max_in = P, stride, max_in
+        if generator not in ("auto", "staged"):
+            raise ValueError("generator must be auto|staged")
         self.bwd_variant = hip.gen_bwd_variant(int(H), int(max_in), int(d), int(stride))
+        if generator == "staged":
+            self.bwd_variant = 2 if hip.gen_staged_supported(int(H), int(max_in), int(d)) else 0
         if self.bwd_variant == 0:
             raise native.NativeExtensionError(
                 "generator backward: H=%d with %d inputs per node does not fit in LDS" % (H, max_in))

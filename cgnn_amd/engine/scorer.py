@@ -60,15 +60,42 @@ def _fault_indices():
     return {int(x) for x in spec[len("nan@job:"):].split(",") if x.strip()}
 
 
-def _group_batches(jobs: Sequence[Job], batch: int):
-    """Group compatible jobs (same [d, N]) into batches of at most `batch`."""
+def _group_batches(jobs: Sequence[Job], batch: int, H: Optional[int] = None):
+    """Group compatible jobs (same [d, N]) into batches of at most `batch`.  With ``H``
+    (device batches) also by generator-kernel family (engine.batch.kernel_family of each
+    program alone), and a per-sample batch whose combined inputs / program length no
+    longer fit that family is split: every model trains on the kernels it would get
+    alone, so its score does not depend on the batch it lands in."""
+    fam = None
+    if H is not None:
+        from .batch import kernel_family
+        cache = {}
+
+        def fam(p):
+            k = (p.n_vars, p.max_in, len(p.prog))
+            if k not in cache:
+                cache[k] = kernel_family(p.n_vars, H, p.max_in, len(p.prog))
+            return cache[k]
     groups = {}
     for i, j in enumerate(jobs):
-        groups.setdefault((j.program.n_vars, j.data.shape[1]), []).append(i)
+        key = (j.program.n_vars, j.data.shape[1]) + ((fam(j.program),) if fam else ())
+        groups.setdefault(key, []).append(i)
     out = []
-    for idx in groups.values():
+
+    def emit(idx, family):
+        if family == 1 and len(idx) > 1:
+            p = [jobs[i].program for i in idx]
+            from .batch import kernel_family
+            if kernel_family(p[0].n_vars, H, max(q.max_in for q in p), max(len(q.prog) for q in p)) != 1:
+                h = len(idx) // 2
+                emit(idx[:h], family)
+                emit(idx[h:], family)
+                return
+        out.append(idx)
+
+    for key, idx in groups.items():
         for s in range(0, len(idx), batch):
-            out.append(idx[s:s + batch])
+            emit(idx[s:s + batch], key[2] if fam else None)
     return out
 
 
@@ -109,7 +136,7 @@ def _run_local(jobs: Sequence[Job], cfg) -> np.ndarray:
     if devices:
         from .batch import DeviceTrainer
         batches = []
-        for idx in _group_batches(jobs, max(1, cfg.batch_models)):
+        for idx in _group_batches(jobs, max(1, cfg.batch_models), H=cfg.h_layer_dim):
             if _device_batch_ok(jobs, idx, cfg):
                 batches.append(idx)
                 continue
@@ -164,7 +191,7 @@ def _run_long(jobs: Sequence[Job], cfg) -> np.ndarray:
     devices = pdist.devices_for(cfg)
     dev = devices[0] if devices else torch.device("cpu")
     t0 = time.perf_counter()
-    for idx in _group_batches(jobs, max(1, cfg.batch_models)):
+    for idx in _group_batches(jobs, max(1, cfg.batch_models), H=cfg.h_layer_dim if devices else None):
         if devices and not _device_batch_ok(jobs, idx, cfg):
             # every rank trains the whole job on the fp64 CPU reference (same scores on
             # every rank: no exchange needed)

@@ -203,6 +203,27 @@ def partition_order(name: str, seed: int = 0, scale: float = 1.0, homophily: flo
     return order
 
 
+def shared_partition_order(name: str, seed: int = 0, scale: float = 1.0, **kw) -> np.ndarray:
+    """``partition_order`` computed ONCE per job: rank 0 runs the pass with every CPU of
+    its node (the other ranks wait in the broadcast, holding no copy of the structure)
+    and broadcasts the order (parallel.dist.broadcast_host_array).  One process: plain
+    ``partition_order``."""
+    from ..parallel import dist as pdist
+    if not pdist.is_distributed():
+        return partition_order(name, seed=seed, scale=scale, **kw)
+    n = _scaled_shape(name, scale)[0]
+    order = None
+    if pdist.rank() == 0:
+        pdist.set_host_threads(pdist.host_cpus())
+        try:
+            order = partition_order(name, seed=seed, scale=scale, **kw)
+        finally:
+            pdist.set_host_threads()          # back to this rank's share
+    dt = np.int32 if n < (1 << 31) else np.int64
+    out = pdist.broadcast_host_array(None if order is None else order.astype(dt), n, dtype=dt)
+    return out.astype(np.int64)
+
+
 def synthetic_shard(name: str, rank: int, world: int, seed: int = 0, device=None, scale: float = 1.0,
                     homophily: float = 0.8, feat_noise: float = 4.0, label_noise: float = 0.25,
                     id_order: str = "shuffled", feature_dtype=torch.float32, partition: str = "none",

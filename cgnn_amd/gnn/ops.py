@@ -396,6 +396,39 @@ def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step, row0=0, kimg=None):
     return True
 
 
+def agg_queue(device):
+    """Work-queue words of ``agg_fwd`` (zero; each launch leaves them zero)."""
+    return torch.zeros(native.hip().gnn_agg_fwd_queue_words(), dtype=torch.int32, device=device)
+
+
+def agg_fwd(rowptr, col, Xs, AX, W1, b1, W2, dinv, Z2, F, p, key, step, row0=0, kimg=None, queue=None):
+    """The layer-1 aggregation fused with the dense forward (GPU, one kernel):
+    AX = spmm(rowptr, col, Xs, rscale=dinv, unit_col=F) (bit-identical to ``spmm``), then
+    ``dense_fwd(AX, ...)`` with H1 not stored.  ``queue``: an ``agg_queue`` buffer.
+    Returns False when no compiled variant covers the shape (the caller runs the two
+    kernels instead)."""
+    n = rowptr.numel() - 1
+    HD, C = W1.shape[1], W2.shape[1]
+    if checks.enabled():
+        checks.csr(rowptr, col, Xs.shape[0], "agg_fwd")
+        checks.rows(AX, n, "agg_fwd AX")
+        checks.rows(Z2, n, "agg_fwd Z2")
+        checks.rows(dinv, n, "agg_fwd dinv")
+    if queue is None:
+        queue = agg_queue(AX.device)
+    sv, sp = _step_args(step)
+    rc = native.hip().gnn_agg_fwd(rowptr.data_ptr(), col.data_ptr(), Xs.data_ptr(), AX.data_ptr(), W1.data_ptr(),
+                                  b1.data_ptr(), W2.data_ptr(), dinv.data_ptr(), Z2.data_ptr(), n, F, AX.shape[1],
+                                  HD, C, Z2.shape[1], float(p), int(key[0]), int(key[1]), sv, int(row0), _st(AX),
+                                  step_ptr=sp, kimg=kimg.data_ptr() if kimg is not None else 0,
+                                  ctr=queue.data_ptr())
+    if rc == 0:
+        return True
+    if rc != -1:
+        raise RuntimeError("gnn_agg_fwd failed (%d)" % rc)
+    return False
+
+
 def dense_bwd(dY2, W2, H1, dP1, p):
     """dP1 = (dY2 W2^T) * [H1 > 0] / (1-p)."""
     n = dP1.shape[0]

@@ -111,3 +111,51 @@ def combine_scores(n: int, idx: np.ndarray, local: np.ndarray) -> np.ndarray:
     out = buf.cpu().numpy()
     out[own.cpu().numpy() > 0] = np.nan
     return out
+
+
+def host_cpus() -> int:
+    """CPUs this process may run on (its affinity set, not the machine's count)."""
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
+
+
+def set_host_threads(n: Optional[int] = None) -> int:
+    """Threads of the host C++ runtime (graph generation, reorder, partition).  Default:
+    this rank's share of the node's CPUs -- torch.distributed.run pins OMP_NUM_THREADS=1,
+    which would leave the setup of every rank single-threaded.  Returns the count set."""
+    from .. import native
+    if n is None:
+        lw = int(os.environ.get("LOCAL_WORLD_SIZE", str(world_size())))
+        n = max(1, host_cpus() // max(lw, 1))
+    native.rt().set_num_threads(int(n))
+    return int(n)
+
+
+def broadcast_host_array(arr: Optional[np.ndarray], n: int, dtype=np.int64, src: int = 0,
+                         chunk_bytes: int = 256 << 20) -> np.ndarray:
+    """Broadcast a 1-D host array of ``n`` elements from rank ``src`` (the other ranks
+    pass None).  Over RCCL it travels through one device staging buffer of at most
+    ``chunk_bytes`` (a 111 M-entry partition order is 0.9 GB); over gloo directly."""
+    if not is_distributed():
+        return np.asarray(arr)
+    import torch.distributed as dist
+    tdt = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32,
+           np.dtype(np.float32): torch.float32}[np.dtype(dtype)]
+    out = np.asarray(arr, dtype=dtype) if rank() == src else np.empty(n, dtype=dtype)
+    if out.shape != (n,):
+        raise ValueError("broadcast_host_array: rank %d holds %s, expected (%d,)" % (rank(), out.shape, n))
+    host = torch.from_numpy(out)
+    if dist.get_backend() != "nccl":
+        dist.broadcast(host, src)
+        return out
+    per = max(1, chunk_bytes // out.itemsize)
+    stage = torch.empty(min(per, n), dtype=tdt, device=torch.device("cuda", torch.cuda.current_device()))
+    for a in range(0, n, per):
+        b = min(n, a + per)
+        if rank() == src:
+            stage[:b - a].copy_(host[a:b])
+        dist.broadcast(stage[:b - a], src)
+        if rank() != src:
+            host[a:b].copy_(stage[:b - a])
+    torch.cuda.synchronize()
+    return out
+

@@ -19,10 +19,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("nproc,launcher", [(2, "torchrun"), (2, "self"), (4, "self")])  # 4: halo path
+# 4: halo path; 8: the driver's node size (halo plans, train-column slots and row blocks
+# at the shapes of the 8-GPU scaling run)
+@pytest.mark.parametrize("nproc,launcher", [(2, "torchrun"), (2, "self"), (4, "self"), (8, "torchrun")])
 def test_bench_gloo_ranks_print_one_json_line(nproc, launcher):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    env["OMP_NUM_THREADS"] = "2"
+    env["OMP_NUM_THREADS"] = "1" if nproc > 4 else "2"
     args = ["bench.py", "--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--device", "cpu",
             "--scale", "0.002", "--hidden", "64"]
     if launcher == "torchrun":

@@ -278,3 +278,39 @@ def test_moment_matching_loss_b8():
     one = float(MomentMatchingLoss(x, y, 1))         # the reference's default returned 0 (off by one)
     assert one == pytest.approx(float(torch.sqrt(((x.mean(0) - y.mean(0)) ** 2).sum())), rel=1e-12)
     assert float(MomentMatchingLoss(x, y, 2)) > one
+
+
+def _dag_with_max_in(d, k, seed):
+    """A DAG over d variables whose node d-1 has k parents, every other node <= 2."""
+    rng = np.random.default_rng(seed)
+    g = DirectedGraph()
+    names = ["V%d" % i for i in range(d)]
+    for i in range(1, d - 1):
+        for p in rng.choice(i, size=min(i, 2), replace=False):
+            g.add(names[int(p)], names[i])
+    for p in rng.choice(d - 1, size=k, replace=False):
+        g.add(names[int(p)], names[d - 1])
+    return g
+
+
+def test_device_batches_keep_each_program_on_its_own_kernel_family():
+    """the generator kernels (per-sample or level-scheduled) are chosen per
+    program, never from batch-wide maxima, so a candidate's score cannot depend on its
+    batch-mates: d = 140 programs with 4 and 20 inputs on one node fall in different
+    families and are batched apart, and every batch's combined shape keeps its family."""
+    from cgnn_amd.engine.batch import kernel_family
+    from cgnn_amd.engine.scorer import Job, _group_batches
+    d, H, N = 140, 20, 50
+    progs = [program_for_dag(_dag_with_max_in(d, k, s), H) for s, k in enumerate([3, 19, 3, 19, 3, 3, 19])]
+    fams = [kernel_family(d, H, p.max_in, len(p.prog)) for p in progs]
+    assert sorted(set(fams)) == [1, 2], fams
+    data = np.zeros((d, N), np.float32)
+    jobs = [Job(p, data, (0, i)) for i, p in enumerate(progs)]
+    batches = _group_batches(jobs, 16, H=H)
+    assert sorted(i for b in batches for i in b) == list(range(len(jobs)))
+    for b in batches:
+        assert len({fams[i] for i in b}) == 1, (b, fams)
+        ps = [progs[i] for i in b]
+        assert kernel_family(d, H, max(p.max_in for p in ps), max(len(p.prog) for p in ps)) == fams[b[0]]
+    # without H (the CPU reference path) only the shape matters
+    assert len(_group_batches(jobs, 16)) == 1

@@ -25,7 +25,7 @@ def _init(rank, world, port):
     os.environ["WORLD_SIZE"] = str(world)
     os.environ["LOCAL_RANK"] = str(rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.set_num_threads(2)
+    torch.set_num_threads(max(1, min(2, 8 // world)))
 
 
 def _score_worker(rank, world, port, out):
@@ -95,7 +95,7 @@ def _gcn_worker(rank, world, port, out, halo=None, strip=False, kw=None):
 @pytest.mark.parametrize("world,halo,overlap,all_rows,train_halo", [
     (2, False, "0", "0", "0"), (2, True, "0", "0", "0"), (4, None, "0", "0", "0"), (2, False, "1", "0", "1"),
     (4, None, "1", "0", "1"), (2, True, "1", "1", "1"), (4, None, "1", "1", "1"), (3, True, "1", "0", "1"),
-    (3, None, "1", "0", "strip")])
+    (3, None, "1", "0", "strip"), (8, None, "1", "0", "1"), (8, None, "1", "0", "strip")])
 def test_gcn_row_partition_matches_single_process(world, halo, overlap, all_rows, train_halo):
     """Row-partitioned GCN over gloo ranks == one process; layer-2 rows of other
     ranks by all-gather or by the halo all-to-all (the default from 4 ranks); the
@@ -222,9 +222,10 @@ def test_grad_bucketer_averages_gradients():
 
 def _sage_dp_worker(rank, world, port, out):
     _init(rank, world, port)
+    torch.set_num_threads(1)
     from cgnn_amd.gnn.data import synthetic
     from cgnn_amd.gnn.sage import SAGETrainer
-    g = synthetic("ogbn-products", seed=0, scale=0.001)
+    g = synthetic("ogbn-products", seed=0, scale=0.001 if world <= 2 else 0.004)
     tr = SAGETrainer(g, hidden=32, layers=3, fanouts=(5, 4, 3), batch_size=64, seed=rank * 7, prefetch=False)
     n_batches = len(tr._batches())
     l0 = tr.train_epoch()
@@ -233,16 +234,18 @@ def _sage_dp_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_sage_data_parallel_keeps_replicas_identical():
-    """3-layer SAGE mini-batch DP over 2 gloo ranks (different init seeds are
-    overwritten by rank 0's broadcast): same number of steps on both ranks, and
+@pytest.mark.parametrize("world", [2, 8])
+def test_sage_data_parallel_keeps_replicas_identical(world):
+    """3-layer SAGE mini-batch DP over 2 and 8 gloo ranks (different init seeds are
+    overwritten by rank 0's broadcast): same number of steps on every rank, and
     the averaged gradients keep the replicas bitwise identical."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_sage_dp_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    assert out[0][0] == out[1][0] > 0
-    np.testing.assert_array_equal(out[0][3], out[1][3])
-    assert np.isfinite(out[0][1]) and np.isfinite(out[1][2])
+    mp.spawn(_sage_dp_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    assert all(out[r][0] == out[0][0] > 0 for r in range(world))
+    for r in range(1, world):
+        np.testing.assert_array_equal(out[0][3], out[r][3])
+    assert np.isfinite(out[0][1]) and np.isfinite(out[0][2])
 
 
 def _gat_params(tr):
@@ -312,7 +315,7 @@ def test_sharded_gat_matches_single_process(world, chunk):
 @pytest.mark.parametrize("world,chunk,strip,l1x", [(2, 4 << 30, False, False), (4, 4 << 30, False, False),
                                                    (2, 16 << 10, False, False), (4, 16 << 10, False, False),
                                                    (3, 4 << 30, True, False), (2, 4 << 30, False, True),
-                                                   (4, 16 << 10, False, True)])
+                                                   (4, 16 << 10, False, True), (8, 16 << 10, False, False)])
 def test_sharded_fused_gat_matches_single_process(world, chunk, strip, l1x):
     """The fused GAT epoch (gat_fused: every dense op a HIP kernel on a GPU; its fp32
     reference branches here) sharded over gloo ranks equals the one-process fused
@@ -366,7 +369,7 @@ def test_sharded_fused_gat_matches_single_process(world, chunk, strip, l1x):
     np.testing.assert_array_equal(out[0][2], out[1][2])
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_fused_gat_locality_partition_matches_single_process(world):
     """Shards of the locality partition (partition_order: the reorder pass over the
     graph's structure, computed by every rank on its own) train like the one-process
@@ -447,3 +450,34 @@ def test_collectives_selftest_gloo_two_ranks():
     mp.spawn(_selftest_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     for r in range(2):
         assert out[r]["backend"] == "gloo" and out[r]["world_size"] == 2, out[r]
+
+
+def _order_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from cgnn_amd.gnn import data
+    calls = []
+    real = data.partition_order
+
+    def counted(*a, **k):
+        calls.append(rank)
+        return real(*a, **k)
+
+    data.partition_order = counted
+    order = data.shared_partition_order("ogbn-products", seed=3, scale=0.002)
+    out[rank] = (order, list(calls))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shared_partition_order_runs_once_and_broadcasts(world):
+    """The papers100M locality partition is computed by rank 0 only and broadcast
+    (every rank recomputed the whole 111 M-node pass): every rank gets
+    the one-process order."""
+    from cgnn_amd.gnn.data import partition_order
+    ref = partition_order("ogbn-products", seed=3, scale=0.002)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_order_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        np.testing.assert_array_equal(out[r][0], ref)
+        assert out[r][1] == ([0] if r == 0 else [])

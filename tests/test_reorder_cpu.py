@@ -152,3 +152,18 @@ def test_median_refinement_is_a_permutation_and_narrows_the_band():
     lb = locality(g, w, new_id=base.numpy())
     lr = locality(g, w, new_id=nid.numpy())
     assert lr[64] > lb[64] and lr[256] > lb[256], (lb, lr)
+
+
+def test_shard_rejects_an_order_that_is_not_a_permutation():
+    """a duplicate or out-of-range entry in ``order`` would leave rows without
+    ids (split mask and labels read garbage): the generator refuses it."""
+    from cgnn_amd.gnn.data import partition_order, synthetic_shard
+    order = partition_order("ogbn-products", seed=5, scale=0.002)
+    bad = order.copy()
+    bad[1] = bad[0]                                   # a duplicate
+    with pytest.raises(ValueError, match="permutation"):
+        synthetic_shard("ogbn-products", 0, 2, seed=5, scale=0.002, order=bad)
+    bad = order.copy()
+    bad[3] = len(order)                               # out of range
+    with pytest.raises(ValueError, match="permutation"):
+        synthetic_shard("ogbn-products", 0, 2, seed=5, scale=0.002, order=bad)

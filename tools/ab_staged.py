@@ -21,7 +21,6 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="", help="kernel:W:placement, e.g. bwd:4:2 (profiling runs)")
     a = ap.parse_args()
-    os.environ["CGNN_GEN_STAGED"] = "1"
     import numpy as np
     import torch
     from bench_cgnn_batch import random_dag_program
@@ -32,7 +31,7 @@ def main():
     prog = random_dag_program(a.d, a.edges, a.h, 0, 0)
     data = np.random.default_rng(1).normal(size=(a.d, a.n)).astype(np.float32)
     tr = DeviceTrainer([prog] * a.R, [data] * a.R, [model_key(0, r) for r in range(a.R)], a.h, "cuda:0",
-                       graph_chunk=0)
+                       graph_chunk=0, generator="staged")
     tr.run(3, 1)
     torch.cuda.synchronize()
     st = torch.cuda.current_stream().cuda_stream

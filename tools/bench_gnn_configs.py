@@ -92,6 +92,8 @@ def main():
     if world > 1:
         pdist.init_process_group("gloo" if (cpu or a.shared_gpu) else "nccl")
     rank = pdist.rank()
+    if world > 1 and os.environ.get("OMP_NUM_THREADS") == "1":
+        pdist.set_host_threads()          # this rank's share of the cores (torchrun pins 1)
     if cpu:
         dev = torch.device("cpu")
     else:
@@ -193,13 +195,20 @@ def main():
         t0 = time.perf_counter()
         order = None
         if a.partition == "locality":
-            from cgnn_amd.gnn.data import partition_order
-            order = partition_order("ogbn-papers100M", seed=a.seed, scale=a.scale)
+            # once per job (rank 0, every core) and broadcast: each rank computing the
+            # whole 111 M-node pass held its own 13 GB structure and ran it on 1/8 of the cores
+            from cgnn_amd.gnn.data import shared_partition_order
+            order = shared_partition_order("ogbn-papers100M", seed=a.seed, scale=a.scale)
         part_s = time.perf_counter() - t0
         shard = synthetic_shard("ogbn-papers100M", srank, sworld, seed=a.seed, device=dev, scale=a.scale,
                                 order=order)
         del order
         gen_s = time.perf_counter() - t0 - part_s
+        if world > 1:                     # every rank's setup split, reported by rank 0
+            import torch.distributed as dist
+            split = [None] * world
+            dist.all_gather_object(split, {"partition_s": round(part_s, 2), "gen_s": round(gen_s, 2)})
+            res["setup_per_rank"] = split
         n_nodes, nnz_local, n_local = shard.n, shard.nnz, shard.n_local
         tr = ShardedGATTrainer(shard, heads=4, head_dim=32, dropout=0.5, lr=0.005, seed=a.seed, emulate=emu,
                                fused=False if a.unfused else None)
@@ -219,7 +228,8 @@ def main():
                    if dev.type == "cuda" else "fp32",
                    peak_gpu_mem_gib=round(peak, 2) if peak is not None else None,
                    shard={"rank": srank, "world": sworld, "rows": n_local, "nnz": nnz_local, "gen_s": round(gen_s, 2),
-                          "partition": a.partition, "partition_s": round(part_s, 2), "rank_local_generation": True},
+                          "partition": a.partition, "partition_s": round(part_s, 2), "rank_local_generation": True,
+                          "partition_computed_by": "rank 0, broadcast" if world > 1 else "this process"},
                    halo=tr.halo_stats(), emulated=emu is not None, reordered=a.partition == "locality",
                    fused=tr.fused is not None,
                    layer1_train_pruned=bool(tr.fused is not None and tr.fused._g1 is not None),
