@@ -153,13 +153,10 @@ __device__ __forceinline__ void gather_sum(const int* __restrict__ col, const vo
     if ((U == 8 || U == 16) && L >= 8) {
       for (; k + 8 <= cnt; k += 8) {
         int j[8];
-#ifdef GATHER_DPP
-        if (L == 16 && !CS) {
+        if (L == 16 && !CS) {        // the ids by DPP row broadcast: no LDS permutes
           if (k == 0) row_bcast8<0>(myj, j);
           else row_bcast8<8>(myj, j);
-        } else
-#endif
-        {
+        } else {
 #pragma unroll
           for (int u = 0; u < 8; ++u) j[u] = __shfl(myj, sub_base + k + u, 64);
         }

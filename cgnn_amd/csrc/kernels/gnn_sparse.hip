@@ -471,7 +471,8 @@ __global__ void cast_bf16_kernel(const float* __restrict__ src, uint16_t* __rest
 // ---------------------------------------------------------------- launchers
 // Gathers unrolled 8 rows deep, the next chunk's column ids requested during the current
 // chunk's gathers (round 4: headline +1-5 %, arxiv +1.2 %, profiles/r04_spmm).  Measured
-// alternatives, kept out: 4 deep (slower on the products shape), and round 2's
+// alternatives, kept out: 16 deep (2.21 vs 2.05 ms on the products layer 1, round 5: 82
+// VGPRs, 5 waves / SIMD), 4 deep (slower on the products shape), and round 2's
 // software-pipelined gather that combined the early column ids with non-temporal index
 // loads / output stores and 16 raw rows in flight per lane: 30 % SLOWER (F = 100: 3.43 vs
 // 2.64 ms) -- non-temporal stores alone double a store-heavy kernel's time (r04_lin).
@@ -506,11 +507,6 @@ static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void*
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
                          int relu, int uc, int wc, const float* init, int ldi, const float* cs, int ir,
                          hipStream_t st) {
-#ifdef SPMM_U16
-  if (L == 16 && xbf == 1 && ybf == 1 && !cs)
-    return spmm_dispatch_u<L, 16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
-                                  ldi, cs, ir, st);
-#endif
   return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
                                ldi, cs, ir, st);
 }

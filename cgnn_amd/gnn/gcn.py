@@ -200,7 +200,11 @@ class GCNTrainer:
         # (Measured, not kept: on one GPU the same double buffer filled on a side stream,
         # so the next epoch's layer-1 aggregation overlaps this epoch's dense kernels --
         # neutral, 208.2 vs 208.8 epochs/s: the SpMM's blocks occupy every CU and the dense
-        # forward only starts as they drain.)
+        # forward only starts as they drain.  Round 5: started after the dense forward,
+        # beside the latency-bound layer-2 / transposed aggregations, with the epoch's chain
+        # on a high-priority stream -- neutral again, 315.5 vs 315.6: the dispatcher shares
+        # the CUs between the two queues regardless of priority, the transposed aggregation
+        # stretched from 0.23 to 2.18 ms beside the SpMM (profiles/r05_pref).)
         self.AX_next = torch.zeros_like(self.AX) if self.multi else None
         self._ax_ready = False
         if self.multi:

@@ -686,3 +686,4 @@ def test_gcn_fused_aggregation_trains_bitwise_like_two_kernels():
     assert torch.equal(a.params, b.params)
     ea, eb = a.evaluate(), b.evaluate()
     assert ea == eb
+
