@@ -58,7 +58,8 @@ void cgnn_engine_run(void*, int, int, int, int);
 // Fourier (random-feature) MMD
 int rff_launch_freqs(float*, const uint32_t*, const int*, int, int, int, int, int, int, hipStream_t);
 int rff_launch_fwd_bwd(int, const float*, const float*, const float*, float*, float*, float*, int,
-                       int, int, int, int, float, hipStream_t, int);
+                       int, int, int, int, float, hipStream_t, int, float*, int);
+long rff_wide_scratch_floats(int, int, int);
 // GNN track
 int gnn_launch_spmm(const int*, const int*, const void*, void*, const float*, const float*, int,
                     int, int, int, int, int, int, int, const float*, int, const float*, int, int, hipStream_t);
@@ -134,7 +135,7 @@ static void chk(int rc, const char* what) {
 class PyEngine {
  public:
   PyEngine(std::vector<int> icfg, std::vector<float> fcfg, std::vector<uint64_t> ptrs, uint64_t stream) {
-    if (icfg.size() < 21 || fcfg.size() < 5 || ptrs.size() < 22) throw std::invalid_argument("engine config size");
+    if (icfg.size() < 21 || fcfg.size() < 5 || ptrs.size() < 23) throw std::invalid_argument("engine config size");
     std::vector<const void*> p(ptrs.size());
     for (size_t k = 0; k < ptrs.size(); ++k) p[k] = reinterpret_cast<const void*>(ptrs[k]);
     h_ = cgnn_engine_create(icfg.data(), fcfg.data(), p.data(), S(stream));
@@ -266,14 +267,15 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("rff_fwd_bwd", [](int mode, uint64_t xhat, uint64_t data, uint64_t w, uint64_t feat, uint64_t loss,
                           uint64_t grad, int N, int D, int F, int R, int k, float norm, uint64_t st,
-                          int force_valu) {
+                          int force_valu, uint64_t scratch, int force_wide) {
     chk(rff_launch_fwd_bwd(mode, Pt<const float>(xhat), Pt<const float>(data), Pt<const float>(w),
                            Pt<float>(feat), Pt<float>(loss), Pt<float>(grad), N, D, F, R, k, norm, S(st),
-                           force_valu),
+                           force_valu, Pt<float>(scratch), force_wide),
         "rff_fwd_bwd");
   }, py::arg("mode"), py::arg("xhat"), py::arg("data"), py::arg("w"), py::arg("feat"), py::arg("loss"),
      py::arg("grad"), py::arg("N"), py::arg("D"), py::arg("F"), py::arg("R"), py::arg("k"), py::arg("norm"),
-     py::arg("st"), py::arg("force_valu") = 0);
+     py::arg("st"), py::arg("force_valu") = 0, py::arg("scratch") = 0, py::arg("force_wide") = 0);
+  m.def("rff_wide_scratch_floats", &rff_wide_scratch_floats);
 
   m.def("gnn_spmm", [](uint64_t rowptr, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, uint64_t bias,
                        int n_rows, int F, int ld_x, int ld_y, int x_bf16, int y_bf16, int relu, int unit_col,

@@ -47,7 +47,7 @@ int cgnn_launch_init(float*, float*, float*, const int*, int, int, const uint32_
 int cgnn_launch_advance(int*, int, int, hipStream_t);
 int rff_launch_freqs(float*, const uint32_t*, const int*, int, int, int, int, int, int, hipStream_t);
 int rff_launch_fwd_bwd(int, const float*, const float*, const float*, float*, float*, float*, int,
-                       int, int, int, int, float, hipStream_t, int);
+                       int, int, int, int, float, hipStream_t, int, float*, int);
 }
 
 namespace cgnn {
@@ -86,6 +86,7 @@ struct EngineBuffers {
   const uint32_t* keys = nullptr;
   float* rff_w = nullptr;       // [R][7k][D+1]
   float* rff_diff = nullptr;    // [R][7k]
+  float* rff_scratch = nullptr; // wide joints (D > 256): rff_wide_scratch_floats(N, 7k, R)
   float* xnorm = nullptr;       // [R][N] squared norms of xhat rows (written by gen_fwd)
   const float* ynorm = nullptr; // [R][N] squared norms of the data rows
   float* dxs = nullptr;         // [R][d_true][N] dL/dx scratch of a staged backward whose state is global
@@ -131,7 +132,7 @@ class Engine {
                              c_.R, st_), "rff_freqs");
       check(rff_launch_fwd_bwd(train ? 0 : 1, b_.xhat, b_.data, b_.rff_w, b_.rff_diff, b_.lpart,
                                b_.gradp, c_.N, c_.D, rff_features(), c_.R, c_.rff_k,
-                               sqrtf(2.f / (float)c_.rff_k), st_, 0), "rff");
+                               sqrtf(2.f / (float)c_.rff_k), st_, 0, b_.rff_scratch, 0), "rff");
     } else if (c_.mfma) {
       const float inv = 1.f / ((float)c_.N * (float)c_.N);
       check(cgnn_launch_mmd_mfma(train ? (need_loss ? 0 : 3) : 1, c_.D, b_.xhat, b_.data, b_.xnorm, b_.ynorm,
@@ -282,7 +283,7 @@ extern "C" void* cgnn_engine_create(const int* icfg, const float* fcfg, const vo
   b.loss_acc = (float*)ptrs[12]; b.loss_hist = (float*)ptrs[13]; b.step = (int*)ptrs[14];
   b.keys = (const uint32_t*)ptrs[15]; b.rff_w = (float*)ptrs[16]; b.rff_diff = (float*)ptrs[17];
   b.xnorm = (float*)ptrs[18]; b.ynorm = (const float*)ptrs[19]; b.dxs = (float*)ptrs[20];
-  b.sched = (const int*)ptrs[21];
+  b.sched = (const int*)ptrs[21]; b.rff_scratch = (float*)ptrs[22];
   return new cgnn::Engine(c, b, st);
 }
 

@@ -566,14 +566,18 @@ extern "C" int cgnn_staged_plan(int Dt, int H, int max_in, int W, int extra, int
   // resident wins (d = 200, H = 20: sample state in LDS at 4 waves / CU 3.76 ms, in
   // global memory at 16 waves / CU 1.59 ms; profiles/r04_cgnn_wide), at most 4 waves
   // per block (wider blocks idle on the narrow sub-stages); ties keep the LDS state
-  const int wb = std::min(W, 4);
+  // Nodes with many inputs (a slab per wave grows with max_in) take narrower blocks
+  // before giving up: 4, 2, then 1 wave per block.
   const int cap = 16;                    // ~120 VGPRs: 4 waves per SIMD
-  int best = -1, best_waves = 0;
-  for (int place = 0; place < 3; ++place) {
-    const size_t lds = bwd_lds(Dt, wb, max_in, place >= 1, place == 2, extra);
-    if (lds > LDS_MAX) continue;
-    const int waves = std::min(cap, (int)(LDS_MAX / lds) * wb);
-    if (waves > best_waves) { best = place; best_waves = waves; }
+  int best = -1, best_waves = 0, wb = std::min(W, 4);
+  for (; wb >= 1 && best < 0; wb /= 2) {
+    for (int place = 0; place < 3; ++place) {
+      const size_t lds = bwd_lds(Dt, wb, max_in, place >= 1, place == 2, extra);
+      if (lds > LDS_MAX) continue;
+      const int waves = std::min(cap, (int)(LDS_MAX / lds) * wb);
+      if (waves > best_waves) { best = place; best_waves = waves; }
+    }
+    if (best >= 0) break;
   }
   if (best < 0) return -1;
   out[0] = fxg; out[1] = best >= 1; out[2] = best == 2; out[3] = W; out[4] = wb;

@@ -332,6 +332,8 @@ __device__ __forceinline__ f4v mma16(h8 a, h8 b, f4v c) {
 }
 
 // half offset of (row j, chunk c of 8 halfs) in a [32][ZS] image: skew 2 (j & 7) chunks
+constexpr int MMD_MAX_D = 16384;
+
 template <int ZS>
 __device__ __forceinline__ int zoff(int j, int c) { return j * ZS + 8 * (c + 2 * (j & 7)); }
 
@@ -575,15 +577,18 @@ __global__ __launch_bounds__(512) void mmd_mfma16_kernel(
 // block's own group is staged last, so the gradient reads it from the same LDS image.
 // Staging is synchronous (no register prefetch): two blocks per CU overlap it.
 // ============================================================================
-template <int KD, int MODE>
+// KD (the padded joint width, a multiple of 256 here) is a launch argument: the groups
+// are walked by a rolled loop, so one instantiation covers every width above 256.
+template <int MODE>
 __global__ __launch_bounds__(512) void mmd_mfma16g_kernel(
     const float* __restrict__ xhat, const float* __restrict__ data,
     const float* __restrict__ xnorm, const float* __restrict__ ynorm,
     float* __restrict__ grad_part, float* __restrict__ loss_part,
-    int N, int R, int tiles_per_chunk, float grad_scale, int row_begin, int n_rows) {
+    int N, int R, int tiles_per_chunk, float grad_scale, int row_begin, int n_rows, int KD) {
   constexpr bool GRAD = MODE == 0 || MODE == 3;
   constexpr bool LOSS = MODE != 3;
-  constexpr int KG = 256, NG = (KD + KG - 1) / KG;
+  constexpr int KG = 256;
+  const int NG = (KD + KG - 1) / KG;
   constexpr int ZS = (KG + 14 * 8 + 127) / 128 * 128;       // 384 halfs per skewed row
   constexpr int NCH = KG / 8;                                // 32 chunks per row
   constexpr int TPT = MT * NCH / 512;                        // 2 staging tasks per thread
@@ -761,22 +766,31 @@ __global__ __launch_bounds__(512) void mmd_mfma16g_kernel(
   }
 }
 
+// the dimension-grouped kernel for any padded width KD > 256 (a multiple of 256)
+int launch_mmd_mfma_grouped(int mode, int KD, const float* xhat, const float* data, const float* xn,
+                            const float* yn, float* gpart, float* lpart, int N, int R, int n_chunks, int tpc,
+                            float gscale, int row_begin, int n_rows, hipStream_t st) {
+  const int n_rb = (n_rows + WAVES * MT - 1) / (WAVES * MT);
+  const int NG = (KD + 255) / 256;
+  dim3 grid(n_rb * NG, n_chunks, R), block(512);
+#define WIDEG(M, A, B, C, D2) hipLaunchKernelGGL((mmd_mfma16g_kernel<M>), grid, block, 0, st, A, B, C, D2, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows, KD)
+  if (mode == 0) WIDEG(0, xhat, data, xn, yn);
+  else if (mode == 3) WIDEG(3, xhat, data, xn, yn);
+  else if (mode == 1) WIDEG(1, xhat, data, xn, yn);
+  else if (mode == 2) WIDEG(2, data, data, yn, yn);
+  else return -3;
+#undef WIDEG
+  return (int)hipGetLastError();
+}
+
 template <int KD>
 int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const float* xn, const float* yn,
                       float* gpart, float* lpart, int N, int R, int n_chunks, int tpc, float gscale,
                       int row_begin, int n_rows, hipStream_t st, int wide) {
   const int n_rb = (n_rows + WAVES * MT - 1) / (WAVES * MT);
   if constexpr (KD > 256) {
-    constexpr int NG = (KD + 255) / 256;
-    dim3 grid(n_rb * NG, n_chunks, R), block(512);
-#define WIDEG(M, A, B, C, D2) hipLaunchKernelGGL((mmd_mfma16g_kernel<KD, M>), grid, block, 0, st, A, B, C, D2, gpart, lpart, N, R, tpc, gscale, row_begin, n_rows)
-    if (mode == 0) WIDEG(0, xhat, data, xn, yn);
-    else if (mode == 3) WIDEG(3, xhat, data, xn, yn);
-    else if (mode == 1) WIDEG(1, xhat, data, xn, yn);
-    else if (mode == 2) WIDEG(2, data, data, yn, yn);
-    else return -3;
-#undef WIDEG
-    return (int)hipGetLastError();
+    return launch_mmd_mfma_grouped(mode, KD, xhat, data, xn, yn, gpart, lpart, N, R, n_chunks, tpc, gscale,
+                                   row_begin, n_rows, st);
   }
   if (wide < 0) wide = KD >= 128;
   if (KD >= 128 && wide) {
@@ -812,13 +826,13 @@ int launch_mmd_mfma_d(int mode, const float* xhat, const float* data, const floa
 }  // namespace
 
 // Supported widths (the padded D of engine/batch.py SUPPORTED_D, >= 8; above 64 the
-// matrix-core kernel is the only MMD)
+// matrix-core kernel is the only MMD; above 1024 every multiple of 256 up to MMD_MAX_D)
 extern "C" int cgnn_mmd_mfma_supported(int D) {
   switch (D) {
     case 8: case 12: case 16: case 20: case 24: case 32: case 48: case 64:
     case 80: case 96: case 128: case 160: case 192: case 224: case 256:
     case 320: case 384: case 448: case 512: case 640: case 768: case 896: case 1024: return 1;
-    default: return 0;
+    default: return D > 1024 && D % 256 == 0 && D <= MMD_MAX_D;
   }
 }
 
@@ -838,7 +852,11 @@ extern "C" int cgnn_launch_mmd_mfma_rows(int mode, int D, const float* xhat, con
     CASE_D(80) CASE_D(96) CASE_D(128) CASE_D(160) CASE_D(192) CASE_D(224) CASE_D(256)
     CASE_D(320) CASE_D(384) CASE_D(448) CASE_D(512) CASE_D(640) CASE_D(768) CASE_D(896) CASE_D(1024)
 #undef CASE_D
-    default: return -1;
+    default:
+      if (D > 1024 && D % 256 == 0 && D <= MMD_MAX_D)
+        return launch_mmd_mfma_grouped(mode, D, xhat, data, xnorm, ynorm, gpart, lpart, N, R, n_chunks, tpc, gscale,
+                                       row_begin, n_rows, st);
+      return -1;
   }
 }
 

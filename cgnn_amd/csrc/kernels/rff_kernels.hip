@@ -271,6 +271,162 @@ __global__ __launch_bounds__(256) void rff_mfma_grad_kernel(const float* __restr
     }
 }
 
+// ============================================================================
+// Wide joints (D > 256; CGNN builds one MLP per variable for any d, CGNN.py:63-90): the
+// per-lane W column / accumulator forms above stop at D = 256 (registers), so the
+// projections go through a scratch image instead:
+//   proj:   theta[n][f] = [x_n | 1] . W[f]   (matrix cores, W staged in LDS in k-chunks)
+//           csum[part][nt][f] = sum over the 32 samples of tile nt of cos(theta)
+//           theta of the generated samples kept for the gradient ([R][N][F])
+//   reduce: diff_f = norm (sum_nt csum[0] - sum_nt csum[1]) / N in fixed order, the
+//           loss partials per 256-feature group (the layout of the narrow forms)
+//   grad:   G[k][n] = sum_f W[f][k] S[n][f],  S = -coef diff_f sin(theta)  (matrix cores,
+//           the S tile staged in LDS per f-chunk)
+// All products on v_mfma_f32_32x32x2_f32 (exact fp32, sequential k order).
+// ============================================================================
+namespace {
+constexpr int RW_KC = 32;     // k-chunk of the staged W image (proj)
+constexpr int RW_FC = 64;     // f-chunk of the staged S tile (grad)
+}
+
+// grid (ceil(F / 256), ceil(N / 32), 2 R): block = 8 waves x 32 features, one 32-sample tile
+__global__ __launch_bounds__(512) void rff_wide_proj_kernel(const float* __restrict__ xhat,
+                                                            const float* __restrict__ data,
+                                                            const float* __restrict__ W, float* __restrict__ theta,
+                                                            float* __restrict__ csum, int N, int D, int F) {
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  __shared__ float sW[256 * (RW_KC + 1)];
+  const int part = blockIdx.z & 1, r = blockIdx.z >> 1, nt = blockIdx.y, fb = blockIdx.x;
+  const int NT = gridDim.y;
+  const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31, wv = threadIdx.x >> 6;
+  const int f = fb * 256 + wv * 32 + lr;
+  const int n = nt * 32 + lr;
+  const float* X = (part == 0 ? xhat : data) + (size_t)r * D * N;
+  const float* Wr = W + (size_t)r * F * (D + 1);
+  f32x16 c = {};
+  for (int kc = 0; kc <= D; kc += RW_KC) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 256 * RW_KC; i += 512) {
+      const int fl = i / RW_KC, kk = i - fl * RW_KC;
+      const int fg = fb * 256 + fl, k = kc + kk;
+      sW[fl * (RW_KC + 1) + kk] = (fg < F && k <= D) ? Wr[(size_t)fg * (D + 1) + k] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < RW_KC / 2; ++s) {
+      const int k = kc + 2 * s + h;
+      const float a = n < N ? (k < D ? X[(size_t)k * N + n] : (k == D ? 1.f : 0.f)) : 0.f;
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, sW[(wv * 32 + lr) * (RW_KC + 1) + 2 * s + h], c, 0, 0, 0);
+    }
+  }
+  // lane = feature f, registers = 16 samples of the tile
+  float acc = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int nn = nt * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    acc += nn < N ? cos_rev(c[q]) : 0.f;
+  }
+  acc += __shfl_xor(acc, 32, 64);
+  if (h == 0 && f < F) csum[(((size_t)r * 2 + part) * NT + nt) * F + f] = acc;
+  if (part == 0 && f < F) {
+    float* th = theta + (size_t)r * N * F;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int nn = nt * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (nn < N) th[(size_t)nn * F + f] = c[q];
+    }
+  }
+}
+
+// grid (ceil(F / 256), R), 256 threads: diff and the loss partial of a 256-feature group
+__global__ __launch_bounds__(256) void rff_wide_reduce_kernel(const float* __restrict__ csum,
+                                                              float* __restrict__ diff,
+                                                              float* __restrict__ loss_part, int N, int F, int NT,
+                                                              float norm) {
+  __shared__ float s_red[4];
+  const int r = blockIdx.y;
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  float dlt = 0.f;
+  if (f < F) {
+    const float* cp = csum + (size_t)r * 2 * NT * F + f;
+    float sp = 0.f, st = 0.f;
+    for (int t = 0; t < NT; ++t) {
+      sp += cp[(size_t)t * F];
+      st += cp[(size_t)(NT + t) * F];
+    }
+    dlt = norm * (sp - st) / (float)N;
+    diff[(size_t)r * F + f] = dlt;
+  }
+  const float v = wave_sum(dlt * dlt);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    loss_part[(size_t)r * gridDim.x + blockIdx.x] = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+}
+
+// grid (ceil(D / 256), ceil(N / 32), R): block = 8 waves x 32 gradient rows k, one
+// 32-sample tile; G[k][n] into grad [R][D][N]
+__global__ __launch_bounds__(512) void rff_wide_grad_kernel(const float* __restrict__ theta,
+                                                            const float* __restrict__ W,
+                                                            const float* __restrict__ diff, float* __restrict__ grad,
+                                                            int N, int D, int F, float coef) {
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  __shared__ float sS[32 * (RW_FC + 1)];
+  const int r = blockIdx.z, nt = blockIdx.y;
+  const int lane = threadIdx.x & 63, h = lane >> 5, lr = lane & 31, wv = threadIdx.x >> 6;
+  const int k0 = blockIdx.x * 256 + wv * 32;
+  const float* th = theta + (size_t)r * N * F;
+  const float* Wr = W + (size_t)r * F * (D + 1);
+  const float* dr = diff + (size_t)r * F;
+  f32x16 g = {};
+  for (int fc = 0; fc < F; fc += RW_FC) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 32 * RW_FC; i += 512) {
+      const int nl = i / RW_FC, ff = i - nl * RW_FC;
+      const int nn = nt * 32 + nl, fg = fc + ff;
+      sS[nl * (RW_FC + 1) + ff] = (nn < N && fg < F) ? -coef * dr[fg] * sin_rev(th[(size_t)nn * F + fg]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int s = 0; s < RW_FC / 2; ++s) {
+      const int fg = fc + 2 * s + h, k = k0 + lr;
+      const float a = (fg < F && k < D) ? Wr[(size_t)fg * (D + 1) + k] : 0.f;
+      g = __builtin_amdgcn_mfma_f32_32x32x2f32(a, sS[lr * (RW_FC + 1) + 2 * s + h], g, 0, 0, 0);
+    }
+  }
+  // lane = sample, registers = 16 gradient rows k
+  const int n = nt * 32 + lr;
+  if (n >= N) return;
+  float* gr = grad + (size_t)r * D * N;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int k = k0 + (q & 3) + 8 * (q >> 2) + 4 * h;
+    if (k < D) gr[(size_t)k * N + n] = g[q];
+  }
+}
+
+// scratch floats of the wide form (theta of the generated samples + the cos-sum partials)
+extern "C" long rff_wide_scratch_floats(int N, int F, int R) {
+  const long NT = (N + 31) / 32;
+  return (long)R * N * F + (long)R * 2 * NT * F;
+}
+
+static int rff_wide(int mode, const float* xhat, const float* data, const float* W, float* diff, float* loss_part,
+                    float* grad, int N, int D, int F, int R, float norm, float* scratch, hipStream_t st) {
+  if (!scratch) return -2;
+  const int NT = (N + 31) / 32;
+  float* theta = scratch;
+  float* csum = scratch + (size_t)R * N * F;
+  hipLaunchKernelGGL(rff_wide_proj_kernel, dim3((F + 255) / 256, NT, 2 * R), dim3(512), 0, st, xhat, data, W,
+                     theta, csum, N, D, F);
+  hipLaunchKernelGGL(rff_wide_reduce_kernel, dim3((F + 255) / 256, R), dim3(256), 0, st, csum, diff, loss_part, N,
+                     F, NT, norm);
+  if (mode == 0)
+    hipLaunchKernelGGL(rff_wide_grad_kernel, dim3((D + 255) / 256, NT, R), dim3(512), 0, st, theta, W, diff, grad,
+                       N, D, F, 2.f * norm / (float)N);
+  return (int)hipGetLastError();
+}
+
 extern "C" int rff_launch_freqs(float* W, const uint32_t* keys, const int* step_base, int step_off,
                                 int k, int D, int n_gamma, int d_true, int R, hipStream_t st) {
   const int tot = k * n_gamma * (D + 1);
@@ -315,10 +471,14 @@ static int rff_fb_d(int mode, const float* xhat, const float* data, const float*
 }
 
 // mode 0: loss partials + gradient; mode 1: loss partials only.  force_valu: the vector
-// kernels wherever they exist (D <= 64; A/B and tests)
+// kernels wherever they exist (D <= 64; A/B and tests).  D > 256 (any width): the wide
+// form, with `scratch` of rff_wide_scratch_floats(N, F, R) floats; force_wide = 1 takes
+// it at any D (tests: the two forms agree)
 extern "C" int rff_launch_fwd_bwd(int mode, const float* xhat, const float* data, const float* W,
                                   float* diff, float* loss_part, float* grad, int N, int D, int F,
-                                  int R, int k, float norm, hipStream_t st, int force_valu) {
+                                  int R, int k, float norm, hipStream_t st, int force_valu, float* scratch,
+                                  int force_wide) {
+  if (D > 256 || force_wide) return rff_wide(mode, xhat, data, W, diff, loss_part, grad, N, D, F, R, norm, scratch, st);
   switch (D) {
 #define CASE_D(d) case d: return rff_fb_d<d>(mode, xhat, data, W, diff, loss_part, grad, N, F, R, k, norm, st, force_valu);
     CASE_D(1) CASE_D(2) CASE_D(3) CASE_D(4) CASE_D(6) CASE_D(8) CASE_D(12) CASE_D(16) CASE_D(20)

@@ -18,10 +18,11 @@ from .. import native
 from .program import Program, pack_programs, pack_schedules
 
 # padded variable counts with compiled kernels; above 64 only the matrix-core MMD, above
-# 256 its dimension-grouped form (and no Fourier-feature MMD)
+# 256 its dimension-grouped form and the wide (scratch-image) Fourier-feature MMD
 SUPPORTED_D = (1, 2, 3, 4, 6, 8, 12, 16, 20, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256,
                320, 384, 448, 512, 640, 768, 896, 1024)
-MAX_RFF_D = 256
+MAX_D = 16384             # above 1024: every multiple of 256 (runtime-width grouped MMD)
+WIDE_RFF_D = 256          # above: rff_kernels.hip's wide form (theta scratch image)
 MAX_VALU_D = 64
 MMD_TILE = 256
 TARGET_WGS = 2048
@@ -31,7 +32,9 @@ def padded_dim(d: int) -> int:
     for D in SUPPORTED_D:
         if D >= d:
             return D
-    raise ValueError("CGNN device path supports at most %d variables (got %d)" % (SUPPORTED_D[-1], d))
+    if d <= MAX_D:
+        return (d + 255) // 256 * 256
+    raise ValueError("CGNN device path supports at most %d variables (got %d)" % (MAX_D, d))
 
 
 def mmd_geometry(N: int, R: int = 0):
@@ -102,10 +105,10 @@ def kernel_family(d: int, H: int, max_in: int, prog_len: int = 0) -> int:
 def device_supported(d: int, H: int, max_in: int, prog_len: int = 0, fast_mmd: bool = False) -> bool:
     """True when the device kernels cover a batch of ``d``-variable programs with hidden
     width ``H``, at most ``max_in`` generator inputs per node and programs of at most
-    ``prog_len`` ints: the variable count up to SUPPORTED_D[-1], and either the
+    ``prog_len`` ints: the variable count up to MAX_D, and either the
     per-sample generator kernels (sample state in LDS) or the level-scheduled ones.
     Otherwise ``score_jobs`` trains the batch on the CPU reference path (with a warning)."""
-    if d > SUPPORTED_D[-1] or (fast_mmd and padded_dim(d) > MAX_RFF_D):
+    if d > MAX_D:
         return False
     variant = kernel_family(d, H, max_in, prog_len)
     if variant == 1:
@@ -197,9 +200,6 @@ class DeviceTrainer:
             row_tiles, n_chunks, tpc = mmd_geometry(N, R)
             self.geometry = (row_tiles, n_chunks, tpc)
             self.rff_k = int(nb_vectors) if use_fast_mmd else 0
-            if self.rff_k and D > MAX_RFF_D:
-                raise native.NativeExtensionError(
-                    "Fourier-feature MMD covers at most %d (padded) variables, got %d" % (MAX_RFF_D, D))
             self.mmd_kernel = "rff" if self.rff_k else mmd_kernel_choice(D, mmd_kernel)
             mf_rb, mf_chunks, mf_tpc = mmd_mfma_geometry(N, R)
             F = 7 * self.rff_k
@@ -220,6 +220,9 @@ class DeviceTrainer:
             self.step = torch.zeros(2, dtype=torch.int32, device=dev)
             self.rff_w = torch.zeros(R, max(F, 1), D + 1, **f32)
             self.rff_diff = torch.zeros(R, max(F, 1), **f32)
+            # wide joints: theta of the generated samples + cos-sum partials
+            self.rff_scratch = (torch.zeros(hip.rff_wide_scratch_floats(N, F, R), **f32)
+                                if self.rff_k and D > WIDE_RFF_D else None)
             # squared row norms for the Gram-form (matrix-core) MMD
             self.xnorm = torch.zeros(R, N, **f32)
             self.ynorm = (self.data * self.data).sum(1).contiguous()
@@ -239,7 +242,8 @@ class DeviceTrainer:
             ptrs.append(self.hist.data_ptr() if self.hist_len else 0)
             ptrs += [self.step.data_ptr(), self.keys.data_ptr(), self.rff_w.data_ptr(),
                      self.rff_diff.data_ptr(), self.xnorm.data_ptr(), self.ynorm.data_ptr(),
-                     self.dxs.data_ptr() if self.dxs is not None else 0, self.sched.data_ptr()]
+                     self.dxs.data_ptr() if self.dxs is not None else 0, self.sched.data_ptr(),
+                     self.rff_scratch.data_ptr() if self.rff_scratch is not None else 0]
             self.engine = hip.CgnnEngine(icfg, fcfg, ptrs, stream.cuda_stream)
         self.graph_chunk = int(graph_chunk)
 

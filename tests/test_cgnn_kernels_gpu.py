@@ -291,3 +291,111 @@ def test_in_process_multi_device_round_robin_matches_one_device():
     assert np.all(np.isfinite(one))
     np.testing.assert_array_equal(one, two)
     np.testing.assert_array_equal(one, big)
+
+
+def test_multi_device_graph_search_matches_one_device():
+    """The reference's multi-GPU placement for the graph workload (run_CGNN_graph.py:7
+    sets NB_GPU = 2; runs go round-robin to /gpu:(run % NB_GPU), CGNN.py:187-188): the
+    public CGNN hill climbing with batches dealt over two device entries (device_ids
+    (0, 0): two streams on one MI355X) returns the same graph and scores as one device."""
+    import pandas as pd
+    import cgnn
+    rng = np.random.default_rng(11)
+    n = 300
+    a = rng.normal(size=n)
+    b = np.tanh(a) + 0.3 * rng.normal(size=n)
+    c = b ** 2 + 0.3 * rng.normal(size=n)
+    d = a - c + 0.3 * rng.normal(size=n)
+    df = pd.DataFrame({"A": a, "B": b, "C": c, "D": d})
+    dag = DirectedGraph()
+    for u, v, w in (("B", "A", 0.1), ("B", "C", 0.2), ("D", "C", 0.3), ("A", "D", 0.4)):
+        dag.add(u, v, w)
+    kw = dict(nb_runs=6, train_epochs=20, test_epochs=10, h_layer_dim=8, batch_models=2, gpu=True, seed=5)
+    m = cgnn.CGNN(backend="TensorFlow")
+    one = m.orient_directed_graph(df, dag, device_ids=(0,), **kw)
+    two = m.orient_directed_graph(df, dag, device_ids=(0, 0), **kw)
+    assert sorted(one.get_list_edges()) == sorted(two.get_list_edges())
+
+
+def _shared_gpu_score_worker(rank, world, port, out):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from cgnn_amd.engine.scorer import Job, score_jobs
+    from cgnn_amd.utils.settings import RunConfig
+    rng = np.random.default_rng(9)
+    jobs = [Job(program_for_pair(8), rng.normal(size=(2, 150)).astype(np.float32), model_key(4, r))
+            for r in range(7)]
+    g = DirectedGraph()
+    for u, v in (("V0", "V1"), ("V1", "V2"), ("V0", "V3")):
+        g.add(u, v)
+    jobs += [Job(program_for_dag(g, 8), rng.normal(size=(4, 150)).astype(np.float32), model_key(5, r))
+             for r in range(5)]
+    out[rank] = score_jobs(jobs, RunConfig(gpu=True, train_epochs=10, test_epochs=4, h_layer_dim=8,
+                                           batch_models=3)).tolist()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_sharing_the_gpu_score_like_one_process():
+    """One process per GPU (torchrun) shards the jobs by index over the ranks and
+    all-gathers the scores (parallel/dist.py): 2 gloo ranks sharing cuda:0 give every
+    rank the one-process scores, pairwise and graph jobs alike, bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    from cgnn_amd.engine.scorer import Job, score_jobs
+    from cgnn_amd.utils.settings import RunConfig
+    rng = np.random.default_rng(9)
+    jobs = [Job(program_for_pair(8), rng.normal(size=(2, 150)).astype(np.float32), model_key(4, r))
+            for r in range(7)]
+    g = DirectedGraph()
+    for u, v in (("V0", "V1"), ("V1", "V2"), ("V0", "V3")):
+        g.add(u, v)
+    jobs += [Job(program_for_dag(g, 8), rng.normal(size=(4, 150)).astype(np.float32), model_key(5, r))
+             for r in range(5)]
+    single = score_jobs(jobs, RunConfig(gpu=True, train_epochs=10, test_epochs=4, h_layer_dim=8, batch_models=3))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    mp.start_processes(_shared_gpu_score_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    assert np.all(np.isfinite(single))
+    for r in range(2):
+        np.testing.assert_array_equal(np.array(out[r]), single)
+
+
+@pytest.mark.parametrize("D", [12, 64, 256])
+def test_rff_wide_form_equals_narrow(D):
+    """The wide Fourier-feature form (theta scratch image; the only one above D = 256)
+    against the register forms on the same draws: same loss partials and gradient up to
+    summation order."""
+    hip = native.hip()
+    R, N, k = 2, 301, 40
+    F = 7 * k
+    torch.manual_seed(D + 1)
+    xhat = torch.randn(R, D, N, device="cuda") * 0.5
+    data = torch.randn(R, D, N, device="cuda") * 0.5 + 0.1
+    keys = torch.randint(0, 2**31 - 1, (R, 2), dtype=torch.int32, device="cuda")
+    step = torch.zeros(2, dtype=torch.int32, device="cuda")
+    W = torch.zeros(R, F, D + 1, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    hip.rff_freqs(W.data_ptr(), keys.data_ptr(), step.data_ptr(), 0, k, D, 7, D, R, st)
+    scratch = torch.zeros(hip.rff_wide_scratch_floats(N, F, R), device="cuda")
+    outs = []
+    for wide in (0, 1):
+        diff = torch.zeros(R, F, device="cuda")
+        lp = torch.zeros(R, (F + 255) // 256, device="cuda")
+        gp = torch.zeros(1, R, D, N, device="cuda")
+        hip.rff_fwd_bwd(0, xhat.data_ptr(), data.data_ptr(), W.data_ptr(), diff.data_ptr(), lp.data_ptr(),
+                        gp.data_ptr(), N, D, F, R, k, (2.0 / k) ** 0.5, st, scratch=scratch.data_ptr(),
+                        force_wide=wide)
+        outs.append((lp.sum(1), diff, gp))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(outs[1][0], outs[0][0], rtol=1e-4, atol=1e-7)
+    g = outs[0][2]
+    torch.testing.assert_close(outs[1][2], g, rtol=1e-3, atol=1e-4 * float(g.abs().max()))

@@ -217,3 +217,49 @@ def test_staged_score_independent_of_batch_mates():
     sa, sm = alone.run(6, 3), mixed.run(6, 3)
     np.testing.assert_array_equal(alone.history()[0], mixed.history()[0])
     assert sa[0] == sm[0]
+
+
+@pytest.mark.parametrize("d", [300, 512])
+def test_wide_fast_mmd_trainer_matches_oracle(d):
+    """use_Fast_MMD beyond 256 variables (Loss.py:47-56 has no width cap; CGNN.py:92-93
+    selects it for any graph): the wide Fourier-feature form trains on the GPU and matches
+    the fp64 oracle."""
+    H = 20
+    g = _random_dag(d, seed=d + 7)
+    prog = program_for_dag(g, H)
+    assert device_supported(d, H, prog.max_in, len(prog.prog), fast_mmd=True)
+    N = 120
+    datas = [_data(d, N, s) for s in range(2)]
+    keys = [model_key(17, "wrff", r) for r in range(2)]
+    kw = dict(use_fast_mmd=True, nb_vectors=25)
+    ref = ReferenceTrainer([prog] * 2, datas, keys, H, **kw)
+    ref_scores = ref.run(4, 2)
+    dev = DeviceTrainer([prog] * 2, datas, keys, H, "cuda:0", record_history=4, graph_chunk=2, **kw)
+    assert dev.mmd_kernel == "rff" and dev.rff_scratch is not None
+    scores = dev.run(4, 2)
+    hist, ref_hist = dev.history(), np.array(ref.loss_history)
+    # the first loss (same weights, same draws) to fp32 rounding; afterwards the fp32 and
+    # fp64 trajectories drift apart: with ~300 inputs the projections reach ~10^3 rad
+    # (frequencies 2 gamma N(0, 1), gamma up to 50, SURVEY B12), where cos / sin amplify
+    # the fp32 rounding of theta into the gradient
+    np.testing.assert_allclose(hist[:, 0], ref_hist[:, 0], rtol=1e-5)
+    np.testing.assert_allclose(hist, ref_hist, rtol=2e-2)
+    np.testing.assert_allclose(scores, ref_scores, rtol=2e-2)
+
+
+def test_exact_mmd_trainer_beyond_1024_matches_oracle():
+    """A 1500-variable DAG (padded 1536: the runtime-width grouped MMD) on the GPU
+    against the fp64 oracle."""
+    d, H, N = 1500, 8, 64
+    g = _random_dag(d, seed=3, max_par=2)
+    prog = program_for_dag(g, H)
+    assert padded_dim(d) == 1536 and device_supported(d, H, prog.max_in, len(prog.prog))
+    datas = [_data(d, N, s) for s in range(2)]
+    keys = [model_key(19, "x1500", r) for r in range(2)]
+    ref = ReferenceTrainer([prog] * 2, datas, keys, H)
+    ref_scores = ref.run(3, 2)
+    dev = DeviceTrainer([prog] * 2, datas, keys, H, "cuda:0", record_history=3, graph_chunk=0)
+    assert dev.mmd_kernel == "mfma" and dev.staged
+    scores = dev.run(3, 2)
+    np.testing.assert_allclose(dev.history(), np.array(ref.loss_history), rtol=3e-3, atol=1e-5)
+    np.testing.assert_allclose(scores, ref_scores, rtol=3e-3, atol=1e-5)

@@ -314,3 +314,14 @@ def test_device_batches_keep_each_program_on_its_own_kernel_family():
         assert kernel_family(d, H, max(p.max_in for p in ps), max(len(p.prog) for p in ps)) == fams[b[0]]
     # without H (the CPU reference path) only the shape matters
     assert len(_group_batches(jobs, 16)) == 1
+
+
+@pytest.mark.parametrize("fast", [False, True])
+def test_device_kernels_cover_every_width_to_2048(fast):
+    """no CPU fallback below realistic widths -- every d <= 2048 (exact or
+    Fourier MMD) has device kernels, for sparse DAGs and for nodes with many inputs."""
+    from cgnn_amd.engine.batch import device_supported
+    for d in (2, 22, 65, 200, 257, 300, 512, 1000, 1025, 1500, 2048):
+        for max_in in (2, 8, 64):
+            prog_len = 4 + 8 * d + d * min(max_in, d)
+            assert device_supported(d, 20, min(max_in, d + 1), prog_len, fast_mmd=fast), (d, max_in)
