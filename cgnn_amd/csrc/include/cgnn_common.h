@@ -155,7 +155,21 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
 // deals blocks round-robin over XCDs).  Returns a logical block id such that the
 // blocks resident on one XCD process a CONTIGUOUS range of the work.  Bijective
 // for any grid size (q = n/8, r = n%8).  Speed only -- never correctness.
+#ifndef CGNN_XCD_CHUNK
+#define CGNN_XCD_CHUNK 0
+#endif
 __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nwg) {
+  if constexpr (CGNN_XCD_CHUNK > 0) {
+    // (A/B variant) XCD x takes chunks x, x + 8, ... of CGNN_XCD_CHUNK consecutive
+    // blocks: contiguous work per chunk, spread over the whole range per XCD
+    constexpr unsigned C = CGNN_XCD_CHUNK;
+    const unsigned full = nwg / (8u * C) * (8u * C);
+    if (b < full) {
+      const unsigned xcd = b & 7u, idx = b >> 3;
+      return (idx / C) * (8u * C) + xcd * C + idx % C;
+    }
+    return b;                                   // the ragged tail: identity
+  }
   const unsigned q = nwg >> 3, r = nwg & 7u;
   const unsigned xcd = b & 7u, idx = b >> 3;
   const unsigned base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;

@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <stdint.h>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -104,7 +105,15 @@ int gnn_launch_halo_rows(const void*, long, const long*, void*, long, const long
 long gnn_sample_blocks_scratch(int, int, const int*, const int*);
 int gnn_launch_sample_blocks(const int*, const int*, int, const int*, int, int, const int*, const int*, int* const*,
                              float* const*, int* const*, int* const*, int* const*, int* const*, int* const*,
-                             int* const*, int*, uint8_t*, int*, int*, uint32_t, uint32_t, uint32_t, hipStream_t);
+                             int* const*, int*, uint8_t*, int*, int*, uint32_t, uint32_t, uint32_t, hipStream_t,
+                             int*);
+void* gnn_sw_create(int, hipStream_t, const int*, const int*, int, int, const int*, const int*, uint8_t*, int*, int*,
+                    uint32_t, uint32_t);
+int gnn_sw_add_slot(void*, int* const*, float* const*, int* const*, int* const*, int* const*, int* const*,
+                    int* const*, int* const*, int*, int*);
+long gnn_sw_submit(void*, int, const int*, int, uint32_t, const hipEvent_t*, int);
+int gnn_sw_wait(void*, long, int, hipStream_t);
+void gnn_sw_destroy(void*);
 int gnn_fused_bwd_blocks(int);
 int gnn_fused_bwd_width(int);
 int gnn_fused_bwd_supported(int, int, int);
@@ -279,16 +288,16 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("gnn_spmm", [](uint64_t rowptr, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, uint64_t bias,
                        int n_rows, int F, int ld_x, int ld_y, int x_bf16, int y_bf16, int relu, int unit_col,
-                       uint64_t st, uint64_t init, int ldi, uint64_t cscale, int init_rows, int slab) {
+                       uint64_t st, uint64_t init, int ldi, uint64_t cscale, int init_rows, int short_rows) {
     chk(gnn_launch_spmm(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(x), Pt<void>(y),
                         Pt<const float>(rscale), Pt<const float>(bias), n_rows, F, ld_x, ld_y, x_bf16,
                         y_bf16, relu, unit_col, Pt<const float>(init), ldi, Pt<const float>(cscale), init_rows,
-                        slab, S(st)),
+                        short_rows, S(st)),
         "gnn_spmm");
   }, py::arg("rowptr"), py::arg("col"), py::arg("x"), py::arg("y"), py::arg("rscale"), py::arg("bias"),
      py::arg("n_rows"), py::arg("F"), py::arg("ld_x"), py::arg("ld_y"), py::arg("x_bf16"), py::arg("y_bf16"),
      py::arg("relu"), py::arg("unit_col"), py::arg("st"), py::arg("init") = 0, py::arg("ldi") = 0,
-     py::arg("cscale") = 0, py::arg("init_rows") = -1, py::arg("slab") = 0);
+     py::arg("cscale") = 0, py::arg("init_rows") = -1, py::arg("short_rows") = 0);
   m.def("gnn_spmm_ce", [](uint64_t rowptr, uint64_t col, uint64_t z, uint64_t rscale, uint64_t bias,
                           uint64_t labels, uint64_t mask, uint64_t stats, uint64_t dlogits, uint64_t init, int ldi,
                           int n_rows, int C, int ld, int mode, float inv_count, uint64_t st, uint64_t gslot,
@@ -433,7 +442,8 @@ PYBIND11_MODULE(_hip, m) {
                                 std::vector<uint64_t> inv_deg, std::vector<uint64_t> picks, std::vector<uint64_t> local,
                                 std::vector<uint64_t> src, std::vector<uint64_t> rp_t, std::vector<uint64_t> col_t,
                                 std::vector<uint64_t> cnt_t, uint64_t counts, uint64_t flag, uint64_t map,
-                                uint64_t bscratch, uint32_t k0, uint32_t k1, uint32_t salt, uint64_t st) {
+                                uint64_t bscratch, uint32_t k0, uint32_t k1, uint32_t salt, uint64_t st,
+                                uint64_t counts_host) {
     const size_t L = fan.size();
     if (nd_max.size() != L || optr.size() != L || inv_deg.size() != L || picks.size() != L || local.size() != L ||
         src.size() != L || rp_t.size() != L || col_t.size() != L || cnt_t.size() != L)
@@ -449,8 +459,80 @@ PYBIND11_MODULE(_hip, m) {
     chk(gnn_launch_sample_blocks(Pt<const int>(rowptr), Pt<const int>(col), n, Pt<const int>(seeds), n_seeds,
                                  (int)L, fan.data(), nd_max.data(), a.data(), inv.data(), b.data(), c.data(),
                                  d.data(), e.data(), f.data(), g.data(), Pt<int>(counts), Pt<uint8_t>(flag),
-                                 Pt<int>(map), Pt<int>(bscratch), k0, k1, salt, S(st)), "gnn_sample_blocks");
+                                 Pt<int>(map), Pt<int>(bscratch), k0, k1, salt, S(st), Pt<int>(counts_host)),
+        "gnn_sample_blocks");
+  }, py::arg("rowptr"), py::arg("col"), py::arg("n"), py::arg("seeds"), py::arg("n_seeds"), py::arg("fan"),
+     py::arg("nd_max"), py::arg("optr"), py::arg("inv_deg"), py::arg("picks"), py::arg("local"), py::arg("src"),
+     py::arg("rp_t"), py::arg("col_t"), py::arg("cnt_t"), py::arg("counts"), py::arg("flag"), py::arg("map"),
+     py::arg("bscratch"), py::arg("k0"), py::arg("k1"), py::arg("salt"), py::arg("st"),
+     py::arg("counts_host") = 0);
+  // page-locked, device-mapped, coherent host memory a kernel can publish small results
+  // to (read by the host after an event): returns (host pointer, device pointer)
+  m.def("host_mapped_alloc", [](size_t nbytes) {
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, nbytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !h)
+      throw std::runtime_error("hipHostMalloc failed");
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      throw std::runtime_error("hipHostGetDevicePointer failed");
+    }
+    std::memset(h, 0, nbytes);
+    return py::make_tuple((uint64_t)(uintptr_t)h, (uint64_t)(uintptr_t)d);
   });
+  // native sampling worker (gnn_sampler.hip): handle = opaque pointer
+  m.def("gnn_sw_create", [](int device, uint64_t st, uint64_t rowptr, uint64_t col, int n, std::vector<int> fan,
+                            std::vector<int> nd_max, uint64_t flag, uint64_t map, uint64_t bscratch, uint32_t k0,
+                            uint32_t k1) {
+    if (fan.size() != nd_max.size() || fan.empty()) throw std::runtime_error("gnn_sw_create: bad level lists");
+    for (int f : fan)
+      if (f < 1 || f > 64) throw std::runtime_error("gnn_sw_create: fanouts must be in 1..64");
+    return (uint64_t)(uintptr_t)gnn_sw_create(device, S(st), Pt<const int>(rowptr), Pt<const int>(col), n,
+                                              (int)fan.size(), fan.data(), nd_max.data(), Pt<uint8_t>(flag),
+                                              Pt<int>(map), Pt<int>(bscratch), k0, k1);
+  });
+  m.def("gnn_sw_add_slot", [](uint64_t h, std::vector<uint64_t> optr, std::vector<uint64_t> inv_deg,
+                              std::vector<uint64_t> picks, std::vector<uint64_t> local, std::vector<uint64_t> src,
+                              std::vector<uint64_t> rp_t, std::vector<uint64_t> col_t, std::vector<uint64_t> cnt_t,
+                              uint64_t counts, uint64_t host) {
+    const size_t L = optr.size();
+    if (inv_deg.size() != L || picks.size() != L || local.size() != L || src.size() != L || rp_t.size() != L ||
+        col_t.size() != L || cnt_t.size() != L)
+      throw std::runtime_error("gnn_sw_add_slot: per-level lists differ in length");
+    auto ip = [](const std::vector<uint64_t>& v) {
+      std::vector<int*> o(v.size());
+      for (size_t i = 0; i < v.size(); ++i) o[i] = reinterpret_cast<int*>(v[i]);
+      return o;
+    };
+    std::vector<float*> inv(L);
+    for (size_t i = 0; i < L; ++i) inv[i] = reinterpret_cast<float*>(inv_deg[i]);
+    auto a = ip(optr), b = ip(picks), c = ip(local), d = ip(src), e = ip(rp_t), f = ip(col_t), g = ip(cnt_t);
+    const int r = gnn_sw_add_slot((void*)(uintptr_t)h, a.data(), inv.data(), b.data(), c.data(), d.data(), e.data(),
+                                  f.data(), g.data(), Pt<int>(counts), Pt<int>(host));
+    if (r < 0) throw std::runtime_error("gnn_sw_add_slot failed");
+    return r;
+  });
+  m.def("gnn_sw_submit", [](uint64_t h, int slot, uint64_t seeds, int n, uint32_t salt, std::vector<uint64_t> waits) {
+    std::vector<hipEvent_t> ev;
+    for (uint64_t x : waits)
+      if (x) ev.push_back(reinterpret_cast<hipEvent_t>(x));
+    const long r = gnn_sw_submit((void*)(uintptr_t)h, slot, Pt<const int>(seeds), n, salt, ev.data(), (int)ev.size());
+    if (r <= 0) throw std::runtime_error("gnn_sw_submit: bad slot or seed count");
+    return r;
+  });
+  m.def("gnn_sw_wait", [](uint64_t h, long seq, int slot, uint64_t consumer) {
+    int r;
+    {
+      py::gil_scoped_release nogil;
+      r = gnn_sw_wait((void*)(uintptr_t)h, seq, slot, S(consumer));
+    }
+    chk(r, "gnn_sw_wait (sampling worker)");
+  });
+  m.def("gnn_sw_destroy", [](uint64_t h) {
+    py::gil_scoped_release nogil;
+    gnn_sw_destroy((void*)(uintptr_t)h);
+  });
+  m.def("host_mapped_free", [](uint64_t h) { (void)hipHostFree((void*)(uintptr_t)h); });
   m.def("gnn_fused_bwd_blocks", &gnn_fused_bwd_blocks);
   m.def("gnn_fused_bwd_width", &gnn_fused_bwd_width);
   m.def("gnn_fused_bwd_supported", &gnn_fused_bwd_supported);

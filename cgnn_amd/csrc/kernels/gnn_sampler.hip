@@ -12,6 +12,11 @@
 //                             thread that draws it).
 #include "cgnn_common.h"
 #include <algorithm>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 using namespace cgnn;
 
@@ -312,10 +317,13 @@ __global__ __launch_bounds__(256) void sb_scatter_kernel(const int* __restrict__
   }
 }
 
+// (also clears the scatter cursors: cnt is all zero again for the slot's next batch)
 __global__ __launch_bounds__(256) void sb_bucket_sort_kernel(const int* __restrict__ rp_t,
-                                                             const int* __restrict__ n_dev, int* __restrict__ col_t) {
+                                                             const int* __restrict__ n_dev, int* __restrict__ col_t,
+                                                             int* __restrict__ cnt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= *n_dev) return;
+  cnt[c] = 0;
   const int a = rp_t[c], b = rp_t[c + 1];
   for (int i = a + 1; i < b; ++i) {
     const int x = col_t[i];
@@ -326,6 +334,12 @@ __global__ __launch_bounds__(256) void sb_bucket_sort_kernel(const int* __restri
     }
     col_t[j + 1] = x;
   }
+}
+
+// the level sizes to mapped host memory (read by the host after the batch's event)
+__global__ void sb_publish_kernel(const int* __restrict__ counts, int* __restrict__ host, int n) {
+  const int i = threadIdx.x;
+  if (i < n) __hip_atomic_store(host + i, counts[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 static unsigned blocks_for(long n, int t = 256) { return (unsigned)std::max(1L, (n + t - 1) / t); }
@@ -343,12 +357,15 @@ extern "C" long gnn_sample_blocks_scratch(int n, int L, const int* fan, const in
 // fan[l] the fanout; dst of level 0 = seeds (n_seeds on the host), of level l > 0 =
 // src[l - 1] with its device count counts[2 (l - 1)].  counts[2 l] = n_src of level
 // l, counts[2 l + 1] = its picks.  Transposed CSR built for levels with rp_t[l] != 0.
+// counts_host (optional, device address of mapped host memory): the counts published
+// there by a kernel at the end (no copy call).  cnt_t[l] must be zero on entry; the
+// pipeline leaves it zero.
 extern "C" int gnn_launch_sample_blocks(const int* rowptr, const int* col, int n, const int* seeds, int n_seeds,
                                         int L, const int* fan, const int* nd_max, int* const* optr,
                                         float* const* inv_deg, int* const* picks, int* const* local,
                                         int* const* src, int* const* rp_t, int* const* col_t, int* const* cnt_t,
                                         int* counts, uint8_t* flag, int* map, int* bscratch, uint32_t k0,
-                                        uint32_t k1, uint32_t salt, hipStream_t st) {
+                                        uint32_t k1, uint32_t salt, hipStream_t st, int* counts_host) {
   const int nb = (n + FLAG_BLK - 1) / FLAG_BLK;
   // scan scratch after the flag-scan counts: block sums, block offsets, values
   long vmax = 1;
@@ -390,7 +407,6 @@ extern "C" int gnn_launch_sample_blocks(const int* rowptr, const int* col, int n
     hipLaunchKernelGGL(sb_relabel_kernel, dim3(blocks_for(pmax)), dim3(256), 0, st, picks[l], total, map, local[l]);
     if (rp_t[l]) {
       const long smax = std::min<long>((long)nd_max[l] * (fo + 1), (long)n);
-      (void)hipMemsetAsync(cnt_t[l], 0, sizeof(int) * (size_t)smax, st);
       hipLaunchKernelGGL(sb_hist_kernel, dim3(blocks_for(pmax)), dim3(256), 0, st, local[l], total, cnt_t[l]);
       const unsigned nbt = blocks_for(smax, SB);
       hipLaunchKernelGGL(sb_scanA_kernel, dim3(nbt), dim3(256), 0, st, (const int*)nullptr, (const int*)nullptr, 0,
@@ -400,8 +416,185 @@ extern "C" int gnn_launch_sample_blocks(const int* rowptr, const int* col, int n
       hipLaunchKernelGGL(sb_scanC_kernel, dim3(nbt), dim3(256), 0, st, svals, sboff, 0, nsrc, rp_t[l]);
       hipLaunchKernelGGL(sb_scatter_kernel, dim3(blocks_for(nd_max[l])), dim3(256), 0, st, optr[l], local[l], ndh,
                          nd_dev, rp_t[l], cnt_t[l], col_t[l]);
-      hipLaunchKernelGGL(sb_bucket_sort_kernel, dim3(blocks_for(smax)), dim3(256), 0, st, rp_t[l], nsrc, col_t[l]);
+      hipLaunchKernelGGL(sb_bucket_sort_kernel, dim3(blocks_for(smax)), dim3(256), 0, st, rp_t[l], nsrc, col_t[l],
+                         cnt_t[l]);
     }
   }
+  if (counts_host) hipLaunchKernelGGL(sb_publish_kernel, dim3(1), dim3(64), 0, st, counts, counts_host, 2 * L);
   return (int)hipGetLastError();
+}
+
+// ============================================================================
+// Sampling worker: a native thread that owns the side stream and issues each
+// batch's ~40 pipeline launches, so that the Python thread only posts a job and
+// goes on enqueuing the training step (the host's launch time per batch was the
+// SAGE loop's critical path: profiles/r05_sage).  Jobs run in submission order;
+// each waits for the events it names (seeds ready, the slot's previous reader
+// done), launches gnn_launch_sample_blocks and records the slot's done event.
+// wait(seq) blocks (no GIL) until job seq was issued and its sampling finished,
+// then orders the consumer stream after it.
+// ============================================================================
+namespace {
+struct WorkerSlot {
+  std::vector<int*> optr, picks, local, src, rp_t, col_t, cnt_t;
+  std::vector<float*> inv;
+  int* counts = nullptr;
+  int* host = nullptr;
+  hipEvent_t done = nullptr;
+};
+
+struct WorkerJob {
+  int slot;
+  const int* seeds;
+  int n;
+  uint32_t salt;
+  std::vector<hipEvent_t> waits;
+  uint64_t seq;
+};
+
+struct SampleWorker {
+  int device;
+  hipStream_t st;
+  const int* rowptr;
+  const int* col;
+  int n;
+  std::vector<int> fan, nd_max;
+  uint8_t* flag;
+  int* map;
+  int* bscratch;
+  uint32_t k0, k1;
+  std::vector<WorkerSlot> slots;
+  std::mutex m;
+  std::condition_variable cv_job, cv_done;
+  std::deque<WorkerJob> q;
+  uint64_t submitted = 0, issued = 0;
+  int err = 0;
+  bool stop = false;
+  std::thread th;
+
+  void run() {
+    (void)hipSetDevice(device);
+    for (;;) {
+      WorkerJob j;
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv_job.wait(lk, [&] { return stop || !q.empty(); });
+        if (q.empty()) return;            // stop requested and drained
+        j = std::move(q.front());
+        q.pop_front();
+      }
+      int e = 0;
+      for (hipEvent_t ev : j.waits)
+        if (!e) e = (int)hipStreamWaitEvent(st, ev, 0);
+      WorkerSlot& s = slots[j.slot];
+      if (!e)
+        e = gnn_launch_sample_blocks(rowptr, col, n, j.seeds, j.n, (int)fan.size(), fan.data(), nd_max.data(),
+                                     s.optr.data(), s.inv.data(), s.picks.data(), s.local.data(), s.src.data(),
+                                     s.rp_t.data(), s.col_t.data(), s.cnt_t.data(), s.counts, flag, map, bscratch, k0,
+                                     k1, j.salt, st, s.host);
+      if (!e) e = (int)hipEventRecord(s.done, st);
+      {
+        std::lock_guard<std::mutex> lk(m);
+        if (e && !err) err = e;
+        issued = j.seq;
+      }
+      cv_done.notify_all();
+    }
+  }
+};
+}  // namespace
+
+extern "C" void* gnn_sw_create(int device, hipStream_t st, const int* rowptr, const int* col, int n, int L,
+                               const int* fan, const int* nd_max, uint8_t* flag, int* map, int* bscratch, uint32_t k0,
+                               uint32_t k1) {
+  auto* w = new SampleWorker();
+  w->device = device;
+  w->st = st;
+  w->rowptr = rowptr;
+  w->col = col;
+  w->n = n;
+  w->fan.assign(fan, fan + L);
+  w->nd_max.assign(nd_max, nd_max + L);
+  w->flag = flag;
+  w->map = map;
+  w->bscratch = bscratch;
+  w->k0 = k0;
+  w->k1 = k1;
+  return w;
+}
+
+// per-level pointer arrays of one slot (L entries each); returns the slot index or < 0
+extern "C" int gnn_sw_add_slot(void* h, int* const* optr, float* const* inv, int* const* picks, int* const* local,
+                               int* const* src, int* const* rp_t, int* const* col_t, int* const* cnt_t, int* counts,
+                               int* host) {
+  auto* w = static_cast<SampleWorker*>(h);
+  if (w->th.joinable()) return -1;          // slots are fixed once the thread runs
+  const size_t L = w->fan.size();
+  WorkerSlot s;
+  s.optr.assign(optr, optr + L);
+  s.inv.assign(inv, inv + L);
+  s.picks.assign(picks, picks + L);
+  s.local.assign(local, local + L);
+  s.src.assign(src, src + L);
+  s.rp_t.assign(rp_t, rp_t + L);
+  s.col_t.assign(col_t, col_t + L);
+  s.cnt_t.assign(cnt_t, cnt_t + L);
+  s.counts = counts;
+  s.host = host;
+  if (hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess) return -2;
+  w->slots.push_back(std::move(s));
+  return (int)w->slots.size() - 1;
+}
+
+// post a batch (the events are waited for on the worker's stream before the launches;
+// they must stay alive until the job is issued); returns its sequence number (>= 1)
+extern "C" long gnn_sw_submit(void* h, int slot, const int* seeds, int n, uint32_t salt, const hipEvent_t* waits,
+                              int nw) {
+  auto* w = static_cast<SampleWorker*>(h);
+  if (slot < 0 || slot >= (int)w->slots.size()) return -1;
+  if (n < 0 || n > w->nd_max[0]) return -2;
+  WorkerJob j;
+  j.slot = slot;
+  j.seeds = seeds;
+  j.n = n;
+  j.salt = salt;
+  j.waits.assign(waits, waits + nw);
+  uint64_t seq;
+  {
+    std::lock_guard<std::mutex> lk(w->m);
+    if (!w->th.joinable()) w->th = std::thread([w] { w->run(); });
+    seq = j.seq = ++w->submitted;
+    w->q.push_back(std::move(j));
+  }
+  w->cv_job.notify_one();
+  return (long)seq;
+}
+
+// block until job seq is issued and the sampling of its slot finished; then order the
+// consumer stream after it.  Returns 0 or the first error any job hit.
+extern "C" int gnn_sw_wait(void* h, long seq, int slot, hipStream_t consumer) {
+  auto* w = static_cast<SampleWorker*>(h);
+  if (slot < 0 || slot >= (int)w->slots.size()) return -1;
+  {
+    std::unique_lock<std::mutex> lk(w->m);
+    w->cv_done.wait(lk, [&] { return w->issued >= (uint64_t)seq || w->err; });
+    if (w->err) return w->err;
+  }
+  int e = (int)hipEventSynchronize(w->slots[slot].done);
+  if (!e && consumer) e = (int)hipStreamWaitEvent(consumer, w->slots[slot].done, 0);
+  return e;
+}
+
+extern "C" void gnn_sw_destroy(void* h) {
+  auto* w = static_cast<SampleWorker*>(h);
+  {
+    std::lock_guard<std::mutex> lk(w->m);
+    w->stop = true;
+  }
+  w->cv_job.notify_all();
+  if (w->th.joinable()) w->th.join();
+  (void)hipStreamSynchronize(w->st);
+  for (auto& s : w->slots)
+    if (s.done) (void)hipEventDestroy(s.done);
+  delete w;
 }

@@ -183,6 +183,124 @@ __global__ __launch_bounds__(256) void spmm_kernel(
   }
 }
 
+// Short rows (average degree <= 2: the transposed blocks of sampled GraphSAGE, where
+// most sources were picked once).  spmm_kernel gives each L-lane sub-group ONE row, and
+// a row is a chain of dependent round trips (row bounds -> column id -> column scale
+// and source row -> store) with one source row in flight per lane.  Here a sub-group
+// owns RP consecutive rows: their edges are one contiguous CSR range, so one load per
+// lane brings the row bounds, one more the first L column ids, and the RP rows' first
+// sources load together -- RP rows per round trip.  Rows of 2-3 entries add their
+// further sources one by one; rows of 4+ (or past the first L edges) take gather_sum.
+// Per row the same adds in the same order as spmm_kernel (whose 1-steps they are):
+// bit-identical output.  Blocks map to rows in launch order (see below).
+template <int L, int XBF, int YBF, int RP, bool CS>
+__global__ __launch_bounds__(256) void spmm_short_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const void* __restrict__ X,
+    void* __restrict__ Y, const float* __restrict__ rscale, const float* __restrict__ bias,
+    int n_rows, int F, int ldx, int ldy, int relu, int unit_col, int wcols,
+    const float* __restrict__ init, int ldi, const float* __restrict__ cscale, int init_rows) {
+  constexpr int RPW = 64 / L;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / L, sl = lane - sub * L, sub_base = sub * L;
+  // NO XCD remap: the sources are in-edges of random destinations (no L2 locality to
+  // keep), and the rows with an init (the destinations, a prefix) must spread over all
+  // eight XCDs -- remapped, the first XCD alone read the whole fp32 init (+43 us of 83,
+  // profiles/r05_sage)
+  const unsigned blk = blockIdx.x;
+  const int r0 = ((blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub) * RP;
+  if (r0 >= n_rows) return;                       // uniform per sub-group
+  const int f0 = sl * 8;
+  const bool fv = f0 < F;
+  // spmm_kernel's epilogue for one row
+  auto store_row = [&](int row, float* acc) {
+    if (init && fv && row < init_rows) {
+      const float* ip = init + (size_t)row * ldi + f0;
+      if (f0 + 8 <= F && ((uintptr_t)ip & 15) == 0) {       // two 16-byte loads
+        const float4 u = reinterpret_cast<const float4*>(ip)[0], v = reinterpret_cast<const float4*>(ip)[1];
+        acc[0] += u.x; acc[1] += u.y; acc[2] += u.z; acc[3] += u.w;
+        acc[4] += v.x; acc[5] += v.y; acc[6] += v.z; acc[7] += v.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (f0 + q < F) acc[q] += ip[q];
+      }
+    }
+    const float rs = rscale ? rscale[row] : 1.f;
+    float y[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int f = f0 + q;
+      float v = acc[q] * rs + ((bias && f < F) ? bias[f] : 0.f);
+      if (relu) v = fmaxf(v, 0.f);
+      y[q] = f < F ? v : (f == unit_col ? 1.f : 0.f);
+    }
+    if (YBF == 1) {
+      *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
+    } else if (YBF == 2) {
+      f16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = (_Float16)y[q];
+      *reinterpret_cast<f16x8*>(reinterpret_cast<uint16_t*>(Y) + (size_t)row * ldy + f0) = o;
+    } else {
+      float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(Y) + (size_t)row * ldy + f0);
+      p[0] = make_float4(y[0], y[1], y[2], y[3]);
+      p[1] = make_float4(y[4], y[5], y[6], y[7]);
+    }
+  };
+  const int rpv = rowptr[min(r0 + min(sl, RP), n_rows)];
+  int e[RP + 1];
+#pragma unroll
+  for (int r = 0; r <= RP; ++r) e[r] = __shfl(rpv, sub_base + r, 64);
+  const int eb = e[0], ee = e[RP];
+  const int myj = ee > eb ? col[min(eb + sl, ee - 1)] : 0;
+  const float mycs = CS && ee > eb ? cscale[myj] : 1.f;
+  // a row is long: 4+ entries (gather_sum's grouped steps) or past the first L edges
+  auto is_long = [&](int r) { return e[r + 1] - e[r] >= 4 || e[r + 1] - eb > L; };
+  float acc[RP][8];
+#pragma unroll
+  for (int r = 0; r < RP; ++r) {                  // every row's first source in flight at once
+    const int k = min(e[r] - eb, L - 1);
+    const int j = __shfl(myj, sub_base + k, 64);
+    const float c = CS ? __shfl(mycs, sub_base + k, 64) : 1.f;
+    float a[8];
+    if (fv && ee > eb) load8<XBF>(X, (size_t)j * ldx + f0, a);     // (j is a real id then)
+    const bool has = e[r + 1] > e[r];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      acc[r][q] = 0.f;
+      if (fv && has) acc[r][q] = CS ? fmaf(c, a[q], acc[r][q]) : acc[r][q] + a[q];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RP; ++r) {                  // rows of 2-3 entries: the 1-steps
+    const int deg = e[r + 1] - e[r];
+    if (deg <= 1 || is_long(r)) continue;
+    for (int t = 1; t < deg; ++t) {
+      const int k = e[r] - eb + t;
+      const int j = __shfl(myj, sub_base + k, 64);
+      const float c = CS ? __shfl(mycs, sub_base + k, 64) : 1.f;
+      if (fv) {
+        float a[8];
+        load8<XBF>(X, (size_t)j * ldx + f0, a);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[r][q] = CS ? fmaf(c, a[q], acc[r][q]) : acc[r][q] + a[q];
+      }
+    }
+  }
+  // (no early exit for lanes past wcols: the long rows' gathers read every lane's ids)
+  const bool wv = f0 < wcols;
+#pragma unroll
+  for (int r = 0; r < RP; ++r)
+    if (wv && r0 + r < n_rows && !is_long(r)) store_row(r0 + r, acc[r]);
+  // long rows last, one at a time (the short rows' accumulators are dead by now)
+  for (int r = 0; r < RP; ++r) {
+    if (r0 + r >= n_rows || !is_long(r)) continue;
+    float acc1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    gather_sum<L, XBF, 8, CS>(col, X, e[r], e[r + 1], ldx, f0, fv, sub_base, sl, acc1, cscale);
+    if (wv) store_row(r0 + r, acc1);
+  }
+}
+
 // Short-row aggregate from an ELL image (the GCN backward's train-column adjacency: ~4
 // entries per row): ell[row][0..7] holds the row's column ids (-1 past its end) or, for a
 // row of more than 8 entries, {-2, e0, e1}: its range in the CSR `col`.  One 32-B load
@@ -476,13 +594,23 @@ __global__ void cast_bf16_kernel(const float* __restrict__ src, uint16_t* __rest
 // software-pipelined gather that combined the early column ids with non-temporal index
 // loads / output stores and 16 raw rows in flight per lane: 30 % SLOWER (F = 100: 3.43 vs
 // 2.64 ms) -- non-temporal stores alone double a store-heavy kernel's time (r04_lin).
-template <int L, int U>
+template <int L, int U, int RP>
 static int spmm_dispatch_u(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
                          int relu, int uc, int wc, const float* init, int ldi, const float* cs, int ir, hipStream_t st) {
-  constexpr int RPB = 4 * (64 / L);   // rows per 256-thread block
+  // RP > 0: the short-row kernel, RP rows per sub-group
+  constexpr int RPB = 4 * (64 / L) * (RP > 0 ? RP : 1);   // rows per 256-thread block
   dim3 grid((n_rows + RPB - 1) / RPB), block(256);
-#define CGNN_SPMM(XT, YT, C) hipLaunchKernelGGL((spmm_kernel<L, XT, YT, U, C>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, relu, uc, wc, init, ldi, cs, ir)
+  if (n_rows <= 0) return 0;
+#define CGNN_SPMM(XT, YT, C)                                                                                    \
+  do {                                                                                                         \
+    if constexpr (RP > 0)                                                                                      \
+      hipLaunchKernelGGL((spmm_short_kernel<L, XT, YT, RP, C>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, \
+                         n_rows, F, ldx, ldy, relu, uc, wc, init, ldi, cs, ir);                                \
+    else                                                                                                       \
+      hipLaunchKernelGGL((spmm_kernel<L, XT, YT, U, C>), grid, block, 0, st, rowptr, col, X, Y, rs, bias, n_rows, \
+                         F, ldx, ldy, relu, uc, wc, init, ldi, cs, ir);                                        \
+  } while (0)
   // element-type codes: 0 fp32, 1 bf16, 2 fp16 (fp16 pairs with itself or with fp32);
   // a column scale is compiled for the same-type pairs only
   if (cs) {
@@ -506,37 +634,41 @@ template <int L>
 static int spmm_dispatch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                          const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf,
                          int relu, int uc, int wc, const float* init, int ldi, const float* cs, int ir,
-                         hipStream_t st) {
-  return spmm_dispatch_u<L, 8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
-                               ldi, cs, ir, st);
+                         bool short_rows, hipStream_t st) {
+  if (short_rows)
+    return spmm_dispatch_u<L, 8, 4>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
+                                    ldi, cs, ir, st);
+  return spmm_dispatch_u<L, 8, 0>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init,
+                                  ldi, cs, ir, st);
 }
 
 // one launch writing output columns [0, wcols) of its base (wcols <= 512)
 static int spmm_launch(const int* rowptr, const int* col, const void* X, void* Y, const float* rs,
                        const float* bias, int n_rows, int F, int ldx, int ldy, int xbf, int ybf, int relu,
-                       int uc, int wc, const float* init, int ldi, const float* cs, int ir, hipStream_t st) {
+                       int uc, int wc, const float* init, int ldi, const float* cs, int ir, bool sr,
+                       hipStream_t st) {
   const int w = std::max(F, wc);
-  if (w <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, st);
-  if (w <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, st);
-  if (w <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, st);
-  if (w <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, st);
+  if (w <= 64) return spmm_dispatch<8>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, sr, st);
+  if (w <= 128) return spmm_dispatch<16>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, sr, st);
+  if (w <= 256) return spmm_dispatch<32>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, sr, st);
+  if (w <= 512) return spmm_dispatch<64>(rowptr, col, X, Y, rs, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, uc, wc, init, ldi, cs, ir, sr, st);
   return -1;
 }
 
 extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X, void* Y,
                                const float* rscale, const float* bias, int n_rows, int F, int ldx,
                                int ldy, int xbf, int ybf, int relu, int unit_col, const float* init, int ldi,
-                               const float* cscale, int init_rows, int slab, hipStream_t st) {
-  // slab: output columns per launch (a multiple of 8, at most 512; <= 0: 512)
-  if (slab <= 0) slab = 512;
-  if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy || (slab % 8) || slab > 512) return -3;
+                               const float* cscale, int init_rows, int short_rows, hipStream_t st) {
+  // short_rows: the rows average <= 2 entries (spmm_short_kernel)
+  constexpr int slab = 512;
+  const bool sr = short_rows != 0;
+  if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
   if (init_rows < 0) init_rows = n_rows;
   if (ldy <= slab && F <= slab)
     return spmm_launch(rowptr, col, X, Y, rscale, bias, n_rows, F, ldx, ldy, xbf, ybf, relu, unit_col, ldy, init,
-                       ldi, cscale, init_rows, st);
-  // wide rows (or narrower slabs asked for): column slabs of `slab` output columns
-  // (16-byte aligned offsets), one launch each; the last slabs also write the padding /
-  // ones columns up to ldy
+                       ldi, cscale, init_rows, sr, st);
+  // wide rows: column slabs of 512 output columns (16-byte aligned offsets), one launch
+  // each; the last slabs also write the padding / ones columns up to ldy
   const size_t xs = xbf ? 2 : 4, ys = ybf ? 2 : 4;   // bf16 and fp16 are both 2 bytes
   for (int c0 = 0; c0 < ldy; c0 += slab) {
     const int fc = std::max(0, std::min(slab, F - c0));
@@ -544,7 +676,7 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
     const int rc = spmm_launch(rowptr, col, (const char*)X + (fc ? c0 * xs : 0), (char*)Y + c0 * ys, rscale,
                                bias && fc ? bias + c0 : nullptr, n_rows, fc, ldx, ldy, xbf, ybf, relu,
                                unit_col >= 0 ? unit_col - c0 : -1, wc, init && fc ? init + c0 : nullptr, ldi,
-                               cscale, init_rows, st);
+                               cscale, init_rows, sr, st);
     if (rc) return rc;
   }
   return 0;

@@ -37,16 +37,21 @@ def dtype_code(dt) -> int:
 
 
 def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dtype=torch.bfloat16,
-         ld_out=None, unit_col=-1, init=None, cscale=None, init_rows=None, slab=0):
+         ld_out=None, unit_col=-1, init=None, cscale=None, init_rows=None, short_rows=None):
     """Y[i,:F] = act(rscale[i] * (init[i] + sum_{j in N(i)} cscale[j] X[j,:F]) + bias); X is [*, ldx].
     Padding columns of Y are written 0, except ``unit_col`` which is written 1
     (a ones column that turns the bias gradient into one more GEMM row).
     ``init`` (optional fp32 [init_rows, >=F], default all n rows): partial sums of other
     edges (split aggregation) added to the first ``init_rows`` rows.
     ``cscale`` (optional fp32 per source row): a column scale applied in the gather.
-    ``slab`` (GPU): output columns per launch, a multiple of 8 (0: one launch up to 512
-    columns); narrower slabs gather fewer cache lines per row and launch."""
+    Rows wider than 512 columns run as 512-column slabs (one launch each); narrower
+    slabs were measured slower (round 4, profiles/r04_spmm).
+    ``short_rows`` (default: at most 2 entries per row on average, from ``col``'s
+    length): the kernel that gives each sub-group 4 consecutive rows (a transposed
+    sampled block); bit-identical to the one-row-per-sub-group kernel."""
     n = rowptr.numel() - 1
+    if short_rows is None:
+        short_rows = col.numel() <= 2 * n
     ldo = ld_out or X.shape[1]
     if out is None:
         out = torch.empty(n, ldo, dtype=out_dtype, device=X.device)
@@ -64,7 +69,7 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
                      _st(X), init.data_ptr() if init is not None else 0,
                      init.stride(0) if init is not None else 0,
                      cscale.data_ptr() if cscale is not None else 0,
-                     -1 if init_rows is None else int(init_rows), int(slab))
+                     -1 if init_rows is None else int(init_rows), int(bool(short_rows)))
         return out
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, F, dtype=torch.float32)

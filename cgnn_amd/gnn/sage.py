@@ -32,6 +32,7 @@ with hipBLASLt GEMMs (``_SageLinear``), the A/B baseline.
 """
 from __future__ import annotations
 
+import collections
 import math
 import queue
 import threading
@@ -364,6 +365,7 @@ class SAGETrainer:
         self.sampler = sampler or ("pipelined" if self.dev.type == "cuda" else "host")
         self._dsampler = None
         self._psampler = None
+        self._main = None
         if self.fanouts and self.sampler == "device":
             from .sampler import DeviceSampler
             self._dsampler = DeviceSampler(g.rowptr, g.col, self.fanouts[:layers], seed)
@@ -488,26 +490,19 @@ class SAGETrainer:
         batches = self._batches()
         losses = []
         if self._psampler is not None and batches:
-            ps = self._psampler
-            # the epoch's seeds uploaded once; batch k + 1 samples on the side stream while k trains
-            flat = torch.as_tensor(np.concatenate(batches).astype(np.int32), device=self.dev)
-            # the epoch's labels gathered once too (fused path), not per batch
-            yflat = self.y32[flat.long()] if self.fused else None
-            seeds, labels, o = [], [], 0
-            for b in batches:
-                seeds.append(flat[o:o + len(b)])
-                labels.append(yflat[o:o + len(b)] if yflat is not None else None)
-                o += len(b)
-            salt = lambda k: (self.epoch * 100003 + k) * self.world + self.rank
-            pend = ps.enqueue(seeds[0], salt(0))
-            for k in range(len(batches)):
-                nxt = ps.enqueue(seeds[k + 1], salt(k + 1)) if k + 1 < len(batches) else None
-                blocks, nodes_in = pend.resolve()
-                torch.cuda.current_stream(self.dev).wait_event(pend.slot.done)
-                losses.append(self._step(blocks, nodes_in, seeds[k], labels[k]))
-                ps.consumed(pend)
-                pend = nxt
-        elif self._dsampler is not None:
+            if self._main is None:
+                self._main = torch.cuda.Stream(device=self.dev)
+            # the batch loop on a stream of its own: work on the legacy default stream is
+            # implicitly ordered against the sampler's stream, which serialised every
+            # batch's sampling behind the previous batch's training (kernel trace, round 5)
+            cur = torch.cuda.current_stream(self.dev)
+            self._main.wait_stream(cur)
+            with torch.cuda.stream(self._main):
+                loss = self._pipelined_epoch(batches)
+            cur.wait_stream(self._main)
+            self.epoch += 1
+            return loss
+        if self._dsampler is not None:
             for k, b in enumerate(batches):
                 seeds_t = torch.as_tensor(b, device=self.dev)
                 blocks, nodes_in = self._dsampler.sample(seeds_t, (self.epoch * 100003 + k) * self.world + self.rank)
@@ -535,6 +530,37 @@ class SAGETrainer:
                 blocks, nodes_in = self._to_device(self.sample(b, (self.epoch * 100003 + k) * self.world + self.rank))
                 losses.append(self._step(blocks, nodes_in, torch.as_tensor(b, device=self.dev)))
         self.epoch += 1
+        return float(torch.stack(losses).mean())
+
+    def _pipelined_epoch(self, batches):
+        ps = self._psampler
+        losses = []
+        # the epoch's seeds uploaded once; batch k + 1 samples on the side stream while k trains
+        flat = torch.as_tensor(np.concatenate(batches).astype(np.int32), device=self.dev)
+        # the epoch's labels gathered once too (fused path), not per batch
+        yflat = self.y32[flat.long()] if self.fused else None
+        seeds, labels, o = [], [], 0
+        for b in batches:
+            seeds.append(flat[o:o + len(b)])
+            labels.append(yflat[o:o + len(b)] if yflat is not None else None)
+            o += len(b)
+        salt = lambda k: (self.epoch * 100003 + k) * self.world + self.rank
+        # the seeds are valid from here on: the sampler waits for this event and for the
+        # training that last read a slot, never for the whole training stream
+        ready = torch.cuda.Event()
+        ready.record()
+        # slots - 1 batches sampled ahead: batch k + 2's sampling runs beside batch k's
+        # training and is long done when the host asks for it
+        depth, nb = len(ps.slots) - 1, len(batches)
+        pend = collections.deque(ps.enqueue(seeds[j], salt(j), ready) for j in range(min(depth, nb)))
+        for k in range(nb):
+            if k + depth < nb:
+                pend.append(ps.enqueue(seeds[k + depth], salt(k + depth), ready))
+            cur = pend.popleft()
+            blocks, nodes_in = cur.resolve()
+            torch.cuda.current_stream(self.dev).wait_event(cur.slot.done)
+            losses.append(self._step(blocks, nodes_in, seeds[k], labels[k]))
+            ps.consumed(cur)
         return float(torch.stack(losses).mean())
 
     @torch.no_grad()

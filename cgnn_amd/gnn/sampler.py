@@ -20,7 +20,9 @@ NumPy (tests).
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+import ctypes
+import weakref
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -159,7 +161,7 @@ def sample_reference(rowptr: np.ndarray, col: np.ndarray, seeds: np.ndarray, fan
 class _Slot:
     """Device buffers of one in-flight mini-batch (upper-bound sizes)."""
 
-    def __init__(self, dev, n, batch, fanouts, need_t):
+    def __init__(self, dev, n, batch, fanouts, need_t, publish):
         i32 = dict(dtype=torch.int32, device=dev)
         self.nd_max = []
         nd = batch
@@ -179,15 +181,29 @@ class _Slot:
             if need_t[l]:
                 self.rp_t.append(torch.zeros(smax + 1, **i32))
                 self.col_t.append(torch.zeros(max(ndm * fo, 1), **i32))
+                # zero between batches: the pipeline's last kernel clears what it counted
                 self.cnt_t.append(torch.zeros(smax, **i32))
             else:
                 self.rp_t.append(None)
                 self.col_t.append(None)
                 self.cnt_t.append(None)
         self.counts = torch.zeros(2 * len(fanouts), **i32)
-        self.counts_host = torch.zeros(2 * len(fanouts), dtype=torch.int32).pin_memory()
-        self.done = None          # event: the sampling of this slot's batch finished
-        self.free = None          # event: the training that read this slot finished
+        self.host_ptr = 0         # device address of the mapped counts (publish), else 0
+        if publish:
+            # page-locked, device-mapped host memory the pipeline's last kernel writes the
+            # level sizes to: no copy call per batch
+            hip = native.hip()
+            h, d = hip.host_mapped_alloc(4 * 2 * len(fanouts))
+            weakref.finalize(self, hip.host_mapped_free, h)
+            self.counts_host = torch.from_numpy(np.ctypeslib.as_array(
+                (ctypes.c_int32 * (2 * len(fanouts))).from_address(h)))
+            self.host_ptr = d
+        else:
+            self.counts_host = torch.zeros(2 * len(fanouts), dtype=torch.int32).pin_memory()
+        self.done = torch.cuda.Event()      # the sampling of this slot's batch finished
+        self.free = torch.cuda.Event()      # the training that read this slot finished
+        self.widx = -1                      # the slot's index in the native worker
+        self.keep = None                    # what a posted job refers to (events, seeds)
 
 
 class SampledBatch:
@@ -195,15 +211,22 @@ class SampledBatch:
     waits for that work only and returns (blocks input layer first, input node ids
     int32) with host-known sizes."""
 
-    def __init__(self, slot, fanouts, n_seeds):
+    def __init__(self, slot, fanouts, n_seeds, waiter=None):
         self.slot, self.fanouts, self.n_seeds = slot, fanouts, n_seeds
+        self.waiter = waiter      # (worker handle, job sequence number): threaded sampler
         self._res = None
 
     def resolve(self):
         if self._res is None:
             sl = self.slot
-            sl.done.synchronize()
-            c = sl.counts_host.tolist()
+            if self.waiter is not None:
+                # the worker issued the job and its sampling finished; the current stream
+                # is ordered after it
+                h, seq = self.waiter
+                native.hip().gnn_sw_wait(h, seq, sl.widx, torch.cuda.current_stream(sl.counts.device).cuda_stream)
+            else:
+                sl.done.synchronize()
+            c = sl.counts_host.tolist()          # a copy: the slot is refilled later
             blocks = []
             nd = self.n_seeds
             for l in range(len(self.fanouts)):
@@ -220,18 +243,35 @@ class SampledBatch:
 
 class PipelinedSampler:
     """The whole multi-level sampling of a mini-batch as ONE native call
-    (``gnn_sample_blocks``: ~10 HIP kernels per level, device-side row counts, no
-    host synchronisation) on a side stream, double-buffered: batch k + 1 is
-    sampled while batch k trains, and the host reads the level sizes with one
-    pinned copy.  Same draws and relabelling as :class:`DeviceSampler` (bitwise
-    equal blocks); the transposed CSRs the backward needs (every block but the
-    input layer's) are built on the device too, deterministically (histogram,
-    scan, scatter, per-bucket sort)."""
+    (``gnn_sample_blocks``: ~13 HIP kernels per level, device-side row counts, no
+    host synchronisation inside) on a high-priority side stream, over ``slots``
+    buffers: batch k + 1 (and k + 2) is sampled while batch k trains.  The level
+    sizes reach the host through mapped host memory a kernel writes (``publish``;
+    else one pinned copy per batch).  Same draws and relabelling as
+    :class:`DeviceSampler` (bitwise equal blocks); the transposed CSRs the backward
+    needs (every block but the input layer's) are built on the device too,
+    deterministically (histogram, scan, scatter, per-bucket sort).
+
+    A slot waits only for the training that last read it (``consumed``) and for the
+    event the caller says its seeds are ready at (``enqueue(ready=...)``), not for
+    the whole main stream: with three slots, the sampling of batch k + 1 starts
+    while batch k - 1 still trains, and is done before the host asks for it
+    (profiles/r05_sage).
+
+    ``threaded`` (default): a native worker thread owns the side stream and issues the
+    launches (``gnn_sw_*`` in gnn_sampler.hip); the Python thread only posts the batch,
+    so the ~40 sampling launches no longer add to the host time of the training loop.
+
+    Capturing each slot's pipeline as a hipGraph (seed count and salt read on the
+    device) was tried in round 5: the uncaptured launches pass the bitwise test, the
+    replayed graph faulted (illegal address) on the first replay; not kept."""
 
     def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, fanouts: Sequence[int], batch: int, seed: int = 0,
-                 slots: int = 2):
+                 slots: int = 3, publish: bool = True, threaded: bool = True):
         if not rowptr.is_cuda:
             raise ValueError("PipelinedSampler needs the CSR on a GPU")
+        if slots < 2:
+            raise ValueError("the pipelined sampler needs at least two slots")
         self.rowptr, self.col = rowptr.contiguous(), col.contiguous()
         self.dev = rowptr.device
         self.n = rowptr.numel() - 1
@@ -239,19 +279,40 @@ class PipelinedSampler:
         if any(f > 64 or f < 1 for f in self.fanouts):
             raise ValueError("device sampler fanouts must be in 1..64")
         self.batch = int(batch)
+        self.publish = bool(publish)
         self.key = model_key(seed, "neighbour-sampler")
         L = len(self.fanouts)
         need_t = [l < L - 1 for l in range(L)]
-        self.slots = [_Slot(self.dev, self.n, self.batch, self.fanouts, need_t) for _ in range(slots)]
+        self.slots = [_Slot(self.dev, self.n, self.batch, self.fanouts, need_t, self.publish) for _ in range(slots)]
         self.flag = torch.zeros(self.n + 1, dtype=torch.uint8, device=self.dev)
         self.map = torch.zeros(self.n + 1, dtype=torch.int32, device=self.dev)
         ns = native.hip().gnn_sample_blocks_scratch(self.n, self.fanouts, self.slots[0].nd_max)
         self.bscratch = torch.zeros(ns, dtype=torch.int32, device=self.dev)
-        self.stream = torch.cuda.Stream(device=self.dev)
+        # a high-priority stream: the next batch's sampling is on the loop's critical path
+        self.stream = torch.cuda.Stream(device=self.dev, priority=-1)
         self._next = 0
+        self._w = None
+        if threaded:
+            if not self.publish:
+                raise ValueError("the threaded sampler needs publish=True (no copy on its stream)")
+            hip = native.hip()
+            p = lambda ts: [t.data_ptr() if t is not None else 0 for t in ts]
+            dev_index = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+            self._w = hip.gnn_sw_create(dev_index, self.stream.cuda_stream, self.rowptr.data_ptr(),
+                                        self.col.data_ptr(), self.n, self.fanouts, self.slots[0].nd_max,
+                                        self.flag.data_ptr(), self.map.data_ptr(), self.bscratch.data_ptr(),
+                                        int(self.key[0]), int(self.key[1]))
+            # runs before the buffers are released: joins the thread, drains the stream
+            weakref.finalize(self, hip.gnn_sw_destroy, self._w)
+            for sl in self.slots:
+                sl.widx = hip.gnn_sw_add_slot(self._w, p(sl.optr), p(sl.inv), p(sl.picks), p(sl.local), p(sl.src),
+                                              p(sl.rp_t), p(sl.col_t), p(sl.cnt_t), sl.counts.data_ptr(),
+                                              sl.host_ptr)
 
-    def enqueue(self, seeds: torch.Tensor, salt: int) -> SampledBatch:
-        """Start sampling ``seeds`` (int32 device tensor, <= batch) on the side stream."""
+    def enqueue(self, seeds: torch.Tensor, salt: int, ready: Optional[torch.cuda.Event] = None) -> SampledBatch:
+        """Start sampling ``seeds`` (int32 device tensor, <= batch) on the side stream.
+        ``ready``: an event after which the seeds are valid (default: everything enqueued
+        on the current stream so far)."""
         if seeds.numel() > self.batch:
             raise ValueError("more seeds than the sampler's batch bound")
         from ..utils import checks
@@ -262,19 +323,31 @@ class PipelinedSampler:
         self._next = (self._next + 1) % len(self.slots)
         main = torch.cuda.current_stream(self.dev)
         seeds = seeds.to(dtype=torch.int32).contiguous()
+        if self._w is not None:
+            if ready is None:
+                ready = torch.cuda.Event()
+                ready.record(main)
+            sl.keep = (ready, seeds)          # alive until the job is issued (and resolved)
+            seeds.record_stream(self.stream)
+            seq = native.hip().gnn_sw_submit(self._w, sl.widx, seeds.data_ptr(), int(seeds.numel()),
+                                             int(salt) & 0xFFFFFFFF, [ready.cuda_event, sl.free.cuda_event])
+            return SampledBatch(sl, self.fanouts, int(seeds.numel()), waiter=(self._w, seq))
+        p = lambda ts: [t.data_ptr() if t is not None else 0 for t in ts]
         with torch.cuda.stream(self.stream):
-            self.stream.wait_stream(main)            # the seeds were written on the main stream
-            if sl.free is not None:
-                self.stream.wait_event(sl.free)      # the slot's previous batch has trained
-            p = lambda ts: [t.data_ptr() if t is not None else 0 for t in ts]
+            if ready is None:
+                self.stream.wait_stream(main)
+            else:
+                self.stream.wait_event(ready)
+            # the slot's previous batch has trained (no-op before the first record)
+            self.stream.wait_event(sl.free)
             native.hip().gnn_sample_blocks(
                 self.rowptr.data_ptr(), self.col.data_ptr(), self.n, seeds.data_ptr(), int(seeds.numel()),
                 self.fanouts, sl.nd_max, p(sl.optr), p(sl.inv), p(sl.picks), p(sl.local), p(sl.src), p(sl.rp_t),
                 p(sl.col_t), p(sl.cnt_t), sl.counts.data_ptr(), self.flag.data_ptr(), self.map.data_ptr(),
                 self.bscratch.data_ptr(), int(self.key[0]), int(self.key[1]), int(salt) & 0xFFFFFFFF,
-                self.stream.cuda_stream)
-            sl.counts_host.copy_(sl.counts, non_blocking=True)
-            sl.done = torch.cuda.Event()
+                self.stream.cuda_stream, counts_host=sl.host_ptr)
+            if not self.publish:
+                sl.counts_host.copy_(sl.counts, non_blocking=True)
             sl.done.record(self.stream)
             seeds.record_stream(self.stream)
         return SampledBatch(sl, self.fanouts, int(seeds.numel()))
@@ -284,6 +357,4 @@ class PipelinedSampler:
         stream): the slot may be refilled after it."""
         main = torch.cuda.current_stream(self.dev)
         main.wait_event(batch.slot.done)
-        ev = torch.cuda.Event()
-        ev.record(main)
-        batch.slot.free = ev
+        batch.slot.free.record(main)

@@ -35,6 +35,47 @@ def test_spmm_matches_reference(F, ld, xbf, ybf):
     np.testing.assert_allclose(got.float().numpy(), ref.float().numpy(), rtol=tol, atol=tol)
 
 
+def _short_csr(n_rows, n_src, seed):
+    """CSR with mostly 0-3 entries per row and a few long rows (4..40), at random places."""
+    rng = np.random.default_rng(seed)
+    deg = rng.choice([0, 1, 1, 1, 2, 3], n_rows)
+    longr = rng.random(n_rows) < 0.05
+    deg[longr] = rng.integers(4, 41, int(longr.sum()))
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    col = rng.integers(0, n_src, int(rp[-1])).astype(np.int32)
+    return torch.from_numpy(rp), torch.from_numpy(col)
+
+
+@pytest.mark.parametrize("F,ld", [(256, 256), (100, 104), (40, 40), (600, 608)])
+@pytest.mark.parametrize("xdt,ydt,cs,init", [(torch.bfloat16, torch.bfloat16, True, True),
+                                             (torch.bfloat16, torch.bfloat16, False, False),
+                                             (torch.float32, torch.float32, True, False),
+                                             (torch.bfloat16, torch.float32, False, True),
+                                             (torch.float16, torch.float16, True, True)])
+def test_spmm_short_rows_bitwise_equals_row_kernel(F, ld, xdt, ydt, cs, init):
+    """The 4-rows-per-sub-group kernel (transposed sampled blocks) against the one-row
+    kernel: bit-identical, every row-length class (0-3 entries, long rows, rows past a
+    sub-group's first L edges, a partial last group); and against the fp32 reference."""
+    n_rows, n_src = 5003, 3001
+    rp, col = _short_csr(n_rows, n_src, 7)
+    torch.manual_seed(1)
+    X = torch.randn(n_src, ld)
+    X[:, F:] = 0
+    X = X.to(xdt).cuda()
+    csc = (torch.rand(n_src) + 0.5).cuda() if cs else None
+    rs = (torch.rand(n_rows) + 0.5).cuda()
+    ini = torch.randn(1200, ld).cuda() if init else None
+    kw = dict(rscale=rs, cscale=csc, init=ini, init_rows=1200 if init else None, out_dtype=ydt)
+    rpc, colc = rp.cuda(), col.cuda()
+    a = ops.spmm(rpc, colc, X, F, short_rows=True, **kw)
+    b = ops.spmm(rpc, colc, X, F, short_rows=False, **kw)
+    assert torch.equal(a, b)
+    ref = ops.spmm(rp, col, X.cpu().float(), F, rscale=rs.cpu(), cscale=None if csc is None else csc.cpu(),
+                   init=None if ini is None else ini.cpu(), init_rows=1200 if init else None, out_dtype=torch.float32)
+    tol = 1e-4 if ydt == torch.float32 and xdt == torch.float32 else 3e-2
+    np.testing.assert_allclose(a.float().cpu().numpy(), ref.numpy(), rtol=tol, atol=tol)
+
+
 @pytest.mark.parametrize("F,ld", [(1433, 1440), (1024, 1032), (600, 608)])
 def test_spmm_wide_rows_with_ones_column(F, ld):
     """Rows wider than one 512-column slab (Cora / Citeseer / Reddit widths): every

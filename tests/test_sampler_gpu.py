@@ -13,22 +13,24 @@ from cgnn_amd.gnn.sampler import DeviceSampler, PipelinedSampler
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("slots,publish,threaded", [(2, False, False), (3, True, False), (3, True, True)])
 @pytest.mark.parametrize("fanouts,batch", [([15, 10, 5], 1024), ([5, 5], 300), ([25, 64], 64)])
-def test_pipelined_sampler_matches_device_sampler(fanouts, batch):
+def test_pipelined_sampler_matches_device_sampler(fanouts, batch, slots, publish, threaded):
     g = synthetic("ogbn-products", seed=5, device="cuda:0", scale=0.02)
     ref = DeviceSampler(g.rowptr, g.col, fanouts, seed=3)
-    ps = PipelinedSampler(g.rowptr, g.col, fanouts, batch, seed=3)
+    ps = PipelinedSampler(g.rowptr, g.col, fanouts, batch, seed=3, slots=slots, publish=publish,
+                          threaded=threaded)
     rng = np.random.default_rng(0)
     pend = []
-    for k in range(5):                       # several in flight through the two slots
+    for k in range(7):                       # several in flight through the slots (each reused)
         seeds = torch.as_tensor(rng.choice(g.n, batch - (k % 2) * 7, replace=False).astype(np.int32),
                                 device="cuda:0")
-        pend.append((seeds, ps.enqueue(seeds, 1000 + k)))
-        if len(pend) == 2:
-            s0, b0 = pend.pop(0)
-            _check(ref, s0, b0, 1000 + k - 1)
-    for s0, b0 in pend:
-        _check(ref, s0, b0, 1004)
+        pend.append((seeds, 1000 + k, ps.enqueue(seeds, 1000 + k)))
+        if len(pend) == slots:
+            s0, salt, b0 = pend.pop(0)
+            _check(ref, s0, b0, salt)
+    for s0, salt, b0 in pend:
+        _check(ref, s0, b0, salt)
 
 
 def _check(ref, seeds, sb, salt):

@@ -11,10 +11,14 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _libasan():
-    out = subprocess.run(["g++", "-print-file-name=libasan.so"], stdout=subprocess.PIPE, text=True)
+def _gcc_lib(name):
+    out = subprocess.run(["g++", "-print-file-name=" + name], stdout=subprocess.PIPE, text=True)
     path = out.stdout.strip()
     return path if os.path.isabs(path) and os.path.exists(path) else None
+
+
+def _libasan():
+    return _gcc_lib("libasan.so")
 
 
 def test_runtime_under_address_and_ub_sanitizers(tmp_path):
@@ -25,7 +29,11 @@ def test_runtime_under_address_and_ub_sanitizers(tmp_path):
         pytest.skip("no libasan for the host compiler")
     target = str(tmp_path / ("_rt" + _build.EXT))
     _build.build_rt(force=True, debug=True, target=target)
-    env = dict(os.environ, LD_PRELOAD=asan, CGNN_RT_LIB=target,
+    # libstdc++ preloaded right after ASan: python itself does not link it, and ASan's
+    # __cxa_throw interceptor must resolve the real one when the runtime throws (a
+    # rejected argument), or the process aborts in the interceptor
+    pre = asan + (":" + _gcc_lib("libstdc++.so") if _gcc_lib("libstdc++.so") else "")
+    env = dict(os.environ, LD_PRELOAD=pre, CGNN_RT_LIB=target,
                ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1", OMP_NUM_THREADS="4")
     probe = subprocess.run([sys.executable, "-c", "from cgnn_amd import native; print(native.rt().__file__)"],

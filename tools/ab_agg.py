@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--only-agg", action="store_true")
     ap.add_argument("--only-spmm", action="store_true")
+    ap.add_argument("--only-ell", action="store_true", help="the backward's train-column aggregation (spmm_ell)")
     a = ap.parse_args()
     g = synthetic("ogbn-products", seed=0, device="cuda:0", scale=a.scale)
     tr = GCNTrainer(g, hidden=256, rank=0, world=1, reorder=True, fuse_agg=True)
@@ -56,8 +57,11 @@ def main():
         ops.agg_fwd(rp, col, tr.Xs, tr.AX, tr.W1, tr.b1, tr.W2, tr.dinv, tr.Z2loc, F, 0.5, key, step, 0,
                     kimg=tr._kimg, queue=tr._agg_queue)
 
-    todo = (("agg", agg),) if a.only_agg else (("spmm", spmm),) if a.only_spmm else (
-        ("spmm", spmm), ("dense", dense), ("agg", agg))
+    def ell():
+        ops.spmm_ell(tr._ell_T, tr.col_T, tr.Gc, tr.C, rscale=tr.dinv, out=tr.dY2)
+
+    todo = (("agg", agg),) if a.only_agg else (("spmm", spmm),) if a.only_spmm else (("ell", ell),) if a.only_ell \
+        else (("spmm", spmm), ("dense", dense), ("agg", agg))
     for name, fn in todo:
         res[name + "_us"], res[name + "_min_us"] = timed(fn, a.iters)
     print(json.dumps(res), flush=True)
