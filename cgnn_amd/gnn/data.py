@@ -203,22 +203,34 @@ def partition_order(name: str, seed: int = 0, scale: float = 1.0, homophily: flo
     return order
 
 
+# who ran the last shared_partition_order pass in this process, and for how long
+LAST_PARTITION = {"computed_here": False, "compute_s": 0.0}
+
+
 def shared_partition_order(name: str, seed: int = 0, scale: float = 1.0, **kw) -> np.ndarray:
     """``partition_order`` computed ONCE per job: rank 0 runs the pass with every CPU of
     its node (the other ranks wait in the broadcast, holding no copy of the structure)
     and broadcasts the order (parallel.dist.broadcast_host_array).  One process: plain
     ``partition_order``."""
+    import time
     from ..parallel import dist as pdist
+    global LAST_PARTITION
     if not pdist.is_distributed():
-        return partition_order(name, seed=seed, scale=scale, **kw)
+        t = time.perf_counter()
+        order = partition_order(name, seed=seed, scale=scale, **kw)
+        LAST_PARTITION = {"computed_here": True, "compute_s": round(time.perf_counter() - t, 2)}
+        return order
     n = _scaled_shape(name, scale)[0]
     order = None
+    LAST_PARTITION = {"computed_here": False, "compute_s": 0.0}
     if pdist.rank() == 0:
         pdist.set_host_threads(pdist.host_cpus())
+        t = time.perf_counter()
         try:
             order = partition_order(name, seed=seed, scale=scale, **kw)
         finally:
             pdist.set_host_threads()          # back to this rank's share
+        LAST_PARTITION = {"computed_here": True, "compute_s": round(time.perf_counter() - t, 2)}
     dt = np.int32 if n < (1 << 31) else np.int64
     out = pdist.broadcast_host_array(None if order is None else order.astype(dt), n, dtype=dt)
     return out.astype(np.int64)

@@ -27,6 +27,16 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 
+def _progress(msg):
+    """A progress line on stderr (long setups: the GPU runner takes a silent job as hung)."""
+    from cgnn_amd.parallel import dist as pdist
+    sys.stderr.write("[bench_gnn_configs rank %d %.1fs] %s\n" % (pdist.rank(), time.perf_counter() - _T0, msg))
+    sys.stderr.flush()
+
+
+_T0 = time.perf_counter()
+
+
 def _sync(dev):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
@@ -198,16 +208,24 @@ def main():
             # once per job (rank 0, every core) and broadcast: each rank computing the
             # whole 111 M-node pass held its own 13 GB structure and ran it on 1/8 of the cores
             from cgnn_amd.gnn.data import shared_partition_order
+            _progress("partition order (rank 0 computes, then broadcast)")
             order = shared_partition_order("ogbn-papers100M", seed=a.seed, scale=a.scale)
         part_s = time.perf_counter() - t0
+        _progress("partition done in %.1f s; generating the shard" % part_s)
         shard = synthetic_shard("ogbn-papers100M", srank, sworld, seed=a.seed, device=dev, scale=a.scale,
                                 order=order)
         del order
         gen_s = time.perf_counter() - t0 - part_s
+        _progress("shard generated in %.1f s" % gen_s)
         if world > 1:                     # every rank's setup split, reported by rank 0
             import torch.distributed as dist
             split = [None] * world
-            dist.all_gather_object(split, {"partition_s": round(part_s, 2), "gen_s": round(gen_s, 2)})
+            from cgnn_amd.gnn import data as gdata
+            mine = {"partition_s": round(part_s, 2), "gen_s": round(gen_s, 2)}
+            if a.partition == "locality":      # waiting in the broadcast vs running the pass
+                mine.update(partition_computed_here=gdata.LAST_PARTITION["computed_here"],
+                            partition_compute_s=gdata.LAST_PARTITION["compute_s"])
+            dist.all_gather_object(split, mine)
             res["setup_per_rank"] = split
         n_nodes, nnz_local, n_local = shard.n, shard.nnz, shard.n_local
         tr = ShardedGATTrainer(shard, heads=4, head_dim=32, dropout=0.5, lr=0.005, seed=a.seed, emulate=emu,
@@ -216,6 +234,7 @@ def main():
             tr.halo.grad_wire = torch.bfloat16
         del shard
         setup = time.perf_counter() - t_setup
+        _progress("trainer ready (setup %.1f s); timing %d + %d epochs" % (setup, warmup, steps))
         if dev.type == "cuda":
             torch.cuda.reset_peak_memory_stats(dev)
         dt = _timed(tr.train_step, steps, warmup, dev)
