@@ -86,7 +86,7 @@ struct EngineBuffers {
   const uint32_t* keys = nullptr;
   float* rff_w = nullptr;       // [R][7k][D+1]
   float* rff_diff = nullptr;    // [R][7k]
-  float* rff_scratch = nullptr; // wide joints (D > 256): rff_wide_scratch_floats(N, 7k, R)
+  float* rff_scratch = nullptr; // the wide form (engine.batch.WIDE_RFF_D): rff_wide_scratch_floats(N, 7k, R)
   float* xnorm = nullptr;       // [R][N] squared norms of xhat rows (written by gen_fwd)
   const float* ynorm = nullptr; // [R][N] squared norms of the data rows
   float* dxs = nullptr;         // [R][d_true][N] dL/dx scratch of a staged backward whose state is global
@@ -132,7 +132,8 @@ class Engine {
                              c_.R, st_), "rff_freqs");
       check(rff_launch_fwd_bwd(train ? 0 : 1, b_.xhat, b_.data, b_.rff_w, b_.rff_diff, b_.lpart,
                                b_.gradp, c_.N, c_.D, rff_features(), c_.R, c_.rff_k,
-                               sqrtf(2.f / (float)c_.rff_k), st_, 0, b_.rff_scratch, 0), "rff");
+                               sqrtf(2.f / (float)c_.rff_k), st_, 0, b_.rff_scratch,
+                               b_.rff_scratch != nullptr), "rff");
     } else if (c_.mfma) {
       const float inv = 1.f / ((float)c_.N * (float)c_.N);
       check(cgnn_launch_mmd_mfma(train ? (need_loss ? 0 : 3) : 1, c_.D, b_.xhat, b_.data, b_.xnorm, b_.ynorm,

@@ -168,7 +168,7 @@ template <int L, int G, int WT, int EC>
 __global__ __launch_bounds__(256) GAT_WAVES_ATTR void gat_fwd_kernel(GatFwdArgs a) {
   constexpr int RPW = 64 / L;
   const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
-  const int row = (xcd_remap(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
+  const int row = (xcd_remap_chunked<64>(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
   const bool rv = row < a.n;
   const int f0 = 8 * sl, K = a.K, HF = a.HF;
   const bool fv = rv && f0 < HF;
@@ -414,7 +414,7 @@ template <int L, int G, int WT, int EC>
 __global__ __launch_bounds__(256) GAT_WAVES_ATTR void gat_col_kernel(GatColArgs a) {
   constexpr int RPW = 64 / L;
   const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
-  const int row = (xcd_remap(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
+  const int row = (xcd_remap_chunked<64>(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * RPW + sub;
   const bool rv = row < a.n;
   const int f0 = 8 * sl, K = a.K, HF = a.HF;
   const bool fv = rv && f0 < HF;

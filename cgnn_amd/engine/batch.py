@@ -22,7 +22,9 @@ from .program import Program, pack_programs, pack_schedules
 SUPPORTED_D = (1, 2, 3, 4, 6, 8, 12, 16, 20, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256,
                320, 384, 448, 512, 640, 768, 896, 1024)
 MAX_D = 16384             # above 1024: every multiple of 256 (runtime-width grouped MMD)
-WIDE_RFF_D = 256          # above: rff_kernels.hip's wide form (theta scratch image)
+# above: rff_kernels.hip's wide form (theta scratch image); at and below: the forms compiled
+# per width.  The wide form is 2-11x faster from D = 64 up (tools/ab_rff.py, profiles/r05_rff)
+WIDE_RFF_D = 32
 MAX_VALU_D = 64
 MMD_TILE = 256
 TARGET_WGS = 2048

@@ -80,6 +80,9 @@ def main():
     ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--partition", choices=["locality", "none"], default="locality",
                     help="papers-gat2: locality partition of the sharded graph (data.partition_order, timed in setup)")
+    ap.add_argument("--order-cache", default=None,
+                    help="papers-gat2, one process: load the partition order from this .npy file, or compute and "
+                         "save it there (A/B runs of one shape)")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal: every rank on cuda:0 with gloo collectives (multi-rank path on one GPU)")
     ap.add_argument("--sampler", choices=["pipelined", "device", "host"], default=None,
@@ -208,8 +211,14 @@ def main():
             # once per job (rank 0, every core) and broadcast: each rank computing the
             # whole 111 M-node pass held its own 13 GB structure and ran it on 1/8 of the cores
             from cgnn_amd.gnn.data import shared_partition_order
-            _progress("partition order (rank 0 computes, then broadcast)")
-            order = shared_partition_order("ogbn-papers100M", seed=a.seed, scale=a.scale)
+            if a.order_cache and world == 1 and os.path.exists(a.order_cache):
+                _progress("partition order from %s" % a.order_cache)
+                order = np.load(a.order_cache)
+            else:
+                _progress("partition order (rank 0 computes, then broadcast)")
+                order = shared_partition_order("ogbn-papers100M", seed=a.seed, scale=a.scale)
+                if a.order_cache and world == 1:
+                    np.save(a.order_cache, order)
         part_s = time.perf_counter() - t0
         _progress("partition done in %.1f s; generating the shard" % part_s)
         shard = synthetic_shard("ogbn-papers100M", srank, sworld, seed=a.seed, device=dev, scale=a.scale,
