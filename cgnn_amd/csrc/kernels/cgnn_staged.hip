@@ -254,12 +254,19 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
 // --------------------------------------------------------------------------- backward
 // per-wave LDS slab (floats)
 __host__ __device__ __forceinline__ int bwd_si(int max_in) { return (max_in + 2) | 1; }
+// parents whose dL/dparent partials a lane keeps in registers (PPR kernels): nodes of at
+// most PPR_MAX parents, i.e. max_in <= PPR_MAX + 1 (an input is the own noise)
+constexpr int PPR_MAX = 12;
+__host__ __device__ __forceinline__ bool bwd_ppr(int max_in) { return max_in <= PPR_MAX + 1; }
 __host__ __device__ __forceinline__ int bwd_slab(int max_in) {
-  // [64][SI] (padded even) + [64][ZS] + Gm pairs + weight rows + dL/dparent partials
-  return WAVE * (bwd_si(max_in) + 1) + WAVE * ZS + (max_in + 1) * HZ + (max_in + 2) * HZ + max_in * WAVE;
+  // [64][SI] (padded even) + [64][ZS] + Gm pairs + weight rows (+ dL/dparent partials,
+  // unless they live in registers: at d = 200 that is 12.6 -> 9.8 KB per wave, 3 -> 4
+  // four-wave blocks per CU)
+  return WAVE * (bwd_si(max_in) + 1) + WAVE * ZS + (max_in + 1) * HZ + (max_in + 2) * HZ +
+         (bwd_ppr(max_in) ? 0 : max_in * WAVE);
 }
 
-template <bool XG, bool DG>
+template <bool XG, bool DG, bool PPR>
 __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
     const int* __restrict__ prog, int ps, const int* __restrict__ sched, int ss,
     const float* __restrict__ params, int P, const float* __restrict__ xhat, const float* __restrict__ noise,
@@ -286,9 +293,10 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
   float* slab = s_dx + (DG ? 0 : (size_t)Dt * WAVE) + (size_t)wave * bwd_slab(max_in);
   float* s_in = slab;                                        // [64][SI]
   float* s_z = slab + WAVE * (SI + 1);                       // [64][ZS]
-  f2* s_g = reinterpret_cast<f2*>(s_z + WAVE * ZS);          // [(max_in + 1) * HZP]
+  f2* s_g = reinterpret_cast<f2*>(s_z + WAVE * ZS);          // Gm: [(max_in + 1)][HZ] floats
   float* s_w = s_z + WAVE * ZS + (max_in + 1) * HZ;          // [max_in + 2][16] weight rows
-  float* s_pp = s_w + (max_in + 2) * HZ;                     // [max_in][64] dL/dparent
+  float* s_pp = s_w + (max_in + 2) * HZ;                     // [max_in][64] dL/dparent (!PPR)
+  float pp[PPR ? PPR_MAX : 1];                                // dL/dparent (PPR)
   float* my_in = s_in + lane * SI;
   float* my_z = s_z + lane * ZS;
 
@@ -439,67 +447,74 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
         for (int q = 0; q < HZ; ++q) mg[q] = (q < hc && pre[q] > 0.f) ? gout : 0.f;
         // ---- this chunk's share of dL/dparent, kept in the slab until the node ends ----
         wrow(nin + 1, w2);
-        for (int j = 0; j < npar; ++j) {
-          wrow(j, w);
-          float s = 0.f;
+        if constexpr (PPR) {
 #pragma unroll
-          for (int q = 0; q < HZ; ++q) s = fmaf(w[q] * w2[q], mg[q], s);
-          s_pp[j * WAVE + lane] = q0 == 0 ? s : s_pp[j * WAVE + lane] + s;
+          for (int j = 0; j < PPR_MAX; ++j)
+            if (j < npar) {                    // wave-uniform
+              wrow(j, w);
+              float s = 0.f;
+#pragma unroll
+              for (int q = 0; q < HZ; ++q) s = fmaf(w[q] * w2[q], mg[q], s);
+              pp[j] = q0 == 0 ? s : pp[j] + s;
+            }
+        } else {
+          for (int j = 0; j < npar; ++j) {
+            wrow(j, w);
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < HZ; ++q) s = fmaf(w[q] * w2[q], mg[q], s);
+            s_pp[j * WAVE + lane] = q0 == 0 ? s : s_pp[j * WAVE + lane] + s;
+          }
         }
 #pragma unroll
         for (int qp = 0; qp < HZP; ++qp)
           *reinterpret_cast<f2*>(my_z + 2 * qp) = f2{mg[2 * qp], mg[2 * qp + 1]};
         wave_sync();
 
-        // ---- Gm[j][q] = sum_s in[s][j] mg[s][q] over the 64 samples: items (row j,
-        // column pair), the samples split over 2 or 4 lane groups when items are few ----
-        const int hp = (hc + 1) >> 1;
-        const int n_items = (nin + 1) * hp;
-        const int grp = n_items <= 16 ? 4 : n_items <= 32 ? 2 : 1;
-        const int span = WAVE / grp;
-        const int part = lane / span, il = lane - part * span;
-        const int s_lo = part * span, s_n = span;
-        for (int it0 = 0; it0 < n_items; it0 += span) {
-          const int it = it0 + il;
-          f2 acc0 = {0.f, 0.f}, acc1 = {0.f, 0.f};
-          if (it < n_items) {
-            const int j = it / hp, qp = it - j * hp;
-            const float* a = s_in + s_lo * SI + j;
-            const float* zb = s_z + s_lo * ZS + 2 * qp;
+        // ---- Gm[j][q] = sum_s in[s][j] mg[s][q] over the 64 samples on the matrix cores
+        // (v_mfma_f32_16x16x4_f32: fp32 products, fp32 accumulation): A = in^T (16 input
+        // rows x 4 samples, from the input slab), B = mg (4 samples x 16 units, from the
+        // mg slab), 16 k-steps for the tile's 64 samples; D = 16 input rows x 16 units
+        // (lane 16 g + c: rows 4 g .. 4 g + 3, unit c).  Replaces a per-lane item loop of
+        // 64 LDS reads and 64 VALU per chunk with 32 LDS reads and 16 MFMAs. ----
+        {
+          typedef float f32x4 __attribute__((ext_vector_type(4)));
+          float* s_gf = reinterpret_cast<float*>(s_g);              // [max_in + 1][HZ]
+          const int jq = lane & 15, sg = lane >> 4;
+          const float w2q = s_w[(nin + 1) * HZ + jq];
+          for (int j0 = 0; j0 <= nin; j0 += 16) {
+            const int jr = min(j0 + jq, nin);
+            const float am = j0 + jq <= nin ? 1.f : 0.f;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-            for (int s2 = 0; s2 < s_n; s2 += 2) {
-              const float a0 = a[s2 * SI], a1 = a[(s2 + 1) * SI];
-              const f2 z0 = *reinterpret_cast<const f2*>(zb + s2 * ZS);
-              const f2 z1 = *reinterpret_cast<const f2*>(zb + (s2 + 1) * ZS);
-              acc0 = f2{a0, a0} * z0 + acc0;
-              acc1 = f2{a1, a1} * z1 + acc1;
+            for (int t = 0; t < WAVE / 4; ++t) {
+              const int smp = 4 * t + sg;
+              const float a = s_in[smp * SI + jr] * am;
+              const float b = s_z[smp * ZS + jq];
+              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
             }
-          }
-          f2 acc = acc0 + acc1;
-          if (grp >= 2) acc += f2{__shfl_xor(acc.x, 32), __shfl_xor(acc.y, 32)};
-          if (grp == 4) acc += f2{__shfl_xor(acc.x, 16), __shfl_xor(acc.y, 16)};
-          if (part == 0 && it < n_items) {
-            const int j = it / hp, qp = it - j * hp, q = 2 * qp;
-            const f2 w2p = *reinterpret_cast<const f2*>(s_w + (nin + 1) * HZ + q);
-            s_g[j * HZP + qp] = acc;
-            gp[poff + j * H + q0 + q] = w2p.x * acc.x;                 // dW1 / db1
-            if (q + 1 < hc) gp[poff + j * H + q0 + q + 1] = w2p.y * acc.y;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int j = j0 + 4 * sg + i;
+              if (j <= nin && jq < hc) {
+                s_gf[j * HZ + jq] = acc[i];
+                gp[poff + j * H + q0 + jq] = w2q * acc[i];                // dW1 / db1
+              }
+            }
           }
         }
         wave_sync();
         // dW2[q] = sum_j W1ext[j][q] Gm[j][q]
         if (lane < hc) {
+          const float* s_gf = reinterpret_cast<const float*>(s_g);
           float s = 0.f;
-          for (int j = 0; j <= nin; ++j) {
-            const f2 gm = s_g[j * HZP + (lane >> 1)];
-            s = fmaf(s_w[j * HZ + lane], (lane & 1) ? gm.y : gm.x, s);
-          }
+          for (int j = 0; j <= nin; ++j) s = fmaf(s_w[j * HZ + lane], s_gf[j * HZ + lane], s);
           gp[poff + (nin + 1) * H + q0 + lane] = s;
         }
         wave_sync();
       }
       // ---- push dL/dparent (each parent is this wave's alone in the sub-stage) ----
-      for (int j0 = 0; j0 < npar; j0 += 8) {
+      auto push = [&](int j0, auto part) {
         float cur[8];
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
@@ -510,13 +525,20 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
         for (int jj = 0; jj < 8; ++jj)
           if (j0 + jj < npar) {
             const int pv = uni(pg + paroff + j0 + jj);
-            const float v = cur[jj] + s_pp[(j0 + jj) * WAVE + lane];
+            const float v = cur[jj] + part(jj);
             if (DG) {
               if (valid) dx[(size_t)pv * N + n] = v;
             } else {
               s_dx[pv * WAVE + lane] = v;
             }
           }
+      };
+      if constexpr (PPR) {
+        // static register indices: batches at 0 and 8 (PPR_MAX = 12)
+        if (npar > 0) push(0, [&](int jj) { return pp[jj]; });
+        if (npar > 8) push(8, [&](int jj) { return 8 + jj < PPR_MAX ? pp[(8 + jj) % PPR_MAX] : 0.f; });
+      } else {
+        for (int j0 = 0; j0 < npar; j0 += 8) push(j0, [&](int jj) { return s_pp[(j0 + jj) * WAVE + lane]; });
       }
       const float g2 = wave_sum(gout);                               // db2
       if (lane == 0) gp[poff + (nin + 2) * H] = g2;
@@ -648,15 +670,19 @@ extern "C" int cgnn_launch_gen_bwd_staged(const int* prog, int ps, const int* sc
   const int T = cgnn_staged_tiles(N);
   const size_t lds = bwd_lds(Dt, wb, max_in, xg, dg, 0);
   dim3 grid((unsigned)(T * R)), block(WAVE * wb);
-#define BWD(XG, DG)                                                                                            \
-  {                                                                                                            \
-    allow_lds(gen_bwd_staged_kernel<XG, DG>, lds);                                                             \
-    hipLaunchKernelGGL((gen_bwd_staged_kernel<XG, DG>), grid, block, lds, st, prog, ps, sched, ss, params, P,  \
-                       xhat, noise, NS, gradp, n_chunks, R, N, D, Dt, H, max_in, T, gpart, dxs);               \
+#define BWD(XG, DG, PPR)                                                                                          \
+  {                                                                                                               \
+    allow_lds(gen_bwd_staged_kernel<XG, DG, PPR>, lds);                                                           \
+    hipLaunchKernelGGL((gen_bwd_staged_kernel<XG, DG, PPR>), grid, block, lds, st, prog, ps, sched, ss, params, P, \
+                       xhat, noise, NS, gradp, n_chunks, R, N, D, Dt, H, max_in, T, gpart, dxs);                  \
   }
-  if (!xg) BWD(false, false)
-  else if (!dg) BWD(true, false)
-  else BWD(true, true)
+#define BWD_P(PPR)                     \
+  if (!xg) BWD(false, false, PPR)      \
+  else if (!dg) BWD(true, false, PPR)  \
+  else BWD(true, true, PPR)
+  if (bwd_ppr(max_in)) BWD_P(true)
+  else BWD_P(false)
+#undef BWD_P
 #undef BWD
   return (int)hipGetLastError();
 }
