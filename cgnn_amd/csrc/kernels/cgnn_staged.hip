@@ -256,12 +256,13 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
 __host__ __device__ __forceinline__ int bwd_si(int max_in) { return (max_in + 2) | 1; }
 // parents whose dL/dparent partials a lane keeps in registers (PPR kernels): nodes of at
 // most PPR_MAX parents, i.e. max_in <= PPR_MAX + 1 (an input is the own noise)
-constexpr int PPR_MAX = 12;
+constexpr int PPR_MAX = 16;
 __host__ __device__ __forceinline__ bool bwd_ppr(int max_in) { return max_in <= PPR_MAX + 1; }
 __host__ __device__ __forceinline__ int bwd_slab(int max_in) {
-  // [64][SI] (padded even) + [64][ZS] + Gm pairs + weight rows (+ dL/dparent partials,
-  // unless they live in registers: at d = 200 that is 12.6 -> 9.8 KB per wave, 3 -> 4
-  // four-wave blocks per CU)
+  // [64][SI] (padded even) + [64][ZS] + Gm rows + weight rows (+ dL/dparent partials,
+  // unless they live in registers: d = 200 with 400 edges (max_in 11) 12.6 -> 9.8 KB per
+  // wave, 3 -> 4 four-wave blocks per CU; with 736 edges (max_in 17) 16.4 -> 12.1 KB,
+  // 2 -> 3 blocks)
   return WAVE * (bwd_si(max_in) + 1) + WAVE * ZS + (max_in + 1) * HZ + (max_in + 2) * HZ +
          (bwd_ppr(max_in) ? 0 : max_in * WAVE);
 }
@@ -426,49 +427,56 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
           }
         }
         wave_sync();
-        auto wrow = [&](int row, float* w) {        // 16 weights of a row (LDS broadcast)
+        // ---- the chunk's recompute and dL/dparent share (a 4-wide path for tail chunks
+        // of <= 4 units measured slower: its registers cost the occupancy,
+        // profiles/r05_cgnn_bwd) ----
+        {
+          constexpr int CW = HZ;
+          auto wrow = [&](int row, float* w) {      // CW weights of a row (LDS broadcast)
 #pragma unroll
-          for (int c = 0; c < HZ / 4; ++c) {
-            const float4 v4 = *reinterpret_cast<const float4*>(s_w + row * HZ + 4 * c);
-            w[4 * c] = v4.x; w[4 * c + 1] = v4.y; w[4 * c + 2] = v4.z; w[4 * c + 3] = v4.w;
+            for (int c = 0; c < CW / 4; ++c) {
+              const float4 v4 = *reinterpret_cast<const float4*>(s_w + row * HZ + 4 * c);
+              w[4 * c] = v4.x; w[4 * c + 1] = v4.y; w[4 * c + 2] = v4.z; w[4 * c + 3] = v4.w;
+            }
+          };
+          // recompute this chunk's pre-activations (one sample per lane)
+          float pre[CW], w[CW], w2[CW];
+          wrow(nin, pre);
+          for (int j = 0; j < nin; ++j) {
+            const float x = my_in[j];
+            wrow(j, w);
+#pragma unroll
+            for (int q = 0; q < CW; ++q) pre[q] = fmaf(w[q], x, pre[q]);
           }
-        };
-        // ---- recompute this chunk's pre-activations (one sample per lane) ----
-        float pre[HZ], w[HZ], w2[HZ];
-        wrow(nin, pre);
-        for (int j = 0; j < nin; ++j) {
-          const float x = my_in[j];
-          wrow(j, w);
+          float mg[CW];
 #pragma unroll
-          for (int q = 0; q < HZ; ++q) pre[q] = fmaf(w[q], x, pre[q]);
-        }
-        float mg[HZ];
+          for (int q = 0; q < CW; ++q) mg[q] = (q < hc && pre[q] > 0.f) ? gout : 0.f;
+          // this chunk's share of dL/dparent, kept until the node ends
+          wrow(nin + 1, w2);
+          if constexpr (PPR) {
 #pragma unroll
-        for (int q = 0; q < HZ; ++q) mg[q] = (q < hc && pre[q] > 0.f) ? gout : 0.f;
-        // ---- this chunk's share of dL/dparent, kept in the slab until the node ends ----
-        wrow(nin + 1, w2);
-        if constexpr (PPR) {
+            for (int j = 0; j < PPR_MAX; ++j)
+              if (j < npar) {                  // wave-uniform
+                wrow(j, w);
+                float s = 0.f;
 #pragma unroll
-          for (int j = 0; j < PPR_MAX; ++j)
-            if (j < npar) {                    // wave-uniform
+                for (int q = 0; q < CW; ++q) s = fmaf(w[q] * w2[q], mg[q], s);
+                pp[j] = q0 == 0 ? s : pp[j] + s;
+              }
+          } else {
+            for (int j = 0; j < npar; ++j) {
               wrow(j, w);
               float s = 0.f;
 #pragma unroll
-              for (int q = 0; q < HZ; ++q) s = fmaf(w[q] * w2[q], mg[q], s);
-              pp[j] = q0 == 0 ? s : pp[j] + s;
+              for (int q = 0; q < CW; ++q) s = fmaf(w[q] * w2[q], mg[q], s);
+              s_pp[j * WAVE + lane] = q0 == 0 ? s : s_pp[j * WAVE + lane] + s;
             }
-        } else {
-          for (int j = 0; j < npar; ++j) {
-            wrow(j, w);
-            float s = 0.f;
-#pragma unroll
-            for (int q = 0; q < HZ; ++q) s = fmaf(w[q] * w2[q], mg[q], s);
-            s_pp[j * WAVE + lane] = q0 == 0 ? s : s_pp[j * WAVE + lane] + s;
           }
-        }
 #pragma unroll
-        for (int qp = 0; qp < HZP; ++qp)
-          *reinterpret_cast<f2*>(my_z + 2 * qp) = f2{mg[2 * qp], mg[2 * qp + 1]};
+          for (int qp = 0; qp < HZP; ++qp)
+            *reinterpret_cast<f2*>(my_z + 2 * qp) =
+                2 * qp < CW ? f2{mg[min(2 * qp, CW - 1)], mg[min(2 * qp + 1, CW - 1)]} : f2{0.f, 0.f};
+        }
         wave_sync();
 
         // ---- Gm[j][q] = sum_s in[s][j] mg[s][q] over the 64 samples on the matrix cores
@@ -534,7 +542,7 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
           }
       };
       if constexpr (PPR) {
-        // static register indices: batches at 0 and 8 (PPR_MAX = 12)
+        // static register indices: batches at 0 and 8 (PPR_MAX = 16)
         if (npar > 0) push(0, [&](int jj) { return pp[jj]; });
         if (npar > 8) push(8, [&](int jj) { return 8 + jj < PPR_MAX ? pp[(8 + jj) % PPR_MAX] : 0.f; });
       } else {
