@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 5: staged CGNN backward with the recompute and dL/dparent on v_mfma_f32_16x16x4_f32
+# (tree) against the committed VALU form (bwdP16)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05_cgnnbwd6
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_cgnn_wide_gpu.py tests/test_cgnn_kernels_gpu.py -x -q --timeout 300 --timeout-method thread -k "staged or wide" > $O/tests.log 2>&1 \
+   || { echo tests failed; grep -E "FAILED|Error|assert" $O/tests.log | head; tail -n 20 $O/tests.log; exit 1; }
+tail -n 1 $O/tests.log
+for e in 736 400; do
+for v in bwdP16 tree; do
+  if [ $v = tree ]; then unset CGNN_HIP_LIB; else export CGNN_HIP_LIB=$PWD/abv/$v/_hip.cpython-310-x86_64-linux-gnu.so; fi
+  timeout -k 10 300 python -u tools/ab_staged.py --d 200 --edges $e --R 256 --n 500 --h 20 --only bwd:4:2 > $O/ab_${v}_$e.log 2>&1 || { echo ab $v failed; tail $O/ab_${v}_$e.log; exit 1; }
+  echo $v $e $(grep bwd $O/ab_${v}_$e.log)
+done
+done
+for v in bwdP16 tree; do
+  if [ $v = tree ]; then unset CGNN_HIP_LIB; else export CGNN_HIP_LIB=$PWD/abv/$v/_hip.cpython-310-x86_64-linux-gnu.so; fi
+  timeout -k 10 300 python -u tools/bench_cgnn_batch.py --d 200 --edges 736 --R 256 --n 500 --h 20 > $O/batch_${v}_736.log 2>&1 || { echo batch $v failed; tail $O/batch_$v.log; exit 1; }
+  echo $v $(grep '^{' $O/batch_${v}_736.log | cut -c1-300)
+done
+echo done
