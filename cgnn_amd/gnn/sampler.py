@@ -158,6 +158,13 @@ def sample_reference(rowptr: np.ndarray, col: np.ndarray, seeds: np.ndarray, fan
     return out_blocks
 
 
+# priority of the sampler's stream.  With two batches sampled ahead the sampling is off
+# the critical path, and a normal-priority stream leaves the training kernels first
+# pick of the CUs: 10.21 / 10.30 epochs/s against 10.12 / 9.99 at high priority
+# (tools/ab_sage_prio.py, profiles/r05_sage/ab_sage_prio.log)
+STREAM_PRIORITY = 0
+
+
 class _Slot:
     """Device buffers of one in-flight mini-batch (upper-bound sizes)."""
 
@@ -244,7 +251,7 @@ class SampledBatch:
 class PipelinedSampler:
     """The whole multi-level sampling of a mini-batch as ONE native call
     (``gnn_sample_blocks``: ~13 HIP kernels per level, device-side row counts, no
-    host synchronisation inside) on a high-priority side stream, over ``slots``
+    host synchronisation inside) on a side stream, over ``slots``
     buffers: batch k + 1 (and k + 2) is sampled while batch k trains.  The level
     sizes reach the host through mapped host memory a kernel writes (``publish``;
     else one pinned copy per batch).  Same draws and relabelling as
@@ -288,8 +295,8 @@ class PipelinedSampler:
         self.map = torch.zeros(self.n + 1, dtype=torch.int32, device=self.dev)
         ns = native.hip().gnn_sample_blocks_scratch(self.n, self.fanouts, self.slots[0].nd_max)
         self.bscratch = torch.zeros(ns, dtype=torch.int32, device=self.dev)
-        # a high-priority stream: the next batch's sampling is on the loop's critical path
-        self.stream = torch.cuda.Stream(device=self.dev, priority=-1)
+        # stream priority (STREAM_PRIORITY; -1 = high, 0 = normal)
+        self.stream = torch.cuda.Stream(device=self.dev, priority=STREAM_PRIORITY)
         self._next = 0
         self._w = None
         if threaded:
