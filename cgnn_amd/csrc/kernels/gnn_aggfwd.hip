@@ -43,6 +43,9 @@ constexpr int TILE = 32;
 constexpr int NQ = 8;                 // work queues (XCDs)
 constexpr int RING = 4;               // chunk slots per block
 constexpr int RQ = 64;                // ready-tile queue entries per block
+// A/B build options (tools/build_variant.sh -D..., profiles/r05_agg): AGG_RPC = rows per
+// chunk claim in units of 64 (the kept value 1); AGG_GATHER_ONLY = skip the dense tiles
+// (times the gather half alone).  Neither changes the default build's results.
 #ifndef AGG_RPC
 #define AGG_RPC 1
 #endif
