@@ -159,7 +159,7 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
 // ordered graph shard: papers100M GAT rank-0-of-8 dry run 38.8 -> 34.8 ms at scale 0.5,
 // profiles/r05_gat).  Bijective; the ragged tail (< 8 C blocks) keeps its ids.
 template <unsigned C>
-__device__ __forceinline__ unsigned xcd_remap_chunked(unsigned b, unsigned nwg) {
+__host__ __device__ __forceinline__ unsigned xcd_remap_chunked(unsigned b, unsigned nwg) {
   const unsigned full = nwg / (8u * C) * (8u * C);
   if (b >= full) return b;
   const unsigned xcd = b & 7u, idx = b >> 3;
@@ -173,7 +173,7 @@ __device__ __forceinline__ unsigned xcd_remap_chunked(unsigned b, unsigned nwg) 
 #ifndef CGNN_XCD_CHUNK
 #define CGNN_XCD_CHUNK 0
 #endif
-__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nwg) {
+__host__ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nwg) {
   // (A/B builds: -DCGNN_XCD_CHUNK=C turns every contiguous remap into the chunked one)
   if constexpr (CGNN_XCD_CHUNK > 0) return xcd_remap_chunked<CGNN_XCD_CHUNK>(b, nwg);
   const unsigned q = nwg >> 3, r = nwg & 7u;

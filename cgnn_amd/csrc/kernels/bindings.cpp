@@ -4,6 +4,7 @@
 // extension never allocates device memory itself, PyTorch's caching allocator
 // owns all buffers.
 #include <hip/hip_runtime.h>
+#include "cgnn_common.h"
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <stdint.h>
@@ -533,6 +534,17 @@ PYBIND11_MODULE(_hip, m) {
     gnn_sw_destroy((void*)(uintptr_t)h);
   });
   m.def("host_mapped_free", [](uint64_t h) { (void)hipHostFree((void*)(uintptr_t)h); });
+  // the XCD block remaps of the kernels (cgnn_common.h), evaluated on the host (tests:
+  // every form is a bijection of the grid)
+  m.def("xcd_remap_table", [](unsigned nwg, unsigned chunk) {
+    std::vector<unsigned> out(nwg);
+    for (unsigned b = 0; b < nwg; ++b)
+      out[b] = chunk == 0 ? cgnn::xcd_remap(b, nwg)
+               : chunk == 64 ? cgnn::xcd_remap_chunked<64>(b, nwg)
+               : chunk == 512 ? cgnn::xcd_remap_chunked<512>(b, nwg)
+               : throw std::runtime_error("xcd_remap_table: chunk must be 0, 64 or 512");
+    return out;
+  });
   m.def("gnn_fused_bwd_blocks", &gnn_fused_bwd_blocks);
   m.def("gnn_fused_bwd_width", &gnn_fused_bwd_width);
   m.def("gnn_fused_bwd_supported", &gnn_fused_bwd_supported);
