@@ -735,10 +735,17 @@ extern "C" int cgnn_staged_plan(int, int, int, int, int, int*);
 // batch elsewhere).  The choice depends only on the arguments: the scorer evaluates it
 // per program and batches programs of one family together (engine/scorer.py), so a
 // model's kernels -- and its score -- do not depend on its batch-mates.
+// The per-sample kernels walk the whole program in one wave, the level-scheduled ones
+// share a level's nodes over W waves: above GEN_PER_SAMPLE_MAX_D variables the latter
+// win (R = 256, N = 500, H = 20 train step: d = 22 334 vs 411 us, d = 40 735 vs 631,
+// d = 64 1777 vs 845, d = 100 3174 vs 1372; profiles/r05_family).
+constexpr int GEN_PER_SAMPLE_MAX_D = 32;
 extern "C" int cgnn_gen_bwd_variant(int H, int max_in, int Dt, int prog_stride) {
-  if (cgnn_gen_supported_h(H) && cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride) <= 160 * 1024) return 1;
+  const bool per_sample = cgnn_gen_supported_h(H) && cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride) <= 160 * 1024;
   int plan[5];
-  return cgnn_staged_plan(Dt, H, max_in, 8, 0, plan) == 0 ? 2 : 0;
+  const bool staged = cgnn_staged_plan(Dt, H, max_in, 8, 0, plan) == 0;
+  if (per_sample && (Dt <= GEN_PER_SAMPLE_MAX_D || !staged)) return 1;
+  return staged ? 2 : 0;
 }
 
 // whether the level-scheduled kernels cover (Dt, H, max_in) at all (a forced staged batch)

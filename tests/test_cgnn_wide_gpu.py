@@ -90,9 +90,9 @@ def test_staged_forward_bitwise_equals_per_sample():
     """The level-scheduled forward evaluates every node with the per-sample kernel's
     fmaf order, and the noise kernel draws the same Philox normals: the generated
     samples are bitwise equal."""
-    g = _random_dag(40, seed=3)
+    g = _random_dag(30, seed=3)                 # <= 32 variables: per-sample by default
     prog = program_for_dag(g, 20)
-    datas = [_data(40, 300, s) for s in range(3)]
+    datas = [_data(30, 300, s) for s in range(3)]
     keys = [model_key(4, "gb", r) for r in range(3)]
     a = DeviceTrainer([prog] * 3, datas, keys, 20, "cuda:0")
     assert a.bwd_variant == 1 and not a.staged

@@ -296,24 +296,26 @@ def _dag_with_max_in(d, k, seed):
 def test_device_batches_keep_each_program_on_its_own_kernel_family():
     """the generator kernels (per-sample or level-scheduled) are chosen per
     program, never from batch-wide maxima, so a candidate's score cannot depend on its
-    batch-mates: d = 140 programs with 4 and 20 inputs on one node fall in different
-    families and are batched apart, and every batch's combined shape keeps its family."""
+    batch-mates.  The family follows the variable count (per-sample up to 32 variables,
+    level-scheduled above, profiles/r05_family), whatever a program's widest node: at
+    d = 30 and d = 140, programs with 3 and 19 inputs on one node share their width's
+    family, every batch keeps one family, and its combined shape keeps it."""
     from cgnn_amd.engine.batch import kernel_family
     from cgnn_amd.engine.scorer import Job, _group_batches
-    d, H, N = 140, 20, 50
-    progs = [program_for_dag(_dag_with_max_in(d, k, s), H) for s, k in enumerate([3, 19, 3, 19, 3, 3, 19])]
-    fams = [kernel_family(d, H, p.max_in, len(p.prog)) for p in progs]
-    assert sorted(set(fams)) == [1, 2], fams
-    data = np.zeros((d, N), np.float32)
-    jobs = [Job(p, data, (0, i)) for i, p in enumerate(progs)]
-    batches = _group_batches(jobs, 16, H=H)
-    assert sorted(i for b in batches for i in b) == list(range(len(jobs)))
-    for b in batches:
-        assert len({fams[i] for i in b}) == 1, (b, fams)
-        ps = [progs[i] for i in b]
-        assert kernel_family(d, H, max(p.max_in for p in ps), max(len(p.prog) for p in ps)) == fams[b[0]]
-    # without H (the CPU reference path) only the shape matters
-    assert len(_group_batches(jobs, 16)) == 1
+    H, N = 20, 50
+    for d, fam in ((30, 1), (140, 2)):
+        progs = [program_for_dag(_dag_with_max_in(d, k, s), H) for s, k in enumerate([3, 19, 3, 19, 3, 3, 19])]
+        fams = [kernel_family(d, H, p.max_in, len(p.prog)) for p in progs]
+        assert set(fams) == {fam}, (d, fams)
+        data = np.zeros((d, N), np.float32)
+        jobs = [Job(p, data, (0, i)) for i, p in enumerate(progs)]
+        batches = _group_batches(jobs, 16, H=H)
+        assert sorted(i for b in batches for i in b) == list(range(len(jobs)))
+        for b in batches:
+            ps = [progs[i] for i in b]
+            assert kernel_family(d, H, max(p.max_in for p in ps), max(len(p.prog) for p in ps)) == fam
+        # without H (the CPU reference path) only the shape matters
+        assert len(_group_batches(jobs, 16)) == 1
 
 
 @pytest.mark.parametrize("fast", [False, True])

@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--test", type=int, default=100)
     ap.add_argument("--fast", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no hipGraph replay (for PMC collection)")
+    ap.add_argument("--generator", choices=["auto", "staged"], default="auto",
+                    help="generator kernels: the batch's kernel family, or the level-scheduled ones (A/B)")
     a = ap.parse_args()
     import torch
     from cgnn_amd.engine.batch import DeviceTrainer
@@ -55,7 +57,7 @@ def main():
     prog = random_dag_program(a.d, a.edges, a.h, 0, a.conf)
     data = np.random.default_rng(1).normal(size=(a.d, a.n)).astype(np.float32)
     tr = DeviceTrainer([prog] * a.R, [data] * a.R, [model_key(0, r) for r in range(a.R)], a.h, "cuda:0",
-                       use_fast_mmd=a.fast, graph_chunk=0 if a.eager else 50)
+                       use_fast_mmd=a.fast, graph_chunk=0 if a.eager else 50, generator=a.generator)
     tr.run(10, 10)                                   # warm-up: graph capture, first launches
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -69,6 +71,7 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(json.dumps({"bench": "cgnn_batch", "d": a.d, "edges": a.edges, "conf": a.conf, "N": a.n, "R": a.R,
+                      "generator": "staged" if tr.staged else "per-sample",
                       "H": a.h, "us_per_train_step": 1e6 * (t1 - t0) / a.train,
                       "us_per_eval_step": 1e6 * (t2 - t1) / a.test,
                       "model_steps_per_s": a.R * (a.train + a.test) / (t2 - t0)}))
