@@ -1,6 +1,6 @@
 """Host time against GPU time of one rank's GCN epoch at 8-rank size:
-the products graph at scale 1/8 (one rank's share of the rows), ``GCNTrainer`` with
-``collectives=True`` on a 1-rank ``nccl`` group, so every exchange branch of the
+the products graph at scale 1/8 (one rank's share of the rows), reordered as bench.py
+does, ``GCNTrainer`` with ``collectives=True`` on a 1-rank ``nccl`` group, so every exchange branch of the
 multi-rank epoch runs (async all-gather / all-to-all on RCCL's stream, split
 aggregation, backward all-gather overlap, gradient all-reduce), each the identity.
 
@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--scale", type=float, default=0.125)
     ap.add_argument("--epochs", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--forms", default="one_gpu_captured,collectives,collectives_halo",
+                    help="comma-separated subset of the forms to run")
     a = ap.parse_args()
     import torch.distributed as dist
     from cgnn_amd.gnn.data import synthetic
@@ -66,9 +68,12 @@ def main():
     dist.init_process_group("nccl", rank=0, world_size=1)
     dev = torch.device("cuda", 0)
     g = synthetic("ogbn-products", seed=0, device=dev, scale=a.scale)
-    for name, kw in (("one_gpu_captured", {}), ("collectives", dict(collectives=True)),
-                     ("collectives_halo", dict(collectives=True, halo=True))):
-        tr = GCNTrainer(g, hidden=256, rank=0, world=1, **kw)
+    forms = (("one_gpu_captured", {}), ("collectives", dict(collectives=True)),
+             ("collectives_halo", dict(collectives=True, halo=True)))
+    for name, kw in forms:
+        if name not in a.forms.split(","):
+            continue
+        tr = GCNTrainer(g, hidden=256, rank=0, world=1, reorder=True, **kw)     # as bench.py
         res = {"form": name, "scale": a.scale, "rows": g.n, "nnz": g.nnz, "multi": bool(tr.multi),
                "captured": bool(getattr(tr, "_graph", None) is not None and
                                 getattr(getattr(tr, "_graph", None), "graph", None) is not None)}
