@@ -737,9 +737,10 @@ extern "C" int cgnn_staged_plan(int, int, int, int, int, int*);
 // model's kernels -- and its score -- do not depend on its batch-mates.
 // The per-sample kernels walk the whole program in one wave, the level-scheduled ones
 // share a level's nodes over W waves: above GEN_PER_SAMPLE_MAX_D variables the latter
-// win (R = 256, N = 500, H = 20 train step: d = 22 334 vs 411 us, d = 40 735 vs 631,
-// d = 64 1777 vs 845, d = 100 3174 vs 1372; profiles/r05_family).
-constexpr int GEN_PER_SAMPLE_MAX_D = 32;
+// win (R = 256, N = 500, H = 20, train / eval step us: d = 28 538 / 169 vs 545 / 222,
+// d = 30 563 / 172 vs 509 / 204, d = 40 735 vs 631, d = 64 1777 vs 845, d = 100 3174 vs
+// 1372; profiles/r05_family).
+constexpr int GEN_PER_SAMPLE_MAX_D = 28;
 extern "C" int cgnn_gen_bwd_variant(int H, int max_in, int Dt, int prog_stride) {
   const bool per_sample = cgnn_gen_supported_h(H) && cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride) <= 160 * 1024;
   int plan[5];

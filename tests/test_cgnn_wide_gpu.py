@@ -90,9 +90,9 @@ def test_staged_forward_bitwise_equals_per_sample():
     """The level-scheduled forward evaluates every node with the per-sample kernel's
     fmaf order, and the noise kernel draws the same Philox normals: the generated
     samples are bitwise equal."""
-    g = _random_dag(30, seed=3)                 # <= 32 variables: per-sample by default
+    g = _random_dag(28, seed=3)                 # <= 28 variables: per-sample by default
     prog = program_for_dag(g, 20)
-    datas = [_data(30, 300, s) for s in range(3)]
+    datas = [_data(28, 300, s) for s in range(3)]
     keys = [model_key(4, "gb", r) for r in range(3)]
     a = DeviceTrainer([prog] * 3, datas, keys, 20, "cuda:0")
     assert a.bwd_variant == 1 and not a.staged
@@ -108,11 +108,13 @@ def test_staged_forward_bitwise_equals_per_sample():
 def test_staged_training_matches_per_sample():
     """Same model trained by the per-sample and the level-scheduled kernels: only the
     backward's summation orders differ."""
-    g = _random_dag(30, seed=4)
+    g = _random_dag(28, seed=4)                 # <= 28 variables: per-sample by default
     prog = program_for_dag(g, 20)
-    datas = [_data(30, 257, s) for s in range(2)]
+    datas = [_data(28, 257, s) for s in range(2)]
     keys = [model_key(5, "st", r) for r in range(2)]
-    sa = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0").run(12, 4)
+    ta = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0")
+    assert not ta.staged
+    sa = ta.run(12, 4)
     tb = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0", generator="staged")
     assert tb.staged
     np.testing.assert_allclose(tb.run(12, 4), sa, rtol=2e-4, atol=1e-7)
