@@ -267,7 +267,12 @@ __host__ __device__ __forceinline__ int bwd_slab(int max_in) {
          (bwd_ppr(max_in) ? 0 : max_in * WAVE);
 }
 
-template <bool XG, bool DG, bool PPR>
+// CW: hidden units per chunk (the compute width; the LDS rows stay HZ = 16 wide).  12 when
+// it takes as many chunks as 16 (H <= 12, 17..24, 33..36): H = 20 runs 12 + 8 units of
+// work instead of 16 + 16 (bwd_cw).
+__host__ __device__ __forceinline__ int bwd_cw(int H) { return (H + 11) / 12 == (H + 15) / 16 ? 12 : 16; }
+
+template <bool XG, bool DG, bool PPR, int CW>
 __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
     const int* __restrict__ prog, int ps, const int* __restrict__ sched, int ss,
     const float* __restrict__ params, int P, const float* __restrict__ xhat, const float* __restrict__ noise,
@@ -392,16 +397,16 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
       my_in[nin] = 1.f;
       const float gout = valid ? gnx : 0.f;
 
-      for (int q0 = 0; q0 < H; q0 += HZ) {
-        const int hc = min(HZ, H - q0);
+      for (int q0 = 0; q0 < H; q0 += CW) {
+        const int hc = min(CW, H - q0);
         // ---- this chunk's weights into the slab (units q >= hc of a tail chunk zeroed),
         // then the next loads go out ----
         const int nel = (nin + 2) * HZ;
         float wcur[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) wcur[k] = wnx[k];
-        if (q0 + HZ < H) {
-          load_w(cur, q0 + HZ, wnx);
+        if (q0 + CW < H) {
+          load_w(cur, q0 + CW, wnx);
         } else if (i + W < e) {
           const Nd nx = node_at(i + W);
           load_w(nx, 0, wnx);
@@ -431,7 +436,7 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
         // of <= 4 units measured slower: its registers cost the occupancy,
         // profiles/r05_cgnn_bwd) ----
         {
-          constexpr int CW = HZ;
+          static_assert(CW % 4 == 0 && CW <= HZ, "chunk width");
           auto wrow = [&](int row, float* w) {      // CW weights of a row (LDS broadcast)
 #pragma unroll
             for (int c = 0; c < CW / 4; ++c) {
@@ -678,18 +683,22 @@ extern "C" int cgnn_launch_gen_bwd_staged(const int* prog, int ps, const int* sc
   const int T = cgnn_staged_tiles(N);
   const size_t lds = bwd_lds(Dt, wb, max_in, xg, dg, 0);
   dim3 grid((unsigned)(T * R)), block(WAVE * wb);
-#define BWD(XG, DG, PPR)                                                                                          \
+#define BWD(XG, DG, PPR, CW)                                                                                        \
   {                                                                                                               \
-    allow_lds(gen_bwd_staged_kernel<XG, DG, PPR>, lds);                                                           \
-    hipLaunchKernelGGL((gen_bwd_staged_kernel<XG, DG, PPR>), grid, block, lds, st, prog, ps, sched, ss, params, P, \
-                       xhat, noise, NS, gradp, n_chunks, R, N, D, Dt, H, max_in, T, gpart, dxs);                  \
+    allow_lds(gen_bwd_staged_kernel<XG, DG, PPR, CW>, lds);                                                       \
+    hipLaunchKernelGGL((gen_bwd_staged_kernel<XG, DG, PPR, CW>), grid, block, lds, st, prog, ps, sched, ss, params, \
+                       P, xhat, noise, NS, gradp, n_chunks, R, N, D, Dt, H, max_in, T, gpart, dxs);               \
   }
-#define BWD_P(PPR)                     \
-  if (!xg) BWD(false, false, PPR)      \
-  else if (!dg) BWD(true, false, PPR)  \
-  else BWD(true, true, PPR)
-  if (bwd_ppr(max_in)) BWD_P(true)
-  else BWD_P(false)
+#define BWD_P(PPR, CW)                     \
+  if (!xg) BWD(false, false, PPR, CW)      \
+  else if (!dg) BWD(true, false, PPR, CW)  \
+  else BWD(true, true, PPR, CW)
+#define BWD_C(PPR)                  \
+  if (bwd_cw(H) == 12) BWD_P(PPR, 12) \
+  else BWD_P(PPR, 16)
+  if (bwd_ppr(max_in)) BWD_C(true)
+  else BWD_C(false)
+#undef BWD_C
 #undef BWD_P
 #undef BWD
   return (int)hipGetLastError();
