@@ -41,8 +41,6 @@ namespace {
 
 constexpr int WAVE = 64;
 constexpr int HZ = 16;            // hidden units per backward chunk
-constexpr int ZS = HZ + 2;        // per-lane mg row stride (floats, even: f2 pairs)
-constexpr int HZP = HZ / 2;
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
@@ -254,23 +252,23 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
 // --------------------------------------------------------------------------- backward
 // per-wave LDS slab (floats)
 __host__ __device__ __forceinline__ int bwd_si(int max_in) { return (max_in + 2) | 1; }
+// CW: hidden units per backward chunk (the compute width; the weight rows stay HZ = 16
+// wide).  12 when it takes as many chunks as 16 (H <= 12, 17..24, 33..36): H = 20 runs
+// 12 + 8 units of work instead of 16 + 16.
+__host__ __device__ __forceinline__ int bwd_cw(int H) { return (H + 11) / 12 == (H + 15) / 16 ? 12 : 16; }
 // parents whose dL/dparent partials a lane keeps in registers (PPR kernels): nodes of at
 // most PPR_MAX parents, i.e. max_in <= PPR_MAX + 1 (an input is the own noise)
 constexpr int PPR_MAX = 16;
 __host__ __device__ __forceinline__ bool bwd_ppr(int max_in) { return max_in <= PPR_MAX + 1; }
-__host__ __device__ __forceinline__ int bwd_slab(int max_in) {
-  // [64][SI] (padded even) + [64][ZS] + Gm rows + weight rows (+ dL/dparent partials,
+__host__ __device__ __forceinline__ int bwd_slab(int max_in, int cw) {
+  // [64][SI] (padded even) + [64][cw + 2] mg rows + weight rows (+ dL/dparent partials,
   // unless they live in registers: d = 200 with 400 edges (max_in 11) 12.6 -> 9.8 KB per
   // wave, 3 -> 4 four-wave blocks per CU; with 736 edges (max_in 17) 16.4 -> 12.1 KB,
-  // 2 -> 3 blocks)
-  return WAVE * (bwd_si(max_in) + 1) + WAVE * ZS + (max_in + 1) * HZ + (max_in + 2) * HZ +
-         (bwd_ppr(max_in) ? 0 : max_in * WAVE);
+  // 2 -> 3 blocks; without the Gm rows (dW2 from the MFMA registers) and with 14-float mg
+  // rows at cw = 12: 9.7 KB, 4 blocks)
+  return WAVE * (bwd_si(max_in) + 1) + WAVE * (cw + 2) + (max_in + 2) * HZ + (bwd_ppr(max_in) ? 0 : max_in * WAVE);
 }
 
-// CW: hidden units per chunk (the compute width; the LDS rows stay HZ = 16 wide).  12 when
-// it takes as many chunks as 16 (H <= 12, 17..24, 33..36): H = 20 runs 12 + 8 units of
-// work instead of 16 + 16 (bwd_cw).
-__host__ __device__ __forceinline__ int bwd_cw(int H) { return (H + 11) / 12 == (H + 15) / 16 ? 12 : 16; }
 
 template <bool XG, bool DG, bool PPR, int CW>
 __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
@@ -296,15 +294,15 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
   const int SI = bwd_si(max_in);
   float* s_x = smem;
   float* s_dx = s_x + (XG ? 0 : (size_t)Dt * WAVE);
-  float* slab = s_dx + (DG ? 0 : (size_t)Dt * WAVE) + (size_t)wave * bwd_slab(max_in);
+  constexpr int ZC = CW + 2;                                 // mg row stride (even: f2 pairs)
+  float* slab = s_dx + (DG ? 0 : (size_t)Dt * WAVE) + (size_t)wave * bwd_slab(max_in, CW);
   float* s_in = slab;                                        // [64][SI]
-  float* s_z = slab + WAVE * (SI + 1);                       // [64][ZS]
-  f2* s_g = reinterpret_cast<f2*>(s_z + WAVE * ZS);          // Gm: [(max_in + 1)][HZ] floats
-  float* s_w = s_z + WAVE * ZS + (max_in + 1) * HZ;          // [max_in + 2][16] weight rows
+  float* s_z = slab + WAVE * (SI + 1);                       // [64][ZC]
+  float* s_w = s_z + WAVE * ZC;                              // [max_in + 2][16] weight rows
   float* s_pp = s_w + (max_in + 2) * HZ;                     // [max_in][64] dL/dparent (!PPR)
   float pp[PPR ? PPR_MAX : 1];                                // dL/dparent (PPR)
   float* my_in = s_in + lane * SI;
-  float* my_z = s_z + lane * ZS;
+  float* my_z = s_z + lane * ZC;
 
   auto xget = [&](int v) -> float { return XG ? xr[(size_t)v * N + nc] : s_x[v * WAVE + lane]; };
 
@@ -478,23 +476,23 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
             }
           }
 #pragma unroll
-          for (int qp = 0; qp < HZP; ++qp)
-            *reinterpret_cast<f2*>(my_z + 2 * qp) =
-                2 * qp < CW ? f2{mg[min(2 * qp, CW - 1)], mg[min(2 * qp + 1, CW - 1)]} : f2{0.f, 0.f};
+          for (int qp = 0; qp < CW / 2; ++qp) *reinterpret_cast<f2*>(my_z + 2 * qp) = f2{mg[2 * qp], mg[2 * qp + 1]};
         }
         wave_sync();
 
         // ---- Gm[j][q] = sum_s in[s][j] mg[s][q] over the 64 samples on the matrix cores
         // (v_mfma_f32_16x16x4_f32: fp32 products, fp32 accumulation): A = in^T (16 input
         // rows x 4 samples, from the input slab), B = mg (4 samples x 16 units, from the
-        // mg slab), 16 k-steps for the tile's 64 samples; D = 16 input rows x 16 units
-        // (lane 16 g + c: rows 4 g .. 4 g + 3, unit c).  Replaces a per-lane item loop of
-        // 64 LDS reads and 64 VALU per chunk with 32 LDS reads and 16 MFMAs. ----
+        // mg slab; columns >= CW read the next row and are discarded), 16 k-steps for the
+        // tile's 64 samples; D = 16 input rows x 16 units (lane 16 g + c: rows 4 g .. 4 g + 3,
+        // unit c).  dW1 / db1 = w2 Gm straight from the accumulators, and dW2[q] =
+        // sum_j W1ext[j][q] Gm[j][q] as per-lane partials over the lane's rows, summed over
+        // the four row groups by two cross-lane adds (no Gm rows in LDS). ----
         {
           typedef float f32x4 __attribute__((ext_vector_type(4)));
-          float* s_gf = reinterpret_cast<float*>(s_g);              // [max_in + 1][HZ]
           const int jq = lane & 15, sg = lane >> 4;
           const float w2q = s_w[(nin + 1) * HZ + jq];
+          float d2 = 0.f;
           for (int j0 = 0; j0 <= nin; j0 += 16) {
             const int jr = min(j0 + jq, nin);
             const float am = j0 + jq <= nin ? 1.f : 0.f;
@@ -503,26 +501,21 @@ __global__ __launch_bounds__(512) void gen_bwd_staged_kernel(
             for (int t = 0; t < WAVE / 4; ++t) {
               const int smp = 4 * t + sg;
               const float a = s_in[smp * SI + jr] * am;
-              const float b = s_z[smp * ZS + jq];
+              const float b = s_z[smp * ZC + jq];
               acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int j = j0 + 4 * sg + i;
-              if (j <= nin && jq < hc) {
-                s_gf[j * HZ + jq] = acc[i];
-                gp[poff + j * H + q0 + jq] = w2q * acc[i];                // dW1 / db1
+              if (j <= nin) {
+                d2 = fmaf(s_w[j * HZ + jq], acc[i], d2);
+                if (jq < hc) gp[poff + j * H + q0 + jq] = w2q * acc[i];   // dW1 / db1
               }
             }
           }
-        }
-        wave_sync();
-        // dW2[q] = sum_j W1ext[j][q] Gm[j][q]
-        if (lane < hc) {
-          const float* s_gf = reinterpret_cast<const float*>(s_g);
-          float s = 0.f;
-          for (int j = 0; j <= nin; ++j) s = fmaf(s_w[j * HZ + lane], s_gf[j * HZ + lane], s);
-          gp[poff + (nin + 1) * H + q0 + lane] = s;
+          d2 += __shfl_xor(d2, 16, 64);
+          d2 += __shfl_xor(d2, 32, 64);
+          if (lane < hc) gp[poff + (nin + 1) * H + q0 + lane] = d2;       // dW2
         }
         wave_sync();
       }
@@ -581,9 +574,9 @@ size_t fwd_lds(int Dt, int W, bool xg, int max_in, int hc, int extra) {
   const size_t hcs = (size_t)((hc + 3) & ~3);
   return sizeof(float) * ((size_t)extra + (xg ? 0 : (size_t)Dt * WAVE) + (size_t)W * (max_in + 2) * hcs);
 }
-size_t bwd_lds(int Dt, int W, int max_in, bool xg, bool dg, int extra) {
+size_t bwd_lds(int Dt, int W, int H, int max_in, bool xg, bool dg, int extra) {
   return sizeof(float) * ((size_t)extra + (xg ? 0 : (size_t)Dt * WAVE) + (dg ? 0 : (size_t)Dt * WAVE) +
-                          (size_t)W * bwd_slab(max_in));
+                          (size_t)W * bwd_slab(max_in, bwd_cw(H)));
 }
 
 
@@ -607,7 +600,7 @@ extern "C" int cgnn_staged_plan(int Dt, int H, int max_in, int W, int extra, int
   int best = -1, best_waves = 0, wb = std::min(W, 4);
   for (; wb >= 1 && best < 0; wb /= 2) {
     for (int place = 0; place < 3; ++place) {
-      const size_t lds = bwd_lds(Dt, wb, max_in, place >= 1, place == 2, extra);
+      const size_t lds = bwd_lds(Dt, wb, H, max_in, place >= 1, place == 2, extra);
       if (lds > LDS_MAX) continue;
       const int waves = std::min(cap, (int)(LDS_MAX / lds) * wb);
       if (waves > best_waves) { best = place; best_waves = waves; }
@@ -677,11 +670,11 @@ extern "C" int cgnn_launch_gen_bwd_staged(const int* prog, int ps, const int* sc
     xg = force >= 1;
     dg = force == 2;
     wb = W;
-    if (bwd_lds(Dt, wb, max_in, xg, dg, 0) > LDS_MAX) return -2;
+    if (bwd_lds(Dt, wb, H, max_in, xg, dg, 0) > LDS_MAX) return -2;
   }
   if (dg && !dxs) return -2;
   const int T = cgnn_staged_tiles(N);
-  const size_t lds = bwd_lds(Dt, wb, max_in, xg, dg, 0);
+  const size_t lds = bwd_lds(Dt, wb, H, max_in, xg, dg, 0);
   dim3 grid((unsigned)(T * R)), block(WAVE * wb);
 #define BWD(XG, DG, PPR, CW)                                                                                        \
   {                                                                                                               \
