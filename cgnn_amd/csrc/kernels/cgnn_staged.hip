@@ -592,12 +592,14 @@ extern "C" int cgnn_staged_plan(int Dt, int H, int max_in, int W, int extra, int
   const int fxg = fwd_lds(Dt, W, false, max_in, fwd_hc(H), extra) <= LDS_MAX ? 0 : 1;
   // backward: latency-bound per node, so the placement that keeps the most waves per CU
   // resident wins (d = 200, H = 20: sample state in LDS at 4 waves / CU 3.76 ms, in
-  // global memory at 16 waves / CU 1.59 ms; profiles/r04_cgnn_wide), at most 4 waves
-  // per block (wider blocks idle on the narrow sub-stages); ties keep the LDS state
+  // global memory at 16 waves / CU 1.59 ms; profiles/r04_cgnn_wide), at most 2 waves
+  // per block (wider blocks idle on the narrow sub-stages: d = 200, H = 20 backward with
+  // 1 / 2 / 4 / 8 waves per block 1421 / 995 / 1068 / 1282 us at 400 edges, 1598 / 1181 /
+  // 1447 / 2121 us at 736; profiles/r05_cgnn_bwd/wsweep); ties keep the LDS state.
   // Nodes with many inputs (a slab per wave grows with max_in) take narrower blocks
-  // before giving up: 4, 2, then 1 wave per block.
-  const int cap = 16;                    // ~120 VGPRs: 4 waves per SIMD
-  int best = -1, best_waves = 0, wb = std::min(W, 4);
+  // before giving up: 2, then 1 wave per block.
+  const int cap = 16;                    // ~110 VGPRs: 4 waves per SIMD
+  int best = -1, best_waves = 0, wb = std::min(W, 2);
   for (; wb >= 1 && best < 0; wb /= 2) {
     for (int place = 0; place < 3; ++place) {
       const size_t lds = bwd_lds(Dt, wb, H, max_in, place >= 1, place == 2, extra);
