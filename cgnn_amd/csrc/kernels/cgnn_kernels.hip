@@ -737,10 +737,11 @@ extern "C" int cgnn_staged_plan(int, int, int, int, int, int*);
 // model's kernels -- and its score -- do not depend on its batch-mates.
 // The per-sample kernels walk the whole program in one wave, the level-scheduled ones
 // share a level's nodes over W waves: above GEN_PER_SAMPLE_MAX_D variables the latter
-// win (R = 256, N = 500, H = 20, train / eval step us: d = 28 538 / 169 vs 545 / 222,
-// d = 30 563 / 172 vs 509 / 204, d = 40 735 vs 631, d = 64 1777 vs 845, d = 100 3174 vs
-// 1372; profiles/r05_family).
-constexpr int GEN_PER_SAMPLE_MAX_D = 28;
+// win.  R = 256, N = 500, H = 20, train step us, per-sample vs level-scheduled, after the
+// round-5 backward changes: d = 22 326 vs 348, d = 24 375 vs 395, d = 26 520 vs 425,
+// d = 28 496 vs 377 (profiles/r05_family/after_bwd; before them the crossover was
+// between 28 and 30).
+constexpr int GEN_PER_SAMPLE_MAX_D = 24;
 extern "C" int cgnn_gen_bwd_variant(int H, int max_in, int Dt, int prog_stride) {
   const bool per_sample = cgnn_gen_supported_h(H) && cgnn_gen_bwd_lds(H, max_in, Dt, prog_stride) <= 160 * 1024;
   int plan[5];

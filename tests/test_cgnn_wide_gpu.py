@@ -90,9 +90,9 @@ def test_staged_forward_bitwise_equals_per_sample():
     """The level-scheduled forward evaluates every node with the per-sample kernel's
     fmaf order, and the noise kernel draws the same Philox normals: the generated
     samples are bitwise equal."""
-    g = _random_dag(28, seed=3)                 # <= 28 variables: per-sample by default
+    g = _random_dag(24, seed=3)                 # <= 24 variables: per-sample by default
     prog = program_for_dag(g, 20)
-    datas = [_data(28, 300, s) for s in range(3)]
+    datas = [_data(24, 300, s) for s in range(3)]
     keys = [model_key(4, "gb", r) for r in range(3)]
     a = DeviceTrainer([prog] * 3, datas, keys, 20, "cuda:0")
     assert a.bwd_variant == 1 and not a.staged
@@ -108,9 +108,9 @@ def test_staged_forward_bitwise_equals_per_sample():
 def test_staged_training_matches_per_sample():
     """Same model trained by the per-sample and the level-scheduled kernels: only the
     backward's summation orders differ."""
-    g = _random_dag(28, seed=4)                 # <= 28 variables: per-sample by default
+    g = _random_dag(24, seed=4)                 # <= 24 variables: per-sample by default
     prog = program_for_dag(g, 20)
-    datas = [_data(28, 257, s) for s in range(2)]
+    datas = [_data(24, 257, s) for s in range(2)]
     keys = [model_key(5, "st", r) for r in range(2)]
     ta = DeviceTrainer([prog] * 2, datas, keys, 20, "cuda:0")
     assert not ta.staged

@@ -296,14 +296,14 @@ def _dag_with_max_in(d, k, seed):
 def test_device_batches_keep_each_program_on_its_own_kernel_family():
     """the generator kernels (per-sample or level-scheduled) are chosen per
     program, never from batch-wide maxima, so a candidate's score cannot depend on its
-    batch-mates.  The family follows the variable count (per-sample up to 28 variables,
+    batch-mates.  The family follows the variable count (per-sample up to 24 variables,
     level-scheduled above, profiles/r05_family), whatever a program's widest node: at
-    d = 28 and d = 140, programs with 3 and 19 inputs on one node share their width's
+    d = 24 and d = 140, programs with 3 and 19 inputs on one node share their width's
     family, every batch keeps one family, and its combined shape keeps it."""
     from cgnn_amd.engine.batch import kernel_family
     from cgnn_amd.engine.scorer import Job, _group_batches
     H, N = 20, 50
-    for d, fam in ((28, 1), (140, 2)):
+    for d, fam in ((24, 1), (140, 2)):
         progs = [program_for_dag(_dag_with_max_in(d, k, s), H) for s, k in enumerate([3, 19, 3, 19, 3, 3, 19])]
         fams = [kernel_family(d, H, p.max_in, len(p.prog)) for p in progs]
         assert set(fams) == {fam}, (d, fams)
