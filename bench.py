@@ -59,8 +59,6 @@ def main():
                          "or auto (features aligned, layer-2 rows packed: the same as mixed)")
     ap.add_argument("--no-fused", action="store_true", help="hipBLASLt GEMMs + separate epilogues")
     ap.add_argument("--capture", action="store_true", help="replay the epoch from a hipGraph (one GPU)")
-    ap.add_argument("--no-fuse-agg", action="store_true",
-                    help="layer-1 aggregation and dense forward as two kernels (A/B; default on one GPU: one)")
     ap.add_argument("--id-order", choices=["shuffled", "banded"], default="shuffled",
                     help="synthetic node ids: shuffled (no locality in the ids, like a real dataset) or "
                          "the generator's banded ids (locality for free; A/B only)")
@@ -141,8 +139,7 @@ def main():
                     fused=not a.no_fused,
                     align_rows={'auto': None, 'aligned': True, 'packed': False, 'mixed': None}[a.rows],
                     align_c=False if a.rows == "mixed" else None,
-                    capture=a.capture, reorder=a.reorder != "none",
-                    fuse_agg=False if a.no_fuse_agg else None)
+                    capture=a.capture, reorder=a.reorder != "none")
     n_nodes, nnz = g.n, g.nnz
     del g
     sync()

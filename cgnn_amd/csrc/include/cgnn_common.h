@@ -170,12 +170,7 @@ __host__ __device__ __forceinline__ unsigned xcd_remap_chunked(unsigned b, unsig
 // deals blocks round-robin over XCDs).  Returns a logical block id such that the
 // blocks resident on one XCD process a CONTIGUOUS range of the work.  Bijective
 // for any grid size (q = n/8, r = n%8).  Speed only -- never correctness.
-#ifndef CGNN_XCD_CHUNK
-#define CGNN_XCD_CHUNK 0
-#endif
 __host__ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned nwg) {
-  // (A/B builds: -DCGNN_XCD_CHUNK=C turns every contiguous remap into the chunked one)
-  if constexpr (CGNN_XCD_CHUNK > 0) return xcd_remap_chunked<CGNN_XCD_CHUNK>(b, nwg);
   const unsigned q = nwg >> 3, r = nwg & 7u;
   const unsigned xcd = b & 7u, idx = b >> 3;
   const unsigned base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
@@ -258,5 +253,17 @@ __device__ __forceinline__ uint32_t pk_nz(uint32_t x) {
 // moves to bit 2i + 16, so (spread >> 2i) & 0x10001 is the keep pair of values 2i, 2i + 1
 __device__ __forceinline__ uint32_t keep_spread(uint32_t m) { return (m & 0x5555u) | ((m & 0xaaaau) << 15); }
 
+
+// CUs of the current device (cached per device; 256 on MI355X) for persistent grids
+inline int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    hipDeviceProp_t prop;
+    cached[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
+  }
+  return cached[dev];
+}
 
 }  // namespace cgnn

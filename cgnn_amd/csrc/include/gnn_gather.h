@@ -1,8 +1,7 @@
 // Row-gather primitives of the CSR aggregation kernels (gnn_sparse.hip: spmm,
-// spmm_ce, ...; gnn_aggfwd.hip: the layer-1 aggregation fused with the GCN dense
-// forward).  One header so that every kernel summing gathered rows uses the same
-// instructions in the same order: a fused kernel's aggregate is bit-identical to the
-// standalone spmm's.
+// spmm_ce, spmm_ell, ...).  One header so that every kernel summing gathered rows uses
+// the same instructions in the same order: a fused kernel's aggregate is bit-identical
+// to the standalone spmm's.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

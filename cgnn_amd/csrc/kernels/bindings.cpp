@@ -73,7 +73,8 @@ int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, flo
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
 int gnn_spmm_ce_blocks(int, int);
 int gnn_launch_ell_build(const int*, const int*, int*, int, hipStream_t);
-int gnn_launch_spmm_ell(const int*, const int*, const void*, void*, const float*, int, int, int, int, hipStream_t);
+int gnn_launch_spmm_ell(const int*, const int*, const void*, void*, const float*, int, int, int, int, long,
+                        const int*, int, hipStream_t);
 int gnn_slab_sum(const float*, long, int, float*, int, float*, const int*, hipStream_t);
 int gnn_launch_sample_neighbors(const int*, const int*, const int*, int, int, const int*, int*, uint32_t, uint32_t,
                                 uint32_t, hipStream_t);
@@ -85,10 +86,6 @@ int gnn_launch_dense_fwd(const void*, const float*, const float*, const float*, 
                          const int*, void*, hipStream_t);
 long gnn_keep_image_halfwords(int, int);
 int gnn_launch_keep_image(void*, int, int, float, uint32_t, uint32_t, uint32_t, uint32_t, const int*, hipStream_t);
-int gnn_agg_fwd_queue_words();
-int gnn_launch_agg_fwd(const int*, const int*, const void*, void*, const float*, const float*, const float*,
-                       const float*, void*, int, int, int, int, int, int, float, uint32_t, uint32_t, uint32_t,
-                       uint32_t, const int*, void*, int*, hipStream_t);
 int gnn_launch_gat_fwd(const int*, const int*, const void*, const float*, const float*, const int*, float*, float*,
                        void*, int, int, int, int, const float*, void*, int, float, uint32_t, uint32_t, uint32_t,
                        const int*, uint32_t, hipStream_t);
@@ -321,9 +318,10 @@ PYBIND11_MODULE(_hip, m) {
     chk(gnn_launch_ell_build(Pt<const int>(rowptr), Pt<const int>(col), Pt<int>(ell), n_rows, S(st)), "gnn_ell_build");
   });
   m.def("gnn_spmm_ell", [](uint64_t ell, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, int n_rows, int F,
-                           int ldx, int ldy, uint64_t st) {
+                           int ldx, int ldy, long n_x_rows, uint64_t long_rows, int n_long, uint64_t st) {
     chk(gnn_launch_spmm_ell(Pt<const int>(ell), Pt<const int>(col), Pt<const void>(x), Pt<void>(y),
-                            Pt<const float>(rscale), n_rows, F, ldx, ldy, S(st)), "gnn_spmm_ell");
+                            Pt<const float>(rscale), n_rows, F, ldx, ldy, n_x_rows, Pt<const int>(long_rows),
+                            n_long, S(st)), "gnn_spmm_ell");
   });
   m.def("gnn_slab_sum", [](uint64_t P, long rows, int W, uint64_t stage, int G, uint64_t out, uint64_t map,
                            uint64_t st) {
@@ -354,19 +352,6 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("n"), py::arg("F"), py::arg("ldx"), py::arg("HD"), py::arg("C"), py::arg("ldc"), py::arg("p"),
      py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"), py::arg("step_ptr") = 0,
      py::arg("kimg") = 0);
-  m.def("gnn_agg_fwd_queue_words", &gnn_agg_fwd_queue_words);
-  m.def("gnn_agg_fwd", [](uint64_t rowptr, uint64_t col, uint64_t xs, uint64_t ax, uint64_t w1, uint64_t b1,
-                          uint64_t w2, uint64_t dinv, uint64_t z2, int n, int F, int ldx, int HD, int C, int ldc,
-                          float p, uint32_t k0, uint32_t k1, uint32_t step, uint32_t row0, uint64_t st,
-                          uint64_t stepp, uint64_t kimg, uint64_t ctr) {
-    return gnn_launch_agg_fwd(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(xs), Pt<void>(ax),
-                              Pt<const float>(w1), Pt<const float>(b1), Pt<const float>(w2), Pt<const float>(dinv),
-                              Pt<void>(z2), n, F, ldx, HD, C, ldc, p, k0, k1, step, row0, Pt<const int>(stepp),
-                              Pt<void>(kimg), Pt<int>(ctr), S(st));
-  }, py::arg("rowptr"), py::arg("col"), py::arg("xs"), py::arg("ax"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
-     py::arg("dinv"), py::arg("z2"), py::arg("n"), py::arg("F"), py::arg("ldx"), py::arg("HD"), py::arg("C"),
-     py::arg("ldc"), py::arg("p"), py::arg("k0"), py::arg("k1"), py::arg("step"), py::arg("row0"), py::arg("st"),
-     py::arg("step_ptr") = 0, py::arg("kimg") = 0, py::arg("ctr") = 0);
   m.def("gnn_keep_image_halfwords", &gnn_keep_image_halfwords);
   m.def("gnn_keep_image", [](uint64_t kimg, int n, int HD, float p, uint32_t k0, uint32_t k1, uint32_t step,
                              uint32_t row0, uint64_t st, uint64_t stepp) {

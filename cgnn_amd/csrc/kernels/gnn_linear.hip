@@ -240,17 +240,6 @@ __device__ __forceinline__ void copy_image(uint4* __restrict__ dst, const uint4*
   for (; i < n16; i += bd) dst[i] = src[i];
 }
 
-int device_cus() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev >= 64) return 256;
-  if (!cached[dev]) {
-    hipDeviceProp_t prop;
-    cached[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
-  }
-  return cached[dev];
-}
-
 }  // namespace
 
 // ============================================================================

@@ -30,73 +30,6 @@ namespace {
 
 struct bf16x8 { uint32_t w[4]; };
 
-// Sum the bf16 rows X[col[e]] for e in [e0, e1) minus the gap [g0, g1) (the edges served
-// from LDS by the windowed kernel) into acc; 8 raw rows in flight per lane.
-template <int L>
-__device__ __forceinline__ void gather_sum_gap(const int* __restrict__ col, const uint16_t* __restrict__ X,
-                                               int e0, int e1, int g0, int g1, int ldx, int f0, bool fv,
-                                               int sub_base, int sl, float* acc) {
-  const int gap = g1 - g0;
-  const int v1 = e1 - gap;                       // virtual edge range [e0, v1)
-  for (int e = e0; e < v1; e += L) {
-    const int ve = e + sl;
-    const int myj = (ve < v1) ? col[ve + (ve >= g0 ? gap : 0)] : 0;
-    const int cnt = min(L, v1 - e);
-    int k = 0;
-    for (; k + 8 <= cnt; k += 8) {
-      int j[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) j[u] = __shfl(myj, sub_base + k + u, 64);
-      if (fv) {
-        uint4 r[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) r[u] = load_raw16(X, (size_t)j[u] * ldx + f0);
-#pragma unroll
-        for (int u = 0; u < 8; u += 2) acc_bf16_pair(acc, r[u], r[u + 1]);
-      }
-    }
-    for (; k + 2 <= cnt; k += 2) {
-      const int j0 = __shfl(myj, sub_base + k, 64), j1 = __shfl(myj, sub_base + k + 1, 64);
-      if (fv) acc_bf16_pair(acc, load_raw16(X, (size_t)j0 * ldx + f0), load_raw16(X, (size_t)j1 * ldx + f0));
-    }
-    if (k < cnt) {
-      const int j0 = __shfl(myj, sub_base + k, 64);
-      if (fv) acc_bf16_pair(acc, load_raw16(X, (size_t)j0 * ldx + f0), make_uint4(0, 0, 0, 0));
-    }
-  }
-}
-
-// Sum the window rows s_win[col[e] - w0] (LDS, pitch LP 16-B chunks) for e in [a, b)
-template <int L, int LP>
-__device__ __forceinline__ void gather_sum_lds(const int* __restrict__ col, const uint4* s_win, int a, int b,
-                                               int w0, int sl, bool fv, int sub_base, float* acc) {
-  for (int e = a; e < b; e += L) {
-    const int myj = (e + sl < b) ? (col[e + sl] - w0) * LP : 0;
-    const int cnt = min(L, b - e);
-    int k = 0;
-    for (; k + 8 <= cnt; k += 8) {
-      int j[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) j[u] = __shfl(myj, sub_base + k + u, 64);
-      if (fv) {
-        uint4 r[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) r[u] = s_win[j[u] + sl];
-#pragma unroll
-        for (int u = 0; u < 8; u += 2) acc_bf16_pair(acc, r[u], r[u + 1]);
-      }
-    }
-    for (; k + 2 <= cnt; k += 2) {
-      const int j0 = __shfl(myj, sub_base + k, 64), j1 = __shfl(myj, sub_base + k + 1, 64);
-      if (fv) acc_bf16_pair(acc, s_win[j0 + sl], s_win[j1 + sl]);
-    }
-    if (k < cnt) {
-      const int j0 = __shfl(myj, sub_base + k, 64);
-      if (fv) acc_bf16_pair(acc, s_win[j0 + sl], make_uint4(0, 0, 0, 0));
-    }
-  }
-}
-
 }  // namespace
 
 
@@ -336,6 +269,105 @@ __global__ __launch_bounds__(256, 8) void spmm_ell_kernel(const int* __restrict_
     for (int u = 0; u < 8; u += 2) acc_bf16_pair(acc, r[u], r[u + 1]);
   }
   if (!rv || f0 >= ldy) return;
+  const float rs = rscale ? rscale[row] : 1.f;
+  float y[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) y[q] = f0 + q < F ? acc[q] * rs : 0.f;
+  *reinterpret_cast<uint4*>(Y + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
+}
+
+// The same aggregate as a persistent grid (8 waves per SIMD on every CU) in which each
+// wave loops over groups of 8 rows and loads the NEXT group's ELL indices right after
+// issuing the current group's gathers: the index round trip of group k + 1 runs under
+// the gathers of group k, so a group costs one exposed round trip instead of two (the
+// one-shot form above is latency-bound: 217 us on the headline shape against a ~60 us
+// traffic floor).  Loads and stores are counted in issue order (vmcnt), so the prefetch
+// is issued AFTER the gathers (the scheduling barriers pin that order), and every
+// gather and the row store go through buffer descriptors with out-of-range offsets for
+// inactive lanes (the hardware returns 0 / drops the store): no branches, so the waits
+// are exact counts that leave the prefetch in flight.  Rows of more than 8 entries are
+// skipped here (their store is dropped) and summed by spmm_ell_long_kernel from the
+// image's list of long rows: a data-dependent inner loop in this one would make every
+// wait of the loop a full drain.  Same adds in the same order as spmm_ell_kernel:
+// bit-identical output.  Tables below 2^31 bytes (the launcher checks).
+__global__ __launch_bounds__(256, 8) void spmm_ell_pipe_kernel(const int* __restrict__ ell,
+                                                            const uint16_t* __restrict__ X,
+                                                            uint16_t* __restrict__ Y,
+                                                            const float* __restrict__ rscale, int n_rows, int F,
+                                                            int ldx, int ldy, uint32_t x_bytes) {
+  constexpr int L = 8, RPW = 8;
+  constexpr uint32_t OOB = 0x80000000u;
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  const int n_groups = (n_rows + RPW - 1) / RPW;
+  const int f0 = sl * 8;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(X), (short)0,
+                                                                      (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(Y, (short)0,
+                                                                      (int)((uint32_t)n_rows * (uint32_t)ldy * 2u),
+                                                                      0x00020000);
+  // a valid address for the row-scale load when there is no rscale (the value is unused)
+  const float* rsb = rscale ? rscale : reinterpret_cast<const float*>(ell);
+  int g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (g >= n_groups) return;                 // uniform per wave
+  // clamped, unconditional loads (a "load or -1" branches and waits at the join)
+  int nj = ell[(size_t)min(g * RPW + sub, n_rows - 1) * 8 + sl];
+  // a dropped store behind the first index load: the loop is entered with the same
+  // count of younger operations as its back edge (the previous row store), so the loop
+  // head's wait for the indices is one vmcnt(1) that never waits for a row store
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_raw_buffer_store_b32(0u, yr, OOB, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  do {
+    const int row = g * RPW + sub;
+    const bool rv = row < n_rows;
+    const int myj = nj;
+    const int j0 = __shfl(myj, sub * L, 64);
+    const bool ok = rv && j0 != -2;          // a short row of this wave's group
+    const bool fv = ok && f0 < F;
+    uint4 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = __shfl(myj, sub * L + u, 64);
+      const uint32_t off = (fv && j >= 0) ? ((uint32_t)j * (uint32_t)ldx + (uint32_t)f0) * 2u : OOB;
+      r[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+    // the row scale is independent of the indices: loaded beside the gathers
+    const float rsv = rsb[rscale ? min(row, n_rows - 1) : 0];
+    __builtin_amdgcn_sched_barrier(0);
+    nj = ell[(size_t)min((g + nw) * RPW + sub, n_rows - 1) * 8 + sl];
+    __builtin_amdgcn_sched_barrier(0);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) acc_bf16_pair(acc, r[u], r[u + 1]);
+    const float rs = rscale ? rsv : 1.f;
+    float y[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) y[q] = f0 + q < F ? acc[q] * rs : 0.f;
+    const uint32_t yo = (ok && f0 < ldy) ? ((uint32_t)row * (uint32_t)ldy + (uint32_t)f0) * 2u : OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, f32x8_to_bf16(y)), yr, yo, 0, 0);
+    g += nw;
+  } while (g < n_groups);
+}
+
+// The long rows (more than 8 entries) of an ELL image, listed in `rows`: one 8-lane
+// sub-group per row over its CSR range, exactly spmm_ell_kernel's long-row path.
+__global__ __launch_bounds__(256) void spmm_ell_long_kernel(const int* __restrict__ rows, int n_long,
+                                                          const int* __restrict__ ell, const int* __restrict__ col,
+                                                          const uint16_t* __restrict__ X, uint16_t* __restrict__ Y,
+                                                          const float* __restrict__ rscale, int F, int ldx,
+                                                          int ldy) {
+  constexpr int L = 8;
+  const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
+  const int k = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + sub;
+  if (k >= n_long) return;                   // uniform per sub-group
+  const int row = rows[k];
+  const int f0 = sl * 8;
+  const int e0 = ell[(size_t)row * 8 + 1], e1 = ell[(size_t)row * 8 + 2];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  gather_sum<L, 1, 8>(col, X, e0, e1, ldx, f0, f0 < F, sub * L, sl, acc);
+  if (f0 >= ldy) return;
   const float rs = rscale ? rscale[row] : 1.f;
   float y[8];
 #pragma unroll
@@ -747,11 +779,23 @@ extern "C" int gnn_launch_ell_build(const int* rowptr, const int* col, int* ell,
 }
 
 extern "C" int gnn_launch_spmm_ell(const int* ell, const int* col, const void* X, void* Y, const float* rscale,
-                                   int n_rows, int F, int ldx, int ldy, hipStream_t st) {
+                                   int n_rows, int F, int ldx, int ldy, long n_x_rows, const int* long_rows,
+                                   int n_long, hipStream_t st) {
   if (F > 64 || ldx % 8 || ldy % 8 || F > ldx) return -3;
   if (n_rows <= 0) return 0;
-  hipLaunchKernelGGL(spmm_ell_kernel, dim3((n_rows + 31) / 32), dim3(256), 0, st, ell, col, (const uint16_t*)X,
-                     (uint16_t*)Y, rscale, n_rows, F, ldx, ldy);
+  static const int form = getenv("CGNN_ELL_FORM") ? atoi(getenv("CGNN_ELL_FORM")) : 1;   // A/B (temporary)
+  if (form == 1 && long_rows && n_x_rows * ldx * 2 < (1l << 31) && (long)n_rows * ldy * 2 < (1l << 31)) {
+    const int groups = (n_rows + 7) / 8;
+    const int blocks = std::max(1, std::min((groups + 3) / 4, device_cus() * 8));
+    hipLaunchKernelGGL(spmm_ell_pipe_kernel, dim3(blocks), dim3(256), 0, st, ell, (const uint16_t*)X,
+                       (uint16_t*)Y, rscale, n_rows, F, ldx, ldy, (uint32_t)(n_x_rows * ldx * 2));
+    if (n_long > 0)
+      hipLaunchKernelGGL(spmm_ell_long_kernel, dim3((n_long + 31) / 32), dim3(256), 0, st, long_rows, n_long, ell,
+                         col, (const uint16_t*)X, (uint16_t*)Y, rscale, F, ldx, ldy);
+  } else {
+    hipLaunchKernelGGL(spmm_ell_kernel, dim3((n_rows + 31) / 32), dim3(256), 0, st, ell, col, (const uint16_t*)X,
+                       (uint16_t*)Y, rscale, n_rows, F, ldx, ldy);
+  }
   return (int)hipGetLastError();
 }
 

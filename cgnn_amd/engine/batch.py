@@ -262,10 +262,25 @@ class DeviceTrainer:
         with torch.cuda.device(self.device):
             self.engine.run(0, int(epochs), self.graph_chunk, self.hist_len > 0)
 
-    def evaluate(self, epochs: int):
+    def evaluate(self, epochs: int, log_every: int = 0, log=None):
+        """Enqueue ``epochs`` evaluation steps (the score accumulates in ``loss_acc``).
+        ``log_every`` > 0: ``log(it, losses[R])`` with the loss of every step
+        ``it % log_every == 0`` (the reference's verbose evaluate, CGNN.py:147-149); the
+        steps run in the same order with the same draws, in chunks that end at those
+        steps (one host read of ``loss_last`` each)."""
+        epochs = int(epochs)
         with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
             self.loss_acc.zero_()
-            self.engine.run(1, int(epochs), self.graph_chunk, False)
+            if log_every <= 0 or log is None:
+                self.engine.run(1, epochs, self.graph_chunk, False)
+                return
+            it = 0
+            while it < epochs:
+                self.engine.run(1, 1, 0, False)
+                log(it, self.loss_last.cpu().numpy())
+                k = min(int(log_every) - 1, epochs - it - 1)
+                self.engine.run(1, k, self.graph_chunk, False)
+                it += 1 + k
 
     def _join(self):
         torch.cuda.current_stream(self.device).wait_stream(self.stream)

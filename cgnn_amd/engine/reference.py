@@ -156,13 +156,16 @@ class ReferenceTrainer:
             self.rng_step += 1
             self.opt_step += 1
 
-    def evaluate(self, epochs: int) -> np.ndarray:
+    def evaluate(self, epochs: int, log_every: int = 0, log=None) -> np.ndarray:
+        """Mean test loss per model; ``log(it, losses[R])`` every ``log_every`` steps."""
         R = len(self.programs)
         acc = np.zeros(R)
         with torch.no_grad():
             for it in range(epochs):
-                for r in range(R):
-                    acc[r] += float(self.loss(r, self.params[r]))
+                cur = np.array([float(self.loss(r, self.params[r])) for r in range(R)])
+                acc += cur
+                if log is not None and log_every > 0 and it % log_every == 0:
+                    log(it, cur)
                 self.rng_step += 1
         return acc / max(epochs, 1)
 

@@ -223,16 +223,24 @@ def shared_partition_order(name: str, seed: int = 0, scale: float = 1.0, **kw) -
     n = _scaled_shape(name, scale)[0]
     order = None
     LAST_PARTITION = {"computed_here": False, "compute_s": 0.0}
+    err = None
     if pdist.rank() == 0:
         pdist.set_host_threads(pdist.host_cpus())
         t = time.perf_counter()
         try:
             order = partition_order(name, seed=seed, scale=scale, **kw)
+        except Exception as e:                # the other ranks learn it from the status word
+            err = e
         finally:
             pdist.set_host_threads()          # back to this rank's share
         LAST_PARTITION = {"computed_here": True, "compute_s": round(time.perf_counter() - t, 2)}
     dt = np.int32 if n < (1 << 31) else np.int64
-    out = pdist.broadcast_host_array(None if order is None else order.astype(dt), n, dtype=dt)
+    try:
+        out = pdist.broadcast_host_array(None if order is None else order.astype(dt), n, dtype=dt)
+    except RuntimeError:
+        if err is not None:
+            raise err
+        raise
     return out.astype(np.int64)
 
 

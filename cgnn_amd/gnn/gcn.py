@@ -106,7 +106,7 @@ class GCNTrainer:
                  halo: Optional[bool] = None, capture: Optional[bool] = None, reorder: bool = False,
                  align_c: Optional[bool] = None, collectives: Optional[bool] = None,
                  train_rows_only: bool = True, l1_train_neighbours: bool = True, train_halo: bool = True,
-                 bwd_overlap: bool = True, fuse_agg: Optional[bool] = None):
+                 bwd_overlap: bool = True):
         # train_rows_only / l1_train_neighbours: training epochs aggregate layer 2 only at
         # the train rows and layer 1 only at the rows those read (the update is the same;
         # False: every row, for equivalence tests).  train_halo: a multi-rank run's
@@ -284,19 +284,6 @@ class GCNTrainer:
                           ops.fused_bwd_supported(self.F, hidden, self.C))
         self._gpart = None
         self._grad_index = None
-        # fuse_agg (one GPU, fully fused path; off by default): the layer-1 aggregation and
-        # the dense forward as ONE kernel (ops.agg_fwd: 16-wave blocks take 64-row chunks,
-        # the waves gather rows and the finished 32-row tiles' matrix products run on the
-        # waves that are ahead).  AX is bit-identical to the two-kernel path.  Measured
-        # slower on the products shape (3.07 vs 2.05 + 0.29 ms, profiles/r05_agg): the
-        # dense weights' LDS caps the launch at 16 waves per CU, too few for the
-        # latency-bound gathers (the standalone SpMM runs 32).
-        if fuse_agg is None:
-            fuse_agg = False
-        self._agg_queue = None
-        if (bool(fuse_agg) and self.fused_bwd and not self.multi and self.ldx <= 128
-                and self.ldx >= _ru(self.F, 16)):
-            self._agg_queue = ops.agg_queue(dev)
         # the training forward's dropout masks as the fused backward reads them (1 bit per
         # element: 78 MB for ogbn-products): the backward draws no Philox of its own
         self._kimg = (ops.keep_image(self.nloc, hidden, dev)
@@ -489,16 +476,11 @@ class GCNTrainer:
         # a prefetched AX restricted to the train-neighbour rows serves training only
         fresh = not self._ax_ready or not (train or self._l1 is None)
         self._ax_ready = False
-        done = False
-        if fresh and self._agg_queue is not None:
-            rp, col = self._l1 if (train and self._l1 is not None) else (self.rowptr, self.col)
-            done = ops.agg_fwd(rp, col, self.Xs, self.AX, self.W1, self.b1, self.W2, self.dinv, self.Z2loc, F, p,
-                               self.key, self._dropout_step(), self.r0, kimg=kimg, queue=self._agg_queue)
-        if fresh and not done:
+        if fresh:
             self._aggregate_features(self.AX, train)
         if not self.fused_bwd:           # bf16 W2 of the unfused fallbacks (the fused kernels read fp32)
             self.W2b[:, :C] = self.W2.to(torch.bfloat16)
-        if not done and not (self.fused and ops.dense_fwd(self.AX, self.W1, self.b1, self.W2, self.dinv,
+        if not (self.fused and ops.dense_fwd(self.AX, self.W1, self.b1, self.W2, self.dinv,
                                                           None if self.fused_bwd else H1,
                                                           self.Z2loc[:n], F, p, self.key, self._dropout_step(),
                                                           self.r0, kimg=kimg)):

@@ -96,16 +96,32 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
 _DB_INDEX = {}
 
 
+class EllImage:
+    """ELL image of a CSR for ``spmm_ell``.  ``ell``: int32 [n, 8], the row's column ids
+    (-1 past its end), or {-2, e0, e1, -1...} for a row of more than 8 entries (its CSR
+    range); ``long_rows``: int32 [n_long], the ids of those rows, ascending (the GPU
+    sums them in a launch of their own, so the short-row loop has no data-dependent
+    inner loop)."""
+    __slots__ = ("ell", "long_rows", "n_long")
+
+    def __init__(self, ell, long_rows):
+        self.ell, self.long_rows, self.n_long = ell, long_rows, int(long_rows.numel())
+
+    @property
+    def n(self):
+        return self.ell.shape[0]
+
+
 def ell_image(rowptr, col):
-    """ELL image of a CSR for ``spmm_ell``: int32 [n, 8], the row's column ids (-1 past
-    its end), or {-2, e0, e1, -1...} for a row of more than 8 entries (its CSR range)."""
+    """:class:`EllImage` of the CSR (rowptr, col), built once at setup."""
     n = rowptr.numel() - 1
     ell = torch.empty(n, 8, dtype=torch.int32, device=col.device)
-    if col.is_cuda:
-        native.hip().gnn_ell_build(rowptr.data_ptr(), col.data_ptr(), ell.data_ptr(), n, _st(col))
-        return ell
     rp = rowptr.long()
     deg = rp[1:] - rp[:-1]
+    long_rows = torch.nonzero(deg > 8).flatten().to(torch.int32).contiguous()
+    if col.is_cuda:
+        native.hip().gnn_ell_build(rowptr.data_ptr(), col.data_ptr(), ell.data_ptr(), n, _st(col))
+        return EllImage(ell, long_rows)
     ell.fill_(-1)
     for u in range(8):
         has = deg > u
@@ -115,19 +131,20 @@ def ell_image(rowptr, col):
     ell[longr, 0] = -2
     ell[longr, 1] = rp[:-1][longr].to(torch.int32)
     ell[longr, 2] = rp[1:][longr].to(torch.int32)
-    return ell
+    return EllImage(ell, long_rows)
 
 
-def spmm_ell(ell, col, X, F, rscale=None, out=None):
-    """Y[i,:F] = rscale[i] * sum_{j in N(i)} X[j,:F] from an ``ell_image`` (bf16, F <= 64;
-    the same sums as ``spmm`` over the CSR the image was built from)."""
+def spmm_ell(img, col, X, F, rscale=None, out=None):
+    """Y[i,:F] = rscale[i] * sum_{j in N(i)} X[j,:F] from an :class:`EllImage` (bf16,
+    F <= 64; the same sums as ``spmm`` over the CSR the image was built from)."""
+    ell = img.ell
     n = ell.shape[0]
     if out is None:
         out = torch.empty(n, X.shape[1], dtype=torch.bfloat16, device=X.device)
     if X.is_cuda:
         native.hip().gnn_spmm_ell(ell.data_ptr(), col.data_ptr(), X.data_ptr(), out.data_ptr(),
                                   rscale.data_ptr() if rscale is not None else 0, n, F, X.shape[1],
-                                  out.shape[1], _st(X))
+                                  out.shape[1], X.shape[0], img.long_rows.data_ptr(), img.n_long, _st(X))
         return out
     acc = torch.zeros(n, F, dtype=torch.float32)
     for u in range(8):
@@ -399,39 +416,6 @@ def dense_fwd(AX, W1, b1, W2, dinv, H1, Z2, F, p, key, step, row0=0, kimg=None):
     Z2.zero_()
     Z2[:, :C] = (y2 * dinv[:n, None]).to(torch.bfloat16)
     return True
-
-
-def agg_queue(device):
-    """Work-queue words of ``agg_fwd`` (zero; each launch leaves them zero)."""
-    return torch.zeros(native.hip().gnn_agg_fwd_queue_words(), dtype=torch.int32, device=device)
-
-
-def agg_fwd(rowptr, col, Xs, AX, W1, b1, W2, dinv, Z2, F, p, key, step, row0=0, kimg=None, queue=None):
-    """The layer-1 aggregation fused with the dense forward (GPU, one kernel):
-    AX = spmm(rowptr, col, Xs, rscale=dinv, unit_col=F) (bit-identical to ``spmm``), then
-    ``dense_fwd(AX, ...)`` with H1 not stored.  ``queue``: an ``agg_queue`` buffer.
-    Returns False when no compiled variant covers the shape (the caller runs the two
-    kernels instead)."""
-    n = rowptr.numel() - 1
-    HD, C = W1.shape[1], W2.shape[1]
-    if checks.enabled():
-        checks.csr(rowptr, col, Xs.shape[0], "agg_fwd")
-        checks.rows(AX, n, "agg_fwd AX")
-        checks.rows(Z2, n, "agg_fwd Z2")
-        checks.rows(dinv, n, "agg_fwd dinv")
-    if queue is None:
-        queue = agg_queue(AX.device)
-    sv, sp = _step_args(step)
-    rc = native.hip().gnn_agg_fwd(rowptr.data_ptr(), col.data_ptr(), Xs.data_ptr(), AX.data_ptr(), W1.data_ptr(),
-                                  b1.data_ptr(), W2.data_ptr(), dinv.data_ptr(), Z2.data_ptr(), n, F, AX.shape[1],
-                                  HD, C, Z2.shape[1], float(p), int(key[0]), int(key[1]), sv, int(row0), _st(AX),
-                                  step_ptr=sp, kimg=kimg.data_ptr() if kimg is not None else 0,
-                                  ctr=queue.data_ptr())
-    if rc == 0:
-        return True
-    if rc != -1:
-        raise RuntimeError("gnn_agg_fwd failed (%d)" % rc)
-    return False
 
 
 def dense_bwd(dY2, W2, H1, dP1, p):

@@ -211,6 +211,7 @@ class _Slot:
         self.free = torch.cuda.Event()      # the training that read this slot finished
         self.widx = -1                      # the slot's index in the native worker
         self.keep = None                    # what a posted job refers to (events, seeds)
+        self.pending = None                 # the SampledBatch last enqueued into this slot
 
 
 class SampledBatch:
@@ -327,6 +328,12 @@ class PipelinedSampler:
             checks.index(seeds, self.n, "sample_blocks seeds")
             checks.csr(self.rowptr, self.col, self.n, "sample_blocks graph", n_rows=self.n)
         sl = self.slots[self._next]
+        if sl.pending is not None and sl.pending._res is None:
+            # the slot's previous batch was never resolved: refilling it would overwrite
+            # blocks a caller may still read and, in threaded mode, free the ready event
+            # (sl.keep) before the worker has issued the earlier job's wait on it
+            raise RuntimeError("PipelinedSampler.enqueue: more than %d batches outstanding; resolve() "
+                               "the oldest before enqueueing another" % len(self.slots))
         self._next = (self._next + 1) % len(self.slots)
         main = torch.cuda.current_stream(self.dev)
         seeds = seeds.to(dtype=torch.int32).contiguous()
@@ -338,7 +345,8 @@ class PipelinedSampler:
             seeds.record_stream(self.stream)
             seq = native.hip().gnn_sw_submit(self._w, sl.widx, seeds.data_ptr(), int(seeds.numel()),
                                              int(salt) & 0xFFFFFFFF, [ready.cuda_event, sl.free.cuda_event])
-            return SampledBatch(sl, self.fanouts, int(seeds.numel()), waiter=(self._w, seq))
+            sl.pending = SampledBatch(sl, self.fanouts, int(seeds.numel()), waiter=(self._w, seq))
+            return sl.pending
         p = lambda ts: [t.data_ptr() if t is not None else 0 for t in ts]
         with torch.cuda.stream(self.stream):
             if ready is None:
@@ -357,7 +365,8 @@ class PipelinedSampler:
                 sl.counts_host.copy_(sl.counts, non_blocking=True)
             sl.done.record(self.stream)
             seeds.record_stream(self.stream)
-        return SampledBatch(sl, self.fanouts, int(seeds.numel()))
+        sl.pending = SampledBatch(sl, self.fanouts, int(seeds.numel()))
+        return sl.pending
 
     def consumed(self, batch: SampledBatch):
         """Mark the end of the training that reads ``batch`` (enqueued on the current

@@ -84,8 +84,7 @@ class CGNN_model(object):
             return program_for_confounders(self.graph, self.cfg.h_layer_dim)
         return program_for_dag(self.graph, self.cfg.h_layer_dim, self.nodes)
 
-    def _make(self, data):
-        import torch
+    def _make(self, data, record=0):
         from ..parallel import dist as pdist
         data = np.ascontiguousarray(np.asarray(data, dtype=np.float32).T)
         key = model_key(self.cfg.seed, "cgnn", self.run)
@@ -95,29 +94,46 @@ class CGNN_model(object):
             return DeviceTrainer([self._program()], [data], [key], self.cfg.h_layer_dim, devs[0],
                                  learning_rate=self.cfg.learning_rate, init_std=self.cfg.init_std,
                                  use_fast_mmd=self.cfg.use_Fast_MMD,
-                                 nb_vectors=self.cfg.nb_vectors_approx_MMD)
+                                 nb_vectors=self.cfg.nb_vectors_approx_MMD, record_history=record)
         from ..engine.reference import ReferenceTrainer
         return ReferenceTrainer([self._program()], [data], [key], self.cfg.h_layer_dim,
                                 learning_rate=self.cfg.learning_rate, init_std=self.cfg.init_std,
                                 use_fast_mmd=self.cfg.use_Fast_MMD,
                                 nb_vectors=self.cfg.nb_vectors_approx_MMD)
 
+    def _log(self, it, score):
+        # the reference's progress line (CGNN.py:123-127, 147-149)
+        print('Pair:{}, Run:{}, Iter:{}, score:{}'.format(self.idx, self.run, it, score))
+
     def train(self, data, verbose=True, **kwargs):
-        epochs = kwargs.get("train_epochs", self.cfg.train_epochs)
-        self._trainer = self._make(data)
-        if hasattr(self._trainer, "start"):
-            self._trainer.start()
-        self._trainer.train(epochs)
+        """Fit the model; with ``verbose`` the training loss of every 100th iteration is
+        printed as the reference does (recorded on the device, printed after the run)."""
+        epochs = int(kwargs.get("train_epochs", self.cfg.train_epochs))
+        self._trainer = self._make(data, record=epochs if verbose else 0)
+        tr = self._trainer
+        if hasattr(tr, "start"):
+            tr.start()
+            tr.train(epochs)
+            hist = tr.history()[0] if verbose else None
+        else:
+            tr.train(epochs)
+            hist = tr.loss_history[0][-epochs:] if verbose else None
+        if verbose:
+            for it in range(0, epochs, 100):
+                self._log(it, float(hist[it]))
 
     def evaluate(self, data, verbose=True, **kwargs):
-        epochs = kwargs.get("test_epochs", self.cfg.test_epochs)
+        """Mean test MMD over ``test_epochs`` evaluation steps (every 100th step's loss
+        printed with ``verbose``)."""
+        epochs = int(kwargs.get("test_epochs", self.cfg.test_epochs))
         if self._trainer is None:
             self.train(data, verbose)
+        log = (lambda it, v: self._log(it, float(v[0]))) if verbose else None
         if hasattr(self._trainer, "start"):
-            self._trainer.evaluate(epochs)
+            self._trainer.evaluate(epochs, log_every=100 if verbose else 0, log=log)
             self._trainer._test_epochs = max(epochs, 1)
             return float(self._trainer.collect()[0])
-        return float(self._trainer.evaluate(epochs)[0])
+        return float(self._trainer.evaluate(epochs, log_every=100 if verbose else 0, log=log)[0])
 
     def generate(self, data, **kwargs):
         if self._trainer is None:

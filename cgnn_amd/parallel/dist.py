@@ -134,17 +134,27 @@ def broadcast_host_array(arr: Optional[np.ndarray], n: int, dtype=np.int64, src:
                          chunk_bytes: int = 256 << 20) -> np.ndarray:
     """Broadcast a 1-D host array of ``n`` elements from rank ``src`` (the other ranks
     pass None).  Over RCCL it travels through one device staging buffer of at most
-    ``chunk_bytes`` (a 111 M-entry partition order is 0.9 GB); over gloo directly."""
+    ``chunk_bytes`` (a 111 M-entry partition order is 0.9 GB); over gloo directly.
+    A status word goes first: if ``src`` has no valid array (None, or the wrong shape
+    -- e.g. the pass that should have produced it raised), EVERY rank raises instead
+    of the others blocking in the data broadcast until the collective times out."""
     if not is_distributed():
         return np.asarray(arr)
     import torch.distributed as dist
     tdt = {np.dtype(np.int64): torch.int64, np.dtype(np.int32): torch.int32,
            np.dtype(np.float32): torch.float32}[np.dtype(dtype)]
+    nccl = dist.get_backend() == "nccl"
+    sdev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+    ok = rank() != src or (arr is not None and np.shape(arr) == (n,))
+    status = torch.tensor([1 if ok else 0], dtype=torch.int64, device=sdev)
+    dist.broadcast(status, src)
+    if int(status.item()) != 1:
+        held = None if arr is None else np.shape(arr)
+        raise RuntimeError("broadcast_host_array: source rank %d has no valid array (holds %s, expected (%d,))"
+                           % (src, held if rank() == src else "?", n))
     out = np.asarray(arr, dtype=dtype) if rank() == src else np.empty(n, dtype=dtype)
-    if out.shape != (n,):
-        raise ValueError("broadcast_host_array: rank %d holds %s, expected (%d,)" % (rank(), out.shape, n))
     host = torch.from_numpy(out)
-    if dist.get_backend() != "nccl":
+    if not nccl:
         dist.broadcast(host, src)
         return out
     per = max(1, chunk_bytes // out.itemsize)

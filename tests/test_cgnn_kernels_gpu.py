@@ -155,6 +155,26 @@ def test_graph_replay_equals_eager():
     np.testing.assert_array_equal(a, b)   # bitwise: deterministic reductions, no atomics
 
 
+def test_verbose_object_api_logs_without_changing_the_score(capsys):
+    """CGNN_model on the GPU: verbose train/evaluate print iterations 0, 100, ... (the
+    recorded history; the chunked evaluation reads loss_last), and the score is bitwise
+    the silent run's."""
+    from cgnn_amd.models.cgnn import CGNN_model
+    g = _toy_dag()
+    data = _data(5, 300, 1).T
+    kw = dict(train_epochs=230, test_epochs=120, h_layer_dim=20, gpu=True, nb_gpu=1)
+    a = CGNN_model(300, g, run=1, idx=2, **kw)
+    a.train(data, verbose=True)
+    sa = a.evaluate(data, verbose=True)
+    lines = [l for l in capsys.readouterr().out.splitlines() if l.startswith("Pair:")]
+    assert [int(l.split("Iter:")[1].split(",")[0]) for l in lines] == [0, 100, 200, 0, 100]
+    b = CGNN_model(300, g, run=1, idx=2, **kw)
+    b.train(data, verbose=False)
+    sb = b.evaluate(data, verbose=False)
+    assert capsys.readouterr().out.count("Pair:") == 0
+    assert sa == sb
+
+
 def test_batch_composition_does_not_change_scores():
     H = 20
     g = _toy_dag()

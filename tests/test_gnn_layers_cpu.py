@@ -231,7 +231,7 @@ def test_spmm_ell_reference_matches_spmm():
     X[:, :C] = torch.randn(n, C).to(torch.bfloat16)
     rs = torch.rand(n) + 0.5
     ell = ops.ell_image(rp, col)
-    assert int((ell[:, 0] == -2).sum()) == 5
+    assert int((ell.ell[:, 0] == -2).sum()) == 5 and ell.long_rows.tolist() == [0, 1, 2, 3, 4]
     got = ops.spmm_ell(ell, col, X, C, rscale=rs)
     ref = ops.spmm(rp, col, X, C, rscale=rs, out=torch.empty(n, ld, dtype=torch.bfloat16))
     assert torch.allclose(got.float(), ref.float(), rtol=1e-2, atol=1e-2)

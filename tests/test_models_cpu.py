@@ -192,6 +192,33 @@ def test_cgnn_model_object_api():
     assert np.isfinite(run_CGNN_tf(df, g, 0, 0, **TINY))
 
 
+def test_cgnn_model_verbose_prints_every_100_iterations(capsys):
+    """CGNN_model.train / evaluate(verbose=True) print the reference's progress line
+    (CGNN.py:123-127, 147-149) at iterations 0, 100, 200, ...; the score is the same as
+    a silent run's (same draws)."""
+    from cgnn.CGNN import CGNN_tf
+    df = chain_data(n=60)
+    g = DirectedGraph()
+    g.add("A", "B")
+    g.add("B", "C")
+    kw = dict(TINY, train_epochs=205, test_epochs=150)
+    data = df[["A", "B", "C"]].values
+    m = CGNN_tf(len(df), g, 0, 3, **kw)
+    m.train(data, verbose=True)
+    score = m.evaluate(data, verbose=True)
+    lines = [l for l in capsys.readouterr().out.splitlines() if l.startswith("Pair:")]
+    its = [int(l.split("Iter:")[1].split(",")[0]) for l in lines]
+    assert its == [0, 100, 200, 0, 100]
+    assert all(l.startswith("Pair:3, Run:0, Iter:") for l in lines)
+    hist = m._trainer.loss_history[0]
+    assert float(lines[1].split("score:")[1]) == pytest.approx(hist[100], rel=1e-6)
+    q = CGNN_tf(len(df), g, 0, 3, **kw)
+    q.train(data, verbose=False)
+    s2 = q.evaluate(data, verbose=False)
+    assert capsys.readouterr().out.count("Pair:") == 0
+    assert s2 == pytest.approx(score, rel=1e-9)
+
+
 def test_gnn_plugin_names():
     from cgnn.GNN import GNN_tf, tf_run_instance
     df = chain_data()

@@ -211,14 +211,27 @@ def main():
             # once per job (rank 0, every core) and broadcast: each rank computing the
             # whole 111 M-node pass held its own 13 GB structure and ran it on 1/8 of the cores
             from cgnn_amd.gnn.data import shared_partition_order
+            # the cache holds what it was computed for; another seed or scale at the same n
+            # would pass synthetic_shard's permutation check and silently skew the timing
+            ident = np.array([a.seed, int(round(a.scale * 1e9))], dtype=np.int64)
+            cached = None
             if a.order_cache and world == 1 and os.path.exists(a.order_cache):
-                _progress("partition order from %s" % a.order_cache)
-                order = np.load(a.order_cache)
+                z = np.load(a.order_cache)          # a bare .npy (older caches) has no identity
+                if isinstance(z, np.lib.npyio.NpzFile):
+                    if ("ident" in z.files and "dataset" in z.files and str(z["dataset"]) == "ogbn-papers100M"
+                            and np.array_equal(z["ident"], ident)):
+                        cached = z["order"]
+                    z.close()
+                _progress("partition order from %s" % a.order_cache if cached is not None
+                          else "order cache %s is for another graph: recomputing" % a.order_cache)
+            if cached is not None:
+                order = cached
             else:
                 _progress("partition order (rank 0 computes, then broadcast)")
                 order = shared_partition_order("ogbn-papers100M", seed=a.seed, scale=a.scale)
                 if a.order_cache and world == 1:
-                    np.save(a.order_cache, order)
+                    with open(a.order_cache, "wb") as fh:
+                        np.savez(fh, order=order, ident=ident, dataset=np.array("ogbn-papers100M"))
         part_s = time.perf_counter() - t0
         _progress("partition done in %.1f s; generating the shard" % part_s)
         shard = synthetic_shard("ogbn-papers100M", srank, sworld, seed=a.seed, device=dev, scale=a.scale,

@@ -1,7 +1,6 @@
 """One steady-state training epoch out of a rocprofv3 kernel trace of bench.py: the
-dispatches from the k-th training forward (``gcn_agg_fwd``, the fused layer-1 aggregation
-+ dense forward, or the layer-1 ``spmm_kernel`` before a ``gcn_dense_fwd``) up to the
-next one, with durations and the gaps between them.
+dispatches from the k-th training forward (the layer-1 ``spmm_kernel`` before a
+``gcn_dense_fwd``) up to the next one, with durations and the gaps between them.
 
     python tools/epoch_trace.py <run_kernel_trace.csv> [k]
 """
@@ -14,13 +13,11 @@ def main():
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    fw = [i for i, r in enumerate(rows) if "gcn_dense_fwd" in r["Kernel_Name"] or "gcn_agg_fwd" in r["Kernel_Name"]]
+    fw = [i for i, r in enumerate(rows) if "gcn_dense_fwd" in r["Kernel_Name"]]
     if len(fw) <= k + 1:
         sys.exit("only %d dense forwards in the trace" % len(fw))
     # the epoch starts with its layer-1 SpMM: back up from the forward to the previous spmm
     def start(i):
-        if "gcn_agg_fwd" in rows[i]["Kernel_Name"]:
-            return i
         while i > 0 and "spmm_kernel" not in rows[i]["Kernel_Name"]:
             i -= 1
         return i
