@@ -33,6 +33,7 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int WAVES = 16;           // 1024-thread blocks: 4 waves per SIMD share the LDS weights
 constexpr int TILE = 32;
@@ -363,23 +364,37 @@ __global__ __launch_bounds__(WAVES * 64) void gcn_dense_bwd_kernel(
 //   gW2[h][c]   += sum_rows H1^T[h][row] dY2[row][c]
 // Block = HD/32 waves; wave w owns hidden block w (32 units) for all four products,
 // so its W1 / W2^T B fragments (KS + KC bf16x8) sit in registers for the whole launch
-// and its weight-gradient tiles (KF/32 + 2 of 32x32) in its accumulators.  The
-// recompute chains produce ROWS x HIDDEN tiles (lane = hidden unit, registers = 16
-// rows of the tile) that are ALREADY the A operands of the contractions over the rows
-// (dP1^T, H1^T: hidden x rows; the k order inside a 16-row step is permuted -- rows
-// 4h..4h+3, 8+4h..8+4h+3 -- and the transposed B reads of AX / dY2 use the same
-// permutation).  Per 32-row tile the block stages the AX / dY2 rows once, row-major
-// in swizzled 256-B rows (the recompute reads them by rows with b128, the contractions
-// by columns with ds_read_b64_tr_b16), and the tile's keep image from the forward;
-// double-buffered behind a register prefetch of the tile after next: one block
-// barrier per tile.
+// and its weight-gradient tiles in its accumulators.  The recompute chains
+// (v_mfma_f32_32x32x16_bf16, K = 16 KS exactly) produce ROWS x HIDDEN tiles (lane =
+// hidden unit, registers = 16 rows of the tile).  The contractions over the 32 rows
+// run on v_mfma_f32_16x16x32_bf16 (K = 32 rows in one instruction; output tiles of
+// 16 hidden x 16 features, so the gradient's feature / class padding is to 16, not 32:
+// KS + KC tiles per hidden half instead of 2 (KF/32 + 2) 32x32 halves -- 9 % fewer MFMA
+// cycles and 16 fewer accumulator registers).  Their A operands (16 hidden x 32 rows)
+// come from the recompute accumulators by one v_permlane16_swap per packed dword pair:
+// lane groups 0 / 2 keep the pairs {0, 1, 4, 5} of their 32x32 rows and trade {2, 3,
+// 6, 7} with groups 1 / 3, which then hold the other hidden half -- k-slot e of lane
+// group g is tile row b_g + (e & 3) + 16 (e >> 2), b_g = 8 (g & 1) + 4 (g >> 1), and
+// the transposed B reads of AX / dY2 fetch those rows (conflict-free in the swizzled
+// image: the rows one 32-lane half reads differ in bits 2-3).  Per 32-row tile the
+// block stages the AX / dY2 rows once, row-major in swizzled 256-B rows (the recompute
+// reads them by rows with b128, the contractions by columns with ds_read_b64_tr_b16),
+// and the tile's keep image from the forward; double-buffered behind a register
+// prefetch of the tile after next: one block barrier per tile.
+// Round 6 (profiles/r06_bwd): this form 429-440 us against 445-449 for the round-5
+// 32x32 contractions.  Measured slower and not kept: waves 4-7 staggered by half a tile
+// (contraction of tile t - 1 before tile t's recompute; ring of three buffers; 590 us --
+// two code paths, 256 VGPRs and spills), and a software pipeline in every wave (tile
+// t + 1's epilogue interleaved with tile t's contractions by sched_group_barrier, the
+// weight fragments moved to LDS to make room; 530 us).
 // Epilogue on packed bf16 pairs (two rows per dword): relu as a signed 16-bit max, the
 // keep bits and the relu derivative as 16-bit multiplies by 0 / 1 -- no compares,
 // selects or per-element bit extracts, and no Philox: the forward drew the masks (a
 // draw costs ~60 VALU instructions, a third of them quarter-rate 32-bit multiplies,
 // and every wave of the round-3 form re-drew its tile's).
-// Output: one fp32 slab per block, gpart[block][HD][KF + 64] = [gW1^T | gW2], summed in
-// fixed order afterwards.
+// Output: one fp32 slab per block, gpart[block][HD][KF + 64] = [gW1^T | gW2] (KF = the
+// feature columns rounded up to 32; padding columns written 0), summed in fixed order
+// afterwards.
 // ============================================================================
 // LDS bytes: two staging buffers (AX | dY2, [32][128] bf16 each) + two keep images
 constexpr size_t fused_bwd_lds(int HD) { return sizeof(uint16_t) * 2 * 2 * 32 * 128 + 2 * (size_t)(HD / 32) * 128; }
@@ -392,8 +407,9 @@ __global__ __launch_bounds__(HD * 2, 1) void gcn_fused_bwd_kernel(
   constexpr int NW = HD / 32;                 // waves per block = hidden blocks
   constexpr int NT = NW * 64;
   constexpr int KP = KS * 16;                 // layer-1 K (features + ones column), padded
-  constexpr int KF = (KP + 31) / 32 * 32;     // gW1^T columns (f), padded to whole tiles
+  constexpr int KF = (KP + 31) / 32 * 32;     // gW1^T slab columns (f), 32-aligned
   constexpr int CP = KC * 16;                 // classes, padded
+  constexpr int NF = KS;                      // 16-wide feature tiles of the contraction
   constexpr int KCH = DROP ? NW * 8 : 0;      // 16-B chunks of one tile's keep image
   static_assert(KF <= 128 && CP <= 64, "staging rows are 256 B");
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
@@ -403,7 +419,7 @@ __global__ __launch_bounds__(HD * 2, 1) void gcn_fused_bwd_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63, h = lane >> 5, lr = lane & 31;
   const int wv = tid >> 6;
-  const int gb = (lane >> 4) & 1, qq = (lane >> 2) & 3, pq = lane & 3;
+  const int qq = (lane >> 2) & 3, pq = lane & 3;
 
   // B fragments of the two recompute chains (lane = hidden unit, k = 16 s + 8 h + j)
   bf16x8 w1f[KS], w2f[KC];
@@ -449,11 +465,14 @@ __global__ __launch_bounds__(HD * 2, 1) void gcn_fused_bwd_kernel(
   const int uh = (lr >> 2) & 1;
   const uint32_t kq = 4u * (lr >> 3) + (lr & 3);
 
-  f32x16 g1[KF / 32], g2[2];
+  f32x4 g1[2][NF], g2[2][KC];                 // [hidden half][16-wide column tile]
 #pragma unroll
-  for (int q = 0; q < KF / 32; ++q) g1[q] = f32x16{};
-  g2[0] = f32x16{};
-  g2[1] = f32x16{};
+  for (int hb = 0; hb < 2; ++hb) {
+#pragma unroll
+    for (int q = 0; q < NF; ++q) g1[hb][q] = f32x4{};
+#pragma unroll
+    for (int q = 0; q < KC; ++q) g2[hb][q] = f32x4{};
+  }
 
   // prefetch registers: AX chunks i = tid + k NT (chunk i = row i % 32, column chunk
   // i / 32); dY2 chunks in the same form, and the tile's keep image (KCH chunks) in the
@@ -560,43 +579,71 @@ __global__ __launch_bounds__(HD * 2, 1) void gcn_fused_bwd_kernel(
       ah[i] = x;
       ad[i] = pk_mul16(cvt_pk(dh[2 * i], dh[2 * i + 1]), pk_nz(x));
     }
-    bf16x8 ah1[2], adp[2];
+    // 16x16x32 A operands of the two hidden halves (see the header): pairs {0, 1, 4, 5}
+    // stay, {2, 3, 6, 7} go to the neighbouring lane group
+    bf16x8 aH[2], aD[2];
+    {
+      constexpr int KEEP[4] = {0, 1, 4, 5}, SEND[4] = {2, 3, 6, 7};
+      uint32_t h0[4], h1[4], d0[4], d1[4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      ah1[s] = __builtin_bit_cast(bf16x8, make_uint4(ah[4 * s], ah[4 * s + 1], ah[4 * s + 2], ah[4 * s + 3]));
-      adp[s] = __builtin_bit_cast(bf16x8, make_uint4(ad[4 * s], ad[4 * s + 1], ad[4 * s + 2], ad[4 * s + 3]));
+      for (int k = 0; k < 4; ++k) {
+        const auto sh = __builtin_amdgcn_permlane16_swap(ah[KEEP[k]], ah[SEND[k]], false, false);
+        const auto sd = __builtin_amdgcn_permlane16_swap(ad[KEEP[k]], ad[SEND[k]], false, false);
+        h0[k] = sh[0];
+        h1[k] = sh[1];
+        d0[k] = sd[0];
+        d1[k] = sd[1];
+      }
+      aH[0] = __builtin_bit_cast(bf16x8, make_uint4(h0[0], h0[1], h0[2], h0[3]));
+      aH[1] = __builtin_bit_cast(bf16x8, make_uint4(h1[0], h1[1], h1[2], h1[3]));
+      aD[0] = __builtin_bit_cast(bf16x8, make_uint4(d0[0], d0[1], d0[2], d0[3]));
+      aD[1] = __builtin_bit_cast(bf16x8, make_uint4(d1[0], d1[1], d1[2], d1[3]));
     }
 
-    // ---- contractions over the tile's 32 rows (two k-steps of 16, permuted rows) ----
+    // ---- contractions over the tile's 32 rows: one 16x16x32 MFMA per output tile ----
+    // B fragment of column tile q: rows rb and rb + 16 (k-slots 0..3 / 4..7) of lane
+    // group g4, 16 columns from chunk 2q; lane 4 qq + pq addresses row qq, columns 4 pq
+    {
+      const int g4 = lane >> 4;
+      const int rb = 8 * (g4 & 1) + 4 * (g4 >> 1) + qq;
+      const int cx = 8 * (pq & 1);
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const int ra = 16 * s2 + 4 * h + qq;      // block rows ra (+8 for the second read)
-      const int cb = 2 * gb + (pq >> 1), cx = 8 * (pq & 1);
-#pragma unroll
-      for (int q = 0; q < KF / 32; ++q) {
-        const bf16x8 bx = tr_frag(sAX, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 8, 4 * q + cb) + cx);
-        g1[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(adp[s2], bx, g1[q], 0, 0, 0);
+      for (int q = 0; q < NF; ++q) {
+        const int ch = 2 * q + (pq >> 1);
+        const bf16x8 bx = tr_frag(sAX, stg_off(rb, ch) + cx, stg_off(rb + 16, ch) + cx);
+        g1[0][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aD[0], bx, g1[0][q], 0, 0, 0);
+        g1[1][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aD[1], bx, g1[1][q], 0, 0, 0);
       }
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const bf16x8 by = tr_frag(sDY, stg_off(ra, 4 * q + cb) + cx, stg_off(ra + 8, 4 * q + cb) + cx);
-        g2[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1[s2], by, g2[q], 0, 0, 0);
+      for (int q = 0; q < KC; ++q) {
+        const int ch = 2 * q + (pq >> 1);
+        const bf16x8 by = tr_frag(sDY, stg_off(rb, ch) + cx, stg_off(rb + 16, ch) + cx);
+        g2[0][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aH[0], by, g2[0][q], 0, 0, 0);
+        g2[1][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aH[1], by, g2[1][q], 0, 0, 0);
       }
     }
     __syncthreads();      // this buffer is rewritten two tiles on; the next one is staged
   }
 
-  // ---- this block's partial slab: rows = hidden 32 wv + m, columns [f | KF + c] ----
+  // ---- this block's partial slab: rows = hidden 32 wv + 16 hb + m, columns [f | KF + c]
+  // (16x16 tile: lane = column, register v = row 4 (lane >> 4) + v); padding columns 0 ----
   const float gs = DROP ? scale : 1.f;        // the kept units' 1/(1-p)
   float* gp = gpart + (size_t)blockIdx.x * HD * (KF + 64);
+  const int cl = lane & 15;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int hrow = 32 * wv + (q & 3) + 8 * (q >> 2) + 4 * h;
-    float* dst = gp + (size_t)hrow * (KF + 64);
+  for (int hb = 0; hb < 2; ++hb) {
 #pragma unroll
-    for (int fb = 0; fb < KF / 32; ++fb) dst[32 * fb + lr] = g1[fb][q] * gs;
-    dst[KF + lr] = g2[0][q] * gs;
-    dst[KF + 32 + lr] = g2[1][q] * gs;
+    for (int v = 0; v < 4; ++v) {
+      float* dst = gp + (size_t)(32 * wv + 16 * hb + 4 * (lane >> 4) + v) * (KF + 64);
+#pragma unroll
+      for (int q = 0; q < NF; ++q) dst[16 * q + cl] = g1[hb][q][v] * gs;
+#pragma unroll
+      for (int q = NF; q < KF / 16; ++q) dst[16 * q + cl] = 0.f;
+#pragma unroll
+      for (int q = 0; q < KC; ++q) dst[KF + 16 * q + cl] = g2[hb][q][v] * gs;
+#pragma unroll
+      for (int q = KC; q < 4; ++q) dst[KF + 16 * q + cl] = 0.f;
+    }
   }
 }
 

@@ -286,11 +286,14 @@ __global__ __launch_bounds__(256, 8) void spmm_ell_kernel(const int* __restrict_
 // gather and the row store go through buffer descriptors with out-of-range offsets for
 // inactive lanes (the hardware returns 0 / drops the store): no branches, so the waits
 // are exact counts that leave the prefetch in flight.  Rows of more than 8 entries are
-// skipped here (their store is dropped) and summed by spmm_ell_long_kernel from the
-// image's list of long rows: a data-dependent inner loop in this one would make every
-// wait of the loop a full drain.  Same adds in the same order as spmm_ell_kernel:
-// bit-identical output.  Tables below 2^31 bytes (the launcher checks).
+// skipped in that loop (their store is dropped): a data-dependent inner loop inside it
+// would make every wait of the loop a full drain.  After it, the waves sum the image's
+// list of long rows, one per 8-lane sub-group, over their CSR ranges.  Same adds in the
+// same order as spmm_ell_kernel: bit-identical output.  Tables below 2^31 bytes (the
+// launcher checks).
 __global__ __launch_bounds__(256, 8) void spmm_ell_pipe_kernel(const int* __restrict__ ell,
+                                                            const int* __restrict__ col,
+                                                            const int* __restrict__ long_rows, int n_long,
                                                             const uint16_t* __restrict__ X,
                                                             uint16_t* __restrict__ Y,
                                                             const float* __restrict__ rscale, int n_rows, int F,
@@ -309,8 +312,11 @@ __global__ __launch_bounds__(256, 8) void spmm_ell_pipe_kernel(const int* __rest
                                                                       0x00020000);
   // a valid address for the row-scale load when there is no rscale (the value is unused)
   const float* rsb = rscale ? rscale : reinterpret_cast<const float*>(ell);
-  int g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (g >= n_groups) return;                 // uniform per wave
+  // (measured: giving each XCD a contiguous eighth of the row groups, so that the
+  // compact-G rows it gathers could stay in its L2, was neutral -- 174.8 vs 175.0 us)
+  const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  int g = wave;
+  if (g < n_groups) {                        // uniform per wave
   // clamped, unconditional loads (a "load or -1" branches and waits at the join)
   int nj = ell[(size_t)min(g * RPW + sub, n_rows - 1) * 8 + sl];
   // a dropped store behind the first index load: the loop is entered with the same
@@ -349,30 +355,21 @@ __global__ __launch_bounds__(256, 8) void spmm_ell_pipe_kernel(const int* __rest
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, f32x8_to_bf16(y)), yr, yo, 0, 0);
     g += nw;
   } while (g < n_groups);
-}
-
-// The long rows (more than 8 entries) of an ELL image, listed in `rows`: one 8-lane
-// sub-group per row over its CSR range, exactly spmm_ell_kernel's long-row path.
-__global__ __launch_bounds__(256) void spmm_ell_long_kernel(const int* __restrict__ rows, int n_long,
-                                                          const int* __restrict__ ell, const int* __restrict__ col,
-                                                          const uint16_t* __restrict__ X, uint16_t* __restrict__ Y,
-                                                          const float* __restrict__ rscale, int F, int ldx,
-                                                          int ldy) {
-  constexpr int L = 8;
-  const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
-  const int k = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + sub;
-  if (k >= n_long) return;                   // uniform per sub-group
-  const int row = rows[k];
-  const int f0 = sl * 8;
-  const int e0 = ell[(size_t)row * 8 + 1], e1 = ell[(size_t)row * 8 + 2];
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  gather_sum<L, 1, 8>(col, X, e0, e1, ldx, f0, f0 < F, sub * L, sl, acc);
-  if (f0 >= ldy) return;
-  const float rs = rscale ? rscale[row] : 1.f;
-  float y[8];
+  }
+  // the long rows: one per sub-group, over its CSR range (spmm_ell_kernel's long path;
+  // 4-steps: for bf16 rows the same pair adds in the same order as its 8-steps -- two
+  // acc_bf16_pair per 4-step -- with half the loads live, no spills at 64 VGPRs)
+  for (int k = wave * RPW + sub; k < n_long; k += nw * RPW) {
+    const int row = long_rows[k];
+    const int e0 = ell[(size_t)row * 8 + 1], e1 = ell[(size_t)row * 8 + 2];
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    gather_sum<L, 1, 4>(col, X, e0, e1, ldx, f0, f0 < F, sub * L, sl, acc);
+    const float rs = rscale ? rscale[row] : 1.f;
+    float y[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) y[q] = f0 + q < F ? acc[q] * rs : 0.f;
-  *reinterpret_cast<uint4*>(Y + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
+    for (int q = 0; q < 8; ++q) y[q] = f0 + q < F ? acc[q] * rs : 0.f;
+    if (f0 < ldy) *reinterpret_cast<uint4*>(Y + (size_t)row * ldy + f0) = f32x8_to_bf16(y);
+  }
 }
 
 // ell image of a CSR for spmm_ell_kernel (one thread per row)
@@ -783,15 +780,14 @@ extern "C" int gnn_launch_spmm_ell(const int* ell, const int* col, const void* X
                                    int n_long, hipStream_t st) {
   if (F > 64 || ldx % 8 || ldy % 8 || F > ldx) return -3;
   if (n_rows <= 0) return 0;
-  static const int form = getenv("CGNN_ELL_FORM") ? atoi(getenv("CGNN_ELL_FORM")) : 1;   // A/B (temporary)
-  if (form == 1 && long_rows && n_x_rows * ldx * 2 < (1l << 31) && (long)n_rows * ldy * 2 < (1l << 31)) {
+  // the pipelined kernel addresses X and Y through buffer descriptors (32-bit offsets);
+  // larger tables (or a caller without the long-row list) take the one-shot kernel
+  if (long_rows && n_x_rows * ldx * 2 < (1l << 31) && (long)n_rows * ldy * 2 < (1l << 31)) {
     const int groups = (n_rows + 7) / 8;
     const int blocks = std::max(1, std::min((groups + 3) / 4, device_cus() * 8));
-    hipLaunchKernelGGL(spmm_ell_pipe_kernel, dim3(blocks), dim3(256), 0, st, ell, (const uint16_t*)X,
-                       (uint16_t*)Y, rscale, n_rows, F, ldx, ldy, (uint32_t)(n_x_rows * ldx * 2));
-    if (n_long > 0)
-      hipLaunchKernelGGL(spmm_ell_long_kernel, dim3((n_long + 31) / 32), dim3(256), 0, st, long_rows, n_long, ell,
-                         col, (const uint16_t*)X, (uint16_t*)Y, rscale, F, ldx, ldy);
+    hipLaunchKernelGGL(spmm_ell_pipe_kernel, dim3(blocks), dim3(256), 0, st, ell, col, long_rows, n_long,
+                       (const uint16_t*)X, (uint16_t*)Y, rscale, n_rows, F, ldx, ldy,
+                       (uint32_t)(n_x_rows * ldx * 2));
   } else {
     hipLaunchKernelGGL(spmm_ell_kernel, dim3((n_rows + 31) / 32), dim3(256), 0, st, ell, col, (const uint16_t*)X,
                        (uint16_t*)Y, rscale, n_rows, F, ldx, ldy);

@@ -147,11 +147,12 @@ def spmm_ell(img, col, X, F, rscale=None, out=None):
                                   out.shape[1], X.shape[0], img.long_rows.data_ptr(), img.n_long, _st(X))
         return out
     acc = torch.zeros(n, F, dtype=torch.float32)
+    short = ell[:, 0] != -2                    # a long row's slots hold its CSR range
     for u in range(8):
         j = ell[:, u].long()
-        ok = j >= 0
+        ok = (j >= 0) & short
         acc[ok] += X[j[ok], :F].float()
-    longr = (ell[:, 0] == -2).nonzero().flatten()
+    longr = (~short).nonzero().flatten()
     for i in longr.tolist():
         e0, e1 = int(ell[i, 1]), int(ell[i, 2])
         acc[i] = X[col[e0:e1].long(), :F].float().sum(0)

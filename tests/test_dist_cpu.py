@@ -481,3 +481,32 @@ def test_shared_partition_order_runs_once_and_broadcasts(world):
     for r in range(world):
         np.testing.assert_array_equal(out[r][0], ref)
         assert out[r][1] == ([0] if r == 0 else [])
+
+
+def _order_fail_worker(rank, world, port, out):
+    _init(rank, world, port)
+    from cgnn_amd.gnn import data
+
+    def broken(*a, **k):
+        raise MemoryError("partition pass failed on rank 0")
+
+    data.partition_order = broken
+    try:
+        data.shared_partition_order("ogbn-products", seed=3, scale=0.002)
+        out[rank] = "returned"
+    except MemoryError:
+        out[rank] = "MemoryError"
+    except RuntimeError as e:
+        out[rank] = "RuntimeError: " + str(e)[:60]
+    dist.destroy_process_group()
+
+
+def test_shared_partition_order_failure_raises_on_every_rank():
+    """a pass that raises on rank 0 makes every rank raise (status word ahead
+    of the broadcast) instead of leaving the other ranks blocked in the collective."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_order_fail_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+    assert out[0] == "MemoryError"
+    for r in (1, 2):
+        assert out[r].startswith("RuntimeError: broadcast_host_array: source rank 0"), out[r]
