@@ -36,10 +36,13 @@ travel -- a training halo negotiated once at setup, one all-to-all per epoch
 Evaluation aggregates every row, with the full halo from 4 ranks on (``halo``)
 and an all-gather of Z2 below that.  The backward all-gathers the compact G (train
 rows only, padded to the largest rank's count: 1/12 of Z2's bytes), plus one
-all-reduce of the ~40k gradient floats.  Each exchange runs asynchronously on
-RCCL's stream while the rank aggregates the edges whose source rows it owns;
-the remaining edges are added afterwards through an fp32 partial, and the next
-epoch's layer-1 SpMM (parameter-independent) overlaps the forward exchange.
+all-reduce of the ~40k gradient floats.  In training both exchanges run
+asynchronously on RCCL's stream beside one half each of the next epoch's layer-1
+SpMM (parameter-independent; rows [0, n/2) beside the forward's halo exchange,
+[n/2, n) beside the backward's all-gather), and each aggregation that needs them
+is then ONE pass: layer 2 over [Z2 rows | received rows] in one buffer, the
+backward over the whole train-column ELL image.  (Evaluation keeps the split
+local / remote aggregation through an fp32 partial.)
 """
 from __future__ import annotations
 
@@ -217,22 +220,17 @@ class GCNTrainer:
         self.gslot, self.rp_T, self.col_T, self.maxT = self._train_columns(g, per)
         self.Gc_loc = torch.zeros(self.maxT, self.ldc, **bf)
         self.Gc = torch.zeros(self.maxT * self.world, self.ldc, **bf) if self.multi else self.Gc_loc
+        # bwd_overlap (several ranks): the all-gather of the compact gradient runs while the
+        # second half of the next epoch's layer-1 aggregation is computed (False: blocking,
+        # the half runs after it).  The backward aggregation itself is always one pass
+        # over the whole train-column adjacency once G is complete -- round 5 split it
+        # into this rank's own train columns (overlapped) and the rest, through an fp32
+        # partial of every row: two launches and 2 x 59 MB of partial traffic per
+        # 1/8-size epoch (37.6 + 29.8 us against ~22 us unsplit, profiles/r06_multirank)
         self._bwd_overlap = self.multi and bool(bwd_overlap)
-        # the train-column adjacency's rows are short (~4 entries): on the GPU the unsplit
-        # backward aggregation reads them from an ELL image (ops.spmm_ell: two dependent
-        # round trips per row instead of three)
-        self._ell_T = None
-        if dev.type == "cuda" and not self._bwd_overlap:
-            self._ell_T = ops.ell_image(self.rp_T, self.col_T)
-        if self._bwd_overlap:
-            # backward aggregation split like the forward's: the edges to this rank's own
-            # train rows (slots [rank * maxT, + maxT), read straight from Gc_loc) run while
-            # the all-gather of the other ranks' compact gradients is in flight.  Default
-            # on: the 4-rank one-GPU rehearsal reproduces the serial schedule's loss bit
-            # for bit (profiles/r02_final/r4_ov{0,1}.log); bwd_overlap=False serialises
-            lo = self.rank * self.maxT
-            self.rpT_loc, self.colT_loc, self.rpT_rem, self.colT_rem = self._split_local(
-                lo, lo + self.maxT, self.rp_T, self.col_T)
+        # the train-column adjacency's rows are short (~4 entries): on the GPU the
+        # backward aggregation reads them from an ELL image (ops.spmm_ell)
+        self._ell_T = ops.ell_image(self.rp_T, self.col_T) if dev.type == "cuda" else None
         self.H1 = torch.zeros(self.npad, hidden, **bf)
         self.dH1 = torch.zeros(self.npad, hidden, **bf)
         self.W2b = torch.zeros(hidden, self.ldc, **bf)
@@ -272,6 +270,37 @@ class GCNTrainer:
         self._l1 = None
         if self._l2 is not None and l1_train_neighbours:
             self._l1 = self._train_neighbour_csr(g)
+        # several ranks: the next epoch's layer-1 aggregation (parameter-independent) runs
+        # in two row halves, the first beside the forward's layer-2 exchange, the second
+        # beside the backward's gradient all-gather; each half a CSR of its own (row
+        # pointers rebased, the columns a view)
+        self._ax_halves = None
+        if self.multi:
+            rp, col = self._l1 if self._l1 is not None else (self.rowptr, self.col)
+            h = self.nloc // 2
+            self._ax_halves = []
+            for a, b in ((0, h), (h, self.nloc)):
+                e0, e1 = int(rp[a]), int(rp[b])
+                self._ax_halves.append((a, b, (rp[a:b + 1] - e0).contiguous(), col[e0:e1]))
+        # several ranks, training halo: layer 2 in ONE pass after the exchange -- the
+        # exchange lands right behind this rank's Z2 rows (Z2ext = [Z2loc | received rows])
+        # and the train rows' columns index that buffer (local c -> c - r0, remote ->
+        # per + its position in the plan).  Round 5 aggregated the local edges into an
+        # fp32 partial while the exchange was in flight: one more launch without the
+        # long-row split of spmm_ce (47.7 us against ~10 us, profiles/r06_multirank); the
+        # exchange is now covered by the first half of the next epoch's layer-1 SpMM.
+        self.Z2ext = None
+        l2 = self._l2
+        if l2 is not None and l2.plan is not None:
+            R = max(sum(l2.plan.recv_splits), 1)
+            self.Z2ext = torch.zeros(per + R, self.ldc, **bf)
+            self.Z2loc = self.Z2ext[:per]         # (the evaluation's exchange buffers stay separate)
+            l2.plan.Zrecv = self.Z2ext[per:per + R]
+            c = l2.col.long()
+            loc = (c >= r0) & (c < r1)
+            need = l2.plan.need
+            rem = torch.searchsorted(need, c).clamp_max(max(need.numel() - 1, 0))
+            l2.col_ext = torch.where(loc, c - r0, per + rem).to(torch.int32).contiguous()
         self._async = None                 # collectives overlapped? (decided at first use)
         self.epoch = 0
         self.last_stats = None
@@ -468,6 +497,12 @@ class GCNTrainer:
         rp, col = self._l1 if (train and self._l1 is not None) else (self.rowptr, self.col)
         ops.spmm(rp, col, self.Xs, self.F, rscale=self.dinv, out=out, unit_col=self.F)
 
+    def _aggregate_half(self, k):
+        """Rows of half ``k`` of the next epoch's layer-1 aggregation, into AX_next."""
+        a, b, rp, col = self._ax_halves[k]
+        if b > a:
+            ops.spmm(rp, col, self.Xs, self.F, rscale=self.dinv[a:b], out=self.AX_next[a:b], unit_col=self.F)
+
     def forward(self, train: bool):
         n, F, C = self.nloc, self.F, self.C
         H1 = self.H1[:n]
@@ -494,17 +529,24 @@ class GCNTrainer:
             torch.mul(y2, self.dinv[:, None], out=y2)
             self.Z2loc[:n] = y2.to(torch.bfloat16)
         l2 = self._l2 if train else None          # train rows only (see __init__)
-        if self.multi:
-            # the Z2 exchange is the epoch's one large transfer (up to [n, 48] bf16, 7/8
-            # of it inbound at 8 ranks): the rank-local layer-2 edges and, in training, the
-            # next epoch's layer-1 aggregation (parameter-independent) run while it is in flight
+        if self.multi and l2 is not None and l2.plan is not None:
+            # training halo: the exchange fills Z2ext behind the local rows while the first
+            # half of the next epoch's layer-1 aggregation runs; then one layer-2 pass
+            work, _ = self._exchange_z2(l2.plan)
+            self._aggregate_half(0)
+            work.wait()
+            rp, col, init, zsrc = l2.rp, l2.col_ext, None, self.Z2ext
+        elif self.multi:
+            # the Z2 exchange (up to [n, 48] bf16, 7/8 of it inbound at 8 ranks): the
+            # rank-local layer-2 edges and, in training, the first half of the next epoch's
+            # layer-1 aggregation run while it is in flight
             work, zsrc = self._exchange_z2(l2.plan if l2 is not None else None)
             if l2 is not None:
                 ops.spmm(l2.rp_loc, l2.col_loc, self.Z2loc, C, out=l2.part, out_dtype=torch.float32)
             else:
                 ops.spmm(self.rp_loc, self.col_loc, self.Z2loc, C, out=self.part, out_dtype=torch.float32)
             if train:
-                self._aggregate_features(self.AX_next, True)
+                self._aggregate_half(0)
             work.wait()
             if l2 is not None:
                 rp, col, init = l2.rp_rem, l2.col_rem, l2.part
@@ -526,18 +568,20 @@ class GCNTrainer:
 
     def backward(self, stats):
         n, F, C = self.nloc, self.F, self.C
-        if self.multi and self._bwd_overlap:
-            work = self._collective(torch.distributed.all_gather_into_tensor, self.Gc, self.Gc_loc)
-            ops.spmm(self.rpT_loc, self.colT_loc, self.Gc_loc, C, out=self.part, out_dtype=torch.float32)
-            work.wait()
-            ops.spmm(self.rpT_rem, self.colT_rem, self.Gc, C, rscale=self.dinv, out=self.dY2, init=self.part)
-        else:
-            if self.multi:
-                torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc)
-            if self._ell_T is not None:
-                ops.spmm_ell(self._ell_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
+        if self.multi:
+            # the compact gradients of every rank; the second half of the next epoch's
+            # layer-1 aggregation runs beside the all-gather (bwd_overlap) or after it
+            if self._bwd_overlap:
+                work = self._collective(torch.distributed.all_gather_into_tensor, self.Gc, self.Gc_loc)
+                self._aggregate_half(1)
+                work.wait()
             else:
-                ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
+                torch.distributed.all_gather_into_tensor(self.Gc, self.Gc_loc)
+                self._aggregate_half(1)
+        if self._ell_T is not None:
+            ops.spmm_ell(self._ell_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
+        else:
+            ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
         self.gb2.copy_(stats[4:4 + C])
         if self.fused_bwd:
             if self._grad_index is None:
