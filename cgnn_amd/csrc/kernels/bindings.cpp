@@ -101,6 +101,7 @@ int gnn_launch_gat_row_ce(const float*, int, const float*, int, const int*, cons
 int gnn_launch_gat_pack_grad(const float*, const float*, const float*, int, int, void*, int, long, hipStream_t);
 int gnn_launch_halo_rows(const void*, long, const long*, void*, long, const long*, long, int, int, hipStream_t);
 long gnn_sample_blocks_scratch(int, int, const int*, const int*);
+long gnn_sample_flag_bytes(int);
 int gnn_launch_sample_blocks(const int*, const int*, int, const int*, int, int, const int*, const int*, int* const*,
                              float* const*, int* const*, int* const*, int* const*, int* const*, int* const*,
                              int* const*, int*, uint8_t*, int*, int*, uint32_t, uint32_t, uint32_t, hipStream_t,
@@ -418,6 +419,7 @@ PYBIND11_MODULE(_hip, m) {
     chk(gnn_launch_halo_rows(Pt<const void>(src), sp, Pt<const long>(sidx), Pt<void>(dst), dp, Pt<const long>(didx),
                              rows, words, mode, S(st)), "gnn_halo_rows");
   });
+  m.def("gnn_sample_flag_bytes", &gnn_sample_flag_bytes);
   m.def("gnn_sample_blocks_scratch", [](int n, std::vector<int> fan, std::vector<int> nd_max) {
     if (fan.size() != nd_max.size()) throw std::runtime_error("gnn_sample_blocks_scratch: list lengths differ");
     return gnn_sample_blocks_scratch(n, (int)fan.size(), fan.data(), nd_max.data());

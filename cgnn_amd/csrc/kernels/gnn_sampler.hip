@@ -24,8 +24,9 @@ template <int MAXF>
 __global__ __launch_bounds__(256) void sample_neighbors_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const int* __restrict__ nodes, int n,
     int fanout, const int* __restrict__ out_ptr, int* __restrict__ out_col, uint32_t k0, uint32_t k1,
-    uint32_t salt, const int* __restrict__ n_dev) {
-  // n_dev (optional): the row count lives in device memory (the grid covers an upper bound)
+    uint32_t salt, const int* __restrict__ n_dev, uint8_t* __restrict__ flag) {
+  // n_dev (optional): the row count lives in device memory (the grid covers an upper bound);
+  // flag (optional): flag[pick] = 1 for every pick (the pipeline's source marks)
   if (n_dev) n = *n_dev;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -33,7 +34,11 @@ __global__ __launch_bounds__(256) void sample_neighbors_kernel(
   const int s = rowptr[v], deg = rowptr[v + 1] - s;
   int* dst = out_col + out_ptr[i];
   if (fanout < 0 || deg <= fanout) {
-    for (int k = 0; k < deg; ++k) dst[k] = col[s + k];
+    for (int k = 0; k < deg; ++k) {
+      const int c = col[s + k];
+      dst[k] = c;
+      if (flag) flag[c] = 1;
+    }
     return;
   }
   int sel[MAXF];
@@ -47,7 +52,11 @@ __global__ __launch_bounds__(256) void sample_neighbors_kernel(
     for (int q = 0; q < m; ++q) dup |= (sel[q] == t);
     sel[m] = dup ? j : t;
   }
-  for (int k = 0; k < fanout; ++k) dst[k] = col[s + sel[k]];
+  for (int k = 0; k < fanout; ++k) {
+    const int c = col[s + sel[k]];
+    dst[k] = c;
+    if (flag) flag[c] = 1;
+  }
 }
 
 extern "C" int gnn_launch_sample_neighbors(const int* rowptr, const int* col, const int* nodes, int n, int fanout,
@@ -57,10 +66,10 @@ extern "C" int gnn_launch_sample_neighbors(const int* rowptr, const int* col, co
   dim3 grid((n + 255) / 256), block(256);
   if (fanout <= 16)
     hipLaunchKernelGGL((sample_neighbors_kernel<16>), grid, block, 0, st, rowptr, col, nodes, n, fanout, out_ptr,
-                       out_col, k0, k1, salt, (const int*)nullptr);
+                       out_col, k0, k1, salt, (const int*)nullptr, (uint8_t*)nullptr);
   else if (fanout <= 64)
     hipLaunchKernelGGL((sample_neighbors_kernel<64>), grid, block, 0, st, rowptr, col, nodes, n, fanout, out_ptr,
-                       out_col, k0, k1, salt, (const int*)nullptr);
+                       out_col, k0, k1, salt, (const int*)nullptr, (uint8_t*)nullptr);
   else
     return -3;
   return (int)hipGetLastError();
@@ -73,54 +82,29 @@ extern "C" int gnn_launch_sample_neighbors(const int* rowptr, const int* col, co
 // enqueues all levels at once and learns the sizes with ONE copy at the end --
 // on a side stream, while the previous batch trains.
 //
-// Level l (destinations = seeds for l = 0, else the sources of level l - 1):
-//   count_scan    cnt = min(deg, fanout), exclusive scan -> rowptr, 1 / cnt,
-//                 total picks                                   (one block)
-//   sample        Floyd picks (sample_neighbors_kernel, device row count)
-//   mark          flag[pick] = 1
+// Level l (destinations = seeds for l = 0, else the sources of level l - 1), 7
+// launches, 11 with the transposed CSR (16 before round 6):
+//   count_scan    cnt = min(deg, fanout) -> per-block sums, then the exclusive scan
+//                 -> rowptr, 1 / cnt, total picks: every block of the second pass sums
+//                 its predecessors' block sums itself (at most a few hundred), so no
+//                 single-block middle pass
+//   sample        Floyd picks (sample_neighbors_kernel, device row count), marking
+//                 flag[pick] = 1 as they are written
 //   dst_fix       flag[dst] = 0, map[dst] = i, src[i] = dst
-//   flag_scan     per 4096-id block counts, scan of the block counts (one
-//                 block; n_src = n_dst + new sources), then compaction: the new
-//                 sources in increasing id order -> src[n_dst + k], map, flag = 0
-//   relabel       local[e] = map[pick[e]]
-//   transpose     (blocks the backward scatters through) histogram, scan,
+//   flag_scan     per 4096-id block counts (16 flags per thread), then compaction
+//                 (each block sums its predecessors' counts; n_src = n_dst + new
+//                 sources): the new sources in increasing id order -> src[n_dst + k],
+//                 map, flag = 0
+//   relabel       local[e] = map[pick[e]] (+ the transposed CSR's histogram)
+//   transpose     (blocks the backward scatters through) scan of the histogram,
 //                 per-destination scatter, per-bucket insertion sort: the
 //                 transposed CSR in increasing destination order (deterministic)
 // No state needs resetting between levels or batches: every flag set is cleared
 // by dst_fix / compaction, and map entries are only read for ids set this level.
 // ============================================================================
 namespace {
-constexpr int SCAN_T = 1024;
 constexpr int FLAG_BLK = 4096;
 
-// exclusive scan of v(i), i < n, by one block (thread t owns a contiguous chunk);
-// out[i] = prefix, out[n] = total; returns nothing (total also in *total if given)
-template <class V>
-__device__ void block_scan(int n, V v, int* __restrict__ out, int* __restrict__ total) {
-  __shared__ int part[SCAN_T];
-  const int t = threadIdx.x;
-  const int chunk = (n + SCAN_T - 1) / SCAN_T;
-  const int a = min(n, t * chunk), b = min(n, a + chunk);
-  int s = 0;
-  for (int i = a; i < b; ++i) s += v(i);
-  part[t] = s;
-  __syncthreads();
-  for (int off = 1; off < SCAN_T; off <<= 1) {          // Hillis-Steele inclusive scan
-    const int x = t >= off ? part[t - off] : 0;
-    __syncthreads();
-    part[t] += x;
-    __syncthreads();
-  }
-  int run = part[t] - s;                               // exclusive prefix of this chunk
-  for (int i = a; i < b; ++i) {
-    out[i] = run;
-    run += v(i);
-  }
-  if (t == SCAN_T - 1) {
-    out[n] = part[t];
-    if (total) *total = part[t];
-  }
-}
 }  // namespace
 
 // ---- multi-block exclusive scans with a device-side length (grid over an upper bound):
@@ -181,28 +165,29 @@ __global__ __launch_bounds__(256) void sb_scanA_kernel(const int* __restrict__ r
   if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(SCAN_T) void sb_scanB_kernel(const int* __restrict__ bsum, int n_host,
-                                                          const int* __restrict__ n_dev, int* __restrict__ boff,
-                                                          int* __restrict__ out, int* __restrict__ total) {
-  __shared__ int tot;
-  const int n = n_dev ? *n_dev : n_host;
-  const int nb = (n + SB - 1) / SB;
-  auto v = [&](int i) { return bsum[i]; };
-  block_scan(nb, v, boff, &tot);
+// sum of v over the block (every thread gets it); sh: 4 ints of shared memory
+__device__ __forceinline__ int block_sum256(int v, int* sh) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  __syncthreads();                              // sh may still be read by a previous use
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    out[n] = tot;
-    if (total) *total = tot;
-  }
+  return sh[0] + sh[1] + sh[2] + sh[3];
 }
 
-__global__ __launch_bounds__(256) void sb_scanC_kernel(const int* __restrict__ vals, const int* __restrict__ boff,
-                                                       int n_host, const int* __restrict__ n_dev,
-                                                       int* __restrict__ out) {
-  __shared__ int shw[4];
+// second pass of the scan: block b's offset is the sum of bsum[0..b) (each block adds its
+// predecessors' sums itself), then the block-local scan of vals; the last block with data
+// (block 0 when n == 0) writes out[n] = total and *total
+__global__ __launch_bounds__(256) void sb_scan_fin_kernel(const int* __restrict__ vals, const int* __restrict__ bsum,
+                                                          int n_host, const int* __restrict__ n_dev,
+                                                          int* __restrict__ out, int* __restrict__ total) {
+  __shared__ int shw[4], shr[4];
   const int n = n_dev ? *n_dev : n_host;
   const int base = blockIdx.x * SB;
-  if (base >= n) return;
+  if (blockIdx.x > 0 && base >= n) return;      // uniform per block
+  int pre = 0;
+  for (int q = threadIdx.x; q < (int)blockIdx.x; q += 256) pre += bsum[q];
+  pre = block_sum256(pre, shr);
   int v[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -210,19 +195,18 @@ __global__ __launch_bounds__(256) void sb_scanC_kernel(const int* __restrict__ v
     v[q] = i < n ? vals[i] : 0;
   }
   int tot;
-  int run = boff[blockIdx.x] + block_excl_scan4(v[0], v[1], v[2], v[3], &tot, shw);
+  int run = pre + block_excl_scan4(v[0], v[1], v[2], v[3], &tot, shw);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int i = base + 4 * threadIdx.x + q;
     if (i < n) out[i] = run;
     run += v[q];
   }
-}
-
-__global__ __launch_bounds__(256) void sb_mark_kernel(const int* __restrict__ picks, const int* __restrict__ total,
-                                                      uint8_t* __restrict__ flag) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < *total) flag[picks[e]] = 1;
+  const int last = n > 0 ? (n - 1) / SB : 0;
+  if ((int)blockIdx.x == last && threadIdx.x == 0) {
+    out[n] = pre + tot;
+    if (total) *total = pre + tot;
+  }
 }
 
 __global__ __launch_bounds__(256) void sb_dst_fix_kernel(const int* __restrict__ nodes, int n_host,
@@ -237,71 +221,62 @@ __global__ __launch_bounds__(256) void sb_dst_fix_kernel(const int* __restrict__
   src[i] = v;
 }
 
-__global__ __launch_bounds__(256) void sb_flag_count_kernel(const uint8_t* __restrict__ flag, int n,
+// 0/1 flag bytes of a word, summed
+__device__ __forceinline__ int flag_sum4(uint32_t w) { return (int)((w * 0x01010101u) >> 24); }
+
+// per 4096-id block: the count of set flags (16 flags per thread, one 16-B load; the flag
+// array is padded to whole blocks, gnn_sample_flag_bytes)
+__global__ __launch_bounds__(256) void sb_flag_count_kernel(const uint8_t* __restrict__ flag,
                                                             int* __restrict__ bcount) {
-  __shared__ int ws[4];
-  const int base = blockIdx.x * FLAG_BLK;
-  int s = 0;
-  for (int i = base + threadIdx.x; i < min(n, base + FLAG_BLK); i += 256) s += flag[i];
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) bcount[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+  __shared__ int sh[4];
+  const uint4 w = reinterpret_cast<const uint4*>(flag + (size_t)blockIdx.x * FLAG_BLK)[threadIdx.x];
+  const int c = block_sum256(flag_sum4(w.x) + flag_sum4(w.y) + flag_sum4(w.z) + flag_sum4(w.w), sh);
+  if (threadIdx.x == 0) bcount[blockIdx.x] = c;
 }
 
-// exclusive scan of the block counts; n_src = n_dst + new sources
-__global__ __launch_bounds__(SCAN_T) void sb_block_scan_kernel(const int* __restrict__ bcount, int nb,
-                                                               int* __restrict__ boff, int n_dst_host,
-                                                               const int* __restrict__ n_dst_dev,
-                                                               int* __restrict__ n_src) {
-  __shared__ int tot;
-  auto v = [&](int i) { return bcount[i]; };
-  block_scan(nb, v, boff, &tot);
-  __syncthreads();
-  if (threadIdx.x == 0) *n_src = (n_dst_dev ? *n_dst_dev : n_dst_host) + tot;
-}
-
-// the new sources of each 4096-id block in increasing id order (wave ballots)
-__global__ __launch_bounds__(256) void sb_compact_kernel(uint8_t* __restrict__ flag, int n,
-                                                         const int* __restrict__ boff, int n_dst_host,
-                                                         const int* __restrict__ n_dst_dev, int* __restrict__ map,
-                                                         int* __restrict__ src) {
-  __shared__ int wsum[4];
+// the new sources of each 4096-id block in increasing id order: 16 consecutive ids per
+// thread, the block's offset the sum of its predecessors' counts (no single-block scan
+// pass); the last block writes n_src = n_dst + new sources
+__global__ __launch_bounds__(256) void sb_compact_kernel(uint8_t* __restrict__ flag, const int* __restrict__ bcount,
+                                                         int n_dst_host, const int* __restrict__ n_dst_dev,
+                                                         int* __restrict__ map, int* __restrict__ src,
+                                                         int* __restrict__ n_src) {
+  __shared__ int shw[4], shr[4];
   const int nd = n_dst_dev ? *n_dst_dev : n_dst_host;
-  const int base = blockIdx.x * FLAG_BLK;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int run = boff[blockIdx.x];
-  for (int c0 = base; c0 < min(n, base + FLAG_BLK); c0 += 256) {
-    const int i = c0 + threadIdx.x;
-    const bool f = i < n && flag[i];
-    const unsigned long long bal = __ballot(f);
-    const int before = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wsum[w] = __popcll(bal);
-    __syncthreads();
-    int woff = 0;
-    for (int q = 0; q < w; ++q) woff += wsum[q];
-    const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    if (f) {
-      const int k = run + woff + before;
-      map[i] = nd + k;
-      src[nd + k] = i;
-      flag[i] = 0;
+  int pre = 0;
+  for (int q = threadIdx.x; q < (int)blockIdx.x; q += 256) pre += bcount[q];
+  pre = block_sum256(pre, shr);
+  uint4* wp = reinterpret_cast<uint4*>(flag + (size_t)blockIdx.x * FLAG_BLK) + threadIdx.x;
+  const uint4 w = *wp;
+  const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+  const int c0 = flag_sum4(w.x), c1 = flag_sum4(w.y), c2 = flag_sum4(w.z), c3 = flag_sum4(w.w);
+  int tot;
+  int k = pre + block_excl_scan4(c0, c1, c2, c3, &tot, shw);
+  if (c0 + c1 + c2 + c3) {
+    const int i0 = blockIdx.x * FLAG_BLK + 16 * threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if ((ww[q >> 2] >> (8 * (q & 3))) & 0xffu) {
+        map[i0 + q] = nd + k;
+        src[nd + k] = i0 + q;
+        ++k;
+      }
     }
-    run += tot;
-    __syncthreads();
+    *wp = make_uint4(0u, 0u, 0u, 0u);
   }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_src = nd + pre + tot;
 }
 
+// local[e] = map[pick[e]]; cnt (optional): the transposed CSR's histogram of local ids
 __global__ __launch_bounds__(256) void sb_relabel_kernel(const int* __restrict__ picks, const int* __restrict__ total,
-                                                         const int* __restrict__ map, int* __restrict__ local) {
+                                                         const int* __restrict__ map, int* __restrict__ local,
+                                                         int* __restrict__ cnt) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < *total) local[e] = map[picks[e]];
-}
-
-__global__ __launch_bounds__(256) void sb_hist_kernel(const int* __restrict__ local, const int* __restrict__ total,
-                                                      int* __restrict__ cnt) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < *total) atomicAdd(&cnt[local[e]], 1);
+  if (e < *total) {
+    const int l = map[picks[e]];
+    local[e] = l;
+    if (cnt) atomicAdd(&cnt[l], 1);
+  }
 }
 
 __global__ __launch_bounds__(256) void sb_scatter_kernel(const int* __restrict__ optr, const int* __restrict__ local,
@@ -353,6 +328,10 @@ extern "C" long gnn_sample_blocks_scratch(int n, int L, const int* fan, const in
   return 2 * nb + 2 + 2 * sbmax + vmax;
 }
 
+// bytes of the pipeline's flag array for n ids: whole 4096-id blocks (the flag passes
+// read 16 bytes per thread without a bound check; the padding is never set)
+extern "C" long gnn_sample_flag_bytes(int n) { return ((long)n + FLAG_BLK) / FLAG_BLK * FLAG_BLK; }
+
 // One level per entry of the arrays (L levels): nd_max[l] bounds the destinations,
 // fan[l] the fanout; dst of level 0 = seeds (n_seeds on the host), of level l > 0 =
 // src[l - 1] with its device count counts[2 (l - 1)].  counts[2 l] = n_src of level
@@ -372,8 +351,7 @@ extern "C" int gnn_launch_sample_blocks(const int* rowptr, const int* col, int n
   for (int l = 0; l < L; ++l) vmax = std::max(vmax, std::min<long>((long)nd_max[l] * (fan[l] + 1), (long)n) + 1);
   const long sbmax = (vmax + SB - 1) / SB + 1;
   int* sbsum = bscratch + 2 * nb + 2;
-  int* sboff = sbsum + sbmax;
-  int* svals = sboff + sbmax;
+  int* svals = sbsum + 2 * sbmax;
   for (int l = 0; l < L; ++l) {
     const int fo = fan[l];
     if (fo < 1 || fo > 64) return -3;
@@ -387,33 +365,28 @@ extern "C" int gnn_launch_sample_blocks(const int* rowptr, const int* col, int n
     const unsigned nbs = blocks_for(nd_max[l], SB);
     hipLaunchKernelGGL(sb_scanA_kernel, dim3(nbs), dim3(256), 0, st, rowptr, nodes, fo, inv_deg[l], (int*)nullptr,
                        ndh, nd_dev, svals, sbsum);
-    hipLaunchKernelGGL(sb_scanB_kernel, dim3(1), dim3(SCAN_T), 0, st, sbsum, ndh, nd_dev, sboff, optr[l], total);
-    hipLaunchKernelGGL(sb_scanC_kernel, dim3(nbs), dim3(256), 0, st, svals, sboff, ndh, nd_dev, optr[l]);
+    hipLaunchKernelGGL(sb_scan_fin_kernel, dim3(nbs), dim3(256), 0, st, svals, sbsum, ndh, nd_dev, optr[l], total);
     const uint32_t lsalt = salt * 16u + (uint32_t)l;
     if (fo <= 16)
       hipLaunchKernelGGL((sample_neighbors_kernel<16>), dim3(blocks_for(nd_max[l])), dim3(256), 0, st, rowptr, col,
-                         nodes, ndh, fo, optr[l], picks[l], k0, k1, lsalt, nd_dev);
+                         nodes, ndh, fo, optr[l], picks[l], k0, k1, lsalt, nd_dev, flag);
     else
       hipLaunchKernelGGL((sample_neighbors_kernel<64>), dim3(blocks_for(nd_max[l])), dim3(256), 0, st, rowptr, col,
-                         nodes, ndh, fo, optr[l], picks[l], k0, k1, lsalt, nd_dev);
-    hipLaunchKernelGGL(sb_mark_kernel, dim3(blocks_for(pmax)), dim3(256), 0, st, picks[l], total, flag);
+                         nodes, ndh, fo, optr[l], picks[l], k0, k1, lsalt, nd_dev, flag);
     hipLaunchKernelGGL(sb_dst_fix_kernel, dim3(blocks_for(nd_max[l])), dim3(256), 0, st, nodes, ndh, nd_dev, flag,
                        map, src[l]);
-    hipLaunchKernelGGL(sb_flag_count_kernel, dim3(nb), dim3(256), 0, st, flag, n, bscratch);
-    hipLaunchKernelGGL(sb_block_scan_kernel, dim3(1), dim3(SCAN_T), 0, st, bscratch, nb, bscratch + nb + 1, ndh,
-                       nd_dev, nsrc);
-    hipLaunchKernelGGL(sb_compact_kernel, dim3(nb), dim3(256), 0, st, flag, n, bscratch + nb + 1, ndh, nd_dev, map,
-                       src[l]);
-    hipLaunchKernelGGL(sb_relabel_kernel, dim3(blocks_for(pmax)), dim3(256), 0, st, picks[l], total, map, local[l]);
+    hipLaunchKernelGGL(sb_flag_count_kernel, dim3(nb), dim3(256), 0, st, flag, bscratch);
+    hipLaunchKernelGGL(sb_compact_kernel, dim3(nb), dim3(256), 0, st, flag, bscratch, ndh, nd_dev, map, src[l],
+                       nsrc);
+    hipLaunchKernelGGL(sb_relabel_kernel, dim3(blocks_for(pmax)), dim3(256), 0, st, picks[l], total, map, local[l],
+                       rp_t[l] ? cnt_t[l] : (int*)nullptr);
     if (rp_t[l]) {
       const long smax = std::min<long>((long)nd_max[l] * (fo + 1), (long)n);
-      hipLaunchKernelGGL(sb_hist_kernel, dim3(blocks_for(pmax)), dim3(256), 0, st, local[l], total, cnt_t[l]);
       const unsigned nbt = blocks_for(smax, SB);
       hipLaunchKernelGGL(sb_scanA_kernel, dim3(nbt), dim3(256), 0, st, (const int*)nullptr, (const int*)nullptr, 0,
                          (float*)nullptr, cnt_t[l], 0, nsrc, svals, sbsum);
-      hipLaunchKernelGGL(sb_scanB_kernel, dim3(1), dim3(SCAN_T), 0, st, sbsum, 0, nsrc, sboff, rp_t[l],
+      hipLaunchKernelGGL(sb_scan_fin_kernel, dim3(nbt), dim3(256), 0, st, svals, sbsum, 0, nsrc, rp_t[l],
                          (int*)nullptr);
-      hipLaunchKernelGGL(sb_scanC_kernel, dim3(nbt), dim3(256), 0, st, svals, sboff, 0, nsrc, rp_t[l]);
       hipLaunchKernelGGL(sb_scatter_kernel, dim3(blocks_for(nd_max[l])), dim3(256), 0, st, optr[l], local[l], ndh,
                          nd_dev, rp_t[l], cnt_t[l], col_t[l]);
       hipLaunchKernelGGL(sb_bucket_sort_kernel, dim3(blocks_for(smax)), dim3(256), 0, st, rp_t[l], nsrc, col_t[l],

@@ -251,8 +251,9 @@ class SampledBatch:
 
 class PipelinedSampler:
     """The whole multi-level sampling of a mini-batch as ONE native call
-    (``gnn_sample_blocks``: ~13 HIP kernels per level, device-side row counts, no
-    host synchronisation inside) on a side stream, over ``slots``
+    (``gnn_sample_blocks``: 7 HIP kernels per level, 11 with the transposed CSR --
+    16 before round 6 -- device-side row counts, no host synchronisation inside) on a
+    side stream, over ``slots``
     buffers: batch k + 1 (and k + 2) is sampled while batch k trains.  The level
     sizes reach the host through mapped host memory a kernel writes (``publish``;
     else one pinned copy per batch).  Same draws and relabelling as
@@ -268,7 +269,7 @@ class PipelinedSampler:
 
     ``threaded`` (default): a native worker thread owns the side stream and issues the
     launches (``gnn_sw_*`` in gnn_sampler.hip); the Python thread only posts the batch,
-    so the ~40 sampling launches no longer add to the host time of the training loop.
+    so the ~30 sampling launches no longer add to the host time of the training loop.
 
     Capturing each slot's pipeline as a hipGraph (seed count and salt read on the
     device) was tried in round 5: the uncaptured launches pass the bitwise test, the
@@ -292,7 +293,8 @@ class PipelinedSampler:
         L = len(self.fanouts)
         need_t = [l < L - 1 for l in range(L)]
         self.slots = [_Slot(self.dev, self.n, self.batch, self.fanouts, need_t, self.publish) for _ in range(slots)]
-        self.flag = torch.zeros(self.n + 1, dtype=torch.uint8, device=self.dev)
+        # padded to whole 4096-id blocks (the flag passes read 16 flags per thread)
+        self.flag = torch.zeros(native.hip().gnn_sample_flag_bytes(self.n), dtype=torch.uint8, device=self.dev)
         self.map = torch.zeros(self.n + 1, dtype=torch.int32, device=self.dev)
         ns = native.hip().gnn_sample_blocks_scratch(self.n, self.fanouts, self.slots[0].nd_max)
         self.bscratch = torch.zeros(ns, dtype=torch.int32, device=self.dev)
