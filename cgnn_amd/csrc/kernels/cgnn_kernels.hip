@@ -547,27 +547,52 @@ __global__ __launch_bounds__(BS) void gen_bwd_kernel(
 // ============================================================================
 // K5: TF1 Adam with fused fixed-order reduction of the G gradient slabs.
 //   lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t);  theta -= lr_t * m / (sqrt(v) + eps)
-// grid = (ceil(P/256), R)
+// grid = (ceil(P/1024), R): four consecutive parameters per thread (P % 4 == 0,
+// pack_programs), the slabs read as 16-B loads, eight in flight per thread (the round-5
+// form -- one parameter per thread, one dependent load per slab -- ran at ~1 TB/s:
+// 88 us per step on the 200-variable orientation slice).  Per parameter the same adds in
+// the same order: bitwise the same update.
 // ============================================================================
 __global__ __launch_bounds__(256) void adam_tf1_kernel(
     float* __restrict__ params, float* __restrict__ m, float* __restrict__ v,
     const float* __restrict__ gpart, int G, const int* __restrict__ prog, int prog_stride, int P,
     const int* __restrict__ step_base, int step_off, float lr, float beta1, float beta2, float eps) {
   const int r = blockIdx.y;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
   const int Pr = prog[(size_t)r * prog_stride + 1];
-  if (p >= Pr) return;
-  float g = 0.f;
-  const float* gp = gpart + (size_t)r * G * P + p;
-  for (int k = 0; k < G; ++k) g += gp[(size_t)k * P];
+  if (p0 >= Pr) return;
+  const float4* gp = reinterpret_cast<const float4*>(gpart + (size_t)r * G * P + p0);
+  const int P4 = P >> 2;
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+  for (int k = 0; k < G; ++k) {
+    const float4 x = gp[(size_t)k * P4];
+    g.x += x.x;
+    g.y += x.y;
+    g.z += x.z;
+    g.w += x.w;
+  }
   const float tstep = (float)(step_base[1] + step_off + 1);   // optimizer step count
   const float lr_t = lr * sqrtf(1.f - powf(beta2, tstep)) / (1.f - powf(beta1, tstep));
-  const size_t idx = (size_t)r * P + p;
-  const float mm = beta1 * m[idx] + (1.f - beta1) * g;
-  const float vv = beta2 * v[idx] + (1.f - beta2) * g * g;
-  m[idx] = mm;
-  v[idx] = vv;
-  params[idx] -= lr_t * mm / (sqrtf(vv) + eps);
+  const size_t idx = (size_t)r * P + p0;
+  const float4 m0 = *reinterpret_cast<const float4*>(m + idx), v0 = *reinterpret_cast<const float4*>(v + idx);
+  const float4 t0 = *reinterpret_cast<const float4*>(params + idx);
+  const float gg[4] = {g.x, g.y, g.z, g.w}, mo[4] = {m0.x, m0.y, m0.z, m0.w}, vo[4] = {v0.x, v0.y, v0.z, v0.w};
+  float to[4] = {t0.x, t0.y, t0.z, t0.w}, mn[4], vn[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    mn[q] = beta1 * mo[q] + (1.f - beta1) * gg[q];
+    vn[q] = beta2 * vo[q] + (1.f - beta2) * gg[q] * gg[q];
+    if (p0 + q < Pr) {
+      to[q] -= lr_t * mn[q] / (sqrtf(vn[q]) + eps);
+    } else {                                  // padding parameters stay untouched
+      mn[q] = mo[q];
+      vn[q] = vo[q];
+    }
+  }
+  *reinterpret_cast<float4*>(m + idx) = make_float4(mn[0], mn[1], mn[2], mn[3]);
+  *reinterpret_cast<float4*>(v + idx) = make_float4(vn[0], vn[1], vn[2], vn[3]);
+  *reinterpret_cast<float4*>(params + idx) = make_float4(to[0], to[1], to[2], to[3]);
 }
 
 // Parameter init N(0, std^2) from Philox (weights AND biases, CGNN.py:71-74).
@@ -779,7 +804,8 @@ extern "C" int cgnn_launch_adam(float* params, float* m, float* v, const float* 
                                 const int* prog, int prog_stride, int P, const int* step_base,
                                 int step_off, float lr, float b1, float b2, float eps, int R,
                                 hipStream_t st) {
-  dim3 grid((P + 255) / 256, R), block(256);
+  if (P % 4) return -3;                       // pack_programs pads P to whole float4s
+  dim3 grid((P + 1023) / 1024, R), block(256);
   hipLaunchKernelGGL(adam_tf1_kernel, grid, block, 0, st, params, m, v, gpart, G, prog, prog_stride,
                      P, step_base, step_off, lr, b1, b2, eps);
   return (int)hipGetLastError();

@@ -196,7 +196,11 @@ class GCNTrainer:
         # AX/H1/dH1/dY2 padded with zero rows to a multiple of CHUNK for the split-K GEMMs)
         n = self.nloc
         self.npad = (n + CHUNK - 1) // CHUNK * CHUNK
-        self.AX = torch.zeros(self.npad, self.ldx, **bf)
+        # AX (the layer-1 aggregate: written once by the SpMM, streamed by the dense
+        # forward and backward, never gathered) packed to whole 16-B chunks of its F + 1
+        # columns: 208-B rows for ogbn-products instead of the gathered features' 256
+        self.ldax = _ru8(self.F + 1)
+        self.AX = torch.zeros(self.npad, self.ldax, **bf)
         # multi-GPU: the layer-1 aggregation of the NEXT epoch is computed into a second
         # buffer while the forward all-gather of Z2 is in flight (it does not depend on the
         # parameters), then the buffers swap; every epoch still performs its own SpMM
