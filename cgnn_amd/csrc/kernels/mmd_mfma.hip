@@ -320,7 +320,9 @@ __global__ __launch_bounds__(256) void mmd_mfma_kernel(
 //   G[i][d] += sum_j W[i][j] Z[j][d]    A = the lane's own 8 W values (k-slot e <->
 //      j = 4g + e for e < 4, 16 + 4g + e - 4 after; g = l>>4), B = Z^T through
 //      the transposed reads of rows 4g..4g+3 and 16+4g..16+4g+3.
-// No symmetric skipping here (every mode evaluates the whole pred-pred block).
+// Evaluation (loss only) skips the pred-pred tiles left of a row block's diagonal and
+// counts those right of it twice; training evaluates the whole pred-pred block (the
+// mirrored gradient would need a second, column-side accumulation).
 // ============================================================================
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef short s4v __attribute__((ext_vector_type(4)));
@@ -358,8 +360,13 @@ __global__ __launch_bounds__(512) void mmd_mfma16_kernel(
   __shared__ __attribute__((aligned(16))) float s_n[2][MT];
   __shared__ float s_red[W16];
 
-  const int rb = blockIdx.x, chunk = blockIdx.y, r = blockIdx.z;
-  const int n_chunks = gridDim.y, n_rb = gridDim.x;
+  // a model's (row block, chunk) blocks rotated by the model index: blocks are dealt
+  // round-robin over the 8 XCDs, and with 4 row blocks x 2 chunks the unrotated grid put
+  // every model's chunk 0 on XCDs 0-3 and chunk 1 on 4-7 -- so blocks of unequal length
+  // (the symmetric evaluation below) left half the chip idle at the end
+  const int n_chunks = gridDim.y, n_rb = gridDim.x, r = blockIdx.z;
+  const int lid = (int)((blockIdx.x + gridDim.x * blockIdx.y + blockIdx.z) % (gridDim.x * gridDim.y));
+  const int rb = lid % n_rb, chunk = lid / n_rb;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int i = row_begin + rb * (W16 * 16) + wave * 16 + li;
@@ -388,8 +395,18 @@ __global__ __launch_bounds__(512) void mmd_mfma16_kernel(
 
   const int TX = (N + MT - 1) / MT;
   const int ct = MODE == 2 ? TX : 2 * TX;
-  const int t_begin = chunk * tiles_per_chunk;
+  int t_begin = chunk * tiles_per_chunk;
   const int t_end = min(ct, t_begin + tiles_per_chunk);
+  // symmetric pred-pred block (loss only, all rows in this launch, a chunk of pred tiles
+  // only): the row block starts at its own diagonal tile; tiles right of its 128 x 128
+  // diagonal block count twice (each stands for its mirror, left of another block's
+  // diagonal), the diagonal block once
+  constexpr int RBT = W16 * 16 / MT;        // column tiles per row block
+  // (every chunk either all pred or all true tiles, so every skipped tile's mirror is
+  // counted by a symmetric block)
+  const bool sym = (MODE == 1 || MODE == 2) && row_begin == 0 && n_rows == N && t_end <= TX &&
+                   (MODE == 2 || TX % tiles_per_chunk == 0);
+  if (sym) t_begin = max(t_begin, RBT * rb);
 
   // staging: task k -> (column jj = task & 31, chunk c = task >> 5): 8 consecutive dims
   float stage[TPT][8];
@@ -496,7 +513,7 @@ __global__ __launch_bounds__(512) void mmd_mfma16_kernel(
         }
       }
     }
-    if (LOSS) lacc = fmaf(pred_part ? 1.f : -2.f, tl2.x + tl2.y, lacc);
+    if (LOSS) lacc = fmaf(pred_part ? (sym && tile >= RBT * (rb + 1) ? 2.f : 1.f) : -2.f, tl2.x + tl2.y, lacc);
 
     if (GRAD) {
       rowsum += rs2.x + rs2.y;

@@ -265,3 +265,42 @@ def test_exact_mmd_trainer_beyond_1024_matches_oracle():
     scores = dev.run(3, 2)
     np.testing.assert_allclose(dev.history(), np.array(ref.loss_history), rtol=3e-3, atol=1e-5)
     np.testing.assert_allclose(scores, ref_scores, rtol=3e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("N", [500, 130, 97])
+def test_wide_mmd_eval_symmetric_matches_full(N):
+    """The matrix-core MMD's evaluation (loss only: pred-pred tiles left of each row
+    block's diagonal skipped, those right of it counted twice, blocks rotated over the
+    XCDs per model) sums to the loss the training launch computes over every tile; the
+    true-true launch (also symmetric) against the fp64 oracle's constant term."""
+    from cgnn_amd import native
+    from cgnn_amd.engine.batch import mmd_mfma_geometry, padded_dim
+    hip = native.hip()
+    d, R = 200, 3
+    D = padded_dim(d)
+    g = torch.Generator().manual_seed(N)
+    P = torch.zeros(R, D, N)
+    T = torch.zeros(R, D, N)
+    P[:, :d] = torch.randn(R, d, N, generator=g) * 0.3
+    T[:, :d] = torch.randn(R, d, N, generator=g) * 0.3 + 0.05
+    P, T = P.cuda(), T.cuda()
+    pn, tn = (P * P).sum(1).contiguous(), (T * T).sum(1).contiguous()
+    rb, chunks, tpc = mmd_mfma_geometry(N, R)
+    st = torch.cuda.current_stream().cuda_stream
+    gradp = torch.empty(chunks, R, D, N, device="cuda")
+    full = torch.zeros(R, rb * chunks, device="cuda")
+    ev = torch.zeros(R, rb * chunks, device="cuda")
+    tt = torch.zeros(R, rb * chunks, device="cuda")
+    hip.mmd_mfma(0, D, P.data_ptr(), T.data_ptr(), pn.data_ptr(), tn.data_ptr(), gradp.data_ptr(),
+                 full.data_ptr(), N, R, chunks, tpc, 1.0, st)
+    hip.mmd_mfma(1, D, P.data_ptr(), T.data_ptr(), pn.data_ptr(), tn.data_ptr(), gradp.data_ptr(),
+                 ev.data_ptr(), N, R, chunks, tpc, 0.0, st)
+    hip.mmd_mfma(2, D, T.data_ptr(), T.data_ptr(), tn.data_ptr(), tn.data_ptr(), gradp.data_ptr(),
+                 tt.data_ptr(), N, R, chunks, tpc, 0.0, st)
+    np.testing.assert_allclose(ev.sum(1).cpu().numpy(), full.sum(1).cpu().numpy(), rtol=2e-5)
+    # the true-true sum of the seven-bandwidth kernel, fp64
+    Td = T[:, :d].double().cpu()
+    d2 = ((Td[:, :, :, None] - Td[:, :, None, :]) ** 2).sum(1)
+    from cgnn_amd.engine.reference import GAMMAS
+    ref = sum(torch.exp(-gm * d2) for gm in GAMMAS).sum((1, 2))
+    np.testing.assert_allclose(tt.sum(1).cpu().numpy(), ref.numpy(), rtol=1e-4)
