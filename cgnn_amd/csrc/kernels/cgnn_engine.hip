@@ -3,7 +3,8 @@
 //
 //   train step : gen_fwd -> mmd(train) -> loss_finalize -> gen_bwd -> adam
 //   eval step  : gen_fwd -> mmd(eval)  -> loss_finalize(accumulate)
-// (wide graphs: gen_fwd = gen_noise + gen_fwd_staged, gen_bwd = gen_bwd_staged)
+// (wide graphs: gen_fwd = gen_fwd_staged, which draws the step's noise itself, gen_bwd =
+// gen_bwd_staged)
 //
 // A chunk of `chunk` steps (step offsets baked in as literals) plus one
 // advance_step node is captured once per (kind, chunk) and replayed; the RNG
@@ -33,6 +34,9 @@ int cgnn_launch_gen_bwd(const int*, int, const float*, int, const float*, const 
 int cgnn_staged_tiles(int);
 int cgnn_launch_gen_noise(const int*, int, const uint32_t*, const int*, int, float*, int, int, int, int, int, int,
                           hipStream_t);
+int cgnn_launch_gen_fwd_staged_draw(const int*, int, const int*, int, const float*, int, const float*, float*, float*,
+                                    int, float*, int, int, int, int, int, int, int, hipStream_t, int, const uint32_t*,
+                                    const int*, int, int);
 int cgnn_launch_gen_fwd_staged(const int*, int, const int*, int, const float*, int, const float*, float*,
                                const float*, int, float*, int, int, int, int, int, int, int, hipStream_t, int);
 int cgnn_launch_gen_bwd_staged(const int*, int, const int*, int, const float*, int, const float*, const float*, int,
@@ -173,11 +177,11 @@ class Engine {
 
   void enqueue_gen_fwd(int off) {
     if (c_.staged) {
-      check(cgnn_launch_gen_noise(b_.prog, c_.prog_stride, b_.keys, b_.step, off, b_.noise, c_.NS, c_.N, c_.D,
-                                  c_.d_true, c_.R, 0, st_), "gen_noise");
-      check(cgnn_launch_gen_fwd_staged(b_.prog, c_.prog_stride, b_.sched, c_.sched_stride, b_.params, c_.P, b_.data,
-                                       b_.xhat, b_.noise, c_.NS, b_.xnorm, c_.N, c_.D, c_.d_true, c_.H, c_.max_in,
-                                       c_.R, c_.stage_w, st_, -1), "gen_fwd_staged");
+      // the forward draws the step's noise itself (and stores it for the backward)
+      check(cgnn_launch_gen_fwd_staged_draw(b_.prog, c_.prog_stride, b_.sched, c_.sched_stride, b_.params, c_.P,
+                                            b_.data, b_.xhat, b_.noise, c_.NS, b_.xnorm, c_.N, c_.D, c_.d_true, c_.H,
+                                            c_.max_in, c_.R, c_.stage_w, st_, -1, b_.keys, b_.step, off, 0),
+            "gen_fwd_staged");
     } else {
       check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
                                 b_.xnorm, b_.keys, b_.step, off, c_.N, c_.D, c_.H, c_.R, st_, 0), "gen_fwd");

@@ -70,12 +70,15 @@ __global__ __launch_bounds__(256) void gen_noise_kernel(const int* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------- forward
-template <int HC, bool XG>
+template <int HC, bool XG, bool DRAW>
 __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
     const int* __restrict__ prog, int ps, const int* __restrict__ sched, int ss,
     const float* __restrict__ params, int P, const float* __restrict__ data, float* __restrict__ xhat,
-    const float* __restrict__ noise, int NS, float* __restrict__ xnorm, int N, int D, int Dt, int H, int T,
-    int max_in) {
+    float* __restrict__ noise, int NS, float* __restrict__ xnorm, int N, int D, int Dt, int H, int T,
+    int max_in, const uint32_t* __restrict__ keys, const int* __restrict__ step_base, int step_off, int row0) {
+  // DRAW: the node and confounder noise is drawn here (gen_noise_kernel's draws, keyed
+  // the same) as the nodes consume it, and written to `noise` for the backward -- no
+  // separate noise launch, no noise read in the forward
   constexpr int HCS = (HC + 3) & ~3;      // weight-slab row stride (16-B aligned rows)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int W = blockDim.x >> 6;
@@ -91,8 +94,18 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
   const int* sc = sched + (size_t)r * ss;
   const float* th = params + (size_t)r * P;
   const float* dr = data + (size_t)r * D * N;
-  const float* nz = noise + (size_t)r * NS * N;
+  float* nz = noise + (size_t)r * NS * N;
   float* xr = xhat + (size_t)r * D * N;
+  uint32_t k0 = 0u, k1 = 0u, rstep = 0u;
+  if constexpr (DRAW) {
+    k0 = keys[2 * r];
+    k1 = keys[2 * r + 1];
+    rstep = (uint32_t)(step_base[0] + step_off);
+  }
+  auto own_noise = [&](int var) -> float {
+    if constexpr (DRAW) return rng_normal(k0, k1, (uint32_t)(row0 + nc), (uint32_t)var, rstep, RNG_NODE_NOISE);
+    else return nz[(size_t)var * N + nc];
+  };
   float* s_x = smem;                                        // [Dt][64] (LDS state)
   float* s_w = s_x + (XG ? 0 : (size_t)Dt * WAVE) + (size_t)wave * (max_in + 2) * HCS;   // this wave's weight rows
   auto xget = [&](int v) -> float { return XG ? xr[(size_t)v * N + nc] : s_x[v * WAVE + lane]; };
@@ -135,7 +148,7 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
       const Nd d0 = node_at(b + wave);
       if (d0.kind != KIND_OBS) {
         load_w(d0, 0, wnx);
-        enx = nz[(size_t)d0.var * N + nc];
+        enx = own_noise(d0.var);
       }
     }
     for (int i = b + wave; i < e; i += W) {
@@ -147,7 +160,7 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
           const Nd nx = node_at(i + W);
           if (nx.kind != KIND_OBS) {
             load_w(nx, 0, wnx);
-            enx = nz[(size_t)nx.var * N + nc];
+            enx = own_noise(nx.var);
           }
         }
         continue;
@@ -155,6 +168,7 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
       const int npar = cur.npar, paroff = cur.paroff, ncf = cur.ncf, cfoff = cur.cfoff, nin = cur.nin;
       const float* W1 = cur.W1;
       const float e_own = enx;
+      if (DRAW && valid) nz[(size_t)var * N + n] = e_own;           // for the backward
       float out = W1[(size_t)(nin + 2) * H];                       // b2
       for (int q0 = 0; q0 < H; q0 += HC) {
         // this chunk's weights (rows 0..nin+1, HC units) into the wave's slab
@@ -168,7 +182,7 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
           const Nd nx = node_at(i + W);
           if (nx.kind != KIND_OBS) {
             load_w(nx, 0, wnx);
-            enx = nz[(size_t)nx.var * N + nc];
+            enx = own_noise(nx.var);
           }
         }
 #pragma unroll
@@ -209,9 +223,19 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
         }
         for (int c0 = 0; c0 < ncf; c0 += 8) {
           float v[8];
+          if constexpr (DRAW) {
 #pragma unroll
-          for (int cc = 0; cc < 8; ++cc)
-            v[cc] = nz[(size_t)(D + uni(pg + cfoff + min(c0 + cc, ncf - 1))) * N + nc];
+            for (int cc = 0; cc < 8; ++cc) {
+              const int cid = uni(pg + cfoff + min(c0 + cc, ncf - 1));
+              v[cc] = rng_normal(k0, k1, (uint32_t)(row0 + nc), (uint32_t)cid, rstep, RNG_CONF_NOISE);
+              // (the first chunk's pass writes the stream; nodes sharing it write equal values)
+              if (q0 == 0 && valid && c0 + cc < ncf) nz[(size_t)(D + cid) * N + n] = v[cc];
+            }
+          } else {
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc)
+              v[cc] = nz[(size_t)(D + uni(pg + cfoff + min(c0 + cc, ncf - 1))) * N + nc];
+          }
 #pragma unroll
           for (int cc = 0; cc < 8; ++cc)
             if (c0 + cc < ncf) {
@@ -626,12 +650,15 @@ extern "C" int cgnn_launch_gen_noise(const int* prog, int ps, const uint32_t* ke
   return (int)hipGetLastError();
 }
 
-// forward of R models (noise already drawn).  W waves per block (1..8).  force: -1 the
+// forward of R models.  keys == nullptr: the noise was drawn (gen_noise); else the
+// forward draws it itself (keys, step_base[0] + step_off, row0: gen_noise's keying) and
+// writes it to `noise` for the backward.  W waves per block (1..8).  force: -1 the
 // plan's state placement, 0 LDS, 1 global (tests: every placement is bitwise the same)
-extern "C" int cgnn_launch_gen_fwd_staged(const int* prog, int ps, const int* sched, int ss, const float* params,
-                                          int P, const float* data, float* xhat, const float* noise, int NS,
-                                          float* xnorm, int N, int D, int Dt, int H, int max_in, int R, int W,
-                                          hipStream_t st, int force) {
+extern "C" int cgnn_launch_gen_fwd_staged_draw(const int* prog, int ps, const int* sched, int ss, const float* params,
+                                               int P, const float* data, float* xhat, float* noise, int NS,
+                                               float* xnorm, int N, int D, int Dt, int H, int max_in, int R, int W,
+                                               hipStream_t st, int force, const uint32_t* keys, const int* step_base,
+                                               int step_off, int row0) {
   int plan[5];
   if (cgnn_staged_plan(Dt, H, max_in, W, 0, plan) != 0) return -2;
   const int hc = fwd_hc(H);
@@ -642,9 +669,17 @@ extern "C" int cgnn_launch_gen_fwd_staged(const int* prog, int ps, const int* sc
   dim3 grid((unsigned)(T * R)), block(WAVE * W);
 #define FWD(HC, XG)                                                                                           \
   {                                                                                                           \
-    allow_lds(gen_fwd_staged_kernel<HC, XG>, lds);                                                            \
-    hipLaunchKernelGGL((gen_fwd_staged_kernel<HC, XG>), grid, block, lds, st, prog, ps, sched, ss, params, P, \
-                       data, xhat, noise, NS, xnorm, N, D, Dt, H, T, max_in);                                         \
+    if (keys) {                                                                                               \
+      allow_lds(gen_fwd_staged_kernel<HC, XG, true>, lds);                                                    \
+      hipLaunchKernelGGL((gen_fwd_staged_kernel<HC, XG, true>), grid, block, lds, st, prog, ps, sched, ss,    \
+                         params, P, data, xhat, noise, NS, xnorm, N, D, Dt, H, T, max_in, keys, step_base,     \
+                         step_off, row0);                                                                     \
+    } else {                                                                                                  \
+      allow_lds(gen_fwd_staged_kernel<HC, XG, false>, lds);                                                   \
+      hipLaunchKernelGGL((gen_fwd_staged_kernel<HC, XG, false>), grid, block, lds, st, prog, ps, sched, ss,   \
+                         params, P, data, xhat, noise, NS, xnorm, N, D, Dt, H, T, max_in, keys, step_base,     \
+                         step_off, row0);                                                                     \
+    }                                                                                                         \
   }
 #define FWD_HC(HC) case HC: if (xg) FWD(HC, true) else FWD(HC, false) break;
   switch (fwd_hc(H)) {
@@ -655,6 +690,14 @@ extern "C" int cgnn_launch_gen_fwd_staged(const int* prog, int ps, const int* sc
 #undef FWD_HC
 #undef FWD
   return (int)hipGetLastError();
+}
+
+extern "C" int cgnn_launch_gen_fwd_staged(const int* prog, int ps, const int* sched, int ss, const float* params,
+                                          int P, const float* data, float* xhat, const float* noise, int NS,
+                                          float* xnorm, int N, int D, int Dt, int H, int max_in, int R, int W,
+                                          hipStream_t st, int force) {
+  return cgnn_launch_gen_fwd_staged_draw(prog, ps, sched, ss, params, P, data, xhat, const_cast<float*>(noise), NS,
+                                         xnorm, N, D, Dt, H, max_in, R, W, st, force, nullptr, nullptr, 0, 0);
 }
 
 // backward: gpart [R][T][P] (T = cgnn_staged_tiles(N)); dxs [R][Dt][N] is needed when the
