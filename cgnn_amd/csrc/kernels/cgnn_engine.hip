@@ -175,12 +175,14 @@ class Engine {
                                     nullptr, 0, b_.step, 0, c_.R, st_), "finalize(tt)");
   }
 
-  void enqueue_gen_fwd(int off) {
+  // train: the staged forward stores its noise draws for the backward
+  void enqueue_gen_fwd(int off, bool train) {
     if (c_.staged) {
       // the forward draws the step's noise itself (and stores it for the backward)
       check(cgnn_launch_gen_fwd_staged_draw(b_.prog, c_.prog_stride, b_.sched, c_.sched_stride, b_.params, c_.P,
-                                            b_.data, b_.xhat, b_.noise, c_.NS, b_.xnorm, c_.N, c_.D, c_.d_true, c_.H,
-                                            c_.max_in, c_.R, c_.stage_w, st_, -1, b_.keys, b_.step, off, 0),
+                                            b_.data, b_.xhat, train ? b_.noise : nullptr, c_.NS, b_.xnorm, c_.N,
+                                            c_.D, c_.d_true, c_.H, c_.max_in, c_.R, c_.stage_w, st_, -1, b_.keys,
+                                            b_.step, off, 0),
             "gen_fwd_staged");
     } else {
       check(cgnn_launch_gen_fwd(b_.prog, c_.prog_stride, b_.params, c_.P, b_.data, b_.xhat, b_.noise, c_.NS,
@@ -190,7 +192,7 @@ class Engine {
 
   void enqueue_train_step(int off, bool record_hist) {
     const float inv = loss_scale();
-    enqueue_gen_fwd(off);
+    enqueue_gen_fwd(off, true);
     enqueue_loss(off, true, record_hist);
     // the training loss is only observable through the recorded history
     if (record_hist)
@@ -210,7 +212,7 @@ class Engine {
 
   void enqueue_eval_step(int off) {
     const float inv = loss_scale();
-    enqueue_gen_fwd(off);
+    enqueue_gen_fwd(off, false);
     enqueue_loss(off, false);
     check(cgnn_launch_loss_finalize(b_.lpart, n_parts(), b_.tt, b_.loss_last, b_.loss_acc, inv, 1,
                                     nullptr, 0, b_.step, off, c_.R, st_), "finalize(eval)");

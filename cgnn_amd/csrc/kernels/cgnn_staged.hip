@@ -94,7 +94,9 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
   const int* sc = sched + (size_t)r * ss;
   const float* th = params + (size_t)r * P;
   const float* dr = data + (size_t)r * D * N;
-  float* nz = noise + (size_t)r * NS * N;
+  // DRAW with noise == nullptr (an evaluation step): nothing reads the draws afterwards
+  float* nz = noise ? noise + (size_t)r * NS * N : nullptr;
+  const bool store = DRAW && noise != nullptr;
   float* xr = xhat + (size_t)r * D * N;
   uint32_t k0 = 0u, k1 = 0u, rstep = 0u;
   if constexpr (DRAW) {
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
       const int npar = cur.npar, paroff = cur.paroff, ncf = cur.ncf, cfoff = cur.cfoff, nin = cur.nin;
       const float* W1 = cur.W1;
       const float e_own = enx;
-      if (DRAW && valid) nz[(size_t)var * N + n] = e_own;           // for the backward
+      if (store && valid) nz[(size_t)var * N + n] = e_own;          // for the backward
       float out = W1[(size_t)(nin + 2) * H];                       // b2
       for (int q0 = 0; q0 < H; q0 += HC) {
         // this chunk's weights (rows 0..nin+1, HC units) into the wave's slab
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(512) void gen_fwd_staged_kernel(
               const int cid = uni(pg + cfoff + min(c0 + cc, ncf - 1));
               v[cc] = rng_normal(k0, k1, (uint32_t)(row0 + nc), (uint32_t)cid, rstep, RNG_CONF_NOISE);
               // (the first chunk's pass writes the stream; nodes sharing it write equal values)
-              if (q0 == 0 && valid && c0 + cc < ncf) nz[(size_t)(D + cid) * N + n] = v[cc];
+              if (store && q0 == 0 && valid && c0 + cc < ncf) nz[(size_t)(D + cid) * N + n] = v[cc];
             }
           } else {
 #pragma unroll
@@ -652,7 +654,7 @@ extern "C" int cgnn_launch_gen_noise(const int* prog, int ps, const uint32_t* ke
 
 // forward of R models.  keys == nullptr: the noise was drawn (gen_noise); else the
 // forward draws it itself (keys, step_base[0] + step_off, row0: gen_noise's keying) and
-// writes it to `noise` for the backward.  W waves per block (1..8).  force: -1 the
+// writes it to `noise` for the backward (noise == nullptr: not stored).  W waves per block (1..8).  force: -1 the
 // plan's state placement, 0 LDS, 1 global (tests: every placement is bitwise the same)
 extern "C" int cgnn_launch_gen_fwd_staged_draw(const int* prog, int ps, const int* sched, int ss, const float* params,
                                                int P, const float* data, float* xhat, float* noise, int NS,
