@@ -557,6 +557,10 @@ __global__ __launch_bounds__(256) void adam_tf1_kernel(
     float* __restrict__ params, float* __restrict__ m, float* __restrict__ v,
     const float* __restrict__ gpart, int G, const int* __restrict__ prog, int prog_stride, int P,
     const int* __restrict__ step_base, int step_off, float lr, float beta1, float beta2, float eps) {
+  // no contraction: the float4 form otherwise fuses the moment updates into (packed)
+  // FMAs the scalar round-5 kernel did not have, and the trajectories drift apart
+  // (pinned example predictions, tests/test_examples_gpu.py)
+#pragma clang fp contract(off)
   const int r = blockIdx.y;
   const int p0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
   const int Pr = prog[(size_t)r * prog_stride + 1];
