@@ -65,6 +65,8 @@ long rff_wide_scratch_floats(int, int, int);
 // GNN track
 int gnn_launch_spmm(const int*, const int*, const void*, void*, const float*, const float*, int,
                     int, int, int, int, int, int, int, const float*, int, const float*, int, int, hipStream_t);
+int gnn_launch_spmm_fan(const int*, const int*, const void*, void*, const float*, int, int, int, int, long, long, int,
+                        hipStream_t);
 int gnn_launch_spmm_ce(const int*, const int*, const void*, const float*, const float*,
                        const int*, const uint8_t*, float*, void*, const float*, int, int, int, int, int, float,
                        const int*, int, hipStream_t);
@@ -297,6 +299,12 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("n_rows"), py::arg("F"), py::arg("ld_x"), py::arg("ld_y"), py::arg("x_bf16"), py::arg("y_bf16"),
      py::arg("relu"), py::arg("unit_col"), py::arg("st"), py::arg("init") = 0, py::arg("ldi") = 0,
      py::arg("cscale") = 0, py::arg("init_rows") = -1, py::arg("short_rows") = 0);
+  m.def("gnn_spmm_fan", [](uint64_t rowptr, uint64_t col, uint64_t x, uint64_t y, uint64_t rscale, int n_rows, int F,
+                           int ldx, int ldy, long n_x_rows, long nnz, int max_deg, uint64_t st) {
+    chk(gnn_launch_spmm_fan(Pt<const int>(rowptr), Pt<const int>(col), Pt<const void>(x), Pt<void>(y),
+                            Pt<const float>(rscale), n_rows, F, ldx, ldy, n_x_rows, nnz, max_deg, S(st)),
+        "gnn_spmm_fan");
+  });
   m.def("gnn_spmm_ce", [](uint64_t rowptr, uint64_t col, uint64_t z, uint64_t rscale, uint64_t bias,
                           uint64_t labels, uint64_t mask, uint64_t stats, uint64_t dlogits, uint64_t init, int ldi,
                           int n_rows, int C, int ld, int mode, float inv_count, uint64_t st, uint64_t gslot,

@@ -372,6 +372,110 @@ __global__ __launch_bounds__(256, 8) void spmm_ell_pipe_kernel(const int* __rest
   }
 }
 
+// Rows of at most 8 entries (a sampled GraphSAGE block's input layer: one row per
+// destination, min(degree, fanout) picks) as a persistent pipelined grid -- spmm_kernel
+// <16> there walks three dependent round trips per row (row bounds, column ids, rows)
+// with ~5 gathers each.  Each wave loops over groups of 4 rows (16 lanes per row, F <=
+// 128): the gathers of group g go out with the column ids of group g + nw (whose row
+// bounds arrived one iteration earlier) and the row bounds of group g + 2 nw, so a group
+// costs one exposed round trip.  Gathers, column-id loads and stores use buffer
+// descriptors with out-of-range offsets for inactive lanes (zeros / dropped stores, no
+// branches, exact wait counts).  Per row the same adds in the same order as spmm_kernel's
+// gather_sum<16, 1, 8> (an 8-step for 8 entries, else a 4-step for >= 4, then 1-steps),
+// and its epilogue: bit-identical output.  Tables below 2^31 bytes (the launcher checks).
+__global__ __launch_bounds__(256, 8) void spmm_fan_pipe_kernel(const int* __restrict__ rowptr,
+                                                            const int* __restrict__ col,
+                                                            const uint16_t* __restrict__ X, uint16_t* __restrict__ Y,
+                                                            const float* __restrict__ rscale, int n_rows, int F,
+                                                            int ldx, int ldy, uint32_t x_bytes, uint32_t col_bytes) {
+  constexpr int L = 16, RPW = 4;
+  constexpr uint32_t OOB = 0x80000000u;
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, sub = lane / L, sl = lane - sub * L;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  const int n_groups = (n_rows + RPW - 1) / RPW;
+  const int f0 = sl * 8;
+  const bool fl = f0 < F;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(X), (short)0,
+                                                                      (int)x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(col), (short)0,
+                                                                      (int)col_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(Y, (short)0,
+                                                                      (int)((uint32_t)n_rows * (uint32_t)ldy * 2u),
+                                                                      0x00020000);
+  const float* rsb = rscale ? rscale : reinterpret_cast<const float*>(rowptr);
+  const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  int g = wave;
+  if (g < n_groups) {                        // uniform per wave
+  // row bounds of this group and the next, the column ids of this group (clamped rows;
+  // the ids through the descriptor: an empty row, or one at the end of col, reads zeros)
+  int a0 = rowptr[min(g * RPW + sub, n_rows - 1)], b0 = rowptr[min(g * RPW + sub, n_rows - 1) + 1];
+  int a1 = rowptr[min((g + nw) * RPW + sub, n_rows - 1)], b1 = rowptr[min((g + nw) * RPW + sub, n_rows - 1) + 1];
+  int cj = __builtin_amdgcn_raw_buffer_load_b32(cr, sl < b0 - a0 ? (uint32_t)(a0 + sl) * 4u : OOB, 0, 0);
+  // a dropped store: the loop is entered with the younger-operation count of its back edge
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_raw_buffer_store_b32(0u, yr, OOB, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  do {
+    const int row = g * RPW + sub;
+    const bool rv = row < n_rows;
+    const int cnt = rv ? b0 - a0 : 0;        // <= 8 (the caller's guarantee)
+    const int myj = cj;
+    int j[8];
+    row_bcast8<0>(myj, j);
+    uint4 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t off = (fl && u < cnt) ? ((uint32_t)j[u] * (uint32_t)ldx + (uint32_t)f0) * 2u : OOB;
+      r[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+    const float rsv = rsb[rscale ? min(row, n_rows - 1) : 0];
+    __builtin_amdgcn_sched_barrier(0);
+    // the next group's column ids (its bounds arrived last iteration), then the bounds of
+    // the group after it
+    const int row1 = (g + nw) * RPW + sub;
+    cj = __builtin_amdgcn_raw_buffer_load_b32(cr, (row1 < n_rows && sl < b1 - a1) ? (uint32_t)(a1 + sl) * 4u : OOB,
+                                              0, 0);
+    a0 = a1;
+    b0 = b1;
+    const int row2 = min((g + 2 * nw) * RPW + sub, n_rows - 1);
+    a1 = rowptr[row2];
+    b1 = rowptr[row2 + 1];
+    __builtin_amdgcn_sched_barrier(0);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (cnt == 8) {
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) acc_bf16_pair(acc, r[u], r[u + 1]);
+    } else {
+      const int k = cnt >= 4 ? 4 : 0;
+      if (cnt >= 4) {
+        acc_bf16_pair(acc, r[0], r[1]);
+        acc_bf16_pair(acc, r[2], r[3]);
+      }
+      // (u runs to 7 although cnt <= 7 here: the eighth gather is then used on both
+      // paths and stays with the others, instead of sinking into the 8-entry branch
+      // behind a full drain)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u >= k && u < cnt) {
+          float f[8];
+          bf16x8_to_f32(r[u], f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] = acc[q] + f[q];
+        }
+      }
+    }
+    const float rs = rscale ? rsv : 1.f;
+    float y[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) y[q] = f0 + q < F ? acc[q] * rs + 0.f : 0.f;
+    const uint32_t yo = (rv && f0 < ldy) ? ((uint32_t)row * (uint32_t)ldy + (uint32_t)f0) * 2u : OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, f32x8_to_bf16(y)), yr, yo, 0, 0);
+    g += nw;
+  } while (g < n_groups);
+  }
+}
+
 // ell image of a CSR for spmm_ell_kernel (one thread per row)
 __global__ void ell_build_kernel(const int* __restrict__ rowptr, const int* __restrict__ col, int* __restrict__ ell,
                                  int n_rows) {
@@ -792,6 +896,24 @@ extern "C" int gnn_launch_spmm_ell(const int* ell, const int* col, const void* X
     hipLaunchKernelGGL(spmm_ell_kernel, dim3((n_rows + 31) / 32), dim3(256), 0, st, ell, col, (const uint16_t*)X,
                        (uint16_t*)Y, rscale, n_rows, F, ldx, ldy);
   }
+  return (int)hipGetLastError();
+}
+
+// rows of at most max_deg <= 8 entries, bf16 X / Y, F <= 128 (spmm_fan_pipe_kernel);
+// other shapes take gnn_launch_spmm.  n_x_rows: rows of X (bounds of its descriptor)
+extern "C" int gnn_launch_spmm_fan(const int* rowptr, const int* col, const void* X, void* Y, const float* rscale,
+                                   int n_rows, int F, int ldx, int ldy, long n_x_rows, long nnz, int max_deg,
+                                   hipStream_t st) {
+  if ((ldx % 8) || (ldy % 8) || F > ldx || F > ldy) return -3;
+  if (n_rows <= 0) return 0;
+  if (max_deg > 8 || F > 128 || ldy > 128 || n_x_rows * ldx * 2 >= (1l << 31) || nnz * 4 >= (1l << 31) ||
+      (long)n_rows * ldy * 2 >= (1l << 31))
+    return gnn_launch_spmm(rowptr, col, X, Y, rscale, nullptr, n_rows, F, ldx, ldy, 1, 1, 0, -1, nullptr, 0,
+                           nullptr, -1, 0, st);
+  const int groups = (n_rows + 3) / 4;
+  const int blocks = std::max(1, std::min((groups + 3) / 4, device_cus() * 8));
+  hipLaunchKernelGGL(spmm_fan_pipe_kernel, dim3(blocks), dim3(256), 0, st, rowptr, col, (const uint16_t*)X,
+                     (uint16_t*)Y, rscale, n_rows, F, ldx, ldy, (uint32_t)(n_x_rows * ldx * 2), (uint32_t)(nnz * 4));
   return (int)hipGetLastError();
 }
 

@@ -93,6 +93,29 @@ def spmm(rowptr, col, X, F, rscale=None, bias=None, relu=False, out=None, out_dt
     return out
 
 
+def spmm_fan(rowptr, col, X, F, max_deg, rscale=None, out=None):
+    """``spmm`` (bf16, no bias / init / column scale) for rows of at most ``max_deg``
+    entries -- a sampled block whose fanout bounds every row: at most 8, a pipelined
+    persistent kernel (gnn_sparse.hip, spmm_fan_pipe_kernel); same sums, bit for bit."""
+    n = rowptr.numel() - 1
+    if out is None:
+        out = torch.empty(n, X.shape[1], dtype=torch.bfloat16, device=X.device)
+    if not X.is_cuda:
+        return spmm(rowptr, col, X, F, rscale=rscale, out=out)
+    if X.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
+        raise TypeError("spmm_fan: bf16 in and out")
+    if checks.enabled():
+        checks.csr(rowptr, col, X.shape[0], "spmm_fan")
+        checks.rows(out, n, "spmm_fan out")
+        checks.rows(rscale, n, "spmm_fan rscale")
+        if n > 0 and int((rowptr[1:] - rowptr[:-1]).max()) > max_deg:
+            raise ValueError("spmm_fan: a row has more than max_deg = %d entries" % max_deg)
+    native.hip().gnn_spmm_fan(rowptr.data_ptr(), col.data_ptr(), X.data_ptr(), out.data_ptr(),
+                              rscale.data_ptr() if rscale is not None else 0, n, F, X.shape[1], out.shape[1],
+                              X.shape[0], col.numel(), int(max_deg), _st(X))
+    return out
+
+
 _DB_INDEX = {}
 
 

@@ -189,8 +189,11 @@ class _FusedSAGE:
     initialised exactly like :class:`SAGE` (same generator sequence)."""
 
     def __init__(self, x: torch.Tensor, n_features: int, hidden: int, n_classes: int, layers: int, dropout: float,
-                 lr: float, seed: int):
+                 lr: float, seed: int, fanouts: Optional[Sequence[int]] = None):
         dev = x.device
+        # the blocks' fanouts, input layer first (None: full-graph blocks); a block whose
+        # fanout is at most 8 aggregates on ops.spmm_fan (rows of <= fanout picks)
+        self.fan = list(reversed(list(fanouts)))[:layers] if fanouts else None
         self.dev, self.L, self.C, self.p, self.lr = dev, layers, n_classes, float(dropout), float(lr)
         F = x.shape[1]
         self.dims = [F] + [hidden] * (layers - 1) + [n_classes]
@@ -255,8 +258,13 @@ class _FusedSAGE:
                 x1, idx1 = self.x, idx0[:nd]
             else:
                 col, x1, idx1 = blk.col, h, None
-            agg = ops.spmm(blk.rowptr, col, h, F, rscale=blk.inv_deg,
-                           out=torch.empty(nd, self.ld[k], dtype=torch.bfloat16, device=self.dev))
+            out_agg = torch.empty(nd, self.ld[k], dtype=torch.bfloat16, device=self.dev)
+            # (sampled blocks only -- idx0 given; evaluation passes the full-graph blocks)
+            if (idx0 is not None and self.fan is not None and self.fan[k] <= 8 and h.is_cuda
+                    and h.dtype == torch.bfloat16):
+                agg = ops.spmm_fan(blk.rowptr, col, h, F, self.fan[k], rscale=blk.inv_deg, out=out_agg)
+            else:
+                agg = ops.spmm(blk.rowptr, col, h, F, rscale=blk.inv_deg, out=out_agg)
             out = torch.empty(nd, self.ld[k + 1], dtype=torch.bfloat16, device=self.dev)
             lin_fwd(x1, self.W[k], None if last else self.b[k], x2=agg, K1=F, K2=F, relu=not last,
                     p=self.p if (train and not last) else 0.0, key=self.keys[k], step=step, idx1=idx1, n=nd, out=out)
@@ -377,7 +385,8 @@ class SAGETrainer:
             if not self.x.dtype == torch.bfloat16:
                 self.x = self.x.to(torch.bfloat16)
             self.y32 = g.y.to(torch.int32)
-            self._fused = _FusedSAGE(self.x, g.n_features, hidden, self.C, layers, dropout, lr, seed)
+            self._fused = _FusedSAGE(self.x, g.n_features, hidden, self.C, layers, dropout, lr, seed,
+                                     fanouts=self.fanouts[:layers] if self.fanouts else None)
             self.model, self.opt, self.ddp = None, None, None
             if self.world > 1:       # identical initial parameters on every rank
                 torch.distributed.broadcast(self._fused.params, 0)

@@ -35,6 +35,37 @@ def test_spmm_matches_reference(F, ld, xbf, ybf):
     np.testing.assert_allclose(got.float().numpy(), ref.float().numpy(), rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("n_rows", [1, 5, 1000, 70001])
+@pytest.mark.parametrize("F,ld", [(100, 104), (64, 64), (8, 8), (128, 128)])
+def test_spmm_fan_matches_spmm(n_rows, F, ld):
+    """The pipelined kernel for rows of <= 8 entries (a sampled block's input layer)
+    equals the CSR SpMM bit for bit: rows of 0-8 entries (8: the 8-step; 4-7: a 4-step
+    and 1-steps; < 4: 1-steps), with and without the row scale; rows past n untouched."""
+    rng = np.random.default_rng(n_rows + F)
+    n_src = 3000
+    deg = rng.integers(0, 9, n_rows)
+    deg[::11] = 8
+    deg[::13] = 0
+    rp = torch.zeros(n_rows + 1, dtype=torch.int32)
+    rp[1:] = torch.as_tensor(np.cumsum(deg), dtype=torch.int32)
+    col = torch.as_tensor(rng.integers(0, n_src, int(deg.sum())), dtype=torch.int32)
+    X = torch.zeros(n_src, ld)
+    X[:, :F] = torch.randn(n_src, F)
+    X = X.to(torch.bfloat16).cuda()
+    rs = (torch.rand(n_rows) + 0.5).cuda()
+    rpc, colc = rp.cuda(), col.cuda()
+    for rscale in (rs, None):
+        ref = ops.spmm(rpc, colc, X, F, rscale=rscale,
+                       out=torch.full((n_rows + 3, ld), 7.0, dtype=torch.bfloat16).cuda()[:n_rows])
+        got_full = torch.full((n_rows + 3, ld), 7.0, dtype=torch.bfloat16).cuda()
+        got = ops.spmm_fan(rpc, colc, X, F, 8, rscale=rscale, out=got_full[:n_rows])
+        assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+        assert torch.all(got_full[n_rows:] == 7.0)
+    # a bound above 8 falls back to the CSR SpMM (same result)
+    got = ops.spmm_fan(rpc, colc, X, F, 9, rscale=rs)
+    assert torch.equal(got.view(torch.int16), ops.spmm(rpc, colc, X, F, rscale=rs).view(torch.int16))
+
+
 def _short_csr(n_rows, n_src, seed):
     """CSR with mostly 0-3 entries per row and a few long rows (4..40), at random places."""
     rng = np.random.default_rng(seed)
