@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--train", type=int, default=1000)
     ap.add_argument("--test", type=int, default=500)
     ap.add_argument("--h", type=int, default=20)
+    ap.add_argument("--batch-models", type=int, default=0,
+                    help="models per device batch (runs x candidates; 0: the SETTINGS default)")
     ap.add_argument("--seed", type=int, default=0)
     a = ap.parse_args()
     import cgnn
@@ -43,6 +45,8 @@ def main():
     graph, data = gen.generate(gen_cat=False)[:2]
     n_vars, n_edges = len(graph.get_list_nodes()), len(graph.get_list_edges())
     kw = dict(nb_runs=a.runs, train_epochs=a.train, test_epochs=a.test, h_layer_dim=a.h, gpu=True)
+    if a.batch_models:
+        kw["batch_models"] = a.batch_models
     state = {"cand": 0, "batches": 0, "t0": None, "first": None}
     make = hc.make_evaluator
 
