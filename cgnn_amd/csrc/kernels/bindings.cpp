@@ -70,8 +70,8 @@ int gnn_launch_spmm_fan(const int*, const int*, const void*, void*, const float*
 int gnn_launch_spmm_ce(const int*, const int*, const void*, const float*, const float*,
                        const int*, const uint8_t*, float*, void*, const float*, int, int, int, int, int, float,
                        const int*, int, hipStream_t);
-int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, float, float, float,
-                    const int*, hipStream_t);
+int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, float, float, float, int*, unsigned*,
+                    hipStream_t);
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
 int gnn_spmm_ce_blocks(int, int);
 int gnn_launch_ell_build(const int*, const int*, int*, int, hipStream_t);
@@ -318,10 +318,11 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("C"), py::arg("ld"), py::arg("mode"), py::arg("inv_count"), py::arg("st"), py::arg("gslot") = 0,
      py::arg("n_long") = 0);
   m.def("gnn_adam", [](uint64_t p, uint64_t mm, uint64_t vv, uint64_t g, int n, float lr, float b1, float b2,
-                       float eps, float wd, uint64_t step, uint64_t st) {
+                       float eps, float wd, uint64_t step, uint64_t st, uint64_t done) {
     chk(gnn_launch_adam(Pt<float>(p), Pt<float>(mm), Pt<float>(vv), Pt<const float>(g), n, lr, b1, b2, eps, wd,
-                        Pt<const int>(step), S(st)), "gnn_adam");
-  });
+                        Pt<int>(step), Pt<unsigned>(done), S(st)), "gnn_adam");
+  }, py::arg("p"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("n"), py::arg("lr"), py::arg("b1"),
+     py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"), py::arg("st"), py::arg("done") = 0);
   m.def("gnn_spmm_ce_blocks", &gnn_spmm_ce_blocks);
   m.def("gnn_ell_build", [](uint64_t rowptr, uint64_t col, uint64_t ell, int n_rows, uint64_t st) {
     chk(gnn_launch_ell_build(Pt<const int>(rowptr), Pt<const int>(col), Pt<int>(ell), n_rows, S(st)), "gnn_ell_build");

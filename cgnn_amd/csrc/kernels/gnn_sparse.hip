@@ -698,21 +698,31 @@ __global__ __launch_bounds__(256) void relu_dropout_bwd_kernel(
 }
 
 // PyTorch-semantics Adam (bias-corrected, eps inside) with optional decoupled
-// weight decay, over one flat fp32 parameter buffer.  t = *step + 1.
+// weight decay, over one flat fp32 parameter buffer.  t = *step + 1.  done (optional,
+// zero): the block whose arrival is counted last stores *step = t and re-zeroes *done.
+// Every block has read *step into a register before its arrival (the barrier waits for
+// the load), so no fence is needed -- only the count.
 __global__ void gnn_adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                 const float* __restrict__ g, int n, float lr, float b1, float b2,
-                                float eps, float wd, const int* __restrict__ step) {
+                                float eps, float wd, int* __restrict__ step, unsigned* __restrict__ done) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
   const float t = (float)(*step + 1);
-  const float gi = g[i];
-  const float mi = b1 * m[i] + (1.f - b1) * gi;
-  const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-  m[i] = mi;
-  v[i] = vi;
-  const float mh = mi / (1.f - powf(b1, t));
-  const float vh = vi / (1.f - powf(b2, t));
-  p[i] -= lr * (mh / (sqrtf(vh) + eps) + wd * p[i]);
+  if (i < n) {
+    const float gi = g[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float mh = mi / (1.f - powf(b1, t));
+    const float vh = vi / (1.f - powf(b2, t));
+    p[i] -= lr * (mh / (sqrtf(vh) + eps) + wd * p[i]);
+  }
+  if (!done) return;
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(done, 1u) == gridDim.x - 1) {
+    *step = (int)t;
+    *done = 0u;
+  }
 }
 
 __global__ void cast_bf16_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst, long n) {
@@ -918,10 +928,10 @@ extern "C" int gnn_launch_spmm_fan(const int* rowptr, const int* col, const void
 }
 
 extern "C" int gnn_launch_adam(float* p, float* m, float* v, const float* g, int n, float lr,
-                               float b1, float b2, float eps, float wd, const int* step,
+                               float b1, float b2, float eps, float wd, int* step, unsigned* done,
                                hipStream_t st) {
   hipLaunchKernelGGL(gnn_adam_kernel, dim3((n + 255) / 256), dim3(256), 0, st, p, m, v, g, n, lr, b1,
-                     b2, eps, wd, step);
+                     b2, eps, wd, step, done);
   return (int)hipGetLastError();
 }
 
