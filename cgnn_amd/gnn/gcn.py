@@ -179,7 +179,11 @@ class GCNTrainer:
         flat[:n1] = (torch.rand(n1, generator=gen) * 2 - 1) * a1
         flat[n1 + hidden:n1 + hidden + n2] = (torch.rand(n2, generator=gen) * 2 - 1) * a2
         self.params = flat.to(dev)
-        self.grads = torch.zeros_like(self.params)
+        # the flat gradient, with a 68-float tail: a training epoch's cross-entropy
+        # reduction writes its loss / accuracy sums there and its per-class dlogits sums
+        # straight into gb2 (one reduction, no copy; ops.spmm_ce stats_out)
+        self._grads_ext = torch.zeros(self.n_params + 68, dtype=torch.float32, device=dev)
+        self.grads = self._grads_ext[:self.n_params]
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
         self.step_t = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -192,6 +196,10 @@ class GCNTrainer:
         self.gb1 = self.grads[o[1]:o[2]]
         self.gW2 = self.grads[o[2]:o[3]].view(hidden, self.C)
         self.gb2 = self.grads[o[3]:o[4]]
+        c68 = torch.arange(68, dtype=torch.int64)
+        self._ce_index = torch.where(c68 < 4, self.n_params + c68,
+                                     torch.where(c68 < 4 + self.C, o[3] + c68 - 4, torch.full_like(c68, -1)))
+        self._ce_index = self._ce_index.to(torch.int32).to(dev)
         # activations / workspaces (rows of this rank; Z2/G padded to `per` rows for all-gather;
         # AX/H1/dH1/dY2 padded with zero rows to a multiple of CHUNK for the split-K GEMMs)
         n = self.nloc
@@ -564,10 +572,14 @@ class GCNTrainer:
             dinv, y, mask, gslot = l2.dinv, l2.y, l2.mask, l2.gslot
         else:
             dinv, y, mask, gslot = self.dinv, self.y, self.mask, (self.gslot if train else None)
+        fold = train and zsrc.is_cuda
         stats, _ = ops.spmm_ce(rp, col, zsrc, C, dinv, self.b2, y, mask,
                                1.0 / max(self.n_train, 1), mode=0 if train else 1,
                                G=self.Gc_loc if train else None, init=init, gslot=gslot,
-                               n_long=l2.n_long if l2 is not None else 0)
+                               n_long=l2.n_long if l2 is not None else 0,
+                               stats_out=(self._grads_ext, self._ce_index) if fold else None)
+        if fold:      # (gb2 is written; the tail holds stats[0:4], enough for every reader)
+            stats = self._grads_ext[self.n_params:]
         return stats
 
     def backward(self, stats):
@@ -586,7 +598,8 @@ class GCNTrainer:
             ops.spmm_ell(self._ell_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
         else:
             ops.spmm(self.rp_T, self.col_T, self.Gc, C, rscale=self.dinv, out=self.dY2)
-        self.gb2.copy_(stats[4:4 + C])
+        if not self.dY2.is_cuda:          # (GPU: written by the forward's reduction)
+            self.gb2.copy_(stats[4:4 + C])
         if self.fused_bwd:
             if self._grad_index is None:
                 self._grad_index = ops.fused_bwd_grad_index(

@@ -203,7 +203,7 @@ def long_row_order(deg: torch.Tensor, threshold: Optional[int] = None):
 
 
 def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=None, init=None, gslot=None,
-            db_out=None, n_long=0):
+            db_out=None, n_long=0, stats_out=None):
     """Layer-2 aggregate + log-softmax + NLL.  Returns (stats[68] summed, G).
     ``init`` (optional fp32 [n, >=C]): partial sums of other edges.
     ``gslot`` (optional int32 [n]): G is compact -- row i (a train row, gslot[i] >= 0)
@@ -212,7 +212,11 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
     stats[4:4 + C]) are also summed straight into it -- a second fixed-order pass over
     the partials instead of a device-to-device copy.
     ``n_long``: rows [0, n_long) are long rows the caller ordered first; the GPU kernel
-    gives each of them a whole wave (see ``long_row_order``).  Results do not depend on it."""
+    gives each of them a whole wave (see ``long_row_order``).  Results do not depend on it.
+    ``stats_out`` = (buffer, index) (GPU): ONE fixed-order reduction writes column c of
+    the 68 to buffer[index[c]] (index < 0: dropped) and that buffer is returned -- e.g.
+    the loss / accuracy sums to a scratch tail and the per-class dlogits sums straight
+    into the bias gradient, with no copy or second pass."""
     if checks.enabled():
         checks.csr(rowptr, col, Z.shape[0], "spmm_ce")
         checks.rows(labels, rowptr.numel() - 1, "spmm_ce labels")
@@ -234,6 +238,10 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
                         init.data_ptr() if init is not None else 0, init.shape[1] if init is not None else 0,
                         n, C, ld, mode, float(inv_count), _st(Z),
                         gslot.data_ptr() if gslot is not None else 0, int(n_long))
+        if stats_out is not None:
+            buf, index = stats_out
+            slab_sum(stats, buf, index=index)
+            return buf, G
         out = torch.empty(68, dtype=torch.float32, device=Z.device)
         slab_sum(stats, out)
         if db_out is not None:
