@@ -446,12 +446,14 @@ class SAGETrainer:
         return blocks[::-1], nodes_in
 
     # ----------------------------------------------------------- training
-    def _step(self, blocks, nodes_in, seeds_t, labels=None):
+    def _step(self, blocks, nodes_in, seeds_t, labels=None, summed=False):
+        """One training step; the batch's mean loss (device scalar), or with ``summed``
+        (fused path) the loss summed over the batch -- no division launch per batch."""
         if self.fused:
             if labels is None:
                 labels = self.y32[seeds_t.long()]
             loss = self._fused.step(blocks, nodes_in.to(torch.int32), labels, self.world)
-            return loss[0] / max(int(seeds_t.numel()), 1)
+            return loss[0] if summed else loss[0] / max(int(seeds_t.numel()), 1)
         self.model.train()
         out = self.model(self.x[nodes_in.long()], blocks)
         loss = torch.nn.functional.cross_entropy(out[:, :self.C], self.g.y[seeds_t].long())
@@ -568,8 +570,11 @@ class SAGETrainer:
             cur = pend.popleft()
             blocks, nodes_in = cur.resolve()
             torch.cuda.current_stream(self.dev).wait_event(cur.slot.done)
-            losses.append(self._step(blocks, nodes_in, seeds[k], labels[k]))
+            losses.append(self._step(blocks, nodes_in, seeds[k], labels[k], summed=self.fused))
             ps.consumed(cur)
+        if self.fused:          # the per-batch means from the sums, once per epoch
+            cnt = torch.tensor([max(len(b), 1) for b in batches], dtype=torch.float32)
+            return float((torch.stack(losses).cpu() / cnt).mean())
         return float(torch.stack(losses).mean())
 
     @torch.no_grad()
