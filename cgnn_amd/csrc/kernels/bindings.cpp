@@ -71,13 +71,13 @@ int gnn_launch_spmm_ce(const int*, const int*, const void*, const float*, const 
                        const int*, const uint8_t*, float*, void*, const float*, int, int, int, int, int, float,
                        const int*, int, hipStream_t);
 int gnn_launch_adam(float*, float*, float*, const float*, int, float, float, float, float, float, int*, unsigned*,
-                    hipStream_t);
+                    int, hipStream_t);
 int gnn_launch_cast_bf16(const float*, void*, long, hipStream_t);
 int gnn_spmm_ce_blocks(int, int);
 int gnn_launch_ell_build(const int*, const int*, int*, int, hipStream_t);
 int gnn_launch_spmm_ell(const int*, const int*, const void*, void*, const float*, int, int, int, int, long,
                         const int*, int, hipStream_t);
-int gnn_slab_sum(const float*, long, int, float*, int, float*, const int*, hipStream_t);
+int gnn_slab_sum(const float*, long, int, float*, int, float*, const int*, int*, hipStream_t);
 int gnn_launch_sample_neighbors(const int*, const int*, const int*, int, int, const int*, int*, uint32_t, uint32_t,
                                 uint32_t, hipStream_t);
 int gnn_launch_bias_relu_dropout(void*, const float*, long, int, int, float, uint32_t, uint32_t,
@@ -318,11 +318,12 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("C"), py::arg("ld"), py::arg("mode"), py::arg("inv_count"), py::arg("st"), py::arg("gslot") = 0,
      py::arg("n_long") = 0);
   m.def("gnn_adam", [](uint64_t p, uint64_t mm, uint64_t vv, uint64_t g, int n, float lr, float b1, float b2,
-                       float eps, float wd, uint64_t step, uint64_t st, uint64_t done) {
+                       float eps, float wd, uint64_t step, uint64_t st, uint64_t done, int step_done) {
     chk(gnn_launch_adam(Pt<float>(p), Pt<float>(mm), Pt<float>(vv), Pt<const float>(g), n, lr, b1, b2, eps, wd,
-                        Pt<int>(step), Pt<unsigned>(done), S(st)), "gnn_adam");
+                        Pt<int>(step), Pt<unsigned>(done), step_done, S(st)), "gnn_adam");
   }, py::arg("p"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("n"), py::arg("lr"), py::arg("b1"),
-     py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"), py::arg("st"), py::arg("done") = 0);
+     py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("step"), py::arg("st"), py::arg("done") = 0,
+     py::arg("step_done") = 0);
   m.def("gnn_spmm_ce_blocks", &gnn_spmm_ce_blocks);
   m.def("gnn_ell_build", [](uint64_t rowptr, uint64_t col, uint64_t ell, int n_rows, uint64_t st) {
     chk(gnn_launch_ell_build(Pt<const int>(rowptr), Pt<const int>(col), Pt<int>(ell), n_rows, S(st)), "gnn_ell_build");
@@ -334,10 +335,12 @@ PYBIND11_MODULE(_hip, m) {
                             n_long, S(st)), "gnn_spmm_ell");
   });
   m.def("gnn_slab_sum", [](uint64_t P, long rows, int W, uint64_t stage, int G, uint64_t out, uint64_t map,
-                           uint64_t st) {
-    chk(gnn_slab_sum(Pt<const float>(P), rows, W, Pt<float>(stage), G, Pt<float>(out), Pt<const int>(map), S(st)),
+                           uint64_t st, uint64_t bump) {
+    chk(gnn_slab_sum(Pt<const float>(P), rows, W, Pt<float>(stage), G, Pt<float>(out), Pt<const int>(map),
+                     Pt<int>(bump), S(st)),
         "gnn_slab_sum");
-  });
+  }, py::arg("P"), py::arg("rows"), py::arg("W"), py::arg("stage"), py::arg("G"), py::arg("out"), py::arg("map"),
+     py::arg("st"), py::arg("bump") = 0);
   m.def("gnn_sample_neighbors", [](uint64_t rowptr, uint64_t col, uint64_t nodes, int n, int fanout, uint64_t out_ptr,
                                    uint64_t out_col, uint32_t k0, uint32_t k1, uint32_t salt, uint64_t st) {
     chk(gnn_launch_sample_neighbors(Pt<const int>(rowptr), Pt<const int>(col), Pt<const int>(nodes), n, fanout,

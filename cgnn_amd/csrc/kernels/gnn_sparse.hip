@@ -41,7 +41,11 @@ struct bf16x8 { uint32_t w[4]; };
 // out[c]), so the final pass also scatters the sums into their places (e.g. the weight
 // gradients into the flat parameter-gradient buffer).
 __global__ __launch_bounds__(1024) void slab_sum_kernel(const float* __restrict__ P, long S, int W, long per,
-                                                       float* __restrict__ out, const int* __restrict__ map) {
+                                                       float* __restrict__ out, const int* __restrict__ map,
+                                                       int* __restrict__ bump) {
+  // bump (optional, final pass): block 0 adds 1 to *bump (a step counter advanced here
+  // instead of by a launch of its own; nothing in this kernel reads it)
+  if (bump && gridDim.y == 1 && blockIdx.x == 0 && threadIdx.x == 0) *bump += 1;
   __shared__ float red[16][64];
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6, nrl = blockDim.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -704,9 +708,11 @@ __global__ __launch_bounds__(256) void relu_dropout_bwd_kernel(
 // the load), so no fence is needed -- only the count.
 __global__ void gnn_adam_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                 const float* __restrict__ g, int n, float lr, float b1, float b2,
-                                float eps, float wd, int* __restrict__ step, unsigned* __restrict__ done) {
+                                float eps, float wd, int* __restrict__ step, unsigned* __restrict__ done,
+                                int step_done) {
+  // step_done: *step was already advanced for this update (a slab_sum bump), t = *step
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const float t = (float)(*step + 1);
+  const float t = (float)(*step + (step_done ? 0 : 1));
   if (i < n) {
     const float gi = g[i];
     const float mi = b1 * m[i] + (1.f - b1) * gi;
@@ -829,17 +835,17 @@ extern "C" int gnn_launch_spmm(const int* rowptr, const int* col, const void* X,
 // out[map[c]] = sum_r P[r][c] (fixed order).  stage: fp32 [>= G * W] scratch for the
 // first of two passes when S is large (G groups of rows), or null for one pass.
 extern "C" int gnn_slab_sum(const float* P, long S, int W, float* stage, int G, float* out, const int* map,
-                            hipStream_t st) {
+                            int* bump, hipStream_t st) {
   if (S <= 0 || W <= 0) return -3;
   const unsigned gx = (unsigned)((W + 63) / 64);
   if (stage && G > 1) {
     const long per = (S + G - 1) / G;
     hipLaunchKernelGGL(slab_sum_kernel, dim3(gx, (unsigned)G), dim3(256), 0, st, P, S, W, per, stage,
-                       (const int*)nullptr);
+                       (const int*)nullptr, (int*)nullptr);
     hipLaunchKernelGGL(slab_sum_kernel, dim3(gx, 1), dim3(1024), 0, st, (const float*)stage, (long)G, W,
-                       (long)G, out, map);
+                       (long)G, out, map, bump);
   } else {
-    hipLaunchKernelGGL(slab_sum_kernel, dim3(gx, 1), dim3(S >= 64 ? 1024 : 256), 0, st, P, S, W, S, out, map);
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(gx, 1), dim3(S >= 64 ? 1024 : 256), 0, st, P, S, W, S, out, map, bump);
   }
   return (int)hipGetLastError();
 }
@@ -929,9 +935,9 @@ extern "C" int gnn_launch_spmm_fan(const int* rowptr, const int* col, const void
 
 extern "C" int gnn_launch_adam(float* p, float* m, float* v, const float* g, int n, float lr,
                                float b1, float b2, float eps, float wd, int* step, unsigned* done,
-                               hipStream_t st) {
+                               int step_done, hipStream_t st) {
   hipLaunchKernelGGL(gnn_adam_kernel, dim3((n + 255) / 256), dim3(256), 0, st, p, m, v, g, n, lr, b1,
-                     b2, eps, wd, step, done);
+                     b2, eps, wd, step, step_done ? nullptr : done, step_done);
   return (int)hipGetLastError();
 }
 

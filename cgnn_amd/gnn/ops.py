@@ -203,7 +203,7 @@ def long_row_order(deg: torch.Tensor, threshold: Optional[int] = None):
 
 
 def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=None, init=None, gslot=None,
-            db_out=None, n_long=0, stats_out=None):
+            db_out=None, n_long=0, stats_out=None, bump=None):
     """Layer-2 aggregate + log-softmax + NLL.  Returns (stats[68] summed, G).
     ``init`` (optional fp32 [n, >=C]): partial sums of other edges.
     ``gslot`` (optional int32 [n]): G is compact -- row i (a train row, gslot[i] >= 0)
@@ -250,7 +250,9 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
             if idx is None:
                 c = torch.arange(68, dtype=torch.int32)
                 idx = _DB_INDEX[key] = torch.where((c >= 4) & (c < 4 + C), c - 4, -1).to(torch.int32).to(Z.device)
-            slab_sum(stats, db_out, index=idx)
+            slab_sum(stats, db_out, index=idx, bump=bump)
+        elif bump is not None:
+            raise ValueError("spmm_ce: bump rides on the db_out reduction")
         return out, G
     rows = _row_ids(rowptr)
     acc = torch.zeros(n, C, dtype=torch.float32)
@@ -287,13 +289,15 @@ def spmm_ce(rowptr, col, Z, C, rscale, bias, labels, mask, inv_count, mode=0, G=
 _STAGE = {}
 
 
-def slab_sum(P, out, index=None, groups=None):
+def slab_sum(P, out, index=None, groups=None, bump=None):
     """out[index[c]] = sum_r P[r, c] (``index`` None: out[c]; index < 0: dropped) -- the
     fixed-order column sum of per-block partials (deterministic, no atomics), in one pass
     or, for more than 256 rows, two (``groups`` row groups: 512 above 4096 rows, else one
     group per 32 rows -- a one-pass sum of a few thousand rows is a serial load chain per
     lane in the two blocks of a 68-column reduce, 14 us on arxiv's cross-entropy stats).
-    On the CPU: the same sums with torch."""
+    On the CPU: the same sums with torch.
+    ``bump`` (GPU, int32[1]): incremented by the final pass (a step counter advanced
+    without a launch of its own)."""
     S, W = P.shape
     if not P.is_cuda:
         v = P.sum(0)
@@ -315,7 +319,8 @@ def slab_sum(P, out, index=None, groups=None):
         if stage is None:
             stage = _STAGE[key] = torch.empty(G * W, dtype=torch.float32, device=P.device)
     native.hip().gnn_slab_sum(P.data_ptr(), S, W, stage.data_ptr() if stage is not None else 0, G,
-                              out.data_ptr(), index.data_ptr() if index is not None else 0, _st(P))
+                              out.data_ptr(), index.data_ptr() if index is not None else 0, _st(P),
+                              bump.data_ptr() if bump is not None else 0)
     return out
 
 
@@ -537,13 +542,19 @@ def relu_dropout_bwd_(dH, H, p):
 _ADAM_DONE = {}
 
 
-def adam_(param, grad, m, v, lr, step_t, b1=0.9, b2=0.999, eps=1e-8, wd=0.0):
+def adam_(param, grad, m, v, lr, step_t, b1=0.9, b2=0.999, eps=1e-8, wd=0.0, step_done=False):
     """PyTorch-semantics Adam on flat fp32 buffers; ``step_t`` is a device int32[1]
     holding the number of completed steps (incremented here).  On a GPU, for up to 256
     blocks of parameters, the kernel's last-arriving block increments it (a zeroed
     arrival counter kept per step tensor) instead of a separate launch: the GCN epoch
     +0.3 % (profiles/r06_sage/adam_fold).  Larger grids keep the launch -- 1.2 K blocks
-    counting on one address measured slower (GraphSAGE)."""
+    counting on one address measured slower (GraphSAGE).  ``step_done`` (GPU): a
+    reduction before this update already advanced ``step_t`` (slab_sum's bump)."""
+    if param.is_cuda and step_done:
+        native.hip().gnn_adam(param.data_ptr(), m.data_ptr(), v.data_ptr(), grad.data_ptr(), param.numel(),
+                              float(lr), float(b1), float(b2), float(eps), float(wd), step_t.data_ptr(),
+                              _st(param), 0, 1)
+        return param
     if param.is_cuda:
         fold = param.numel() <= 256 * 256
         done = None

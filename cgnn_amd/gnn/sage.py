@@ -279,8 +279,13 @@ class _FusedSAGE:
         n = logits.shape[0]
         rp, col, ones, tr = self._identity(n)
         G = torch.empty_like(logits)
+        # (GPU: the bias-gradient reduction also advances the step counter -- the
+        # forward has read it for this step's dropout masks -- so Adam needs no
+        # separate increment launch)
+        cuda = logits.is_cuda
         stats, G = ops.spmm_ce(rp, col, logits, self.C, ones, self.b[-1], labels, tr if mask is None else mask,
-                               inv_count, mode=0, G=G, db_out=self.gb[-1] if logits.is_cuda else None)
+                               inv_count, mode=0, G=G, db_out=self.gb[-1] if cuda else None,
+                               bump=self.step_t if cuda else None)
         return stats, G
 
     def backward(self, saved, G, stats):
@@ -312,7 +317,7 @@ class _FusedSAGE:
         self.backward(saved, G, stats)
         if world > 1:
             torch.distributed.all_reduce(self.grads)      # loss already scaled by 1/world: a SUM is the mean
-        ops.adam_(self.params, self.grads, self.m, self.v, self.lr, self.step_t)
+        ops.adam_(self.params, self.grads, self.m, self.v, self.lr, self.step_t, step_done=self.params.is_cuda)
         return stats[0:1]
 
     def state_tensors(self):
